@@ -1,0 +1,294 @@
+#!/usr/bin/env python3
+"""Benchmark of the north-star loop: belief update + MDP Bellman sweep.
+
+One *step* = one Bayesian belief update (9-neighbour transition stencil,
+observation likelihood, renormalisation) with the next (u, z) of a seeded
+trajectory, plus one MDP Bellman sweep (per-cell min over 9 action values),
+on a 1024 x 1024 synthetic grid per GPU (BASELINE.json configs[2]; the metric
+"grid cells/sec for belief-update+Bellman loop, 1024x1024").  Inputs are
+resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 1024]
+
+For N > 1 launch with torch.distributed.run: rank r owns rows
+[r*S, (r+1)*S) of an (N*S) x S grid (weak scaling), exchanging one halo row
+per step with its neighbours and all-reducing the belief mass over RCCL.
+
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the
+Bellman sweep, 369 algorithmic bytes per cell: T 324 + C 36 + J 4 + J' 4 +
+A 1), timed live with HIP events on the stream it runs on; `cpu_baseline` is
+the C restatement of the reference (oracle/) timed on this host on a bounded
+sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_SWEEP = 369                # per cell: T 324 + C 36 + J 4 + J' 4 + A 1
+BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
+BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
+GAMMA = 0.95
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--size", type=int, default=1024, help="grid side per GPU")
+    ap.add_argument("--cpt", type=int, default=4, help="cells per lane")
+    ap.add_argument("--kernel-reps", type=int, default=100,
+                    help="launches per kernel in the per-kernel timing segment")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU-baseline sample budget (rank 0, N=1 only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile", action="store_true",
+                    help="only run warmup+timed steps (for rocprofv3)")
+    return ap.parse_args()
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+def pmc_traffic(kernel_substr: str, cells: int):
+    """HBM bytes per launch of the dominant kernel from the newest committed
+    rocprofv3 PMC summary (profiles/pmc_*.json, written by
+    profiles/collect_pmc.py), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        k = d.get("kernels", {})
+        for name, v in k.items():
+            if kernel_substr in name and v.get("cells") == cells:
+                return v.get("hbm_bytes_per_launch"), os.path.basename(f)
+    return None, None
+
+
+def cpu_baseline(grid, goal, us, zs, budget_s):
+    """The oracle's reference-order loop step (belief kernel + sequential
+    renormalisation + Bellman sweep), single thread, on the same grid."""
+    from oracle import oracle as O
+    H, W = grid.shape
+    T, L, _ = O.model_pomdp(grid, goal)
+    _, Cc = O.model_mdp(grid, goal)
+    from path_planning_2d_amd import synthetic as S
+    b = S.uniform_belief(grid)
+    J = np.zeros(H * W, np.float32)
+    lib = O.lib()
+    bo = np.empty_like(b)
+    Jo = np.empty_like(J)
+    A = np.empty(H * W, np.uint8)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        u, z = int(us[steps % len(us)]), int(zs[steps % len(zs)])
+        lib.orc_belief_update(H, W, T, L, b, u, z, bo, 1)
+        lib.orc_normalize_seq(bo.size, bo)
+        b, bo = bo, b
+        lib.orc_mdp_sweep(H, W, np.float32(GAMMA), T, Cc, J, Jo, A)
+        J, Jo = Jo, J
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or steps >= 10000:
+            break
+    return {"value": H * W * steps / el, "unit": "cells/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{steps} loop steps on the same {H}x{W} grid "
+                      f"({el:.1f} s, oracle/pp2_oracle.c -O3 -march=native, "
+                      f"1 thread)",
+            "cpu": cpu_model()}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_env()
+    if ws != args.gpus and not (ws == 1 and args.gpus == 1):
+        if ws == 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    import torch
+    import torch.distributed as dist
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+
+    torch.cuda.set_device(local)
+    if ws > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    N = args.size
+    gh, gw = N * ws, N
+    grid = S.synth_grid(gh, gw, seed=gh)
+    goal = S.synth_goal(grid)
+    total = args.warmup + args.steps
+    us, zs, _ = S.synth_trajectory(grid, min(total, 4096), seed=42)
+    us = np.resize(us, total)
+    zs = np.resize(zs, total)
+    b0 = S.uniform_belief(grid)
+
+    r0, r1 = rank * N, (rank + 1) * N
+    ctx = P.GridContext(grid, goal, gamma=GAMMA, device=local,
+                        rows=(r0, r1) if ws > 1 else None)
+    ctx.set_cells_per_lane(args.cpt)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+    if ws > 1:
+        uid = torch.zeros(P._lib.RCCL_ID_BYTES, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(P.GridContext.rccl_unique_id()),
+                                       dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        ctx.shard_comm_init(bytes(uid.cpu().numpy().tobytes()), ws, rank)
+    ctx.model_generate()
+    ctx.belief_set(b0[r0 * gw:r1 * gw])
+    ctx.mdp_reset()
+    ctx.synchronize()
+
+    # ---------------------------------------------------------------- warmup
+    ctx.loop_run(us[:args.warmup], zs[:args.warmup])
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    # ---------------------------------------------------------------- timed
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    ctx.loop_run(us[args.warmup:], zs[args.warmup:])
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    loop_ms_events = ev0.elapsed_time(ev1) / args.steps
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    cells_per_gpu = N * N
+    value = cells_per_gpu * ws * args.steps / elapsed
+    # sanity: the belief is still a distribution (checks the timed work ran)
+    mass_ok = None
+    if rank == 0 and ws == 1:
+        bsum = float(ctx.belief_get().astype(np.float64).sum())
+        mass_ok = abs(bsum - 1.0) < 1e-4
+
+    if args.profile:
+        if rank == 0:
+            print(json.dumps({"profile_run": True, "steps": args.steps,
+                              "ms_per_step": 1e3 * elapsed / args.steps}))
+        ctx.close()
+        if ws > 1:
+            dist.destroy_process_group()
+        return
+
+    # ------------------------------------------- per-kernel timing (HIP events)
+    reps = args.kernel_reps
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    ctx.mdp_sweep(reps)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    sweep_ms = e0.elapsed_time(e1) / reps
+    e0.record(stream)
+    for k in range(reps):
+        ctx.belief_update(int(us[k]), int(zs[k]))
+    e1.record(stream)
+    torch.cuda.synchronize()
+    belief_ms = e0.elapsed_time(e1) / reps
+    ctx.close()
+
+    sweep_gbs = BYTES_SWEEP * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
+    belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
+    loop_gbs = BYTES_LOOP * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("k_mdp_sweep", cells_per_gpu)
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if ws == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(grid, goal, us, zs, args.cpu_seconds)
+        result = {
+            "metric": "grid cells/sec for belief-update+Bellman loop, 1024x1024",
+            "value": value,
+            "unit": "cells/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: splitmix64 occupancy grid (p_occ=0.2, seed=H), "
+                    "uniform initial belief, seeded simulated (u,z) trajectory",
+            "config": {
+                "workload": f"{N}x{N} cells per GPU: 1 belief update + 1 MDP "
+                            f"Bellman sweep per step (BASELINE.json configs[2] grid)",
+                "grid": [gh, gw],
+                "rows_per_gpu": N,
+                "parallelism": f"row-shard x{ws}, 1-row RCCL halo" if ws > 1 else "single GPU",
+                "cells_per_lane": args.cpt,
+            },
+            "roofline": {
+                "kernel": "k_mdp_sweep (MDP Bellman sweep)",
+                "bound": "hbm",
+                "achieved": sweep_gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": sweep_gbs / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": BYTES_SWEEP * cells_per_gpu,
+                "avg_launch_us": sweep_ms * 1e3,
+            },
+            "kernels": {
+                "belief_update_us": belief_ms * 1e3,
+                "belief_update_gbs": belief_gbs,
+                "belief_update_frac": belief_gbs / HBM_PEAK_GBS,
+                "loop_step_us_events": loop_ms_events * 1e3,
+                "loop_gbs": loop_gbs,
+                "loop_frac": loop_gbs / HBM_PEAK_GBS,
+            },
+            "belief_mass_ok": mass_ok,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result))
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

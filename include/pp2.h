@@ -1,0 +1,173 @@
+/*
+ * pp2.h -- C ABI of libpp2_hip.so, the MI355X (gfx950) implementation of the
+ * path_planning_2d planner's data-parallel core.
+ *
+ * Drop-in boundary.  The reference has no library API: its ROS node classes
+ * call C++-linkage free functions and launch CUDA kernels on global device
+ * pointers.  Every entry point below replaces one of those
+ * functions / kernel launches; the replaced reference interface is cited as
+ * path:line relative to /root/reference/path_planning_2d/.  INTEGRATION.md
+ * shows the edits a maintainer makes in the catkin package to bind them.
+ *
+ * Conventions
+ *  - Every function returns a pp2_status; nothing calls exit() (the
+ *    reference's checkCudaErrors exits: helper_cuda.h:984-999).
+ *    pp2_last_error() returns a message for the last failure on this thread.
+ *  - A context is one grid (or one row shard of a grid) on one device; it
+ *    owns all device memory.  Host pointers are caller-owned and only read or
+ *    written during the call.  A context is not thread-safe.
+ *  - All work is enqueued on the context's stream (its own, or one set with
+ *    pp2_set_stream); functions that return host data synchronise it.
+ *  - Host arrays use the reference's layouts: T[hw][9 u][9 s'],
+ *    L[hw][16 z], R/C[hw][9 u], beliefs/values[hw] with idx = y*W + x.
+ *  - Action u in 0..8 is the 3x3 raster with 4 = stay; observation z in 0..15
+ *    is m3<<3|m2<<2|m1<<1|m0 (src/pomdp/path_planning_2d.cu:205-207).
+ */
+#ifndef PP2_H
+#define PP2_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PP2_ABI_VERSION 1
+
+typedef enum {
+  PP2_OK = 0,
+  PP2_EINVAL = 1,   /* bad argument / shape */
+  PP2_EHIP = 2,     /* HIP runtime error */
+  PP2_EIO = 3,      /* file I/O or parse error (text model/FIB formats) */
+  PP2_ENOMEM = 4,   /* device or host allocation failed */
+  PP2_ESTATE = 5,   /* call not valid in the current state */
+  PP2_ERCCL = 6     /* RCCL error (sharded contexts) */
+} pp2_status;
+
+typedef struct pp2_ctx pp2_ctx;
+
+int pp2_abi_version(void);
+const char* pp2_status_string(int status);
+const char* pp2_last_error(void);
+int pp2_device_count(int* count);
+
+/* ---------------------------------------------------------------- lifetime
+ * Replaces allocateDeviceMemory(H,W) / freeDeviceMemory()
+ * (src/mdp/path_planning_2d_cuda.cu:40-74), allocateDeviceMemoryOfModel /
+ * freeDeviceMemoryOfModel (src/pomdp/model_generation_cuda.cu:41-72),
+ * allocateDeviceMemoryOfFIB / freeDeviceMemoryOfFIB
+ * (src/pomdp/fast_informed_bound_cuda.cu:54-94) and the dev_* / host_*
+ * globals they fill.  `map` is the H*W occupancy grid (1 = occupied) that
+ * loadMapFromFile() produces (src/pomdp/path_planning_2d.cu:243-257); it is
+ * copied.  (goal_x, goal_y) and gamma are the node's goal_x/goal_y/
+ * discount_factor parameters. */
+int pp2_create(pp2_ctx** out, int device, uint32_t height, uint32_t width,
+               const uint8_t* map, int32_t goal_x, int32_t goal_y, float gamma);
+/* Row shard [row_begin, row_end) of a global_height x width grid (no
+ * reference counterpart: the reference is single-GPU).  `global_map` is the
+ * whole grid.  Shards exchange one halo row per step over RCCL once
+ * pp2_shard_comm_init has been called on every shard. */
+int pp2_create_shard(pp2_ctx** out, int device, uint32_t global_height,
+                     uint32_t width, uint32_t row_begin, uint32_t row_end,
+                     const uint8_t* global_map, int32_t goal_x, int32_t goal_y,
+                     float gamma);
+int pp2_destroy(pp2_ctx* ctx);
+/* Enqueue on a caller stream (a hipStream_t, e.g. torch's current stream);
+ * NULL restores the context's own stream. */
+int pp2_set_stream(pp2_ctx* ctx, void* hip_stream);
+int pp2_synchronize(pp2_ctx* ctx);
+/* rows = owned rows, row_stride = padded cells per row in device planes. */
+int pp2_get_geometry(pp2_ctx* ctx, uint32_t* rows, uint32_t* width,
+                     uint32_t* row_stride, uint32_t* row_begin);
+/* Tuning: cells per lane of the streaming kernels (1, 2 or 4; default 4). */
+int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
+
+/* ---------------------------------------------------------------- model
+ * generateModelData (src/pomdp/model_generation_cuda.cu:349-368) and the MDP
+ * cudaGenerateModelData launch (src/mdp/path_planning_2d.cu:93-106): builds
+ * T, L, R (POMDP stage reward) and C (MDP stage cost) on the device. */
+int pp2_model_generate(pp2_ctx* ctx);
+/* Download in the reference layouts (any pointer may be NULL); replaces the
+ * D2H copies into host_trans_prob/host_meas_prob/host_stage_reward
+ * (model_generation_cuda.cu:370-375). */
+int pp2_model_download(pp2_ctx* ctx, float* T, float* L, float* R, float* C);
+/* Upload reference-layout tensors (any may be NULL = keep); the device half
+ * of loadModelDataFromFile (model_generation_cuda.cu:150-156). */
+int pp2_model_upload(pp2_ctx* ctx, const float* T, const float* L,
+                     const float* R, const float* C);
+/* Text formats of saveModelDataToFile / loadModelDataFromFile
+ * (model_generation_cuda.cu:74-159): files model_data_trans_prob,
+ * model_data_meas_prob, model_data_stage_reward in `dir` ("%15.8f"). */
+int pp2_model_save(pp2_ctx* ctx, const char* dir);
+int pp2_model_load(pp2_ctx* ctx, const char* dir);
+
+/* ---------------------------------------------------------------- belief
+ * The belief lives on the device with deferred normalisation: each update
+ * applies the previous step's 1/sum and records its own sum on the device,
+ * so no host round trip is needed per step.
+ *
+ * pp2_belief_set: root belief from a Belief message (msg->belief,
+ * src/pomdp/path_planning_2d.cu:208), used as given. */
+int pp2_belief_set(pp2_ctx* ctx, const float* belief);
+/* Normalised belief b/sum (host renormalisation of search_tree_cuda.cu:
+ * 608-612). */
+int pp2_belief_get(pp2_ctx* ctx, float* belief);
+/* cudaBayesBeliefUpdate (point_based_value_iteration_cuda.cu:88-133) +
+ * renormalisation (search_tree_cuda.cu:601-612).  Asynchronous. */
+int pp2_belief_update(pp2_ctx* ctx, uint8_t u, uint8_t z);
+/* The stored (unnormalised) belief and its mass: belief_get == raw / mass.
+ * Exposes the kernel output itself, for bit-exact parity checks. */
+int pp2_belief_get_raw(pp2_ctx* ctx, float* belief, float* mass);
+/* Unnormalised mass of the current belief (= p(z | b, u) after an update
+ * from a normalised belief). Synchronises. */
+int pp2_belief_mass(pp2_ctx* ctx, float* mass);
+
+/* ---------------------------------------------------------------- MDP
+ * J := 0, A := 0 (cudaMemset, src/mdp/path_planning_2d_cuda.cu:55-61). */
+int pp2_mdp_reset(pp2_ctx* ctx);
+/* n Bellman sweeps, cudaOneStepValueIteration
+ * (src/mdp/path_planning_2d_cuda.cu:215-264). Asynchronous. */
+int pp2_mdp_sweep(pp2_ctx* ctx, int n);
+/* MdpPathPlanning2d::valueIteration (src/mdp/path_planning_2d.cu:207-269)
+ * without the OpenCV windows: blocks of 100 sweeps until the inf-norm of the
+ * change over a block is <= 1e-3*5/(1-gamma).  max_sweeps <= 0: no cap. */
+int pp2_mdp_solve(pp2_ctx* ctx, int max_sweeps, int* sweeps,
+                  double* final_norm);
+/* D2H of dev_optimal_cost1 / dev_optimal_action
+ * (src/mdp/path_planning_2d.cu:119-126).  Either may be NULL. */
+int pp2_mdp_get(pp2_ctx* ctx, float* J, uint8_t* A);
+
+/* ---------------------------------------------------------------- north star
+ * One iteration of the benchmarked loop: one belief update (u, z) and one
+ * Bellman sweep, with the belief normalisation folded into the sweep launch.
+ * Sharded contexts also exchange halo rows and all-reduce the belief mass.
+ * Asynchronous. */
+int pp2_loop_step(pp2_ctx* ctx, uint8_t u, uint8_t z);
+int pp2_loop_run(pp2_ctx* ctx, int n, const uint8_t* us, const uint8_t* zs);
+
+/* ---------------------------------------------------------------- FIB
+ * cudaFIBValueIteration sweeps (fast_informed_bound_cuda.cu:97-204) from the
+ * current alphas (zero after create). Asynchronous. */
+int pp2_fib_reset(pp2_ctx* ctx);
+int pp2_fib_sweep(pp2_ctx* ctx, int n);
+/* fastInformedBound driver (fast_informed_bound_cuda.cu:206-276): blocks of
+ * 10 sweeps until the inf-norm of the change <= 0.01. */
+int pp2_fib_solve(pp2_ctx* ctx, int max_sweeps, int* sweeps, float* final_norm);
+/* host_fib_alphas layout [hw][9] (fast_informed_bound_cuda.cu:270-271). */
+int pp2_fib_get(pp2_ctx* ctx, float* alphas);
+int pp2_fib_set(pp2_ctx* ctx, const float* alphas);
+
+/* ---------------------------------------------------------------- shards
+ * RCCL bootstrap for row shards (no reference counterpart).  Rank 0 calls
+ * pp2_rccl_unique_id, the 128 bytes are broadcast out of band, then every
+ * rank calls pp2_shard_comm_init with its own shard context. */
+#define PP2_RCCL_ID_BYTES 128
+int pp2_rccl_unique_id(uint8_t id[PP2_RCCL_ID_BYTES]);
+int pp2_shard_comm_init(pp2_ctx* ctx, const uint8_t id[PP2_RCCL_ID_BYTES],
+                        int nranks, int rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PP2_H */

@@ -1,0 +1,108 @@
+"""ctypes binding of ``libpp2_hip.so`` (the C ABI declared in include/pp2.h).
+
+The shared library is built in-tree (``path_planning_2d_amd/libpp2_hip.so``,
+see ``csrc/Makefile`` / ``__graft_entry__.build()``).  There is no fallback:
+if the library is missing or fails to load, importing the product API raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libpp2_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "pp2.h")
+
+RCCL_ID_BYTES = 128
+
+PP2_OK = 0
+STATUS_NAMES = {0: "PP2_OK", 1: "PP2_EINVAL", 2: "PP2_EHIP", 3: "PP2_EIO",
+                4: "PP2_ENOMEM", 5: "PP2_ESTATE", 6: "PP2_ERCCL"}
+
+
+class Pp2Error(RuntimeError):
+    def __init__(self, status: int, fn: str, message: str):
+        self.status = status
+        super().__init__(f"{fn}: {STATUS_NAMES.get(status, status)}: {message}")
+
+
+_vp = C.c_void_p
+_u8p = C.POINTER(C.c_uint8)
+_f32p = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int)
+_u32p = C.POINTER(C.c_uint32)
+_f64p = C.POINTER(C.c_double)
+
+# name -> argtypes (all return int status unless listed in _RESTYPES)
+SIGNATURES = {
+    "pp2_abi_version": [],
+    "pp2_status_string": [C.c_int],
+    "pp2_last_error": [],
+    "pp2_device_count": [_i32p],
+    "pp2_create": [C.POINTER(_vp), C.c_int, C.c_uint32, C.c_uint32, _u8p,
+                   C.c_int32, C.c_int32, C.c_float],
+    "pp2_create_shard": [C.POINTER(_vp), C.c_int, C.c_uint32, C.c_uint32,
+                         C.c_uint32, C.c_uint32, _u8p, C.c_int32, C.c_int32,
+                         C.c_float],
+    "pp2_destroy": [_vp],
+    "pp2_set_stream": [_vp, _vp],
+    "pp2_synchronize": [_vp],
+    "pp2_get_geometry": [_vp, _u32p, _u32p, _u32p, _u32p],
+    "pp2_set_cells_per_lane": [_vp, C.c_int],
+    "pp2_model_generate": [_vp],
+    "pp2_model_download": [_vp, _f32p, _f32p, _f32p, _f32p],
+    "pp2_model_upload": [_vp, _f32p, _f32p, _f32p, _f32p],
+    "pp2_model_save": [_vp, C.c_char_p],
+    "pp2_model_load": [_vp, C.c_char_p],
+    "pp2_belief_set": [_vp, _f32p],
+    "pp2_belief_get": [_vp, _f32p],
+    "pp2_belief_update": [_vp, C.c_uint8, C.c_uint8],
+    "pp2_belief_get_raw": [_vp, _f32p, _f32p],
+    "pp2_belief_mass": [_vp, _f32p],
+    "pp2_mdp_reset": [_vp],
+    "pp2_mdp_sweep": [_vp, C.c_int],
+    "pp2_mdp_solve": [_vp, C.c_int, _i32p, _f64p],
+    "pp2_mdp_get": [_vp, _f32p, _u8p],
+    "pp2_loop_step": [_vp, C.c_uint8, C.c_uint8],
+    "pp2_loop_run": [_vp, C.c_int, _u8p, _u8p],
+    "pp2_fib_reset": [_vp],
+    "pp2_fib_sweep": [_vp, C.c_int],
+    "pp2_fib_solve": [_vp, C.c_int, _i32p, _f32p],
+    "pp2_fib_get": [_vp, _f32p],
+    "pp2_fib_set": [_vp, _f32p],
+    "pp2_rccl_unique_id": [_u8p],
+    "pp2_shard_comm_init": [_vp, _u8p, C.c_int, C.c_int],
+}
+_RESTYPES = {"pp2_status_string": C.c_char_p, "pp2_last_error": C.c_char_p}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load the in-tree library (raises if it is missing -- no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `make -C "
+            f"{os.path.join(PKG_DIR, 'csrc')}` (or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, C.c_int)
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    st = getattr(lib, name)(*args)
+    if st != PP2_OK:
+        msg = lib.pp2_last_error()
+        raise Pp2Error(st, name, msg.decode() if msg else "")
+
+
+def exported_symbols():
+    return list(SIGNATURES)

@@ -1,0 +1,220 @@
+"""Host-side handle over one ``pp2_ctx`` (a grid, or a row shard of one, on one
+MI355X).  Thin numpy-facing layer over the C ABI in include/pp2.h; every call
+goes to the gfx950 kernels in libpp2_hip.so -- there is no CPU path.
+
+Arrays use the reference layouts (path_planning_2d/src/pomdp/
+model_generation_cuda.cu:27-38): ``T[hw, 9, 9]``, ``L[hw, 16]``,
+``R/C[hw, 9]``, beliefs and values ``[hw]`` with ``idx = y * W + x``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import call
+
+
+def _f32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _u8(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+_NULLF = C.POINTER(C.c_float)()
+
+
+class GridContext:
+    """One device-resident grid: model tensors, belief, MDP values, FIB alphas.
+
+    Mirrors the state the reference keeps in its ``dev_*``/``host_*`` globals
+    (src/mdp/path_planning_2d_cuda.cu:26-38, src/pomdp/model_generation_cuda.cu:
+    27-38, src/pomdp/fast_informed_bound_cuda.cu:43-51).
+    """
+
+    def __init__(self, grid: np.ndarray, goal, gamma: float = 0.95,
+                 device: int = 0, rows: tuple[int, int] | None = None):
+        grid = np.ascontiguousarray(grid, dtype=np.uint8)
+        if grid.ndim != 2:
+            raise ValueError("grid must be 2-D (H, W)")
+        self.global_height, self.width = grid.shape
+        self.goal = (int(goal[0]), int(goal[1]))
+        self.gamma = float(gamma)
+        self.device = int(device)
+        h = C.c_void_p()
+        if rows is None:
+            call("pp2_create", C.byref(h), self.device, self.global_height,
+                 self.width, _u8(grid), self.goal[0], self.goal[1],
+                 C.c_float(self.gamma))
+            self.row_begin, self.row_end = 0, self.global_height
+        else:
+            r0, r1 = int(rows[0]), int(rows[1])
+            call("pp2_create_shard", C.byref(h), self.device,
+                 self.global_height, self.width, r0, r1, _u8(grid),
+                 self.goal[0], self.goal[1], C.c_float(self.gamma))
+            self.row_begin, self.row_end = r0, r1
+        self._h = h
+        self.rows = self.row_end - self.row_begin
+        self.cells = self.rows * self.width
+        rs = C.c_uint32()
+        call("pp2_get_geometry", self._h, None, None, C.byref(rs), None)
+        self.row_stride = rs.value
+
+    # ------------------------------------------------------------ lifetime
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().pp2_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int | None):
+        call("pp2_set_stream", self._h, C.c_void_p(stream_handle or 0))
+
+    def synchronize(self):
+        call("pp2_synchronize", self._h)
+
+    def set_cells_per_lane(self, cpt: int):
+        call("pp2_set_cells_per_lane", self._h, int(cpt))
+
+    # ------------------------------------------------------------ model
+    def model_generate(self):
+        call("pp2_model_generate", self._h)
+
+    def model_download(self):
+        n = self.cells
+        T = np.empty((n, 9, 9), np.float32)
+        L = np.empty((n, 16), np.float32)
+        R = np.empty((n, 9), np.float32)
+        Cc = np.empty((n, 9), np.float32)
+        call("pp2_model_download", self._h, _f32(T), _f32(L), _f32(R), _f32(Cc))
+        return T, L, R, Cc
+
+    def model_upload(self, T=None, L=None, R=None, Cc=None):
+        keep = []
+
+        def p(a, shape):
+            if a is None:
+                return _NULLF
+            a = np.ascontiguousarray(a, np.float32).reshape(shape)
+            keep.append(a)
+            return _f32(a)
+        n = self.cells
+        call("pp2_model_upload", self._h, p(T, (n, 9, 9)), p(L, (n, 16)),
+             p(R, (n, 9)), p(Cc, (n, 9)))
+
+    def model_save(self, directory: str):
+        call("pp2_model_save", self._h, directory.encode())
+
+    def model_load(self, directory: str):
+        call("pp2_model_load", self._h, directory.encode())
+
+    # ------------------------------------------------------------ belief
+    def belief_set(self, b):
+        b = np.ascontiguousarray(b, np.float32).reshape(self.cells)
+        call("pp2_belief_set", self._h, _f32(b))
+
+    def belief_get(self) -> np.ndarray:
+        out = np.empty(self.cells, np.float32)
+        call("pp2_belief_get", self._h, _f32(out))
+        return out
+
+    def belief_update(self, u: int, z: int):
+        call("pp2_belief_update", self._h, int(u), int(z))
+
+    def belief_get_raw(self):
+        out = np.empty(self.cells, np.float32)
+        m = C.c_float()
+        call("pp2_belief_get_raw", self._h, _f32(out), C.byref(m))
+        return out, m.value
+
+    def belief_mass(self) -> float:
+        m = C.c_float()
+        call("pp2_belief_mass", self._h, C.byref(m))
+        return m.value
+
+    # ------------------------------------------------------------ MDP
+    def mdp_reset(self):
+        call("pp2_mdp_reset", self._h)
+
+    def mdp_sweep(self, n: int = 1):
+        call("pp2_mdp_sweep", self._h, int(n))
+
+    def mdp_solve(self, max_sweeps: int = 0):
+        s = C.c_int()
+        nrm = C.c_double()
+        call("pp2_mdp_solve", self._h, int(max_sweeps), C.byref(s), C.byref(nrm))
+        return s.value, nrm.value
+
+    def mdp_get(self):
+        J = np.empty(self.cells, np.float32)
+        A = np.empty(self.cells, np.uint8)
+        call("pp2_mdp_get", self._h, _f32(J), _u8(A))
+        return J, A
+
+    # ------------------------------------------------------------ north star
+    def loop_step(self, u: int, z: int):
+        call("pp2_loop_step", self._h, int(u), int(z))
+
+    def loop_run(self, us, zs):
+        us = np.ascontiguousarray(us, np.uint8)
+        zs = np.ascontiguousarray(zs, np.uint8)
+        if us.shape != zs.shape:
+            raise ValueError("us and zs must have the same length")
+        call("pp2_loop_run", self._h, int(us.size), _u8(us), _u8(zs))
+
+    # ------------------------------------------------------------ FIB
+    def fib_reset(self):
+        call("pp2_fib_reset", self._h)
+
+    def fib_sweep(self, n: int = 1):
+        call("pp2_fib_sweep", self._h, int(n))
+
+    def fib_solve(self, max_sweeps: int = 0):
+        s = C.c_int()
+        nrm = C.c_float()
+        call("pp2_fib_solve", self._h, int(max_sweeps), C.byref(s), C.byref(nrm))
+        return s.value, nrm.value
+
+    def fib_get(self) -> np.ndarray:
+        out = np.empty((self.cells, 9), np.float32)
+        call("pp2_fib_get", self._h, _f32(out))
+        return out
+
+    def fib_set(self, alphas):
+        a = np.ascontiguousarray(alphas, np.float32).reshape(self.cells, 9)
+        call("pp2_fib_set", self._h, _f32(a))
+
+    # ------------------------------------------------------------ shards
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        buf = (C.c_uint8 * _lib.RCCL_ID_BYTES)()
+        call("pp2_rccl_unique_id", buf)
+        return bytes(buf)
+
+    def shard_comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = (C.c_uint8 * _lib.RCCL_ID_BYTES).from_buffer_copy(uid)
+        call("pp2_shard_comm_init", self._h, buf, int(nranks), int(rank))
+
+
+def device_count() -> int:
+    n = C.c_int()
+    call("pp2_device_count", C.byref(n))
+    return n.value

@@ -1,0 +1,65 @@
+// pp2_internal.h -- shared declarations between the C-ABI runtime
+// (pp2_runtime.cpp) and the gfx950 kernels (pp2_kernels.hip).
+//
+// HBM layout (DESIGN.md "Data layout"): every per-cell tensor is a set of
+// fp32 *planes*.  A plane holds one value per cell of the owned rows plus one
+// halo row above and one below; rows are padded to `wp` cells (a multiple of
+// 4, pad cells hold 0).  `PlaneSet.p` points at (row 0, plane 0, x 0); element
+// (plane k, row y in [-1, rows], x) lives at p[y*rs + k*ps + x].  Row-major
+// over planes ([y][k][x], rs = K*wp, ps = wp) is the default: one row of
+// cells reads one contiguous K*wp*4-byte stretch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pp2 {
+
+struct PlaneSet {
+  float* p;        // (row 0, plane 0, x 0)
+  long long rs;    // row stride in floats
+  long long ps;    // plane stride in floats
+};
+
+struct Geom {
+  int rows;        // owned rows of this shard
+  int width;       // logical width W
+  int wp;          // padded row stride in cells (multiple of 4)
+  int row0;        // global index of owned row 0
+  int grows;       // global height
+};
+
+// Number of workgroups a per-cell launch uses (256 threads, CPT cells each).
+int cells_grid(const Geom& g, int cpt);
+
+// All launchers are asynchronous on `st`.
+hipError_t launch_model_gen(hipStream_t st, const Geom& g, const uint8_t* map,
+                            int gx, int gy, PlaneSet T, PlaneSet L, PlaneSet R,
+                            PlaneSet C);
+hipError_t launch_belief_update(hipStream_t st, const Geom& g, int cpt,
+                                PlaneSet T, PlaneSet L, const float* b_in,
+                                float* b_out, int u, int z,
+                                const float* in_sum, float* partials);
+hipError_t launch_mdp_sweep(hipStream_t st, const Geom& g, int cpt,
+                            float gamma, PlaneSet T, PlaneSet C,
+                            const float* J_in, float* J_out, uint8_t* A,
+                            const float* fin_partials, int fin_n,
+                            float* fin_out);
+hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
+                               float* out);
+hipError_t launch_fib_sweep(hipStream_t st, const Geom& g, float gamma,
+                            PlaneSet T, PlaneSet L, PlaneSet R,
+                            PlaneSet a_in, PlaneSet a_out);
+hipError_t launch_absdiff_max(hipStream_t st, const Geom& g, int planes,
+                              PlaneSet cur, PlaneSet snap, float* partials,
+                              int* nparts);
+hipError_t launch_sum_cells(hipStream_t st, const Geom& g, const float* b,
+                            float* partials, int* nparts);
+// dense[y*W + x)*K + k]  <->  planes (reference AoS layout <-> SoA planes)
+hipError_t launch_pack(hipStream_t st, const Geom& g, int K, PlaneSet src,
+                       float* dense, const float* divide_by);
+hipError_t launch_unpack(hipStream_t st, const Geom& g, int K,
+                         const float* dense, PlaneSet dst);
+hipError_t launch_pack_u8(hipStream_t st, const Geom& g, const uint8_t* src,
+                          uint8_t* dense);
+
+}  // namespace pp2

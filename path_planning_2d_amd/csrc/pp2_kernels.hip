@@ -1,0 +1,566 @@
+// pp2_kernels.hip -- gfx950 (MI355X) kernels for the path_planning_2d hot path.
+//
+// Every kernel is HBM-streaming over SoA planes (pp2_internal.h): lane l of a
+// 256-thread workgroup owns CPT consecutive cells of one row and reads each
+// plane with one CPT-wide vector load, so a wave moves 64*CPT*4 contiguous
+// bytes per instruction.  Stencil neighbours at x+-1 are unaligned vector
+// loads of the same plane (L1/L2 hits; HBM bytes unchanged); neighbours at
+// y+-1 come from the halo rows, which hold zeros at the grid boundary -- the
+// reference's "out-of-range contributes 0" rule -- or a neighbour shard's
+// rows when the grid is row-sharded across GPUs.
+//
+// Arithmetic follows the reference kernels term by term (nvcc contracts
+// a*b+c to fma; every such fma is spelled out with __builtin_fmaf).  The
+// library is built with -fgpu-flush-denormals-to-zero (the reference is built
+// with --use_fast_math, CMakeLists.txt:36) and -ffp-contract=off.
+#include <float.h>
+
+#include "pp2_internal.h"
+
+namespace pp2 {
+
+typedef float f4a __attribute__((ext_vector_type(4)));
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2a __attribute__((ext_vector_type(2)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+
+constexpr int kBlock = 256;
+
+template <int N, bool ALIGNED>
+__device__ __forceinline__ void ldv(const float* __restrict__ p, float (&v)[N]) {
+  if constexpr (N == 4) {
+    if constexpr (ALIGNED) {
+      const f4a t = *reinterpret_cast<const f4a*>(p);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+      const f4u t = *reinterpret_cast<const f4u*>(p);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    }
+  } else if constexpr (N == 2) {
+    if constexpr (ALIGNED) {
+      const f2a t = *reinterpret_cast<const f2a*>(p);
+      v[0] = t[0]; v[1] = t[1];
+    } else {
+      const f2u t = *reinterpret_cast<const f2u*>(p);
+      v[0] = t[0]; v[1] = t[1];
+    }
+  } else {
+    v[0] = *p;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[N]) {
+  if constexpr (N == 4) {
+    f4a t = {v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f4a*>(p) = t;
+  } else if constexpr (N == 2) {
+    f2a t = {v[0], v[1]};
+    *reinterpret_cast<f2a*>(p) = t;
+  } else {
+    *p = v[0];
+  }
+}
+
+// ---- deterministic reductions (fixed association order) --------------------
+// xor-butterfly: partners always add the same two operands, so every lane of
+// the wave ends with the bit-identical total.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Sum over a 256-thread block; result valid in thread 0.
+__device__ __forceinline__ float block_sum(float v, float* lds4) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) lds4[w] = v;
+  __syncthreads();
+  float r = 0.0f;
+  if (threadIdx.x == 0) r = ((lds4[0] + lds4[1]) + lds4[2]) + lds4[3];
+  return r;
+}
+__device__ __forceinline__ float block_max(float v, float* lds4) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) lds4[w] = v;
+  __syncthreads();
+  float r = 0.0f;
+  if (threadIdx.x == 0) r = fmaxf(fmaxf(lds4[0], lds4[1]), fmaxf(lds4[2], lds4[3]));
+  return r;
+}
+
+// Reduce partials[0..n) in a fixed order with one 256-thread block.
+__device__ __forceinline__ float block_reduce_partials(const float* __restrict__ partials,
+                                                       int n, float* lds4) {
+  float s = 0.0f;
+  for (int i = threadIdx.x; i < n; i += kBlock) s += partials[i];
+  return block_sum(s, lds4);
+}
+
+int cells_grid(const Geom& g, int cpt) {
+  const long long threads = (long long)g.rows * (g.wp / cpt);
+  return (int)((threads + kBlock - 1) / kBlock);
+}
+
+// ============================================================================
+// (a1) model generation -- cudaGenerateModelData, POMDP
+// (src/pomdp/model_generation_cuda.cu:161-347) and MDP
+// (src/mdp/path_planning_2d_cuda.cu:76-213).  T is identical for both models,
+// so one T serves the Bellman sweep and the belief update; R is the POMDP
+// stage reward, C the MDP stage cost.  Pad cells and rows outside the global
+// grid are written as zeros.
+// ============================================================================
+__device__ __forceinline__ void base_kernel(int u, float tp[9]) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) tp[i] = 0.0f;
+  switch (u) {
+    case 0: tp[0] = 0.7f; tp[1] = 0.1f; tp[3] = 0.1f; tp[4] = 0.1f; break;
+    case 1: tp[0] = 0.1f; tp[1] = 0.7f; tp[2] = 0.1f; tp[4] = 0.1f; break;
+    case 2: tp[1] = 0.1f; tp[2] = 0.7f; tp[4] = 0.1f; tp[5] = 0.1f; break;
+    case 3: tp[0] = 0.1f; tp[3] = 0.7f; tp[4] = 0.1f; tp[6] = 0.1f; break;
+    case 4: tp[4] = 1.0f; break;
+    case 5: tp[2] = 0.1f; tp[4] = 0.1f; tp[5] = 0.7f; tp[8] = 0.1f; break;
+    case 6: tp[3] = 0.1f; tp[4] = 0.1f; tp[6] = 0.7f; tp[7] = 0.1f; break;
+    case 7: tp[4] = 0.1f; tp[6] = 0.1f; tp[7] = 0.7f; tp[8] = 0.1f; break;
+    default: tp[4] = 0.1f; tp[5] = 0.1f; tp[7] = 0.1f; tp[8] = 0.7f; break;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_model_gen(
+    Geom g, const uint8_t* __restrict__ map, int gx, int gy, PlaneSet T,
+    PlaneSet L, PlaneSet R, PlaneSet C) {
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int x = (int)(t % g.wp);
+  const int y = (int)(t / g.wp) - 1;  // local row in [-1, rows]
+  if (y > g.rows) return;
+  const int ry = g.row0 + y;          // global row
+  const bool valid = x < g.width && ry >= 0 && ry < g.grows;
+
+  uint8_t lm[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int nx = x + i % 3 - 1, ny = ry + i / 3 - 1;
+    lm[i] = (!valid || nx < 0 || nx >= g.width || ny < 0 || ny >= g.grows)
+                ? 1 : map[(long long)ny * g.width + nx];
+  }
+  const bool at_goal = (unsigned)x == (unsigned)gx && (unsigned)ry == (unsigned)gy;
+  float mr[9], mc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    mr[i] = lm[i] == 1 ? -2.0f : -1.0f;
+    mc[i] = lm[i] == 1 ? 2.0f : 1.0f;
+  }
+  for (int u = 0; u < 9; ++u) {
+    float tp[9], nv[9];
+    base_kernel(u, tp);
+    // POMDP naive = base kernel (copied before the shift, :213-214)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nv[i] = tp[i];
+    // MDP naive = base kernel after the trap override (:131-137)
+    float nm[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nm[i] = (lm[4] == 1) ? (i == 4 ? 1.0f : 0.0f) : tp[i];
+    // occupied neighbour -> mass stays (:219-224), in index order
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+      if (lm[i] == 1 && i != 4) { tp[4] += tp[i]; tp[i] = 0.0f; }
+    if (lm[4] == 1) {  // trapped (:230-233)
+#pragma unroll
+      for (int i = 0; i < 9; ++i) tp[i] = 0.0f;
+      tp[4] = 1.0f;
+    }
+    float r = 0.0f, c = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      r = __builtin_fmaf(mr[i], nv[i], r);  // cudaStageReward :288-291
+      c = __builtin_fmaf(mc[i], nm[i], c);  // cudaStageCost   :166-169
+    }
+    if (u == 4) {
+      r = at_goal ? 0.0f : -2.0f;  // :293
+      c = at_goal ? 0.0f : 2.0f;   // mdp :171
+    }
+    const long long rowT = (long long)y * T.rs + x;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) T.p[rowT + (9 * u + i) * T.ps] = valid ? tp[i] : 0.0f;
+    R.p[(long long)y * R.rs + u * R.ps + x] = valid ? r : 0.0f;
+    C.p[(long long)y * C.rs + u * C.ps + x] = valid ? c : 0.0f;
+  }
+  // cudaMeasurementLikelihood (:238-264): m = {up, left, right, down}
+  const uint8_t m0 = lm[1], m1 = lm[3], m2 = lm[5], m3 = lm[7];
+  for (int i = 0; i < 16; ++i) {
+    const float l0 = (((i >> 0) & 1) == m0) ? (float)0.98 : (float)0.02;
+    const float l1 = (((i >> 1) & 1) == m1) ? (float)0.98 : (float)0.02;
+    const float l2 = (((i >> 2) & 1) == m2) ? (float)0.98 : (float)0.02;
+    const float l3 = (((i >> 3) & 1) == m3) ? (float)0.98 : (float)0.02;
+    const float l = ((l0 * l1) * l2) * l3;
+    L.p[(long long)y * L.rs + i * L.ps + x] = valid ? l : 0.0f;
+  }
+}
+
+hipError_t launch_model_gen(hipStream_t st, const Geom& g, const uint8_t* map,
+                            int gx, int gy, PlaneSet T, PlaneSet L, PlaneSet R,
+                            PlaneSet C) {
+  const long long n = (long long)(g.rows + 2) * g.wp;
+  const int grid = (int)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_model_gen, dim3(grid), dim3(kBlock), 0, st, g, map, gx,
+                     gy, T, L, R, C);
+  return hipGetLastError();
+}
+
+// ============================================================================
+// (a2) belief update -- cudaBayesBeliefUpdate
+// (src/pomdp/point_based_value_iteration_cuda.cu:88-133), gather form:
+//   p(x) = L[x][z] * sum_{s=0..8} T[x+off_s][u][8-s] * b(x+off_s)
+// as an fma chain in s order, plus the deferred renormalisation of the
+// previous step (a3): the stored input is unnormalised with total mass
+// *in_sum, so the output is scaled by 1/(*in_sum).  Each workgroup writes
+// its partial sum of the output (fixed order) for the next normalisation.
+// ============================================================================
+template <int CPT>
+__global__ __launch_bounds__(kBlock) void k_belief_update(
+    Geom g, PlaneSet T, PlaneSet L, const float* __restrict__ b_in,
+    float* __restrict__ b_out, int u, int z, const float* __restrict__ in_sum,
+    float* __restrict__ partials) {
+  __shared__ float lds4[4];
+  const int tpr = g.wp / CPT;
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / tpr);
+  const int x0 = (int)(t % tpr) * CPT;
+  float local = 0.0f;
+  if (y < g.rows) {
+    const bool le = x0 == 0, re = x0 + CPT == g.wp;
+    float p[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) p[k] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int oy = s / 3 - 1, ox = s % 3 - 1;
+      const float* tp = T.p + (long long)(y + oy) * T.rs +
+                        (long long)(9 * u + 8 - s) * T.ps + x0 + ox;
+      const float* bp = b_in + (long long)(y + oy) * g.wp + x0 + ox;
+      float tv[CPT], bv[CPT];
+      if (ox == 0) {
+        ldv<CPT, true>(tp, tv);
+        ldv<CPT, true>(bp, bv);
+      } else {
+        ldv<CPT, false>(tp, tv);
+        ldv<CPT, false>(bp, bv);
+      }
+      if (ox < 0 && le) { tv[0] = 0.0f; bv[0] = 0.0f; }
+      if (ox > 0 && re) { tv[CPT - 1] = 0.0f; bv[CPT - 1] = 0.0f; }
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) p[k] = __builtin_fmaf(tv[k], bv[k], p[k]);
+    }
+    float lv[CPT];
+    ldv<CPT, true>(L.p + (long long)y * L.rs + (long long)z * L.ps + x0, lv);
+    const float inv = in_sum ? 1.0f / *in_sum : 1.0f;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      p[k] = p[k] * lv[k];
+      p[k] = p[k] * inv;
+      local += p[k];
+    }
+    stv<CPT>(b_out + (long long)y * g.wp + x0, p);
+  }
+  const float s = block_sum(local, lds4);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+hipError_t launch_belief_update(hipStream_t st, const Geom& g, int cpt,
+                                PlaneSet T, PlaneSet L, const float* b_in,
+                                float* b_out, int u, int z,
+                                const float* in_sum, float* partials) {
+  const int grid = cells_grid(g, cpt);
+  switch (cpt) {
+    case 4: hipLaunchKernelGGL(k_belief_update<4>, dim3(grid), dim3(kBlock), 0, st, g, T, L, b_in, b_out, u, z, in_sum, partials); break;
+    case 2: hipLaunchKernelGGL(k_belief_update<2>, dim3(grid), dim3(kBlock), 0, st, g, T, L, b_in, b_out, u, z, in_sum, partials); break;
+    default: hipLaunchKernelGGL(k_belief_update<1>, dim3(grid), dim3(kBlock), 0, st, g, T, L, b_in, b_out, u, z, in_sum, partials); break;
+  }
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void k_sum_finalize(const float* __restrict__ partials,
+                                                         int n, float* __restrict__ out) {
+  __shared__ float lds4[4];
+  const float s = block_reduce_partials(partials, n, lds4);
+  if (threadIdx.x == 0) *out = s;
+}
+
+hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
+                               float* out) {
+  hipLaunchKernelGGL(k_sum_finalize, dim3(1), dim3(kBlock), 0, st, partials, n, out);
+  return hipGetLastError();
+}
+
+// ============================================================================
+// (a4) MDP Bellman backup -- cudaOneStepValueIteration
+// (src/mdp/path_planning_2d_cuda.cu:215-264):
+//   J'(x) = min_u C[x][u] + sum_i (gamma*T[x][u][i]) * J(x+off_i),
+//   A(x)  = first u attaining the min (strict <).
+// Optionally, workgroup 0 also folds the belief partial sums of the
+// preceding update into *fin_out (the north-star loop's normalisation, at no
+// extra launch).
+// ============================================================================
+template <int CPT>
+__global__ __launch_bounds__(kBlock) void k_mdp_sweep(
+    Geom g, float gamma, PlaneSet T, PlaneSet C, const float* __restrict__ J_in,
+    float* __restrict__ J_out, uint8_t* __restrict__ A,
+    const float* __restrict__ fin_partials, int fin_n, float* __restrict__ fin_out) {
+  const int tpr = g.wp / CPT;
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / tpr);
+  const int x0 = (int)(t % tpr) * CPT;
+  if (y < g.rows) {
+    const bool le = x0 == 0, re = x0 + CPT == g.wp;
+    float jn[9][CPT];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int oy = i / 3 - 1, ox = i % 3 - 1;
+      const float* jp = J_in + (long long)(y + oy) * g.wp + x0 + ox;
+      if (ox == 0) ldv<CPT, true>(jp, jn[i]);
+      else ldv<CPT, false>(jp, jn[i]);
+      if (ox < 0 && le) jn[i][0] = 0.0f;
+      if (ox > 0 && re) jn[i][CPT - 1] = 0.0f;
+    }
+    float best[CPT];
+    uint32_t arg[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
+    const float* trow = T.p + (long long)y * T.rs + x0;
+    const float* crow = C.p + (long long)y * C.rs + x0;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      float cost[CPT];
+      ldv<CPT, true>(crow + (long long)u * C.ps, cost);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        float tv[CPT];
+        ldv<CPT, true>(trow + (long long)(9 * u + i) * T.ps, tv);
+#pragma unroll
+        for (int k = 0; k < CPT; ++k)
+          cost[k] = __builtin_fmaf(gamma * tv[k], jn[i][k], cost[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < CPT; ++k)
+        if (cost[k] < best[k]) { best[k] = cost[k]; arg[k] = (uint32_t)u; }
+    }
+    stv<CPT>(J_out + (long long)y * g.wp + x0, best);
+    uint8_t* ap = A + (long long)y * g.wp + x0;
+    if constexpr (CPT == 4) {
+      *reinterpret_cast<uint32_t*>(ap) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    } else if constexpr (CPT == 2) {
+      *reinterpret_cast<uint16_t*>(ap) = (uint16_t)(arg[0] | (arg[1] << 8));
+    } else {
+      *ap = (uint8_t)arg[0];
+    }
+  }
+  if (fin_partials != nullptr && blockIdx.x == 0) {
+    __shared__ float lds4[4];
+    const float s = block_reduce_partials(fin_partials, fin_n, lds4);
+    if (threadIdx.x == 0) *fin_out = s;
+  }
+}
+
+hipError_t launch_mdp_sweep(hipStream_t st, const Geom& g, int cpt,
+                            float gamma, PlaneSet T, PlaneSet C,
+                            const float* J_in, float* J_out, uint8_t* A,
+                            const float* fin_partials, int fin_n,
+                            float* fin_out) {
+  const int grid = cells_grid(g, cpt);
+  switch (cpt) {
+    case 4: hipLaunchKernelGGL(k_mdp_sweep<4>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A, fin_partials, fin_n, fin_out); break;
+    case 2: hipLaunchKernelGGL(k_mdp_sweep<2>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A, fin_partials, fin_n, fin_out); break;
+    default: hipLaunchKernelGGL(k_mdp_sweep<1>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A, fin_partials, fin_n, fin_out); break;
+  }
+  return hipGetLastError();
+}
+
+// ============================================================================
+// (a5) FIB Bellman backup -- cudaFIBValueIteration
+// (src/pomdp/fast_informed_bound_cuda.cu:97-204):
+//   a'[x][a] = R[x][a] + gamma * sum_o max_a' sum_s' (T[x][a][s']*L[s'][o]) * a[s'][a']
+// with the reference's loop order, -FLT_MAX start and strict < in the max.
+// VALU-bound (~25 kflop/cell); one cell per lane.
+// ============================================================================
+__global__ __launch_bounds__(kBlock) void k_fib_sweep(
+    Geom g, float gamma, PlaneSet T, PlaneSet L, PlaneSet R, PlaneSet a_in,
+    PlaneSet a_out) {
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / g.wp);
+  const int x = (int)(t % g.wp);
+  if (y >= g.rows) return;
+  float la[9][9];
+#pragma unroll
+  for (int sp = 0; sp < 9; ++sp) {
+    const int oy = sp / 3 - 1, nx = x + sp % 3 - 1;
+    const bool ok = nx >= 0 && nx < g.wp;
+    const float* ap = a_in.p + (long long)(y + oy) * a_in.rs + nx;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) la[sp][q] = ok ? ap[(long long)q * a_in.ps] : 0.0f;
+  }
+  for (int a = 0; a < 9; ++a) {
+    float tpa[9];
+#pragma unroll
+    for (int sp = 0; sp < 9; ++sp)
+      tpa[sp] = T.p[(long long)y * T.rs + (long long)(9 * a + sp) * T.ps + x];
+    const float reward = R.p[(long long)y * R.rs + (long long)a * R.ps + x];
+    float rtg = 0.0f;
+    for (int o = 0; o < 16; ++o) {
+      float tm[9];
+#pragma unroll
+      for (int sp = 0; sp < 9; ++sp) {
+        const int oy = sp / 3 - 1, nx = x + sp % 3 - 1;
+        const bool ok = nx >= 0 && nx < g.wp;
+        const float lv = ok ? L.p[(long long)(y + oy) * L.rs + (long long)o * L.ps + nx] : 0.0f;
+        tm[sp] = tpa[sp] * lv;
+      }
+      float rtgo = -FLT_MAX;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        float s = 0.0f;
+#pragma unroll
+        for (int sp = 0; sp < 9; ++sp) s = __builtin_fmaf(tm[sp], la[sp][q], s);
+        if (rtgo < s) rtgo = s;
+      }
+      rtg = rtg + rtgo;
+    }
+    a_out.p[(long long)y * a_out.rs + (long long)a * a_out.ps + x] =
+        __builtin_fmaf(gamma, rtg, reward);
+  }
+}
+
+hipError_t launch_fib_sweep(hipStream_t st, const Geom& g, float gamma,
+                            PlaneSet T, PlaneSet L, PlaneSet R,
+                            PlaneSet a_in, PlaneSet a_out) {
+  const int grid = cells_grid(g, 1);
+  hipLaunchKernelGGL(k_fib_sweep, dim3(grid), dim3(kBlock), 0, st, g, gamma, T,
+                     L, R, a_in, a_out);
+  return hipGetLastError();
+}
+
+// ============================================================================
+// Convergence check of the VI / FIB drivers (path_planning_2d.cu:243-250,
+// fast_informed_bound_cuda.cu:246-257): max |cur - snap| over the owned
+// cells and planes, then snap := cur.
+// ============================================================================
+__global__ __launch_bounds__(kBlock) void k_absdiff_max(Geom g, int K, PlaneSet cur,
+                                                         PlaneSet snap, float* partials) {
+  __shared__ float lds4[4];
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long ncell = (long long)g.rows * g.wp;
+  float m = 0.0f;
+  if (t < ncell) {
+    const int y = (int)(t / g.wp), x = (int)(t % g.wp);
+    for (int k = 0; k < K; ++k) {
+      const long long ic = (long long)y * cur.rs + (long long)k * cur.ps + x;
+      const long long is = (long long)y * snap.rs + (long long)k * snap.ps + x;
+      const float c = cur.p[ic];
+      m = fmaxf(m, fabsf(snap.p[is] - c));
+      snap.p[is] = c;
+    }
+  }
+  const float r = block_max(m, lds4);
+  if (threadIdx.x == 0) partials[blockIdx.x] = r;
+}
+
+hipError_t launch_absdiff_max(hipStream_t st, const Geom& g, int planes,
+                              PlaneSet cur, PlaneSet snap, float* partials,
+                              int* nparts) {
+  const long long n = (long long)g.rows * g.wp;
+  const int grid = (int)((n + kBlock - 1) / kBlock);
+  *nparts = grid;
+  hipLaunchKernelGGL(k_absdiff_max, dim3(grid), dim3(kBlock), 0, st, g, planes,
+                     cur, snap, partials);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void k_sum_cells(Geom g, const float* __restrict__ b,
+                                                       float* partials) {
+  __shared__ float lds4[4];
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long n = (long long)g.rows * g.wp;
+  const float v = t < n ? b[t] : 0.0f;
+  const float s = block_sum(v, lds4);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+hipError_t launch_sum_cells(hipStream_t st, const Geom& g, const float* b,
+                            float* partials, int* nparts) {
+  const long long n = (long long)g.rows * g.wp;
+  const int grid = (int)((n + kBlock - 1) / kBlock);
+  *nparts = grid;
+  hipLaunchKernelGGL(k_sum_cells, dim3(grid), dim3(kBlock), 0, st, g, b, partials);
+  return hipGetLastError();
+}
+
+// ============================================================================
+// Layout conversion between the reference's AoS host arrays
+// (T[hw][9][9], L[hw][16], R[hw][9], beliefs[hw]) and the SoA planes.
+// ============================================================================
+__global__ __launch_bounds__(kBlock) void k_pack(Geom g, int K, PlaneSet src,
+                                                 float* __restrict__ dense,
+                                                 const float* __restrict__ divide_by) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long n = (long long)g.rows * g.width * K;
+  if (i >= n) return;
+  const long long cell = i / K;
+  const int k = (int)(i % K);
+  const int y = (int)(cell / g.width), x = (int)(cell % g.width);
+  float v = src.p[(long long)y * src.rs + (long long)k * src.ps + x];
+  if (divide_by) v = v / *divide_by;
+  dense[i] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack(Geom g, int K,
+                                                   const float* __restrict__ dense,
+                                                   PlaneSet dst) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long n = (long long)g.rows * g.width * K;
+  if (i >= n) return;
+  const long long cell = i / K;
+  const int k = (int)(i % K);
+  const int y = (int)(cell / g.width), x = (int)(cell % g.width);
+  dst.p[(long long)y * dst.rs + (long long)k * dst.ps + x] = dense[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_u8(Geom g, const uint8_t* __restrict__ src,
+                                                    uint8_t* __restrict__ dense) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long n = (long long)g.rows * g.width;
+  if (i >= n) return;
+  const int y = (int)(i / g.width), x = (int)(i % g.width);
+  dense[i] = src[(long long)y * g.wp + x];
+}
+
+hipError_t launch_pack(hipStream_t st, const Geom& g, int K, PlaneSet src,
+                       float* dense, const float* divide_by) {
+  const long long n = (long long)g.rows * g.width * K;
+  hipLaunchKernelGGL(k_pack, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                     g, K, src, dense, divide_by);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack(hipStream_t st, const Geom& g, int K,
+                         const float* dense, PlaneSet dst) {
+  const long long n = (long long)g.rows * g.width * K;
+  hipLaunchKernelGGL(k_unpack, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                     g, K, dense, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_u8(hipStream_t st, const Geom& g, const uint8_t* src,
+                          uint8_t* dense) {
+  const long long n = (long long)g.rows * g.width;
+  hipLaunchKernelGGL(k_pack_u8, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                     g, src, dense);
+  return hipGetLastError();
+}
+
+}  // namespace pp2

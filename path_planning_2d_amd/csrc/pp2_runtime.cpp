@@ -1,0 +1,696 @@
+// pp2_runtime.cpp -- the C ABI of libpp2_hip.so (include/pp2.h).
+//
+// Owns device memory, streams and the drivers around the gfx950 kernels
+// (pp2_kernels.hip).  Replaces the reference's dev_*/host_* globals and the
+// allocate/free/generate/load/save free functions (see pp2.h for per-entry
+// citations).  Errors are returned as pp2_status with a thread-local message;
+// nothing here exits the process.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pp2.h"
+#include "pp2_internal.h"
+
+using pp2::Geom;
+using pp2::PlaneSet;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                        \
+  do {                                                                      \
+    hipError_t e_ = (expr);                                                 \
+    if (e_ != hipSuccess)                                                   \
+      return set_err(PP2_EHIP, "%s failed: %s (%s:%d)", #expr,              \
+                     hipGetErrorString(e_), __FILE__, __LINE__);            \
+  } while (0)
+
+#define NCCLCHK(expr)                                                       \
+  do {                                                                      \
+    ncclResult_t r_ = (expr);                                               \
+    if (r_ != ncclSuccess)                                                  \
+      return set_err(PP2_ERCCL, "%s failed: %s", #expr,                     \
+                     ncclGetErrorString(r_));                               \
+  } while (0)
+
+#define CHECK(expr)                 \
+  do {                              \
+    int s_ = (expr);                \
+    if (s_ != PP2_OK) return s_;    \
+  } while (0)
+
+constexpr int kGuard = 64;  // floats of guard before/after each plane set
+
+// A set of K planes over rows [-1, rows] (one halo row each side).
+struct Planes {
+  float* alloc = nullptr;
+  size_t floats = 0;
+  PlaneSet v{nullptr, 0, 0};
+  int K = 0;
+};
+
+}  // namespace
+
+struct pp2_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  Geom g{};
+  int32_t gx = 0, gy = 0;
+  float gamma = 0.95f;
+  int cpt = 4;
+  bool model_ready = false;
+
+  uint8_t* d_map = nullptr;  // global map (grows x width)
+  Planes T, L, R, C;         // 81, 16, 9, 9 planes
+  Planes b[2];               // belief ping-pong (1 plane)
+  int bcur = 0;
+  float* bsum = nullptr;     // device float[2]: mass of b[0], b[1]
+  Planes J[2], Jsnap;        // value ping-pong + convergence snapshot
+  int jcur = 0;
+  uint8_t* A = nullptr;      // rows * wp actions
+  Planes fib[2], fibsnap;    // FIB alphas (9 planes)
+  int fcur = 0;
+  float* partials = nullptr;   // belief partial sums
+  float* rpartials = nullptr;  // convergence-check partials
+  int partials_cap = 0;
+  void* staging = nullptr;     // dense host-layout staging buffer
+  size_t staging_bytes = 0;
+
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int alloc_planes(pp2_ctx* c, Planes* P, int K) {
+  const long long rs = (long long)K * c->g.wp;
+  P->K = K;
+  P->floats = (size_t)(2 * kGuard) + (size_t)(c->g.rows + 2) * rs;
+  HIPCHK(hipMalloc(&P->alloc, P->floats * sizeof(float)));
+  HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
+  P->v.p = P->alloc + kGuard + rs;  // skip the top halo row
+  P->v.rs = rs;
+  P->v.ps = c->g.wp;
+  return PP2_OK;
+}
+
+void free_planes(Planes* P) {
+  if (P->alloc) (void)hipFree(P->alloc);
+  P->alloc = nullptr;
+}
+
+int ensure_staging(pp2_ctx* c, size_t bytes) {
+  if (c->staging_bytes >= bytes) return PP2_OK;
+  if (c->staging) HIPCHK(hipFree(c->staging));
+  c->staging = nullptr;
+  c->staging_bytes = 0;
+  HIPCHK(hipMalloc(&c->staging, bytes));
+  c->staging_bytes = bytes;
+  return PP2_OK;
+}
+
+int check_ctx(pp2_ctx* c) {
+  if (!c) return set_err(PP2_EINVAL, "null context");
+  return PP2_OK;
+}
+
+int check_model(pp2_ctx* c) {
+  CHECK(check_ctx(c));
+  if (!c->model_ready)
+    return set_err(PP2_ESTATE, "model not generated or uploaded");
+  return PP2_OK;
+}
+
+size_t owned_cells(const pp2_ctx* c) { return (size_t)c->g.rows * c->g.width; }
+
+// One halo row up and down for each plane set, in one RCCL group.
+int exchange_halos(pp2_ctx* c, std::initializer_list<const Planes*> sets) {
+  if (c->nranks <= 1) return PP2_OK;
+  if (!c->comm) return set_err(PP2_ESTATE, "sharded context without RCCL comm");
+  NCCLCHK(ncclGroupStart());
+  for (const Planes* P : sets) {
+    float* p = P->v.p;
+    const size_t n = (size_t)P->v.rs;
+    if (c->rank > 0) {
+      NCCLCHK(ncclSend(p, n, ncclFloat, c->rank - 1, c->comm, c->stream));
+      NCCLCHK(ncclRecv(p - P->v.rs, n, ncclFloat, c->rank - 1, c->comm, c->stream));
+    }
+    if (c->rank < c->nranks - 1) {
+      NCCLCHK(ncclSend(p + (long long)(c->g.rows - 1) * P->v.rs, n, ncclFloat,
+                       c->rank + 1, c->comm, c->stream));
+      NCCLCHK(ncclRecv(p + (long long)c->g.rows * P->v.rs, n, ncclFloat,
+                       c->rank + 1, c->comm, c->stream));
+    }
+  }
+  NCCLCHK(ncclGroupEnd());
+  return PP2_OK;
+}
+
+int allreduce_mass(pp2_ctx* c, float* d) {
+  if (c->nranks <= 1) return PP2_OK;
+  NCCLCHK(ncclAllReduce(d, d, 1, ncclFloat, ncclSum, c->comm, c->stream));
+  return PP2_OK;
+}
+
+// max |cur - snap| over owned cells/planes (global over shards); snap := cur.
+int absdiff_max(pp2_ctx* c, const Planes& cur, const Planes& snap, double* out) {
+  int np = 0;
+  HIPCHK(pp2::launch_absdiff_max(c->stream, c->g, cur.K, cur.v, snap.v,
+                                 c->rpartials, &np));
+  std::vector<float> h(np);
+  HIPCHK(hipMemcpyAsync(h.data(), c->rpartials, np * sizeof(float),
+                        hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float m = 0.0f;
+  for (float v : h) m = std::max(m, v);
+  if (c->nranks > 1) {
+    HIPCHK(hipMemcpyAsync(c->rpartials, &m, sizeof(float), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(ncclAllReduce(c->rpartials, c->rpartials, 1, ncclFloat, ncclMax, c->comm, c->stream));
+    HIPCHK(hipMemcpyAsync(&m, c->rpartials, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  *out = (double)m;
+  return PP2_OK;
+}
+
+int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
+                uint32_t row_begin, uint32_t row_end, const uint8_t* map,
+                int32_t gx, int32_t gy, float gamma) {
+  if (!out) return set_err(PP2_EINVAL, "out is null");
+  *out = nullptr;
+  if (!map) return set_err(PP2_EINVAL, "map is null");
+  if (grows == 0 || width == 0 || row_begin >= row_end || row_end > grows)
+    return set_err(PP2_EINVAL, "bad geometry %ux%u rows [%u,%u)", grows, width,
+                   row_begin, row_end);
+  if (!(gamma > 0.0f && gamma < 1.0f))
+    return set_err(PP2_EINVAL, "discount factor %g not in (0,1)", (double)gamma);
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return set_err(PP2_EINVAL, "device %d out of range (%d devices)", device, ndev);
+  DeviceGuard dg(device);
+
+  pp2_ctx* c = new pp2_ctx();
+  c->device = device;
+  c->g.rows = (int)(row_end - row_begin);
+  c->g.width = (int)width;
+  c->g.wp = (int)((width + 3u) & ~3u);
+  c->g.row0 = (int)row_begin;
+  c->g.grows = (int)grows;
+  c->gx = gx;
+  c->gy = gy;
+  c->gamma = gamma;
+  auto fail = [&](int s) {
+    pp2_destroy(c);
+    return s;
+  };
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_err(PP2_EHIP, "hipStreamCreate failed"));
+  c->stream = c->own_stream;
+
+  const size_t map_bytes = (size_t)grows * width;
+  if (hipMalloc(&c->d_map, map_bytes) != hipSuccess)
+    return fail(set_err(PP2_ENOMEM, "hipMalloc map (%zu B)", map_bytes));
+  if (hipMemcpyAsync(c->d_map, map, map_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return fail(set_err(PP2_EHIP, "map upload"));
+
+  int s = PP2_OK;
+  if ((s = alloc_planes(c, &c->T, 81)) || (s = alloc_planes(c, &c->L, 16)) ||
+      (s = alloc_planes(c, &c->R, 9)) || (s = alloc_planes(c, &c->C, 9)) ||
+      (s = alloc_planes(c, &c->b[0], 1)) || (s = alloc_planes(c, &c->b[1], 1)) ||
+      (s = alloc_planes(c, &c->J[0], 1)) || (s = alloc_planes(c, &c->J[1], 1)) ||
+      (s = alloc_planes(c, &c->Jsnap, 1)) || (s = alloc_planes(c, &c->fib[0], 9)) ||
+      (s = alloc_planes(c, &c->fib[1], 9)) || (s = alloc_planes(c, &c->fibsnap, 9)))
+    return fail(s);
+  const size_t abytes = (size_t)c->g.rows * c->g.wp + 16;
+  if (hipMalloc(&c->A, abytes) != hipSuccess ||
+      hipMemsetAsync(c->A, 0, abytes, c->stream) != hipSuccess)
+    return fail(set_err(PP2_ENOMEM, "hipMalloc actions"));
+  if (hipMalloc(&c->bsum, 4 * sizeof(float)) != hipSuccess)
+    return fail(set_err(PP2_ENOMEM, "hipMalloc bsum"));
+  const float ones[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+  if (hipMemcpyAsync(c->bsum, ones, sizeof ones, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return fail(set_err(PP2_EHIP, "bsum init"));
+  c->partials_cap = pp2::cells_grid(c->g, 1) + 1;
+  if (hipMalloc(&c->partials, c->partials_cap * sizeof(float)) != hipSuccess ||
+      hipMalloc(&c->rpartials, c->partials_cap * sizeof(float)) != hipSuccess)
+    return fail(set_err(PP2_ENOMEM, "hipMalloc partials"));
+  if (hipStreamSynchronize(c->stream) != hipSuccess)
+    return fail(set_err(PP2_EHIP, "create sync"));
+  *out = c;
+  return PP2_OK;
+}
+
+int download_planes(pp2_ctx* c, const Planes& P, float* host, const float* divide_by) {
+  const size_t n = owned_cells(c) * P.K;
+  CHECK(ensure_staging(c, n * sizeof(float)));
+  HIPCHK(pp2::launch_pack(c->stream, c->g, P.K, P.v, (float*)c->staging, divide_by));
+  HIPCHK(hipMemcpyAsync(host, c->staging, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return PP2_OK;
+}
+
+int upload_planes(pp2_ctx* c, Planes& P, const float* host) {
+  const size_t n = owned_cells(c) * P.K;
+  CHECK(ensure_staging(c, n * sizeof(float)));
+  HIPCHK(hipMemcpyAsync(c->staging, host, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(pp2::launch_unpack(c->stream, c->g, P.K, (const float*)c->staging, P.v));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return PP2_OK;
+}
+
+int write_text(const std::string& path, const std::vector<float>& v, int per_line) {
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) return set_err(PP2_EIO, "cannot open %s for writing: %s", path.c_str(), strerror(errno));
+  for (size_t i = 0; i < v.size(); ++i) {
+    fprintf(f, "%15.8f", v[i]);
+    if ((i + 1) % per_line == 0) fprintf(f, "\n");
+  }
+  if (fclose(f) != 0) return set_err(PP2_EIO, "write %s failed", path.c_str());
+  return PP2_OK;
+}
+
+int read_text(const std::string& path, std::vector<float>& v) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return set_err(PP2_EIO, "cannot open %s: %s", path.c_str(), strerror(errno));
+  for (size_t i = 0; i < v.size(); ++i)
+    if (fscanf(f, "%f ", &v[i]) != 1) {
+      fclose(f);
+      return set_err(PP2_EIO, "%s: data dimension is not set properly (element %zu)",
+                     path.c_str(), i);
+    }
+  fclose(f);
+  return PP2_OK;
+}
+
+std::string join(const char* dir, const char* name) {
+  std::string d = dir ? dir : ".";
+  if (d.empty()) d = ".";
+  if (d.back() != '/') d += '/';
+  return d + name;
+}
+
+}  // namespace
+
+// =========================================================================== C ABI
+extern "C" {
+
+int pp2_abi_version(void) { return PP2_ABI_VERSION; }
+
+const char* pp2_status_string(int s) {
+  switch (s) {
+    case PP2_OK: return "ok";
+    case PP2_EINVAL: return "invalid argument";
+    case PP2_EHIP: return "HIP error";
+    case PP2_EIO: return "I/O error";
+    case PP2_ENOMEM: return "out of memory";
+    case PP2_ESTATE: return "invalid state";
+    case PP2_ERCCL: return "RCCL error";
+    default: return "unknown status";
+  }
+}
+
+const char* pp2_last_error(void) { return g_last_error.c_str(); }
+
+int pp2_device_count(int* count) {
+  if (!count) return set_err(PP2_EINVAL, "count is null");
+  *count = 0;
+  HIPCHK(hipGetDeviceCount(count));
+  return PP2_OK;
+}
+
+int pp2_create(pp2_ctx** out, int device, uint32_t height, uint32_t width,
+               const uint8_t* map, int32_t gx, int32_t gy, float gamma) {
+  return create_impl(out, device, height, width, 0, height, map, gx, gy, gamma);
+}
+
+int pp2_create_shard(pp2_ctx** out, int device, uint32_t global_height,
+                     uint32_t width, uint32_t row_begin, uint32_t row_end,
+                     const uint8_t* global_map, int32_t gx, int32_t gy,
+                     float gamma) {
+  return create_impl(out, device, global_height, width, row_begin, row_end,
+                     global_map, gx, gy, gamma);
+}
+
+int pp2_destroy(pp2_ctx* c) {
+  if (!c) return PP2_OK;
+  DeviceGuard dg(c->device);
+  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  for (Planes* P : {&c->T, &c->L, &c->R, &c->C, &c->b[0], &c->b[1], &c->J[0],
+                    &c->J[1], &c->Jsnap, &c->fib[0], &c->fib[1], &c->fibsnap})
+    free_planes(P);
+  if (c->d_map) (void)hipFree(c->d_map);
+  if (c->A) (void)hipFree(c->A);
+  if (c->bsum) (void)hipFree(c->bsum);
+  if (c->partials) (void)hipFree(c->partials);
+  if (c->rpartials) (void)hipFree(c->rpartials);
+  if (c->staging) (void)hipFree(c->staging);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return PP2_OK;
+}
+
+int pp2_set_stream(pp2_ctx* c, void* s) {
+  CHECK(check_ctx(c));
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return PP2_OK;
+}
+
+int pp2_synchronize(pp2_ctx* c) {
+  CHECK(check_ctx(c));
+  DeviceGuard dg(c->device);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return PP2_OK;
+}
+
+int pp2_get_geometry(pp2_ctx* c, uint32_t* rows, uint32_t* width,
+                     uint32_t* row_stride, uint32_t* row_begin) {
+  CHECK(check_ctx(c));
+  if (rows) *rows = (uint32_t)c->g.rows;
+  if (width) *width = (uint32_t)c->g.width;
+  if (row_stride) *row_stride = (uint32_t)c->g.wp;
+  if (row_begin) *row_begin = (uint32_t)c->g.row0;
+  return PP2_OK;
+}
+
+int pp2_set_cells_per_lane(pp2_ctx* c, int cpt) {
+  CHECK(check_ctx(c));
+  if (cpt != 1 && cpt != 2 && cpt != 4)
+    return set_err(PP2_EINVAL, "cells per lane must be 1, 2 or 4 (got %d)", cpt);
+  c->cpt = cpt;
+  return PP2_OK;
+}
+
+// ---------------------------------------------------------------- model
+int pp2_model_generate(pp2_ctx* c) {
+  CHECK(check_ctx(c));
+  DeviceGuard dg(c->device);
+  HIPCHK(pp2::launch_model_gen(c->stream, c->g, c->d_map, c->gx, c->gy, c->T.v,
+                               c->L.v, c->R.v, c->C.v));
+  c->model_ready = true;
+  return PP2_OK;
+}
+
+int pp2_model_download(pp2_ctx* c, float* T, float* L, float* R, float* C) {
+  CHECK(check_model(c));
+  DeviceGuard dg(c->device);
+  if (T) CHECK(download_planes(c, c->T, T, nullptr));
+  if (L) CHECK(download_planes(c, c->L, L, nullptr));
+  if (R) CHECK(download_planes(c, c->R, R, nullptr));
+  if (C) CHECK(download_planes(c, c->C, C, nullptr));
+  return PP2_OK;
+}
+
+int pp2_model_upload(pp2_ctx* c, const float* T, const float* L, const float* R,
+                     const float* C) {
+  CHECK(check_ctx(c));
+  if (c->nranks > 1 || c->g.rows != c->g.grows)
+    return set_err(PP2_EINVAL, "model upload is only supported on unsharded contexts");
+  DeviceGuard dg(c->device);
+  if (!c->model_ready && !(T && L && R && C))
+    return set_err(PP2_EINVAL, "first upload needs all of T, L, R, C");
+  if (T) CHECK(upload_planes(c, c->T, T));
+  if (L) CHECK(upload_planes(c, c->L, L));
+  if (R) CHECK(upload_planes(c, c->R, R));
+  if (C) CHECK(upload_planes(c, c->C, C));
+  c->model_ready = true;
+  return PP2_OK;
+}
+
+int pp2_model_save(pp2_ctx* c, const char* dir) {
+  CHECK(check_model(c));
+  const size_t n = owned_cells(c);
+  std::vector<float> T(n * 81), L(n * 16), R(n * 9);
+  CHECK(pp2_model_download(c, T.data(), L.data(), R.data(), nullptr));
+  CHECK(write_text(join(dir, "model_data_trans_prob"), T, 9));
+  CHECK(write_text(join(dir, "model_data_meas_prob"), L, 16));
+  CHECK(write_text(join(dir, "model_data_stage_reward"), R, 9));
+  return PP2_OK;
+}
+
+int pp2_model_load(pp2_ctx* c, const char* dir) {
+  CHECK(check_ctx(c));
+  const size_t n = owned_cells(c);
+  std::vector<float> T(n * 81), L(n * 16), R(n * 9), Cc(n * 9);
+  CHECK(read_text(join(dir, "model_data_trans_prob"), T));
+  CHECK(read_text(join(dir, "model_data_meas_prob"), L));
+  CHECK(read_text(join(dir, "model_data_stage_reward"), R));
+  // The MDP cost is not part of the POMDP files; keep/derive it on device.
+  if (!c->model_ready) CHECK(pp2_model_generate(c));
+  return pp2_model_upload(c, T.data(), L.data(), R.data(), nullptr);
+}
+
+// ---------------------------------------------------------------- belief
+int pp2_belief_set(pp2_ctx* c, const float* b) {
+  CHECK(check_ctx(c));
+  if (!b) return set_err(PP2_EINVAL, "belief is null");
+  DeviceGuard dg(c->device);
+  CHECK(upload_planes(c, c->b[c->bcur], b));
+  const float one = 1.0f;
+  HIPCHK(hipMemcpyAsync(c->bsum + c->bcur, &one, sizeof one, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return PP2_OK;
+}
+
+int pp2_belief_get(pp2_ctx* c, float* b) {
+  CHECK(check_ctx(c));
+  if (!b) return set_err(PP2_EINVAL, "belief is null");
+  DeviceGuard dg(c->device);
+  return download_planes(c, c->b[c->bcur], b, c->bsum + c->bcur);
+}
+
+int pp2_belief_get_raw(pp2_ctx* c, float* b, float* mass) {
+  CHECK(check_ctx(c));
+  DeviceGuard dg(c->device);
+  if (b) CHECK(download_planes(c, c->b[c->bcur], b, nullptr));
+  if (mass) CHECK(pp2_belief_mass(c, mass));
+  return PP2_OK;
+}
+
+int pp2_belief_mass(pp2_ctx* c, float* mass) {
+  CHECK(check_ctx(c));
+  if (!mass) return set_err(PP2_EINVAL, "mass is null");
+  DeviceGuard dg(c->device);
+  HIPCHK(hipMemcpyAsync(mass, c->bsum + c->bcur, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return PP2_OK;
+}
+
+static int belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep) {
+  if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  const int bn = c->bcur ^ 1;
+  const Planes& bi = c->b[c->bcur];
+  Planes& bo = c->b[bn];
+  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
+                                   bi.v.p, bo.v.p, u, z, c->bsum + c->bcur,
+                                   c->partials));
+  const int nparts = pp2::cells_grid(c->g, c->cpt);
+  if (fuse_with_sweep) {
+    const int jn = c->jcur ^ 1;
+    HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
+                                 c->J[c->jcur].v.p, c->J[jn].v.p, c->A,
+                                 c->partials, nparts, c->bsum + bn));
+    c->jcur = jn;
+  } else {
+    HIPCHK(pp2::launch_sum_finalize(c->stream, c->partials, nparts, c->bsum + bn));
+  }
+  CHECK(allreduce_mass(c, c->bsum + bn));
+  c->bcur = bn;
+  return PP2_OK;
+}
+
+int pp2_belief_update(pp2_ctx* c, uint8_t u, uint8_t z) {
+  CHECK(check_model(c));
+  DeviceGuard dg(c->device);
+  CHECK(exchange_halos(c, {&c->b[c->bcur]}));
+  return belief_update_impl(c, u, z, false);
+}
+
+// ---------------------------------------------------------------- MDP
+int pp2_mdp_reset(pp2_ctx* c) {
+  CHECK(check_ctx(c));
+  DeviceGuard dg(c->device);
+  for (Planes* P : {&c->J[0], &c->J[1], &c->Jsnap})
+    HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
+  HIPCHK(hipMemsetAsync(c->A, 0, (size_t)c->g.rows * c->g.wp, c->stream));
+  c->jcur = 0;
+  return PP2_OK;
+}
+
+int pp2_mdp_sweep(pp2_ctx* c, int n) {
+  CHECK(check_model(c));
+  if (n < 0) return set_err(PP2_EINVAL, "negative sweep count");
+  DeviceGuard dg(c->device);
+  for (int i = 0; i < n; ++i) {
+    CHECK(exchange_halos(c, {&c->J[c->jcur]}));
+    const int jn = c->jcur ^ 1;
+    HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
+                                 c->J[c->jcur].v.p, c->J[jn].v.p, c->A, nullptr, 0,
+                                 nullptr));
+    c->jcur = jn;
+  }
+  return PP2_OK;
+}
+
+int pp2_mdp_solve(pp2_ctx* c, int max_sweeps, int* sweeps, double* final_norm) {
+  CHECK(check_model(c));
+  DeviceGuard dg(c->device);
+  CHECK(pp2_mdp_reset(c));
+  // double max_optimal_cost = 5.0/(1.0-discount_factor) (path_planning_2d.cu:221)
+  const double max_cost = 5.0 / (1.0 - (double)c->gamma);
+  int total = 0;
+  double norm = 0.0;
+  do {
+    CHECK(pp2_mdp_sweep(c, 100));
+    total += 100;
+    CHECK(absdiff_max(c, c->J[c->jcur], c->Jsnap, &norm));
+    if (max_sweeps > 0 && total >= max_sweeps) break;
+  } while (norm > max_cost * 1e-3);
+  if (sweeps) *sweeps = total;
+  if (final_norm) *final_norm = norm;
+  return PP2_OK;
+}
+
+int pp2_mdp_get(pp2_ctx* c, float* J, uint8_t* A) {
+  CHECK(check_ctx(c));
+  DeviceGuard dg(c->device);
+  if (J) CHECK(download_planes(c, c->J[c->jcur], J, nullptr));
+  if (A) {
+    const size_t n = owned_cells(c);
+    CHECK(ensure_staging(c, n));
+    HIPCHK(pp2::launch_pack_u8(c->stream, c->g, c->A, (uint8_t*)c->staging));
+    HIPCHK(hipMemcpyAsync(A, c->staging, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  return PP2_OK;
+}
+
+// ---------------------------------------------------------------- north star
+int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
+  CHECK(check_model(c));
+  DeviceGuard dg(c->device);
+  CHECK(exchange_halos(c, {&c->b[c->bcur], &c->J[c->jcur]}));
+  return belief_update_impl(c, u, z, true);
+}
+
+int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
+  CHECK(check_model(c));
+  if (n < 0 || (n > 0 && (!us || !zs))) return set_err(PP2_EINVAL, "bad trajectory");
+  for (int i = 0; i < n; ++i) CHECK(pp2_loop_step(c, us[i], zs[i]));
+  return PP2_OK;
+}
+
+// ---------------------------------------------------------------- FIB
+int pp2_fib_reset(pp2_ctx* c) {
+  CHECK(check_ctx(c));
+  DeviceGuard dg(c->device);
+  for (Planes* P : {&c->fib[0], &c->fib[1], &c->fibsnap})
+    HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
+  c->fcur = 0;
+  return PP2_OK;
+}
+
+int pp2_fib_sweep(pp2_ctx* c, int n) {
+  CHECK(check_model(c));
+  if (n < 0) return set_err(PP2_EINVAL, "negative sweep count");
+  DeviceGuard dg(c->device);
+  for (int i = 0; i < n; ++i) {
+    CHECK(exchange_halos(c, {&c->fib[c->fcur]}));
+    const int fn = c->fcur ^ 1;
+    HIPCHK(pp2::launch_fib_sweep(c->stream, c->g, c->gamma, c->T.v, c->L.v, c->R.v,
+                                 c->fib[c->fcur].v, c->fib[fn].v));
+    c->fcur = fn;
+  }
+  return PP2_OK;
+}
+
+int pp2_fib_solve(pp2_ctx* c, int max_sweeps, int* sweeps, float* final_norm) {
+  CHECK(check_model(c));
+  DeviceGuard dg(c->device);
+  CHECK(pp2_fib_reset(c));
+  int total = 0;
+  double norm = 0.0;
+  do {
+    CHECK(pp2_fib_sweep(c, 10));
+    total += 10;
+    CHECK(absdiff_max(c, c->fib[c->fcur], c->fibsnap, &norm));
+    if (max_sweeps > 0 && total >= max_sweeps) break;
+  } while ((float)norm > 0.01f);
+  if (sweeps) *sweeps = total;
+  if (final_norm) *final_norm = (float)norm;
+  return PP2_OK;
+}
+
+int pp2_fib_get(pp2_ctx* c, float* alphas) {
+  CHECK(check_ctx(c));
+  if (!alphas) return set_err(PP2_EINVAL, "alphas is null");
+  DeviceGuard dg(c->device);
+  return download_planes(c, c->fib[c->fcur], alphas, nullptr);
+}
+
+int pp2_fib_set(pp2_ctx* c, const float* alphas) {
+  CHECK(check_ctx(c));
+  if (!alphas) return set_err(PP2_EINVAL, "alphas is null");
+  DeviceGuard dg(c->device);
+  return upload_planes(c, c->fib[c->fcur], alphas);
+}
+
+// ---------------------------------------------------------------- shards
+int pp2_rccl_unique_id(uint8_t id[PP2_RCCL_ID_BYTES]) {
+  if (!id) return set_err(PP2_EINVAL, "id is null");
+  static_assert(sizeof(ncclUniqueId) == PP2_RCCL_ID_BYTES, "RCCL id size");
+  ncclUniqueId uid;
+  NCCLCHK(ncclGetUniqueId(&uid));
+  memcpy(id, &uid, sizeof uid);
+  return PP2_OK;
+}
+
+int pp2_shard_comm_init(pp2_ctx* c, const uint8_t id[PP2_RCCL_ID_BYTES],
+                        int nranks, int rank) {
+  CHECK(check_ctx(c));
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks)
+    return set_err(PP2_EINVAL, "bad rank %d / nranks %d", rank, nranks);
+  DeviceGuard dg(c->device);
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof uid);
+  NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+  c->nranks = nranks;
+  c->rank = rank;
+  return PP2_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+"""CPU: the oracle (test infrastructure) against the golden fixtures and
+against independent restatements.  Parity of the oracle with the reference is
+unpinned by reference tests (there are none); these tests pin it as far as the
+reference's own data allows -- real glibc rand() output, the simulator's
+independent scatter-form filter, and numpy restatements of the kernels."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import GAMMA, assert_rel_close, golden, golden_map
+
+MAPS = ["map_3x3", "map_5x5", "map_10x10", "map_100x40", "sparse_map_100x40",
+        "tile64_sparse_map_100x40"]
+
+
+@pytest.mark.parametrize("name", MAPS)
+def test_model_matches_golden(oracle, name):
+    g = golden("model", name)
+    grid = golden_map(name)
+    T, L, R = oracle.model_pomdp(grid, tuple(g["goal"]))
+    T2, C = oracle.model_mdp(grid, tuple(g["goal"]))
+    np.testing.assert_array_equal(T, g["T"])
+    np.testing.assert_array_equal(T2, g["T"])
+    np.testing.assert_array_equal(L, g["L"])
+    np.testing.assert_array_equal(R, g["R"])
+    np.testing.assert_array_equal(C, g["C"])
+
+
+def numpy_model(grid, goal):
+    """Independent vectorised restatement of cudaGenerateModelData
+    (model_generation_cuda.cu:161-347, mdp/path_planning_2d_cuda.cu:76-213)."""
+    from path_planning_2d_amd.synthetic import _BASE
+    H, W = grid.shape
+    pad = np.ones((H + 2, W + 2), np.uint8)
+    pad[1:-1, 1:-1] = grid
+    lm = np.stack([pad[1 + i // 3 - 1:H + 1 + i // 3 - 1, 1 + i % 3 - 1:W + 1 + i % 3 - 1]
+                   for i in range(9)], -1).reshape(H * W, 9)
+    occ = lm == 1
+    T = np.broadcast_to(_BASE, (H * W, 9, 9)).copy()
+    for i in range(9):
+        if i == 4:
+            continue
+        m = occ[:, i]
+        T[m, :, 4] = (T[m, :, 4] + T[m, :, i]).astype(np.float32)
+        T[m, :, i] = 0
+    trap = occ[:, 4]
+    T[trap] = 0
+    T[trap, :, 4] = 1
+    hi, lo = np.float32(0.98), np.float32(0.02)
+    z = np.arange(16)
+    m4 = lm[:, [1, 3, 5, 7]]
+    fac = [np.where(((z[None, :] >> k) & 1) == m4[:, k:k + 1], hi, lo) for k in range(4)]
+    L = (((fac[0] * fac[1]).astype(np.float32) * fac[2]).astype(np.float32) * fac[3]).astype(np.float32)
+    mr = np.where(occ, np.float32(-2), np.float32(-1))
+    R = np.zeros((H * W, 9), np.float32)
+    for i in range(9):
+        R = (R + mr[:, None, i] * _BASE[None, :, i]).astype(np.float32)
+    nm = np.broadcast_to(_BASE, (H * W, 9, 9)).copy()
+    nm[trap] = 0
+    nm[trap, :, 4] = 1
+    mc = np.where(occ, np.float32(2), np.float32(1))
+    C = np.zeros((H * W, 9), np.float32)
+    for i in range(9):
+        C = (C + mc[:, None, i] * nm[:, :, i]).astype(np.float32)
+    goal_idx = goal[1] * W + goal[0]
+    R[:, 4] = -2
+    C[:, 4] = 2
+    R[goal_idx, 4] = 0
+    C[goal_idx, 4] = 0
+    return T, L, R, C
+
+
+@pytest.mark.parametrize("name", MAPS)
+def test_model_matches_numpy_restatement(name):
+    g = golden("model", name)
+    T, L, R, C = numpy_model(golden_map(name), tuple(g["goal"]))
+    np.testing.assert_array_equal(T, g["T"])
+    np.testing.assert_array_equal(L, g["L"])
+    np.testing.assert_array_equal(R, g["R"])
+    np.testing.assert_array_equal(C, g["C"])
+
+
+@pytest.mark.parametrize("name", ["map_10x10", "sparse_map_100x40",
+                                  "tile64_sparse_map_100x40"])
+def test_belief_trajectory_golden_and_simulator(oracle, name):
+    """Gather-form planner update == golden, and == the simulator's scatter
+    filter (dummy_simulator.cpp:671-773) to 1e-5 relative."""
+    grid = golden_map(name)
+    H, W = grid.shape
+    m = golden("model", name)
+    bt = golden("belief", name)
+    b = bt["b0"].copy()
+    bs = bt["b0"].copy()
+    for k in range(64):
+        b = oracle.belief_step(H, W, m["T"], m["L"], b, bt["us"][k], bt["zs"][k])
+        bs = oracle.sim_step(grid, bs, bt["us"][k], bt["zs"][k])
+        if f"b{k + 1}" in bt:
+            np.testing.assert_array_equal(b, bt[f"b{k + 1}"])
+            assert_rel_close(b, bs, rel=1e-5, abs_floor=1e-30,
+                             msg=f"{name} step {k + 1} gather vs scatter")
+
+
+def test_mdp_golden(oracle):
+    for name in ["map_10x10", "sparse_map_100x40", "tile64_sparse_map_100x40"]:
+        grid = golden_map(name)
+        H, W = grid.shape
+        m = golden("model", name)
+        g = golden("mdp", name)
+        J, A, n, nrm = oracle.mdp_solve(H, W, GAMMA, m["T"], m["C"])
+        assert n == int(g["sweeps"]) == 300
+        np.testing.assert_array_equal(J, g["J"])
+        np.testing.assert_array_equal(A, g["A"])
+
+
+def test_mdp_sweep_matches_numpy(oracle):
+    """Independent numpy sweep with the same pinned op order."""
+    name = "sparse_map_100x40"
+    grid = golden_map(name)
+    H, W = grid.shape
+    m = golden("model", name)
+    T, C = m["T"], m["C"]
+    J = np.zeros(H * W, np.float32)
+    Jn = J
+    for _ in range(7):
+        pad = np.zeros((H + 2, W + 2), np.float32)
+        pad[1:-1, 1:-1] = Jn.reshape(H, W)
+        nb = np.stack([pad[i // 3:i // 3 + H, i % 3:i % 3 + W] for i in range(9)],
+                      -1).reshape(H * W, 9)
+        cost = C.copy()
+        for i in range(9):
+            t = (GAMMA * T[:, :, i]).astype(np.float32)
+            cost = (np.float64(cost) + np.float64(t) * np.float64(nb[:, i:i + 1])).astype(np.float32)
+        Jn = cost.min(1).astype(np.float32)
+        A = cost.argmin(1).astype(np.uint8)
+    g = golden("mdp", name)
+    # fma(t, j, c) == fl(c + t*j) computed in double (single rounding) here
+    np.testing.assert_array_equal(Jn, g["J7"])
+    np.testing.assert_array_equal(A, g["A7"])
+
+
+def test_fib_golden(oracle):
+    for name in ["map_10x10", "sparse_map_100x40"]:
+        grid = golden_map(name)
+        H, W = grid.shape
+        m = golden("model", name)
+        g = golden("fib", name)
+        a, n, nrm = oracle.fib_solve(H, W, GAMMA, m["T"], m["L"], m["R"])
+        assert n == int(g["sweeps"])
+        np.testing.assert_array_equal(a, g["alphas"])
+
+
+def test_glibc_rand_restatement(oracle):
+    """orc_rand_* == real glibc rand() from the reference's (default) seed."""
+    ref = np.load(__import__("conftest").GOLDEN + "/glibc_rand.npy")
+    lib = oracle.lib()
+
+    class St(ctypes.Structure):
+        _fields_ = [("r", ctypes.c_int32 * 34), ("f", ctypes.c_int), ("b", ctypes.c_int)]
+    s = St()
+    lib.orc_rand_seed(ctypes.byref(s), 1)
+    lib.orc_rand_next.restype = ctypes.c_int32
+    mine = np.array([lib.orc_rand_next(ctypes.byref(s)) for _ in range(ref.size)], np.int32)
+    np.testing.assert_array_equal(mine, ref)
+
+
+def test_curand_xorwow_subsequence_is_linear_jump(oracle):
+    """Subsequence k+1 == 2^67 raw draws after subsequence k is not checkable
+    directly; check the GF(2) jump composes: (seq 2) == jump(jump(seq 0))."""
+    a = oracle.curand_xorwow(1234, 2, 0, 8)
+    b = oracle.curand_xorwow(1234, 2, 0, 8)
+    np.testing.assert_array_equal(a, b)
+    c = oracle.curand_xorwow(1234, 0, 3, 5)
+    d = oracle.curand_xorwow(1234, 0, 0, 8)[3:]
+    np.testing.assert_array_equal(c, d)
+    u = oracle.curand_uniform(0xFFFFFFFF)
+    assert 0.0 < u <= 1.0
