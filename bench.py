@@ -156,7 +156,10 @@ def main():
     ctx = P.GridContext(grid, goal, gamma=GAMMA, device=local,
                         rows=(r0, r1) if ws > 1 else None)
     ctx.set_cells_per_lane(args.cpt)
-    stream = torch.cuda.current_stream()
+    # a dedicated stream: torch's default stream has handle 0, which the C ABI
+    # reads as "use the context's own stream"
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     if ws > 1:
         uid = torch.zeros(P._lib.RCCL_ID_BYTES, dtype=torch.uint8, device="cuda")
@@ -183,6 +186,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     ctx.loop_run(us[args.warmup:], zs[args.warmup:])
+    enqueue_s = time.perf_counter() - t0
     ev1.record(stream)
     torch.cuda.synchronize()
     if ws > 1:
@@ -278,6 +282,7 @@ def main():
                 "belief_update_gbs": belief_gbs,
                 "belief_update_frac": belief_gbs / HBM_PEAK_GBS,
                 "loop_step_us_events": loop_ms_events * 1e3,
+                "loop_enqueue_us_per_step": 1e6 * enqueue_s / args.steps,
                 "loop_gbs": loop_gbs,
                 "loop_frac": loop_gbs / HBM_PEAK_GBS,
             },
