@@ -53,6 +53,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline sample budget (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--plan-steps", type=int, default=200,
+                    help="QV-tree plan steps for the p50 (0 disables)")
+    ap.add_argument("--plan-size", type=int, default=256)
+    ap.add_argument("--plan-depth", type=int, default=3)
+    ap.add_argument("--cpu-plan-seconds", type=float, default=15.0)
     ap.add_argument("--profile", action="store_true",
                     help="only run warmup+timed steps (for rocprofv3)")
     return ap.parse_args()
@@ -115,6 +120,87 @@ def cpu_baseline(grid, goal, us, zs, budget_s):
                       f"({el:.1f} s, oracle/pp2_oracle.c -O3 -march=native, "
                       f"1 thread)",
             "cpu": cpu_model()}
+
+
+def plan_step_bench(args, device, stream_handle, with_cpu):
+    """BASELINE configs[1]: 256x256 synthetic grid, POMDP belief update +
+    QV-tree with max_search_tree_depth 3 (FIB upper bound, constant lower
+    bound -5/(1-gamma)).  Closed loop: the planner's action moves a simulated
+    robot (T), whose observation (L) is the next message.  Wall time of each
+    plan step (tree update + expansions + argmax), as beliefCallback measures
+    it (src/pomdp/path_planning_2d.cu:210-231)."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    N = args.plan_size
+    grid = S.synth_grid(N, N, seed=N)
+    goal = S.synth_goal(grid)
+    ctx = P.GridContext(grid, goal, gamma=GAMMA, device=device)
+    ctx.set_stream(stream_handle)
+    ctx.model_generate()
+    t0 = time.perf_counter()
+    fib_sweeps, _ = ctx.fib_solve()
+    fib_s = time.perf_counter() - t0
+    alphas = ctx.fib_get()
+    b0 = S.uniform_belief(grid)
+
+    def run(step_fn, max_steps, budget_s):
+        rng = S.SplitMix64(99)
+        x, y = S.start_cell(grid)
+        times = []
+        a, z, first = 0, 0, True
+        t_start = time.perf_counter()
+        for _ in range(max_steps):
+            t = time.perf_counter()
+            a, _ = step_fn(a, z, b0 if first else None)
+            times.append(time.perf_counter() - t)
+            first = False
+            tp = S.cell_transition(grid, x, y, a)
+            r, c, j = rng.u01(), 0.0, 4
+            for i in range(9):
+                c += float(tp[i])
+                if tp[i] > 0 and r < c:
+                    j = i
+                    break
+            x += j % 3 - 1
+            y += j // 3 - 1
+            lk = S.cell_likelihood(grid, x, y)
+            r, c, z = rng.u01(), 0.0, 15
+            for i in range(16):
+                c += float(lk[i])
+                if r < c:
+                    z = i
+                    break
+            if time.perf_counter() - t_start > budget_s:
+                break
+        ms = np.array(times) * 1e3
+        return ms
+
+    with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
+                         max_online_iteration=15) as pl:
+        run(pl.step, 3, 1e9)  # warm-up (code objects, allocations)
+        pl.reset()
+        ms = run(pl.step, args.plan_steps, 1e9)
+        info = pl.info()
+    ctx.close()
+    out = {"config": f"{N}x{N} synthetic grid, max_search_tree_depth {args.plan_depth}, "
+                     f"max_online_iteration 15, FIB upper bound ({fib_sweeps} sweeps, "
+                     f"{fib_s * 1e3:.1f} ms on GPU), lower bound -5/(1-gamma)",
+           "steps": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
+           "p90_ms": float(np.percentile(ms, 90)), "mean_ms": float(ms.mean()),
+           "first_ms": float(ms[0]), "final_tree_vnodes": int(info["total_vnodes"])}
+    if with_cpu:
+        from oracle import oracle as O
+        T, L, R = O.model_pomdp(grid, goal)
+        opl = O.Planner(grid, T, L, R, alphas, max_depth=args.plan_depth, max_iter=15)
+        cms = run(opl.step, args.plan_steps, args.cpu_plan_seconds)
+        opl.close()
+        out["cpu_baseline"] = {
+            "p50_ms": float(np.percentile(cms, 50)), "p90_ms": float(np.percentile(cms, 90)),
+            "steps": int(cms.size), "cores": 1, "kind": "port",
+            "sample": f"{cms.size} closed-loop plan steps of the oracle's reference-semantics "
+                      f"QV-tree (oracle/pp2_oracle_tree.c, every node holds a host belief), "
+                      f"same grid/alphas"}
+    return out
 
 
 def cpu_model():
@@ -239,12 +325,16 @@ def main():
     traffic, traffic_src = pmc_traffic("k_mdp_sweep", cells_per_gpu)
 
     result = None
+    plan = None
+    if rank == 0 and ws == 1 and args.plan_steps > 0:
+        plan = plan_step_bench(args, local, stream.cuda_stream,
+                               with_cpu=not args.no_cpu_baseline)
     if rank == 0:
         cpu = None
         if ws == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(grid, goal, us, zs, args.cpu_seconds)
         result = {
-            "metric": "grid cells/sec for belief-update+Bellman loop, 1024x1024",
+            "metric": "grid cells/sec for belief-update+Bellman loop, 1024x1024; plan step p50 ms",
             "value": value,
             "unit": "cells/s",
             "n_gpus": ws,
@@ -287,6 +377,7 @@ def main():
                 "loop_frac": loop_gbs / HBM_PEAK_GBS,
             },
             "belief_mass_ok": mass_ok,
+            "plan_step": plan,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result))

@@ -158,6 +158,67 @@ int pp2_fib_solve(pp2_ctx* ctx, int max_sweeps, int* sweeps, float* final_norm);
 int pp2_fib_get(pp2_ctx* ctx, float* alphas);
 int pp2_fib_set(pp2_ctx* ctx, const float* alphas);
 
+/* ---------------------------------------------------------------- QV-tree
+ * Online POMDP planner: QNode / VNode / SearchTree
+ * (include/path_planning_2d/search_tree.h:31-165, src/pomdp/
+ * search_tree_cuda.cu:161-626) driven like PomdpPathPlanning2d::beliefCallback
+ * (src/pomdp/path_planning_2d.cu:199-241).  Tree logic runs on the host
+ * exactly as the reference; every belief update, renormalisation and leaf
+ * bound of one VNode::expand (9 actions x all observations) is one batched
+ * device pass over the context's model (T, L, R) and FIB alphas (set them
+ * with pp2_fib_solve / pp2_fib_set first).  Beliefs of expanded nodes stay
+ * on the device; leaf children are scored without being materialised.
+ *
+ * Sampling follows the reference bit for bit in algorithm: 50 state samples
+ * per QNode from glibc rand() over the fp32 prefix sum of the belief
+ * (search_tree_cuda.cu:326-337), next state and observation from the cuRAND
+ * XORWOW stream curand_init(1234, idx, 0) that every QNode re-creates
+ * (:84-147, :318-323). */
+typedef struct pp2_planner pp2_planner;
+
+typedef struct {
+  int32_t max_search_tree_depth;  /* launch default 50 */
+  int32_t max_online_iteration;   /* launch default 15 */
+  int32_t lower_bound_mode;       /* 0: constant -5/(1-gamma), the reference's
+                                     fallback (search_tree_cuda.cu:382-383) */
+  uint32_t rand_seed;             /* glibc srand seed; reference never seeds: 1 */
+  uint32_t sample_num;            /* observation samples per QNode (:176): 50 */
+  uint64_t curand_seed;           /* curand_init seed (:90): 1234 */
+} pp2_planner_params;
+
+/* Snapshot of the root and its children, for inspection and parity tests. */
+typedef struct {
+  uint32_t depth;
+  float root_upper_bound, root_lower_bound, root_heuristic;
+  uint32_t n_root_children;  /* 0 (unexpanded) or 9 */
+  float q_upper_bound[9], q_lower_bound[9], q_reward[9], q_heuristic[9];
+  uint32_t q_depth[9], q_nchildren[9];
+  uint8_t q_obs[9][16];
+  float q_weight[9][16], v_upper_bound[9][16], v_lower_bound[9][16];
+  uint32_t total_vnodes, total_qnodes, expansions;
+} pp2_tree_info;
+
+int pp2_planner_default_params(pp2_planner_params* p);
+/* PomdpPathPlanning2d::initialize tail (src/pomdp/path_planning_2d.cu:145-155):
+ * binds the planner to a context whose model and FIB alphas are ready. */
+int pp2_planner_create(pp2_planner** out, pp2_ctx* ctx,
+                       const pp2_planner_params* params);
+int pp2_planner_destroy(pp2_planner* p);
+/* One plan step = beliefCallback (:199-241): first call (or after reset)
+ * builds the tree from `belief` (hw floats, used as given); later calls
+ * re-root with (action, observation).  Expands while depth < max depth and
+ * fewer than max_online_iteration expansions, then returns the action with
+ * the largest Q upper bound. */
+int pp2_planner_step(pp2_planner* p, uint8_t action, uint8_t observation,
+                     const float* belief, uint8_t* new_action,
+                     float* new_value);
+/* resetSearchTreeCallback (:275-282). */
+int pp2_planner_reset(pp2_planner* p);
+int pp2_planner_info(pp2_planner* p, pp2_tree_info* info);
+/* The 2*n curand_uniform draws the reference's cudaForwardSampling sees:
+ * u1[i], u2[i] = first and second draw of curand_init(seed, i, 0). */
+int pp2_curand_uniforms(uint64_t seed, int n, float* u1, float* u2);
+
 /* ---------------------------------------------------------------- shards
  * RCCL bootstrap for row shards (no reference counterpart).  Rank 0 calls
  * pp2_rccl_unique_id, the 128 bytes are broadcast out of band, then every

@@ -27,9 +27,10 @@ _u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "pp2_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or (
-            os.path.getmtime(LIB_PATH) < os.path.getmtime(src)):
+    srcs = [os.path.join(HERE, f) for f in
+            ("pp2_oracle.c", "pp2_oracle_tree.c", "pp2_oracle.h")]
+    if force or not os.path.exists(LIB_PATH) or any(
+            os.path.getmtime(LIB_PATH) < os.path.getmtime(s) for s in srcs):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -66,6 +67,13 @@ def lib():
             "orc_synth_map": (None, [I, I, C.c_uint64, D, _u8p]),
             "orc_synth_goal": (I, [I, I, _u8p, C.POINTER(I), C.POINTER(I)]),
             "orc_synth_trajectory": (I, [I, I, _u8p, I, I, C.c_uint64, I, _u8p, _u8p, _i32p]),
+            "orc_planner_create": (C.c_void_p, [I, I, _f32p, _f32p, _f32p, _f32p, F, I, I,
+                                                C.c_uint32, C.c_uint32, C.c_uint64]),
+            "orc_planner_step": (I, [C.c_void_p, C.c_uint8, C.c_uint8, C.c_void_p,
+                                     C.POINTER(C.c_uint8), C.POINTER(F)]),
+            "orc_planner_reset": (None, [C.c_void_p]),
+            "orc_planner_info": (None, [C.c_void_p, C.c_void_p]),
+            "orc_planner_destroy": (None, [C.c_void_p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -221,3 +229,72 @@ def synth_trajectory(grid, goal, seed, n):
     if rc != 0:
         raise ValueError("no free start cell")
     return us, zs, st
+
+
+# ---------------------------------------------------------------- QV-tree
+class TreeInfo(C.Structure):
+    _fields_ = [("depth", C.c_uint32), ("root_upper_bound", C.c_float),
+                ("root_lower_bound", C.c_float), ("root_heuristic", C.c_float),
+                ("n_root_children", C.c_uint32),
+                ("q_upper_bound", C.c_float * 9), ("q_lower_bound", C.c_float * 9),
+                ("q_reward", C.c_float * 9), ("q_heuristic", C.c_float * 9),
+                ("q_depth", C.c_uint32 * 9), ("q_nchildren", C.c_uint32 * 9),
+                ("q_obs", (C.c_uint8 * 16) * 9), ("q_weight", (C.c_float * 16) * 9),
+                ("v_upper_bound", (C.c_float * 16) * 9),
+                ("v_lower_bound", (C.c_float * 16) * 9),
+                ("total_vnodes", C.c_uint32), ("total_qnodes", C.c_uint32),
+                ("expansions", C.c_uint32)]
+
+    def as_dict(self):
+        out = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            out[name] = np.ctypeslib.as_array(v).copy() if hasattr(v, "_length_") else v
+        return out
+
+
+class Planner:
+    """The reference QV-tree planner restated on the host (every node keeps
+    its own belief; sequential fp32 sums; linear find_if sampling)."""
+
+    def __init__(self, grid, T, L, R, alphas, gamma=0.95, max_depth=50,
+                 max_iter=15, rand_seed=1, sample_num=50, curand_seed=1234):
+        H, W = grid.shape
+        self.n = H * W
+        self._keep = [np.ascontiguousarray(a, np.float32) for a in (T, L, R, alphas)]
+        self._h = lib().orc_planner_create(H, W, *self._keep, float(gamma),
+                                           int(max_depth), int(max_iter), rand_seed,
+                                           sample_num, curand_seed)
+
+    def step(self, action, observation, belief=None):
+        a = C.c_uint8()
+        v = C.c_float()
+        bp = None
+        if belief is not None:
+            belief = np.ascontiguousarray(belief, np.float32)
+            self._b = belief
+            bp = belief.ctypes.data_as(C.c_void_p)
+        rc = lib().orc_planner_step(self._h, int(action), int(observation), bp,
+                                    C.byref(a), C.byref(v))
+        if rc != 0:
+            raise RuntimeError(f"orc_planner_step failed ({rc})")
+        return a.value, v.value
+
+    def reset(self):
+        lib().orc_planner_reset(self._h)
+
+    def info(self):
+        t = TreeInfo()
+        lib().orc_planner_info(self._h, C.byref(t))
+        return t.as_dict()
+
+    def close(self):
+        if self._h:
+            lib().orc_planner_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -130,6 +130,29 @@ int orc_synth_trajectory(int H, int W, const uint8_t* map, int gx, int gy,
                          uint64_t seed, int n, uint8_t* us, uint8_t* zs,
                          int32_t* states);
 
+/* ---- QV-tree online planner (a6-a8), pp2_oracle_tree.c ---------------------- */
+typedef struct {
+  uint32_t depth;
+  float root_upper_bound, root_lower_bound, root_heuristic;
+  uint32_t n_root_children;
+  float q_upper_bound[9], q_lower_bound[9], q_reward[9], q_heuristic[9];
+  uint32_t q_depth[9], q_nchildren[9];
+  uint8_t q_obs[9][16];
+  float q_weight[9][16], v_upper_bound[9][16], v_lower_bound[9][16];
+  uint32_t total_vnodes, total_qnodes, expansions;
+} orc_tree_info;
+typedef struct orc_planner orc_planner;
+/* T, L, R, alphas are borrowed (reference layouts; alphas [hw][9]). */
+orc_planner* orc_planner_create(int H, int W, const float* T, const float* L,
+                                const float* R, const float* alphas, float gamma,
+                                int max_depth, int max_iter, uint32_t rand_seed,
+                                uint32_t sample_num, uint64_t curand_seed);
+int orc_planner_step(orc_planner* p, uint8_t a, uint8_t z, const float* belief,
+                     uint8_t* new_action, float* new_value);
+void orc_planner_reset(orc_planner* p);
+void orc_planner_info(orc_planner* p, orc_tree_info* info);
+void orc_planner_destroy(orc_planner* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,7 +7,8 @@ package is the Python host mirror of that boundary.
 """
 from ._lib import Pp2Error, LIB_PATH
 from .core import GridContext, device_count
+from .planner import QVTreePlanner
 from . import maps, synthetic
 
-__all__ = ["GridContext", "device_count", "Pp2Error", "LIB_PATH", "maps",
-           "synthetic"]
+__all__ = ["GridContext", "QVTreePlanner", "device_count", "Pp2Error",
+           "LIB_PATH", "maps", "synthetic"]

@@ -70,6 +70,13 @@ SIGNATURES = {
     "pp2_fib_solve": [_vp, C.c_int, _i32p, _f32p],
     "pp2_fib_get": [_vp, _f32p],
     "pp2_fib_set": [_vp, _f32p],
+    "pp2_planner_default_params": [_vp],
+    "pp2_planner_create": [C.POINTER(_vp), _vp, _vp],
+    "pp2_planner_destroy": [_vp],
+    "pp2_planner_step": [_vp, C.c_uint8, C.c_uint8, _f32p, _u8p, _f32p],
+    "pp2_planner_reset": [_vp],
+    "pp2_planner_info": [_vp, _vp],
+    "pp2_curand_uniforms": [C.c_uint64, C.c_int, _f32p, _f32p],
     "pp2_rccl_unique_id": [_u8p],
     "pp2_shard_comm_init": [_vp, _u8p, C.c_int, C.c_int],
 }

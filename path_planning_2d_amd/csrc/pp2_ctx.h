@@ -1,0 +1,109 @@
+// pp2_ctx.h -- private: the context struct and helpers shared by the C-ABI
+// translation units (pp2_runtime.cpp, pp2_tree.cpp).  Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <initializer_list>
+#include <string>
+
+#include "pp2.h"
+#include "pp2_internal.h"
+
+using pp2::Geom;
+using pp2::PlaneSet;
+
+namespace pp2rt {
+
+int set_err(int code, const char* fmt, ...);
+
+#define HIPCHK(expr)                                                        \
+  do {                                                                      \
+    hipError_t e_ = (expr);                                                 \
+    if (e_ != hipSuccess)                                                   \
+      return set_err(PP2_EHIP, "%s failed: %s (%s:%d)", #expr,              \
+                     hipGetErrorString(e_), __FILE__, __LINE__);            \
+  } while (0)
+
+#define NCCLCHK(expr)                                                       \
+  do {                                                                      \
+    ncclResult_t r_ = (expr);                                               \
+    if (r_ != ncclSuccess)                                                  \
+      return set_err(PP2_ERCCL, "%s failed: %s", #expr,                     \
+                     ncclGetErrorString(r_));                               \
+  } while (0)
+
+#define CHECK(expr)                 \
+  do {                              \
+    int s_ = (expr);                \
+    if (s_ != PP2_OK) return s_;    \
+  } while (0)
+
+constexpr int kGuard = 64;  // floats of guard before/after each plane set
+
+// A set of K planes over rows [-1, rows] (one halo row each side).
+struct Planes {
+  float* alloc = nullptr;
+  size_t floats = 0;
+  PlaneSet v{nullptr, 0, 0};
+  int K = 0;
+};
+
+}  // namespace pp2rt
+
+using pp2rt::Planes;
+using pp2rt::set_err;
+
+struct pp2_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  Geom g{};
+  int32_t gx = 0, gy = 0;
+  float gamma = 0.95f;
+  int cpt = 4;
+  bool model_ready = false;
+
+  uint8_t* d_map = nullptr;  // global map (grows x width)
+  Planes T, L, R, C;         // 81, 16, 9, 9 planes
+  Planes b[2];               // belief ping-pong (1 plane)
+  int bcur = 0;
+  float* bsum = nullptr;     // device float[2]: mass of b[0], b[1]
+  Planes J[2], Jsnap;        // value ping-pong + convergence snapshot
+  int jcur = 0;
+  uint8_t* A = nullptr;      // rows * wp actions
+  Planes fib[2], fibsnap;    // FIB alphas (9 planes)
+  int fcur = 0;
+  float* partials = nullptr;   // belief partial sums
+  float* rpartials = nullptr;  // convergence-check partials
+  int partials_cap = 0;
+  void* staging = nullptr;     // dense host-layout staging buffer
+  size_t staging_bytes = 0;
+
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace pp2rt {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int alloc_planes(pp2_ctx* c, Planes* P, int K);
+void free_planes(Planes* P);
+int ensure_staging(pp2_ctx* c, size_t bytes);
+int check_ctx(pp2_ctx* c);
+int check_model(pp2_ctx* c);
+size_t owned_cells(const pp2_ctx* c);
+int download_planes(pp2_ctx* c, const Planes& P, float* host, const float* divide_by);
+int upload_planes(pp2_ctx* c, Planes& P, const float* host);
+
+}  // namespace pp2rt

@@ -62,4 +62,17 @@ hipError_t launch_unpack(hipStream_t st, const Geom& g, int K,
 hipError_t launch_pack_u8(hipStream_t st, const Geom& g, const uint8_t* src,
                           uint8_t* dense);
 
+// QV-tree expansion: rewards_out[9] = sum_x b(x) R_a(x);
+// stats_out[z][a][10] = {sum_x c, sum_x c*alpha_i}, c = (T_a^T b)(x) L_z(x).
+// rpartials >= tiles*9 floats, spartials >= tiles*16*90 floats, P = 9 planes.
+hipError_t launch_expand(hipStream_t st, const Geom& g, int cpt, PlaneSet T,
+                         const float* b, PlaneSet R, PlaneSet L, PlaneSet F,
+                         PlaneSet P, float* rpartials, float* spartials,
+                         float* rewards_out, float* stats_out);
+// out[0] = sum b, out[1+i] = sum b*alpha_i; partials >= tiles*10 floats
+hipError_t launch_belief_dots(hipStream_t st, const Geom& g, int cpt,
+                              const float* b, PlaneSet F, float* partials,
+                              float* out);
+hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* mass);
+
 }  // namespace pp2

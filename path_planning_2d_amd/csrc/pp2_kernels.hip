@@ -501,6 +501,227 @@ hipError_t launch_sum_cells(hipStream_t st, const Geom& g, const float* b,
 }
 
 // ============================================================================
+// (a6/a7) QV-tree expansion, batched.  One VNode::expand
+// (src/pomdp/search_tree_cuda.cu:437-450) builds 9 QNodes, each running the
+// belief update for every sampled observation z, renormalising, and scoring
+// the child with the FIB upper bound (fast_informed_bound_cuda.cu:278-297).
+// Here the 9 predictions pred_a = T_a^T b are computed once (k_expand_pred),
+// then every (a, z) child's mass  m[a][z] = sum_x pred_a(x) L_z(x)  and FIB
+// dots d[a][z][i] = sum_x (pred_a(x) L_z(x)) alpha_i(x) come out of one pass
+// (k_expand_stats), whatever subset the sampler later keeps.  The child
+// belief pred_a * L_z is the reference kernel's output bit for bit; the sums
+// are fixed-order tree reductions.
+// ============================================================================
+constexpr int kStats = 10;  // per child: mass + 9 FIB dots
+
+template <int CPT>
+__global__ __launch_bounds__(kBlock) void k_expand_pred(
+    Geom g, PlaneSet T, const float* __restrict__ b, PlaneSet R, PlaneSet P,
+    float* __restrict__ rpartials) {
+  __shared__ float red[4][9];
+  const int tpr = g.wp / CPT;
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / tpr);
+  const int x0 = (int)(t % tpr) * CPT;
+  float rew[9];
+#pragma unroll
+  for (int a = 0; a < 9; ++a) rew[a] = 0.0f;
+  if (y < g.rows) {
+    const bool le = x0 == 0, re = x0 + CPT == g.wp;
+    float bv[9][CPT];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int oy = s / 3 - 1, ox = s % 3 - 1;
+      const float* bp = b + (long long)(y + oy) * g.wp + x0 + ox;
+      if (ox == 0) ldv<CPT, true>(bp, bv[s]);
+      else ldv<CPT, false>(bp, bv[s]);
+      if (ox < 0 && le) bv[s][0] = 0.0f;
+      if (ox > 0 && re) bv[s][CPT - 1] = 0.0f;
+    }
+    for (int a = 0; a < 9; ++a) {
+      float p[CPT];
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) p[k] = 0.0f;
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {
+        const int oy = s / 3 - 1, ox = s % 3 - 1;
+        const float* tp = T.p + (long long)(y + oy) * T.rs +
+                          (long long)(9 * a + 8 - s) * T.ps + x0 + ox;
+        float tv[CPT];
+        if (ox == 0) ldv<CPT, true>(tp, tv);
+        else ldv<CPT, false>(tp, tv);
+        if (ox < 0 && le) tv[0] = 0.0f;
+        if (ox > 0 && re) tv[CPT - 1] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) p[k] = __builtin_fmaf(tv[k], bv[s][k], p[k]);
+      }
+      stv<CPT>(P.p + (long long)y * P.rs + (long long)a * P.ps + x0, p);
+      float rv[CPT];
+      ldv<CPT, true>(R.p + (long long)y * R.rs + (long long)a * R.ps + x0, rv);
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) rew[a] += bv[4][k] * rv[k];
+    }
+  }
+  // QNode reward <b, R[:,a]> partials (search_tree_cuda.cu:168-173)
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int a = 0; a < 9; ++a) {
+    const float v = wave_sum(rew[a]);
+    if ((threadIdx.x & 63) == 0) red[w][a] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    const int a = threadIdx.x;
+    rpartials[(long long)blockIdx.x * 9 + a] = ((red[0][a] + red[1][a]) + red[2][a]) + red[3][a];
+  }
+}
+
+// grid = (cell tiles) x 16 observations; partials[tile][z][a][kStats]
+template <int CPT>
+__global__ __launch_bounds__(kBlock) void k_expand_stats(
+    Geom g, PlaneSet P, PlaneSet L, PlaneSet F, float* __restrict__ partials) {
+  __shared__ float red[4][9 * kStats];
+  const int z = blockIdx.y;
+  const int tpr = g.wp / CPT;
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / tpr);
+  const int x0 = (int)(t % tpr) * CPT;
+  float acc[9][kStats];
+#pragma unroll
+  for (int a = 0; a < 9; ++a)
+#pragma unroll
+    for (int i = 0; i < kStats; ++i) acc[a][i] = 0.0f;
+  if (y < g.rows) {
+    float lv[CPT], fv[9][CPT];
+    ldv<CPT, true>(L.p + (long long)y * L.rs + (long long)z * L.ps + x0, lv);
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+      ldv<CPT, true>(F.p + (long long)y * F.rs + (long long)i * F.ps + x0, fv[i]);
+#pragma unroll
+    for (int a = 0; a < 9; ++a) {
+      float pv[CPT];
+      ldv<CPT, true>(P.p + (long long)y * P.rs + (long long)a * P.ps + x0, pv);
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) {
+        const float c = pv[k] * lv[k];  // the reference kernel's child value
+        acc[a][0] += c;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) acc[a][1 + i] = __builtin_fmaf(c, fv[i][k], acc[a][1 + i]);
+      }
+    }
+  }
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int a = 0; a < 9; ++a)
+#pragma unroll
+    for (int i = 0; i < kStats; ++i) {
+      const float v = wave_sum(acc[a][i]);
+      if ((threadIdx.x & 63) == 0) red[w][a * kStats + i] = v;
+    }
+  __syncthreads();
+  if (threadIdx.x < 9 * kStats) {
+    const int j = threadIdx.x;
+    partials[((long long)blockIdx.x * 16 + z) * (9 * kStats) + j] =
+        ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+  }
+}
+
+// sum / FIB dots of one belief: out[0] = sum b, out[1+i] = sum b*alpha_i
+template <int CPT>
+__global__ __launch_bounds__(kBlock) void k_belief_dots(Geom g, const float* __restrict__ b,
+                                                        PlaneSet F, float* __restrict__ partials) {
+  __shared__ float red[4][kStats];
+  const int tpr = g.wp / CPT;
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / tpr);
+  const int x0 = (int)(t % tpr) * CPT;
+  float acc[kStats];
+#pragma unroll
+  for (int i = 0; i < kStats; ++i) acc[i] = 0.0f;
+  if (y < g.rows) {
+    float bv[CPT];
+    ldv<CPT, true>(b + (long long)y * g.wp + x0, bv);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) acc[0] += bv[k];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      float fv[CPT];
+      ldv<CPT, true>(F.p + (long long)y * F.rs + (long long)i * F.ps + x0, fv);
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) acc[1 + i] = __builtin_fmaf(bv[k], fv[k], acc[1 + i]);
+    }
+  }
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < kStats; ++i) {
+    const float v = wave_sum(acc[i]);
+    if ((threadIdx.x & 63) == 0) red[w][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kStats)
+    partials[(long long)blockIdx.x * kStats + threadIdx.x] =
+        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+// out[j] = sum_r partials[r][j], fixed order over r (r = 0..rows-1)
+__global__ __launch_bounds__(kBlock) void k_reduce_columns(const float* __restrict__ partials,
+                                                           int rows, int cols, float* __restrict__ out) {
+  const int j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= cols) return;
+  float s = 0.0f;
+  for (int r = 0; r < rows; ++r) s += partials[(long long)r * cols + j];
+  out[j] = s;
+}
+
+// b := b / *mass over owned cells (materialise a normalised belief in place)
+__global__ __launch_bounds__(kBlock) void k_scale(Geom g, float* __restrict__ b,
+                                                  const float* __restrict__ mass) {
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= (long long)g.rows * g.wp) return;
+  b[t] = b[t] / *mass;
+}
+
+hipError_t launch_expand(hipStream_t st, const Geom& g, int cpt, PlaneSet T,
+                         const float* b, PlaneSet R, PlaneSet L, PlaneSet F,
+                         PlaneSet P, float* rpartials, float* spartials,
+                         float* rewards_out, float* stats_out) {
+  const int tiles = cells_grid(g, cpt);
+  switch (cpt) {
+    case 4:
+      hipLaunchKernelGGL(k_expand_pred<4>, dim3(tiles), dim3(kBlock), 0, st, g, T, b, R, P, rpartials);
+      hipLaunchKernelGGL(k_expand_stats<4>, dim3(tiles, 16), dim3(kBlock), 0, st, g, P, L, F, spartials);
+      break;
+    default:
+      hipLaunchKernelGGL(k_expand_pred<1>, dim3(tiles), dim3(kBlock), 0, st, g, T, b, R, P, rpartials);
+      hipLaunchKernelGGL(k_expand_stats<1>, dim3(tiles, 16), dim3(kBlock), 0, st, g, P, L, F, spartials);
+      break;
+  }
+  hipLaunchKernelGGL(k_reduce_columns, dim3(1), dim3(kBlock), 0, st, rpartials, tiles, 9, rewards_out);
+  const int cols = 16 * 9 * kStats;
+  hipLaunchKernelGGL(k_reduce_columns, dim3((cols + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                     spartials, tiles, cols, stats_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_belief_dots(hipStream_t st, const Geom& g, int cpt, const float* b,
+                              PlaneSet F, float* partials, float* out) {
+  const int tiles = cells_grid(g, cpt);
+  if (cpt == 4)
+    hipLaunchKernelGGL(k_belief_dots<4>, dim3(tiles), dim3(kBlock), 0, st, g, b, F, partials);
+  else
+    hipLaunchKernelGGL(k_belief_dots<1>, dim3(tiles), dim3(kBlock), 0, st, g, b, F, partials);
+  hipLaunchKernelGGL(k_reduce_columns, dim3(1), dim3(kBlock), 0, st, partials, tiles, kStats, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* mass) {
+  const long long n = (long long)g.rows * g.wp;
+  hipLaunchKernelGGL(k_scale, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                     g, b, mass);
+  return hipGetLastError();
+}
+
+// ============================================================================
 // Layout conversion between the reference's AoS host arrays
 // (T[hw][9][9], L[hw][16], R[hw][9], beliefs[hw]) and the SoA planes.
 // ============================================================================

@@ -1,0 +1,656 @@
+// pp2_tree.cpp -- online QV-tree planner (C ABI pp2_planner_*, include/pp2.h).
+//
+// Host tree logic restates QNode / VNode / SearchTree
+// (include/path_planning_2d/search_tree.h:31-165,
+//  src/pomdp/search_tree_cuda.cu:161-626) and the plan step of
+// PomdpPathPlanning2d::beliefCallback (src/pomdp/path_planning_2d.cu:199-241).
+// What changes is where the per-cell work runs: one VNode::expand issues one
+// batched device pass (pp2::launch_expand) that scores every (action,
+// observation) child at once, while the host draws the reference's samples;
+// beliefs are materialised on the device only for nodes that get expanded.
+// Host arithmetic is plain fp32 (built with -ffp-contract=off), as the
+// reference's x86 host code.
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstring>
+#include <set>
+#include <vector>
+
+#include <rocrand/rocrand_xorwow.h>
+
+#include "pp2_ctx.h"
+
+using namespace pp2rt;
+
+namespace {
+
+// glibc random_r, TYPE_3 (x**31 + x**3 + 1), as srand(seed) / rand().
+struct GlibcRand {
+  int32_t r[31];
+  int f = 3, b = 0;
+  void seed(uint32_t s) {
+    int64_t word = (int32_t)(s == 0 ? 1 : s);
+    r[0] = (int32_t)word;
+    for (int i = 1; i < 31; ++i) {
+      const int64_t hi = word / 127773, lo = word % 127773;
+      word = 16807 * lo - 2836 * hi;
+      if (word < 0) word += 2147483647;
+      r[i] = (int32_t)word;
+    }
+    f = 3;
+    b = 0;
+    for (int i = 0; i < 310; ++i) (void)next();
+  }
+  int32_t next() {
+    const uint32_t val = (uint32_t)r[f] + (uint32_t)r[b];
+    r[f] = (int32_t)val;
+    if (++f >= 31) {
+      f = 0;
+      ++b;
+    } else if (++b >= 31) {
+      b = 0;
+    }
+    return (int32_t)(val >> 1);
+  }
+};
+
+// cuRAND XORWOW as curand_init(seed, subsequence, 0) seeds it (CUDA 8
+// curand_kernel.h: salted seed halves, then skipahead by subsequence * 2^67);
+// the 2^67 jump comes from rocRAND's precomputed XORWOW jump matrices.
+struct CurandXorwow : rocrand_device::xorwow_engine {
+  CurandXorwow(uint64_t seed, uint64_t subsequence)
+      : rocrand_device::xorwow_engine(0ULL, 0ULL, 0ULL) {
+    const uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
+    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0;
+    const uint32_t t1 = 2591861531u * s1;
+    m_state.d = 6615241u + t1 + t0;
+    m_state.x[0] = 123456789u + t0;
+    m_state.x[1] = 362436069u ^ t0;
+    m_state.x[2] = 521288629u + t1;
+    m_state.x[3] = 88675123u ^ t1;
+    m_state.x[4] = 5783321u + t0;
+    discard_subsequence(subsequence);
+  }
+};
+
+inline float curand_uniform_of(uint32_t x) {
+  const float inv = 2.3283064e-10f;  // CURAND_2POW32_INV
+  return fmaf((float)x, inv, inv / 2.0f);
+}
+
+struct QNode;
+
+struct VNode {
+  uint8_t observation = 0;
+  float weight = 0.0f;
+  QNode* parent = nullptr;
+  std::vector<QNode*> children;
+  float upper_bound = FLT_MAX;
+  float lower_bound = -FLT_MAX;
+  float heuristic = FLT_MIN;
+  VNode* vnode_to_expand = nullptr;
+  uint32_t depth = 0;
+  int slot = -1;  // device belief slot, -1 = not materialised
+};
+
+struct QNode {
+  uint8_t action = 0;
+  VNode* parent = nullptr;
+  std::vector<VNode*> children;
+  float upper_bound = FLT_MAX;
+  float lower_bound = -FLT_MAX;
+  float heuristic = FLT_MIN;
+  float reward = 0.0f;
+  VNode* vnode_to_expand = nullptr;
+  uint32_t depth = 1;
+};
+
+struct Slot {
+  Planes b;
+  float* mass = nullptr;  // device scalar: unnormalised mass of b
+};
+
+constexpr int kStatsPerChild = 10;
+constexpr int kStatsFloats = 16 * 9 * kStatsPerChild;
+
+}  // namespace
+
+struct pp2_planner {
+  pp2_ctx* ctx = nullptr;
+  pp2_planner_params prm{};
+  float gamma = 0.95f;
+  float lb_const = 0.0f;
+  int W = 0;
+  size_t n = 0;
+  std::vector<float> hT, hL;    // host copies (reference layouts) for sampling
+  std::vector<float> u1, u2;    // the curand_uniform pairs every QNode sees
+  GlibcRand rng;
+
+  std::vector<Slot> slots;
+  std::vector<int> free_slots;
+  Planes P;                     // 9 prediction planes (scratch)
+  float* d_rpart = nullptr;     // tiles * 9
+  float* d_spart = nullptr;     // tiles * 16 * 90
+  float* d_bpart = nullptr;     // belief-update / dots partials
+  float* d_out = nullptr;       // [9 rewards | 1440 stats | 10 dots | 1 mass]
+  float* d_dense = nullptr;     // normalised belief, dense
+  float* h_out = nullptr;       // pinned mirror of d_out
+  float* h_belief = nullptr;    // pinned normalised belief
+  hipEvent_t ev_belief = nullptr;
+
+  VNode* root = nullptr;
+  uint32_t n_vnodes = 0, n_qnodes = 0, expansions = 0;
+};
+
+namespace {
+
+constexpr int kOutRewards = 0;
+constexpr int kOutStats = 9;
+constexpr int kOutDots = 9 + kStatsFloats;
+constexpr int kOutMass = kOutDots + kStatsPerChild;
+constexpr int kOutFloats = kOutMass + 1;
+
+int acquire_slot(pp2_planner* p, int* out) {
+  if (!p->free_slots.empty()) {
+    *out = p->free_slots.back();
+    p->free_slots.pop_back();
+    return PP2_OK;
+  }
+  Slot s;
+  CHECK(alloc_planes(p->ctx, &s.b, 1));
+  HIPCHK(hipMalloc(&s.mass, 64));
+  p->slots.push_back(s);
+  *out = (int)p->slots.size() - 1;
+  return PP2_OK;
+}
+
+void release_slot(pp2_planner* p, int s) {
+  if (s >= 0) p->free_slots.push_back(s);
+}
+
+void delete_vnode_only(pp2_planner* p, VNode* v) {
+  release_slot(p, v->slot);
+  --p->n_vnodes;
+  delete v;
+}
+
+void delete_qnode_only(pp2_planner* p, QNode* q) {
+  --p->n_qnodes;
+  delete q;
+}
+
+void delete_subtree(pp2_planner* p, VNode* v);
+
+void delete_subtree(pp2_planner* p, QNode* q) {
+  for (VNode* v : q->children)
+    if (v) delete_subtree(p, v);
+  delete_qnode_only(p, q);
+}
+
+void delete_subtree(pp2_planner* p, VNode* v) {
+  for (QNode* q : v->children)
+    if (q) delete_subtree(p, q);
+  delete_vnode_only(p, v);
+}
+
+VNode* new_vnode(pp2_planner* p, uint8_t z, float w, QNode* parent) {
+  VNode* v = new VNode();
+  v->observation = z;
+  v->weight = w;
+  v->parent = parent;
+  v->vnode_to_expand = v;  // VNode ctor (search_tree_cuda.cu:385)
+  ++p->n_vnodes;
+  return v;
+}
+
+// The FIB upper bound of a belief with FIB values f_i = dots_i / mass
+// (evaluateFibCpu: std::max_element -> first maximum).
+float fib_upper(const float* dots, float mass) {
+  float best = dots[0] / mass;
+  for (int i = 1; i < 9; ++i) {
+    const float v = dots[i] / mass;
+    if (best < v) best = v;
+  }
+  return best;
+}
+
+// QNode::update (search_tree_cuda.cu:251-286)
+void qnode_update(pp2_planner* p, QNode* q) {
+  float ub_rtg = 0.0f, lb_rtg = 0.0f;
+  for (VNode* v : q->children) {
+    ub_rtg += v->upper_bound * v->weight;
+    lb_rtg += v->lower_bound * v->weight;
+  }
+  q->upper_bound = q->reward + p->gamma * ub_rtg;
+  q->lower_bound = q->reward + p->gamma * lb_rtg;
+  q->heuristic = 0.0f;
+  for (VNode* v : q->children) {
+    const float h = p->gamma * v->weight * v->heuristic;
+    if (h > q->heuristic) {
+      q->heuristic = h;
+      q->vnode_to_expand = v->vnode_to_expand;
+    }
+  }
+  uint32_t child_depth = 0;
+  for (VNode* v : q->children)
+    if (v->depth > child_depth) {
+      child_depth = v->depth;
+      q->depth = child_depth + 1;
+    }
+}
+
+// VNode::update (search_tree_cuda.cu:397-435)
+void vnode_update(VNode* v) {
+  size_t ui = 0, li = 0;
+  for (size_t i = 1; i < v->children.size(); ++i) {
+    if (v->children[ui]->upper_bound < v->children[i]->upper_bound) ui = i;
+    if (v->children[li]->lower_bound < v->children[i]->lower_bound) li = i;
+  }
+  v->upper_bound = v->children[ui]->upper_bound;
+  v->lower_bound = v->children[li]->lower_bound;
+  v->heuristic = -FLT_MAX;
+  for (QNode* q : v->children) {
+    if (q->upper_bound <= v->lower_bound) continue;
+    if (q->heuristic > v->heuristic) {
+      v->heuristic = q->heuristic;
+      v->vnode_to_expand = q->vnode_to_expand;
+    }
+  }
+  uint32_t child_depth = 0;
+  for (QNode* q : v->children)
+    if (q->depth > child_depth) {
+      child_depth = q->depth;
+      v->depth = child_depth + 1;
+    }
+}
+
+// Device copy of a VNode's belief, recomputed from its parent VNode's
+// (always materialised: it was expanded) as the QNode constructor's update:
+// cudaBayesBeliefUpdate + renormalisation (search_tree_cuda.cu:213-231).
+int materialize(pp2_planner* p, VNode* v) {
+  if (v->slot >= 0) return PP2_OK;
+  if (!v->parent || !v->parent->parent)
+    return set_err(PP2_ESTATE, "cannot materialise a detached VNode");
+  VNode* pv = v->parent->parent;
+  CHECK(materialize(p, pv));
+  int s = -1;
+  CHECK(acquire_slot(p, &s));
+  pp2_ctx* c = p->ctx;
+  const Slot& ps = p->slots[pv->slot];
+  const Slot& ns = p->slots[s];
+  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v, ps.b.v.p,
+                                   ns.b.v.p, v->parent->action, v->observation,
+                                   ps.mass, p->d_bpart));
+  HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::cells_grid(c->g, c->cpt),
+                                  ns.mass));
+  v->slot = s;
+  return PP2_OK;
+}
+
+// Root VNode from a belief already in slot `s`: FIB/LB evaluation of the
+// VNode constructor (search_tree_cuda.cu:368-388).
+int make_root(pp2_planner* p, int s, uint8_t z, VNode** out) {
+  pp2_ctx* c = p->ctx;
+  const Slot& sl = p->slots[s];
+  HIPCHK(pp2::launch_belief_dots(c->stream, c->g, c->cpt, sl.b.v.p, c->fib[c->fcur].v,
+                                 p->d_bpart, p->d_out + kOutDots));
+  HIPCHK(hipMemcpyAsync(p->d_out + kOutMass, sl.mass, sizeof(float),
+                        hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(p->h_out + kOutDots, p->d_out + kOutDots,
+                        (kStatsPerChild + 1) * sizeof(float), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  VNode* v = new_vnode(p, z, 0.0f, nullptr);
+  v->slot = s;
+  v->upper_bound = fib_upper(p->h_out + kOutDots + 1, p->h_out[kOutMass]);
+  v->lower_bound = p->lb_const;
+  v->heuristic = v->upper_bound - v->lower_bound;
+  *out = v;
+  return PP2_OK;
+}
+
+// QNode::forwardSampling + the unique-observation count of the QNode
+// constructor (search_tree_cuda.cu:176-196, :311-366) for action a, given
+// the fp32 prefix sum `cdf` of the QNode's belief.
+void sample_observations(pp2_planner* p, const std::vector<float>& cdf, uint8_t a,
+                         std::vector<uint8_t>& zs, std::vector<float>& freq) {
+  const uint32_t N = p->prm.sample_num;
+  const size_t n = cdf.size();
+  std::vector<uint8_t> obs(N);
+  for (uint32_t j = 0; j < N; ++j) {
+    const float r = (float)p->rng.next() / ((float)RAND_MAX + 1.0f);
+    size_t s1 = (size_t)(std::lower_bound(cdf.begin(), cdf.end(), r) - cdf.begin());
+    // find_if(x >= r) runs off the end when rounding leaves cdf.back() < r;
+    // the reference then reads past its arrays.  Take the last cell with mass.
+    if (s1 >= n) {
+      s1 = n - 1;
+      while (s1 > 0 && cdf[s1] == cdf[s1 - 1]) --s1;
+    }
+    float td[9];
+    const float* tp = p->hT.data() + s1 * 81 + (size_t)a * 9;
+    for (int i = 0; i < 9; ++i) td[i] = tp[i];
+    for (int i = 1; i < 9; ++i) td[i] += td[i - 1];
+    uint32_t s2i = 0;
+    for (uint32_t i = 0; i < 9; ++i)
+      if (p->u1[j] <= td[i]) {
+        s2i = i;
+        break;
+      }
+    const uint32_t s2 = (uint32_t)s1 + (s2i / 3 - 1) * (uint32_t)p->W + (s2i % 3 - 1);
+    float ld[16];
+    const float* lp = p->hL.data() + (size_t)s2 * 16;
+    for (int i = 0; i < 16; ++i) ld[i] = lp[i];
+    for (int i = 1; i < 16; ++i) ld[i] += ld[i - 1];
+    uint8_t o = 0;
+    for (uint8_t i = 0; i < 16; ++i)
+      if (p->u2[j] <= ld[i]) {
+        o = i;
+        break;
+      }
+    obs[j] = o;
+  }
+  std::set<uint8_t> uniq(obs.begin(), obs.end());
+  zs.assign(uniq.begin(), uniq.end());
+  freq.resize(zs.size());
+  for (size_t i = 0; i < zs.size(); ++i)
+    freq[i] = (float)std::count(obs.begin(), obs.end(), zs[i]) / (float)N;
+}
+
+// VNode::expand (search_tree_cuda.cu:437-450) with the 9 QNode constructors
+// (:161-242) batched.
+int expand_vnode(pp2_planner* p, VNode* v) {
+  pp2_ctx* c = p->ctx;
+  CHECK(materialize(p, v));
+  const Slot& sl = p->slots[v->slot];
+  const size_t n = p->n;
+  // normalised belief -> host (for the state samples), then the batched
+  // scoring pass runs on the device while the host samples
+  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_dense, sl.mass));
+  HIPCHK(hipMemcpyAsync(p->h_belief, p->d_dense, n * sizeof(float), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipEventRecord(p->ev_belief, c->stream));
+  HIPCHK(pp2::launch_expand(c->stream, c->g, c->cpt, c->T.v, sl.b.v.p, c->R.v, c->L.v,
+                            c->fib[c->fcur].v, p->P.v, p->d_rpart, p->d_spart,
+                            p->d_out + kOutRewards, p->d_out + kOutStats));
+  HIPCHK(hipMemcpyAsync(p->d_out + kOutMass, sl.mass, sizeof(float), hipMemcpyDeviceToDevice,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(p->h_out, p->d_out, kOutFloats * sizeof(float), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipEventSynchronize(p->ev_belief));
+
+  std::vector<float> cdf(n);
+  float acc = 0.0f;
+  for (size_t i = 0; i < n; ++i) {
+    acc = acc + p->h_belief[i];
+    cdf[i] = acc;
+  }
+  std::vector<uint8_t> zs[9];
+  std::vector<float> fq[9];
+  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, cdf, a, zs[a], fq[a]);
+  HIPCHK(hipStreamSynchronize(c->stream));
+
+  for (QNode* q : v->children)
+    if (q) delete_subtree(p, q);
+  v->children.assign(9, nullptr);
+  const float mass = p->h_out[kOutMass];
+  const float* stats = p->h_out + kOutStats;
+  for (uint8_t a = 0; a < 9; ++a) {
+    QNode* q = new QNode();
+    ++p->n_qnodes;
+    q->action = a;
+    q->parent = v;
+    q->reward = p->h_out[kOutRewards + a] / mass;
+    for (size_t k = 0; k < zs[a].size(); ++k) {
+      const uint8_t z = zs[a][k];
+      const float* st = stats + ((size_t)z * 9 + a) * kStatsPerChild;
+      VNode* cv = new_vnode(p, z, fq[a][k], q);
+      cv->upper_bound = fib_upper(st + 1, st[0]);
+      cv->lower_bound = p->lb_const;
+      cv->heuristic = cv->upper_bound - cv->lower_bound;
+      q->children.push_back(cv);
+    }
+    qnode_update(p, q);
+    v->children[a] = q;
+  }
+  vnode_update(v);
+  ++p->expansions;
+  return PP2_OK;
+}
+
+// SearchTree::expand (search_tree_cuda.cu:490-508)
+int tree_expand(pp2_planner* p) {
+  VNode* vte = p->root->vnode_to_expand;
+  if (!vte)
+    return set_err(PP2_ESTATE, "no expandable node (all heuristics are zero)");
+  CHECK(expand_vnode(p, vte));
+  VNode* v = vte;
+  while (v->parent != nullptr) {
+    QNode* q = v->parent;
+    qnode_update(p, q);
+    VNode* pv = q->parent;
+    vnode_update(pv);
+    v = pv;
+  }
+  return PP2_OK;
+}
+
+// SearchTree::update (search_tree_cuda.cu:548-626)
+int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
+  VNode* root = p->root;
+  QNode* root_q = nullptr;
+  for (QNode* q : root->children) {
+    if (q->action == a) root_q = q;
+    else delete_subtree(p, q);
+  }
+  root->children.clear();
+  VNode* root_v = nullptr;
+  if (root_q) {
+    for (VNode* v : root_q->children) {
+      if (v->observation == z) root_v = v;
+      else delete_subtree(p, v);
+    }
+    root_q->children.clear();
+  }
+  if (root_v) {
+    CHECK(materialize(p, root_v));  // from the old root, before it goes
+    delete_qnode_only(p, root_q);
+    delete_vnode_only(p, root);
+    root_v->parent = nullptr;
+    p->root = root_v;
+    return PP2_OK;
+  }
+  // No such child (or the root was never expanded -- the reference
+  // dereferences a null QNode there): a fresh root from the updated belief.
+  int s = -1;
+  CHECK(acquire_slot(p, &s));
+  pp2_ctx* c = p->ctx;
+  const Slot& os = p->slots[root->slot];
+  const Slot& ns = p->slots[s];
+  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v, os.b.v.p,
+                                   ns.b.v.p, a, z, os.mass, p->d_bpart));
+  HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::cells_grid(c->g, c->cpt),
+                                  ns.mass));
+  VNode* nv = nullptr;
+  CHECK(make_root(p, s, 0, &nv));
+  if (root_q) delete_qnode_only(p, root_q);
+  delete_vnode_only(p, root);
+  p->root = nv;
+  return PP2_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pp2_planner_default_params(pp2_planner_params* prm) {
+  if (!prm) return set_err(PP2_EINVAL, "params is null");
+  prm->max_search_tree_depth = 50;
+  prm->max_online_iteration = 15;
+  prm->lower_bound_mode = 0;
+  prm->rand_seed = 1;
+  prm->sample_num = 50;
+  prm->curand_seed = 1234;
+  return PP2_OK;
+}
+
+int pp2_curand_uniforms(uint64_t seed, int n, float* u1, float* u2) {
+  if (n < 0 || (n > 0 && (!u1 || !u2))) return set_err(PP2_EINVAL, "bad arguments");
+  for (int i = 0; i < n; ++i) {
+    CurandXorwow g(seed, (uint64_t)i);
+    u1[i] = curand_uniform_of(g.next());
+    u2[i] = curand_uniform_of(g.next());
+  }
+  return PP2_OK;
+}
+
+int pp2_planner_destroy(pp2_planner* p);
+
+int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* prm) {
+  if (!out) return set_err(PP2_EINVAL, "out is null");
+  *out = nullptr;
+  CHECK(check_model(c));
+  if (c->nranks > 1 || c->g.rows != c->g.grows)
+    return set_err(PP2_EINVAL, "the QV-tree planner needs an unsharded context");
+  pp2_planner_params d;
+  pp2_planner_default_params(&d);
+  if (!prm) prm = &d;
+  if (prm->lower_bound_mode != 0)
+    return set_err(PP2_EINVAL, "lower_bound_mode %d not supported (0 = constant)",
+                   prm->lower_bound_mode);
+  if (prm->sample_num == 0) return set_err(PP2_EINVAL, "sample_num must be > 0");
+  DeviceGuard dg(c->device);
+  pp2_planner* p = new pp2_planner();
+  p->ctx = c;
+  p->prm = *prm;
+  p->gamma = c->gamma;
+  // search_tree_cuda.cu:383 (commented fallback): -5.0f / (1.0f - gamma)
+  p->lb_const = -5.0f / (1.0f - p->gamma);
+  p->W = c->g.width;
+  p->n = owned_cells(c);
+  auto fail = [&](int s) {
+    pp2_planner_destroy(p);
+    return s;
+  };
+  p->hT.resize(p->n * 81);
+  p->hL.resize(p->n * 16);
+  int s = pp2_model_download(c, p->hT.data(), p->hL.data(), nullptr, nullptr);
+  if (s) return fail(s);
+  p->u1.resize(prm->sample_num);
+  p->u2.resize(prm->sample_num);
+  pp2_curand_uniforms(prm->curand_seed, (int)prm->sample_num, p->u1.data(), p->u2.data());
+  p->rng.seed(prm->rand_seed);
+  const int tiles1 = pp2::cells_grid(c->g, 1);
+  if ((s = alloc_planes(c, &p->P, 9))) return fail(s);
+  if (hipMalloc(&p->d_rpart, (size_t)tiles1 * 9 * sizeof(float)) != hipSuccess ||
+      hipMalloc(&p->d_spart, (size_t)tiles1 * kStatsFloats * sizeof(float)) != hipSuccess ||
+      hipMalloc(&p->d_bpart, (size_t)(tiles1 + 1) * kStatsPerChild * sizeof(float)) != hipSuccess ||
+      hipMalloc(&p->d_out, kOutFloats * sizeof(float)) != hipSuccess ||
+      hipMalloc(&p->d_dense, p->n * sizeof(float)) != hipSuccess ||
+      hipHostMalloc(&p->h_out, kOutFloats * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&p->h_belief, p->n * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_belief, hipEventDisableTiming) != hipSuccess)
+    return fail(set_err(PP2_ENOMEM, "planner scratch allocation failed"));
+  *out = p;
+  return PP2_OK;
+}
+
+int pp2_planner_reset(pp2_planner* p) {
+  if (!p) return set_err(PP2_EINVAL, "null planner");
+  if (p->root) delete_subtree(p, p->root);
+  p->root = nullptr;
+  return PP2_OK;
+}
+
+int pp2_planner_destroy(pp2_planner* p) {
+  if (!p) return PP2_OK;
+  DeviceGuard dg(p->ctx->device);
+  (void)hipStreamSynchronize(p->ctx->stream);
+  pp2_planner_reset(p);
+  for (Slot& s : p->slots) {
+    free_planes(&s.b);
+    if (s.mass) (void)hipFree(s.mass);
+  }
+  free_planes(&p->P);
+  for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_out, p->d_dense})
+    if (d) (void)hipFree(d);
+  if (p->h_out) (void)hipHostFree(p->h_out);
+  if (p->h_belief) (void)hipHostFree(p->h_belief);
+  if (p->ev_belief) (void)hipEventDestroy(p->ev_belief);
+  delete p;
+  return PP2_OK;
+}
+
+int pp2_planner_step(pp2_planner* p, uint8_t action, uint8_t observation,
+                     const float* belief, uint8_t* new_action, float* new_value) {
+  if (!p) return set_err(PP2_EINVAL, "null planner");
+  pp2_ctx* c = p->ctx;
+  DeviceGuard dg(c->device);
+  if (!p->root) {
+    if (!belief) return set_err(PP2_EINVAL, "first plan step needs a belief");
+    // new SearchTree(msg->belief) (path_planning_2d.cu:212-213)
+    int s = -1;
+    CHECK(acquire_slot(p, &s));
+    CHECK(upload_planes(c, p->slots[s].b, belief));
+    const float one = 1.0f;
+    HIPCHK(hipMemcpyAsync(p->slots[s].mass, &one, sizeof one, hipMemcpyHostToDevice, c->stream));
+    CHECK(make_root(p, s, 0, &p->root));
+  } else {
+    if (action > 8 || observation > 15)
+      return set_err(PP2_EINVAL, "action %u / observation %u out of range", action, observation);
+    CHECK(tree_update(p, action, observation));
+  }
+  // while (getDepth() < max_search_tree_depth &&
+  //        update_counter++ < max_online_iteration) expand();   (:219-223)
+  int counter = 0;
+  while (p->root->depth < (uint32_t)p->prm.max_search_tree_depth &&
+         counter++ < p->prm.max_online_iteration)
+    CHECK(tree_expand(p));
+  // SearchTree::getOptimalAction (search_tree_cuda.cu:510-524)
+  uint8_t a = 0;
+  float r = -FLT_MAX;
+  for (const QNode* q : p->root->children)
+    if (q->upper_bound > r) {
+      r = q->upper_bound;
+      a = q->action;
+    }
+  if (new_action) *new_action = a;
+  if (new_value) *new_value = r;
+  return PP2_OK;
+}
+
+int pp2_planner_info(pp2_planner* p, pp2_tree_info* info) {
+  if (!p || !info) return set_err(PP2_EINVAL, "null argument");
+  memset(info, 0, sizeof *info);
+  info->total_vnodes = p->n_vnodes;
+  info->total_qnodes = p->n_qnodes;
+  info->expansions = p->expansions;
+  const VNode* r = p->root;
+  if (!r) return PP2_OK;
+  info->depth = r->depth;
+  info->root_upper_bound = r->upper_bound;
+  info->root_lower_bound = r->lower_bound;
+  info->root_heuristic = r->heuristic;
+  info->n_root_children = (uint32_t)r->children.size();
+  for (size_t a = 0; a < r->children.size() && a < 9; ++a) {
+    const QNode* q = r->children[a];
+    info->q_upper_bound[a] = q->upper_bound;
+    info->q_lower_bound[a] = q->lower_bound;
+    info->q_reward[a] = q->reward;
+    info->q_heuristic[a] = q->heuristic;
+    info->q_depth[a] = q->depth;
+    info->q_nchildren[a] = (uint32_t)q->children.size();
+    for (size_t k = 0; k < q->children.size() && k < 16; ++k) {
+      info->q_obs[a][k] = q->children[k]->observation;
+      info->q_weight[a][k] = q->children[k]->weight;
+      info->v_upper_bound[a][k] = q->children[k]->upper_bound;
+      info->v_lower_bound[a][k] = q->children[k]->lower_bound;
+    }
+  }
+  return PP2_OK;
+}
+
+}  // extern "C"

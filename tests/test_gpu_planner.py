@@ -1,0 +1,107 @@
+"""GPU parity of the QV-tree planner (C++ tree over batched gfx950 expansion
+passes) against the oracle's reference-semantics tree (every node holding
+its own host belief, sequential fp32 sums).
+
+Both draw the reference's samples: glibc rand() state samples over the fp32
+prefix sum of the node belief, and the cuRAND XORWOW uniforms of
+curand_init(1234, i, 0).  Tree shape (children, observations, weights,
+depth, expansions) must match exactly; bounds and rewards to rel 1e-5."""
+import numpy as np
+import pytest
+
+from conftest import GAMMA, golden, golden_map
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_close(a, b, rel=1e-5, atol=1e-6):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.all(np.abs(a - b) <= np.maximum(rel * np.abs(b), atol))
+
+
+def compare(gi, oi, where):
+    for k in ("depth", "expansions", "n_root_children", "total_vnodes", "total_qnodes"):
+        assert gi[k] == oi[k], f"{where}: {k} {gi[k]} != {oi[k]}"
+    n = gi["n_root_children"]
+    assert np.array_equal(gi["q_nchildren"][:n], oi["q_nchildren"][:n]), where
+    assert np.array_equal(gi["q_depth"][:n], oi["q_depth"][:n]), where
+    for a in range(n):
+        m = gi["q_nchildren"][a]
+        assert np.array_equal(gi["q_obs"][a][:m], oi["q_obs"][a][:m]), where
+        assert np.array_equal(gi["q_weight"][a][:m], oi["q_weight"][a][:m]), where
+        assert rel_close(gi["v_upper_bound"][a][:m], oi["v_upper_bound"][a][:m]), where
+        assert np.array_equal(gi["v_lower_bound"][a][:m], oi["v_lower_bound"][a][:m]), where
+    for k in ("q_upper_bound", "q_lower_bound", "q_reward", "q_heuristic"):
+        assert rel_close(gi[k][:n], oi[k][:n]), f"{where}: {k}"
+    for k in ("root_upper_bound", "root_lower_bound", "root_heuristic"):
+        assert rel_close(gi[k], oi[k]), f"{where}: {k}"
+
+
+@pytest.mark.parametrize("name,max_depth,max_iter,steps", [
+    ("map_10x10", 50, 15, 6),
+    ("sparse_map_100x40", 3, 15, 8),
+    ("sparse_map_100x40", 50, 15, 4),
+    ("tile64_sparse_map_100x40", 5, 15, 5),
+])
+def test_planner_matches_oracle(oracle, name, max_depth, max_iter, steps):
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = golden_map(name)
+    m = golden("model", name)
+    H, W = grid.shape
+    with P.GridContext(grid, tuple(m["goal"]), gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_solve()
+        alphas = ctx.fib_get()
+        a_ref, _, _ = oracle.fib_solve(H, W, GAMMA, m["T"], m["L"], m["R"])
+        np.testing.assert_array_equal(alphas, a_ref)
+        opl = oracle.Planner(grid, m["T"], m["L"], m["R"], alphas,
+                             max_depth=max_depth, max_iter=max_iter)
+        with P.QVTreePlanner(ctx, max_search_tree_depth=max_depth,
+                             max_online_iteration=max_iter) as gpl:
+            _, zs, _ = S.synth_trajectory(grid, steps, seed=7)
+            b0 = S.uniform_belief(grid)
+            a_g, v_g = gpl.step(0, 0, b0)
+            a_o, v_o = opl.step(0, 0, b0)
+            compare(gpl.info(), opl.info(), f"{name} step 0")
+            assert a_g == a_o
+            assert rel_close(v_g, v_o)
+            for k in range(steps):
+                # both planners receive the oracle's action and the same z;
+                # z may or may not exist under the root (re-root vs new root)
+                a_g, v_g = gpl.step(a_o, int(zs[k]))
+                a_o, v_o = opl.step(a_o, int(zs[k]))
+                compare(gpl.info(), opl.info(), f"{name} step {k + 1}")
+                assert a_g == a_o, f"{name} step {k + 1}: action {a_g} != {a_o}"
+                assert rel_close(v_g, v_o)
+            gpl.reset()
+            assert gpl.info()["total_vnodes"] == 0
+    opl.close()
+
+
+def test_planner_256_plan_step(oracle):
+    """BASELINE config 2 shape: 256x256 synthetic grid, depth 3."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(256, 256, 256)
+    goal = S.synth_goal(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_solve(max_sweeps=40)
+        alphas = ctx.fib_get()
+        T, L, R = oracle.model_pomdp(grid, goal)
+        opl = oracle.Planner(grid, T, L, R, alphas, max_depth=3, max_iter=15)
+        with P.QVTreePlanner(ctx, max_search_tree_depth=3, max_online_iteration=15) as gpl:
+            b0 = S.uniform_belief(grid)
+            a_g, _ = gpl.step(0, 0, b0)
+            a_o, _ = opl.step(0, 0, b0)
+            compare(gpl.info(), opl.info(), "256 step 0")
+            assert a_g == a_o
+            _, zs, _ = S.synth_trajectory(grid, 2, seed=3)
+            for k in range(2):
+                a_g, _ = gpl.step(a_o, int(zs[k]))
+                a_o, _ = opl.step(a_o, int(zs[k]))
+                compare(gpl.info(), opl.info(), f"256 step {k + 1}")
+                assert a_g == a_o
+        opl.close()

@@ -175,3 +175,34 @@ def test_curand_xorwow_subsequence_is_linear_jump(oracle):
     np.testing.assert_array_equal(c, d)
     u = oracle.curand_uniform(0xFFFFFFFF)
     assert 0.0 < u <= 1.0
+
+
+def test_product_curand_stream_matches_oracle(oracle):
+    """The product's cuRAND XORWOW (rocRAND's precomputed 2^67 jump matrices)
+    equals the oracle's independent GF(2) matrix-power jump, for the 50
+    subsequences every QNode re-creates (search_tree_cuda.cu:84-92)."""
+    from path_planning_2d_amd.planner import curand_uniforms
+    u1, u2 = curand_uniforms(1234, 50)
+    for i in range(50):
+        x = oracle.curand_xorwow(1234, i, 0, 2)
+        assert u1[i] == oracle.curand_uniform(x[0])
+        assert u2[i] == oracle.curand_uniform(x[1])
+
+
+def test_oracle_planner_runs(oracle):
+    """The reference-semantics tree on the sparse map: depth advances by 2
+    per expansion level (QNode::update depth quirk, search_tree_cuda.cu:
+    277-283) and 9 QNodes hang under an expanded root."""
+    from path_planning_2d_amd import synthetic as S
+    name = "sparse_map_100x40"
+    g = golden_map(name)
+    m = golden("model", name)
+    f = golden("fib", name)
+    pl = oracle.Planner(g, m["T"], m["L"], m["R"], f["alphas"], max_depth=3,
+                        max_iter=15)
+    a, v = pl.step(0, 0, S.uniform_belief(g))
+    info = pl.info()
+    assert info["expansions"] == 2 and info["depth"] == 4
+    assert info["n_root_children"] == 9
+    assert v == max(info["q_upper_bound"])
+    assert a == int(np.argmax(info["q_upper_bound"]))
