@@ -68,7 +68,7 @@ def lib():
             "orc_synth_goal": (I, [I, I, _u8p, C.POINTER(I), C.POINTER(I)]),
             "orc_synth_trajectory": (I, [I, I, _u8p, I, I, C.c_uint64, I, _u8p, _u8p, _i32p]),
             "orc_planner_create": (C.c_void_p, [I, I, _f32p, _f32p, _f32p, _f32p, F, I, I,
-                                                C.c_uint32, C.c_uint32, C.c_uint64]),
+                                                C.c_uint32, C.c_uint32, C.c_uint64, I]),
             "orc_planner_step": (I, [C.c_void_p, C.c_uint8, C.c_uint8, C.c_void_p,
                                      C.POINTER(C.c_uint8), C.POINTER(F)]),
             "orc_planner_reset": (None, [C.c_void_p]),
@@ -258,13 +258,14 @@ class Planner:
     its own belief; sequential fp32 sums; linear find_if sampling)."""
 
     def __init__(self, grid, T, L, R, alphas, gamma=0.95, max_depth=50,
-                 max_iter=15, rand_seed=1, sample_num=50, curand_seed=1234):
+                 max_iter=15, rand_seed=1, sample_num=50, curand_seed=1234,
+                 accurate=False):
         H, W = grid.shape
         self.n = H * W
         self._keep = [np.ascontiguousarray(a, np.float32) for a in (T, L, R, alphas)]
         self._h = lib().orc_planner_create(H, W, *self._keep, float(gamma),
                                            int(max_depth), int(max_iter), rand_seed,
-                                           sample_num, curand_seed)
+                                           sample_num, curand_seed, int(accurate))
 
     def step(self, action, observation, belief=None):
         a = C.c_uint8()

@@ -142,11 +142,15 @@ typedef struct {
   uint32_t total_vnodes, total_qnodes, expansions;
 } orc_tree_info;
 typedef struct orc_planner orc_planner;
-/* T, L, R, alphas are borrowed (reference layouts; alphas [hw][9]). */
+/* T, L, R, alphas are borrowed (reference layouts; alphas [hw][9]).
+ * accurate = 0: the reference's arithmetic (sequential fp32 sums);
+ * accurate = 1: fp64 accumulation of normalisation sums, rewards and FIB
+ *               dots -- the accuracy reference for the device tree sums. */
 orc_planner* orc_planner_create(int H, int W, const float* T, const float* L,
                                 const float* R, const float* alphas, float gamma,
                                 int max_depth, int max_iter, uint32_t rand_seed,
-                                uint32_t sample_num, uint64_t curand_seed);
+                                uint32_t sample_num, uint64_t curand_seed,
+                                int accurate);
 int orc_planner_step(orc_planner* p, uint8_t a, uint8_t z, const float* belief,
                      uint8_t* new_action, float* new_value);
 void orc_planner_reset(orc_planner* p);

@@ -50,6 +50,7 @@ struct orc_planner {
   const float *T, *L, *R, *alphas;
   float gamma, lb_const;
   int max_depth, max_iter;
+  int accurate; /* 1: fp64 accumulation of sums/dots (accuracy reference) */
   uint32_t sample_num;
   float* u1;
   float* u2;
@@ -66,7 +67,16 @@ static OV* ov_new(orc_planner* p, const float* b, uint8_t z, float w, OQ* parent
   v->weight = w;
   v->parent = parent;
   uint8_t dummy;
-  orc_fib_eval(p->n, v->belief, p->alphas, &v->ub, &dummy);
+  if (p->accurate) {
+    double f[9] = {0};
+    for (size_t k = 0; k < p->n; ++k)
+      for (int i = 0; i < 9; ++i) f[i] += (double)v->belief[k] * p->alphas[9 * k + i];
+    int best = 0;
+    for (int i = 1; i < 9; ++i) if ((float)f[best] < (float)f[i]) best = i;
+    v->ub = (float)f[best];
+  } else {
+    orc_fib_eval(p->n, v->belief, p->alphas, &v->ub, &dummy);
+  }
   v->lb = p->lb_const;
   v->heuristic = v->ub - v->lb;
   v->vte = v;
@@ -156,7 +166,13 @@ static OQ* oq_new(orc_planner* p, const float* b, uint8_t a, OV* parent) {
   q->heuristic = FLT_MIN;
   q->depth = 1;
   ++p->n_qnodes;
-  q->reward = orc_reward_dot(p->n, q->belief, p->R, a);
+  if (p->accurate) {
+    double r = 0.0;
+    for (size_t k = 0; k < p->n; ++k) r += (double)q->belief[k] * p->R[9 * k + a];
+    q->reward = (float)r;
+  } else {
+    q->reward = orc_reward_dot(p->n, q->belief, p->R, a);
+  }
   uint8_t* obs = (uint8_t*)malloc(p->sample_num);
   forward_sampling(p, q->belief, a, obs);
   int count[16] = {0};
@@ -167,7 +183,8 @@ static OQ* oq_new(orc_planner* p, const float* b, uint8_t a, OV* parent) {
     if (!count[z]) continue;
     float w = (float)count[z] / (float)p->sample_num;
     orc_belief_update(p->H, p->W, p->T, p->L, q->belief, a, z, out, 1);
-    orc_normalize_seq(p->n, out);
+    if (p->accurate) orc_normalize_f64(p->n, out);
+    else orc_normalize_seq(p->n, out);
     q->children[q->nchildren++] = ov_new(p, out, (uint8_t)z, w, q);
   }
   free(out);
@@ -237,7 +254,8 @@ static void tree_update(orc_planner* p, uint8_t a, uint8_t z) {
   }
   float* cur = (float*)malloc(p->n * sizeof(float));
   orc_belief_update(p->H, p->W, p->T, p->L, root->belief, a, z, cur, 1);
-  orc_normalize_seq(p->n, cur);
+  if (p->accurate) orc_normalize_f64(p->n, cur);
+  else orc_normalize_seq(p->n, cur);
   OV* nv = ov_new(p, cur, 0, 0.0f, NULL);
   free(cur);
   if (rq) { free(rq->belief); free(rq); --p->n_qnodes; }
@@ -248,8 +266,10 @@ static void tree_update(orc_planner* p, uint8_t a, uint8_t z) {
 orc_planner* orc_planner_create(int H, int W, const float* T, const float* L,
                                 const float* R, const float* alphas, float gamma,
                                 int max_depth, int max_iter, uint32_t rand_seed,
-                                uint32_t sample_num, uint64_t curand_seed) {
+                                uint32_t sample_num, uint64_t curand_seed,
+                                int accurate) {
   orc_planner* p = (orc_planner*)calloc(1, sizeof(orc_planner));
+  p->accurate = accurate;
   p->H = H; p->W = W; p->n = (size_t)H * W;
   p->T = T; p->L = L; p->R = R; p->alphas = alphas;
   p->gamma = gamma;
