@@ -220,7 +220,26 @@ int pp2_planner_info(pp2_planner* p, pp2_tree_info* info);
 int pp2_curand_uniforms(uint64_t seed, int n, float* u1, float* u2);
 
 /* ---------------------------------------------------------------- shards
- * RCCL bootstrap for row shards (no reference counterpart).  Rank 0 calls
+ * Two transports for row shards (no reference counterpart):
+ *  - one process per GPU: RCCL (pp2_rccl_unique_id / pp2_shard_comm_init);
+ *    then every per-context call exchanges its halos itself;
+ *  - one process driving several shard contexts (one or more devices): a
+ *    shard group, whose pp2_shard_group_* calls run each step phase-wise
+ *    over all shards, moving halo rows and the belief mass with device
+ *    copies.  Grouped contexts reject the per-context stepping calls. */
+typedef struct pp2_shard_group pp2_shard_group;
+/* ctxs[i] must be the shards of one grid in row order (pp2_create_shard). */
+int pp2_shard_group_create(pp2_shard_group** out, pp2_ctx* const* ctxs, int n);
+int pp2_shard_group_destroy(pp2_shard_group* g);
+int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z);
+int pp2_shard_group_belief_update(pp2_shard_group* g, uint8_t u, uint8_t z);
+int pp2_shard_group_mdp_sweep(pp2_shard_group* g, int n);
+int pp2_shard_group_mdp_solve(pp2_shard_group* g, int max_sweeps, int* sweeps,
+                              double* final_norm);
+int pp2_shard_group_fib_sweep(pp2_shard_group* g, int n);
+int pp2_shard_group_synchronize(pp2_shard_group* g);
+
+/* RCCL bootstrap for row shards (no reference counterpart).  Rank 0 calls
  * pp2_rccl_unique_id, the 128 bytes are broadcast out of band, then every
  * rank calls pp2_shard_comm_init with its own shard context. */
 #define PP2_RCCL_ID_BYTES 128

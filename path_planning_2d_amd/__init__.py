@@ -6,9 +6,9 @@ HIP kernels in ``libpp2_hip.so`` behind the C ABI ``include/pp2.h``.  This
 package is the Python host mirror of that boundary.
 """
 from ._lib import Pp2Error, LIB_PATH
-from .core import GridContext, device_count
+from .core import GridContext, ShardGroup, device_count
 from .planner import QVTreePlanner
 from . import maps, synthetic
 
-__all__ = ["GridContext", "QVTreePlanner", "device_count", "Pp2Error",
+__all__ = ["GridContext", "ShardGroup", "QVTreePlanner", "device_count", "Pp2Error",
            "LIB_PATH", "maps", "synthetic"]

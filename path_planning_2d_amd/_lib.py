@@ -77,6 +77,14 @@ SIGNATURES = {
     "pp2_planner_reset": [_vp],
     "pp2_planner_info": [_vp, _vp],
     "pp2_curand_uniforms": [C.c_uint64, C.c_int, _f32p, _f32p],
+    "pp2_shard_group_create": [C.POINTER(_vp), C.POINTER(_vp), C.c_int],
+    "pp2_shard_group_destroy": [_vp],
+    "pp2_shard_group_loop_step": [_vp, C.c_uint8, C.c_uint8],
+    "pp2_shard_group_belief_update": [_vp, C.c_uint8, C.c_uint8],
+    "pp2_shard_group_mdp_sweep": [_vp, C.c_int],
+    "pp2_shard_group_mdp_solve": [_vp, C.c_int, _i32p, _f64p],
+    "pp2_shard_group_fib_sweep": [_vp, C.c_int],
+    "pp2_shard_group_synchronize": [_vp],
     "pp2_rccl_unique_id": [_u8p],
     "pp2_shard_comm_init": [_vp, _u8p, C.c_int, C.c_int],
 }

@@ -218,3 +218,90 @@ def device_count() -> int:
     n = C.c_int()
     call("pp2_device_count", C.byref(n))
     return n.value
+
+
+class ShardGroup:
+    """Row shards of one grid driven from one process (pp2_shard_group_*):
+    halo rows and the belief mass move by device copies between the shard
+    contexts, which may live on one or several devices.
+
+    ``bounds`` are the row boundaries, e.g. (0, 256, 512, ..., H)."""
+
+    def __init__(self, grid: np.ndarray, goal, bounds, gamma: float = 0.95,
+                 devices=None):
+        bounds = [int(b) for b in bounds]
+        n = len(bounds) - 1
+        devices = list(devices) if devices is not None else [0] * n
+        self.shards = [GridContext(grid, goal, gamma=gamma, device=devices[i],
+                                   rows=(bounds[i], bounds[i + 1]))
+                       for i in range(n)]
+        arr = (C.c_void_p * n)(*[s.handle.value for s in self.shards])
+        h = C.c_void_p()
+        call("pp2_shard_group_create", C.byref(h), arr, n)
+        self._h = h
+        self.bounds = bounds
+
+    def model_generate(self):
+        for s in self.shards:
+            s.model_generate()
+
+    def belief_set(self, b):
+        b = np.ascontiguousarray(b, np.float32).reshape(-1)
+        for s in self.shards:
+            s.belief_set(b[s.row_begin * s.width:s.row_end * s.width])
+
+    def belief_get(self):
+        return np.concatenate([s.belief_get() for s in self.shards])
+
+    def mdp_reset(self):
+        for s in self.shards:
+            s.mdp_reset()
+        self.synchronize()
+
+    def mdp_get(self):
+        parts = [s.mdp_get() for s in self.shards]
+        return (np.concatenate([p[0] for p in parts]),
+                np.concatenate([p[1] for p in parts]))
+
+    def fib_get(self):
+        return np.concatenate([s.fib_get() for s in self.shards])
+
+    def fib_reset(self):
+        for s in self.shards:
+            s.fib_reset()
+        self.synchronize()
+
+    def loop_step(self, u, z):
+        call("pp2_shard_group_loop_step", self._h, int(u), int(z))
+
+    def belief_update(self, u, z):
+        call("pp2_shard_group_belief_update", self._h, int(u), int(z))
+
+    def mdp_sweep(self, n=1):
+        call("pp2_shard_group_mdp_sweep", self._h, int(n))
+
+    def mdp_solve(self, max_sweeps=0):
+        s = C.c_int()
+        nrm = C.c_double()
+        call("pp2_shard_group_mdp_solve", self._h, int(max_sweeps), C.byref(s),
+             C.byref(nrm))
+        return s.value, nrm.value
+
+    def fib_sweep(self, n=1):
+        call("pp2_shard_group_fib_sweep", self._h, int(n))
+
+    def synchronize(self):
+        call("pp2_shard_group_synchronize", self._h)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().pp2_shard_group_destroy(self._h)
+            self._h = None
+        for s in getattr(self, "shards", []):
+            s.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -82,6 +82,8 @@ struct pp2_ctx {
 
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  pp2_shard_group* group = nullptr;  // single-process shard group, if any
+  int grank = 0;                     // rank (row-block order) inside the group
 };
 
 namespace pp2rt {
@@ -104,6 +106,14 @@ int check_ctx(pp2_ctx* c);
 int check_model(pp2_ctx* c);
 size_t owned_cells(const pp2_ctx* c);
 int download_planes(pp2_ctx* c, const Planes& P, float* host, const float* divide_by);
+int belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep);
+int mdp_sweep_once(pp2_ctx* c);
+int fib_sweep_once(pp2_ctx* c);
+int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* out);
+
+// Halo-exchanged state of a shard.
+enum HaloKind { HALO_BELIEF, HALO_VALUE, HALO_FIB };
+const Planes& halo_planes(pp2_ctx* c, HaloKind k);
 int upload_planes(pp2_ctx* c, Planes& P, const float* host);
 
 }  // namespace pp2rt

@@ -78,12 +78,25 @@ int check_model(pp2_ctx* c) {
 
 size_t owned_cells(const pp2_ctx* c) { return (size_t)c->g.rows * c->g.width; }
 
-// One halo row up and down for each plane set, in one RCCL group.
-int exchange_halos(pp2_ctx* c, std::initializer_list<const Planes*> sets) {
+const Planes& halo_planes(pp2_ctx* c, HaloKind k) {
+  switch (k) {
+    case HALO_BELIEF: return c->b[c->bcur];
+    case HALO_VALUE: return c->J[c->jcur];
+    default: return c->fib[c->fcur];
+  }
+}
+
+// One halo row up and down for each state kind, in one RCCL group
+// (multi-process shards).  Shards of a single-process group exchange through
+// the pp2_shard_group_* drivers instead.
+int exchange_halos(pp2_ctx* c, std::initializer_list<HaloKind> kinds) {
+  if (c->group)
+    return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
   if (c->nranks <= 1) return PP2_OK;
   if (!c->comm) return set_err(PP2_ESTATE, "sharded context without RCCL comm");
   NCCLCHK(ncclGroupStart());
-  for (const Planes* P : sets) {
+  for (HaloKind k : kinds) {
+    const Planes* P = &halo_planes(c, k);
     float* p = P->v.p;
     const size_t n = (size_t)P->v.rs;
     if (c->rank > 0) {
@@ -107,17 +120,12 @@ int allreduce_mass(pp2_ctx* c, float* d) {
   return PP2_OK;
 }
 
-// max |cur - snap| over owned cells/planes (global over shards); snap := cur.
+int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* out);
+
+// max |cur - snap| over owned cells/planes (global over RCCL shards); snap := cur.
 int absdiff_max(pp2_ctx* c, const Planes& cur, const Planes& snap, double* out) {
-  int np = 0;
-  HIPCHK(pp2::launch_absdiff_max(c->stream, c->g, cur.K, cur.v, snap.v,
-                                 c->rpartials, &np));
-  std::vector<float> h(np);
-  HIPCHK(hipMemcpyAsync(h.data(), c->rpartials, np * sizeof(float),
-                        hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
   float m = 0.0f;
-  for (float v : h) m = std::max(m, v);
+  CHECK(absdiff_local_max(c, cur, snap, &m));
   if (c->nranks > 1) {
     HIPCHK(hipMemcpyAsync(c->rpartials, &m, sizeof(float), hipMemcpyHostToDevice, c->stream));
     NCCLCHK(ncclAllReduce(c->rpartials, c->rpartials, 1, ncclFloat, ncclMax, c->comm, c->stream));
@@ -245,9 +253,64 @@ std::string join(const char* dir, const char* name) {
   return d + name;
 }
 
+int mdp_sweep_once(pp2_ctx* c) {
+  const int jn = c->jcur ^ 1;
+  HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
+                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A, nullptr, 0,
+                               nullptr));
+  c->jcur = jn;
+  return PP2_OK;
+}
+
+int fib_sweep_once(pp2_ctx* c) {
+  const int fn = c->fcur ^ 1;
+  HIPCHK(pp2::launch_fib_sweep(c->stream, c->g, c->gamma, c->T.v, c->L.v, c->R.v,
+                               c->fib[c->fcur].v, c->fib[fn].v));
+  c->fcur = fn;
+  return PP2_OK;
+}
+
+// max |cur - snap| over this shard (snap := cur); synchronises.
+int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* out) {
+  int np = 0;
+  HIPCHK(pp2::launch_absdiff_max(c->stream, c->g, cur.K, cur.v, snap.v,
+                                 c->rpartials, &np));
+  std::vector<float> h(np);
+  HIPCHK(hipMemcpyAsync(h.data(), c->rpartials, np * sizeof(float),
+                        hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float m = 0.0f;
+  for (float v : h) m = std::max(m, v);
+  *out = m;
+  return PP2_OK;
+}
+
 }  // namespace pp2rt
 
 using namespace pp2rt;
+
+int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep) {
+  if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  const int bn = c->bcur ^ 1;
+  const Planes& bi = c->b[c->bcur];
+  Planes& bo = c->b[bn];
+  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
+                                   bi.v.p, bo.v.p, u, z, c->bsum + c->bcur,
+                                   c->partials));
+  const int nparts = pp2::cells_grid(c->g, c->cpt);
+  if (fuse_with_sweep) {
+    const int jn = c->jcur ^ 1;
+    HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
+                                 c->J[c->jcur].v.p, c->J[jn].v.p, c->A,
+                                 c->partials, nparts, c->bsum + bn));
+    c->jcur = jn;
+  } else {
+    HIPCHK(pp2::launch_sum_finalize(c->stream, c->partials, nparts, c->bsum + bn));
+  }
+  CHECK(allreduce_mass(c, c->bsum + bn));
+  c->bcur = bn;
+  return PP2_OK;
+}
 
 // =========================================================================== C ABI
 extern "C" {
@@ -435,33 +498,10 @@ int pp2_belief_mass(pp2_ctx* c, float* mass) {
   return PP2_OK;
 }
 
-static int belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep) {
-  if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
-  const int bn = c->bcur ^ 1;
-  const Planes& bi = c->b[c->bcur];
-  Planes& bo = c->b[bn];
-  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
-                                   bi.v.p, bo.v.p, u, z, c->bsum + c->bcur,
-                                   c->partials));
-  const int nparts = pp2::cells_grid(c->g, c->cpt);
-  if (fuse_with_sweep) {
-    const int jn = c->jcur ^ 1;
-    HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
-                                 c->J[c->jcur].v.p, c->J[jn].v.p, c->A,
-                                 c->partials, nparts, c->bsum + bn));
-    c->jcur = jn;
-  } else {
-    HIPCHK(pp2::launch_sum_finalize(c->stream, c->partials, nparts, c->bsum + bn));
-  }
-  CHECK(allreduce_mass(c, c->bsum + bn));
-  c->bcur = bn;
-  return PP2_OK;
-}
-
 int pp2_belief_update(pp2_ctx* c, uint8_t u, uint8_t z) {
   CHECK(check_model(c));
   DeviceGuard dg(c->device);
-  CHECK(exchange_halos(c, {&c->b[c->bcur]}));
+  CHECK(exchange_halos(c, {HALO_BELIEF}));
   return belief_update_impl(c, u, z, false);
 }
 
@@ -481,12 +521,8 @@ int pp2_mdp_sweep(pp2_ctx* c, int n) {
   if (n < 0) return set_err(PP2_EINVAL, "negative sweep count");
   DeviceGuard dg(c->device);
   for (int i = 0; i < n; ++i) {
-    CHECK(exchange_halos(c, {&c->J[c->jcur]}));
-    const int jn = c->jcur ^ 1;
-    HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
-                                 c->J[c->jcur].v.p, c->J[jn].v.p, c->A, nullptr, 0,
-                                 nullptr));
-    c->jcur = jn;
+    CHECK(exchange_halos(c, {HALO_VALUE}));
+    CHECK(mdp_sweep_once(c));
   }
   return PP2_OK;
 }
@@ -528,7 +564,7 @@ int pp2_mdp_get(pp2_ctx* c, float* J, uint8_t* A) {
 int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   CHECK(check_model(c));
   DeviceGuard dg(c->device);
-  CHECK(exchange_halos(c, {&c->b[c->bcur], &c->J[c->jcur]}));
+  CHECK(exchange_halos(c, {HALO_BELIEF, HALO_VALUE}));
   return belief_update_impl(c, u, z, true);
 }
 
@@ -554,11 +590,8 @@ int pp2_fib_sweep(pp2_ctx* c, int n) {
   if (n < 0) return set_err(PP2_EINVAL, "negative sweep count");
   DeviceGuard dg(c->device);
   for (int i = 0; i < n; ++i) {
-    CHECK(exchange_halos(c, {&c->fib[c->fcur]}));
-    const int fn = c->fcur ^ 1;
-    HIPCHK(pp2::launch_fib_sweep(c->stream, c->g, c->gamma, c->T.v, c->L.v, c->R.v,
-                                 c->fib[c->fcur].v, c->fib[fn].v));
-    c->fcur = fn;
+    CHECK(exchange_halos(c, {HALO_FIB}));
+    CHECK(fib_sweep_once(c));
   }
   return PP2_OK;
 }

@@ -1,0 +1,277 @@
+// pp2_shards.cpp -- single-process row-shard groups (pp2_shard_group_*).
+//
+// One host thread drives the row shards of one grid, each a pp2_ctx on its own
+// stream (and device, or all on one device).  Every step runs phase-wise:
+//   1. each shard waits for its neighbours' previous step, then copies their
+//      boundary rows into its halo rows (device-to-device / peer copies);
+//   2. each shard runs its local kernels (the same launches as unsharded);
+//   3. the shards' partial belief masses are combined in rank order on shard
+//      0's stream and copied back to every shard.
+// This is the RCCL path of pp2_runtime.cpp (ncclSend/ncclRecv halo rows +
+// ncclAllReduce of the mass) with a different transport, so it exercises the
+// same shard geometry, halo semantics and mass bookkeeping on one GPU.
+#include <algorithm>
+#include <vector>
+
+#include "pp2_ctx.h"
+
+using namespace pp2rt;
+
+struct pp2_shard_group {
+  std::vector<pp2_ctx*> ctx;
+  std::vector<hipEvent_t> ev_done, ev_local;
+  hipEvent_t ev_total = nullptr;
+  float* d_gather = nullptr;  // on shard 0's device: n masses + total
+};
+
+namespace {
+
+int wait_neighbours(pp2_shard_group* g) {
+  const int n = (int)g->ctx.size();
+  for (int r = 0; r < n; ++r) {
+    DeviceGuard dg(g->ctx[r]->device);
+    if (r > 0) HIPCHK(hipStreamWaitEvent(g->ctx[r]->stream, g->ev_done[r - 1], 0));
+    if (r < n - 1) HIPCHK(hipStreamWaitEvent(g->ctx[r]->stream, g->ev_done[r + 1], 0));
+  }
+  return PP2_OK;
+}
+
+int exchange_local(pp2_shard_group* g, std::initializer_list<HaloKind> kinds) {
+  const int n = (int)g->ctx.size();
+  for (int r = 0; r < n; ++r) {
+    pp2_ctx* c = g->ctx[r];
+    DeviceGuard dg(c->device);
+    for (HaloKind k : kinds) {
+      const Planes& P = halo_planes(c, k);
+      const size_t bytes = (size_t)P.v.rs * sizeof(float);
+      if (r > 0) {
+        pp2_ctx* up = g->ctx[r - 1];
+        const Planes& Q = halo_planes(up, k);
+        HIPCHK(hipMemcpyAsync(P.v.p - P.v.rs, Q.v.p + (long long)(up->g.rows - 1) * Q.v.rs,
+                              bytes, hipMemcpyDefault, c->stream));
+      }
+      if (r < n - 1) {
+        const Planes& Q = halo_planes(g->ctx[r + 1], k);
+        HIPCHK(hipMemcpyAsync(P.v.p + (long long)c->g.rows * P.v.rs, Q.v.p, bytes,
+                              hipMemcpyDefault, c->stream));
+      }
+    }
+  }
+  return PP2_OK;
+}
+
+// Global mass = sum of shard masses in rank order, written to every shard.
+int combine_mass(pp2_shard_group* g) {
+  const int n = (int)g->ctx.size();
+  pp2_ctx* c0 = g->ctx[0];
+  for (int r = 0; r < n; ++r) {
+    DeviceGuard dg(g->ctx[r]->device);
+    HIPCHK(hipEventRecord(g->ev_local[r], g->ctx[r]->stream));
+  }
+  {
+    DeviceGuard dg(c0->device);
+    for (int r = 0; r < n; ++r) {
+      HIPCHK(hipStreamWaitEvent(c0->stream, g->ev_local[r], 0));
+      pp2_ctx* c = g->ctx[r];
+      HIPCHK(hipMemcpyAsync(g->d_gather + r, c->bsum + c->bcur, sizeof(float),
+                            hipMemcpyDefault, c0->stream));
+    }
+    HIPCHK(pp2::launch_sum_finalize(c0->stream, g->d_gather, n, g->d_gather + n));
+    HIPCHK(hipEventRecord(g->ev_total, c0->stream));
+  }
+  for (int r = 0; r < n; ++r) {
+    pp2_ctx* c = g->ctx[r];
+    DeviceGuard dg(c->device);
+    HIPCHK(hipStreamWaitEvent(c->stream, g->ev_total, 0));
+    HIPCHK(hipMemcpyAsync(c->bsum + c->bcur, g->d_gather + n, sizeof(float),
+                          hipMemcpyDefault, c->stream));
+  }
+  return PP2_OK;
+}
+
+int mark_done(pp2_shard_group* g) {
+  for (size_t r = 0; r < g->ctx.size(); ++r) {
+    DeviceGuard dg(g->ctx[r]->device);
+    HIPCHK(hipEventRecord(g->ev_done[r], g->ctx[r]->stream));
+  }
+  return PP2_OK;
+}
+
+int check_group(pp2_shard_group* g) {
+  if (!g || g->ctx.empty()) return set_err(PP2_EINVAL, "null shard group");
+  for (pp2_ctx* c : g->ctx) CHECK(check_model(c));
+  return PP2_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pp2_shard_group_destroy(pp2_shard_group* g);
+
+int pp2_shard_group_create(pp2_shard_group** out, pp2_ctx* const* ctxs, int n) {
+  if (!out || !ctxs || n < 1) return set_err(PP2_EINVAL, "bad shard group arguments");
+  *out = nullptr;
+  int next_row = 0, grows = -1, width = -1;
+  for (int r = 0; r < n; ++r) {
+    pp2_ctx* c = ctxs[r];
+    CHECK(check_ctx(c));
+    if (c->group || c->nranks > 1)
+      return set_err(PP2_ESTATE, "context %d already belongs to a group / RCCL comm", r);
+    if (grows < 0) { grows = c->g.grows; width = c->g.width; }
+    if (c->g.grows != grows || c->g.width != width || c->g.row0 != next_row)
+      return set_err(PP2_EINVAL, "contexts are not consecutive row shards of one grid");
+    next_row += c->g.rows;
+  }
+  if (next_row != grows) return set_err(PP2_EINVAL, "shards do not cover the grid");
+  pp2_shard_group* g = new pp2_shard_group();
+  g->ctx.assign(ctxs, ctxs + n);
+  g->ev_done.assign(n, nullptr);
+  g->ev_local.assign(n, nullptr);
+  auto fail = [&](int s) {
+    pp2_shard_group_destroy(g);
+    return s;
+  };
+  // peer access between the shards' devices (a no-op on one device)
+  for (int r = 0; r < n; ++r)
+    for (int q = 0; q < n; ++q) {
+      const int a = ctxs[r]->device, b = ctxs[q]->device;
+      if (a == b) continue;
+      DeviceGuard dg(a);
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can) {
+        hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+          return fail(set_err(PP2_EHIP, "peer access %d->%d: %s", a, b, hipGetErrorString(e)));
+        (void)hipGetLastError();
+      }
+    }
+  for (int r = 0; r < n; ++r) {
+    DeviceGuard dg(ctxs[r]->device);
+    if (hipEventCreateWithFlags(&g->ev_done[r], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->ev_local[r], hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(g->ev_done[r], ctxs[r]->stream) != hipSuccess)
+      return fail(set_err(PP2_EHIP, "shard group events"));
+  }
+  {
+    DeviceGuard dg(ctxs[0]->device);
+    if (hipEventCreateWithFlags(&g->ev_total, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&g->d_gather, (n + 1) * sizeof(float)) != hipSuccess)
+      return fail(set_err(PP2_ENOMEM, "shard group scratch"));
+  }
+  for (int r = 0; r < n; ++r) {
+    ctxs[r]->group = g;
+    ctxs[r]->grank = r;
+  }
+  *out = g;
+  return PP2_OK;
+}
+
+int pp2_shard_group_destroy(pp2_shard_group* g) {
+  if (!g) return PP2_OK;
+  (void)pp2_shard_group_synchronize(g);
+  for (size_t r = 0; r < g->ctx.size(); ++r) {
+    DeviceGuard dg(g->ctx[r]->device);
+    if (g->ev_done[r]) (void)hipEventDestroy(g->ev_done[r]);
+    if (g->ev_local[r]) (void)hipEventDestroy(g->ev_local[r]);
+    if (g->ctx[r]->group == g) g->ctx[r]->group = nullptr;
+  }
+  if (!g->ctx.empty()) {
+    DeviceGuard dg(g->ctx[0]->device);
+    if (g->ev_total) (void)hipEventDestroy(g->ev_total);
+    if (g->d_gather) (void)hipFree(g->d_gather);
+  }
+  delete g;
+  return PP2_OK;
+}
+
+int pp2_shard_group_synchronize(pp2_shard_group* g) {
+  if (!g) return set_err(PP2_EINVAL, "null shard group");
+  for (pp2_ctx* c : g->ctx) {
+    DeviceGuard dg(c->device);
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  return PP2_OK;
+}
+
+int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z) {
+  CHECK(check_group(g));
+  CHECK(wait_neighbours(g));
+  CHECK(exchange_local(g, {HALO_BELIEF, HALO_VALUE}));
+  for (pp2_ctx* c : g->ctx) {
+    DeviceGuard dg(c->device);
+    CHECK(belief_update_impl(c, u, z, true));
+  }
+  CHECK(combine_mass(g));
+  return mark_done(g);
+}
+
+int pp2_shard_group_belief_update(pp2_shard_group* g, uint8_t u, uint8_t z) {
+  CHECK(check_group(g));
+  CHECK(wait_neighbours(g));
+  CHECK(exchange_local(g, {HALO_BELIEF}));
+  for (pp2_ctx* c : g->ctx) {
+    DeviceGuard dg(c->device);
+    CHECK(belief_update_impl(c, u, z, false));
+  }
+  CHECK(combine_mass(g));
+  return mark_done(g);
+}
+
+int pp2_shard_group_mdp_sweep(pp2_shard_group* g, int n) {
+  CHECK(check_group(g));
+  if (n < 0) return set_err(PP2_EINVAL, "negative sweep count");
+  for (int i = 0; i < n; ++i) {
+    CHECK(wait_neighbours(g));
+    CHECK(exchange_local(g, {HALO_VALUE}));
+    for (pp2_ctx* c : g->ctx) {
+      DeviceGuard dg(c->device);
+      CHECK(mdp_sweep_once(c));
+    }
+    CHECK(mark_done(g));
+  }
+  return PP2_OK;
+}
+
+int pp2_shard_group_fib_sweep(pp2_shard_group* g, int n) {
+  CHECK(check_group(g));
+  if (n < 0) return set_err(PP2_EINVAL, "negative sweep count");
+  for (int i = 0; i < n; ++i) {
+    CHECK(wait_neighbours(g));
+    CHECK(exchange_local(g, {HALO_FIB}));
+    for (pp2_ctx* c : g->ctx) {
+      DeviceGuard dg(c->device);
+      CHECK(fib_sweep_once(c));
+    }
+    CHECK(mark_done(g));
+  }
+  return PP2_OK;
+}
+
+int pp2_shard_group_mdp_solve(pp2_shard_group* g, int max_sweeps, int* sweeps,
+                              double* final_norm) {
+  CHECK(check_group(g));
+  for (pp2_ctx* c : g->ctx) CHECK(pp2_mdp_reset(c));
+  CHECK(mark_done(g));
+  const double max_cost = 5.0 / (1.0 - (double)g->ctx[0]->gamma);
+  int total = 0;
+  double norm = 0.0;
+  do {
+    CHECK(pp2_shard_group_mdp_sweep(g, 100));
+    total += 100;
+    float m = 0.0f;
+    for (pp2_ctx* c : g->ctx) {
+      DeviceGuard dg(c->device);
+      float mr = 0.0f;
+      CHECK(absdiff_local_max(c, c->J[c->jcur], c->Jsnap, &mr));
+      m = std::max(m, mr);
+    }
+    norm = (double)m;
+    if (max_sweeps > 0 && total >= max_sweeps) break;
+  } while (norm > max_cost * 1e-3);
+  if (sweeps) *sweeps = total;
+  if (final_norm) *final_norm = norm;
+  return PP2_OK;
+}
+
+}  // extern "C"
