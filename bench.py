@@ -14,9 +14,11 @@ For N > 1 launch with torch.distributed.run: rank r owns rows
 [r*S, (r+1)*S) of an (N*S) x S grid (weak scaling), exchanging one halo row
 per step with its neighbours and all-reducing the belief mass over RCCL.
 
-Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the
-Bellman sweep, 369 algorithmic bytes per cell: T 324 + C 36 + J 4 + J' 4 +
-A 1), timed live with HIP events on the stream it runs on; `cpu_baseline` is
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant (and only)
+kernel of a step, k_loop_step -- the fused belief update + Bellman sweep, 417
+algorithmic bytes per cell (belief: T_u 36 + L_z 4 + b 4 + b' 4; sweep: T 324
++ C 36 + J 4 + J' 4 + A 1) -- timed live with HIP events around the timed
+steps on the stream it runs on; `cpu_baseline` is
 the C restatement of the reference (oracle/) timed on this host on a bounded
 sample of the same workload.
 """
@@ -322,7 +324,7 @@ def main():
     sweep_gbs = BYTES_SWEEP * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
     belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
     loop_gbs = BYTES_LOOP * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("k_mdp_sweep", cells_per_gpu)
+    traffic, traffic_src = pmc_traffic("k_loop_step", cells_per_gpu)
 
     result = None
     plan = None
@@ -356,18 +358,21 @@ def main():
                 "cells_per_lane": args.cpt,
             },
             "roofline": {
-                "kernel": "k_mdp_sweep (MDP Bellman sweep)",
+                "kernel": "k_loop_step (fused belief update + MDP Bellman sweep)",
                 "bound": "hbm",
-                "achieved": sweep_gbs,
+                "achieved": loop_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": sweep_gbs / HBM_PEAK_GBS,
+                "frac": loop_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": BYTES_SWEEP * cells_per_gpu,
-                "avg_launch_us": sweep_ms * 1e3,
+                "algorithmic_bytes_per_launch": BYTES_LOOP * cells_per_gpu,
+                "avg_launch_us": loop_ms_events * 1e3,
             },
             "kernels": {
+                "mdp_sweep_us": sweep_ms * 1e3,
+                "mdp_sweep_gbs": sweep_gbs,
+                "mdp_sweep_frac": sweep_gbs / HBM_PEAK_GBS,
                 "belief_update_us": belief_ms * 1e3,
                 "belief_update_gbs": belief_gbs,
                 "belief_update_frac": belief_gbs / HBM_PEAK_GBS,

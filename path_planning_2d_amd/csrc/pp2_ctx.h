@@ -74,7 +74,9 @@ struct pp2_ctx {
   uint8_t* A = nullptr;      // rows * wp actions
   Planes fib[2], fibsnap;    // FIB alphas (9 planes)
   int fcur = 0;
-  float* partials = nullptr;   // belief partial sums
+  float* pbuf[2] = {nullptr, nullptr};  // per-block partial masses of b[0], b[1]
+  bool pending[2] = {false, false};     // mass of b[i] still in pbuf[i]
+  int pcount[2] = {0, 0};               // number of partials in pbuf[i]
   float* rpartials = nullptr;  // convergence-check partials
   int partials_cap = 0;
   void* staging = nullptr;     // dense host-layout staging buffer
@@ -107,6 +109,8 @@ int check_model(pp2_ctx* c);
 size_t owned_cells(const pp2_ctx* c);
 int download_planes(pp2_ctx* c, const Planes& P, float* host, const float* divide_by);
 int belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep);
+int loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass);
+int ensure_mass(pp2_ctx* c);
 int mdp_sweep_once(pp2_ctx* c);
 int fib_sweep_once(pp2_ctx* c);
 int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* out);

@@ -96,14 +96,6 @@ __device__ __forceinline__ float block_max(float v, float* lds4) {
   return r;
 }
 
-// Reduce partials[0..n) in a fixed order with one 256-thread block.
-__device__ __forceinline__ float block_reduce_partials(const float* __restrict__ partials,
-                                                       int n, float* lds4) {
-  float s = 0.0f;
-  for (int i = threadIdx.x; i < n; i += kBlock) s += partials[i];
-  return block_sum(s, lds4);
-}
-
 int cells_grid(const Geom& g, int cpt) {
   const long long threads = (long long)g.rows * (g.wp / cpt);
   return (int)((threads + kBlock - 1) / kBlock);
@@ -286,16 +278,25 @@ hipError_t launch_belief_update(hipStream_t st, const Geom& g, int cpt,
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(kBlock) void k_sum_finalize(const float* __restrict__ partials,
-                                                         int n, float* __restrict__ out) {
-  __shared__ float lds4[4];
-  const float s = block_reduce_partials(partials, n, lds4);
+// One wave, lane-strided then xor-butterfly: the same association as
+// wave_reduce_partials in k_loop_step, so a mass finalised here and one
+// reduced inside the next fused step are bit-identical.
+__device__ __forceinline__ float wave_reduce_partials(const float* __restrict__ p, int n) {
+  const int lane = threadIdx.x & 63;
+  float s = 0.0f;
+  for (int i = lane; i < n; i += 64) s += p[i];
+  return wave_sum(s);
+}
+
+__global__ __launch_bounds__(64) void k_sum_finalize(const float* __restrict__ partials,
+                                                     int n, float* __restrict__ out) {
+  const float s = wave_reduce_partials(partials, n);
   if (threadIdx.x == 0) *out = s;
 }
 
 hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
                                float* out) {
-  hipLaunchKernelGGL(k_sum_finalize, dim3(1), dim3(kBlock), 0, st, partials, n, out);
+  hipLaunchKernelGGL(k_sum_finalize, dim3(1), dim3(64), 0, st, partials, n, out);
   return hipGetLastError();
 }
 
@@ -304,15 +305,11 @@ hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
 // (src/mdp/path_planning_2d_cuda.cu:215-264):
 //   J'(x) = min_u C[x][u] + sum_i (gamma*T[x][u][i]) * J(x+off_i),
 //   A(x)  = first u attaining the min (strict <).
-// Optionally, workgroup 0 also folds the belief partial sums of the
-// preceding update into *fin_out (the north-star loop's normalisation, at no
-// extra launch).
 // ============================================================================
 template <int CPT>
 __global__ __launch_bounds__(kBlock) void k_mdp_sweep(
     Geom g, float gamma, PlaneSet T, PlaneSet C, const float* __restrict__ J_in,
-    float* __restrict__ J_out, uint8_t* __restrict__ A,
-    const float* __restrict__ fin_partials, int fin_n, float* __restrict__ fin_out) {
+    float* __restrict__ J_out, uint8_t* __restrict__ A) {
   const int tpr = g.wp / CPT;
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const int y = (int)(t / tpr);
@@ -335,18 +332,30 @@ __global__ __launch_bounds__(kBlock) void k_mdp_sweep(
     for (int k = 0; k < CPT; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
     const float* trow = T.p + (long long)y * T.rs + x0;
     const float* crow = C.p + (long long)y * C.rs + x0;
+    // Register double-buffering over actions: the 10 vector loads of action
+    // u+1 (C and 9 T planes) are issued before action u is reduced, so each
+    // wave keeps 10-20 dwordx4 loads in flight instead of one.
+    float cb[2][CPT], tb[2][9][CPT];
+    ldv<CPT, true>(crow, cb[0]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) ldv<CPT, true>(trow + (long long)i * T.ps, tb[0][i]);
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
-      float cost[CPT];
-      ldv<CPT, true>(crow + (long long)u * C.ps, cost);
+      const int cur = u & 1, nxt = cur ^ 1;
+      if (u < 8) {
+        ldv<CPT, true>(crow + (long long)(u + 1) * C.ps, cb[nxt]);
 #pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        float tv[CPT];
-        ldv<CPT, true>(trow + (long long)(9 * u + i) * T.ps, tv);
+        for (int i = 0; i < 9; ++i)
+          ldv<CPT, true>(trow + (long long)(9 * (u + 1) + i) * T.ps, tb[nxt][i]);
+      }
+      float cost[CPT];
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) cost[k] = cb[cur][k];
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
 #pragma unroll
         for (int k = 0; k < CPT; ++k)
-          cost[k] = __builtin_fmaf(gamma * tv[k], jn[i][k], cost[k]);
-      }
+          cost[k] = __builtin_fmaf(gamma * tb[cur][i][k], jn[i][k], cost[k]);
 #pragma unroll
       for (int k = 0; k < CPT; ++k)
         if (cost[k] < best[k]) { best[k] = cost[k]; arg[k] = (uint32_t)u; }
@@ -361,24 +370,166 @@ __global__ __launch_bounds__(kBlock) void k_mdp_sweep(
       *ap = (uint8_t)arg[0];
     }
   }
-  if (fin_partials != nullptr && blockIdx.x == 0) {
-    __shared__ float lds4[4];
-    const float s = block_reduce_partials(fin_partials, fin_n, lds4);
-    if (threadIdx.x == 0) *fin_out = s;
-  }
 }
 
 hipError_t launch_mdp_sweep(hipStream_t st, const Geom& g, int cpt,
                             float gamma, PlaneSet T, PlaneSet C,
-                            const float* J_in, float* J_out, uint8_t* A,
-                            const float* fin_partials, int fin_n,
-                            float* fin_out) {
+                            const float* J_in, float* J_out, uint8_t* A) {
   const int grid = cells_grid(g, cpt);
   switch (cpt) {
-    case 4: hipLaunchKernelGGL(k_mdp_sweep<4>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A, fin_partials, fin_n, fin_out); break;
-    case 2: hipLaunchKernelGGL(k_mdp_sweep<2>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A, fin_partials, fin_n, fin_out); break;
-    default: hipLaunchKernelGGL(k_mdp_sweep<1>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A, fin_partials, fin_n, fin_out); break;
+    case 4: hipLaunchKernelGGL(k_mdp_sweep<4>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A); break;
+    case 2: hipLaunchKernelGGL(k_mdp_sweep<2>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A); break;
+    default: hipLaunchKernelGGL(k_mdp_sweep<1>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A); break;
   }
+  return hipGetLastError();
+}
+
+// ============================================================================
+// North-star loop step, fused: one launch = one belief update (a2, with the
+// previous step's renormalisation a3) + one Bellman sweep (a4) over the same
+// rows.  Compared with the two kernels back to back this removes a launch
+// boundary and the belief kernel's ramp/tail, and the belief's T_u rows are
+// the rows the sweep of this and the neighbouring rows stream anyway, so they
+// mostly hit L2 / the Infinity Cache instead of HBM.
+//  * block -> row mapping is XCD-aware: the blocks dispatched to one XCD
+//    (same blockIdx % 8) take consecutive rows, so rows y-1, y, y+1 share an
+//    L2 (a speed choice only; any dispatch order is correct);
+//  * every wave re-reduces the previous step's per-block belief partials in
+//    a fixed order (bit-identical in all blocks), so the 1/sum of the input
+//    is known without a separate finalize launch;
+//  * arithmetic per cell is exactly k_belief_update's and k_mdp_sweep's.
+// ============================================================================
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  const int q = n / 8, r = n % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <int CPT>
+__global__ __launch_bounds__(kBlock) void k_loop_step(
+    Geom g, float gamma, PlaneSet T, PlaneSet L, PlaneSet C,
+    const float* __restrict__ b_in, float* __restrict__ b_out, int u, int z,
+    const float* __restrict__ in_partials, int in_n, const float* __restrict__ in_sum,
+    float* __restrict__ in_sum_out, float* __restrict__ out_partials,
+    const float* __restrict__ J_in, float* __restrict__ J_out, uint8_t* __restrict__ A) {
+  __shared__ float lds4[4];
+  const int tpr = g.wp / CPT;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const long long t = (long long)blk * kBlock + threadIdx.x;
+  const int y = (int)(t / tpr);
+  const int x0 = (int)(t % tpr) * CPT;
+  float local = 0.0f;
+  // the previous step's mass (identical bits in every wave of every block)
+  float S = 1.0f;
+  if (in_partials) S = wave_reduce_partials(in_partials, in_n);
+  else if (in_sum) S = *in_sum;
+  if (in_sum_out && blockIdx.x == 0 && threadIdx.x == 0) *in_sum_out = S;
+  if (y < g.rows) {
+    const bool le = x0 == 0, re = x0 + CPT == g.wp;
+    // ---- belief update (k_belief_update)
+    float p[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) p[k] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int oy = s / 3 - 1, ox = s % 3 - 1;
+      const float* tp = T.p + (long long)(y + oy) * T.rs +
+                        (long long)(9 * u + 8 - s) * T.ps + x0 + ox;
+      const float* bp = b_in + (long long)(y + oy) * g.wp + x0 + ox;
+      float tv[CPT], bv[CPT];
+      if (ox == 0) {
+        ldv<CPT, true>(tp, tv);
+        ldv<CPT, true>(bp, bv);
+      } else {
+        ldv<CPT, false>(tp, tv);
+        ldv<CPT, false>(bp, bv);
+      }
+      if (ox < 0 && le) { tv[0] = 0.0f; bv[0] = 0.0f; }
+      if (ox > 0 && re) { tv[CPT - 1] = 0.0f; bv[CPT - 1] = 0.0f; }
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) p[k] = __builtin_fmaf(tv[k], bv[k], p[k]);
+    }
+    float lv[CPT];
+    ldv<CPT, true>(L.p + (long long)y * L.rs + (long long)z * L.ps + x0, lv);
+    const float inv = 1.0f / S;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      p[k] = p[k] * lv[k];
+      p[k] = p[k] * inv;
+      local += p[k];
+    }
+    stv<CPT>(b_out + (long long)y * g.wp + x0, p);
+
+    // ---- Bellman sweep (k_mdp_sweep)
+    float jn[9][CPT];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int oy = i / 3 - 1, ox = i % 3 - 1;
+      const float* jp = J_in + (long long)(y + oy) * g.wp + x0 + ox;
+      if (ox == 0) ldv<CPT, true>(jp, jn[i]);
+      else ldv<CPT, false>(jp, jn[i]);
+      if (ox < 0 && le) jn[i][0] = 0.0f;
+      if (ox > 0 && re) jn[i][CPT - 1] = 0.0f;
+    }
+    float best[CPT];
+    uint32_t arg[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
+    const float* trow = T.p + (long long)y * T.rs + x0;
+    const float* crow = C.p + (long long)y * C.rs + x0;
+    float cb[2][CPT], tb[2][9][CPT];
+    ldv<CPT, true>(crow, cb[0]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) ldv<CPT, true>(trow + (long long)i * T.ps, tb[0][i]);
+#pragma unroll
+    for (int a = 0; a < 9; ++a) {
+      const int cur = a & 1, nxt = cur ^ 1;
+      if (a < 8) {
+        ldv<CPT, true>(crow + (long long)(a + 1) * C.ps, cb[nxt]);
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+          ldv<CPT, true>(trow + (long long)(9 * (a + 1) + i) * T.ps, tb[nxt][i]);
+      }
+      float cost[CPT];
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) cost[k] = cb[cur][k];
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int k = 0; k < CPT; ++k)
+          cost[k] = __builtin_fmaf(gamma * tb[cur][i][k], jn[i][k], cost[k]);
+#pragma unroll
+      for (int k = 0; k < CPT; ++k)
+        if (cost[k] < best[k]) { best[k] = cost[k]; arg[k] = (uint32_t)a; }
+    }
+    stv<CPT>(J_out + (long long)y * g.wp + x0, best);
+    uint8_t* ap = A + (long long)y * g.wp + x0;
+    if constexpr (CPT == 4) {
+      *reinterpret_cast<uint32_t*>(ap) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    } else if constexpr (CPT == 2) {
+      *reinterpret_cast<uint16_t*>(ap) = (uint16_t)(arg[0] | (arg[1] << 8));
+    } else {
+      *ap = (uint8_t)arg[0];
+    }
+  }
+  const float bs = block_sum(local, lds4);
+  if (threadIdx.x == 0) out_partials[blk] = bs;
+}
+
+hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
+                            PlaneSet T, PlaneSet L, PlaneSet C, const float* b_in,
+                            float* b_out, int u, int z, const float* in_partials,
+                            int in_n, const float* in_sum, float* in_sum_out,
+                            float* out_partials, const float* J_in, float* J_out,
+                            uint8_t* A) {
+  const int grid = cells_grid(g, cpt);
+#define PP2_LOOP_ARGS g, gamma, T, L, C, b_in, b_out, u, z, in_partials, in_n, in_sum, \
+                      in_sum_out, out_partials, J_in, J_out, A
+  switch (cpt) {
+    case 4: hipLaunchKernelGGL(k_loop_step<4>, dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS); break;
+    case 2: hipLaunchKernelGGL(k_loop_step<2>, dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS); break;
+    default: hipLaunchKernelGGL(k_loop_step<1>, dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS); break;
+  }
+#undef PP2_LOOP_ARGS
   return hipGetLastError();
 }
 

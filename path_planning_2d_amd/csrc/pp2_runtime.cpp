@@ -195,7 +195,8 @@ int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
   if (hipMemcpyAsync(c->bsum, ones, sizeof ones, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return fail(set_err(PP2_EHIP, "bsum init"));
   c->partials_cap = pp2::cells_grid(c->g, 1) + 1;
-  if (hipMalloc(&c->partials, c->partials_cap * sizeof(float)) != hipSuccess ||
+  if (hipMalloc(&c->pbuf[0], c->partials_cap * sizeof(float)) != hipSuccess ||
+      hipMalloc(&c->pbuf[1], c->partials_cap * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->rpartials, c->partials_cap * sizeof(float)) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "hipMalloc partials"));
   if (hipStreamSynchronize(c->stream) != hipSuccess)
@@ -256,8 +257,7 @@ std::string join(const char* dir, const char* name) {
 int mdp_sweep_once(pp2_ctx* c) {
   const int jn = c->jcur ^ 1;
   HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
-                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A, nullptr, 0,
-                               nullptr));
+                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A));
   c->jcur = jn;
   return PP2_OK;
 }
@@ -289,26 +289,53 @@ int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* 
 
 using namespace pp2rt;
 
+int pp2rt::ensure_mass(pp2_ctx* c) {
+  if (!c->pending[c->bcur]) return PP2_OK;
+  HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[c->bcur], c->pcount[c->bcur],
+                                  c->bsum + c->bcur));
+  c->pending[c->bcur] = false;
+  return PP2_OK;
+}
+
+// Belief update alone (k_belief_update), mass finalised eagerly.
 int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep) {
+  if (fuse_with_sweep) return loop_step_fused(c, u, z, true);
   if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  CHECK(ensure_mass(c));
   const int bn = c->bcur ^ 1;
-  const Planes& bi = c->b[c->bcur];
-  Planes& bo = c->b[bn];
-  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
-                                   bi.v.p, bo.v.p, u, z, c->bsum + c->bcur,
-                                   c->partials));
   const int nparts = pp2::cells_grid(c->g, c->cpt);
-  if (fuse_with_sweep) {
-    const int jn = c->jcur ^ 1;
-    HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
-                                 c->J[c->jcur].v.p, c->J[jn].v.p, c->A,
-                                 c->partials, nparts, c->bsum + bn));
-    c->jcur = jn;
-  } else {
-    HIPCHK(pp2::launch_sum_finalize(c->stream, c->partials, nparts, c->bsum + bn));
-  }
+  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
+                                   c->b[c->bcur].v.p, c->b[bn].v.p, u, z,
+                                   c->bsum + c->bcur, c->pbuf[bn]));
+  HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bn], nparts, c->bsum + bn));
+  c->pending[bn] = false;
   CHECK(allreduce_mass(c, c->bsum + bn));
   c->bcur = bn;
+  return PP2_OK;
+}
+
+// One fused north-star step (k_loop_step).  The input mass is reduced inside
+// the kernel when still pending; the output mass stays pending (eager_mass =
+// false) or is finalised (and all-reduced across RCCL shards) right away.
+int pp2rt::loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass) {
+  if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  const int bc = c->bcur, bn = bc ^ 1, jn = c->jcur ^ 1;
+  const int nparts = pp2::cells_grid(c->g, c->cpt);
+  const bool pend = c->pending[bc];
+  HIPCHK(pp2::launch_loop_step(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->L.v, c->C.v,
+                               c->b[bc].v.p, c->b[bn].v.p, u, z,
+                               pend ? c->pbuf[bc] : nullptr, c->pcount[bc],
+                               c->bsum + bc, pend ? c->bsum + bc : nullptr, c->pbuf[bn],
+                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A));
+  c->pending[bc] = false;
+  c->pcount[bn] = nparts;
+  c->pending[bn] = true;
+  c->bcur = bn;
+  c->jcur = jn;
+  if (eager_mass || c->nranks > 1) {
+    CHECK(ensure_mass(c));
+    CHECK(allreduce_mass(c, c->bsum + bn));
+  }
   return PP2_OK;
 }
 
@@ -364,7 +391,8 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->d_map) (void)hipFree(c->d_map);
   if (c->A) (void)hipFree(c->A);
   if (c->bsum) (void)hipFree(c->bsum);
-  if (c->partials) (void)hipFree(c->partials);
+  for (float* pb : c->pbuf)
+    if (pb) (void)hipFree(pb);
   if (c->rpartials) (void)hipFree(c->rpartials);
   if (c->staging) (void)hipFree(c->staging);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -468,6 +496,7 @@ int pp2_belief_set(pp2_ctx* c, const float* b) {
   if (!b) return set_err(PP2_EINVAL, "belief is null");
   DeviceGuard dg(c->device);
   CHECK(upload_planes(c, c->b[c->bcur], b));
+  c->pending[c->bcur] = false;
   const float one = 1.0f;
   HIPCHK(hipMemcpyAsync(c->bsum + c->bcur, &one, sizeof one, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -478,6 +507,7 @@ int pp2_belief_get(pp2_ctx* c, float* b) {
   CHECK(check_ctx(c));
   if (!b) return set_err(PP2_EINVAL, "belief is null");
   DeviceGuard dg(c->device);
+  CHECK(ensure_mass(c));
   return download_planes(c, c->b[c->bcur], b, c->bsum + c->bcur);
 }
 
@@ -493,6 +523,7 @@ int pp2_belief_mass(pp2_ctx* c, float* mass) {
   CHECK(check_ctx(c));
   if (!mass) return set_err(PP2_EINVAL, "mass is null");
   DeviceGuard dg(c->device);
+  CHECK(ensure_mass(c));
   HIPCHK(hipMemcpyAsync(mass, c->bsum + c->bcur, sizeof(float), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return PP2_OK;
@@ -565,7 +596,7 @@ int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   CHECK(check_model(c));
   DeviceGuard dg(c->device);
   CHECK(exchange_halos(c, {HALO_BELIEF, HALO_VALUE}));
-  return belief_update_impl(c, u, z, true);
+  return loop_step_fused(c, u, z, false);
 }
 
 int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {

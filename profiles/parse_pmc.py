@@ -19,7 +19,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
-ALGO = {"k_mdp_sweep": 369, "k_belief_update": 48}
+ALGO = {"k_mdp_sweep": 369, "k_belief_update": 48, "k_loop_step": 417}
 
 
 def short(name):
