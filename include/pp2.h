@@ -82,6 +82,14 @@ int pp2_get_geometry(pp2_ctx* ctx, uint32_t* rows, uint32_t* width,
                      uint32_t* row_stride, uint32_t* row_begin);
 /* Tuning: cells per lane of the streaming kernels (1, 2 or 4; default 4). */
 int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
+/* Tuning knobs (results are identical for every setting):
+ *  PP2_TUNE_CELLS_PER_LANE  1, 2 or 4
+ *  PP2_TUNE_NT_STREAMS      1 (default) = non-temporal loads of the
+ *                           once-read T/C streams (loop and sweep kernels,
+ *                           CPT 4): -8 % time per loop step measured */
+#define PP2_TUNE_CELLS_PER_LANE 1
+#define PP2_TUNE_NT_STREAMS 2
+int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
 /* ---------------------------------------------------------------- model
  * generateModelData (src/pomdp/model_generation_cuda.cu:349-368) and the MDP

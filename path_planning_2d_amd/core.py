@@ -94,6 +94,12 @@ class GridContext:
     def set_cells_per_lane(self, cpt: int):
         call("pp2_set_cells_per_lane", self._h, int(cpt))
 
+    TUNE_CELLS_PER_LANE = 1
+    TUNE_NT_STREAMS = 2
+
+    def set_tuning(self, key: int, value: int):
+        call("pp2_set_tuning", self._h, int(key), int(value))
+
     # ------------------------------------------------------------ model
     def model_generate(self):
         call("pp2_model_generate", self._h)

@@ -62,6 +62,7 @@ struct pp2_ctx {
   int32_t gx = 0, gy = 0;
   float gamma = 0.95f;
   int cpt = 4;
+  bool nt_streams = true;   // non-temporal loads of the once-read T/C streams
   bool model_ready = false;
 
   uint8_t* d_map = nullptr;  // global map (grows x width)

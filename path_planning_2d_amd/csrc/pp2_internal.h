@@ -41,7 +41,8 @@ hipError_t launch_belief_update(hipStream_t st, const Geom& g, int cpt,
                                 const float* in_sum, float* partials);
 hipError_t launch_mdp_sweep(hipStream_t st, const Geom& g, int cpt,
                             float gamma, PlaneSet T, PlaneSet C,
-                            const float* J_in, float* J_out, uint8_t* A);
+                            const float* J_in, float* J_out, uint8_t* A,
+                            bool nt);
 // Fused north-star step (belief update + Bellman sweep).  The input belief's
 // mass comes from in_partials[0..in_n) (reduced in-kernel) or *in_sum; block
 // 0 stores it to *in_sum_out if non-null.  out_partials gets one partial sum
@@ -51,7 +52,7 @@ hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
                             float* b_out, int u, int z, const float* in_partials,
                             int in_n, const float* in_sum, float* in_sum_out,
                             float* out_partials, const float* J_in, float* J_out,
-                            uint8_t* A);
+                            uint8_t* A, bool nt);
 hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
                                float* out);
 hipError_t launch_fib_sweep(hipStream_t st, const Geom& g, float gamma,

@@ -49,6 +49,17 @@ __device__ __forceinline__ void ldv(const float* __restrict__ p, float (&v)[N]) 
   }
 }
 
+// Non-temporal variant for streams read exactly once per launch (T, C).
+template <int N, bool NT>
+__device__ __forceinline__ void ldv_stream(const float* __restrict__ p, float (&v)[N]) {
+  if constexpr (NT && N == 4) {
+    const f4a t = __builtin_nontemporal_load(reinterpret_cast<const f4a*>(p));
+    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+  } else {
+    ldv<N, true>(p, v);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[N]) {
   if constexpr (N == 4) {
@@ -306,7 +317,7 @@ hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
 //   J'(x) = min_u C[x][u] + sum_i (gamma*T[x][u][i]) * J(x+off_i),
 //   A(x)  = first u attaining the min (strict <).
 // ============================================================================
-template <int CPT>
+template <int CPT, bool NT>
 __global__ __launch_bounds__(kBlock) void k_mdp_sweep(
     Geom g, float gamma, PlaneSet T, PlaneSet C, const float* __restrict__ J_in,
     float* __restrict__ J_out, uint8_t* __restrict__ A) {
@@ -336,17 +347,17 @@ __global__ __launch_bounds__(kBlock) void k_mdp_sweep(
     // u+1 (C and 9 T planes) are issued before action u is reduced, so each
     // wave keeps 10-20 dwordx4 loads in flight instead of one.
     float cb[2][CPT], tb[2][9][CPT];
-    ldv<CPT, true>(crow, cb[0]);
+    ldv_stream<CPT, NT>(crow, cb[0]);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) ldv<CPT, true>(trow + (long long)i * T.ps, tb[0][i]);
+    for (int i = 0; i < 9; ++i) ldv_stream<CPT, NT>(trow + (long long)i * T.ps, tb[0][i]);
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
       const int cur = u & 1, nxt = cur ^ 1;
       if (u < 8) {
-        ldv<CPT, true>(crow + (long long)(u + 1) * C.ps, cb[nxt]);
+        ldv_stream<CPT, NT>(crow + (long long)(u + 1) * C.ps, cb[nxt]);
 #pragma unroll
         for (int i = 0; i < 9; ++i)
-          ldv<CPT, true>(trow + (long long)(9 * (u + 1) + i) * T.ps, tb[nxt][i]);
+          ldv_stream<CPT, NT>(trow + (long long)(9 * (u + 1) + i) * T.ps, tb[nxt][i]);
       }
       float cost[CPT];
 #pragma unroll
@@ -374,12 +385,15 @@ __global__ __launch_bounds__(kBlock) void k_mdp_sweep(
 
 hipError_t launch_mdp_sweep(hipStream_t st, const Geom& g, int cpt,
                             float gamma, PlaneSet T, PlaneSet C,
-                            const float* J_in, float* J_out, uint8_t* A) {
+                            const float* J_in, float* J_out, uint8_t* A, bool nt) {
   const int grid = cells_grid(g, cpt);
   switch (cpt) {
-    case 4: hipLaunchKernelGGL(k_mdp_sweep<4>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A); break;
-    case 2: hipLaunchKernelGGL(k_mdp_sweep<2>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A); break;
-    default: hipLaunchKernelGGL(k_mdp_sweep<1>, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A); break;
+    case 4:
+      if (nt) hipLaunchKernelGGL((k_mdp_sweep<4, true>), dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A);
+      else hipLaunchKernelGGL((k_mdp_sweep<4, false>), dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A);
+      break;
+    case 2: hipLaunchKernelGGL((k_mdp_sweep<2, false>), dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A); break;
+    default: hipLaunchKernelGGL((k_mdp_sweep<1, false>), dim3(grid), dim3(kBlock), 0, st, g, gamma, T, C, J_in, J_out, A); break;
   }
   return hipGetLastError();
 }
@@ -404,7 +418,7 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <int CPT>
+template <int CPT, bool NT>
 __global__ __launch_bounds__(kBlock) void k_loop_step(
     Geom g, float gamma, PlaneSet T, PlaneSet L, PlaneSet C,
     const float* __restrict__ b_in, float* __restrict__ b_out, int u, int z,
@@ -477,17 +491,17 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
     const float* trow = T.p + (long long)y * T.rs + x0;
     const float* crow = C.p + (long long)y * C.rs + x0;
     float cb[2][CPT], tb[2][9][CPT];
-    ldv<CPT, true>(crow, cb[0]);
+    ldv_stream<CPT, NT>(crow, cb[0]);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) ldv<CPT, true>(trow + (long long)i * T.ps, tb[0][i]);
+    for (int i = 0; i < 9; ++i) ldv_stream<CPT, NT>(trow + (long long)i * T.ps, tb[0][i]);
 #pragma unroll
     for (int a = 0; a < 9; ++a) {
       const int cur = a & 1, nxt = cur ^ 1;
       if (a < 8) {
-        ldv<CPT, true>(crow + (long long)(a + 1) * C.ps, cb[nxt]);
+        ldv_stream<CPT, NT>(crow + (long long)(a + 1) * C.ps, cb[nxt]);
 #pragma unroll
         for (int i = 0; i < 9; ++i)
-          ldv<CPT, true>(trow + (long long)(9 * (a + 1) + i) * T.ps, tb[nxt][i]);
+          ldv_stream<CPT, NT>(trow + (long long)(9 * (a + 1) + i) * T.ps, tb[nxt][i]);
       }
       float cost[CPT];
 #pragma unroll
@@ -520,14 +534,17 @@ hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
                             float* b_out, int u, int z, const float* in_partials,
                             int in_n, const float* in_sum, float* in_sum_out,
                             float* out_partials, const float* J_in, float* J_out,
-                            uint8_t* A) {
+                            uint8_t* A, bool nt) {
   const int grid = cells_grid(g, cpt);
 #define PP2_LOOP_ARGS g, gamma, T, L, C, b_in, b_out, u, z, in_partials, in_n, in_sum, \
                       in_sum_out, out_partials, J_in, J_out, A
   switch (cpt) {
-    case 4: hipLaunchKernelGGL(k_loop_step<4>, dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS); break;
-    case 2: hipLaunchKernelGGL(k_loop_step<2>, dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS); break;
-    default: hipLaunchKernelGGL(k_loop_step<1>, dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS); break;
+    case 4:
+      if (nt) hipLaunchKernelGGL((k_loop_step<4, true>), dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS);
+      else hipLaunchKernelGGL((k_loop_step<4, false>), dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS);
+      break;
+    case 2: hipLaunchKernelGGL((k_loop_step<2, false>), dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS); break;
+    default: hipLaunchKernelGGL((k_loop_step<1, false>), dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS); break;
   }
 #undef PP2_LOOP_ARGS
   return hipGetLastError();

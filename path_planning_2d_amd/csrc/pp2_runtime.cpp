@@ -257,7 +257,7 @@ std::string join(const char* dir, const char* name) {
 int mdp_sweep_once(pp2_ctx* c) {
   const int jn = c->jcur ^ 1;
   HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
-                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A));
+                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A, c->nt_streams));
   c->jcur = jn;
   return PP2_OK;
 }
@@ -326,7 +326,7 @@ int pp2rt::loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass) {
                                c->b[bc].v.p, c->b[bn].v.p, u, z,
                                pend ? c->pbuf[bc] : nullptr, c->pcount[bc],
                                c->bsum + bc, pend ? c->bsum + bc : nullptr, c->pbuf[bn],
-                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A));
+                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A, c->nt_streams));
   c->pending[bc] = false;
   c->pcount[bn] = nparts;
   c->pending[bn] = true;
@@ -421,6 +421,15 @@ int pp2_get_geometry(pp2_ctx* c, uint32_t* rows, uint32_t* width,
   if (row_stride) *row_stride = (uint32_t)c->g.wp;
   if (row_begin) *row_begin = (uint32_t)c->g.row0;
   return PP2_OK;
+}
+
+int pp2_set_tuning(pp2_ctx* c, int key, int value) {
+  CHECK(check_ctx(c));
+  switch (key) {
+    case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
+    case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
+    default: return set_err(PP2_EINVAL, "unknown tuning key %d", key);
+  }
 }
 
 int pp2_set_cells_per_lane(pp2_ctx* c, int cpt) {
