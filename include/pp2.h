@@ -227,6 +227,30 @@ int pp2_planner_info(pp2_planner* p, pp2_tree_info* info);
  * u1[i], u2[i] = first and second draw of curand_init(seed, i, 0). */
 int pp2_curand_uniforms(uint64_t seed, int n, float* u1, float* u2);
 
+/* ---------------------------------------------------------------- rollouts
+ * Batched QV-tree rollouts (BASELINE configs[4]: 4096 copies x depth 5 at
+ * 512x512): C copies of a root belief each follow their own (u_k, z_k),
+ * k < depth.  Per copy and step: reward r_k = <b_k, R[:,u_k]> (QNode reward,
+ * search_tree_cuda.cu:168-173), observation likelihood p_k = sum of the
+ * unnormalised update, b_{k+1} = normalise(L_zk . T_uk^T b_k) (the
+ * reference update + renormalisation); leaf: FIB bound max_i <b_depth,
+ * alpha_i> (evaluateFibCpu); value = sum_k gamma^k r_k + gamma^depth * leaf.
+ * Beliefs are stored as per-copy max-normalised fp16 (2 B per cell-copy),
+ * arithmetic is fp32; expect ~1e-3 relative agreement with an fp32 rollout. */
+typedef struct pp2_rollout pp2_rollout;
+int pp2_rollout_create(pp2_rollout** out, pp2_ctx* ctx, int copies, int depth);
+int pp2_rollout_destroy(pp2_rollout* r);
+/* root belief (hw floats) copied into every copy */
+int pp2_rollout_set_root(pp2_rollout* r, const float* belief);
+/* us, zs: [depth][copies].  Asynchronous. */
+int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs);
+/* rewards, obs_prob: [depth][copies]; leaf_upper, value: [copies]; any may be
+ * NULL.  Synchronises. */
+int pp2_rollout_results(pp2_rollout* r, float* rewards, float* obs_prob,
+                        float* leaf_upper, float* value);
+/* normalised fp32 belief of one copy after the run (hw floats) */
+int pp2_rollout_get_belief(pp2_rollout* r, int copy, float* belief);
+
 /* ---------------------------------------------------------------- shards
  * Two transports for row shards (no reference counterpart):
  *  - one process per GPU: RCCL (pp2_rccl_unique_id / pp2_shard_comm_init);

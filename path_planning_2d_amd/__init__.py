@@ -7,8 +7,8 @@ package is the Python host mirror of that boundary.
 """
 from ._lib import Pp2Error, LIB_PATH
 from .core import GridContext, ShardGroup, device_count
-from .planner import QVTreePlanner
+from .planner import BatchedRollout, QVTreePlanner
 from . import maps, synthetic
 
-__all__ = ["GridContext", "ShardGroup", "QVTreePlanner", "device_count", "Pp2Error",
+__all__ = ["GridContext", "ShardGroup", "QVTreePlanner", "BatchedRollout", "device_count", "Pp2Error",
            "LIB_PATH", "maps", "synthetic"]

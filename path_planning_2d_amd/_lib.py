@@ -78,6 +78,12 @@ SIGNATURES = {
     "pp2_planner_reset": [_vp],
     "pp2_planner_info": [_vp, _vp],
     "pp2_curand_uniforms": [C.c_uint64, C.c_int, _f32p, _f32p],
+    "pp2_rollout_create": [C.POINTER(_vp), _vp, C.c_int, C.c_int],
+    "pp2_rollout_destroy": [_vp],
+    "pp2_rollout_set_root": [_vp, _f32p],
+    "pp2_rollout_run": [_vp, _u8p, _u8p],
+    "pp2_rollout_results": [_vp, _f32p, _f32p, _f32p, _f32p],
+    "pp2_rollout_get_belief": [_vp, C.c_int, _f32p],
     "pp2_shard_group_create": [C.POINTER(_vp), C.POINTER(_vp), C.c_int],
     "pp2_shard_group_destroy": [_vp],
     "pp2_shard_group_loop_step": [_vp, C.c_uint8, C.c_uint8],

@@ -84,4 +84,19 @@ hipError_t launch_belief_dots(hipStream_t st, const Geom& g, int cpt,
                               float* out);
 hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* mass);
 
+// Batched fp16 rollouts (pp2_rollout.cpp).  Beliefs: fp16 [copy][rows+2][wp],
+// cstride halfs per copy, copy plane origin at row -1.  A chunk is a run of
+// copies (indices copies[first .. first+n)) sharing the step's action.
+int rollout_waves(const Geom& g);
+hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
+                               PlaneSet R, const void* bin, void* bout, long long cstride,
+                               int nchunks, const int* chunk_u, const int* chunk_first,
+                               const int* chunk_n, const int* copies, const uint8_t* zs,
+                               const float* in_stats, float* partials, float* stats_out,
+                               int ncopies);
+hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const void* b,
+                               long long cstride, int ncopies, float* partials, float* out);
+hipError_t launch_rollout_broadcast(hipStream_t st, const void* src, void* dst,
+                                    long long cstride, int ncopies);
+
 }  // namespace pp2

@@ -890,6 +890,241 @@ hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* ma
 }
 
 // ============================================================================
+// Batched fp16 QV-tree rollouts (BASELINE configs[4]).  C copies of a belief
+// advance `depth` steps of the reference update (a2/a3), each copy with its
+// own (u, z) per step; every step scores the copy's QNode reward
+// <b, R[:,u]> (search_tree_cuda.cu:168-173), and the leaf is scored with the
+// FIB bound (fast_informed_bound_cuda.cu:278-297).
+//  * beliefs live as fp16 planes [copy][row][x] (2 B per cell-copy), each
+//    copy max-normalised: the update of step k multiplies by 1/max_k, so the
+//    stored values stay O(1) and tiny probabilities keep fp16 precision;
+//  * the math is fp32 (the reference fma chain on fp16-decoded inputs);
+//  * copies are grouped by action: one block loads its T_u stencil rows once
+//    and reuses them for up to kRollChunk copies (T_u amortised over copies);
+//  * per (copy, wave) partial sums of {stored sum, stored max, reward dot} are
+//    reduced per copy by k_rollout_reduce.
+// ============================================================================
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h4u __attribute__((ext_vector_type(4), aligned(2)));
+
+template <bool ALIGNED>
+__device__ __forceinline__ void ldh4(const _Float16* __restrict__ p, float (&v)[4]) {
+  h4 t;
+  if constexpr (ALIGNED) t = *reinterpret_cast<const h4*>(p);
+  else t = *reinterpret_cast<const h4u*>(p);
+  v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
+}
+
+constexpr int kRollStats = 3;  // stored sum, stored max, reward dot
+
+__global__ __launch_bounds__(kBlock) void k_rollout_step(
+    Geom g, PlaneSet T, PlaneSet L, PlaneSet R, const _Float16* __restrict__ bin,
+    _Float16* __restrict__ bout, long long cstride, const int* __restrict__ chunk_u,
+    const int* __restrict__ chunk_first, const int* __restrict__ chunk_n,
+    const int* __restrict__ copies, const uint8_t* __restrict__ zs,
+    const float* __restrict__ in_stats, float* __restrict__ partials, int nwaves) {
+  const int tpr = g.wp / 4;
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / tpr);
+  const int x0 = (int)(t % tpr) * 4;
+  const int ch = blockIdx.y;
+  const int u = chunk_u[ch], first = chunk_first[ch], n = chunk_n[ch];
+  const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const bool live = y < g.rows;
+  const bool le = x0 == 0, re = x0 + 4 == g.wp;
+  float tv[9][4], rv[4];
+  if (live) {
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int oy = s / 3 - 1, ox = s % 3 - 1;
+      const float* tp = T.p + (long long)(y + oy) * T.rs + (long long)(9 * u + 8 - s) * T.ps + x0 + ox;
+      if (ox == 0) ldv<4, true>(tp, tv[s]);
+      else ldv<4, false>(tp, tv[s]);
+      if (ox < 0 && le) tv[s][0] = 0.0f;
+      if (ox > 0 && re) tv[s][3] = 0.0f;
+    }
+    ldv<4, true>(R.p + (long long)y * R.rs + (long long)u * R.ps + x0, rv);
+  }
+  for (int j = 0; j < n; ++j) {
+    const int c = copies[first + j];
+    float sum = 0.0f, mx = 0.0f, rew = 0.0f;
+    if (live) {
+      const _Float16* bc = bin + (long long)c * cstride;
+      float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bcen[4];
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {
+        const int oy = s / 3 - 1, ox = s % 3 - 1;
+        const _Float16* bp = bc + (long long)(y + oy) * g.wp + x0 + ox;
+        float bv[4];
+        if (ox == 0) ldh4<true>(bp, bv);
+        else ldh4<false>(bp, bv);
+        if (ox < 0 && le) bv[0] = 0.0f;
+        if (ox > 0 && re) bv[3] = 0.0f;
+        if (s == 4) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) bcen[k] = bv[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[k] = __builtin_fmaf(tv[s][k], bv[k], p[k]);
+      }
+      float lv[4];
+      ldv<4, true>(L.p + (long long)y * L.rs + (long long)zs[c] * L.ps + x0, lv);
+      const float inv = 1.0f / in_stats[c * kRollStats + 1];  // 1 / stored max
+      h4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float v = (p[k] * lv[k]) * inv;
+        o[k] = (_Float16)v;
+        const float vr = (float)o[k];
+        sum += vr;
+        mx = fmaxf(mx, vr);
+        rew = __builtin_fmaf(bcen[k], rv[k], rew);
+      }
+      *reinterpret_cast<h4*>(bout + (long long)c * cstride + (long long)y * g.wp + x0) = o;
+    }
+    sum = wave_sum(sum);
+    mx = wave_max(mx);
+    rew = wave_sum(rew);
+    if ((threadIdx.x & 63) == 0) {
+      float* pp = partials + ((long long)c * nwaves + wave) * kRollStats;
+      pp[0] = sum;
+      pp[1] = mx;
+      pp[2] = rew;
+    }
+  }
+}
+
+// per copy: out[c] = {sum, max, reward} over its nwaves partials (fixed order)
+__global__ __launch_bounds__(64) void k_rollout_reduce(const float* __restrict__ partials,
+                                                       int nwaves, int copies,
+                                                       float* __restrict__ out) {
+  const int c = blockIdx.x;
+  if (c >= copies) return;
+  const float* pp = partials + (long long)c * nwaves * kRollStats;
+  float s = 0.0f, m = 0.0f, r = 0.0f;
+  for (int i = threadIdx.x; i < nwaves; i += 64) {
+    s += pp[i * kRollStats + 0];
+    m = fmaxf(m, pp[i * kRollStats + 1]);
+    r += pp[i * kRollStats + 2];
+  }
+  s = wave_sum(s);
+  m = wave_max(m);
+  r = wave_sum(r);
+  if (threadIdx.x == 0) {
+    out[c * kRollStats + 0] = s;
+    out[c * kRollStats + 1] = m;
+    out[c * kRollStats + 2] = r;
+  }
+}
+
+// Leaf FIB dots of every copy: partials[c][wave][10] = {sum, dot_0..dot_8}
+__global__ __launch_bounds__(kBlock) void k_rollout_leaf(Geom g, PlaneSet F,
+                                                         const _Float16* __restrict__ b,
+                                                         long long cstride, int copies,
+                                                         float* __restrict__ partials,
+                                                         int nwaves) {
+  const int tpr = g.wp / 4;
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / tpr);
+  const int x0 = (int)(t % tpr) * 4;
+  const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const bool live = y < g.rows;
+  float fv[9][4];
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+      ldv<4, true>(F.p + (long long)y * F.rs + (long long)i * F.ps + x0, fv[i]);
+  }
+  for (int c = blockIdx.y; c < copies; c += gridDim.y) {
+    float acc[kStats];
+#pragma unroll
+    for (int i = 0; i < kStats; ++i) acc[i] = 0.0f;
+    if (live) {
+      float bv[4];
+      ldh4<true>(b + (long long)c * cstride + (long long)y * g.wp + x0, bv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[0] += bv[k];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) acc[1 + i] = __builtin_fmaf(bv[k], fv[i][k], acc[1 + i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kStats; ++i) acc[i] = wave_sum(acc[i]);
+    if ((threadIdx.x & 63) == 0) {
+      float* pp = partials + ((long long)c * nwaves + wave) * kStats;
+#pragma unroll
+      for (int i = 0; i < kStats; ++i) pp[i] = acc[i];
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_rollout_leaf_reduce(const float* __restrict__ partials,
+                                                            int nwaves, int copies,
+                                                            float* __restrict__ out) {
+  const int c = blockIdx.x;
+  if (c >= copies) return;
+  const float* pp = partials + (long long)c * nwaves * kStats;
+  for (int i = 0; i < kStats; ++i) {
+    float s = 0.0f;
+    for (int w = threadIdx.x; w < nwaves; w += 64) s += pp[w * kStats + i];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) out[c * kStats + i] = s;
+  }
+}
+
+// broadcast one fp16 plane image (rows+2 halo rows, wp) into every copy
+__global__ __launch_bounds__(kBlock) void k_rollout_broadcast(const _Float16* __restrict__ src,
+                                                              _Float16* __restrict__ dst,
+                                                              long long cstride, int copies) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= cstride) return;
+  const _Float16 v = src[i];
+  for (int c = blockIdx.y; c < copies; c += gridDim.y) dst[(long long)c * cstride + i] = v;
+}
+
+int rollout_waves(const Geom& g) { return cells_grid(g, 4) * (kBlock / 64); }
+
+hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
+                               PlaneSet R, const void* bin, void* bout, long long cstride,
+                               int nchunks, const int* chunk_u, const int* chunk_first,
+                               const int* chunk_n, const int* copies, const uint8_t* zs,
+                               const float* in_stats, float* partials, float* stats_out,
+                               int ncopies) {
+  const int tiles = cells_grid(g, 4);
+  const int nw = rollout_waves(g);
+  // copy planes start at row -1: the kernels index rows from row 0
+  hipLaunchKernelGGL(k_rollout_step, dim3(tiles, nchunks), dim3(kBlock), 0, st, g, T, L, R,
+                     (const _Float16*)bin + g.wp, (_Float16*)bout + g.wp, cstride, chunk_u, chunk_first,
+                     chunk_n, copies, zs, in_stats, partials, nw);
+  hipLaunchKernelGGL(k_rollout_reduce, dim3(ncopies), dim3(64), 0, st, partials, nw, ncopies,
+                     stats_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const void* b,
+                               long long cstride, int ncopies, float* partials,
+                               float* out) {
+  const int tiles = cells_grid(g, 4);
+  const int nw = rollout_waves(g);
+  const int gy = ncopies < 64 ? ncopies : 64;
+  hipLaunchKernelGGL(k_rollout_leaf, dim3(tiles, gy), dim3(kBlock), 0, st, g, F,
+                     (const _Float16*)b + g.wp, cstride, ncopies, partials, nw);
+  hipLaunchKernelGGL(k_rollout_leaf_reduce, dim3(ncopies), dim3(64), 0, st, partials, nw,
+                     ncopies, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout_broadcast(hipStream_t st, const void* src, void* dst,
+                                    long long cstride, int ncopies) {
+  const int gx = (int)((cstride + kBlock - 1) / kBlock);
+  const int gy = ncopies < 256 ? ncopies : 256;
+  hipLaunchKernelGGL(k_rollout_broadcast, dim3(gx, gy), dim3(kBlock), 0, st,
+                     (const _Float16*)src, (_Float16*)dst, cstride, ncopies);
+  return hipGetLastError();
+}
+
+// ============================================================================
 // Layout conversion between the reference's AoS host arrays
 // (T[hw][9][9], L[hw][16], R[hw][9], beliefs[hw]) and the SoA planes.
 // ============================================================================

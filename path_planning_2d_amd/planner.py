@@ -124,3 +124,56 @@ def curand_uniforms(seed: int, n: int):
          u1.ctypes.data_as(C.POINTER(C.c_float)),
          u2.ctypes.data_as(C.POINTER(C.c_float)))
     return u1, u2
+
+
+class BatchedRollout:
+    """Batched fp16 QV-tree rollouts (pp2_rollout_*; BASELINE configs[4]):
+    ``copies`` copies of a root belief, each following its own ``depth``-step
+    (u, z) sequence; per-copy rewards, observation likelihoods, FIB leaf bound
+    and discounted value."""
+
+    def __init__(self, ctx: GridContext, copies: int, depth: int):
+        self.ctx = ctx
+        self.copies = int(copies)
+        self.depth = int(depth)
+        h = C.c_void_p()
+        call("pp2_rollout_create", C.byref(h), ctx.handle, self.copies, self.depth)
+        self._h = h
+
+    def set_root(self, belief):
+        b = np.ascontiguousarray(belief, np.float32).reshape(self.ctx.cells)
+        call("pp2_rollout_set_root", self._h, b.ctypes.data_as(C.POINTER(C.c_float)))
+
+    def run(self, us, zs):
+        us = np.ascontiguousarray(us, np.uint8).reshape(self.depth, self.copies)
+        zs = np.ascontiguousarray(zs, np.uint8).reshape(self.depth, self.copies)
+        call("pp2_rollout_run", self._h, us.ctypes.data_as(C.POINTER(C.c_uint8)),
+             zs.ctypes.data_as(C.POINTER(C.c_uint8)))
+
+    def results(self):
+        f = C.POINTER(C.c_float)
+        r = np.empty((self.depth, self.copies), np.float32)
+        p = np.empty((self.depth, self.copies), np.float32)
+        ub = np.empty(self.copies, np.float32)
+        v = np.empty(self.copies, np.float32)
+        call("pp2_rollout_results", self._h, r.ctypes.data_as(f), p.ctypes.data_as(f),
+             ub.ctypes.data_as(f), v.ctypes.data_as(f))
+        return {"rewards": r, "obs_prob": p, "leaf_upper": ub, "value": v}
+
+    def belief(self, copy: int):
+        out = np.empty(self.ctx.cells, np.float32)
+        call("pp2_rollout_get_belief", self._h, int(copy),
+             out.ctypes.data_as(C.POINTER(C.c_float)))
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            from ._lib import load
+            load().pp2_rollout_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -158,3 +158,40 @@ def synth_trajectory(grid: np.ndarray, n: int, seed: int = 42):
                 break
         us[k], zs[k], st[k] = u, z, y * W + x
     return us, zs, st
+
+
+def rollout_trajectories(grid: np.ndarray, belief: np.ndarray, copies: int, depth: int,
+                         seed: int = 5):
+    """(us, zs) of shape [depth, copies] for batched rollouts: each copy draws a
+    true start cell from ``belief`` and simulates u ~ U{0..8}, s' ~ T, z ~ L,
+    so every observation has positive likelihood under its copy's belief."""
+    H, W = grid.shape
+    rng = SplitMix64(seed)
+    cdf = np.cumsum(belief.astype(np.float64))
+    us = np.empty((depth, copies), np.uint8)
+    zs = np.empty((depth, copies), np.uint8)
+    for c in range(copies):
+        cell = int(min(np.searchsorted(cdf, rng.u01() * cdf[-1], side="right"), H * W - 1))
+        while belief[cell] <= 0:
+            cell -= 1
+        x, y = cell % W, cell // W
+        for k in range(depth):
+            u = min(int(rng.u01() * 9.0), 8)
+            tp = cell_transition(grid, x, y, u)
+            r, acc, j = rng.u01(), 0.0, 4
+            for i in range(9):
+                acc += float(tp[i])
+                if tp[i] > 0 and r < acc:
+                    j = i
+                    break
+            x += j % 3 - 1
+            y += j // 3 - 1
+            lk = cell_likelihood(grid, x, y)
+            r, acc, z = rng.u01(), 0.0, 15
+            for i in range(16):
+                acc += float(lk[i])
+                if r < acc:
+                    z = i
+                    break
+            us[k, c], zs[k, c] = u, z
+    return us, zs
