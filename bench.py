@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--plan-size", type=int, default=256)
     ap.add_argument("--plan-depth", type=int, default=3)
     ap.add_argument("--cpu-plan-seconds", type=float, default=15.0)
+    ap.add_argument("--rollout-copies", type=int, default=4096,
+                    help="batched fp16 rollout copies (0 disables)")
+    ap.add_argument("--rollout-depth", type=int, default=5)
+    ap.add_argument("--rollout-size", type=int, default=512)
     ap.add_argument("--profile", action="store_true",
                     help="only run warmup+timed steps (for rocprofv3)")
     return ap.parse_args()
@@ -205,6 +209,51 @@ def plan_step_bench(args, device, stream_handle, with_cpu):
     return out
 
 
+def rollout_bench(args, device, stream):
+    """BASELINE configs[4]: 512x512 grid, 4096 belief copies x depth 5, fp16
+    beliefs.  Algorithmic bytes per cell-copy-step: fp16 belief read 2 +
+    write 2 (T_u / L_z / R_u amortised over the copies sharing the action),
+    plus 2 per cell-copy for the FIB leaf pass."""
+    import torch
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    N, C, D = args.rollout_size, args.rollout_copies, args.rollout_depth
+    grid = S.synth_grid(N, N, seed=N)
+    goal = S.synth_goal(grid)
+    b0 = S.uniform_belief(grid)
+    us, zs = S.rollout_trajectories(grid, b0, C, D, seed=13)
+    ctx = P.GridContext(grid, goal, gamma=GAMMA, device=device)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.model_generate()
+    ctx.fib_solve(max_sweeps=40)
+    with P.BatchedRollout(ctx, C, D) as r:
+        r.set_root(b0)
+        r.run(us, zs)  # warm-up
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(5):
+            r.set_root(b0)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            r.run(us, zs)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        res = r.results()
+    ctx.close()
+    ms = float(np.median(times))
+    cell_copy_steps = N * N * C * D
+    algo_bytes = cell_copy_steps * 4 + N * N * C * 2
+    return {"config": f"{N}x{N} grid, {C} belief copies x depth {D}, fp16 beliefs "
+                      f"(fp32 math), copies grouped by action",
+            "ms_per_rollout": ms,
+            "cell_copy_steps_per_s": cell_copy_steps / (ms * 1e-3),
+            "algorithmic_GBps": algo_bytes / (ms * 1e-3) / 1e9,
+            "hbm_frac": algo_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "mean_value": float(res["value"].mean())}
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -331,6 +380,9 @@ def main():
     if rank == 0 and ws == 1 and args.plan_steps > 0:
         plan = plan_step_bench(args, local, stream.cuda_stream,
                                with_cpu=not args.no_cpu_baseline)
+    rollout = None
+    if rank == 0 and ws == 1 and args.rollout_copies > 0:
+        rollout = rollout_bench(args, local, stream)
     if rank == 0:
         cpu = None
         if ws == 1 and not args.no_cpu_baseline:
@@ -383,6 +435,7 @@ def main():
             },
             "belief_mass_ok": mass_ok,
             "plan_step": plan,
+            "rollout": rollout,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result))

@@ -88,6 +88,8 @@ hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* ma
 // cstride halfs per copy, copy plane origin at row -1.  A chunk is a run of
 // copies (indices copies[first .. first+n)) sharing the step's action.
 int rollout_waves(const Geom& g);
+int rollout_chunk();      // copies per chunk (block) of the selected variant
+int rollout_min_chunk();  // smallest chunk of any variant (sizes chunk tables)
 hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
                                PlaneSet R, const void* bin, void* bout, long long cstride,
                                int nchunks, const int* chunk_u, const int* chunk_first,

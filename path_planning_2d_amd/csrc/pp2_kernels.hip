@@ -14,6 +14,7 @@
 // library is built with -fgpu-flush-denormals-to-zero (the reference is built
 // with --use_fast_math, CMakeLists.txt:36) and -ffp-contract=off.
 #include <float.h>
+#include <stdlib.h>
 
 #include "pp2_internal.h"
 
@@ -915,25 +916,79 @@ __device__ __forceinline__ void ldh4(const _Float16* __restrict__ p, float (&v)[
   v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
 }
 
-constexpr int kRollStats = 3;  // stored sum, stored max, reward dot
+struct RollRaw {  // one copy's raw stencil loads for one lane (4 cells)
+  h4 m[3];              // rows y-1, y, y+1 at x0..x0+3
+  uint32_t lw[3], rw[3];  // halves x0-2..x0-1 and x0+4..x0+5 of each row
+  float l[4];           // L_z at x0..x0+3
+};
 
+__device__ __forceinline__ _Float16 h2_lo(uint32_t w) {
+  return __builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu));
+}
+__device__ __forceinline__ _Float16 h2_hi(uint32_t w) {
+  return __builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+}
+
+// b points at (row y, x0) of one copy; every address is dword aligned (x0 is
+// a multiple of 4) and lies inside the copy's halo rows or the guards.
+__device__ __forceinline__ void roll_load(RollRaw& q, const _Float16* __restrict__ b, int wp,
+                                          const float* __restrict__ lp) {
+#pragma unroll
+  for (int row = 0; row < 3; ++row) {
+    const _Float16* bp = b + (long long)(row - 1) * wp;
+    q.m[row] = *reinterpret_cast<const h4*>(bp);
+    q.lw[row] = *reinterpret_cast<const uint32_t*>(bp - 2);
+    q.rw[row] = *reinterpret_cast<const uint32_t*>(bp + 4);
+  }
+  const float4 l4 = *reinterpret_cast<const float4*>(lp);
+  q.l[0] = l4.x; q.l[1] = l4.y; q.l[2] = l4.z; q.l[3] = l4.w;
+}
+
+constexpr int kRollStats = 3;  // stored sum, stored max, reward dot
+constexpr int kRollIter = 8;   // 1024-cell slabs per block tile
+constexpr int kRollChunk = 8;  // copies per block (sharing one action)
+
+// A block owns kRollIter consecutive 1024-cell slabs (row-major over the
+// padded grid) for one chunk of <= kRollChunk copies that share the action:
+// the T_u stencil and R_u of a slab are loaded once for all copies, and each
+// copy's {sum, max, reward} stays in registers until one wave reduction per
+// copy at the end of the tile.
+template <int CH, int PF>
 __global__ __launch_bounds__(kBlock) void k_rollout_step(
     Geom g, PlaneSet T, PlaneSet L, PlaneSet R, const _Float16* __restrict__ bin,
     _Float16* __restrict__ bout, long long cstride, const int* __restrict__ chunk_u,
-    const int* __restrict__ chunk_first, const int* __restrict__ chunk_n,
-    const int* __restrict__ copies, const uint8_t* __restrict__ zs,
-    const float* __restrict__ in_stats, float* __restrict__ partials, int nwaves) {
-  const int tpr = g.wp / 4;
-  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const int y = (int)(t / tpr);
-  const int x0 = (int)(t % tpr) * 4;
+    const int* __restrict__ chunk_first, const int* __restrict__ copies,
+    const uint8_t* __restrict__ zs, const float* __restrict__ in_stats,
+    float* __restrict__ partials, int nwaves) {
+  // Chunks always hold CH entries (the host repeats a partial chunk's last
+  // copy; a repeat writes the same belief and partials as the original), and
+  // lanes past the grid end clamp to its last cell: the slab loop has no
+  // branches, so the compiler's vmcnt waits can follow the prefetch pipeline.
   const int ch = blockIdx.y;
-  const int u = chunk_u[ch], first = chunk_first[ch], n = chunk_n[ch];
+  const int u = chunk_u[ch], first = chunk_first[ch];
   const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  const bool live = y < g.rows;
-  const bool le = x0 == 0, re = x0 + 4 == g.wp;
-  float tv[9][4], rv[4];
-  if (live) {
+  const long long ncells = (long long)g.rows * g.wp;
+  const long long tile0 = (long long)blockIdx.x * kRollIter * (kBlock * 4);
+  const int iters = (int)min((long long)kRollIter, (ncells - tile0 + kBlock * 4 - 1) / (kBlock * 4));
+  long long cbase[CH];
+  int cid[CH], zc[CH];
+  float inv[CH], acc[CH][kRollStats];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int c = copies[first + j];
+    cid[j] = c;
+    cbase[j] = (long long)c * cstride;
+    zc[j] = zs[c];
+    inv[j] = 1.0f / in_stats[c * kRollStats + 1];  // 1 / stored max
+    acc[j][0] = acc[j][1] = acc[j][2] = 0.0f;
+  }
+  for (int it = 0; it < iters; ++it) {
+    const long long cell_raw = tile0 + (long long)it * (kBlock * 4) + threadIdx.x * 4;
+    const bool valid = cell_raw < ncells;
+    const long long cell = valid ? cell_raw : ncells - 4;
+    const int y = (int)(cell / g.wp), x0 = (int)(cell % g.wp);
+    const bool le = x0 == 0, re = x0 + 4 == g.wp;
+    float tv[9][4], rv[4];
 #pragma unroll
     for (int s = 0; s < 9; ++s) {
       const int oy = s / 3 - 1, ox = s % 3 - 1;
@@ -944,52 +999,65 @@ __global__ __launch_bounds__(kBlock) void k_rollout_step(
       if (ox > 0 && re) tv[s][3] = 0.0f;
     }
     ldv<4, true>(R.p + (long long)y * R.rs + (long long)u * R.ps + x0, rv);
-  }
-  for (int j = 0; j < n; ++j) {
-    const int c = copies[first + j];
-    float sum = 0.0f, mx = 0.0f, rew = 0.0f;
-    if (live) {
-      const _Float16* bc = bin + (long long)c * cstride;
+    const long long off = (long long)y * g.wp + x0;
+    const float* lrow = L.p + (long long)y * L.rs + x0;
+    // software pipeline over the chunk: copy j+PF's loads are in flight while
+    // copy j is computed (one copy at a time leaves too few bytes in flight
+    // per wave to cover HBM latency)
+    RollRaw q[PF + 1];
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      roll_load(q[j], bin + cbase[j] + off, g.wp, lrow + (long long)zc[j] * L.ps);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (j + PF < CH)
+        roll_load(q[(j + PF) % (PF + 1)], bin + cbase[j + PF] + off, g.wp,
+                  lrow + (long long)zc[j + PF] * L.ps);
+      const RollRaw& r = q[j % (PF + 1)];
       float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bcen[4];
 #pragma unroll
-      for (int s = 0; s < 9; ++s) {
-        const int oy = s / 3 - 1, ox = s % 3 - 1;
-        const _Float16* bp = bc + (long long)(y + oy) * g.wp + x0 + ox;
-        float bv[4];
-        if (ox == 0) ldh4<true>(bp, bv);
-        else ldh4<false>(bp, bv);
-        if (ox < 0 && le) bv[0] = 0.0f;
-        if (ox > 0 && re) bv[3] = 0.0f;
-        if (s == 4) {
+      for (int row = 0; row < 3; ++row) {
+        // x+-1 neighbours: aligned 8-byte centre load + the adjacent halves
+        // of the dwords either side (fp16 x+-1 loads are not dword aligned)
+        float w[6];
+        w[0] = le ? 0.0f : (float)h2_hi(r.lw[row]);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) bcen[k] = bv[k];
+        for (int k = 0; k < 4; ++k) w[1 + k] = (float)r.m[row][k];
+        w[5] = re ? 0.0f : (float)h2_lo(r.rw[row]);
+        if (row == 1) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) bcen[k] = w[1 + k];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) p[k] = __builtin_fmaf(tv[s][k], bv[k], p[k]);
+        for (int ox = -1; ox <= 1; ++ox) {
+          const int s = row * 3 + (ox + 1);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) p[k] = __builtin_fmaf(tv[s][k], w[k + 1 + ox], p[k]);
+        }
       }
-      float lv[4];
-      ldv<4, true>(L.p + (long long)y * L.rs + (long long)zs[c] * L.ps + x0, lv);
-      const float inv = 1.0f / in_stats[c * kRollStats + 1];  // 1 / stored max
       h4 o;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float v = (p[k] * lv[k]) * inv;
+        const float v = (p[k] * r.l[k]) * inv[j];
         o[k] = (_Float16)v;
-        const float vr = (float)o[k];
-        sum += vr;
-        mx = fmaxf(mx, vr);
-        rew = __builtin_fmaf(bcen[k], rv[k], rew);
+        const float vr = valid ? (float)o[k] : 0.0f;
+        acc[j][0] += vr;
+        acc[j][1] = fmaxf(acc[j][1], vr);
+        acc[j][2] = __builtin_fmaf(valid ? bcen[k] : 0.0f, rv[k], acc[j][2]);
       }
-      *reinterpret_cast<h4*>(bout + (long long)c * cstride + (long long)y * g.wp + x0) = o;
+      __builtin_nontemporal_store(o, reinterpret_cast<h4*>(bout + cbase[j] + off));
     }
-    sum = wave_sum(sum);
-    mx = wave_max(mx);
-    rew = wave_sum(rew);
+  }
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const float sm = wave_sum(acc[j][0]);
+    const float mx = wave_max(acc[j][1]);
+    const float rw = wave_sum(acc[j][2]);
     if ((threadIdx.x & 63) == 0) {
-      float* pp = partials + ((long long)c * nwaves + wave) * kRollStats;
-      pp[0] = sum;
+      float* pp = partials + ((long long)cid[j] * nwaves + wave) * kRollStats;
+      pp[0] = sm;
       pp[1] = mx;
-      pp[2] = rew;
+      pp[2] = rw;
     }
   }
 }
@@ -1017,44 +1085,60 @@ __global__ __launch_bounds__(64) void k_rollout_reduce(const float* __restrict__
   }
 }
 
-// Leaf FIB dots of every copy: partials[c][wave][10] = {sum, dot_0..dot_8}
+// Leaf FIB dots of every copy: partials[c][wave][10] = {sum, dot_0..dot_8};
+// same tiling as k_rollout_step, the alpha planes loaded once per slab.
 __global__ __launch_bounds__(kBlock) void k_rollout_leaf(Geom g, PlaneSet F,
                                                          const _Float16* __restrict__ b,
                                                          long long cstride, int copies,
                                                          float* __restrict__ partials,
                                                          int nwaves) {
-  const int tpr = g.wp / 4;
-  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const int y = (int)(t / tpr);
-  const int x0 = (int)(t % tpr) * 4;
+  // branch-free like k_rollout_step: copies past the end repeat the last one
+  // (identical partials), lanes past the grid end add nothing
+  const int c0 = blockIdx.y * kRollChunk;
   const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  const bool live = y < g.rows;
-  float fv[9][4];
-  if (live) {
+  const long long ncells = (long long)g.rows * g.wp;
+  const long long tile0 = (long long)blockIdx.x * kRollIter * (kBlock * 4);
+  const int iters = (int)min((long long)kRollIter, (ncells - tile0 + kBlock * 4 - 1) / (kBlock * 4));
+  long long cbase[kRollChunk];
+  float acc[kRollChunk][kStats];
+#pragma unroll
+  for (int j = 0; j < kRollChunk; ++j) {
+    cbase[j] = (long long)min(c0 + j, copies - 1) * cstride;
+#pragma unroll
+    for (int i = 0; i < kStats; ++i) acc[j][i] = 0.0f;
+  }
+  for (int it = 0; it < iters; ++it) {
+    const long long cell_raw = tile0 + (long long)it * (kBlock * 4) + threadIdx.x * 4;
+    const bool valid = cell_raw < ncells;
+    const long long cell = valid ? cell_raw : ncells - 4;
+    const int y = (int)(cell / g.wp), x0 = (int)(cell % g.wp);
+    const long long off = (long long)y * g.wp + x0;
+    float bq[kRollChunk][4];
+#pragma unroll
+    for (int j = 0; j < kRollChunk; ++j) ldh4<true>(b + cbase[j] + off, bq[j]);
+    float fv[9][4];
 #pragma unroll
     for (int i = 0; i < 9; ++i)
       ldv<4, true>(F.p + (long long)y * F.rs + (long long)i * F.ps + x0, fv[i]);
-  }
-  for (int c = blockIdx.y; c < copies; c += gridDim.y) {
-    float acc[kStats];
 #pragma unroll
-    for (int i = 0; i < kStats; ++i) acc[i] = 0.0f;
-    if (live) {
-      float bv[4];
-      ldh4<true>(b + (long long)c * cstride + (long long)y * g.wp + x0, bv);
+    for (int j = 0; j < kRollChunk; ++j) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        acc[0] += bv[k];
+        const float bv = valid ? bq[j][k] : 0.0f;
+        acc[j][0] += bv;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) acc[1 + i] = __builtin_fmaf(bv[k], fv[i][k], acc[1 + i]);
+        for (int i = 0; i < 9; ++i) acc[j][1 + i] = __builtin_fmaf(bv, fv[i][k], acc[j][1 + i]);
       }
     }
+  }
 #pragma unroll
-    for (int i = 0; i < kStats; ++i) acc[i] = wave_sum(acc[i]);
+  for (int j = 0; j < kRollChunk; ++j) {
+#pragma unroll
+    for (int i = 0; i < kStats; ++i) acc[j][i] = wave_sum(acc[j][i]);
     if ((threadIdx.x & 63) == 0) {
-      float* pp = partials + ((long long)c * nwaves + wave) * kStats;
+      float* pp = partials + ((long long)min(c0 + j, copies - 1) * nwaves + wave) * kStats;
 #pragma unroll
-      for (int i = 0; i < kStats; ++i) pp[i] = acc[i];
+      for (int i = 0; i < kStats; ++i) pp[i] = acc[j][i];
     }
   }
 }
@@ -1083,7 +1167,29 @@ __global__ __launch_bounds__(kBlock) void k_rollout_broadcast(const _Float16* __
   for (int c = blockIdx.y; c < copies; c += gridDim.y) dst[(long long)c * cstride + i] = v;
 }
 
-int rollout_waves(const Geom& g) { return cells_grid(g, 4) * (kBlock / 64); }
+int rollout_tiles(const Geom& g) {
+  const long long cells = (long long)g.rows * g.wp;
+  const long long per = (long long)kRollIter * kBlock * 4;
+  return (int)((cells + per - 1) / per);
+}
+int rollout_waves(const Geom& g) { return rollout_tiles(g) * (kBlock / 64); }
+
+// (copies per chunk, prefetch distance) variants of k_rollout_step;
+// PP2_ROLLOUT_VARIANT selects one for A/B runs (tools/prof_rollout.py).
+namespace {
+struct RollVariant { int ch, pf; };
+constexpr RollVariant kRollVariants[] = {{8, 1}, {8, 2}, {4, 1}, {4, 2}, {16, 1}, {8, 3}};
+int roll_variant() {
+  static const int v = [] {
+    const char* e = getenv("PP2_ROLLOUT_VARIANT");
+    const int i = e ? atoi(e) : 0;
+    return (i >= 0 && i < (int)(sizeof(kRollVariants) / sizeof(kRollVariants[0]))) ? i : 0;
+  }();
+  return v;
+}
+}  // namespace
+int rollout_chunk() { return kRollVariants[roll_variant()].ch; }
+int rollout_min_chunk() { return 4; }
 
 hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
                                PlaneSet R, const void* bin, void* bout, long long cstride,
@@ -1091,12 +1197,24 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
                                const int* chunk_n, const int* copies, const uint8_t* zs,
                                const float* in_stats, float* partials, float* stats_out,
                                int ncopies) {
-  const int tiles = cells_grid(g, 4);
+  const int tiles = rollout_tiles(g);
   const int nw = rollout_waves(g);
   // copy planes start at row -1: the kernels index rows from row 0
-  hipLaunchKernelGGL(k_rollout_step, dim3(tiles, nchunks), dim3(kBlock), 0, st, g, T, L, R,
-                     (const _Float16*)bin + g.wp, (_Float16*)bout + g.wp, cstride, chunk_u, chunk_first,
-                     chunk_n, copies, zs, in_stats, partials, nw);
+  const dim3 grid(tiles, nchunks);
+  const _Float16* bi = (const _Float16*)bin + g.wp;
+  _Float16* bo = (_Float16*)bout + g.wp;
+#define PP2_ROLL(CH, PF)                                                                   \
+  hipLaunchKernelGGL((k_rollout_step<CH, PF>), grid, dim3(kBlock), 0, st, g, T, L, R, bi, bo, \
+                     cstride, chunk_u, chunk_first, copies, zs, in_stats, partials, nw)
+  switch (roll_variant()) {
+    case 1: PP2_ROLL(8, 2); break;
+    case 2: PP2_ROLL(4, 1); break;
+    case 3: PP2_ROLL(4, 2); break;
+    case 4: PP2_ROLL(16, 1); break;
+    case 5: PP2_ROLL(8, 3); break;
+    default: PP2_ROLL(8, 1); break;
+  }
+#undef PP2_ROLL
   hipLaunchKernelGGL(k_rollout_reduce, dim3(ncopies), dim3(64), 0, st, partials, nw, ncopies,
                      stats_out);
   return hipGetLastError();
@@ -1105,9 +1223,9 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
 hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const void* b,
                                long long cstride, int ncopies, float* partials,
                                float* out) {
-  const int tiles = cells_grid(g, 4);
+  const int tiles = rollout_tiles(g);
   const int nw = rollout_waves(g);
-  const int gy = ncopies < 64 ? ncopies : 64;
+  const int gy = (ncopies + kRollChunk - 1) / kRollChunk;
   hipLaunchKernelGGL(k_rollout_leaf, dim3(tiles, gy), dim3(kBlock), 0, st, g, F,
                      (const _Float16*)b + g.wp, cstride, ncopies, partials, nw);
   hipLaunchKernelGGL(k_rollout_leaf_reduce, dim3(ncopies), dim3(64), 0, st, partials, nw,

@@ -15,7 +15,7 @@
 using namespace pp2rt;
 
 namespace {
-constexpr int kChunk = 32;
+constexpr int kMaxChunk = 64;  // bound on rollout_chunk() (chunk padding room)
 constexpr int kRollStats = 3;
 constexpr int kLeafStats = 10;
 }  // namespace
@@ -63,7 +63,7 @@ int pp2_rollout_create(pp2_rollout** out, pp2_ctx* c, int copies, int depth) {
   r->copies = copies;
   r->depth = depth;
   r->cstride = (long long)(c->g.rows + 2) * c->g.wp + 16;  // + guard, keeps copies 32-B aligned
-  r->maxchunks = copies / kChunk + 9 + 1;
+  r->maxchunks = copies / pp2::rollout_min_chunk() + 9 + 1;
   const size_t bbytes = (size_t)r->cstride * copies * sizeof(_Float16) + 128;
   const int nw = pp2::rollout_waves(c->g);
   auto fail = [&](int s) {
@@ -78,7 +78,7 @@ int pp2_rollout_create(pp2_rollout** out, pp2_ctx* c, int copies, int depth) {
       hipMalloc(&r->d_stats, (size_t)(depth + 1) * copies * kRollStats * sizeof(float)) != hipSuccess ||
       hipMalloc(&r->d_leaf, (size_t)copies * kLeafStats * sizeof(float)) != hipSuccess ||
       hipMalloc(&r->d_partials, (size_t)copies * nw * kLeafStats * sizeof(float)) != hipSuccess ||
-      hipMalloc(&r->d_chunks, (size_t)depth * (3 * r->maxchunks + copies) * sizeof(int)) != hipSuccess ||
+      hipMalloc(&r->d_chunks, (size_t)depth * (3 * r->maxchunks + copies + 9 * kMaxChunk) * sizeof(int)) != hipSuccess ||
       hipMalloc(&r->d_zs, (size_t)depth * copies) != hipSuccess ||
       hipMalloc(&r->d_root, (size_t)r->cstride * sizeof(_Float16)) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "rollout scratch"));
@@ -126,7 +126,9 @@ int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs) {
   pp2_ctx* c = r->ctx;
   DeviceGuard dg(c->device);
   const int C = r->copies, D = r->depth, M = r->maxchunks;
-  const long long stride = 3LL * M + C;
+  const int kChunk = pp2::rollout_chunk();
+  if (kChunk > kMaxChunk) return set_err(PP2_ESTATE, "rollout chunk too large");
+  const long long stride = 3LL * M + C + 9LL * kChunk;
   std::vector<int> host((size_t)D * stride, 0);
   r->nchunks.assign(D, 0);
   for (int k = 0; k < D; ++k) {
@@ -134,22 +136,27 @@ int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs) {
     int* cf = cu + M;
     int* cn = cf + M;
     int* cp = cn + M;
-    // copies grouped by action, chunks of <= kChunk
+    // copies grouped by action, chunks of exactly kChunk entries: a partial
+    // chunk repeats its last copy (the kernel has no per-copy bounds checks)
     int pos = 0, nc = 0;
     for (int u = 0; u < 9; ++u) {
-      const int start = pos;
+      int in_chunk = 0, last = -1;
       for (int i = 0; i < C; ++i) {
         const uint8_t a = us[(size_t)k * C + i];
         if (a > 8 || zs[(size_t)k * C + i] > 15)
           return set_err(PP2_EINVAL, "step %d copy %d: action/observation out of range", k, i);
-        if (a == u) cp[pos++] = i;
+        if (a != u) continue;
+        if (in_chunk == 0) {
+          cu[nc] = u;
+          cf[nc] = pos;
+          cn[nc] = 0;
+          ++nc;
+        }
+        cp[pos++] = last = i;
+        ++cn[nc - 1];
+        if (++in_chunk == kChunk) in_chunk = 0;
       }
-      for (int f = start; f < pos; f += kChunk) {
-        cu[nc] = u;
-        cf[nc] = f;
-        cn[nc] = std::min(kChunk, pos - f);
-        ++nc;
-      }
+      for (; in_chunk != 0 && in_chunk < kChunk; ++in_chunk) cp[pos++] = last;
     }
     r->nchunks[k] = nc;
   }
