@@ -15,12 +15,18 @@ For N > 1 launch with torch.distributed.run: rank r owns rows
 per step with its neighbours and all-reducing the belief mass over RCCL.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant (and only)
-kernel of a step, k_loop_step -- the fused belief update + Bellman sweep, 417
-algorithmic bytes per cell (belief: T_u 36 + L_z 4 + b 4 + b' 4; sweep: T 324
-+ C 36 + J 4 + J' 4 + A 1) -- timed live with HIP events around the timed
-steps on the stream it runs on; `cpu_baseline` is
-the C restatement of the reference (oracle/) timed on this host on a bounded
-sample of the same workload.
+kernel of a step, timed live with HIP events around the timed steps on the
+stream it runs on:
+  * k_loop_step_coded (default; the model is dictionary-coded, see
+    DESIGN.md "Coded model"): 19 algorithmic HBM bytes per cell (code 2, b 4,
+    b' 4, J 4, J' 4, A 1); its binding resource is LDS (400 B of dictionary
+    reads per cell), reported beside it as `roofline_lds`;
+  * k_loop_step (dense planes, `dense_path` leg, or --dense): 417 bytes per
+    cell (belief: T_u 36 + L_z 4 + b 4 + b' 4; sweep: T 324 + C 36 + J 4 + J'
+    4 + A 1).
+Both give bit-identical beliefs, values and actions (tests/test_gpu_coded.py).
+`cpu_baseline` is the C restatement of the reference (oracle/) timed on this
+host on a bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -40,6 +46,10 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_SWEEP = 369                # per cell: T 324 + C 36 + J 4 + J' 4 + A 1
 BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
 BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
+BYTES_LOOP_CODED = 19            # per cell: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1
+BYTES_SWEEP_CODED = 15           # per cell: code 2 + J 4 + J' 4 + A 1 (+ J halo reuse)
+LDS_BYTES_LOOP_CODED = 400       # per cell: T gather 9*4 + L_z 4 + sweep 9*(9+1)*4
+LDS_PEAK_GBS = 150000.0          # ds_read_b64/b128 chip aggregate (MI355X_MICROARCH.md LDS)
 GAMMA = 0.95
 
 
@@ -64,6 +74,8 @@ def parse():
                     help="batched fp16 rollout copies (0 disables)")
     ap.add_argument("--rollout-depth", type=int, default=5)
     ap.add_argument("--rollout-size", type=int, default=512)
+    ap.add_argument("--dense", action="store_true",
+                    help="time the dense-plane kernels as the main loop")
     ap.add_argument("--profile", action="store_true",
                     help="only run warmup+timed steps (for rocprofv3)")
     return ap.parse_args()
@@ -76,7 +88,7 @@ def dist_env():
     return ws, rank, local
 
 
-def pmc_traffic(kernel_substr: str, cells: int):
+def pmc_traffic(kernel_substr: str, cells: int, exclude: str | None = None):
     """HBM bytes per launch of the dominant kernel from the newest committed
     rocprofv3 PMC summary (profiles/pmc_*.json, written by
     profiles/collect_pmc.py), or None."""
@@ -88,7 +100,8 @@ def pmc_traffic(kernel_substr: str, cells: int):
             continue
         k = d.get("kernels", {})
         for name, v in k.items():
-            if kernel_substr in name and v.get("cells") == cells:
+            if (kernel_substr in name and v.get("cells") == cells
+                    and not (exclude and exclude in name)):
                 return v.get("hbm_bytes_per_launch"), os.path.basename(f)
     return None, None
 
@@ -306,6 +319,9 @@ def main():
         dist.broadcast(uid, src=0)
         ctx.shard_comm_init(bytes(uid.cpu().numpy().tobytes()), ws, rank)
     ctx.model_generate()
+    if args.dense:
+        ctx.set_tuning(ctx.TUNE_CODED_MODEL, 0)
+    dict_entries, coded = ctx.model_dict_info()
     ctx.belief_set(b0[r0 * gw:r1 * gw])
     ctx.mdp_reset()
     ctx.synchronize()
@@ -357,23 +373,44 @@ def main():
     reps = args.kernel_reps
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    ctx.mdp_sweep(reps)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    sweep_ms = e0.elapsed_time(e1) / reps
-    e0.record(stream)
-    for k in range(reps):
-        ctx.belief_update(int(us[k]), int(zs[k]))
-    e1.record(stream)
-    torch.cuda.synchronize()
-    belief_ms = e0.elapsed_time(e1) / reps
+
+    def timed(fn):
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    def loop_reps():
+        ctx.loop_run(us[:reps], zs[:reps])
+
+    sweep_ms = timed(lambda: ctx.mdp_sweep(reps))  # coded when active
+    belief_ms = timed(lambda: [ctx.belief_update(int(us[k]), int(zs[k])) for k in range(reps)])
+    dense = None
+    if coded:
+        ctx.set_tuning(ctx.TUNE_CODED_MODEL, 0)
+        dloop_ms = timed(loop_reps)
+        dsweep_ms = timed(lambda: ctx.mdp_sweep(reps))
+        ctx.set_tuning(ctx.TUNE_CODED_MODEL, 1)
+        dloop_gbs = BYTES_LOOP * cells_per_gpu / (dloop_ms * 1e-3) / 1e9
+        dense = {"kernel": "k_loop_step (dense model planes)",
+                 "loop_step_us": dloop_ms * 1e3,
+                 "cells_per_s": cells_per_gpu / (dloop_ms * 1e-3),
+                 "loop_gbs": dloop_gbs, "loop_frac": dloop_gbs / HBM_PEAK_GBS,
+                 "algorithmic_bytes_per_cell": BYTES_LOOP,
+                 "mdp_sweep_us": dsweep_ms * 1e3,
+                 "mdp_sweep_frac": BYTES_SWEEP * cells_per_gpu / (dsweep_ms * 1e-3) / 1e9
+                 / HBM_PEAK_GBS}
     ctx.close()
 
-    sweep_gbs = BYTES_SWEEP * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
+    bytes_loop = BYTES_LOOP_CODED if coded else BYTES_LOOP
+    bytes_sweep = BYTES_SWEEP_CODED if coded else BYTES_SWEEP
+    loop_kernel = "k_loop_step_coded" if coded else "k_loop_step"
+    sweep_gbs = bytes_sweep * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
     belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
-    loop_gbs = BYTES_LOOP * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("k_loop_step", cells_per_gpu)
+    loop_gbs = bytes_loop * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(loop_kernel, cells_per_gpu,
+                                       exclude=None if coded else "coded")
 
     result = None
     plan = None
@@ -408,9 +445,11 @@ def main():
                 "rows_per_gpu": N,
                 "parallelism": f"row-shard x{ws}, 1-row RCCL halo" if ws > 1 else "single GPU",
                 "cells_per_lane": args.cpt,
+                "model": (f"dictionary-coded ({dict_entries} entries, uint16 code per cell)"
+                          if coded else "dense fp32 planes"),
             },
             "roofline": {
-                "kernel": "k_loop_step (fused belief update + MDP Bellman sweep)",
+                "kernel": f"{loop_kernel} (fused belief update + MDP Bellman sweep)",
                 "bound": "hbm",
                 "achieved": loop_gbs,
                 "peak": HBM_PEAK_GBS,
@@ -418,10 +457,18 @@ def main():
                 "frac": loop_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": BYTES_LOOP * cells_per_gpu,
+                "algorithmic_bytes_per_launch": bytes_loop * cells_per_gpu,
                 "avg_launch_us": loop_ms_events * 1e3,
             },
+            "roofline_lds": ({
+                "achieved": LDS_BYTES_LOOP_CODED * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9,
+                "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                "frac": LDS_BYTES_LOOP_CODED * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
+                / LDS_PEAK_GBS,
+                "bytes_per_cell": LDS_BYTES_LOOP_CODED} if coded else None),
+            "dense_path": dense,
             "kernels": {
+                "mdp_sweep_kernel": "k_mdp_sweep_coded" if coded else "k_mdp_sweep",
                 "mdp_sweep_us": sweep_ms * 1e3,
                 "mdp_sweep_gbs": sweep_gbs,
                 "mdp_sweep_frac": sweep_gbs / HBM_PEAK_GBS,

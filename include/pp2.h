@@ -86,9 +86,13 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *  PP2_TUNE_CELLS_PER_LANE  1, 2 or 4
  *  PP2_TUNE_NT_STREAMS      1 (default) = non-temporal loads of the
  *                           once-read T/C streams (loop and sweep kernels,
- *                           CPT 4): -8 % time per loop step measured */
+ *                           CPT 4): -8 % time per loop step measured
+ *  PP2_TUNE_CODED_MODEL     1 (default) = loop step and MDP sweep read the
+ *                           dictionary-coded model (pp2_model_dict_info)
+ *                           when one exists; 0 = always the dense planes */
 #define PP2_TUNE_CELLS_PER_LANE 1
 #define PP2_TUNE_NT_STREAMS 2
+#define PP2_TUNE_CODED_MODEL 3
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
 /* ---------------------------------------------------------------- model
@@ -109,6 +113,14 @@ int pp2_model_upload(pp2_ctx* ctx, const float* T, const float* L,
  * model_data_meas_prob, model_data_stage_reward in `dir` ("%15.8f"). */
 int pp2_model_save(pp2_ctx* ctx, const char* dir);
 int pp2_model_load(pp2_ctx* ctx, const char* dir);
+/* Dictionary-coded model (no reference counterpart; a lossless re-encoding of
+ * the arrays above).  Every call that sets the model (generate / upload /
+ * load) rebuilds it: one uint16 code per cell plus one dictionary row per
+ * distinct per-cell (T, C, L) tuple, checked bitwise against every cell.
+ * entries = dictionary rows (0: more than the LDS budget allows, dense path
+ * only); active = 1 when pp2_loop_step / pp2_mdp_sweep use it.  Results are
+ * bit-identical either way. */
+int pp2_model_dict_info(pp2_ctx* ctx, int* entries, int* active);
 
 /* ---------------------------------------------------------------- belief
  * The belief lives on the device with deferred normalisation: each update

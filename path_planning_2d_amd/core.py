@@ -96,6 +96,7 @@ class GridContext:
 
     TUNE_CELLS_PER_LANE = 1
     TUNE_NT_STREAMS = 2
+    TUNE_CODED_MODEL = 3
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))
@@ -103,6 +104,12 @@ class GridContext:
     # ------------------------------------------------------------ model
     def model_generate(self):
         call("pp2_model_generate", self._h)
+
+    def model_dict_info(self):
+        """(entries, active) of the dictionary-coded model (pp2_model_dict_info)."""
+        e, a = C.c_int(0), C.c_int(0)
+        call("pp2_model_dict_info", self._h, C.byref(e), C.byref(a))
+        return e.value, bool(a.value)
 
     def model_download(self):
         n = self.cells

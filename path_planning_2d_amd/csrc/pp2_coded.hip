@@ -1,0 +1,434 @@
+// pp2_coded.hip -- the dictionary-coded model path (gfx950).
+//
+// The generated model is a function of each cell's 3x3 occupancy (SURVEY.md
+// §8 a1: at most 257 distinct transition patterns), so the dense model --
+// T 324 B + C 36 B + R 36 B + L 64 B per cell, the bulk of the north-star
+// loop's HBM traffic -- is mostly repetition.  The coded path stores
+//   * code  : uint16 per cell (rows -1..rows, same padded geometry), and
+//   * dict  : one row per distinct per-cell (T, C, L) tuple (kDictRow
+//             floats): [u][T_u0..T_u8, C_u] (90) | L[16] | pad.
+// R (the POMDP stage reward) is left out: it also varies with the occupancy
+// around an occupied cell (another 256 patterns), and only the rollout reads
+// it, once per cell per slab for a whole chunk of copies, from its plane.
+// built from the dense planes by exact tuple equality (hash on the GPU,
+// first-appearance numbering on the host, then a bitwise verification pass
+// over every cell; any mismatch leaves the context on the dense path).  A
+// kernel stages the dictionary's T/C rows in LDS once per workgroup and reads
+// only codes, beliefs and values from HBM.  Per-cell arithmetic is exactly
+// the dense kernels' (same operands, same fmaf order), and the belief partial
+// sums use the dense kernels' cell->block mapping and reduction tree, so the
+// coded and dense paths give bit-identical beliefs, masses, values and actions.
+#include "pp2_device.h"
+
+namespace pp2 {
+
+namespace {
+
+constexpr int kQuarter = kBlock;  // a dense-kernel block: 256 threads, 1024 cells
+
+// ---------------------------------------------------------------- build
+__device__ __forceinline__ float tuple_value(const PlaneSet& T, const PlaneSet& C,
+                                             const PlaneSet& R, const PlaneSet& L, int y,
+                                             int x, int k) {
+  if (k < 90) {
+    const int u = k / 10, i = k % 10;
+    return i < 9 ? T.p[(long long)y * T.rs + (long long)(9 * u + i) * T.ps + x]
+                 : C.p[(long long)y * C.rs + (long long)u * C.ps + x];
+  }
+  if (k < kDictTuple) return L.p[(long long)y * L.rs + (long long)(k - 90) * L.ps + x];
+  return 0.0f;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t h) {
+  h ^= h >> 31;
+  h *= 0x7fb5d329728ea185ull;
+  h ^= h >> 27;
+  h *= 0x81dadef4bc2dd44dull;
+  h ^= h >> 33;
+  return h;
+}
+
+// hash of the kDictTuple-value tuple of every cell in rows [-1, rows]
+__global__ __launch_bounds__(kBlock) void k_dict_hash(Geom g, PlaneSet T, PlaneSet C,
+                                                      PlaneSet R, PlaneSet L,
+                                                      uint64_t* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long n = (long long)(g.rows + 2) * g.wp;
+  if (i >= n) return;
+  const int y = (int)(i / g.wp) - 1, x = (int)(i % g.wp);
+  uint64_t h = 0x9e3779b97f4a7c15ull;
+  for (int k = 0; k < kDictTuple; ++k) {
+    const uint32_t w = __float_as_uint(tuple_value(T, C, R, L, y, x, k));
+    h = mix64(h ^ (w + 0x632be59bd9b4e019ull * (uint64_t)(k + 1)));
+  }
+  out[i] = h;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dict_gather(Geom g, PlaneSet T, PlaneSet C,
+                                                        PlaneSet R, PlaneSet L,
+                                                        const int* __restrict__ reps, int E,
+                                                        float* __restrict__ dict) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= E * kDictRow) return;
+  const int e = i / kDictRow, k = i % kDictRow;
+  const int cell = reps[e];
+  const int y = cell / g.wp - 1, x = cell % g.wp;
+  dict[i] = tuple_value(T, C, R, L, y, x, k);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dict_verify(Geom g, PlaneSet T, PlaneSet C,
+                                                        PlaneSet R, PlaneSet L,
+                                                        const uint16_t* __restrict__ code,
+                                                        const float* __restrict__ dict,
+                                                        int* __restrict__ bad) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const long long n = (long long)(g.rows + 2) * g.wp;
+  if (i >= n) return;
+  const int y = (int)(i / g.wp) - 1, x = (int)(i % g.wp);
+  const float* d = dict + (long long)code[i] * kDictRow;
+  int diff = 0;
+  for (int k = 0; k < kDictTuple; ++k)
+    diff |= __float_as_uint(tuple_value(T, C, R, L, y, x, k)) != __float_as_uint(d[k]);
+  if (diff) atomicOr(bad, 1);
+}
+
+// ---------------------------------------------------------------- kernels
+// Two LDS row layouts per dictionary entry:
+//  * full   (kDictTC = 90 floats): [a][T_a0..T_a8, C_a];
+//  * sparse (kSpRow = 54 floats):  [a][T_a at kSup[a][0..3], C_a, 0] -- only
+//    the base-kernel support of each action (at most 4 cells; the host checks
+//    every other T entry of every row is +0.0 before choosing it).
+// Sparse Bellman rows skip the T == 0 terms: fmaf(gamma*0, J, cost) == cost
+// for the finite, non-negative J and cost of the MDP (J starts at 0, C >= 0),
+// so values and actions stay bit-identical to the dense kernel.
+template <bool SPARSE>
+struct Layout {
+  static constexpr int row = SPARSE ? kSpRow : kDictTC;
+  static constexpr int blk = SPARSE ? 6 : 10;  // floats per action block
+};
+
+// Global -> LDS copy of n floats (src and dst 16-B aligned, src readable up
+// to n rounded up to 4): 16-B loads, eight in flight per thread before the
+// LDS stores, so staging costs a few L2 round trips rather than one per float.
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, int n, float* dst) {
+  const int n4 = (n + 3) >> 2;
+  const f4a* s4 = reinterpret_cast<const f4a*>(src);
+  f4a* d4 = reinterpret_cast<f4a*>(dst);
+  for (int base = 0; base < n4; base += 8 * (int)blockDim.x) {
+    f4a v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + j * (int)blockDim.x + (int)threadIdx.x;
+      if (i < n4) v[j] = s4[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + j * (int)blockDim.x + (int)threadIdx.x;
+      if (i < n4) d4[i] = v[j];
+    }
+  }
+}
+
+// Bellman backup of 4 cells from their codes (k_mdp_sweep's arithmetic).
+template <bool SPARSE>
+__device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&cc)[4],
+                                             const float (&jn)[9][4], float gamma,
+                                             float (&best)[4], uint32_t (&arg)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
+  if constexpr (SPARSE) {
+    // fully unrolled (support positions index jn at compile time); the
+    // scheduling barrier keeps one action's LDS reads live at a time
+#pragma unroll
+    for (int a = 0; a < 9; ++a) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f2a* row = reinterpret_cast<const f2a*>(sTC + cc[k] * kSpRow + a * 6);
+        const f2a t01 = row[0];
+        const f2a t23 = kSupN[a] > 2 ? row[1] : f2a{0.0f, 0.0f};
+        const f2a cz = row[2];
+        const float tv[4] = {t01[0], t01[1], t23[0], t23[1]};
+        float cost = cz[0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < kSupN[a]) cost = __builtin_fmaf(gamma * tv[j], jn[kSup[a][j]][k], cost);
+        if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    // one action at a time: 4 cells x 10 dictionary floats live (a fully
+    // unrolled action loop hoists all 360 LDS reads and spills)
+#pragma unroll 1
+    for (int a = 0; a < 9; ++a) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f2a* row = reinterpret_cast<const f2a*>(sTC + cc[k] * kDictTC + a * 10);
+        const f2a t01 = row[0], t23 = row[1], t45 = row[2], t67 = row[3], t8c = row[4];
+        const float tv[9] = {t01[0], t01[1], t23[0], t23[1], t45[0], t45[1], t67[0], t67[1], t8c[0]};
+        float cost = t8c[1];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) cost = __builtin_fmaf(gamma * tv[i], jn[i][k], cost);
+        if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void load_jn(const float* __restrict__ J_in, int wp, int y, int x0,
+                                        bool le, bool re, float (&jn)[9][4]) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int oy = i / 3 - 1, ox = i % 3 - 1;
+    const float* jp = J_in + (long long)(y + oy) * wp + x0 + ox;
+    if (ox == 0) ldv<4, true>(jp, jn[i]);
+    else ldv<4, false>(jp, jn[i]);
+    if (ox < 0 && le) jn[i][0] = 0.0f;
+    if (ox > 0 && re) jn[i][3] = 0.0f;
+  }
+}
+
+__device__ __forceinline__ void store_ja(float* __restrict__ J_out, uint8_t* __restrict__ A,
+                                         long long off, const float (&best)[4],
+                                         const uint32_t (&arg)[4]) {
+  stv<4>(J_out + off, best);
+  *reinterpret_cast<uint32_t*>(A + off) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+}
+
+// Fused north-star step on the coded model (k_loop_step's semantics).  A
+// workgroup is QPB dense-kernel blocks ("quarters" of 256 threads): quarter q
+// of tile t is dense block d = QPB*t + q with the same 1024 cells, the same
+// lane->cell map and the same block_sum tree, and writes out_partials[d] -- so
+// the mass of the output equals the dense kernel's bit for bit.
+//   rows: dictionary rows in the LDS layout (E x Layout::row floats)
+//   lz:   L_z column of the dictionary (E floats)
+template <bool SPARSE, int QPB, int MINB>
+__global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
+    Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
+    const float* __restrict__ lz, int E, const float* __restrict__ b_in,
+    float* __restrict__ b_out, int u, const float* __restrict__ in_partials, int in_n,
+    const float* __restrict__ in_sum, float* __restrict__ in_sum_out,
+    float* __restrict__ out_partials, int dense_blocks, const float* __restrict__ J_in,
+    float* __restrict__ J_out, uint8_t* __restrict__ A) {
+  using LY = Layout<SPARSE>;
+  extern __shared__ float lds[];
+  float* sTC = lds;
+  float* sL = lds + ((E * LY::row + 3) & ~3);
+  float* red = sL + ((E + 3) & ~3);  // one sum per wave
+  stage_rows(rows, E * LY::row, sTC);
+  stage_rows(lz, E, sL);
+  float S = 1.0f;
+  if (in_partials) S = wave_reduce_partials(in_partials, in_n);
+  else if (in_sum) S = *in_sum;
+  if (in_sum_out && blockIdx.x == 0 && threadIdx.x == 0) *in_sum_out = S;
+  const float inv = 1.0f / S;
+  // belief gather: LDS slot of T[.][u][i] inside the action-u block, or -1
+  // when i is outside u's support on the sparse layout (T == 0 there)
+  int slot[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    if constexpr (SPARSE) {
+      slot[i] = -1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < kSupN[u] && kSup[u][j] == i) slot[i] = j;
+    } else {
+      slot[i] = i;
+    }
+  }
+  __syncthreads();
+  const int tpr = g.wp / 4;
+  const int q = threadIdx.x / kQuarter, tq = threadIdx.x % kQuarter;
+  const int ntiles = (dense_blocks + QPB - 1) / QPB;
+  const int ublk = u * LY::blk;
+  for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
+    const int d = tile * QPB + q;
+    const long long t = (long long)d * kQuarter + tq;
+    const int y = (int)(t / tpr);
+    const int x0 = (int)(t % tpr) * 4;
+    float local = 0.0f;
+    if (y < g.rows) {
+      const bool le = x0 == 0, re = x0 + 4 == g.wp;
+      CodeWin w;
+      load_codes(code, g.wp, y, x0, w);
+      // ---- belief update: p = L_z * sum_s T[x+off_s][u][8-s] b(x+off_s)
+      float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {
+        const int oy = s / 3 - 1, ox = s % 3 - 1;
+        const float* bp = b_in + (long long)(y + oy) * g.wp + x0 + ox;
+        float bv[4];
+        if (ox == 0) ldv<4, true>(bp, bv);
+        else ldv<4, false>(bp, bv);
+        const int sl = slot[8 - s];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float tv = sl >= 0 ? sTC[w.c[oy + 1][k + 1 + ox] * LY::row + ublk + sl] : 0.0f;
+          float b = bv[k];
+          if (ox < 0 && k == 0 && le) { tv = 0.0f; b = 0.0f; }
+          if (ox > 0 && k == 3 && re) { tv = 0.0f; b = 0.0f; }
+          p[k] = __builtin_fmaf(tv, b, p[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        p[k] = p[k] * sL[w.c[1][k + 1]];
+        p[k] = p[k] * inv;
+        local += p[k];
+      }
+      const long long off = (long long)y * g.wp + x0;
+      stv<4>(b_out + off, p);
+      // ---- Bellman sweep
+      float jn[9][4];
+      load_jn(J_in, g.wp, y, x0, le, re, jn);
+      const uint32_t cc[4] = {w.c[1][1], w.c[1][2], w.c[1][3], w.c[1][4]};
+      float best[4];
+      uint32_t arg[4];
+      coded_sweep4<SPARSE>(sTC, cc, jn, gamma, best, arg);
+      store_ja(J_out, A, off, best, arg);
+    }
+    // block_sum per quarter (same tree as the dense kernel's 256-thread block)
+    const float ws = wave_sum(local);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ws;
+    __syncthreads();
+    if (tq == 0 && d < dense_blocks)
+      out_partials[d] = ((red[4 * q] + red[4 * q + 1]) + red[4 * q + 2]) + red[4 * q + 3];
+    __syncthreads();
+  }
+}
+
+template <bool SPARSE, int QPB, int MINB>
+__global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
+    Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
+    int E, const float* __restrict__ J_in, float* __restrict__ J_out,
+    uint8_t* __restrict__ A) {
+  using LY = Layout<SPARSE>;
+  constexpr int NT = QPB * kQuarter;
+  extern __shared__ float lds[];
+  stage_rows(rows, E * LY::row, lds);
+  __syncthreads();
+  const int tpr = g.wp / 4;
+  const long long nthreads = (long long)g.rows * tpr;
+  const int ntiles = (int)((nthreads + NT - 1) / NT);
+  for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
+    const long long t = (long long)tile * NT + threadIdx.x;
+    const int y = (int)(t / tpr);
+    const int x0 = (int)(t % tpr) * 4;
+    if (y >= g.rows) continue;
+    const bool le = x0 == 0, re = x0 + 4 == g.wp;
+    const long long off = (long long)y * g.wp + x0;
+    const uint2 m = *reinterpret_cast<const uint2*>(code + off);
+    const uint32_t cc[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
+    float jn[9][4];
+    load_jn(J_in, g.wp, y, x0, le, re, jn);
+    float best[4];
+    uint32_t arg[4];
+    coded_sweep4<SPARSE>(lds, cc, jn, gamma, best, arg);
+    store_ja(J_out, A, off, best, arg);
+  }
+}
+
+int g_num_cus = 0;
+
+int coded_grid(int ntiles, int per_cu) {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      g_num_cus = n;
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  const int cap = g_num_cus * per_cu;
+  return ntiles < cap ? ntiles : cap;
+}
+
+// Opt a kernel into more than the default dynamic LDS once per process.  A
+// refusal is not fatal here: the launch itself reports an oversized request.
+void allow_lds(const void* fn, bool& done) {
+  if (done) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDictLdsMaxBytes);
+  (void)hipGetLastError();
+  done = true;
+}
+
+}  // namespace
+
+size_t coded_loop_lds_bytes(int E, bool sparse) {
+  const size_t rows = ((size_t)E * (sparse ? kSpRow : kDictTC) + 3) & ~(size_t)3;
+  return (rows + (size_t)((E + 3) & ~3) + 16) * sizeof(float);
+}
+
+hipError_t launch_dict_hash(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
+                            PlaneSet L, uint64_t* out) {
+  const long long n = (long long)(g.rows + 2) * g.wp;
+  hipLaunchKernelGGL(k_dict_hash, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     st, g, T, C, R, L, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_dict_gather(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
+                              PlaneSet L, const int* reps, int E, float* dict) {
+  const int n = E * kDictRow;
+  hipLaunchKernelGGL(k_dict_gather, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, g, T,
+                     C, R, L, reps, E, dict);
+  return hipGetLastError();
+}
+
+hipError_t launch_dict_verify(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
+                              PlaneSet L, const uint16_t* code_all, const float* dict, int* bad) {
+  const long long n = (long long)(g.rows + 2) * g.wp;
+  hipLaunchKernelGGL(k_dict_verify, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     st, g, T, C, R, L, code_all, dict, bad);
+  return hipGetLastError();
+}
+
+// Launch shapes (workgroups of QPB x 256 threads, MINB per CU; one lane = 4
+// cells): the sparse loop kernel 2 x 512 threads (<= 128 VGPRs, 4 waves per
+// SIMD, 2 x ~60 KB LDS), the sparse sweep 2 x 1024 (<= 64 VGPRs, 8 waves per
+// SIMD); full rows (up to ~160 KB LDS) one 1024-thread workgroup per CU.
+hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
+                                  const uint16_t* code, const float* rows, const float* lz,
+                                  int E, bool sparse, const float* b_in, float* b_out, int u,
+                                  const float* in_partials, int in_n, const float* in_sum,
+                                  float* in_sum_out, float* out_partials, const float* J_in,
+                                  float* J_out, uint8_t* A) {
+  const size_t lds = coded_loop_lds_bytes(E, sparse);
+  const int dense_blocks = cells_grid(g, 4);
+#define PP2_LOOPC(SP, Q, MB)                                                                   \
+  do {                                                                                         \
+    if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                              \
+    static bool attr = false;                                                                  \
+    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB>), attr);             \
+    const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                               \
+    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB>), dim3(grid), dim3(Q * kQuarter), lds, st, \
+                       g, gamma, code, rows, lz, E, b_in, b_out, u, in_partials, in_n, in_sum, \
+                       in_sum_out, out_partials, dense_blocks, J_in, J_out, A);                \
+  } while (0)
+  if (sparse) PP2_LOOPC(true, 2, 2);
+  else PP2_LOOPC(false, 4, 1);
+#undef PP2_LOOPC
+  return hipGetLastError();
+}
+
+hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
+                                  const uint16_t* code, const float* rows, int E, bool sparse,
+                                  const float* J_in, float* J_out, uint8_t* A) {
+  const size_t lds = (((size_t)E * (sparse ? kSpRow : kDictTC) + 3) & ~(size_t)3) * sizeof(float);
+  const long long nthreads = (long long)g.rows * (g.wp / 4);
+#define PP2_SWEEPC(SP, Q, MB)                                                                  \
+  do {                                                                                         \
+    if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                              \
+    static bool attr = false;                                                                  \
+    allow_lds(reinterpret_cast<const void*>(&k_mdp_sweep_coded<SP, Q, MB>), attr);             \
+    const int nt = Q * kQuarter;                                                               \
+    const int grid = coded_grid((int)((nthreads + nt - 1) / nt), MB);                          \
+    hipLaunchKernelGGL((k_mdp_sweep_coded<SP, Q, MB>), dim3(grid), dim3(nt), lds, st, g, gamma, \
+                       code, rows, E, J_in, J_out, A);                                         \
+  } while (0)
+  if (sparse) PP2_SWEEPC(true, 4, 2);
+  else PP2_SWEEPC(false, 4, 1);
+#undef PP2_SWEEPC
+  return hipGetLastError();
+}
+
+}  // namespace pp2

@@ -80,6 +80,15 @@ struct pp2_ctx {
   int pcount[2] = {0, 0};               // number of partials in pbuf[i]
   float* rpartials = nullptr;  // convergence-check partials
   int partials_cap = 0;
+  // dictionary-coded model (pp2_coded.hip), rebuilt whenever the model changes
+  uint16_t* code_alloc = nullptr;  // code plane allocation (guards + rows -1..rows)
+  uint16_t* d_code = nullptr;      // code plane at (row 0, x 0)
+  float* d_dict = nullptr;         // kDictMax * kDictRow floats
+  float* d_rows = nullptr;         // LDS-layout rows (sparse: kSpRow, else kDictTC floats)
+  float* d_dl = nullptr;           // L transposed: [z][entry]
+  int dict_n = 0;                  // entries; 0 = no dictionary (dense path only)
+  bool dict_sparse = false;        // every T row is zero off the base-kernel support
+  bool use_coded = true;           // PP2_TUNE_CODED_MODEL
   void* staging = nullptr;     // dense host-layout staging buffer
   size_t staging_bytes = 0;
 
@@ -113,6 +122,8 @@ int belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep);
 int loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass);
 int ensure_mass(pp2_ctx* c);
 int mdp_sweep_once(pp2_ctx* c);
+int build_model_dict(pp2_ctx* c);
+bool coded_active(const pp2_ctx* c);
 int fib_sweep_once(pp2_ctx* c);
 int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* out);
 

@@ -1,0 +1,140 @@
+// pp2_device.h -- device-side helpers shared by the gfx950 kernel files
+// (pp2_kernels.hip, pp2_coded.hip): vector loads/stores over the SoA planes
+// and the deterministic (fixed-association) wave/block reductions.
+#pragma once
+#include <float.h>
+#include <stdint.h>
+
+#include "pp2_internal.h"
+
+namespace pp2 {
+
+typedef float f4a __attribute__((ext_vector_type(4)));
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2a __attribute__((ext_vector_type(2)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+
+constexpr int kBlock = 256;
+
+template <int N, bool ALIGNED>
+__device__ __forceinline__ void ldv(const float* __restrict__ p, float (&v)[N]) {
+  if constexpr (N == 4) {
+    if constexpr (ALIGNED) {
+      const f4a t = *reinterpret_cast<const f4a*>(p);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+      const f4u t = *reinterpret_cast<const f4u*>(p);
+      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    }
+  } else if constexpr (N == 2) {
+    if constexpr (ALIGNED) {
+      const f2a t = *reinterpret_cast<const f2a*>(p);
+      v[0] = t[0]; v[1] = t[1];
+    } else {
+      const f2u t = *reinterpret_cast<const f2u*>(p);
+      v[0] = t[0]; v[1] = t[1];
+    }
+  } else {
+    v[0] = *p;
+  }
+}
+
+// Non-temporal variant for streams read exactly once per launch (T, C).
+template <int N, bool NT>
+__device__ __forceinline__ void ldv_stream(const float* __restrict__ p, float (&v)[N]) {
+  if constexpr (NT && N == 4) {
+    const f4a t = __builtin_nontemporal_load(reinterpret_cast<const f4a*>(p));
+    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+  } else {
+    ldv<N, true>(p, v);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[N]) {
+  if constexpr (N == 4) {
+    f4a t = {v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f4a*>(p) = t;
+  } else if constexpr (N == 2) {
+    f2a t = {v[0], v[1]};
+    *reinterpret_cast<f2a*>(p) = t;
+  } else {
+    *p = v[0];
+  }
+}
+
+// ---- deterministic reductions (fixed association order) --------------------
+// xor-butterfly: partners always add the same two operands, so every lane of
+// the wave ends with the bit-identical total.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Sum over a 256-thread block; result valid in thread 0.
+__device__ __forceinline__ float block_sum(float v, float* lds4) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) lds4[w] = v;
+  __syncthreads();
+  float r = 0.0f;
+  if (threadIdx.x == 0) r = ((lds4[0] + lds4[1]) + lds4[2]) + lds4[3];
+  return r;
+}
+__device__ __forceinline__ float block_max(float v, float* lds4) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) lds4[w] = v;
+  __syncthreads();
+  float r = 0.0f;
+  if (threadIdx.x == 0) r = fmaxf(fmaxf(lds4[0], lds4[1]), fmaxf(lds4[2], lds4[3]));
+  return r;
+}
+
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h4u __attribute__((ext_vector_type(4), aligned(2)));
+
+// One wave, lane-strided then xor-butterfly: the same association as
+// wave_reduce_partials in k_loop_step, so a mass finalised here and one
+// reduced inside the next fused step are bit-identical.
+__device__ __forceinline__ float wave_reduce_partials(const float* __restrict__ p, int n) {
+  const int lane = threadIdx.x & 63;
+  float s = 0.0f;
+  for (int i = lane; i < n; i += 64) s += p[i];
+  return wave_sum(s);
+}
+
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  const int q = n / 8, r = n % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// codes of rows y-1, y, y+1 at x0-1 .. x0+4 (dword-aligned loads only)
+struct CodeWin {
+  uint32_t c[3][6];
+};
+
+__device__ __forceinline__ void load_codes(const uint16_t* __restrict__ code, int wp, int y,
+                                           int x0, CodeWin& w) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const uint16_t* cp = code + (long long)(y + r - 1) * wp + x0;
+    const uint2 m = *reinterpret_cast<const uint2*>(cp);
+    const uint32_t lw = *reinterpret_cast<const uint32_t*>(cp - 2);
+    const uint32_t rw = *reinterpret_cast<const uint32_t*>(cp + 4);
+    w.c[r][0] = lw >> 16;
+    w.c[r][1] = m.x & 0xffffu;
+    w.c[r][2] = m.x >> 16;
+    w.c[r][3] = m.y & 0xffffu;
+    w.c[r][4] = m.y >> 16;
+    w.c[r][5] = rw & 0xffffu;
+  }
+}
+
+}  // namespace pp2

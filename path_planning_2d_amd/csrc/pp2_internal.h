@@ -90,8 +90,10 @@ hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* ma
 int rollout_waves(const Geom& g);
 int rollout_chunk();      // copies per chunk (block) of the selected variant
 int rollout_min_chunk();  // smallest chunk of any variant (sizes chunk tables)
+// code/dict/E: the coded model (E > 0; pp2_coded.hip) or E = 0 for the planes
 hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
-                               PlaneSet R, const void* bin, void* bout, long long cstride,
+                               PlaneSet R, const uint16_t* code, const float* dict, int E,
+                               const void* bin, void* bout, long long cstride,
                                int nchunks, const int* chunk_u, const int* chunk_first,
                                const int* chunk_n, const int* copies, const uint8_t* zs,
                                const float* in_stats, float* partials, float* stats_out,
@@ -100,5 +102,41 @@ hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const 
                                long long cstride, int ncopies, float* partials, float* out);
 hipError_t launch_rollout_broadcast(hipStream_t st, const void* src, void* dst,
                                     long long cstride, int ncopies);
+
+// Dictionary-coded model (pp2_coded.hip).  code: uint16 per cell over rows
+// [-1, rows] (same geometry as a plane); dict: kDictRow floats per entry,
+// [u][T_u0..T_u8, C_u] (kDictTC) | L[16] | pad.
+constexpr int kDictTC = 90;
+constexpr int kDictL = 90;       // offset of L[16]
+constexpr int kDictTuple = 106;  // floats compared per cell
+constexpr int kDictRow = 108;
+constexpr size_t kDictLdsMaxBytes = 160 * 1024;
+constexpr int kDictMax = 448;  // coded_loop_lds_bytes(kDictMax, false) <= kDictLdsMaxBytes
+// Sparse LDS rows: per action a, T at the base kernel's support kSup[a][0 ..
+// kSupN[a]) (base_kernel in pp2_kernels.hip; occupied neighbours and traps
+// only move mass to the centre, which is in every support), then C_a, then 0.
+constexpr int kSpRow = 54;  // 9 actions x 6 floats
+constexpr int kSupN[9] = {4, 4, 4, 4, 1, 4, 4, 4, 4};
+constexpr int kSup[9][4] = {{0, 1, 3, 4}, {0, 1, 2, 4}, {1, 2, 4, 5}, {0, 3, 4, 6}, {4, 0, 0, 0},
+                            {2, 4, 5, 8}, {3, 4, 6, 7}, {4, 6, 7, 8}, {4, 5, 7, 8}};
+size_t coded_loop_lds_bytes(int entries, bool sparse);
+hipError_t launch_dict_hash(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
+                            PlaneSet L, uint64_t* out);
+hipError_t launch_dict_gather(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
+                              PlaneSet L, const int* reps, int entries, float* dict);
+hipError_t launch_dict_verify(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
+                              PlaneSet L, const uint16_t* code_all, const float* dict, int* bad);
+// code = code plane at (row 0, x 0); rows = LDS-layout dictionary rows (E x
+// kSpRow if sparse else E x kDictTC); lz = the L_z column (E floats).  Same
+// contract as launch_loop_step (cpt 4).
+hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
+                                  const uint16_t* code, const float* rows, const float* lz,
+                                  int entries, bool sparse, const float* b_in, float* b_out,
+                                  int u, const float* in_partials, int in_n,
+                                  const float* in_sum, float* in_sum_out, float* out_partials,
+                                  const float* J_in, float* J_out, uint8_t* A);
+hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
+                                  const uint16_t* code, const float* rows, int entries,
+                                  bool sparse, const float* J_in, float* J_out, uint8_t* A);
 
 }  // namespace pp2

@@ -16,97 +16,9 @@
 #include <float.h>
 #include <stdlib.h>
 
-#include "pp2_internal.h"
+#include "pp2_device.h"
 
 namespace pp2 {
-
-typedef float f4a __attribute__((ext_vector_type(4)));
-typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
-typedef float f2a __attribute__((ext_vector_type(2)));
-typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
-
-constexpr int kBlock = 256;
-
-template <int N, bool ALIGNED>
-__device__ __forceinline__ void ldv(const float* __restrict__ p, float (&v)[N]) {
-  if constexpr (N == 4) {
-    if constexpr (ALIGNED) {
-      const f4a t = *reinterpret_cast<const f4a*>(p);
-      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
-    } else {
-      const f4u t = *reinterpret_cast<const f4u*>(p);
-      v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
-    }
-  } else if constexpr (N == 2) {
-    if constexpr (ALIGNED) {
-      const f2a t = *reinterpret_cast<const f2a*>(p);
-      v[0] = t[0]; v[1] = t[1];
-    } else {
-      const f2u t = *reinterpret_cast<const f2u*>(p);
-      v[0] = t[0]; v[1] = t[1];
-    }
-  } else {
-    v[0] = *p;
-  }
-}
-
-// Non-temporal variant for streams read exactly once per launch (T, C).
-template <int N, bool NT>
-__device__ __forceinline__ void ldv_stream(const float* __restrict__ p, float (&v)[N]) {
-  if constexpr (NT && N == 4) {
-    const f4a t = __builtin_nontemporal_load(reinterpret_cast<const f4a*>(p));
-    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
-  } else {
-    ldv<N, true>(p, v);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[N]) {
-  if constexpr (N == 4) {
-    f4a t = {v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<f4a*>(p) = t;
-  } else if constexpr (N == 2) {
-    f2a t = {v[0], v[1]};
-    *reinterpret_cast<f2a*>(p) = t;
-  } else {
-    *p = v[0];
-  }
-}
-
-// ---- deterministic reductions (fixed association order) --------------------
-// xor-butterfly: partners always add the same two operands, so every lane of
-// the wave ends with the bit-identical total.
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
-}
-
-// Sum over a 256-thread block; result valid in thread 0.
-__device__ __forceinline__ float block_sum(float v, float* lds4) {
-  v = wave_sum(v);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) lds4[w] = v;
-  __syncthreads();
-  float r = 0.0f;
-  if (threadIdx.x == 0) r = ((lds4[0] + lds4[1]) + lds4[2]) + lds4[3];
-  return r;
-}
-__device__ __forceinline__ float block_max(float v, float* lds4) {
-  v = wave_max(v);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) lds4[w] = v;
-  __syncthreads();
-  float r = 0.0f;
-  if (threadIdx.x == 0) r = fmaxf(fmaxf(lds4[0], lds4[1]), fmaxf(lds4[2], lds4[3]));
-  return r;
-}
 
 int cells_grid(const Geom& g, int cpt) {
   const long long threads = (long long)g.rows * (g.wp / cpt);
@@ -290,16 +202,6 @@ hipError_t launch_belief_update(hipStream_t st, const Geom& g, int cpt,
   return hipGetLastError();
 }
 
-// One wave, lane-strided then xor-butterfly: the same association as
-// wave_reduce_partials in k_loop_step, so a mass finalised here and one
-// reduced inside the next fused step are bit-identical.
-__device__ __forceinline__ float wave_reduce_partials(const float* __restrict__ p, int n) {
-  const int lane = threadIdx.x & 63;
-  float s = 0.0f;
-  for (int i = lane; i < n; i += 64) s += p[i];
-  return wave_sum(s);
-}
-
 __global__ __launch_bounds__(64) void k_sum_finalize(const float* __restrict__ partials,
                                                      int n, float* __restrict__ out) {
   const float s = wave_reduce_partials(partials, n);
@@ -414,10 +316,6 @@ hipError_t launch_mdp_sweep(hipStream_t st, const Geom& g, int cpt,
 //    is known without a separate finalize launch;
 //  * arithmetic per cell is exactly k_belief_update's and k_mdp_sweep's.
 // ============================================================================
-__device__ __forceinline__ int xcd_remap(int b, int n) {
-  const int q = n / 8, r = n % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
 
 template <int CPT, bool NT>
 __global__ __launch_bounds__(kBlock) void k_loop_step(
@@ -905,8 +803,6 @@ hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* ma
 //  * per (copy, wave) partial sums of {stored sum, stored max, reward dot} are
 //    reduced per copy by k_rollout_reduce.
 // ============================================================================
-typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-typedef _Float16 h4u __attribute__((ext_vector_type(4), aligned(2)));
 
 template <bool ALIGNED>
 __device__ __forceinline__ void ldh4(const _Float16* __restrict__ p, float (&v)[4]) {
@@ -930,7 +826,9 @@ __device__ __forceinline__ _Float16 h2_hi(uint32_t w) {
 }
 
 // b points at (row y, x0) of one copy; every address is dword aligned (x0 is
-// a multiple of 4) and lies inside the copy's halo rows or the guards.
+// a multiple of 4) and lies inside the copy's halo rows or the guards.  The
+// L_z load is skipped on the coded path (L comes from the LDS dictionary).
+template <bool WITH_L>
 __device__ __forceinline__ void roll_load(RollRaw& q, const _Float16* __restrict__ b, int wp,
                                           const float* __restrict__ lp) {
 #pragma unroll
@@ -940,8 +838,10 @@ __device__ __forceinline__ void roll_load(RollRaw& q, const _Float16* __restrict
     q.lw[row] = *reinterpret_cast<const uint32_t*>(bp - 2);
     q.rw[row] = *reinterpret_cast<const uint32_t*>(bp + 4);
   }
-  const float4 l4 = *reinterpret_cast<const float4*>(lp);
-  q.l[0] = l4.x; q.l[1] = l4.y; q.l[2] = l4.z; q.l[3] = l4.w;
+  if constexpr (WITH_L) {
+    const float4 l4 = *reinterpret_cast<const float4*>(lp);
+    q.l[0] = l4.x; q.l[1] = l4.y; q.l[2] = l4.z; q.l[3] = l4.w;
+  }
 }
 
 constexpr int kRollStats = 3;  // stored sum, stored max, reward dot
@@ -953,9 +853,13 @@ constexpr int kRollChunk = 8;  // copies per block (sharing one action)
 // the T_u stencil and R_u of a slab are loaded once for all copies, and each
 // copy's {sum, max, reward} stays in registers until one wave reduction per
 // copy at the end of the tile.
-template <int CH, int PF>
+// CODED: T_u and L come from the dictionary-coded model (pp2_coded.hip)
+// staged in LDS (the T_u column of the chunk's action, all 16 L columns)
+// instead of the dense planes; same values, so bit-identical results.
+template <int CH, int PF, bool CODED>
 __global__ __launch_bounds__(kBlock) void k_rollout_step(
-    Geom g, PlaneSet T, PlaneSet L, PlaneSet R, const _Float16* __restrict__ bin,
+    Geom g, PlaneSet T, PlaneSet L, PlaneSet R, const uint16_t* __restrict__ code,
+    const float* __restrict__ dict, int E, const _Float16* __restrict__ bin,
     _Float16* __restrict__ bout, long long cstride, const int* __restrict__ chunk_u,
     const int* __restrict__ chunk_first, const int* __restrict__ copies,
     const uint8_t* __restrict__ zs, const float* __restrict__ in_stats,
@@ -967,6 +871,16 @@ __global__ __launch_bounds__(kBlock) void k_rollout_step(
   const int ch = blockIdx.y;
   const int u = chunk_u[ch], first = chunk_first[ch];
   const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  extern __shared__ float rlds[];
+  float* sT = rlds;           // [E][9]  T_u
+  float* sL = rlds + E * 9;   // [E][16] L
+  if constexpr (CODED) {
+    for (int i = threadIdx.x; i < E * 9; i += kBlock)
+      sT[i] = dict[(long long)(i / 9) * kDictRow + u * 10 + i % 9];
+    for (int i = threadIdx.x; i < E * 16; i += kBlock)
+      sL[i] = dict[(long long)(i / 16) * kDictRow + kDictL + i % 16];
+    __syncthreads();
+  }
   const long long ncells = (long long)g.rows * g.wp;
   const long long tile0 = (long long)blockIdx.x * kRollIter * (kBlock * 4);
   const int iters = (int)min((long long)kRollIter, (ncells - tile0 + kBlock * 4 - 1) / (kBlock * 4));
@@ -989,14 +903,30 @@ __global__ __launch_bounds__(kBlock) void k_rollout_step(
     const int y = (int)(cell / g.wp), x0 = (int)(cell % g.wp);
     const bool le = x0 == 0, re = x0 + 4 == g.wp;
     float tv[9][4], rv[4];
+    uint32_t lc[4] = {0, 0, 0, 0};  // coded: L row offsets of the 4 cells
+    if constexpr (CODED) {
+      CodeWin w;
+      load_codes(code, g.wp, y, x0, w);
 #pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      const int oy = s / 3 - 1, ox = s % 3 - 1;
-      const float* tp = T.p + (long long)(y + oy) * T.rs + (long long)(9 * u + 8 - s) * T.ps + x0 + ox;
-      if (ox == 0) ldv<4, true>(tp, tv[s]);
-      else ldv<4, false>(tp, tv[s]);
-      if (ox < 0 && le) tv[s][0] = 0.0f;
-      if (ox > 0 && re) tv[s][3] = 0.0f;
+      for (int s = 0; s < 9; ++s) {
+        const int oy = s / 3 - 1, ox = s % 3 - 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tv[s][k] = sT[w.c[oy + 1][k + 1 + ox] * 9 + 8 - s];
+        if (ox < 0 && le) tv[s][0] = 0.0f;
+        if (ox > 0 && re) tv[s][3] = 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lc[k] = w.c[1][k + 1] * 16;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {
+        const int oy = s / 3 - 1, ox = s % 3 - 1;
+        const float* tp = T.p + (long long)(y + oy) * T.rs + (long long)(9 * u + 8 - s) * T.ps + x0 + ox;
+        if (ox == 0) ldv<4, true>(tp, tv[s]);
+        else ldv<4, false>(tp, tv[s]);
+        if (ox < 0 && le) tv[s][0] = 0.0f;
+        if (ox > 0 && re) tv[s][3] = 0.0f;
+      }
     }
     ldv<4, true>(R.p + (long long)y * R.rs + (long long)u * R.ps + x0, rv);
     const long long off = (long long)y * g.wp + x0;
@@ -1007,11 +937,11 @@ __global__ __launch_bounds__(kBlock) void k_rollout_step(
     RollRaw q[PF + 1];
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-      roll_load(q[j], bin + cbase[j] + off, g.wp, lrow + (long long)zc[j] * L.ps);
+      roll_load<!CODED>(q[j], bin + cbase[j] + off, g.wp, lrow + (long long)zc[j] * L.ps);
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       if (j + PF < CH)
-        roll_load(q[(j + PF) % (PF + 1)], bin + cbase[j + PF] + off, g.wp,
+        roll_load<!CODED>(q[(j + PF) % (PF + 1)], bin + cbase[j + PF] + off, g.wp,
                   lrow + (long long)zc[j + PF] * L.ps);
       const RollRaw& r = q[j % (PF + 1)];
       float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bcen[4];
@@ -1038,7 +968,10 @@ __global__ __launch_bounds__(kBlock) void k_rollout_step(
       h4 o;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float v = (p[k] * r.l[k]) * inv[j];
+        float lz;
+        if constexpr (CODED) lz = sL[lc[k] + zc[j]];
+        else lz = r.l[k];
+        const float v = (p[k] * lz) * inv[j];
         o[k] = (_Float16)v;
         const float vr = valid ? (float)o[k] : 0.0f;
         acc[j][0] += vr;
@@ -1192,7 +1125,8 @@ int rollout_chunk() { return kRollVariants[roll_variant()].ch; }
 int rollout_min_chunk() { return 4; }
 
 hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
-                               PlaneSet R, const void* bin, void* bout, long long cstride,
+                               PlaneSet R, const uint16_t* code, const float* dict, int E,
+                               const void* bin, void* bout, long long cstride,
                                int nchunks, const int* chunk_u, const int* chunk_first,
                                const int* chunk_n, const int* copies, const uint8_t* zs,
                                const float* in_stats, float* partials, float* stats_out,
@@ -1203,9 +1137,18 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
   const dim3 grid(tiles, nchunks);
   const _Float16* bi = (const _Float16*)bin + g.wp;
   _Float16* bo = (_Float16*)bout + g.wp;
-#define PP2_ROLL(CH, PF)                                                                   \
-  hipLaunchKernelGGL((k_rollout_step<CH, PF>), grid, dim3(kBlock), 0, st, g, T, L, R, bi, bo, \
-                     cstride, chunk_u, chunk_first, copies, zs, in_stats, partials, nw)
+#define PP2_ROLL(CH, PF)                                                                    \
+  do {                                                                                      \
+    if (E > 0)                                                                              \
+      hipLaunchKernelGGL((k_rollout_step<CH, PF, true>), grid, dim3(kBlock), lds, st, g, T,  \
+                         L, R, code, dict, E, bi, bo, cstride, chunk_u, chunk_first, copies, \
+                         zs, in_stats, partials, nw);                                       \
+    else                                                                                    \
+      hipLaunchKernelGGL((k_rollout_step<CH, PF, false>), grid, dim3(kBlock), 0, st, g, T,   \
+                         L, R, code, dict, 0, bi, bo, cstride, chunk_u, chunk_first, copies, \
+                         zs, in_stats, partials, nw);                                       \
+  } while (0)
+  const size_t lds = (size_t)E * 25 * sizeof(float);
   switch (roll_variant()) {
     case 1: PP2_ROLL(8, 2); break;
     case 2: PP2_ROLL(4, 1); break;

@@ -165,7 +165,9 @@ int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs) {
   HIPCHK(hipMemcpyAsync(r->d_zs, zs, (size_t)D * C, hipMemcpyHostToDevice, c->stream));
   for (int k = 0; k < D; ++k) {
     const int* base = r->d_chunks + k * stride;
-    HIPCHK(pp2::launch_rollout_step(c->stream, c->g, c->T.v, c->L.v, c->R.v, r->buf[k & 1],
+    const bool coded = coded_active(c);
+    HIPCHK(pp2::launch_rollout_step(c->stream, c->g, c->T.v, c->L.v, c->R.v, c->d_code,
+                                    c->d_dict, coded ? c->dict_n : 0, r->buf[k & 1],
                                     r->buf[(k + 1) & 1], r->cstride, r->nchunks[k], base,
                                     base + M, base + 2 * M, base + 3 * M,
                                     r->d_zs + (size_t)k * C,

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "pp2_ctx.h"
@@ -254,8 +255,128 @@ std::string join(const char* dir, const char* name) {
   return d + name;
 }
 
+bool coded_active(const pp2_ctx* c) { return c->use_coded && c->dict_n > 0 && c->cpt == 4; }
+
+// Dictionary of the distinct per-cell model tuples (T, C, L) over rows
+// [-1, rows]: GPU hash per cell, first-appearance numbering on the host, GPU
+// gather of one representative per entry, then a bitwise check of every cell
+// against its entry.  More than kDictMax entries or any mismatch (a hash
+// collision) leaves dict_n = 0, i.e. the dense kernels.
+int build_model_dict(pp2_ctx* c) {
+  c->dict_n = 0;
+  const long long n = (long long)(c->g.rows + 2) * c->g.wp;
+  if (!c->code_alloc) {
+    if (hipMalloc(&c->code_alloc, (size_t)(n + 2 * kGuard) * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&c->d_dict, (size_t)pp2::kDictMax * pp2::kDictRow * sizeof(float)) != hipSuccess ||
+        hipMalloc(&c->d_rows, ((size_t)pp2::kDictMax * pp2::kDictTC + 4) * sizeof(float)) != hipSuccess ||
+        hipMalloc(&c->d_dl, (size_t)pp2::kDictMax * 16 * sizeof(float)) != hipSuccess)
+      return set_err(PP2_ENOMEM, "hipMalloc model dictionary");
+    HIPCHK(hipMemsetAsync(c->code_alloc, 0, (size_t)(n + 2 * kGuard) * sizeof(uint16_t), c->stream));
+    c->d_code = c->code_alloc + kGuard + c->g.wp;
+  }
+  uint64_t* d_hash = nullptr;
+  int* d_aux = nullptr;
+  if (hipMalloc(&d_hash, (size_t)n * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&d_aux, (size_t)(pp2::kDictMax + 1) * sizeof(int)) != hipSuccess) {
+    (void)hipFree(d_hash);
+    return set_err(PP2_ENOMEM, "hipMalloc dictionary scratch");
+  }
+  struct Free {
+    void* a;
+    void* b;
+    ~Free() { (void)hipFree(a); (void)hipFree(b); }
+  } fr{d_hash, d_aux};
+  std::vector<uint64_t> h((size_t)n);
+  HIPCHK(pp2::launch_dict_hash(c->stream, c->g, c->T.v, c->C.v, c->R.v, c->L.v, d_hash));
+  HIPCHK(hipMemcpyAsync(h.data(), d_hash, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  std::vector<uint16_t> code((size_t)n);
+  std::vector<int> reps;
+  std::unordered_map<uint64_t, int> ids;
+  ids.reserve(1024);
+  uint64_t last_h = 0;
+  int last_id = -1;
+  for (long long i = 0; i < n; ++i) {
+    if (last_id >= 0 && h[i] == last_h) { code[i] = (uint16_t)last_id; continue; }
+    auto it = ids.find(h[i]);
+    int id;
+    if (it == ids.end()) {
+      if ((int)reps.size() >= pp2::kDictMax) return PP2_OK;  // too many patterns: dense path
+      id = (int)reps.size();
+      ids.emplace(h[i], id);
+      reps.push_back((int)i);
+    } else {
+      id = it->second;
+    }
+    code[i] = (uint16_t)id;
+    last_h = h[i];
+    last_id = id;
+  }
+  const int E = (int)reps.size();
+  const int zero = 0;
+  HIPCHK(hipMemcpyAsync(c->code_alloc + kGuard, code.data(), (size_t)n * sizeof(uint16_t),
+                        hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d_aux, reps.data(), E * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d_aux + pp2::kDictMax, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(pp2::launch_dict_gather(c->stream, c->g, c->T.v, c->C.v, c->R.v, c->L.v, d_aux, E,
+                                 c->d_dict));
+  HIPCHK(pp2::launch_dict_verify(c->stream, c->g, c->T.v, c->C.v, c->R.v, c->L.v,
+                                 c->code_alloc + kGuard, c->d_dict, d_aux + pp2::kDictMax));
+  int bad = 1;
+  std::vector<float> dh((size_t)E * pp2::kDictRow);
+  HIPCHK(hipMemcpyAsync(&bad, d_aux + pp2::kDictMax, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(dh.data(), c->d_dict, dh.size() * sizeof(float), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (bad) return PP2_OK;
+  // LDS-layout rows: sparse when every T entry off the base-kernel support is
+  // +0.0 (always so for generated models), else the full [a][T..,C] rows
+  bool sparse = true;
+  for (int e = 0; e < E && sparse; ++e)
+    for (int a = 0; a < 9 && sparse; ++a)
+      for (int i = 0; i < 9; ++i) {
+        bool in = false;
+        for (int j = 0; j < pp2::kSupN[a]; ++j) in |= pp2::kSup[a][j] == i;
+        uint32_t bits;
+        std::memcpy(&bits, &dh[(size_t)e * pp2::kDictRow + a * 10 + i], 4);
+        if (!in && bits != 0) { sparse = false; break; }
+      }
+  const int rw = sparse ? pp2::kSpRow : pp2::kDictTC;
+  const int es = (E + 3) & ~3;  // L_z column stride (16-B aligned columns)
+  std::vector<float> rows((size_t)E * rw + 4, 0.0f), dl((size_t)16 * es, 0.0f);
+  for (int e = 0; e < E; ++e) {
+    const float* src = &dh[(size_t)e * pp2::kDictRow];
+    float* dst = &rows[(size_t)e * rw];
+    if (sparse) {
+      for (int a = 0; a < 9; ++a) {
+        for (int j = 0; j < pp2::kSupN[a]; ++j) dst[a * 6 + j] = src[a * 10 + pp2::kSup[a][j]];
+        dst[a * 6 + 4] = src[a * 10 + 9];
+      }
+    } else {
+      std::memcpy(dst, src, pp2::kDictTC * sizeof(float));
+    }
+    for (int z = 0; z < 16; ++z) dl[(size_t)z * es + e] = src[pp2::kDictL + z];
+  }
+  HIPCHK(hipMemcpyAsync(c->d_rows, rows.data(), rows.size() * sizeof(float),
+                        hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_dl, dl.data(), dl.size() * sizeof(float), hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->dict_sparse = sparse;
+  c->dict_n = E;
+  return PP2_OK;
+}
+
 int mdp_sweep_once(pp2_ctx* c) {
   const int jn = c->jcur ^ 1;
+  if (coded_active(c)) {
+    HIPCHK(pp2::launch_mdp_sweep_coded(c->stream, c->g, c->gamma, c->d_code, c->d_rows,
+                                       c->dict_n, c->dict_sparse, c->J[c->jcur].v.p,
+                                       c->J[jn].v.p, c->A));
+    c->jcur = jn;
+    return PP2_OK;
+  }
   HIPCHK(pp2::launch_mdp_sweep(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->C.v,
                                c->J[c->jcur].v.p, c->J[jn].v.p, c->A, c->nt_streams));
   c->jcur = jn;
@@ -322,11 +443,20 @@ int pp2rt::loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass) {
   const int bc = c->bcur, bn = bc ^ 1, jn = c->jcur ^ 1;
   const int nparts = pp2::cells_grid(c->g, c->cpt);
   const bool pend = c->pending[bc];
-  HIPCHK(pp2::launch_loop_step(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->L.v, c->C.v,
-                               c->b[bc].v.p, c->b[bn].v.p, u, z,
-                               pend ? c->pbuf[bc] : nullptr, c->pcount[bc],
-                               c->bsum + bc, pend ? c->bsum + bc : nullptr, c->pbuf[bn],
-                               c->J[c->jcur].v.p, c->J[jn].v.p, c->A, c->nt_streams));
+  if (coded_active(c)) {
+    HIPCHK(pp2::launch_loop_step_coded(c->stream, c->g, c->gamma, c->d_code, c->d_rows,
+                                       c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3), c->dict_n,
+                                       c->dict_sparse, c->b[bc].v.p, c->b[bn].v.p, u,
+                                       pend ? c->pbuf[bc] : nullptr, c->pcount[bc],
+                                       c->bsum + bc, pend ? c->bsum + bc : nullptr,
+                                       c->pbuf[bn], c->J[c->jcur].v.p, c->J[jn].v.p, c->A));
+  } else {
+    HIPCHK(pp2::launch_loop_step(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->L.v, c->C.v,
+                                 c->b[bc].v.p, c->b[bn].v.p, u, z,
+                                 pend ? c->pbuf[bc] : nullptr, c->pcount[bc],
+                                 c->bsum + bc, pend ? c->bsum + bc : nullptr, c->pbuf[bn],
+                                 c->J[c->jcur].v.p, c->J[jn].v.p, c->A, c->nt_streams));
+  }
   c->pending[bc] = false;
   c->pcount[bn] = nparts;
   c->pending[bn] = true;
@@ -395,6 +525,9 @@ int pp2_destroy(pp2_ctx* c) {
     if (pb) (void)hipFree(pb);
   if (c->rpartials) (void)hipFree(c->rpartials);
   if (c->staging) (void)hipFree(c->staging);
+  if (c->code_alloc) (void)hipFree(c->code_alloc);
+  for (float* p : {c->d_dict, c->d_rows, c->d_dl})
+    if (p) (void)hipFree(p);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return PP2_OK;
@@ -428,6 +561,7 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
   switch (key) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
+    case PP2_TUNE_CODED_MODEL: c->use_coded = value != 0; return PP2_OK;
     default: return set_err(PP2_EINVAL, "unknown tuning key %d", key);
   }
 }
@@ -447,6 +581,13 @@ int pp2_model_generate(pp2_ctx* c) {
   HIPCHK(pp2::launch_model_gen(c->stream, c->g, c->d_map, c->gx, c->gy, c->T.v,
                                c->L.v, c->R.v, c->C.v));
   c->model_ready = true;
+  return build_model_dict(c);
+}
+
+int pp2_model_dict_info(pp2_ctx* c, int* entries, int* active) {
+  CHECK(check_ctx(c));
+  if (entries) *entries = c->dict_n;
+  if (active) *active = coded_active(c) ? 1 : 0;
   return PP2_OK;
 }
 
@@ -473,7 +614,7 @@ int pp2_model_upload(pp2_ctx* c, const float* T, const float* L, const float* R,
   if (R) CHECK(upload_planes(c, c->R, R));
   if (C) CHECK(upload_planes(c, c->C, C));
   c->model_ready = true;
-  return PP2_OK;
+  return build_model_dict(c);
 }
 
 int pp2_model_save(pp2_ctx* c, const char* dir) {

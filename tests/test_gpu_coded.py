@@ -1,0 +1,229 @@
+"""GPU: the dictionary-coded model path (pp2_coded.hip) against the dense
+kernels and the oracle.
+
+The coded kernels compute every cell with the dense kernels' operands and fmaf
+order, and reduce the belief mass over the same cell->block map and tree, so
+the bar is bit equality with the dense path -- raw beliefs, masses, values and
+actions -- after every step, on golden maps, ragged synthetic grids and the
+1024x1024 bench grid.  Parity with the reference then follows from the dense
+path's parity (test_gpu_parity.py), and is re-checked here against the oracle.
+"""
+import numpy as np
+import pytest
+
+from conftest import GAMMA, golden, golden_map
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pp2():
+    import path_planning_2d_amd as P
+    assert P.device_count() >= 1, "no GPU visible"
+    return P
+
+
+def ctx_pair(pp2, grid, goal):
+    a = pp2.GridContext(grid, goal, gamma=float(GAMMA))
+    b = pp2.GridContext(grid, goal, gamma=float(GAMMA))
+    a.model_generate()
+    b.model_generate()
+    b.set_tuning(b.TUNE_CODED_MODEL, 0)
+    ea, aa = a.model_dict_info()
+    eb, ab = b.model_dict_info()
+    assert aa and ea > 0 and ea == eb and not ab
+    return a, b
+
+
+def grids():
+    from path_planning_2d_amd import synthetic as S
+    out = []
+    for name in ("map_3x3", "map_10x10", "sparse_map_100x40", "tile64_sparse_map_100x40"):
+        out.append((name, golden_map(name), tuple(golden("model", name)["goal"])))
+    for H, W, seed in ((97, 131, 3), (1, 7, 1), (5, 1, 2), (256, 256, 256), (33, 1030, 9)):
+        g = S.synth_grid(H, W, seed)
+        g[0, 0] = 0
+        out.append((f"synth_{H}x{W}", g, (0, 0)))
+    return out
+
+
+GRIDS = grids()
+
+
+@pytest.mark.parametrize("name,grid,goal", GRIDS, ids=[g[0] for g in GRIDS])
+def test_dictionary_covers_model(pp2, name, grid, goal):
+    with pp2.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        entries, active = ctx.model_dict_info()
+    # 3x3 occupancy determines the tuple: <= 256 free-centre patterns, 16
+    # trapped (L depends on 4 neighbours), the goal and the zero cell
+    assert active and 1 <= entries <= 256 + 16 + 2
+
+
+@pytest.mark.parametrize("name,grid,goal", GRIDS, ids=[g[0] for g in GRIDS])
+def test_loop_coded_equals_dense_bit_exact(pp2, name, grid, goal):
+    from path_planning_2d_amd import synthetic as S
+    steps = 6
+    us, zs, _ = S.synth_trajectory(grid, steps, seed=7)
+    b0 = S.uniform_belief(grid)
+    a, b = ctx_pair(pp2, grid, goal)
+    with a, b:
+        for c in (a, b):
+            c.belief_set(b0)
+            c.mdp_reset()
+        for k in range(steps):
+            a.loop_step(int(us[k]), int(zs[k]))
+            b.loop_step(int(us[k]), int(zs[k]))
+            ra, ma = a.belief_get_raw()
+            rb, mb = b.belief_get_raw()
+            np.testing.assert_array_equal(ra, rb, err_msg=f"raw belief, step {k}")
+            assert np.float32(ma) == np.float32(mb), (k, ma, mb)
+            Ja, Aa = a.mdp_get()
+            Jb, Ab = b.mdp_get()
+            np.testing.assert_array_equal(Ja, Jb, err_msg=f"J, step {k}")
+            np.testing.assert_array_equal(Aa, Ab, err_msg=f"A, step {k}")
+
+
+def test_loop_1024_coded_equals_dense(pp2):
+    from path_planning_2d_amd import synthetic as S
+    N = 1024
+    grid = S.synth_grid(N, N, N)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 4, seed=42)
+    b0 = S.uniform_belief(grid)
+    a, b = ctx_pair(pp2, grid, goal)
+    with a, b:
+        for c in (a, b):
+            c.belief_set(b0)
+            c.mdp_reset()
+            c.loop_run(us, zs)
+        np.testing.assert_array_equal(a.belief_get(), b.belief_get())
+        Ja, Aa = a.mdp_get()
+        Jb, Ab = b.mdp_get()
+        np.testing.assert_array_equal(Ja, Jb)
+        np.testing.assert_array_equal(Aa, Ab)
+
+
+@pytest.mark.parametrize("name", ["map_10x10", "sparse_map_100x40", "tile64_sparse_map_100x40"])
+def test_mdp_coded_matches_golden(pp2, name):
+    """Coded sweeps reproduce the reference's values/actions bit for bit."""
+    grid = golden_map(name)
+    m = golden("model", name)
+    g = golden("mdp", name)
+    with pp2.GridContext(grid, tuple(m["goal"]), gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        assert ctx.model_dict_info()[1]
+        ctx.mdp_reset()
+        ctx.mdp_sweep(7)
+        J, A = ctx.mdp_get()
+        np.testing.assert_array_equal(J, g["J7"])
+        np.testing.assert_array_equal(A, g["A7"])
+
+
+def test_mdp_solve_coded_equals_dense(pp2, oracle):
+    from path_planning_2d_amd import synthetic as S
+    N = 256
+    grid = S.synth_grid(N, N, N)
+    goal = S.synth_goal(grid)
+    a, b = ctx_pair(pp2, grid, goal)
+    with a, b:
+        ra = a.mdp_solve()
+        rb = b.mdp_solve()
+        assert ra == rb
+        Ja, Aa = a.mdp_get()
+        Jb, Ab = b.mdp_get()
+        np.testing.assert_array_equal(Ja, Jb)
+        np.testing.assert_array_equal(Aa, Ab)
+    T, _, _ = oracle.model_pomdp(grid, goal)
+    _, Cc = oracle.model_mdp(grid, goal)
+    Jo = np.zeros(N * N, np.float32)
+    for _ in range(25):
+        Jo, Ao = oracle.mdp_sweep(N, N, GAMMA, T, Cc, Jo)
+    with pp2.GridContext(grid, goal, gamma=float(GAMMA)) as c:
+        c.model_generate()
+        c.mdp_reset()
+        c.mdp_sweep(25)
+        J, A = c.mdp_get()
+    np.testing.assert_array_equal(J, Jo)
+    np.testing.assert_array_equal(A, Ao)
+
+
+def test_toggling_paths_mid_run(pp2):
+    """Pending partial masses hand over between the coded and dense kernels."""
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(64, 72, 5)
+    grid[0, 0] = 0
+    us, zs, _ = S.synth_trajectory(grid, 8, seed=3)
+    b0 = S.uniform_belief(grid)
+    a, b = ctx_pair(pp2, grid, (0, 0))
+    with a, b:
+        for c in (a, b):
+            c.belief_set(b0)
+            c.mdp_reset()
+        for k in range(8):
+            a.set_tuning(a.TUNE_CODED_MODEL, k % 2)
+            a.loop_step(int(us[k]), int(zs[k]))
+            b.loop_step(int(us[k]), int(zs[k]))
+        np.testing.assert_array_equal(a.belief_get(), b.belief_get())
+        np.testing.assert_array_equal(a.mdp_get()[0], b.mdp_get()[0])
+
+
+def test_irregular_model_falls_back_to_dense(pp2):
+    """A model with more distinct cells than the LDS dictionary holds runs on
+    the dense kernels (and a regular one re-enables the coded path)."""
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(40, 48, 11)
+    grid[0, 0] = 0
+    with pp2.GridContext(grid, (0, 0), gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        T, L, R, Cc = ctx.model_download()
+        e0, _ = ctx.model_dict_info()
+        rng = np.random.default_rng(0)
+        Tn = (T * (1.0 + 1e-3 * rng.random(T.shape))).astype(np.float32)
+        ctx.model_upload(Tn, L, R, Cc)
+        assert ctx.model_dict_info() == (0, False)
+        b0 = S.uniform_belief(grid)
+        ctx.belief_set(b0)
+        ctx.belief_update(1, 3)
+        assert np.isfinite(ctx.belief_get()).all()
+        ctx.model_upload(T, L, R, Cc)
+        assert ctx.model_dict_info() == (e0, True)
+        # perturbing one cell whose tuple is shared adds exactly one entry
+        tup = np.concatenate([T.reshape(len(T), -1), Cc, L], axis=1)
+        _, inv, cnt = np.unique(tup, axis=0, return_inverse=True, return_counts=True)
+        cell = int(np.nonzero(cnt[inv.reshape(-1)] >= 2)[0][0])
+        T1 = T.copy()
+        T1[cell, 0, 0] = np.float32(0.3)
+        ctx.model_upload(T1, L, R, Cc)
+        e1, act = ctx.model_dict_info()
+        assert act and e1 == e0 + 1
+
+
+def test_off_support_model_uses_full_rows(pp2):
+    """A T entry outside its action's base-kernel support rules out the
+    sparse LDS rows; the full-row coded kernels must still match dense."""
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(48, 60, 21)
+    grid[0, 0] = 0
+    us, zs, _ = S.synth_trajectory(grid, 5, seed=8)
+    us[:] = 4  # the stay action reads the off-support entry below
+    b0 = S.uniform_belief(grid)
+    a, b = ctx_pair(pp2, grid, (0, 0))
+    with a, b:
+        T, L, R, Cc = a.model_download()
+        cell = 17 * 60 + 23
+        T[cell, 4, 0] = np.float32(0.25)  # stay action: support is {4} only
+        for c in (a, b):
+            c.model_upload(T, L, R, Cc)
+            c.belief_set(b0)
+            c.mdp_reset()
+        assert a.model_dict_info()[1] and not b.model_dict_info()[1]
+        for k in range(5):
+            a.loop_step(int(us[k]), int(zs[k]))
+            b.loop_step(int(us[k]), int(zs[k]))
+        np.testing.assert_array_equal(a.belief_get_raw()[0], b.belief_get_raw()[0])
+        np.testing.assert_array_equal(a.mdp_get()[0], b.mdp_get()[0])
+        np.testing.assert_array_equal(a.mdp_get()[1], b.mdp_get()[1])
+        a.mdp_sweep(9)
+        b.mdp_sweep(9)
+        np.testing.assert_array_equal(a.mdp_get()[0], b.mdp_get()[0])

@@ -101,3 +101,33 @@ def test_rollout_config5_512_4096x5(oracle):
             pick = [0, 1, 777, 2048, 4095]
             oc = oracle_rollout(oracle, grid, T, L, R, alphas, b0, us, zs, pick)
             check(res, oc, r)
+
+
+@pytest.mark.parametrize("H,W,copies,depth", [(37, 53, 61, 4), (128, 128, 300, 5)])
+def test_rollout_coded_equals_dense(H, W, copies, depth):
+    """The coded-model rollout (T_u / R_u / L from the LDS dictionary) gives
+    bit-identical results and beliefs to the dense-plane rollout."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(H, W, seed=H * W)
+    goal = S.synth_goal(grid)
+    b0 = S.uniform_belief(grid)
+    us, zs = S.rollout_trajectories(grid, b0, copies, depth, seed=5)
+    out = []
+    for coded in (1, 0):
+        with P.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
+            ctx.model_generate()
+            ctx.set_tuning(ctx.TUNE_CODED_MODEL, coded)
+            assert ctx.model_dict_info()[1] == bool(coded)
+            ctx.fib_solve(max_sweeps=20)
+            with P.BatchedRollout(ctx, copies, depth) as r:
+                r.set_root(b0)
+                r.run(us, zs)
+                res = r.results()
+                beliefs = [r.belief(c) for c in (0, copies // 2, copies - 1)]
+        out.append((res, beliefs))
+    (ra, ba), (rb, bb) = out
+    for k in ra:
+        np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
+    for x, y in zip(ba, bb):
+        np.testing.assert_array_equal(x, y)
