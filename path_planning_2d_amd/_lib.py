@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libpp2_hip.so")
+# PP2_LIBRARY points at a diagnostic build of the same ABI (tools/micro/).
+LIB_PATH = os.environ.get("PP2_LIBRARY") or os.path.join(PKG_DIR, "libpp2_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "pp2.h")
 
 RCCL_ID_BYTES = 128

@@ -18,9 +18,21 @@
 // the dense kernels' (same operands, same fmaf order), and the belief partial
 // sums use the dense kernels' cell->block mapping and reduction tree, so the
 // coded and dense paths give bit-identical beliefs, masses, values and actions.
+#include <stdlib.h>
+
 #include "pp2_device.h"
 
 namespace pp2 {
+
+#ifdef PP2_PHASE_TRACE
+// Diagnostic build only (tools/micro/phase_trace.sh): thread 0 of each
+// workgroup records s_memrealtime (100 MHz) at the fused step's phase points.
+__device__ unsigned long long g_phase[1024][8];
+#define PP2_PHASE(i) \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define PP2_PHASE(i) (void)0
+#endif
 
 namespace {
 
@@ -107,30 +119,32 @@ struct Layout {
   static constexpr int blk = SPARSE ? 6 : 10;  // floats per action block
 };
 
-// Global -> LDS copy of n floats (src and dst 16-B aligned, src readable up
-// to n rounded up to 4): 16-B loads, eight in flight per thread before the
-// LDS stores, so staging costs a few L2 round trips rather than one per float.
+// Global -> LDS copy of n floats with LDS-DMA (global_load_lds_dwordx4: no
+// VGPR round trip, so the registers of an already-issued tile load stay
+// free).  One wave-instruction writes 1 KiB contiguously at a wave-uniform
+// base; the last one's tail lanes re-read the final 16 B of src and land in
+// the slack up to lds_span(n) floats.  The __syncthreads() that follows
+// waits for the DMA (vmcnt(0)).
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+__host__ __device__ constexpr int lds_span(int n) { return (n + 255) & ~255; }
+
 __device__ __forceinline__ void stage_rows(const float* __restrict__ src, int n, float* dst) {
   const int n4 = (n + 3) >> 2;
-  const f4a* s4 = reinterpret_cast<const f4a*>(src);
-  f4a* d4 = reinterpret_cast<f4a*>(dst);
-  for (int base = 0; base < n4; base += 8 * (int)blockDim.x) {
-    f4a v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = base + j * (int)blockDim.x + (int)threadIdx.x;
-      if (i < n4) v[j] = s4[i];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = base + j * (int)blockDim.x + (int)threadIdx.x;
-      if (i < n4) d4[i] = v[j];
-    }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int c = wave; c * 64 < n4; c += nw) {
+    int i = c * 64 + lane;
+    if (i >= n4) i = n4 - 1;
+    __builtin_amdgcn_global_load_lds((glb_void*)(src + 4 * i), (lds_void*)(dst + c * 256), 16, 0,
+                                     0);
   }
 }
 
 // Bellman backup of 4 cells from their codes (k_mdp_sweep's arithmetic).
-template <bool SPARSE>
+// CELL_GRAIN: scheduling barrier after every cell (kernels capped at 64
+// VGPRs) instead of after every action.
+template <bool SPARSE, bool CELL_GRAIN>
 __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&cc)[4],
                                              const float (&jn)[9][4], float gamma,
                                              float (&best)[4], uint32_t (&arg)[4]) {
@@ -138,7 +152,7 @@ __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&
   for (int k = 0; k < 4; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
   if constexpr (SPARSE) {
     // fully unrolled (support positions index jn at compile time); the
-    // scheduling barrier keeps one action's LDS reads live at a time
+    // scheduling barrier keeps one cell's dictionary row live at a time
 #pragma unroll
     for (int a = 0; a < 9; ++a) {
 #pragma unroll
@@ -153,8 +167,9 @@ __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&
         for (int j = 0; j < 4; ++j)
           if (j < kSupN[a]) cost = __builtin_fmaf(gamma * tv[j], jn[kSup[a][j]][k], cost);
         if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
+        if (CELL_GRAIN) __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      if (!CELL_GRAIN) __builtin_amdgcn_sched_barrier(0);
     }
   } else {
     // one action at a time: 4 cells x 10 dictionary floats live (a fully
@@ -195,11 +210,117 @@ __device__ __forceinline__ void store_ja(float* __restrict__ J_out, uint8_t* __r
   *reinterpret_cast<uint32_t*>(A + off) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
 }
 
+// A lane's 3-row stencil window over its 4 cells: x0-1 .. x0+4 of rows
+// y-1, y, y+1 (one aligned 16-B load and two dword loads per row).  Values
+// outside the grid's x range are 0.
+struct Win6 {
+  float v[3][6];
+};
+
+__device__ __forceinline__ void load_win6(const float* __restrict__ base, int wp, int y, int x0,
+                                          bool le, bool re, Win6& w) {
+
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const float* p = base + (long long)(y + r - 1) * wp + x0;
+    const f4a m = *reinterpret_cast<const f4a*>(p);
+    const float l = p[-1], rt = p[4];
+    w.v[r][0] = le ? 0.0f : l;
+    w.v[r][1] = m[0];
+    w.v[r][2] = m[1];
+    w.v[r][3] = m[2];
+    w.v[r][4] = m[3];
+    w.v[r][5] = re ? 0.0f : rt;
+  }
+}
+
+// Packed codes of the same window: per row the dword at x0-2 (x0-1 in its
+// high half), the 4 codes at x0..x0+3, the dword at x0+4 (x0+4 in its low half).
+struct CodeWin6 {
+  uint32_t lw[3], m0[3], m1[3], rw[3];
+  __device__ __forceinline__ uint32_t at(int r, int c) const {
+    switch (c) {
+      case 0: return lw[r] >> 16;
+      case 1: return m0[r] & 0xffffu;
+      case 2: return m0[r] >> 16;
+      case 3: return m1[r] & 0xffffu;
+      case 4: return m1[r] >> 16;
+      default: return rw[r] & 0xffffu;
+    }
+  }
+};
+
+__device__ __forceinline__ void load_codes6(const uint16_t* __restrict__ code, int wp, int y,
+                                            int x0, CodeWin6& w) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const uint16_t* cp = code + (long long)(y + r - 1) * wp + x0;
+    const uint2 m = *reinterpret_cast<const uint2*>(cp);
+    w.m0[r] = m.x;
+    w.m1[r] = m.y;
+    w.lw[r] = *reinterpret_cast<const uint32_t*>(cp - 2);
+    w.rw[r] = *reinterpret_cast<const uint32_t*>(cp + 4);
+  }
+}
+
+// The two halves of a coded fused step for one lane's 4 cells.
+template <bool SPARSE>
+__device__ __forceinline__ void belief_cells(const Geom& g, const float* sTC, const float* sL,
+                                             const int (&slot)[9], int ublk, float inv,
+                                             const CodeWin6& cw, const Win6& win, int y, int x0,
+                                             float* __restrict__ b_out, float& local) {
+  using LY = Layout<SPARSE>;
+  const bool lx = x0 == 0, rx = x0 + 4 == g.wp;
+  // p = L_z * sum_s T[x+off_s][u][8-s] b(x+off_s), in s order
+  float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const int oy = s / 3, ox = s % 3 - 1;
+    const int sl = slot[8 - s];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float tv = sl >= 0 ? sTC[cw.at(oy, k + 1 + ox) * LY::row + ublk + sl] : 0.0f;
+      if (ox < 0 && k == 0 && lx) tv = 0.0f;
+      if (ox > 0 && k == 3 && rx) tv = 0.0f;
+      p[k] = __builtin_fmaf(tv, win.v[oy][k + 1 + ox], p[k]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // <= 4 gathers in flight (64-VGPR budget)
+  }
+  local = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    p[k] = p[k] * sL[cw.at(1, k + 1)];
+    p[k] = p[k] * inv;
+    local += p[k];
+  }
+  stv<4>(b_out + (long long)y * g.wp + x0, p);
+}
+
+template <bool SPARSE>
+__device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, float gamma,
+                                            uint32_t m0, uint32_t m1, const Win6& win, int y,
+                                            int x0, float* __restrict__ J_out,
+                                            uint8_t* __restrict__ A) {
+  float jn[9][4];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) jn[i][k] = win.v[i / 3][k + i % 3];
+  const uint32_t cc[4] = {m0 & 0xffffu, m0 >> 16, m1 & 0xffffu, m1 >> 16};
+  float best[4];
+  uint32_t arg[4];
+  coded_sweep4<SPARSE, true>(sTC, cc, jn, gamma, best, arg);
+  store_ja(J_out, A, (long long)y * g.wp + x0, best, arg);
+}
+
 // Fused north-star step on the coded model (k_loop_step's semantics).  A
-// workgroup is QPB dense-kernel blocks ("quarters" of 256 threads): quarter q
-// of tile t is dense block d = QPB*t + q with the same 1024 cells, the same
-// lane->cell map and the same block_sum tree, and writes out_partials[d] -- so
-// the mass of the output equals the dense kernel's bit for bit.
+// workgroup of QPB x 256 threads covers QPB dense-kernel blocks per tile:
+// lane (q, t) of tile tl is the dense kernel's thread t of block QPB*tl + q,
+// with the same 4 cells, and writes that block's wave partial 4*d + wave, so
+// masses -- and everything else -- are bit-identical to the dense path.  The
+// first tile's codes and belief window are in flight while the dictionary
+// stages; the value window is loaded after the belief update (its registers
+// would not fit beside the belief's); no barrier follows the stores.
 //   rows: dictionary rows in the LDS layout (E x Layout::row floats)
 //   lz:   L_z column of the dictionary (E floats)
 template <bool SPARSE, int QPB, int MINB>
@@ -213,8 +334,24 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   using LY = Layout<SPARSE>;
   extern __shared__ float lds[];
   float* sTC = lds;
-  float* sL = lds + ((E * LY::row + 3) & ~3);
-  float* red = sL + ((E + 3) & ~3);  // one sum per wave
+  float* sL = lds + lds_span(E * LY::row);
+  PP2_PHASE(0);
+  const int q = threadIdx.x / kQuarter, tq = threadIdx.x % kQuarter;
+  const int tpr = g.wp / 4;
+  const int ntiles = (dense_blocks + QPB - 1) / QPB;
+  const int tile0 = xcd_remap(blockIdx.x, gridDim.x);
+  // cell of this lane in tile tl (lanes past the last row read row rows-1)
+#define PP2_CELL(tl, y, x0, ok)                                        \
+  const long long t_ = (long long)(QPB * (tl) + q) * kQuarter + tq;     \
+  int y = (int)(t_ / tpr);                                              \
+  const int x0 = (int)(t_ % tpr) * 4;                                   \
+  const bool ok = y < g.rows;                                           \
+  if (!ok) y = g.rows - 1
+  PP2_CELL(tile0 < ntiles ? tile0 : 0, y, x0, ok);
+  CodeWin6 cw;
+  Win6 bw;
+  load_codes6(code, g.wp, y, x0, cw);
+  load_win6(b_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, bw);
   stage_rows(rows, E * LY::row, sTC);
   stage_rows(lz, E, sL);
   float S = 1.0f;
@@ -236,65 +373,43 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       slot[i] = i;
     }
   }
-  __syncthreads();
-  const int tpr = g.wp / 4;
-  const int q = threadIdx.x / kQuarter, tq = threadIdx.x % kQuarter;
-  const int ntiles = (dense_blocks + QPB - 1) / QPB;
   const int ublk = u * LY::blk;
-  for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
-    const int d = tile * QPB + q;
-    const long long t = (long long)d * kQuarter + tq;
-    const int y = (int)(t / tpr);
-    const int x0 = (int)(t % tpr) * 4;
+  __syncthreads();
+  PP2_PHASE(1);
+  if (tile0 >= ntiles) return;
+  {
+    // compute only on lanes with a cell (a divergent region, as in the dense
+    // kernel); unconditional compute with a guarded store spills heavily
     float local = 0.0f;
-    if (y < g.rows) {
-      const bool le = x0 == 0, re = x0 + 4 == g.wp;
-      CodeWin w;
-      load_codes(code, g.wp, y, x0, w);
-      // ---- belief update: p = L_z * sum_s T[x+off_s][u][8-s] b(x+off_s)
-      float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int s = 0; s < 9; ++s) {
-        const int oy = s / 3 - 1, ox = s % 3 - 1;
-        const float* bp = b_in + (long long)(y + oy) * g.wp + x0 + ox;
-        float bv[4];
-        if (ox == 0) ldv<4, true>(bp, bv);
-        else ldv<4, false>(bp, bv);
-        const int sl = slot[8 - s];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float tv = sl >= 0 ? sTC[w.c[oy + 1][k + 1 + ox] * LY::row + ublk + sl] : 0.0f;
-          float b = bv[k];
-          if (ox < 0 && k == 0 && le) { tv = 0.0f; b = 0.0f; }
-          if (ox > 0 && k == 3 && re) { tv = 0.0f; b = 0.0f; }
-          p[k] = __builtin_fmaf(tv, b, p[k]);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        p[k] = p[k] * sL[w.c[1][k + 1]];
-        p[k] = p[k] * inv;
-        local += p[k];
-      }
-      const long long off = (long long)y * g.wp + x0;
-      stv<4>(b_out + off, p);
-      // ---- Bellman sweep
-      float jn[9][4];
-      load_jn(J_in, g.wp, y, x0, le, re, jn);
-      const uint32_t cc[4] = {w.c[1][1], w.c[1][2], w.c[1][3], w.c[1][4]};
-      float best[4];
-      uint32_t arg[4];
-      coded_sweep4<SPARSE>(sTC, cc, jn, gamma, best, arg);
-      store_ja(J_out, A, off, best, arg);
+    if (ok) {
+      belief_cells<SPARSE>(g, sTC, sL, slot, ublk, inv, cw, bw, y, x0, b_out, local);
+      PP2_PHASE(2);
+      Win6 jw;
+      load_win6(J_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, jw);
+      sweep_cells<SPARSE>(g, sTC, gamma, cw.m0[1], cw.m1[1], jw, y, x0, J_out, A);
+      PP2_PHASE(3);
     }
-    // block_sum per quarter (same tree as the dense kernel's 256-thread block)
-    const float ws = wave_sum(local);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ws;
-    __syncthreads();
-    if (tq == 0 && d < dense_blocks)
-      out_partials[d] = ((red[4 * q] + red[4 * q + 1]) + red[4 * q + 2]) + red[4 * q + 3];
-    __syncthreads();
+    const int d = QPB * tile0 + q;
+    if (d < dense_blocks) write_wave_partial(local, out_partials, d);
   }
+  // ---- further tiles (grids larger than the resident workgroups)
+  for (int tl = tile0 + gridDim.x; tl < ntiles; tl += gridDim.x) {
+    PP2_CELL(tl, yy, xx, okk);
+    float local = 0.0f;
+    if (okk) {
+      CodeWin6 c2;
+      Win6 w2;
+      load_codes6(code, g.wp, yy, xx, c2);
+      load_win6(b_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
+      belief_cells<SPARSE>(g, sTC, sL, slot, ublk, inv, c2, w2, yy, xx, b_out, local);
+      load_win6(J_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
+      sweep_cells<SPARSE>(g, sTC, gamma, c2.m0[1], c2.m1[1], w2, yy, xx, J_out, A);
+    }
+    const int d = QPB * tl + q;
+    if (d < dense_blocks) write_wave_partial(local, out_partials, d);
+  }
+#undef PP2_CELL
+  PP2_PHASE(4);
 }
 
 template <bool SPARSE, int QPB, int MINB>
@@ -305,12 +420,13 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
   using LY = Layout<SPARSE>;
   constexpr int NT = QPB * kQuarter;
   extern __shared__ float lds[];
-  stage_rows(rows, E * LY::row, lds);
-  __syncthreads();
   const int tpr = g.wp / 4;
   const long long nthreads = (long long)g.rows * tpr;
   const int ntiles = (int)((nthreads + NT - 1) / NT);
-  for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
+  int tile = xcd_remap(blockIdx.x, gridDim.x);
+  stage_rows(rows, E * LY::row, lds);
+  __syncthreads();
+  for (; tile < ntiles; tile += gridDim.x) {
     const long long t = (long long)tile * NT + threadIdx.x;
     const int y = (int)(t / tpr);
     const int x0 = (int)(t % tpr) * 4;
@@ -323,7 +439,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
     load_jn(J_in, g.wp, y, x0, le, re, jn);
     float best[4];
     uint32_t arg[4];
-    coded_sweep4<SPARSE>(lds, cc, jn, gamma, best, arg);
+    coded_sweep4<SPARSE, true>(lds, cc, jn, gamma, best, arg);
     store_ja(J_out, A, off, best, arg);
   }
 }
@@ -354,8 +470,7 @@ void allow_lds(const void* fn, bool& done) {
 }  // namespace
 
 size_t coded_loop_lds_bytes(int E, bool sparse) {
-  const size_t rows = ((size_t)E * (sparse ? kSpRow : kDictTC) + 3) & ~(size_t)3;
-  return (rows + (size_t)((E + 3) & ~3) + 16) * sizeof(float);
+  return ((size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) + lds_span(E)) * sizeof(float);
 }
 
 hipError_t launch_dict_hash(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
@@ -394,16 +509,18 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   float* J_out, uint8_t* A) {
   const size_t lds = coded_loop_lds_bytes(E, sparse);
   const int dense_blocks = cells_grid(g, 4);
-#define PP2_LOOPC(SP, Q, MB)                                                                   \
-  do {                                                                                         \
-    if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                              \
-    static bool attr = false;                                                                  \
-    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB>), attr);             \
-    const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                               \
-    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB>), dim3(grid), dim3(Q * kQuarter), lds, st, \
-                       g, gamma, code, rows, lz, E, b_in, b_out, u, in_partials, in_n, in_sum, \
-                       in_sum_out, out_partials, dense_blocks, J_in, J_out, A);                \
+#define PP2_LOOPC(SP, Q, MB)                                                                    \
+  do {                                                                                          \
+    if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                               \
+    static bool attr = false;                                                                   \
+    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB>), attr);              \
+    const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                                \
+    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB>), dim3(grid), dim3(Q * kQuarter), lds, st,  \
+                       g, gamma, code, rows, lz, E, b_in, b_out, u, in_partials, in_n, in_sum,  \
+                       in_sum_out, out_partials, dense_blocks, J_in, J_out, A);                 \
   } while (0)
+  // sparse rows: two 512-thread workgroups per CU (~60 KB LDS each, <= 128
+  // VGPRs, 4 waves per SIMD); full rows: one 1024-thread workgroup per CU
   if (sparse) PP2_LOOPC(true, 2, 2);
   else PP2_LOOPC(false, 4, 1);
 #undef PP2_LOOPC
@@ -413,7 +530,7 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
 hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int E, bool sparse,
                                   const float* J_in, float* J_out, uint8_t* A) {
-  const size_t lds = (((size_t)E * (sparse ? kSpRow : kDictTC) + 3) & ~(size_t)3) * sizeof(float);
+  const size_t lds = (size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) * sizeof(float);
   const long long nthreads = (long long)g.rows * (g.wp / 4);
 #define PP2_SWEEPC(SP, Q, MB)                                                                  \
   do {                                                                                         \
@@ -432,3 +549,10 @@ hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
 }
 
 }  // namespace pp2
+
+#ifdef PP2_PHASE_TRACE
+extern "C" int pp2_debug_phase_trace(unsigned long long* out, int nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pp2::g_phase),
+                             sizeof(unsigned long long) * 8 * nblocks) == hipSuccess ? 0 : 2;
+}
+#endif

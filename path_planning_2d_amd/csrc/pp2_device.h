@@ -100,14 +100,28 @@ __device__ __forceinline__ float block_max(float v, float* lds4) {
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h4u __attribute__((ext_vector_type(4), aligned(2)));
 
-// One wave, lane-strided then xor-butterfly: the same association as
-// wave_reduce_partials in k_loop_step, so a mass finalised here and one
-// reduced inside the next fused step are bit-identical.
+// Belief mass partials are written per wave (4 per 256-cell-thread block,
+// wave order), so no kernel needs a block barrier after its stores.  The
+// consumer folds each block's four as ((w0 + w1) + w2) + w3 -- block_sum's
+// association -- then sums blocks lane-strided and xor-butterflies: the same
+// tree in k_sum_finalize and in every fused step, so a mass finalised
+// separately and one reduced inside a later kernel are bit-identical.
+// n = number of wave partials (a multiple of 4, p 16-B aligned).
 __device__ __forceinline__ float wave_reduce_partials(const float* __restrict__ p, int n) {
   const int lane = threadIdx.x & 63;
   float s = 0.0f;
-  for (int i = lane; i < n; i += 64) s += p[i];
+  for (int i = lane; i < (n >> 2); i += 64) {
+    const f4a w = reinterpret_cast<const f4a*>(p)[i];
+    s += ((w[0] + w[1]) + w[2]) + w[3];
+  }
   return wave_sum(s);
+}
+
+// Per-wave partial of a 256-thread block (or of one 256-thread quarter of a
+// larger workgroup): lane 0 of wave w of the quarter writes p[4*blk + w].
+__device__ __forceinline__ void write_wave_partial(float v, float* __restrict__ p, long long blk) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) p[4 * blk + ((threadIdx.x >> 6) & 3)] = v;
 }
 
 __device__ __forceinline__ int xcd_remap(int b, int n) {

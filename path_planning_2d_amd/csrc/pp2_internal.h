@@ -30,6 +30,8 @@ struct Geom {
 
 // Number of workgroups a per-cell launch uses (256 threads, CPT cells each).
 int cells_grid(const Geom& g, int cpt);
+// Belief-mass partials a belief / loop launch writes: one per wave.
+inline int mass_partials(const Geom& g, int cpt) { return 4 * cells_grid(g, cpt); }
 
 // All launchers are asynchronous on `st`.
 hipError_t launch_model_gen(hipStream_t st, const Geom& g, const uint8_t* map,
@@ -53,8 +55,11 @@ hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
                             int in_n, const float* in_sum, float* in_sum_out,
                             float* out_partials, const float* J_in, float* J_out,
                             uint8_t* A, bool nt);
+// Mass of a belief from its n wave partials (n a multiple of 4).
 hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
                                float* out);
+// out = v[0] + v[1] + ... + v[n-1], in index order.
+hipError_t launch_sum_ordered(hipStream_t st, const float* v, int n, float* out);
 hipError_t launch_fib_sweep(hipStream_t st, const Geom& g, float gamma,
                             PlaneSet T, PlaneSet L, PlaneSet R,
                             PlaneSet a_in, PlaneSet a_out);
@@ -111,7 +116,7 @@ constexpr int kDictL = 90;       // offset of L[16]
 constexpr int kDictTuple = 106;  // floats compared per cell
 constexpr int kDictRow = 108;
 constexpr size_t kDictLdsMaxBytes = 160 * 1024;
-constexpr int kDictMax = 448;  // coded_loop_lds_bytes(kDictMax, false) <= kDictLdsMaxBytes
+constexpr int kDictMax = 440;  // coded_loop_lds_bytes(kDictMax, false) <= kDictLdsMaxBytes
 // Sparse LDS rows: per action a, T at the base kernel's support kSup[a][0 ..
 // kSupN[a]) (base_kernel in pp2_kernels.hip; occupied neighbours and traps
 // only move mass to the centre, which is in every support), then C_a, then 0.

@@ -144,8 +144,7 @@ __global__ __launch_bounds__(kBlock) void k_belief_update(
     Geom g, PlaneSet T, PlaneSet L, const float* __restrict__ b_in,
     float* __restrict__ b_out, int u, int z, const float* __restrict__ in_sum,
     float* __restrict__ partials) {
-  __shared__ float lds4[4];
-  const int tpr = g.wp / CPT;
+    const int tpr = g.wp / CPT;
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const int y = (int)(t / tpr);
   const int x0 = (int)(t % tpr) * CPT;
@@ -185,8 +184,7 @@ __global__ __launch_bounds__(kBlock) void k_belief_update(
     }
     stv<CPT>(b_out + (long long)y * g.wp + x0, p);
   }
-  const float s = block_sum(local, lds4);
-  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+  write_wave_partial(local, partials, blockIdx.x);
 }
 
 hipError_t launch_belief_update(hipStream_t st, const Geom& g, int cpt,
@@ -206,6 +204,19 @@ __global__ __launch_bounds__(64) void k_sum_finalize(const float* __restrict__ p
                                                      int n, float* __restrict__ out) {
   const float s = wave_reduce_partials(partials, n);
   if (threadIdx.x == 0) *out = s;
+}
+
+// Plain sum of n values in index order (the shard masses of a shard group).
+__global__ void k_sum_ordered(const float* __restrict__ v, int n, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  float s = 0.0f;
+  for (int i = 0; i < n; ++i) s += v[i];
+  *out = s;
+}
+
+hipError_t launch_sum_ordered(hipStream_t st, const float* v, int n, float* out) {
+  hipLaunchKernelGGL(k_sum_ordered, dim3(1), dim3(64), 0, st, v, n, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
@@ -324,8 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
     const float* __restrict__ in_partials, int in_n, const float* __restrict__ in_sum,
     float* __restrict__ in_sum_out, float* __restrict__ out_partials,
     const float* __restrict__ J_in, float* __restrict__ J_out, uint8_t* __restrict__ A) {
-  __shared__ float lds4[4];
-  const int tpr = g.wp / CPT;
+    const int tpr = g.wp / CPT;
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const long long t = (long long)blk * kBlock + threadIdx.x;
   const int y = (int)(t / tpr);
@@ -424,8 +434,7 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
       *ap = (uint8_t)arg[0];
     }
   }
-  const float bs = block_sum(local, lds4);
-  if (threadIdx.x == 0) out_partials[blk] = bs;
+  write_wave_partial(local, out_partials, blk);
 }
 
 hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
@@ -550,19 +559,17 @@ hipError_t launch_absdiff_max(hipStream_t st, const Geom& g, int planes,
 
 __global__ __launch_bounds__(kBlock) void k_sum_cells(Geom g, const float* __restrict__ b,
                                                        float* partials) {
-  __shared__ float lds4[4];
-  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const long long n = (long long)g.rows * g.wp;
   const float v = t < n ? b[t] : 0.0f;
-  const float s = block_sum(v, lds4);
-  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+  write_wave_partial(v, partials, blockIdx.x);
 }
 
 hipError_t launch_sum_cells(hipStream_t st, const Geom& g, const float* b,
                             float* partials, int* nparts) {
   const long long n = (long long)g.rows * g.wp;
   const int grid = (int)((n + kBlock - 1) / kBlock);
-  *nparts = grid;
+  *nparts = 4 * grid;
   hipLaunchKernelGGL(k_sum_cells, dim3(grid), dim3(kBlock), 0, st, g, b, partials);
   return hipGetLastError();
 }

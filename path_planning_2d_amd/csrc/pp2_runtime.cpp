@@ -195,7 +195,7 @@ int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
   const float ones[4] = {1.0f, 1.0f, 1.0f, 1.0f};
   if (hipMemcpyAsync(c->bsum, ones, sizeof ones, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return fail(set_err(PP2_EHIP, "bsum init"));
-  c->partials_cap = pp2::cells_grid(c->g, 1) + 1;
+  c->partials_cap = pp2::mass_partials(c->g, 1) + 4;
   if (hipMalloc(&c->pbuf[0], c->partials_cap * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->pbuf[1], c->partials_cap * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->rpartials, c->partials_cap * sizeof(float)) != hipSuccess)
@@ -424,7 +424,7 @@ int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_s
   if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
   CHECK(ensure_mass(c));
   const int bn = c->bcur ^ 1;
-  const int nparts = pp2::cells_grid(c->g, c->cpt);
+  const int nparts = pp2::mass_partials(c->g, c->cpt);
   HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
                                    c->b[c->bcur].v.p, c->b[bn].v.p, u, z,
                                    c->bsum + c->bcur, c->pbuf[bn]));
@@ -441,7 +441,7 @@ int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_s
 int pp2rt::loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass) {
   if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
   const int bc = c->bcur, bn = bc ^ 1, jn = c->jcur ^ 1;
-  const int nparts = pp2::cells_grid(c->g, c->cpt);
+  const int nparts = pp2::mass_partials(c->g, c->cpt);
   const bool pend = c->pending[bc];
   if (coded_active(c)) {
     HIPCHK(pp2::launch_loop_step_coded(c->stream, c->g, c->gamma, c->d_code, c->d_rows,

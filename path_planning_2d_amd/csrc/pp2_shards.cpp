@@ -76,7 +76,7 @@ int combine_mass(pp2_shard_group* g) {
       HIPCHK(hipMemcpyAsync(g->d_gather + r, c->bsum + c->bcur, sizeof(float),
                             hipMemcpyDefault, c0->stream));
     }
-    HIPCHK(pp2::launch_sum_finalize(c0->stream, g->d_gather, n, g->d_gather + n));
+    HIPCHK(pp2::launch_sum_ordered(c0->stream, g->d_gather, n, g->d_gather + n));
     HIPCHK(hipEventRecord(g->ev_total, c0->stream));
   }
   for (int r = 0; r < n; ++r) {

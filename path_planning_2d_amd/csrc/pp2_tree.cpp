@@ -285,7 +285,7 @@ int materialize(pp2_planner* p, VNode* v) {
   HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v, ps.b.v.p,
                                    ns.b.v.p, v->parent->action, v->observation,
                                    ps.mass, p->d_bpart));
-  HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::cells_grid(c->g, c->cpt),
+  HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
                                   ns.mass));
   v->slot = s;
   return PP2_OK;
@@ -472,7 +472,7 @@ int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
   const Slot& ns = p->slots[s];
   HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v, os.b.v.p,
                                    ns.b.v.p, a, z, os.mass, p->d_bpart));
-  HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::cells_grid(c->g, c->cpt),
+  HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
                                   ns.mass));
   VNode* nv = nullptr;
   CHECK(make_root(p, s, 0, &nv));
