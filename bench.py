@@ -47,7 +47,7 @@ BYTES_SWEEP = 369                # per cell: T 324 + C 36 + J 4 + J' 4 + A 1
 BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
 BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
 BYTES_LOOP_CODED = 19            # per cell: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1
-BYTES_SWEEP_CODED = 15           # per cell: code 2 + J 4 + J' 4 + A 1 (+ J halo reuse)
+BYTES_SWEEP_CODED = 11           # per cell: code 2 + J 4 + J' 4 + A 1
 LDS_BYTES_LOOP_CODED = 400       # per cell: T gather 9*4 + L_z 4 + sweep 9*(9+1)*4
 LDS_PEAK_GBS = 150000.0          # ds_read_b64/b128 chip aggregate (MI355X_MICROARCH.md LDS)
 GAMMA = 0.95

@@ -19,10 +19,13 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
-ALGO = {"k_mdp_sweep": 369, "k_belief_update": 48, "k_loop_step": 417}
+# algorithmic HBM bytes per cell (bench.py docstring / DESIGN.md)
+ALGO = {"k_mdp_sweep": 369, "k_belief_update": 48, "k_loop_step": 417,
+        "k_loop_step_coded": 19, "k_mdp_sweep_coded": 11}
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     return name.split("(")[0].replace("void ", "").replace("pp2::", "")
 
 
