@@ -93,6 +93,10 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
 #define PP2_TUNE_CELLS_PER_LANE 1
 #define PP2_TUNE_NT_STREAMS 2
 #define PP2_TUNE_CODED_MODEL 3
+/*  PP2_TUNE_HALO_DEPTH      row shards (RCCL or shard group): loop steps per
+ *                           halo exchange = halo rows exchanged, 1..8
+ *                           (default: the most the smallest shard allows) */
+#define PP2_TUNE_HALO_DEPTH 4
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
 /* ---------------------------------------------------------------- model

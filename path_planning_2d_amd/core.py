@@ -97,6 +97,7 @@ class GridContext:
     TUNE_CELLS_PER_LANE = 1
     TUNE_NT_STREAMS = 2
     TUNE_CODED_MODEL = 3
+    TUNE_HALO_DEPTH = 4
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))
@@ -283,6 +284,11 @@ class ShardGroup:
         for s in self.shards:
             s.fib_reset()
         self.synchronize()
+
+    def set_halo_depth(self, k: int):
+        """Loop steps per halo exchange (= halo rows exchanged), on every shard."""
+        for s in self.shards:
+            s.set_tuning(GridContext.TUNE_HALO_DEPTH, int(k))
 
     def loop_step(self, u, z):
         call("pp2_shard_group_loop_step", self._h, int(u), int(z))

@@ -65,9 +65,9 @@ __global__ __launch_bounds__(kBlock) void k_dict_hash(Geom g, PlaneSet T, PlaneS
                                                       PlaneSet R, PlaneSet L,
                                                       uint64_t* __restrict__ out) {
   const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const long long n = (long long)(g.rows + 2) * g.wp;
+  const long long n = (long long)(g.rows + 2 * g.halo) * g.wp;
   if (i >= n) return;
-  const int y = (int)(i / g.wp) - 1, x = (int)(i % g.wp);
+  const int y = (int)(i / g.wp) - g.halo, x = (int)(i % g.wp);
   uint64_t h = 0x9e3779b97f4a7c15ull;
   for (int k = 0; k < kDictTuple; ++k) {
     const uint32_t w = __float_as_uint(tuple_value(T, C, R, L, y, x, k));
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kBlock) void k_dict_gather(Geom g, PlaneSet T, Plan
   if (i >= E * kDictRow) return;
   const int e = i / kDictRow, k = i % kDictRow;
   const int cell = reps[e];
-  const int y = cell / g.wp - 1, x = cell % g.wp;
+  const int y = cell / g.wp - g.halo, x = cell % g.wp;
   dict[i] = tuple_value(T, C, R, L, y, x, k);
 }
 
@@ -94,9 +94,9 @@ __global__ __launch_bounds__(kBlock) void k_dict_verify(Geom g, PlaneSet T, Plan
                                                         const float* __restrict__ dict,
                                                         int* __restrict__ bad) {
   const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const long long n = (long long)(g.rows + 2) * g.wp;
+  const long long n = (long long)(g.rows + 2 * g.halo) * g.wp;
   if (i >= n) return;
-  const int y = (int)(i / g.wp) - 1, x = (int)(i % g.wp);
+  const int y = (int)(i / g.wp) - g.halo, x = (int)(i % g.wp);
   const float* d = dict + (long long)code[i] * kDictRow;
   int diff = 0;
   for (int k = 0; k < kDictTuple; ++k)
@@ -299,7 +299,7 @@ __device__ __forceinline__ void belief_cells(const Geom& g, const float* sTC, co
 template <bool SPARSE>
 __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, float gamma,
                                             uint32_t m0, uint32_t m1, const Win6& win, int y,
-                                            int x0, float* __restrict__ J_out,
+                                            int x0, bool own, float* __restrict__ J_out,
                                             uint8_t* __restrict__ A) {
   float jn[9][4];
 #pragma unroll
@@ -310,7 +310,10 @@ __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, flo
   float best[4];
   uint32_t arg[4];
   coded_sweep4<SPARSE, true>(sTC, cc, jn, gamma, best, arg);
-  store_ja(J_out, A, (long long)y * g.wp + x0, best, arg);
+  const long long off = (long long)y * g.wp + x0;
+  stv<4>(J_out + off, best);
+  if (own)
+    *reinterpret_cast<uint32_t*>(A + off) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
 }
 
 // Fused north-star step on the coded model (k_loop_step's semantics).  A
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     float* __restrict__ b_out, int u, const float* __restrict__ in_partials, int in_n,
     const float* __restrict__ in_sum, float* __restrict__ in_sum_out,
     float* __restrict__ out_partials, int dense_blocks, const float* __restrict__ J_in,
-    float* __restrict__ J_out, uint8_t* __restrict__ A) {
+    float* __restrict__ J_out, uint8_t* __restrict__ A, int own0, int own1) {
   using LY = Layout<SPARSE>;
   extern __shared__ float lds[];
   float* sTC = lds;
@@ -383,10 +386,12 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     float local = 0.0f;
     if (ok) {
       belief_cells<SPARSE>(g, sTC, sL, slot, ublk, inv, cw, bw, y, x0, b_out, local);
+      const bool own = y >= own0 && y < own1;
+      if (!own) local = 0.0f;
       PP2_PHASE(2);
       Win6 jw;
       load_win6(J_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, jw);
-      sweep_cells<SPARSE>(g, sTC, gamma, cw.m0[1], cw.m1[1], jw, y, x0, J_out, A);
+      sweep_cells<SPARSE>(g, sTC, gamma, cw.m0[1], cw.m1[1], jw, y, x0, own, J_out, A);
       PP2_PHASE(3);
     }
     const int d = QPB * tile0 + q;
@@ -402,8 +407,10 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       load_codes6(code, g.wp, yy, xx, c2);
       load_win6(b_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
       belief_cells<SPARSE>(g, sTC, sL, slot, ublk, inv, c2, w2, yy, xx, b_out, local);
+      const bool own = yy >= own0 && yy < own1;
+      if (!own) local = 0.0f;
       load_win6(J_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
-      sweep_cells<SPARSE>(g, sTC, gamma, c2.m0[1], c2.m1[1], w2, yy, xx, J_out, A);
+      sweep_cells<SPARSE>(g, sTC, gamma, c2.m0[1], c2.m1[1], w2, yy, xx, own, J_out, A);
     }
     const int d = QPB * tl + q;
     if (d < dense_blocks) write_wave_partial(local, out_partials, d);
@@ -475,7 +482,7 @@ size_t coded_loop_lds_bytes(int E, bool sparse) {
 
 hipError_t launch_dict_hash(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
                             PlaneSet L, uint64_t* out) {
-  const long long n = (long long)(g.rows + 2) * g.wp;
+  const long long n = (long long)(g.rows + 2 * g.halo) * g.wp;
   hipLaunchKernelGGL(k_dict_hash, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      st, g, T, C, R, L, out);
   return hipGetLastError();
@@ -491,7 +498,7 @@ hipError_t launch_dict_gather(hipStream_t st, const Geom& g, PlaneSet T, PlaneSe
 
 hipError_t launch_dict_verify(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
                               PlaneSet L, const uint16_t* code_all, const float* dict, int* bad) {
-  const long long n = (long long)(g.rows + 2) * g.wp;
+  const long long n = (long long)(g.rows + 2 * g.halo) * g.wp;
   hipLaunchKernelGGL(k_dict_verify, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      st, g, T, C, R, L, code_all, dict, bad);
   return hipGetLastError();
@@ -506,7 +513,7 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   int E, bool sparse, const float* b_in, float* b_out, int u,
                                   const float* in_partials, int in_n, const float* in_sum,
                                   float* in_sum_out, float* out_partials, const float* J_in,
-                                  float* J_out, uint8_t* A) {
+                                  float* J_out, uint8_t* A, int own0, int own1) {
   const size_t lds = coded_loop_lds_bytes(E, sparse);
   const int dense_blocks = cells_grid(g, 4);
 #define PP2_LOOPC(SP, Q, MB)                                                                    \
@@ -517,7 +524,7 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
     const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                                \
     hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB>), dim3(grid), dim3(Q * kQuarter), lds, st,  \
                        g, gamma, code, rows, lz, E, b_in, b_out, u, in_partials, in_n, in_sum,  \
-                       in_sum_out, out_partials, dense_blocks, J_in, J_out, A);                 \
+                       in_sum_out, out_partials, dense_blocks, J_in, J_out, A, own0, own1);     \
   } while (0)
   // sparse rows: two 512-thread workgroups per CU (~60 KB LDS each, <= 128
   // VGPRs, 4 waves per SIMD); full rows: one 1024-thread workgroup per CU

@@ -26,6 +26,7 @@ struct Geom {
   int wp;          // padded row stride in cells (multiple of 4)
   int row0;        // global index of owned row 0
   int grows;       // global height
+  int halo;        // halo rows above and below the owned rows in every plane
 };
 
 // Number of workgroups a per-cell launch uses (256 threads, CPT cells each).
@@ -48,13 +49,15 @@ hipError_t launch_mdp_sweep(hipStream_t st, const Geom& g, int cpt,
 // Fused north-star step (belief update + Bellman sweep).  The input belief's
 // mass comes from in_partials[0..in_n) (reduced in-kernel) or *in_sum; block
 // 0 stores it to *in_sum_out if non-null.  out_partials gets one partial sum
-// of the output belief per block.
+// of the output belief per wave.  Rows [own0, own1) are the shard's own: only
+// they add to the mass and store actions (the others are recomputed halo rows
+// of an extended-domain launch).
 hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
                             PlaneSet T, PlaneSet L, PlaneSet C, const float* b_in,
                             float* b_out, int u, int z, const float* in_partials,
                             int in_n, const float* in_sum, float* in_sum_out,
                             float* out_partials, const float* J_in, float* J_out,
-                            uint8_t* A, bool nt);
+                            uint8_t* A, bool nt, int own0, int own1);
 // Mass of a belief from its n wave partials (n a multiple of 4).
 hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
                                float* out);
@@ -139,7 +142,8 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   int entries, bool sparse, const float* b_in, float* b_out,
                                   int u, const float* in_partials, int in_n,
                                   const float* in_sum, float* in_sum_out, float* out_partials,
-                                  const float* J_in, float* J_out, uint8_t* A);
+                                  const float* J_in, float* J_out, uint8_t* A, int own0,
+                                  int own1);
 hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int entries,
                                   bool sparse, const float* J_in, float* J_out, uint8_t* A);

@@ -54,8 +54,8 @@ __global__ __launch_bounds__(kBlock) void k_model_gen(
     PlaneSet L, PlaneSet R, PlaneSet C) {
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const int x = (int)(t % g.wp);
-  const int y = (int)(t / g.wp) - 1;  // local row in [-1, rows]
-  if (y > g.rows) return;
+  const int y = (int)(t / g.wp) - g.halo;  // local row in [-halo, rows + halo)
+  if (y >= g.rows + g.halo) return;
   const int ry = g.row0 + y;          // global row
   const bool valid = x < g.width && ry >= 0 && ry < g.grows;
 
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kBlock) void k_model_gen(
 hipError_t launch_model_gen(hipStream_t st, const Geom& g, const uint8_t* map,
                             int gx, int gy, PlaneSet T, PlaneSet L, PlaneSet R,
                             PlaneSet C) {
-  const long long n = (long long)(g.rows + 2) * g.wp;
+  const long long n = (long long)(g.rows + 2 * g.halo) * g.wp;
   const int grid = (int)((n + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(k_model_gen, dim3(grid), dim3(kBlock), 0, st, g, map, gx,
                      gy, T, L, R, C);
@@ -334,8 +334,11 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
     const float* __restrict__ b_in, float* __restrict__ b_out, int u, int z,
     const float* __restrict__ in_partials, int in_n, const float* __restrict__ in_sum,
     float* __restrict__ in_sum_out, float* __restrict__ out_partials,
-    const float* __restrict__ J_in, float* __restrict__ J_out, uint8_t* __restrict__ A) {
-    const int tpr = g.wp / CPT;
+    const float* __restrict__ J_in, float* __restrict__ J_out, uint8_t* __restrict__ A,
+    int own0, int own1) {
+  // rows [own0, own1) are this shard's own: only they add to the belief mass
+  // and store actions (an extended-domain launch also recomputes halo rows)
+  const int tpr = g.wp / CPT;
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const long long t = (long long)blk * kBlock + threadIdx.x;
   const int y = (int)(t / tpr);
@@ -346,6 +349,7 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
   if (in_partials) S = wave_reduce_partials(in_partials, in_n);
   else if (in_sum) S = *in_sum;
   if (in_sum_out && blockIdx.x == 0 && threadIdx.x == 0) *in_sum_out = S;
+  const bool own = y >= own0 && y < own1;
   if (y < g.rows) {
     const bool le = x0 == 0, re = x0 + CPT == g.wp;
     // ---- belief update (k_belief_update)
@@ -378,7 +382,7 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
     for (int k = 0; k < CPT; ++k) {
       p[k] = p[k] * lv[k];
       p[k] = p[k] * inv;
-      local += p[k];
+      if (own) local += p[k];
     }
     stv<CPT>(b_out + (long long)y * g.wp + x0, p);
 
@@ -425,13 +429,15 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
         if (cost[k] < best[k]) { best[k] = cost[k]; arg[k] = (uint32_t)a; }
     }
     stv<CPT>(J_out + (long long)y * g.wp + x0, best);
-    uint8_t* ap = A + (long long)y * g.wp + x0;
-    if constexpr (CPT == 4) {
-      *reinterpret_cast<uint32_t*>(ap) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
-    } else if constexpr (CPT == 2) {
-      *reinterpret_cast<uint16_t*>(ap) = (uint16_t)(arg[0] | (arg[1] << 8));
-    } else {
-      *ap = (uint8_t)arg[0];
+    if (own) {
+      uint8_t* ap = A + (long long)y * g.wp + x0;
+      if constexpr (CPT == 4) {
+        *reinterpret_cast<uint32_t*>(ap) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+      } else if constexpr (CPT == 2) {
+        *reinterpret_cast<uint16_t*>(ap) = (uint16_t)(arg[0] | (arg[1] << 8));
+      } else {
+        *ap = (uint8_t)arg[0];
+      }
     }
   }
   write_wave_partial(local, out_partials, blk);
@@ -442,10 +448,10 @@ hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
                             float* b_out, int u, int z, const float* in_partials,
                             int in_n, const float* in_sum, float* in_sum_out,
                             float* out_partials, const float* J_in, float* J_out,
-                            uint8_t* A, bool nt) {
+                            uint8_t* A, bool nt, int own0, int own1) {
   const int grid = cells_grid(g, cpt);
 #define PP2_LOOP_ARGS g, gamma, T, L, C, b_in, b_out, u, z, in_partials, in_n, in_sum, \
-                      in_sum_out, out_partials, J_in, J_out, A
+                      in_sum_out, out_partials, J_in, J_out, A, own0, own1
   switch (cpt) {
     case 4:
       if (nt) hipLaunchKernelGGL((k_loop_step<4, true>), dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS);

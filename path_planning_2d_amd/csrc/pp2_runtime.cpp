@@ -41,10 +41,10 @@ int set_err(int code, const char* fmt, ...) {
 int alloc_planes(pp2_ctx* c, Planes* P, int K) {
   const long long rs = (long long)K * c->g.wp;
   P->K = K;
-  P->floats = (size_t)(2 * kGuard) + (size_t)(c->g.rows + 2) * rs;
+  P->floats = (size_t)(2 * kGuard) + (size_t)(c->g.rows + 2 * c->g.halo) * rs;
   HIPCHK(hipMalloc(&P->alloc, P->floats * sizeof(float)));
   HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
-  P->v.p = P->alloc + kGuard + rs;  // skip the top halo row
+  P->v.p = P->alloc + kGuard + (long long)c->g.halo * rs;  // skip the top halo rows
   P->v.rs = rs;
   P->v.ps = c->g.wp;
   return PP2_OK;
@@ -87,38 +87,61 @@ const Planes& halo_planes(pp2_ctx* c, HaloKind k) {
   }
 }
 
-// One halo row up and down for each state kind, in one RCCL group
-// (multi-process shards).  Shards of a single-process group exchange through
-// the pp2_shard_group_* drivers instead.
-int exchange_halos(pp2_ctx* c, std::initializer_list<HaloKind> kinds) {
+// Every RCCL operation of a context runs on its comm stream, in host issue
+// order (the same on every rank); comm_enter / comm_leave hand the work over
+// from / back to the compute stream.
+int comm_enter(pp2_ctx* c) {
+  HIPCHK(hipEventRecord(c->ev_enter, c->stream));
+  HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_enter, 0));
+  return PP2_OK;
+}
+
+int comm_leave(pp2_ctx* c) {
+  HIPCHK(hipEventRecord(c->ev_leave, c->comm_stream));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_leave, 0));
+  return PP2_OK;
+}
+
+// k halo rows up and down for each state kind, in one RCCL group
+// (multi-process shards): owned rows [0, k) and [rows-k, rows) go to the
+// neighbours' halo rows [rows, rows+k) and [-k, 0).  Shards of a
+// single-process group exchange through the pp2_shard_group_* drivers.
+int exchange_halos_k(pp2_ctx* c, std::initializer_list<HaloKind> kinds, int k) {
   if (c->group)
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
   if (c->nranks <= 1) return PP2_OK;
   if (!c->comm) return set_err(PP2_ESTATE, "sharded context without RCCL comm");
+  CHECK(comm_enter(c));
   NCCLCHK(ncclGroupStart());
-  for (HaloKind k : kinds) {
-    const Planes* P = &halo_planes(c, k);
+  for (HaloKind kd : kinds) {
+    const Planes* P = &halo_planes(c, kd);
     float* p = P->v.p;
-    const size_t n = (size_t)P->v.rs;
+    const long long rs = P->v.rs;
+    const size_t n = (size_t)k * rs;
     if (c->rank > 0) {
-      NCCLCHK(ncclSend(p, n, ncclFloat, c->rank - 1, c->comm, c->stream));
-      NCCLCHK(ncclRecv(p - P->v.rs, n, ncclFloat, c->rank - 1, c->comm, c->stream));
+      NCCLCHK(ncclSend(p, n, ncclFloat, c->rank - 1, c->comm, c->comm_stream));
+      NCCLCHK(ncclRecv(p - k * rs, n, ncclFloat, c->rank - 1, c->comm, c->comm_stream));
     }
     if (c->rank < c->nranks - 1) {
-      NCCLCHK(ncclSend(p + (long long)(c->g.rows - 1) * P->v.rs, n, ncclFloat,
-                       c->rank + 1, c->comm, c->stream));
-      NCCLCHK(ncclRecv(p + (long long)c->g.rows * P->v.rs, n, ncclFloat,
-                       c->rank + 1, c->comm, c->stream));
+      NCCLCHK(ncclSend(p + (long long)(c->g.rows - k) * rs, n, ncclFloat, c->rank + 1, c->comm,
+                       c->comm_stream));
+      NCCLCHK(ncclRecv(p + (long long)c->g.rows * rs, n, ncclFloat, c->rank + 1, c->comm,
+                       c->comm_stream));
     }
   }
   NCCLCHK(ncclGroupEnd());
-  return PP2_OK;
+  return comm_leave(c);
+}
+
+int exchange_halos(pp2_ctx* c, std::initializer_list<HaloKind> kinds) {
+  return exchange_halos_k(c, kinds, 1);
 }
 
 int allreduce_mass(pp2_ctx* c, float* d) {
   if (c->nranks <= 1) return PP2_OK;
-  NCCLCHK(ncclAllReduce(d, d, 1, ncclFloat, ncclSum, c->comm, c->stream));
-  return PP2_OK;
+  CHECK(comm_enter(c));
+  NCCLCHK(ncclAllReduce(d, d, 1, ncclFloat, ncclSum, c->comm, c->comm_stream));
+  return comm_leave(c);
 }
 
 int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* out);
@@ -129,7 +152,10 @@ int absdiff_max(pp2_ctx* c, const Planes& cur, const Planes& snap, double* out) 
   CHECK(absdiff_local_max(c, cur, snap, &m));
   if (c->nranks > 1) {
     HIPCHK(hipMemcpyAsync(c->rpartials, &m, sizeof(float), hipMemcpyHostToDevice, c->stream));
-    NCCLCHK(ncclAllReduce(c->rpartials, c->rpartials, 1, ncclFloat, ncclMax, c->comm, c->stream));
+    CHECK(comm_enter(c));
+    NCCLCHK(ncclAllReduce(c->rpartials, c->rpartials, 1, ncclFloat, ncclMax, c->comm,
+                          c->comm_stream));
+    CHECK(comm_leave(c));
     HIPCHK(hipMemcpyAsync(&m, c->rpartials, sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
   }
@@ -161,6 +187,7 @@ int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
   c->g.wp = (int)((width + 3u) & ~3u);
   c->g.row0 = (int)row_begin;
   c->g.grows = (int)grows;
+  c->g.halo = (row_end - row_begin == grows) ? 1 : kShardHalo;
   c->gx = gx;
   c->gy = gy;
   c->gamma = gamma;
@@ -195,7 +222,9 @@ int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
   const float ones[4] = {1.0f, 1.0f, 1.0f, 1.0f};
   if (hipMemcpyAsync(c->bsum, ones, sizeof ones, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return fail(set_err(PP2_EHIP, "bsum init"));
-  c->partials_cap = pp2::mass_partials(c->g, 1) + 4;
+  Geom gext = c->g;  // extended-domain loop launches cover rows + 2 halo
+  gext.rows += 2 * gext.halo;
+  c->partials_cap = pp2::mass_partials(gext, 1) + 4;
   if (hipMalloc(&c->pbuf[0], c->partials_cap * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->pbuf[1], c->partials_cap * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->rpartials, c->partials_cap * sizeof(float)) != hipSuccess)
@@ -264,7 +293,8 @@ bool coded_active(const pp2_ctx* c) { return c->use_coded && c->dict_n > 0 && c-
 // collision) leaves dict_n = 0, i.e. the dense kernels.
 int build_model_dict(pp2_ctx* c) {
   c->dict_n = 0;
-  const long long n = (long long)(c->g.rows + 2) * c->g.wp;
+  const long long n = (long long)(c->g.rows + 2 * c->g.halo) * c->g.wp;
+  break_pipeline(c);
   if (!c->code_alloc) {
     if (hipMalloc(&c->code_alloc, (size_t)(n + 2 * kGuard) * sizeof(uint16_t)) != hipSuccess ||
         hipMalloc(&c->d_dict, (size_t)pp2::kDictMax * pp2::kDictRow * sizeof(float)) != hipSuccess ||
@@ -272,7 +302,7 @@ int build_model_dict(pp2_ctx* c) {
         hipMalloc(&c->d_dl, (size_t)pp2::kDictMax * 16 * sizeof(float)) != hipSuccess)
       return set_err(PP2_ENOMEM, "hipMalloc model dictionary");
     HIPCHK(hipMemsetAsync(c->code_alloc, 0, (size_t)(n + 2 * kGuard) * sizeof(uint16_t), c->stream));
-    c->d_code = c->code_alloc + kGuard + c->g.wp;
+    c->d_code = c->code_alloc + kGuard + (long long)c->g.halo * c->g.wp;
   }
   uint64_t* d_hash = nullptr;
   int* d_aux = nullptr;
@@ -370,6 +400,7 @@ int build_model_dict(pp2_ctx* c) {
 
 int mdp_sweep_once(pp2_ctx* c) {
   const int jn = c->jcur ^ 1;
+  break_pipeline(c);  // the deep halo rows of J are stale after a sweep
   if (coded_active(c)) {
     HIPCHK(pp2::launch_mdp_sweep_coded(c->stream, c->g, c->gamma, c->d_code, c->d_rows,
                                        c->dict_n, c->dict_sparse, c->J[c->jcur].v.p,
@@ -411,11 +442,20 @@ int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* 
 using namespace pp2rt;
 
 int pp2rt::ensure_mass(pp2_ctx* c) {
-  if (!c->pending[c->bcur]) return PP2_OK;
-  HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[c->bcur], c->pcount[c->bcur],
-                                  c->bsum + c->bcur));
-  c->pending[c->bcur] = false;
-  return PP2_OK;
+  const int bc = c->bcur;
+  if (c->mass_async[bc]) {
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_mass[bc], 0));
+    c->mass_async[bc] = false;
+  }
+  if (!c->pending[bc]) return PP2_OK;
+  HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bc], c->pcount[bc], c->bsum + bc));
+  c->pending[bc] = false;
+  return allreduce_mass(c, c->bsum + bc);  // global mass (RCCL shards)
+}
+
+void pp2rt::break_pipeline(pp2_ctx* c) {
+  c->kstep = 0;
+  c->lag_ready = false;
 }
 
 // Belief update alone (k_belief_update), mass finalised eagerly.
@@ -423,6 +463,7 @@ int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_s
   if (fuse_with_sweep) return loop_step_fused(c, u, z, true);
   if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
   CHECK(ensure_mass(c));
+  break_pipeline(c);
   const int bn = c->bcur ^ 1;
   const int nparts = pp2::mass_partials(c->g, c->cpt);
   HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
@@ -435,37 +476,98 @@ int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_s
   return PP2_OK;
 }
 
-// One fused north-star step (k_loop_step).  The input mass is reduced inside
-// the kernel when still pending; the output mass stays pending (eager_mass =
-// false) or is finalised (and all-reduced across RCCL shards) right away.
+// One fused north-star step over the owned rows extended by e rows each side
+// (a "view": every plane pointer moves up e rows and the view has rows + 2e
+// rows, so the kernels read the halo rows as ordinary neighbours).  Only the
+// owned rows [e, e + rows) of the view add to the belief mass and store
+// actions.  Reads b[bcur], J[jcur]; writes b[bcur^1], J[jcur^1], A and the new
+// belief's mass partials into pbuf[bcur^1].
+int pp2rt::loop_launch(pp2_ctx* c, int e, uint8_t u, uint8_t z, const float* in_partials,
+                       int in_n, const float* in_sum, float* in_sum_out, int* nparts) {
+  const int bc = c->bcur, bn = bc ^ 1, jc = c->jcur, jn = jc ^ 1;
+  Geom g = c->g;
+  g.rows += 2 * e;
+  g.row0 -= e;
+  g.halo -= e;
+  const long long wp = g.wp;
+  auto up = [e](PlaneSet P) {
+    P.p -= (long long)e * P.rs;
+    return P;
+  };
+  const float* b_in = c->b[bc].v.p - e * wp;
+  float* b_out = c->b[bn].v.p - e * wp;
+  const float* J_in = c->J[jc].v.p - e * wp;
+  float* J_out = c->J[jn].v.p - e * wp;
+  uint8_t* A = c->A - e * wp;  // only owned rows are stored
+  if (coded_active(c)) {
+    HIPCHK(pp2::launch_loop_step_coded(c->stream, g, c->gamma, c->d_code - e * wp, c->d_rows,
+                                       c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3),
+                                       c->dict_n, c->dict_sparse, b_in, b_out, u, in_partials,
+                                       in_n, in_sum, in_sum_out, c->pbuf[bn], J_in, J_out, A,
+                                       e, e + c->g.rows));
+    *nparts = pp2::mass_partials(g, 4);
+  } else {
+    HIPCHK(pp2::launch_loop_step(c->stream, g, c->cpt, c->gamma, up(c->T.v), up(c->L.v),
+                                 up(c->C.v), b_in, b_out, u, z, in_partials, in_n, in_sum,
+                                 in_sum_out, c->pbuf[bn], J_in, J_out, A, c->nt_streams, e,
+                                 e + c->g.rows));
+    *nparts = pp2::mass_partials(g, c->cpt);
+  }
+  return PP2_OK;
+}
+
+// One fused north-star step of an unsharded context (k_loop_step).  The input
+// mass is reduced inside the kernel when still pending; the output mass stays
+// pending (eager_mass = false) or is finalised right away.
 int pp2rt::loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass) {
   if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
   const int bc = c->bcur, bn = bc ^ 1, jn = c->jcur ^ 1;
-  const int nparts = pp2::mass_partials(c->g, c->cpt);
   const bool pend = c->pending[bc];
-  if (coded_active(c)) {
-    HIPCHK(pp2::launch_loop_step_coded(c->stream, c->g, c->gamma, c->d_code, c->d_rows,
-                                       c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3), c->dict_n,
-                                       c->dict_sparse, c->b[bc].v.p, c->b[bn].v.p, u,
-                                       pend ? c->pbuf[bc] : nullptr, c->pcount[bc],
-                                       c->bsum + bc, pend ? c->bsum + bc : nullptr,
-                                       c->pbuf[bn], c->J[c->jcur].v.p, c->J[jn].v.p, c->A));
-  } else {
-    HIPCHK(pp2::launch_loop_step(c->stream, c->g, c->cpt, c->gamma, c->T.v, c->L.v, c->C.v,
-                                 c->b[bc].v.p, c->b[bn].v.p, u, z,
-                                 pend ? c->pbuf[bc] : nullptr, c->pcount[bc],
-                                 c->bsum + bc, pend ? c->bsum + bc : nullptr, c->pbuf[bn],
-                                 c->J[c->jcur].v.p, c->J[jn].v.p, c->A, c->nt_streams));
-  }
+  int nparts = 0;
+  CHECK(loop_launch(c, 0, u, z, pend ? c->pbuf[bc] : nullptr, c->pcount[bc], c->bsum + bc,
+                    pend ? c->bsum + bc : nullptr, &nparts));
   c->pending[bc] = false;
   c->pcount[bn] = nparts;
   c->pending[bn] = true;
   c->bcur = bn;
   c->jcur = jn;
-  if (eager_mass || c->nranks > 1) {
+  if (eager_mass) CHECK(ensure_mass(c));
+  return PP2_OK;
+}
+
+// One loop step of an RCCL row shard.  Every kdepth steps the
+// halo rows of b and J are refreshed kdepth rows deep; in between each step
+// recomputes a view one row narrower, so no exchange is needed.  The belief
+// is normalised by the global mass of the belief one step earlier, whose
+// all-reduce ran on the comm stream during the previous step; the new
+// belief's local mass is all-reduced the same way.
+static int sharded_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
+  if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  const int bc = c->bcur, bn = bc ^ 1, jn = c->jcur ^ 1;
+  if (c->kstep == 0) CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, c->kdepth));
+  const float* norm;
+  if (c->lag_ready) {
+    if (c->mass_async[bn]) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_mass[bn], 0));
+    c->mass_async[bn] = false;
+    norm = c->bsum + bn;
+  } else {
     CHECK(ensure_mass(c));
-    CHECK(allreduce_mass(c, c->bsum + bn));
+    norm = c->bsum + bc;
   }
+  int nparts = 0;
+  CHECK(loop_launch(c, c->kdepth - 1 - c->kstep, u, z, nullptr, 0, norm, nullptr, &nparts));
+  HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bn], nparts, c->bsum + bn));
+  HIPCHK(hipEventRecord(c->ev_local, c->stream));
+  HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_local, 0));
+  NCCLCHK(ncclAllReduce(c->bsum + bn, c->bsum + bn, 1, ncclFloat, ncclSum, c->comm,
+                        c->comm_stream));
+  HIPCHK(hipEventRecord(c->ev_mass[bn], c->comm_stream));
+  c->mass_async[bn] = true;
+  c->pending[bc] = c->pending[bn] = false;
+  c->bcur = bn;
+  c->jcur = jn;
+  c->lag_ready = true;
+  c->kstep = (c->kstep + 1) % c->kdepth;
   return PP2_OK;
 }
 
@@ -514,7 +616,11 @@ int pp2_destroy(pp2_ctx* c) {
   DeviceGuard dg(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  for (hipEvent_t e : {c->ev_enter, c->ev_leave, c->ev_local, c->ev_mass[0], c->ev_mass[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
   for (Planes* P : {&c->T, &c->L, &c->R, &c->C, &c->b[0], &c->b[1], &c->J[0],
                     &c->J[1], &c->Jsnap, &c->fib[0], &c->fib[1], &c->fibsnap})
     free_planes(P);
@@ -542,6 +648,7 @@ int pp2_set_stream(pp2_ctx* c, void* s) {
 int pp2_synchronize(pp2_ctx* c) {
   CHECK(check_ctx(c));
   DeviceGuard dg(c->device);
+  if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return PP2_OK;
 }
@@ -562,6 +669,12 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
     case PP2_TUNE_CODED_MODEL: c->use_coded = value != 0; return PP2_OK;
+    case PP2_TUNE_HALO_DEPTH:
+      if (value < 1 || value > c->kdepth_max)
+        return set_err(PP2_EINVAL, "halo depth %d not in [1, %d]", value, c->kdepth_max);
+      c->kdepth = value;
+      break_pipeline(c);
+      return PP2_OK;
     default: return set_err(PP2_EINVAL, "unknown tuning key %d", key);
   }
 }
@@ -645,6 +758,10 @@ int pp2_belief_set(pp2_ctx* c, const float* b) {
   CHECK(check_ctx(c));
   if (!b) return set_err(PP2_EINVAL, "belief is null");
   DeviceGuard dg(c->device);
+  // an all-reduce still in flight may target either mass slot
+  if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
+  c->mass_async[0] = c->mass_async[1] = false;
+  break_pipeline(c);
   CHECK(upload_planes(c, c->b[c->bcur], b));
   c->pending[c->bcur] = false;
   const float one = 1.0f;
@@ -694,6 +811,7 @@ int pp2_mdp_reset(pp2_ctx* c) {
     HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
   HIPCHK(hipMemsetAsync(c->A, 0, (size_t)c->g.rows * c->g.wp, c->stream));
   c->jcur = 0;
+  break_pipeline(c);
   return PP2_OK;
 }
 
@@ -745,7 +863,9 @@ int pp2_mdp_get(pp2_ctx* c, float* J, uint8_t* A) {
 int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   CHECK(check_model(c));
   DeviceGuard dg(c->device);
-  CHECK(exchange_halos(c, {HALO_BELIEF, HALO_VALUE}));
+  if (c->group)
+    return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
+  if (c->nranks > 1) return sharded_loop_step(c, u, z);
   return loop_step_fused(c, u, z, false);
 }
 
@@ -826,9 +946,28 @@ int pp2_shard_comm_init(pp2_ctx* c, const uint8_t id[PP2_RCCL_ID_BYTES],
   DeviceGuard dg(c->device);
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof uid);
+  if (!c->comm_stream) {
+    HIPCHK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&c->ev_enter, &c->ev_leave, &c->ev_local, &c->ev_mass[0], &c->ev_mass[1]})
+      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
   NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
   c->nranks = nranks;
   c->rank = rank;
+  // loop halo depth: no deeper than the halo allocation or any shard's rows
+  int* d = nullptr;
+  int rows = c->g.rows;
+  HIPCHK(hipMalloc(&d, sizeof(int)));
+  HIPCHK(hipMemcpyAsync(d, &rows, sizeof(int), hipMemcpyHostToDevice, c->stream));
+  CHECK(comm_enter(c));
+  NCCLCHK(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, c->comm_stream));
+  CHECK(comm_leave(c));
+  HIPCHK(hipMemcpyAsync(&rows, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipFree(d));
+  c->kdepth_max = std::max(1, std::min(c->g.halo, rows));
+  c->kdepth = c->kdepth_max;
+  break_pipeline(c);
   return PP2_OK;
 }
 

@@ -36,22 +36,24 @@ int wait_neighbours(pp2_shard_group* g) {
   return PP2_OK;
 }
 
-int exchange_local(pp2_shard_group* g, std::initializer_list<HaloKind> kinds) {
+// k halo rows per side: the neighbours' owned rows [rows-k, rows) / [0, k)
+// into this shard's halo rows [-k, 0) / [rows, rows+k).
+int exchange_local(pp2_shard_group* g, std::initializer_list<HaloKind> kinds, int k = 1) {
   const int n = (int)g->ctx.size();
   for (int r = 0; r < n; ++r) {
     pp2_ctx* c = g->ctx[r];
     DeviceGuard dg(c->device);
-    for (HaloKind k : kinds) {
-      const Planes& P = halo_planes(c, k);
-      const size_t bytes = (size_t)P.v.rs * sizeof(float);
+    for (HaloKind kd : kinds) {
+      const Planes& P = halo_planes(c, kd);
+      const size_t bytes = (size_t)k * P.v.rs * sizeof(float);
       if (r > 0) {
         pp2_ctx* up = g->ctx[r - 1];
-        const Planes& Q = halo_planes(up, k);
-        HIPCHK(hipMemcpyAsync(P.v.p - P.v.rs, Q.v.p + (long long)(up->g.rows - 1) * Q.v.rs,
+        const Planes& Q = halo_planes(up, kd);
+        HIPCHK(hipMemcpyAsync(P.v.p - k * P.v.rs, Q.v.p + (long long)(up->g.rows - k) * Q.v.rs,
                               bytes, hipMemcpyDefault, c->stream));
       }
       if (r < n - 1) {
-        const Planes& Q = halo_planes(g->ctx[r + 1], k);
+        const Planes& Q = halo_planes(g->ctx[r + 1], kd);
         HIPCHK(hipMemcpyAsync(P.v.p + (long long)c->g.rows * P.v.rs, Q.v.p, bytes,
                               hipMemcpyDefault, c->stream));
       }
@@ -159,9 +161,14 @@ int pp2_shard_group_create(pp2_shard_group** out, pp2_ctx* const* ctxs, int n) {
         hipMalloc(&g->d_gather, (n + 1) * sizeof(float)) != hipSuccess)
       return fail(set_err(PP2_ENOMEM, "shard group scratch"));
   }
+  int min_rows = ctxs[0]->g.rows;
+  for (int r = 0; r < n; ++r) min_rows = std::min(min_rows, ctxs[r]->g.rows);
   for (int r = 0; r < n; ++r) {
     ctxs[r]->group = g;
     ctxs[r]->grank = r;
+    ctxs[r]->kdepth_max = std::max(1, std::min(ctxs[r]->g.halo, min_rows));
+    ctxs[r]->kdepth = ctxs[r]->kdepth_max;
+    break_pipeline(ctxs[r]);
   }
   *out = g;
   return PP2_OK;
@@ -194,13 +201,32 @@ int pp2_shard_group_synchronize(pp2_shard_group* g) {
   return PP2_OK;
 }
 
+// The RCCL row-shard loop step (pp2_runtime.cpp sharded_loop_step) with
+// device copies as the transport: kdepth-deep halo rows every kdepth steps,
+// views one row narrower in between, each step normalised by the global mass
+// of the belief one step earlier.
 int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z) {
   CHECK(check_group(g));
+  if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  pp2_ctx* c0 = g->ctx[0];
+  for (pp2_ctx* c : g->ctx)
+    if (c->kdepth != c0->kdepth || c->kstep != c0->kstep || c->lag_ready != c0->lag_ready)
+      return set_err(PP2_ESTATE, "shards of the group are out of step (halo depth differs?)");
+  const int K = c0->kdepth;
   CHECK(wait_neighbours(g));
-  CHECK(exchange_local(g, {HALO_BELIEF, HALO_VALUE}));
+  if (c0->kstep == 0) CHECK(exchange_local(g, {HALO_BELIEF, HALO_VALUE}, K));
   for (pp2_ctx* c : g->ctx) {
     DeviceGuard dg(c->device);
-    CHECK(belief_update_impl(c, u, z, true));
+    const int bc = c->bcur, bn = bc ^ 1;
+    const float* norm = c->lag_ready ? c->bsum + bn : c->bsum + bc;
+    int nparts = 0;
+    CHECK(loop_launch(c, K - 1 - c->kstep, u, z, nullptr, 0, norm, nullptr, &nparts));
+    HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bn], nparts, c->bsum + bn));
+    c->pending[bc] = c->pending[bn] = false;
+    c->bcur = bn;
+    c->jcur ^= 1;
+    c->lag_ready = true;
+    c->kstep = (c->kstep + 1) % K;
   }
   CHECK(combine_mass(g));
   return mark_done(g);

@@ -93,6 +93,56 @@ def test_shards_mdp_solve_and_fib():
         np.testing.assert_array_equal(got, ref.fib_get())
 
 
+@pytest.mark.parametrize("depth", [1, 3, 8])
+def test_shards_halo_depths(depth):
+    """Loop steps with halo rows exchanged `depth` deep every `depth` steps
+    (extended-domain views in between) and the lagged belief normalisation,
+    interleaved with belief-only and sweep-only steps that restart the
+    pipeline, against the unsharded grid."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    name = "sparse_map_100x40"
+    grid = golden_map(name)
+    goal = tuple(golden("model", name)["goal"])
+    us, zs, _ = S.synth_trajectory(grid, 40, seed=9)
+    b0 = S.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            P.ShardGroup(grid, goal, (0, 13, 27, 40), gamma=float(GAMMA)) as grp:
+        ref.model_generate()
+        grp.model_generate()
+        grp.set_halo_depth(depth)
+        for c in (ref, grp):
+            c.belief_set(b0)
+            c.mdp_reset()
+        k = 0
+        for phase in (17, 5, 11):
+            for _ in range(phase):
+                ref.loop_step(us[k], zs[k])
+                grp.loop_step(us[k], zs[k])
+                k += 1
+            np.testing.assert_array_equal(grp.mdp_get()[0], ref.mdp_get()[0])
+            np.testing.assert_array_equal(grp.mdp_get()[1], ref.mdp_get()[1])
+            assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5,
+                             msg=f"belief after {k} steps, depth {depth}")
+            ref.belief_update(us[k], zs[k])
+            grp.belief_update(us[k], zs[k])
+            k += 1
+            ref.mdp_sweep(2)
+            grp.mdp_sweep(2)
+
+
+def test_halo_depth_bounds():
+    import path_planning_2d_amd as P
+    grid = golden_map("map_10x10")
+    with P.ShardGroup(grid, (8, 7), (0, 3, 10)) as grp:
+        with pytest.raises(P.Pp2Error):
+            grp.set_halo_depth(4)  # the 3-row shard cannot feed 4 halo rows
+        grp.set_halo_depth(3)
+    with P.GridContext(grid, (8, 7)) as ctx:
+        with pytest.raises(P.Pp2Error):
+            ctx.set_tuning(ctx.TUNE_HALO_DEPTH, 2)  # unsharded: depth 1 only
+
+
 def test_grouped_context_rejects_per_context_stepping():
     import path_planning_2d_amd as P
     grid = golden_map("map_10x10")
