@@ -333,7 +333,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     float* __restrict__ b_out, int u, const float* __restrict__ in_partials, int in_n,
     const float* __restrict__ in_sum, float* __restrict__ in_sum_out,
     float* __restrict__ out_partials, int dense_blocks, const float* __restrict__ J_in,
-    float* __restrict__ J_out, uint8_t* __restrict__ A, int own0, int own1) {
+    float* __restrict__ J_out, uint8_t* __restrict__ A, int own0, int own1, float scale) {
   using LY = Layout<SPARSE>;
   extern __shared__ float lds[];
   float* sTC = lds;
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   if (in_partials) S = wave_reduce_partials(in_partials, in_n);
   else if (in_sum) S = *in_sum;
   if (in_sum_out && blockIdx.x == 0 && threadIdx.x == 0) *in_sum_out = S;
-  const float inv = 1.0f / S;
+  const float inv = (1.0f / S) * scale;  // scale: a power of two (1 unsharded)
   // belief gather: LDS slot of T[.][u][i] inside the action-u block, or -1
   // when i is outside u's support on the sparse layout (T == 0 there)
   int slot[9];
@@ -513,7 +513,7 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   int E, bool sparse, const float* b_in, float* b_out, int u,
                                   const float* in_partials, int in_n, const float* in_sum,
                                   float* in_sum_out, float* out_partials, const float* J_in,
-                                  float* J_out, uint8_t* A, int own0, int own1) {
+                                  float* J_out, uint8_t* A, int own0, int own1, float scale) {
   const size_t lds = coded_loop_lds_bytes(E, sparse);
   const int dense_blocks = cells_grid(g, 4);
 #define PP2_LOOPC(SP, Q, MB)                                                                    \
@@ -524,7 +524,7 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
     const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                                \
     hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB>), dim3(grid), dim3(Q * kQuarter), lds, st,  \
                        g, gamma, code, rows, lz, E, b_in, b_out, u, in_partials, in_n, in_sum,  \
-                       in_sum_out, out_partials, dense_blocks, J_in, J_out, A, own0, own1);     \
+                       in_sum_out, out_partials, dense_blocks, J_in, J_out, A, own0, own1, scale); \
   } while (0)
   // sparse rows: two 512-thread workgroups per CU (~60 KB LDS each, <= 128
   // VGPRs, 4 waves per SIMD); full rows: one 1024-thread workgroup per CU

@@ -41,6 +41,11 @@ int set_err(int code, const char* fmt, ...);
 
 constexpr int kGuard = 64;  // floats of guard before/after each plane set
 constexpr int kShardHalo = 8;  // halo rows allocated per side in row-sharded contexts
+// Row-shard loop blocks start by dividing the belief by its global mass and
+// multiplying by 2^64 (exact), then divide by 1: the stored belief stays far
+// above the flush-to-zero range while it decays by < kdepth observation
+// probabilities inside a block.  Reads divide by the true mass.
+constexpr float kBlockScale = 18446744073709551616.0f;  // 2^64
 
 // A set of K planes over rows [-1, rows] (one halo row each side).
 struct Planes {
@@ -93,20 +98,16 @@ struct pp2_ctx {
   void* staging = nullptr;     // dense host-layout staging buffer
   size_t staging_bytes = 0;
 
-  // Row-sharded loop pipeline: halo rows are exchanged kdepth
-  // rows deep every kdepth loop steps, and each step is normalised by the
-  // global mass of the belief one step earlier, all-reduced asynchronously.
+  // Row-sharded loop blocks: halo rows are exchanged kdepth
+  // rows deep every kdepth loop steps; only a block's first step normalises.
   int kdepth = 1;          // loop halo depth in use
   int kdepth_max = 1;      // min(g.halo, the smallest shard's rows)
   int kstep = 0;           // loop step within the current halo block
-  bool lag_ready = false;  // bsum[bcur ^ 1] = global mass of the belief before b[bcur]
-  bool mass_async[2] = {false, false};  // bsum[i] set by an all-reduce still in flight
 
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   hipStream_t comm_stream = nullptr;  // every RCCL operation of the context, in issue order
-  hipEvent_t ev_enter = nullptr, ev_leave = nullptr, ev_local = nullptr;
-  hipEvent_t ev_mass[2] = {nullptr, nullptr};
+  hipEvent_t ev_enter = nullptr, ev_leave = nullptr;
   pp2_shard_group* group = nullptr;  // single-process shard group, if any
   int grank = 0;                     // rank (row-block order) inside the group
 };
@@ -138,7 +139,7 @@ void break_pipeline(pp2_ctx* c);
 // One fused step over the owned rows extended by e rows each side (partials
 // of the new belief into pbuf[bcur ^ 1]; *nparts = their count).
 int loop_launch(pp2_ctx* c, int e, uint8_t u, uint8_t z, const float* in_partials, int in_n,
-                const float* in_sum, float* in_sum_out, int* nparts);
+                const float* in_sum, float* in_sum_out, int* nparts, float scale = 1.0f);
 int mdp_sweep_once(pp2_ctx* c);
 int build_model_dict(pp2_ctx* c);
 bool coded_active(const pp2_ctx* c);

@@ -51,13 +51,14 @@ hipError_t launch_mdp_sweep(hipStream_t st, const Geom& g, int cpt,
 // 0 stores it to *in_sum_out if non-null.  out_partials gets one partial sum
 // of the output belief per wave.  Rows [own0, own1) are the shard's own: only
 // they add to the mass and store actions (the others are recomputed halo rows
-// of an extended-domain launch).
+// of an extended-domain launch).  The new belief is scaled by scale / mass
+// (scale a power of two, 1 except at the start of a row-shard loop block).
 hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
                             PlaneSet T, PlaneSet L, PlaneSet C, const float* b_in,
                             float* b_out, int u, int z, const float* in_partials,
                             int in_n, const float* in_sum, float* in_sum_out,
                             float* out_partials, const float* J_in, float* J_out,
-                            uint8_t* A, bool nt, int own0, int own1);
+                            uint8_t* A, bool nt, int own0, int own1, float scale = 1.0f);
 // Mass of a belief from its n wave partials (n a multiple of 4).
 hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
                                float* out);
@@ -143,7 +144,7 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   int u, const float* in_partials, int in_n,
                                   const float* in_sum, float* in_sum_out, float* out_partials,
                                   const float* J_in, float* J_out, uint8_t* A, int own0,
-                                  int own1);
+                                  int own1, float scale = 1.0f);
 hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int entries,
                                   bool sparse, const float* J_in, float* J_out, uint8_t* A);

@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
     const float* __restrict__ in_partials, int in_n, const float* __restrict__ in_sum,
     float* __restrict__ in_sum_out, float* __restrict__ out_partials,
     const float* __restrict__ J_in, float* __restrict__ J_out, uint8_t* __restrict__ A,
-    int own0, int own1) {
+    int own0, int own1, float scale) {
   // rows [own0, own1) are this shard's own: only they add to the belief mass
   // and store actions (an extended-domain launch also recomputes halo rows)
   const int tpr = g.wp / CPT;
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void k_loop_step(
     }
     float lv[CPT];
     ldv<CPT, true>(L.p + (long long)y * L.rs + (long long)z * L.ps + x0, lv);
-    const float inv = 1.0f / S;
+    const float inv = (1.0f / S) * scale;  // scale: a power of two (1 unsharded)
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       p[k] = p[k] * lv[k];
@@ -448,10 +448,10 @@ hipError_t launch_loop_step(hipStream_t st, const Geom& g, int cpt, float gamma,
                             float* b_out, int u, int z, const float* in_partials,
                             int in_n, const float* in_sum, float* in_sum_out,
                             float* out_partials, const float* J_in, float* J_out,
-                            uint8_t* A, bool nt, int own0, int own1) {
+                            uint8_t* A, bool nt, int own0, int own1, float scale) {
   const int grid = cells_grid(g, cpt);
 #define PP2_LOOP_ARGS g, gamma, T, L, C, b_in, b_out, u, z, in_partials, in_n, in_sum, \
-                      in_sum_out, out_partials, J_in, J_out, A, own0, own1
+                      in_sum_out, out_partials, J_in, J_out, A, own0, own1, scale
   switch (cpt) {
     case 4:
       if (nt) hipLaunchKernelGGL((k_loop_step<4, true>), dim3(grid), dim3(kBlock), 0, st, PP2_LOOP_ARGS);

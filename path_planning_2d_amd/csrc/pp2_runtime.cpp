@@ -109,8 +109,10 @@ int comm_leave(pp2_ctx* c) {
 int exchange_halos_k(pp2_ctx* c, std::initializer_list<HaloKind> kinds, int k) {
   if (c->group)
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
-  if (c->nranks <= 1) return PP2_OK;
-  if (!c->comm) return set_err(PP2_ESTATE, "sharded context without RCCL comm");
+  if (!c->comm) {
+    if (c->nranks > 1) return set_err(PP2_ESTATE, "sharded context without RCCL comm");
+    return PP2_OK;
+  }
   CHECK(comm_enter(c));
   NCCLCHK(ncclGroupStart());
   for (HaloKind kd : kinds) {
@@ -138,7 +140,7 @@ int exchange_halos(pp2_ctx* c, std::initializer_list<HaloKind> kinds) {
 }
 
 int allreduce_mass(pp2_ctx* c, float* d) {
-  if (c->nranks <= 1) return PP2_OK;
+  if (!c->comm) return PP2_OK;
   CHECK(comm_enter(c));
   NCCLCHK(ncclAllReduce(d, d, 1, ncclFloat, ncclSum, c->comm, c->comm_stream));
   return comm_leave(c);
@@ -165,7 +167,7 @@ int absdiff_max(pp2_ctx* c, const Planes& cur, const Planes& snap, double* out) 
 
 int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
                 uint32_t row_begin, uint32_t row_end, const uint8_t* map,
-                int32_t gx, int32_t gy, float gamma) {
+                int32_t gx, int32_t gy, float gamma, bool shard) {
   if (!out) return set_err(PP2_EINVAL, "out is null");
   *out = nullptr;
   if (!map) return set_err(PP2_EINVAL, "map is null");
@@ -187,7 +189,7 @@ int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
   c->g.wp = (int)((width + 3u) & ~3u);
   c->g.row0 = (int)row_begin;
   c->g.grows = (int)grows;
-  c->g.halo = (row_end - row_begin == grows) ? 1 : kShardHalo;
+  c->g.halo = shard ? kShardHalo : 1;  // shards: room for deep halo exchanges
   c->gx = gx;
   c->gy = gy;
   c->gamma = gamma;
@@ -443,20 +445,13 @@ using namespace pp2rt;
 
 int pp2rt::ensure_mass(pp2_ctx* c) {
   const int bc = c->bcur;
-  if (c->mass_async[bc]) {
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_mass[bc], 0));
-    c->mass_async[bc] = false;
-  }
   if (!c->pending[bc]) return PP2_OK;
   HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bc], c->pcount[bc], c->bsum + bc));
   c->pending[bc] = false;
   return allreduce_mass(c, c->bsum + bc);  // global mass (RCCL shards)
 }
 
-void pp2rt::break_pipeline(pp2_ctx* c) {
-  c->kstep = 0;
-  c->lag_ready = false;
-}
+void pp2rt::break_pipeline(pp2_ctx* c) { c->kstep = 0; }
 
 // Belief update alone (k_belief_update), mass finalised eagerly.
 int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep) {
@@ -483,7 +478,8 @@ int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_s
 // actions.  Reads b[bcur], J[jcur]; writes b[bcur^1], J[jcur^1], A and the new
 // belief's mass partials into pbuf[bcur^1].
 int pp2rt::loop_launch(pp2_ctx* c, int e, uint8_t u, uint8_t z, const float* in_partials,
-                       int in_n, const float* in_sum, float* in_sum_out, int* nparts) {
+                       int in_n, const float* in_sum, float* in_sum_out, int* nparts,
+                       float scale) {
   const int bc = c->bcur, bn = bc ^ 1, jc = c->jcur, jn = jc ^ 1;
   Geom g = c->g;
   g.rows += 2 * e;
@@ -504,13 +500,13 @@ int pp2rt::loop_launch(pp2_ctx* c, int e, uint8_t u, uint8_t z, const float* in_
                                        c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3),
                                        c->dict_n, c->dict_sparse, b_in, b_out, u, in_partials,
                                        in_n, in_sum, in_sum_out, c->pbuf[bn], J_in, J_out, A,
-                                       e, e + c->g.rows));
+                                       e, e + c->g.rows, scale));
     *nparts = pp2::mass_partials(g, 4);
   } else {
     HIPCHK(pp2::launch_loop_step(c->stream, g, c->cpt, c->gamma, up(c->T.v), up(c->L.v),
                                  up(c->C.v), b_in, b_out, u, z, in_partials, in_n, in_sum,
                                  in_sum_out, c->pbuf[bn], J_in, J_out, A, c->nt_streams, e,
-                                 e + c->g.rows));
+                                 e + c->g.rows, scale));
     *nparts = pp2::mass_partials(g, c->cpt);
   }
   return PP2_OK;
@@ -535,38 +531,30 @@ int pp2rt::loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass) {
   return PP2_OK;
 }
 
-// One loop step of an RCCL row shard.  Every kdepth steps the
-// halo rows of b and J are refreshed kdepth rows deep; in between each step
-// recomputes a view one row narrower, so no exchange is needed.  The belief
-// is normalised by the global mass of the belief one step earlier, whose
-// all-reduce ran on the comm stream during the previous step; the new
-// belief's local mass is all-reduced the same way.
+// One loop step of an RCCL row shard.  Steps come in blocks
+// of kdepth.  A block starts by finalising the exact global mass of the
+// current belief (one all-reduce) and refreshing the halo rows of b and J
+// kdepth rows deep (one RCCL group); its first step divides by that mass
+// (times 2^64, exact) and the others by 1.  Step i computes a view
+// kdepth-1-i rows wider than the owned rows per side, so nothing crosses
+// ranks until the next block.
 static int sharded_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
   const int bc = c->bcur, bn = bc ^ 1, jn = c->jcur ^ 1;
-  if (c->kstep == 0) CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, c->kdepth));
-  const float* norm;
-  if (c->lag_ready) {
-    if (c->mass_async[bn]) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_mass[bn], 0));
-    c->mass_async[bn] = false;
-    norm = c->bsum + bn;
-  } else {
+  const bool start = c->kstep == 0;
+  if (start) {
     CHECK(ensure_mass(c));
-    norm = c->bsum + bc;
+    CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, c->kdepth));
   }
   int nparts = 0;
-  CHECK(loop_launch(c, c->kdepth - 1 - c->kstep, u, z, nullptr, 0, norm, nullptr, &nparts));
-  HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bn], nparts, c->bsum + bn));
-  HIPCHK(hipEventRecord(c->ev_local, c->stream));
-  HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_local, 0));
-  NCCLCHK(ncclAllReduce(c->bsum + bn, c->bsum + bn, 1, ncclFloat, ncclSum, c->comm,
-                        c->comm_stream));
-  HIPCHK(hipEventRecord(c->ev_mass[bn], c->comm_stream));
-  c->mass_async[bn] = true;
-  c->pending[bc] = c->pending[bn] = false;
+  CHECK(loop_launch(c, c->kdepth - 1 - c->kstep, u, z, nullptr, 0,
+                    start ? c->bsum + bc : nullptr, nullptr, &nparts,
+                    start ? kBlockScale : 1.0f));
+  c->pending[bc] = false;
+  c->pcount[bn] = nparts;
+  c->pending[bn] = true;
   c->bcur = bn;
   c->jcur = jn;
-  c->lag_ready = true;
   c->kstep = (c->kstep + 1) % c->kdepth;
   return PP2_OK;
 }
@@ -600,7 +588,7 @@ int pp2_device_count(int* count) {
 
 int pp2_create(pp2_ctx** out, int device, uint32_t height, uint32_t width,
                const uint8_t* map, int32_t gx, int32_t gy, float gamma) {
-  return create_impl(out, device, height, width, 0, height, map, gx, gy, gamma);
+  return create_impl(out, device, height, width, 0, height, map, gx, gy, gamma, false);
 }
 
 int pp2_create_shard(pp2_ctx** out, int device, uint32_t global_height,
@@ -608,7 +596,7 @@ int pp2_create_shard(pp2_ctx** out, int device, uint32_t global_height,
                      const uint8_t* global_map, int32_t gx, int32_t gy,
                      float gamma) {
   return create_impl(out, device, global_height, width, row_begin, row_end,
-                     global_map, gx, gy, gamma);
+                     global_map, gx, gy, gamma, true);
 }
 
 int pp2_destroy(pp2_ctx* c) {
@@ -618,7 +606,7 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  for (hipEvent_t e : {c->ev_enter, c->ev_leave, c->ev_local, c->ev_mass[0], c->ev_mass[1]})
+  for (hipEvent_t e : {c->ev_enter, c->ev_leave})
     if (e) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
   for (Planes* P : {&c->T, &c->L, &c->R, &c->C, &c->b[0], &c->b[1], &c->J[0],
@@ -758,9 +746,6 @@ int pp2_belief_set(pp2_ctx* c, const float* b) {
   CHECK(check_ctx(c));
   if (!b) return set_err(PP2_EINVAL, "belief is null");
   DeviceGuard dg(c->device);
-  // an all-reduce still in flight may target either mass slot
-  if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
-  c->mass_async[0] = c->mass_async[1] = false;
   break_pipeline(c);
   CHECK(upload_planes(c, c->b[c->bcur], b));
   c->pending[c->bcur] = false;
@@ -865,7 +850,7 @@ int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   DeviceGuard dg(c->device);
   if (c->group)
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
-  if (c->nranks > 1) return sharded_loop_step(c, u, z);
+  if (c->comm) return sharded_loop_step(c, u, z);  // RCCL shard (any rank count)
   return loop_step_fused(c, u, z, false);
 }
 
@@ -948,7 +933,7 @@ int pp2_shard_comm_init(pp2_ctx* c, const uint8_t id[PP2_RCCL_ID_BYTES],
   memcpy(&uid, id, sizeof uid);
   if (!c->comm_stream) {
     HIPCHK(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&c->ev_enter, &c->ev_leave, &c->ev_local, &c->ev_mass[0], &c->ev_mass[1]})
+    for (hipEvent_t* e : {&c->ev_enter, &c->ev_leave})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));

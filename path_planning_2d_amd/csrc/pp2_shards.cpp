@@ -202,30 +202,32 @@ int pp2_shard_group_synchronize(pp2_shard_group* g) {
 }
 
 // The RCCL row-shard loop step (pp2_runtime.cpp sharded_loop_step) with
-// device copies as the transport: kdepth-deep halo rows every kdepth steps,
-// views one row narrower in between, each step normalised by the global mass
-// of the belief one step earlier.
+// device copies as the transport: a block starts by refreshing the halo rows
+// of b and J kdepth rows deep, and its first step divides by the global mass
+// (times 2^64) and the others by 1; step i computes a view kdepth-1-i rows
+// wider per side.  (The group also combines the mass after every step, so a
+// shard's bsum always holds the global mass for reads.)
 int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z) {
   CHECK(check_group(g));
   if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
   pp2_ctx* c0 = g->ctx[0];
   for (pp2_ctx* c : g->ctx)
-    if (c->kdepth != c0->kdepth || c->kstep != c0->kstep || c->lag_ready != c0->lag_ready)
+    if (c->kdepth != c0->kdepth || c->kstep != c0->kstep)
       return set_err(PP2_ESTATE, "shards of the group are out of step (halo depth differs?)");
   const int K = c0->kdepth;
   CHECK(wait_neighbours(g));
-  if (c0->kstep == 0) CHECK(exchange_local(g, {HALO_BELIEF, HALO_VALUE}, K));
+  const bool start = c0->kstep == 0;
+  if (start) CHECK(exchange_local(g, {HALO_BELIEF, HALO_VALUE}, K));
   for (pp2_ctx* c : g->ctx) {
     DeviceGuard dg(c->device);
     const int bc = c->bcur, bn = bc ^ 1;
-    const float* norm = c->lag_ready ? c->bsum + bn : c->bsum + bc;
     int nparts = 0;
-    CHECK(loop_launch(c, K - 1 - c->kstep, u, z, nullptr, 0, norm, nullptr, &nparts));
+    CHECK(loop_launch(c, K - 1 - c->kstep, u, z, nullptr, 0, start ? c->bsum + bc : nullptr,
+                      nullptr, &nparts, start ? kBlockScale : 1.0f));
     HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bn], nparts, c->bsum + bn));
     c->pending[bc] = c->pending[bn] = false;
     c->bcur = bn;
     c->jcur ^= 1;
-    c->lag_ready = true;
     c->kstep = (c->kstep + 1) % K;
   }
   CHECK(combine_mass(g));

@@ -11,6 +11,8 @@ import pytest
 
 from conftest import GAMMA, assert_rel_close, golden, golden_map
 
+FTZ_FLOOR = 1e-30  # see the module docstring
+
 pytestmark = pytest.mark.gpu
 
 
@@ -33,12 +35,12 @@ def run_pair(P, grid, goal, bounds, steps, seed=42):
         Jg, Ag = grp.mdp_get()
         np.testing.assert_array_equal(Jg, Jr)
         np.testing.assert_array_equal(Ag, Ar)
-        assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5,
+        assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
                          msg="sharded belief")
         # belief-only and sweep-only drivers
         ref.belief_update(us[0], zs[0])
         grp.belief_update(us[0], zs[0])
-        assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5,
+        assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
                          msg="sharded belief update")
         ref.mdp_sweep(3)
         grp.mdp_sweep(3)
@@ -122,7 +124,7 @@ def test_shards_halo_depths(depth):
                 k += 1
             np.testing.assert_array_equal(grp.mdp_get()[0], ref.mdp_get()[0])
             np.testing.assert_array_equal(grp.mdp_get()[1], ref.mdp_get()[1])
-            assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5,
+            assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
                              msg=f"belief after {k} steps, depth {depth}")
             ref.belief_update(us[k], zs[k])
             grp.belief_update(us[k], zs[k])
@@ -150,3 +152,42 @@ def test_grouped_context_rejects_per_context_stepping():
         grp.model_generate()
         with pytest.raises(P.Pp2Error):
             grp.shards[0].loop_step(0, 0)
+
+
+def test_rccl_single_rank_pipeline():
+    """The RCCL shard path on one GPU: a full-grid shard context with a
+    1-rank communicator runs the sharded loop pipeline -- comm stream, events,
+    asynchronous all-reduce of the mass, lagged normalisation, 8-deep
+    extended-domain views (neighbour transfers aside, which need 2 GPUs)."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    name = "sparse_map_100x40"
+    grid = golden_map(name)
+    goal = tuple(golden("model", name)["goal"])
+    H = grid.shape[0]
+    us, zs, _ = S.synth_trajectory(grid, 40, seed=5)
+    b0 = S.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            P.GridContext(grid, goal, gamma=float(GAMMA), rows=(0, H)) as sh:
+        sh.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
+        for c in (ref, sh):
+            c.model_generate()
+            c.belief_set(b0)
+            c.mdp_reset()
+        k = 0
+        for phase in (13, 8):
+            for _ in range(phase):
+                ref.loop_step(us[k], zs[k])
+                sh.loop_step(us[k], zs[k])
+                k += 1
+            np.testing.assert_array_equal(sh.mdp_get()[0], ref.mdp_get()[0])
+            np.testing.assert_array_equal(sh.mdp_get()[1], ref.mdp_get()[1])
+            assert_rel_close(sh.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
+                             msg=f"belief after {k} steps")
+            ref.belief_update(us[k], zs[k])
+            sh.belief_update(us[k], zs[k])
+            k += 1
+            ref.mdp_sweep(3)
+            sh.mdp_sweep(3)
+        assert ref.mdp_solve() == sh.mdp_solve()
+        np.testing.assert_array_equal(sh.mdp_get()[0], ref.mdp_get()[0])
