@@ -55,6 +55,8 @@ def lib():
             "orc_sum_f64": (D, [S, _f32p]),
             "orc_mdp_sweep": (None, [I, I, F, _f32p, _f32p, _f32p, _f32p, _u8p]),
             "orc_mdp_sweep_rows": (None, [I, I, F, _f32p, _f32p, _f32p, _f32p, _u8p, I, I]),
+            "orc_loop_run_mt": (I, [I, I, F, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
+                                    _u8p, I, _u8p, _u8p, I]),
             "orc_mdp_solve": (I, [I, I, F, _f32p, _f32p, _f32p, _u8p, I, C.POINTER(D)]),
             "orc_fib_sweep": (None, [I, I, F, _f32p, _f32p, _f32p, _f32p, _f32p]),
             "orc_fib_solve": (I, [I, I, F, _f32p, _f32p, _f32p, _f32p, I, C.POINTER(F)]),

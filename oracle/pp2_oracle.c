@@ -11,6 +11,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -235,6 +236,66 @@ void orc_mdp_sweep_rows(int H, int W, float gamma, const float* T,
 void orc_mdp_sweep(int H, int W, float gamma, const float* T, const float* C,
                    const float* J_in, float* J_out, uint8_t* A) {
   orc_mdp_sweep_rows(H, W, gamma, T, C, J_in, J_out, A, 0, H);
+}
+
+/* ---- CPU baseline: loop steps row-partitioned over threads ---------------- */
+/* The north-star loop step (belief update, renormalisation, Bellman sweep)
+ * with the rows of every phase split across nthreads pthreads -- the
+ * "std::thread row-partitioned" CPU mode of SURVEY.md §8(d).  Per-thread
+ * partial sums are combined in thread order.  Timing baseline only. */
+typedef struct {
+  int H, W, y0, y1, u, z, phase;
+  float gamma, inv;
+  const float *T, *L, *C, *b, *J;
+  float *bo, *Jo, sum;
+  uint8_t* A;
+} orc_loop_job;
+
+static void* orc_loop_worker(void* arg) {
+  orc_loop_job* j = (orc_loop_job*)arg;
+  if (j->phase == 0) {
+    orc_belief_update_rows(j->H, j->W, j->T, j->L, j->b, j->u, j->z, j->bo, 1, j->y0, j->y1);
+    orc_mdp_sweep_rows(j->H, j->W, j->gamma, j->T, j->C, j->J, j->Jo, j->A, j->y0, j->y1);
+    float s = 0.0f;
+    for (size_t i = (size_t)j->y0 * j->W; i < (size_t)j->y1 * j->W; ++i) s = s + j->bo[i];
+    j->sum = s;
+  } else {
+    for (size_t i = (size_t)j->y0 * j->W; i < (size_t)j->y1 * j->W; ++i) j->bo[i] *= j->inv;
+  }
+  return NULL;
+}
+
+int orc_loop_run_mt(int H, int W, float gamma, const float* T, const float* L, const float* C,
+                    float* b, float* bo, float* J, float* Jo, uint8_t* A, int nsteps,
+                    const uint8_t* us, const uint8_t* zs, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  if (nthreads > H) nthreads = H;
+  pthread_t th[256];
+  orc_loop_job job[256];
+  for (int step = 0; step < nsteps; ++step) {
+    for (int phase = 0; phase < 2; ++phase) {
+      float inv = 0.0f;
+      if (phase == 1) {
+        float s = 0.0f;
+        for (int t = 0; t < nthreads; ++t) s = s + job[t].sum;
+        inv = 1.0f / s;
+      }
+      for (int t = 0; t < nthreads; ++t) {
+        orc_loop_job* j = &job[t];
+        j->H = H; j->W = W; j->u = us[step]; j->z = zs[step]; j->phase = phase;
+        j->y0 = (int)((long long)H * t / nthreads);
+        j->y1 = (int)((long long)H * (t + 1) / nthreads);
+        j->gamma = gamma; j->inv = inv;
+        j->T = T; j->L = L; j->C = C; j->b = b; j->J = J; j->bo = bo; j->Jo = Jo; j->A = A;
+        if (pthread_create(&th[t], NULL, orc_loop_worker, j) != 0) return -1;
+      }
+      for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    }
+    float* tb = b; b = bo; bo = tb;
+    float* tj = J; J = Jo; Jo = tj;
+  }
+  return nsteps;
 }
 
 int orc_mdp_solve(int H, int W, float gamma, const float* T, const float* C,

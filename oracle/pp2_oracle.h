@@ -67,6 +67,10 @@ float orc_sum_seq(size_t n, const float* b);
 /* cudaOneStepValueIteration: src/mdp/path_planning_2d_cuda.cu:215-264 */
 void orc_mdp_sweep(int H, int W, float gamma, const float* T, const float* C,
                    const float* J_in, float* J_out, uint8_t* A);
+/* CPU baseline: nsteps loop steps, rows split over nthreads pthreads. */
+int orc_loop_run_mt(int H, int W, float gamma, const float* T, const float* L, const float* C,
+                    float* b, float* bo, float* J, float* Jo, uint8_t* A, int nsteps,
+                    const uint8_t* us, const uint8_t* zs, int nthreads);
 void orc_mdp_sweep_rows(int H, int W, float gamma, const float* T,
                         const float* C, const float* J_in, float* J_out,
                         uint8_t* A, int y0, int y1);

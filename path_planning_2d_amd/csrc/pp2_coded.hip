@@ -106,10 +106,13 @@ __global__ __launch_bounds__(kBlock) void k_dict_verify(Geom g, PlaneSet T, Plan
 
 // ---------------------------------------------------------------- kernels
 // Two LDS row layouts per dictionary entry:
-//  * full   (kDictTC = 90 floats): [a][T_a0..T_a8, C_a];
-//  * sparse (kSpRow = 54 floats):  [a][T_a at kSup[a][0..3], C_a, 0] -- only
+//  * full   (kDictTC = 90 floats): [a][gT_a0..gT_a8, C_a];
+//  * sparse (kSpRow = 54 floats):  [a][gT_a at kSup[a][0..3], C_a, 0] -- only
 //    the base-kernel support of each action (at most 4 cells; the host checks
 //    every other T entry of every row is +0.0 before choosing it).
+// gT = fl(gamma * T), rounded once on the host exactly as the dense sweep
+// rounds gamma * T per cell (one fp32 multiply, round to nearest).  The belief
+// gather reads raw T from a per-action table (tu: E x 4 sparse / E x 9 full).
 // Sparse Bellman rows skip the T == 0 terms: fmaf(gamma*0, J, cost) == cost
 // for the finite, non-negative J and cost of the MDP (J starts at 0, C >= 0),
 // so values and actions stay bit-identical to the dense kernel.
@@ -117,6 +120,7 @@ template <bool SPARSE>
 struct Layout {
   static constexpr int row = SPARSE ? kSpRow : kDictTC;
   static constexpr int blk = SPARSE ? 6 : 10;  // floats per action block
+  static constexpr int tu = SPARSE ? 4 : 9;    // raw T_u floats per entry (belief gather)
 };
 
 // Global -> LDS copy of n floats with LDS-DMA (global_load_lds_dwordx4: no
@@ -165,7 +169,7 @@ __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&
         float cost = cz[0];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (j < kSupN[a]) cost = __builtin_fmaf(gamma * tv[j], jn[kSup[a][j]][k], cost);
+          if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);
         if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
         if (CELL_GRAIN) __builtin_amdgcn_sched_barrier(0);
       }
@@ -183,7 +187,7 @@ __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&
         const float tv[9] = {t01[0], t01[1], t23[0], t23[1], t45[0], t45[1], t67[0], t67[1], t8c[0]};
         float cost = t8c[1];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) cost = __builtin_fmaf(gamma * tv[i], jn[i][k], cost);
+        for (int i = 0; i < 9; ++i) cost = __builtin_fmaf(tv[i], jn[i][k], cost);
         if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
       }
     }
@@ -265,8 +269,8 @@ __device__ __forceinline__ void load_codes6(const uint16_t* __restrict__ code, i
 
 // The two halves of a coded fused step for one lane's 4 cells.
 template <bool SPARSE>
-__device__ __forceinline__ void belief_cells(const Geom& g, const float* sTC, const float* sL,
-                                             const int (&slot)[9], int ublk, float inv,
+__device__ __forceinline__ void belief_cells(const Geom& g, const float* sTu, const float* sL,
+                                             const int (&slot)[9], float inv,
                                              const CodeWin6& cw, const Win6& win, int y, int x0,
                                              float* __restrict__ b_out, float& local) {
   using LY = Layout<SPARSE>;
@@ -279,7 +283,7 @@ __device__ __forceinline__ void belief_cells(const Geom& g, const float* sTC, co
     const int sl = slot[8 - s];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float tv = sl >= 0 ? sTC[cw.at(oy, k + 1 + ox) * LY::row + ublk + sl] : 0.0f;
+      float tv = sl >= 0 ? sTu[cw.at(oy, k + 1 + ox) * LY::tu + sl] : 0.0f;
       if (ox < 0 && k == 0 && lx) tv = 0.0f;
       if (ox > 0 && k == 3 && rx) tv = 0.0f;
       p[k] = __builtin_fmaf(tv, win.v[oy][k + 1 + ox], p[k]);
@@ -329,8 +333,9 @@ __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, flo
 template <bool SPARSE, int QPB, int MINB>
 __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
-    const float* __restrict__ lz, int E, const float* __restrict__ b_in,
-    float* __restrict__ b_out, int u, const float* __restrict__ in_partials, int in_n,
+    const float* __restrict__ lz, const float* __restrict__ tu, int E,
+    const float* __restrict__ b_in, float* __restrict__ b_out, int u,
+    const float* __restrict__ in_partials, int in_n,
     const float* __restrict__ in_sum, float* __restrict__ in_sum_out,
     float* __restrict__ out_partials, int dense_blocks, const float* __restrict__ J_in,
     float* __restrict__ J_out, uint8_t* __restrict__ A, int own0, int own1, float scale) {
@@ -338,6 +343,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   extern __shared__ float lds[];
   float* sTC = lds;
   float* sL = lds + lds_span(E * LY::row);
+  float* sTu = sL + lds_span(E);
   PP2_PHASE(0);
   const int q = threadIdx.x / kQuarter, tq = threadIdx.x % kQuarter;
   const int tpr = g.wp / 4;
@@ -357,6 +363,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   load_win6(b_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, bw);
   stage_rows(rows, E * LY::row, sTC);
   stage_rows(lz, E, sL);
+  stage_rows(tu, E * LY::tu, sTu);
   float S = 1.0f;
   if (in_partials) S = wave_reduce_partials(in_partials, in_n);
   else if (in_sum) S = *in_sum;
@@ -376,7 +383,6 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       slot[i] = i;
     }
   }
-  const int ublk = u * LY::blk;
   __syncthreads();
   PP2_PHASE(1);
   if (tile0 >= ntiles) return;
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     // kernel); unconditional compute with a guarded store spills heavily
     float local = 0.0f;
     if (ok) {
-      belief_cells<SPARSE>(g, sTC, sL, slot, ublk, inv, cw, bw, y, x0, b_out, local);
+      belief_cells<SPARSE>(g, sTu, sL, slot, inv, cw, bw, y, x0, b_out, local);
       const bool own = y >= own0 && y < own1;
       if (!own) local = 0.0f;
       PP2_PHASE(2);
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       Win6 w2;
       load_codes6(code, g.wp, yy, xx, c2);
       load_win6(b_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
-      belief_cells<SPARSE>(g, sTC, sL, slot, ublk, inv, c2, w2, yy, xx, b_out, local);
+      belief_cells<SPARSE>(g, sTu, sL, slot, inv, c2, w2, yy, xx, b_out, local);
       const bool own = yy >= own0 && yy < own1;
       if (!own) local = 0.0f;
       load_win6(J_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
@@ -477,7 +483,8 @@ void allow_lds(const void* fn, bool& done) {
 }  // namespace
 
 size_t coded_loop_lds_bytes(int E, bool sparse) {
-  return ((size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) + lds_span(E)) * sizeof(float);
+  return ((size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) + lds_span(E) +
+          lds_span(E * (sparse ? 4 : 9))) * sizeof(float);
 }
 
 hipError_t launch_dict_hash(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
@@ -510,7 +517,7 @@ hipError_t launch_dict_verify(hipStream_t st, const Geom& g, PlaneSet T, PlaneSe
 // SIMD); full rows (up to ~160 KB LDS) one 1024-thread workgroup per CU.
 hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, const float* lz,
-                                  int E, bool sparse, const float* b_in, float* b_out, int u,
+                                  const float* tu, int E, bool sparse, const float* b_in, float* b_out, int u,
                                   const float* in_partials, int in_n, const float* in_sum,
                                   float* in_sum_out, float* out_partials, const float* J_in,
                                   float* J_out, uint8_t* A, int own0, int own1, float scale) {
@@ -523,8 +530,9 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
     allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB>), attr);              \
     const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                                \
     hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB>), dim3(grid), dim3(Q * kQuarter), lds, st,  \
-                       g, gamma, code, rows, lz, E, b_in, b_out, u, in_partials, in_n, in_sum,  \
-                       in_sum_out, out_partials, dense_blocks, J_in, J_out, A, own0, own1, scale); \
+                       g, gamma, code, rows, lz, tu, E, b_in, b_out, u, in_partials, in_n,      \
+                       in_sum, in_sum_out, out_partials, dense_blocks, J_in, J_out, A, own0,    \
+                       own1, scale);                                                            \
   } while (0)
   // sparse rows: two 512-thread workgroups per CU (~60 KB LDS each, <= 128
   // VGPRs, 4 waves per SIMD); full rows: one 1024-thread workgroup per CU

@@ -90,8 +90,9 @@ struct pp2_ctx {
   uint16_t* code_alloc = nullptr;  // code plane allocation (guards + rows -1..rows)
   uint16_t* d_code = nullptr;      // code plane at (row 0, x 0)
   float* d_dict = nullptr;         // kDictMax * kDictRow floats
-  float* d_rows = nullptr;         // LDS-layout rows (sparse: kSpRow, else kDictTC floats)
+  float* d_rows = nullptr;         // LDS-layout rows, gamma*T (sparse: kSpRow, else kDictTC)
   float* d_dl = nullptr;           // L transposed: [z][entry]
+  float* d_tu = nullptr;           // raw T per action: [u][entry][4 sparse | 9 full]
   int dict_n = 0;                  // entries; 0 = no dictionary (dense path only)
   bool dict_sparse = false;        // every T row is zero off the base-kernel support
   bool use_coded = true;           // PP2_TUNE_CODED_MODEL

@@ -120,7 +120,7 @@ constexpr int kDictL = 90;       // offset of L[16]
 constexpr int kDictTuple = 106;  // floats compared per cell
 constexpr int kDictRow = 108;
 constexpr size_t kDictLdsMaxBytes = 160 * 1024;
-constexpr int kDictMax = 440;  // coded_loop_lds_bytes(kDictMax, false) <= kDictLdsMaxBytes
+constexpr int kDictMax = 400;  // coded_loop_lds_bytes(kDictMax, false) <= kDictLdsMaxBytes
 // Sparse LDS rows: per action a, T at the base kernel's support kSup[a][0 ..
 // kSupN[a]) (base_kernel in pp2_kernels.hip; occupied neighbours and traps
 // only move mass to the centre, which is in every support), then C_a, then 0.
@@ -136,11 +136,12 @@ hipError_t launch_dict_gather(hipStream_t st, const Geom& g, PlaneSet T, PlaneSe
 hipError_t launch_dict_verify(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
                               PlaneSet L, const uint16_t* code_all, const float* dict, int* bad);
 // code = code plane at (row 0, x 0); rows = LDS-layout dictionary rows (E x
-// kSpRow if sparse else E x kDictTC); lz = the L_z column (E floats).  Same
-// contract as launch_loop_step (cpt 4).
+// kSpRow if sparse else E x kDictTC, T entries pre-multiplied by gamma); lz =
+// the L_z column (E floats); tu = raw T of action u per entry (E x 4 sparse,
+// E x 9 full).  Same contract as launch_loop_step (cpt 4).
 hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, const float* lz,
-                                  int entries, bool sparse, const float* b_in, float* b_out,
+                                  const float* tu, int entries, bool sparse, const float* b_in, float* b_out,
                                   int u, const float* in_partials, int in_n,
                                   const float* in_sum, float* in_sum_out, float* out_partials,
                                   const float* J_in, float* J_out, uint8_t* A, int own0,

@@ -301,7 +301,8 @@ int build_model_dict(pp2_ctx* c) {
     if (hipMalloc(&c->code_alloc, (size_t)(n + 2 * kGuard) * sizeof(uint16_t)) != hipSuccess ||
         hipMalloc(&c->d_dict, (size_t)pp2::kDictMax * pp2::kDictRow * sizeof(float)) != hipSuccess ||
         hipMalloc(&c->d_rows, ((size_t)pp2::kDictMax * pp2::kDictTC + 4) * sizeof(float)) != hipSuccess ||
-        hipMalloc(&c->d_dl, (size_t)pp2::kDictMax * 16 * sizeof(float)) != hipSuccess)
+        hipMalloc(&c->d_dl, (size_t)pp2::kDictMax * 16 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&c->d_tu, ((size_t)9 * pp2::kDictMax * 9 + 4) * sizeof(float)) != hipSuccess)
       return set_err(PP2_ENOMEM, "hipMalloc model dictionary");
     HIPCHK(hipMemsetAsync(c->code_alloc, 0, (size_t)(n + 2 * kGuard) * sizeof(uint16_t), c->stream));
     c->d_code = c->code_alloc + kGuard + (long long)c->g.halo * c->g.wp;
@@ -375,24 +376,38 @@ int build_model_dict(pp2_ctx* c) {
         if (!in && bits != 0) { sparse = false; break; }
       }
   const int rw = sparse ? pp2::kSpRow : pp2::kDictTC;
+  const int tw = sparse ? 4 : 9;
   const int es = (E + 3) & ~3;  // L_z column stride (16-B aligned columns)
   std::vector<float> rows((size_t)E * rw + 4, 0.0f), dl((size_t)16 * es, 0.0f);
+  const size_t tstride = ((size_t)E * tw + 3) & ~(size_t)3;  // 16-B aligned per action
+  std::vector<float> tu(9 * tstride, 0.0f);
+  const float gam = c->gamma;
   for (int e = 0; e < E; ++e) {
     const float* src = &dh[(size_t)e * pp2::kDictRow];
     float* dst = &rows[(size_t)e * rw];
-    if (sparse) {
-      for (int a = 0; a < 9; ++a) {
-        for (int j = 0; j < pp2::kSupN[a]; ++j) dst[a * 6 + j] = src[a * 10 + pp2::kSup[a][j]];
+    for (int a = 0; a < 9; ++a) {
+      // sweep rows hold fl(gamma * T) (the dense sweep's per-cell product)
+      if (sparse) {
+        for (int j = 0; j < pp2::kSupN[a]; ++j) dst[a * 6 + j] = gam * src[a * 10 + pp2::kSup[a][j]];
         dst[a * 6 + 4] = src[a * 10 + 9];
+      } else {
+        for (int i = 0; i < 9; ++i) dst[a * 10 + i] = gam * src[a * 10 + i];
+        dst[a * 10 + 9] = src[a * 10 + 9];
       }
-    } else {
-      std::memcpy(dst, src, pp2::kDictTC * sizeof(float));
+      // belief gather: raw T of action a
+      float* t = &tu[a * tstride + (size_t)e * tw];
+      if (sparse)
+        for (int j = 0; j < pp2::kSupN[a]; ++j) t[j] = src[a * 10 + pp2::kSup[a][j]];
+      else
+        for (int i = 0; i < 9; ++i) t[i] = src[a * 10 + i];
     }
     for (int z = 0; z < 16; ++z) dl[(size_t)z * es + e] = src[pp2::kDictL + z];
   }
   HIPCHK(hipMemcpyAsync(c->d_rows, rows.data(), rows.size() * sizeof(float),
                         hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_dl, dl.data(), dl.size() * sizeof(float), hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_tu, tu.data(), tu.size() * sizeof(float), hipMemcpyHostToDevice,
                         c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->dict_sparse = sparse;
@@ -498,6 +513,7 @@ int pp2rt::loop_launch(pp2_ctx* c, int e, uint8_t u, uint8_t z, const float* in_
   if (coded_active(c)) {
     HIPCHK(pp2::launch_loop_step_coded(c->stream, g, c->gamma, c->d_code - e * wp, c->d_rows,
                                        c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3),
+                                       c->d_tu + (size_t)u * (((size_t)c->dict_n * (c->dict_sparse ? 4 : 9) + 3) & ~(size_t)3),
                                        c->dict_n, c->dict_sparse, b_in, b_out, u, in_partials,
                                        in_n, in_sum, in_sum_out, c->pbuf[bn], J_in, J_out, A,
                                        e, e + c->g.rows, scale));
@@ -620,7 +636,7 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->rpartials) (void)hipFree(c->rpartials);
   if (c->staging) (void)hipFree(c->staging);
   if (c->code_alloc) (void)hipFree(c->code_alloc);
-  for (float* p : {c->d_dict, c->d_rows, c->d_dl})
+  for (float* p : {c->d_dict, c->d_rows, c->d_dl, c->d_tu})
     if (p) (void)hipFree(p);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;

@@ -206,3 +206,37 @@ def test_oracle_planner_runs(oracle):
     assert info["n_root_children"] == 9
     assert v == max(info["q_upper_bound"])
     assert a == int(np.argmax(info["q_upper_bound"]))
+
+
+def test_loop_run_mt_matches_sequence(oracle):
+    """The threaded CPU-baseline loop (rows split over threads) = the
+    single-thread oracle step sequence: values/actions bit-exact, beliefs to
+    rel 1e-5 (it scales by 1/sum instead of dividing)."""
+    import numpy as np
+    from conftest import GAMMA, assert_rel_close, golden_map
+    from path_planning_2d_amd import synthetic as S
+    grid = golden_map("sparse_map_100x40")
+    H, W = grid.shape
+    goal = S.synth_goal(grid)
+    T, L, _ = oracle.model_pomdp(grid, goal)
+    _, Cc = oracle.model_mdp(grid, goal)
+    us, zs, _ = S.synth_trajectory(grid, 6, seed=3)
+    b0 = S.uniform_belief(grid)
+    lib = oracle.lib()
+    b = b0.copy()
+    J = np.zeros(H * W, np.float32)
+    for k in range(6):
+        b = oracle.belief_update(H, W, T, L, b, int(us[k]), int(zs[k]))
+        b = (b / np.float32(b.sum(dtype=np.float32))).astype(np.float32)
+        J, A = oracle.mdp_sweep(H, W, GAMMA, T, Cc, J)
+    bm, bo = b0.copy(), np.empty_like(b0)
+    Jm, Jo = np.zeros(H * W, np.float32), np.empty(H * W, np.float32)
+    Am = np.zeros(H * W, np.uint8)
+    n = lib.orc_loop_run_mt(H, W, np.float32(GAMMA), T, L, Cc, bm, bo, Jm, Jo, Am, 6,
+                            np.ascontiguousarray(us[:6], np.uint8),
+                            np.ascontiguousarray(zs[:6], np.uint8), 4)
+    assert n == 6
+    # 6 steps = even number of swaps: results are back in the first buffers
+    np.testing.assert_array_equal(Jm, J)
+    np.testing.assert_array_equal(Am, A)
+    assert_rel_close(bm, b, rel=1e-5, msg="threaded loop belief")
