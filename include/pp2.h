@@ -181,6 +181,52 @@ int pp2_fib_solve(pp2_ctx* ctx, int max_sweeps, int* sweeps, float* final_norm);
 /* host_fib_alphas layout [hw][9] (fast_informed_bound_cuda.cu:270-271). */
 int pp2_fib_get(pp2_ctx* ctx, float* alphas);
 int pp2_fib_set(pp2_ctx* ctx, const float* alphas);
+/* saveFibDataToFile / loadFibDataFromFile (fast_informed_bound_cuda.cu:
+ * 343-394): dir/fib_alphas (one cell per line, 9 "%15.8f" values) and
+ * dir/fib_actions (the 9 actions, "%10u" per line).  dir NULL: ".". */
+int pp2_fib_save(pp2_ctx* ctx, const char* dir);
+int pp2_fib_load(pp2_ctx* ctx, const char* dir);
+
+/* ---------------------------------------------------------------- PBVI
+ * Point-based value iteration lower bound (src/pomdp/
+ * point_based_value_iteration_cuda.cu), state kept in the context (unsharded
+ * contexts only): the belief set B[S][hw], alpha vectors alphas[S][hw] and
+ * their actions[S] (host_pbvi_alphas / host_pbvi_actions, :51-57).  The
+ * reference's node uses S = 500 (src/pomdp/path_planning_2d.cu:122,140).
+ *
+ * generateBeliefSet (:165-295): S beliefs grown from b0 (hw floats, used as
+ * given).  Three glibc rand() draws per (belief, action) and round from
+ * srand(rand_seed) (the reference never seeds: 1); *rand_calls (may be NULL)
+ * gets the number drawn, so a planner can continue the same stream.  Resets
+ * the alphas to 0 (pointBasedValueIteration, :652-657). */
+int pp2_pbvi_belief_set(pp2_ctx* ctx, const float* b0, uint32_t set_size,
+                        uint32_t rand_seed, uint64_t* rand_calls);
+/* Any S beliefs [S][hw] as the belief set (alphas reset to 0). */
+int pp2_pbvi_set_beliefs(pp2_ctx* ctx, uint32_t set_size, const float* beliefs);
+int pp2_pbvi_get_beliefs(pp2_ctx* ctx, float* beliefs);
+/* backupAlphaVectors (:319-641): `iterations` synchronous point-based
+ * backups from the current alphas; iterations <= 0 runs the reference's
+ * ceil(log(1e-3/5) / log(gamma)) (:440-441).  Asynchronous. */
+int pp2_pbvi_backup(pp2_ctx* ctx, int iterations);
+/* pointBasedValueIteration (:643-676): belief set + zero alphas + backup. */
+int pp2_pbvi_solve(pp2_ctx* ctx, const float* b0, uint32_t set_size,
+                   uint32_t rand_seed, uint64_t* rand_calls);
+/* S (0 before any PBVI call) and whether a belief set is present. */
+int pp2_pbvi_info(pp2_ctx* ctx, uint32_t* set_size, int* has_beliefs);
+/* alphas [S][hw] and actions [S]; either may be NULL. */
+int pp2_pbvi_get(pp2_ctx* ctx, float* alphas, uint8_t* actions);
+int pp2_pbvi_set(pp2_ctx* ctx, uint32_t set_size, const float* alphas,
+                 const uint8_t* actions);
+/* evaluatePbviCpu (:678-699) for n beliefs [n][hw]: values[i] = max over k
+ * of inner_product(b_i, alpha_k) (x-ordered, multiply then add), actions[i]
+ * = the action of the first maximising alpha.  Either output may be NULL. */
+int pp2_pbvi_evaluate(pp2_ctx* ctx, int n, const float* beliefs, float* values,
+                      uint8_t* actions);
+/* savePbviDataToFile / loadPbviDataFromFile (:737-797): dir/pbvi_alphas (one
+ * alpha vector per line, "%15.8f" per cell) and dir/pbvi_actions ("%10u" per
+ * line; read back into uint8 storage, which the reference overflows). */
+int pp2_pbvi_save(pp2_ctx* ctx, const char* dir);
+int pp2_pbvi_load(pp2_ctx* ctx, const char* dir, uint32_t set_size);
 
 /* ---------------------------------------------------------------- QV-tree
  * Online POMDP planner: QNode / VNode / SearchTree

@@ -28,7 +28,7 @@ _u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
 
 def build(force: bool = False) -> str:
     srcs = [os.path.join(HERE, f) for f in
-            ("pp2_oracle.c", "pp2_oracle_tree.c", "pp2_oracle.h")]
+            ("pp2_oracle.c", "pp2_oracle_tree.c", "pp2_oracle_pbvi.c", "pp2_oracle.h")]
     if force or not os.path.exists(LIB_PATH) or any(
             os.path.getmtime(LIB_PATH) < os.path.getmtime(s) for s in srcs):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
@@ -69,6 +69,15 @@ def lib():
             "orc_synth_map": (None, [I, I, C.c_uint64, D, _u8p]),
             "orc_synth_goal": (I, [I, I, _u8p, C.POINTER(I), C.POINTER(I)]),
             "orc_synth_trajectory": (I, [I, I, _u8p, I, I, C.c_uint64, I, _u8p, _u8p, _i32p]),
+            "orc_rand_seed": (None, [C.c_void_p, C.c_uint32]),
+            "orc_rand_next": (C.c_int32, [C.c_void_p]),
+            "orc_pbvi_belief_set": (I, [I, I, _f32p, _f32p, _f32p, I, C.c_void_p, _f32p]),
+            "orc_pbvi_backup": (I, [I, I, F, _f32p, _f32p, _f32p, I, _f32p, _f32p, _u8p, I]),
+            "orc_pbvi_iterations": (I, [F]),
+            "orc_pbvi_eval": (None, [S, _f32p, I, _f32p, _u8p, C.POINTER(F),
+                                     C.POINTER(C.c_uint8)]),
+            "orc_heap_sort_desc": (None, [S, _f32p, np.ctypeslib.ndpointer(np.uintp,
+                                                                          flags="C_CONTIGUOUS")]),
             "orc_planner_create": (C.c_void_p, [I, I, _f32p, _f32p, _f32p, _f32p, F, I, I,
                                                 C.c_uint32, C.c_uint32, C.c_uint64, I]),
             "orc_planner_step": (I, [C.c_void_p, C.c_uint8, C.c_uint8, C.c_void_p,
@@ -301,3 +310,59 @@ class Planner:
             self.close()
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------- PBVI
+class RandState:
+    """glibc rand() state (orc_rand_state), srand(seed)."""
+
+    def __init__(self, seed=1):
+        self.buf = C.create_string_buffer(34 * 4 + 8)
+        lib().orc_rand_seed(self.buf, int(seed))
+
+    def next(self):
+        return lib().orc_rand_next(self.buf)
+
+
+def pbvi_belief_set(H, W, T, L, b0, S, rand_state=None):
+    """generateBeliefSet: (b_set[S, hw], rand state after it)."""
+    rs = rand_state or RandState(1)
+    out = np.zeros((S, H * W), np.float32)
+    st = lib().orc_pbvi_belief_set(H, W, T, L, np.ascontiguousarray(b0, np.float32), int(S),
+                                   rs.buf, out)
+    if st != 0:
+        raise ValueError("orc_pbvi_belief_set failed")
+    return out, rs
+
+
+def pbvi_backup(H, W, gamma, T, L, R, b_set, alphas=None, iterations=0):
+    """backupAlphaVectors from `alphas` (zeros by default): (alphas, actions, iters)."""
+    S = b_set.shape[0]
+    al = (np.zeros((S, H * W), np.float32) if alphas is None
+          else np.array(alphas, np.float32, copy=True).reshape(S, H * W))
+    act = np.zeros(S, np.uint8)
+    n = lib().orc_pbvi_backup(H, W, float(gamma), T, L, R, int(S),
+                              np.ascontiguousarray(b_set, np.float32), al, act, int(iterations))
+    if n < 0:
+        raise MemoryError("orc_pbvi_backup")
+    return al, act, n
+
+
+def pbvi_iterations(gamma):
+    return lib().orc_pbvi_iterations(float(gamma))
+
+
+def pbvi_eval(b, alphas, actions):
+    v = C.c_float()
+    a = C.c_uint8()
+    alphas = np.ascontiguousarray(alphas, np.float32)
+    lib().orc_pbvi_eval(b.size, np.ascontiguousarray(b, np.float32), alphas.shape[0], alphas,
+                        np.ascontiguousarray(actions, np.uint8), C.byref(v), C.byref(a))
+    return v.value, a.value
+
+
+def heap_sort_desc(key):
+    key = np.ascontiguousarray(key, np.float32)
+    idx = np.zeros(key.size, np.uintp)
+    lib().orc_heap_sort_desc(key.size, key, idx)
+    return idx

@@ -134,6 +134,21 @@ int orc_synth_trajectory(int H, int W, const uint8_t* map, int gx, int gy,
                          uint64_t seed, int n, uint8_t* us, uint8_t* zs,
                          int32_t* states);
 
+/* ---- PBVI lower bound, pp2_oracle_pbvi.c -------------------------------------- */
+/* generateBeliefSet (point_based_value_iteration_cuda.cu:165-295): b_set[S][hw]
+ * from b0, drawing rand() from *rs (seed it with orc_rand_seed(rs, 1) for the
+ * reference's unseeded glibc rand()). */
+int orc_pbvi_belief_set(int H, int W, const float* T, const float* L, const float* b0,
+                        int S, orc_rand_state* rs, float* b_set);
+/* backupAlphaVectors (:319-641) from the given alphas[S][hw] (the driver
+ * zeroes them, :652-657); iterations <= 0: the reference's count (:440-441).
+ * Returns the iterations run. */
+int orc_pbvi_backup(int H, int W, float gamma, const float* T, const float* L, const float* R,
+                    int S, const float* b_set, float* alphas, uint8_t* actions, int iterations);
+int orc_pbvi_iterations(float gamma);
+/* indices sorted as the reference's partial_sort (:264-269) leaves them */
+void orc_heap_sort_desc(size_t n, const float* key, size_t* idx);
+
 /* ---- QV-tree online planner (a6-a8), pp2_oracle_tree.c ---------------------- */
 typedef struct {
   uint32_t depth;

@@ -73,6 +73,19 @@ SIGNATURES = {
     "pp2_fib_solve": [_vp, C.c_int, _i32p, _f32p],
     "pp2_fib_get": [_vp, _f32p],
     "pp2_fib_set": [_vp, _f32p],
+    "pp2_fib_save": [_vp, C.c_char_p],
+    "pp2_fib_load": [_vp, C.c_char_p],
+    "pp2_pbvi_belief_set": [_vp, _f32p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)],
+    "pp2_pbvi_set_beliefs": [_vp, C.c_uint32, _f32p],
+    "pp2_pbvi_get_beliefs": [_vp, _f32p],
+    "pp2_pbvi_backup": [_vp, C.c_int],
+    "pp2_pbvi_solve": [_vp, _f32p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)],
+    "pp2_pbvi_info": [_vp, _u32p, _i32p],
+    "pp2_pbvi_get": [_vp, _f32p, _u8p],
+    "pp2_pbvi_set": [_vp, C.c_uint32, _f32p, _u8p],
+    "pp2_pbvi_evaluate": [_vp, C.c_int, _f32p, _f32p, _u8p],
+    "pp2_pbvi_save": [_vp, C.c_char_p],
+    "pp2_pbvi_load": [_vp, C.c_char_p, C.c_uint32],
     "pp2_planner_default_params": [_vp],
     "pp2_planner_create": [C.POINTER(_vp), _vp, _vp],
     "pp2_planner_destroy": [_vp],

@@ -216,6 +216,73 @@ class GridContext:
         a = np.ascontiguousarray(alphas, np.float32).reshape(self.cells, 9)
         call("pp2_fib_set", self._h, _f32(a))
 
+    def fib_save(self, directory: str):
+        call("pp2_fib_save", self._h, directory.encode())
+
+    def fib_load(self, directory: str):
+        call("pp2_fib_load", self._h, directory.encode())
+
+    # ------------------------------------------------------------ PBVI
+    def pbvi_belief_set(self, b0, set_size: int = 500, rand_seed: int = 1) -> int:
+        """generateBeliefSet; returns the number of rand() draws it made."""
+        b0 = np.ascontiguousarray(b0, np.float32).reshape(self.cells)
+        n = C.c_uint64()
+        call("pp2_pbvi_belief_set", self._h, _f32(b0), int(set_size), int(rand_seed),
+             C.byref(n))
+        return n.value
+
+    def pbvi_set_beliefs(self, beliefs):
+        B = np.ascontiguousarray(beliefs, np.float32).reshape(-1, self.cells)
+        call("pp2_pbvi_set_beliefs", self._h, B.shape[0], _f32(B))
+
+    def pbvi_info(self):
+        s = C.c_uint32()
+        h = C.c_int()
+        call("pp2_pbvi_info", self._h, C.byref(s), C.byref(h))
+        return s.value, bool(h.value)
+
+    def pbvi_get_beliefs(self) -> np.ndarray:
+        S, _ = self.pbvi_info()
+        out = np.empty((S, self.cells), np.float32)
+        call("pp2_pbvi_get_beliefs", self._h, _f32(out))
+        return out
+
+    def pbvi_backup(self, iterations: int = 0):
+        call("pp2_pbvi_backup", self._h, int(iterations))
+
+    def pbvi_solve(self, b0, set_size: int = 500, rand_seed: int = 1) -> int:
+        """pointBasedValueIteration; returns the number of rand() draws."""
+        b0 = np.ascontiguousarray(b0, np.float32).reshape(self.cells)
+        n = C.c_uint64()
+        call("pp2_pbvi_solve", self._h, _f32(b0), int(set_size), int(rand_seed), C.byref(n))
+        return n.value
+
+    def pbvi_get(self):
+        S, _ = self.pbvi_info()
+        al = np.empty((S, self.cells), np.float32)
+        act = np.empty(S, np.uint8)
+        call("pp2_pbvi_get", self._h, _f32(al), _u8(act))
+        return al, act
+
+    def pbvi_set(self, alphas, actions):
+        al = np.ascontiguousarray(alphas, np.float32).reshape(-1, self.cells)
+        act = np.ascontiguousarray(actions, np.uint8).reshape(al.shape[0])
+        call("pp2_pbvi_set", self._h, al.shape[0], _f32(al), _u8(act))
+
+    def pbvi_evaluate(self, beliefs):
+        """evaluatePbviCpu over a batch: (values[n], actions[n])."""
+        B = np.ascontiguousarray(beliefs, np.float32).reshape(-1, self.cells)
+        v = np.empty(B.shape[0], np.float32)
+        a = np.empty(B.shape[0], np.uint8)
+        call("pp2_pbvi_evaluate", self._h, B.shape[0], _f32(B), _f32(v), _u8(a))
+        return v, a
+
+    def pbvi_save(self, directory: str):
+        call("pp2_pbvi_save", self._h, directory.encode())
+
+    def pbvi_load(self, directory: str, set_size: int = 500):
+        call("pp2_pbvi_load", self._h, directory.encode(), int(set_size))
+
     # ------------------------------------------------------------ shards
     @staticmethod
     def rccl_unique_id() -> bytes:

@@ -6,6 +6,7 @@
 
 #include <initializer_list>
 #include <string>
+#include <vector>
 
 #include "pp2.h"
 #include "pp2_internal.h"
@@ -54,6 +55,8 @@ struct Planes {
   PlaneSet v{nullptr, 0, 0};
   int K = 0;
 };
+
+struct PbviState;  // pp2_pbvi.cpp
 
 }  // namespace pp2rt
 
@@ -111,6 +114,8 @@ struct pp2_ctx {
   hipEvent_t ev_enter = nullptr, ev_leave = nullptr;
   pp2_shard_group* group = nullptr;  // single-process shard group, if any
   int grank = 0;                     // rank (row-block order) inside the group
+
+  pp2rt::PbviState* pbvi = nullptr;  // PBVI belief set / alpha vectors (pp2_pbvi.cpp)
 };
 
 namespace pp2rt {
@@ -151,5 +156,15 @@ int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* 
 enum HaloKind { HALO_BELIEF, HALO_VALUE, HALO_FIB };
 const Planes& halo_planes(pp2_ctx* c, HaloKind k);
 int upload_planes(pp2_ctx* c, Planes& P, const float* host);
+
+// Reference text formats: "%15.8f" values, per_line to a line / "%u" per line.
+int write_text(const std::string& path, const std::vector<float>& v, int per_line);
+int read_text(const std::string& path, std::vector<float>& v);
+int read_actions(const std::string& path, std::vector<uint8_t>& v);
+std::string join(const char* dir, const char* name);
+
+void pbvi_free(pp2_ctx* c);
+// d_dots[i*S + k] = inner_product(belief i, alpha k) for n device rows of ld floats
+int pbvi_eval_device(pp2_ctx* c, int n, const float* d_beliefs, int ld, float* d_dots);
 
 }  // namespace pp2rt

@@ -1,0 +1,108 @@
+// pp2_pbvi_dev.hip -- PBVI kernels that restate the reference's DEVICE code
+// (built like the other kernel files: FTZ, every fused multiply-add an
+// explicit fmaf, as nvcc --use_fast_math contracts it).
+//
+//   k_pbvi_update    cudaBayesBeliefUpdate (point_based_value_iteration_cuda.cu:88-133)
+//                    over a batch of (source row, action, observation) candidates
+//   k_pbvi_gamma_ao  cudaComputeGammaOA (:297-341) for one action, all 16
+//                    observations and every alpha vector
+#include <hip/hip_runtime.h>
+
+#include "pp2_pbvi_internal.h"
+
+namespace pp2 {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kGaoRows = 16;  // alpha vectors per thread in k_pbvi_gamma_ao
+
+__global__ __launch_bounds__(kThreads) void k_pbvi_update(
+    Geom g, PlaneSet T, PlaneSet L, const float* __restrict__ src, int ld,
+    const int* __restrict__ src_row, const uint8_t* __restrict__ us,
+    const uint8_t* __restrict__ zs, float* __restrict__ out) {
+  const int c = blockIdx.y;
+  const int W = g.width, H = g.rows;
+  const int idx = blockIdx.x * kThreads + threadIdx.x;
+  if (idx >= H * W) return;
+  const int y = idx / W, x = idx - y * W;
+  const int u = us[c], z = zs[c];
+  const float* __restrict__ b = src + (long long)src_row[c] * ld;
+  // p = sum_s T[sidx][u][8-s] * b[sidx] over in-grid neighbours, s ascending
+  float p = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const int sy = y + s / 3 - 1, sx = x + s % 3 - 1;
+    if (sy < 0 || sy >= H || sx < 0 || sx >= W) continue;
+    const float t = T.p[(long long)sy * T.rs + (long long)(9 * u + 8 - s) * T.ps + sx];
+    p = fmaf(t, b[sy * W + sx], p);
+  }
+  out[(long long)c * ld + idx] = p * L.p[(long long)y * L.rs + (long long)z * L.ps + x];
+}
+
+// One thread = one cell x and kGaoRows alpha vectors: the 16x9 products
+// T[x][a][s] * L[nbr_s(x)][o] stay in registers across the alpha rows.
+// Off-grid neighbours enter as 0 * 0 terms, which leave the chain unchanged
+// (it never holds -0), exactly as the reference's skipped terms.
+__global__ __launch_bounds__(kThreads) void k_pbvi_gamma_ao(
+    Geom g, float gamma, PlaneSet T, PlaneSet L, const float* __restrict__ alpha, int ld, int S,
+    int a, float* __restrict__ G, long long ostride) {
+  const int W = g.width, H = g.rows;
+  const int idx = blockIdx.x * kThreads + threadIdx.x;
+  if (idx >= H * W) return;
+  const int y = idx / W, x = idx - y * W;
+  int off[9];
+  bool ok[9];
+  float tm[16][9];
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const int sy = y + s / 3 - 1, sx = x + s % 3 - 1;
+    ok[s] = !(sy < 0 || sy >= H || sx < 0 || sx >= W);
+    off[s] = ok[s] ? sy * W + sx : idx;
+    const float t = T.p[(long long)y * T.rs + (long long)(9 * a + s) * T.ps + x];
+#pragma unroll
+    for (int o = 0; o < 16; ++o)
+      tm[o][s] = ok[s] ? t * L.p[(long long)(ok[s] ? sy : y) * L.rs + (long long)o * L.ps +
+                                 (ok[s] ? sx : x)]
+                       : 0.0f;
+  }
+  const int k1 = min(S, (int)(blockIdx.y + 1) * kGaoRows);
+  for (int k = blockIdx.y * kGaoRows; k < k1; ++k) {
+    const float* __restrict__ al = alpha + (long long)k * ld;
+    float av[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) av[s] = ok[s] ? al[off[s]] : 0.0f;
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int s = 0; s < 9; ++s) acc = fmaf(tm[o][s], av[s], acc);
+      G[o * ostride + (long long)k * ld + idx] = gamma * acc;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_pbvi_update(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
+                              const float* src, int ld, const int* src_row, const uint8_t* us,
+                              const uint8_t* zs, int n, float* out) {
+  if (n <= 0) return hipSuccess;
+  const int hw = g.rows * g.width;
+  dim3 grid((hw + kThreads - 1) / kThreads, n);
+  hipLaunchKernelGGL(k_pbvi_update, grid, dim3(kThreads), 0, st, g, T, L, src, ld, src_row, us,
+                     zs, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pbvi_gamma_ao(hipStream_t st, const Geom& g, float gamma, PlaneSet T,
+                                PlaneSet L, const float* alpha, int ld, int S, int a, float* G,
+                                long long ostride) {
+  if (S <= 0) return hipSuccess;
+  const int hw = g.rows * g.width;
+  dim3 grid((hw + kThreads - 1) / kThreads, (S + kGaoRows - 1) / kGaoRows);
+  hipLaunchKernelGGL(k_pbvi_gamma_ao, grid, dim3(kThreads), 0, st, g, gamma, T, L, alpha, ld, S,
+                     a, G, ostride);
+  return hipGetLastError();
+}
+
+}  // namespace pp2

@@ -1,0 +1,525 @@
+// pp2_pbvi_host.hip -- PBVI kernels that restate the reference's HOST (x86,
+// IEEE, no FMA) and cuBLAS arithmetic.  Built WITHOUT denormal flushing; the
+// only fused multiply-adds are the MFMA's (the pinned Sgemm chain).
+//
+//   k_rows_seq      std::accumulate / std::partial_sum of rows
+//                   (normalizeProbDensity :135-145, sampleFromProbDensity :147-163)
+//   k_rows_div      x /= sum (:142-143)
+//   k_rows_dot      std::inner_product (:610-622, evaluatePbviCpu :678-699)
+//   k_pair_chain    the L1 distances of generateBeliefSet (:238-246) and
+//                   all-pairs inner products
+//   k_pbvi_sample   the three draws of generateBeliefSet (:212-222)
+//   k_pbvi_pick     min over the set / max_element over actions (:238-255)
+//   k_gemm_nt       the per-(a,o) Sgemm (:505-513) on v_mfma_f32_32x32x2_f32
+//   k_argmax_rows   max_element over each belief's row (:531-537)
+//   k_pbvi_gamma_a  Gamma_a = R + sum_o alphas_ao_max (:459-467, Sgeam :542-550)
+//   k_pbvi_select   the best action per belief and its alpha (:610-626)
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <limits.h>
+
+#include "pp2_pbvi_internal.h"
+
+namespace pp2 {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int xcd_map(int b, int n) {
+  const int q = n / 8, r = n % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// ---------------------------------------------------------------- row chains
+// One wave walks 64 rows: 64x64 tiles staged through LDS with coalesced
+// loads, then lane r adds row r's values in x order.
+template <int MODE>
+__global__ __launch_bounds__(64) void k_rows_seq(const float* __restrict__ A, int ld, int rows,
+                                                 int n, float* __restrict__ sums,
+                                                 float* __restrict__ cdf) {
+  __shared__ float t[64][65];
+  const int lane = threadIdx.x, r0 = blockIdx.x * 64;
+  float acc = 0.0f;
+  for (int x0 = 0; x0 < n; x0 += 64) {
+    const int x = x0 + lane;
+    for (int rr = 0; rr < 64; ++rr) {
+      const int r = r0 + rr;
+      t[rr][lane] = (r < rows && x < n) ? A[(long long)r * ld + x] : 0.0f;
+    }
+    __syncthreads();
+    const int m = min(64, n - x0);
+    for (int j = 0; j < m; ++j) {
+      acc = acc + t[lane][j];
+      if (MODE == ROW_CDF) t[lane][j] = acc;
+    }
+    __syncthreads();
+    if (MODE == ROW_CDF) {
+      for (int rr = 0; rr < 64; ++rr) {
+        const int r = r0 + rr;
+        if (r < rows && x < n) cdf[(long long)r * ld + x] = t[rr][lane];
+      }
+      __syncthreads();
+    }
+  }
+  if (sums && r0 + lane < rows) sums[r0 + lane] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_rows_div(float* __restrict__ A, int ld, int n,
+                                                  const float* __restrict__ sums) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= n) return;
+  float* p = A + (long long)blockIdx.y * ld + x;
+  *p = *p / sums[blockIdx.y];
+}
+
+__global__ __launch_bounds__(64) void k_rows_dot(const float* __restrict__ A, int amod,
+                                                 const float* __restrict__ B, int ld, int rows,
+                                                 int n, float* __restrict__ out) {
+  __shared__ float ta[64][65];
+  __shared__ float tb[64][65];
+  const int lane = threadIdx.x, r0 = blockIdx.x * 64;
+  float acc = 0.0f;
+  for (int x0 = 0; x0 < n; x0 += 64) {
+    const int x = x0 + lane;
+    for (int rr = 0; rr < 64; ++rr) {
+      const int r = r0 + rr;
+      const bool in = r < rows && x < n;
+      ta[rr][lane] = in ? A[(long long)(r % amod) * ld + x] : 0.0f;
+      tb[rr][lane] = in ? B[(long long)r * ld + x] : 0.0f;
+    }
+    __syncthreads();
+    const int m = min(64, n - x0);
+    for (int j = 0; j < m; ++j) acc = acc + ta[lane][j] * tb[lane][j];
+    __syncthreads();
+  }
+  if (r0 + lane < rows) out[r0 + lane] = acc;
+}
+
+// ---------------------------------------------------------------- pair chains
+// 64 A rows x 64 B rows per 256-thread block; thread (la, jg) keeps the 16
+// chains (la, 16 jg + m).  A is staged transposed ([x][row]: lane-contiguous
+// reads), B row-major (wave-uniform broadcast reads).
+template <int OP>
+__device__ __forceinline__ float pair_step(float acc, float a, float b) {
+  if constexpr (OP == PAIR_L1)
+    return acc + fabsf(a - b);
+  else
+    return acc + a * b;
+}
+
+template <int OP>
+__global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A, int na,
+                                                    const float* __restrict__ B, int nb, int ld,
+                                                    int n, float* __restrict__ out, int ldo) {
+  __shared__ float sAT[kPbviChunk][64 + 1];
+  __shared__ __attribute__((aligned(16))) float sB[64][kPbviChunk + 4];
+  const int tid = threadIdx.x, la = tid & 63, jg = tid >> 6;
+  const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
+  float acc[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) acc[m] = 0.0f;
+  for (int x0 = 0; x0 < n; x0 += kPbviChunk) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q, row = e >> 3, c4 = (e & 7) * 4;
+      const int ia = i0 + row, jb = j0 + row;
+      const f4 va = ia < na ? *(const f4*)(A + (long long)ia * ld + x0 + c4) : f4{0, 0, 0, 0};
+      const f4 vb = jb < nb ? *(const f4*)(B + (long long)jb * ld + x0 + c4) : f4{0, 0, 0, 0};
+      sAT[c4 + 0][row] = va.x;
+      sAT[c4 + 1][row] = va.y;
+      sAT[c4 + 2][row] = va.z;
+      sAT[c4 + 3][row] = va.w;
+      *(f4*)&sB[row][c4] = vb;
+    }
+    __syncthreads();
+    const int m = min(kPbviChunk, n - x0);
+    int xx = 0;
+    for (; xx + 4 <= m; xx += 4) {
+      const float a0 = sAT[xx][la], a1 = sAT[xx + 1][la], a2 = sAT[xx + 2][la],
+                  a3 = sAT[xx + 3][la];
+#pragma unroll
+      for (int mm = 0; mm < 16; ++mm) {
+        const f4 b = *(const f4*)&sB[jg * 16 + mm][xx];
+        float v = acc[mm];
+        v = pair_step<OP>(v, a0, b.x);
+        v = pair_step<OP>(v, a1, b.y);
+        v = pair_step<OP>(v, a2, b.z);
+        v = pair_step<OP>(v, a3, b.w);
+        acc[mm] = v;
+      }
+    }
+    for (; xx < m; ++xx) {
+      const float av = sAT[xx][la];
+#pragma unroll
+      for (int mm = 0; mm < 16; ++mm) acc[mm] = pair_step<OP>(acc[mm], av, sB[jg * 16 + mm][xx]);
+    }
+    __syncthreads();
+  }
+  if (i0 + la < na) {
+#pragma unroll
+    for (int mm = 0; mm < 16; ++mm) {
+      const int j = j0 + jg * 16 + mm;
+      if (j < nb) out[(long long)(i0 + la) * ldo + j] = acc[mm];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- sampling
+// find_if(partial_sum >= r) over `cnt` values at stride `stride`; when the
+// sum never reaches r, the last index at which it grew (the reference would
+// run past the end).
+__device__ __forceinline__ int sample_small(const float* p, long long stride, int cnt, float r) {
+  float acc = 0.0f;
+  int last = 0;
+  for (int j = 0; j < cnt; ++j) {
+    const float prev = acc;
+    acc = acc + p[(long long)j * stride];
+    if (acc >= r) return j;
+    if (acc != prev) last = j;
+  }
+  return last;
+}
+
+__global__ __launch_bounds__(256) void k_pbvi_sample(Geom g, PlaneSet T, PlaneSet L,
+                                                     const float* __restrict__ cdf, int ld,
+                                                     int rows, const float* __restrict__ rnd,
+                                                     uint8_t* __restrict__ z_out,
+                                                     int* __restrict__ s_out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= 9 * rows) return;
+  const int i = c / 9, a = c - 9 * i;
+  const int W = g.width, H = g.rows, n = H * W;
+  const float* __restrict__ cd = cdf + (long long)i * ld;
+  const float r1 = rnd[3 * c], r2 = rnd[3 * c + 1], r3 = rnd[3 * c + 2];
+  // the cdf is non-decreasing: lower_bound is find_if(x >= r1)
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cd[mid] >= r1) hi = mid; else lo = mid + 1;
+  }
+  if (lo >= n) {  // first index at which the sum reaches its final value
+    const float last = cd[n - 1];
+    lo = 0;
+    hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cd[mid] >= last) hi = mid; else lo = mid + 1;
+    }
+  }
+  const int s = lo, ys = s / W, xs = s - ys * W;
+  const int nl = sample_small(T.p + (long long)ys * T.rs + (long long)(9 * a) * T.ps + xs, T.ps,
+                              9, r2);
+  int ny = ys + nl / 3 - 1, nx = xs + nl % 3 - 1;
+  if (ny < 0 || ny >= H || nx < 0 || nx >= W) ny = ys, nx = xs;  // rand() == 0 on a zero entry
+  const int z = sample_small(L.p + (long long)ny * L.rs + nx, L.ps, 16, r3);
+  z_out[c] = (uint8_t)z;
+  if (s_out) s_out[c] = s;
+}
+
+__global__ __launch_bounds__(256) void k_pbvi_pick(const float* __restrict__ l1, int ldo, int n,
+                                                   int nset, float* __restrict__ best_l1,
+                                                   int* __restrict__ best_a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float m[9];
+  for (int a = 0; a < 9; ++a) {
+    const float* row = l1 + (long long)(9 * i + a) * ldo;
+    float v = FLT_MAX;
+    for (int j = 0; j < nset; ++j)
+      if (row[j] < v) v = row[j];
+    m[a] = v;
+  }
+  int ba = 0;
+  for (int a = 1; a < 9; ++a)
+    if (m[ba] < m[a]) ba = a;
+  best_a[i] = ba;
+  best_l1[i] = m[ba];
+}
+
+// ---------------------------------------------------------------- MFMA GEMM
+// C[i][k] = sum_x A[i][x] * B[k][x] with x in ascending order: each
+// v_mfma_f32_32x32x2_f32 step is fma(a[x+1], b[x+1], fma(a[x], b[x], c)),
+// lane half h holding x = 2t + h.  128x128 tiles, 4 waves of 64x64 (2x2
+// MFMA blocks), x-chunks of 32 staged through LDS with each row's 8-float
+// groups stored as [h][s] (x = 8q + 2s + h -> 8q + 4h + s) so a lane reads
+// four consecutive steps with one ds_read_b128.
+constexpr int GT = kGemmTile, GK = kPbviChunk, GLD = 36;
+
+__global__ __launch_bounds__(256, 2) void k_gemm_nt(const float* __restrict__ A,
+                                                    const float* __restrict__ B,
+                                                    float* __restrict__ C, int Mp, int Np, int ld,
+                                                    long long bstride, long long cstride,
+                                                    int ksplit, int kchunk, long long sstride) {
+  __shared__ __attribute__((aligned(16))) float sA[GT * GLD];
+  __shared__ __attribute__((aligned(16))) float sB[GT * GLD];
+  const int ti_n = Mp / GT, tk_n = Np / GT;
+  const int L = xcd_map(blockIdx.x, gridDim.x);
+  const int ti = L % ti_n;
+  int rest = L / ti_n;
+  const int tk = rest % tk_n;
+  rest /= tk_n;
+  const int sp = rest % ksplit, z = rest / ksplit;
+  const int i0 = ti * GT, k0 = tk * GT;
+  const int xb = sp * kchunk, xe = min(ld, xb + kchunk);
+  const float* __restrict__ Ab = A + (long long)i0 * ld;
+  const float* __restrict__ Bb = B + z * bstride + (long long)k0 * ld;
+  float* __restrict__ Cb = C + z * cstride + sp * sstride;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wi = w & 1, wk = w >> 1;
+  const int r = lane & 31, h = lane >> 5;
+
+  f4 ra[2][2], rb[2][2];
+  auto gload = [&](int x0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = tid + 256 * q, row = p >> 2, c8 = (p & 3) * 8;
+      const f4* pa = (const f4*)(Ab + (long long)row * ld + x0 + c8);
+      const f4* pb = (const f4*)(Bb + (long long)row * ld + x0 + c8);
+      ra[q][0] = pa[0];
+      ra[q][1] = pa[1];
+      rb[q][0] = pb[0];
+      rb[q][1] = pb[1];
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = tid + 256 * q, row = p >> 2, c8 = (p & 3) * 8;
+      float* da = sA + row * GLD + c8;
+      float* db = sB + row * GLD + c8;
+      *(f4*)da = f4{ra[q][0].x, ra[q][0].z, ra[q][1].x, ra[q][1].z};
+      *(f4*)(da + 4) = f4{ra[q][0].y, ra[q][0].w, ra[q][1].y, ra[q][1].w};
+      *(f4*)db = f4{rb[q][0].x, rb[q][0].z, rb[q][1].x, rb[q][1].z};
+      *(f4*)(db + 4) = f4{rb[q][0].y, rb[q][0].w, rb[q][1].y, rb[q][1].w};
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[ib][kb][v] = 0.0f;
+
+  if (xb < xe) gload(xb);
+  for (int x0 = xb; x0 < xe; x0 += GK) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (x0 + GK < xe) gload(x0 + GK);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f4 a[2], b[2];
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+        a[ib] = *(const f4*)(sA + (wi * 64 + ib * 32 + r) * GLD + 8 * q + 4 * h);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        b[kb] = *(const f4*)(sB + (wk * 64 + kb * 32 + r) * GLD + 8 * q + 4 * h);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+            acc[ib][kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ib][s], b[kb][s], acc[ib][kb],
+                                                               0, 0, 0);
+    }
+  }
+  // C/D map of the 32x32 forms: register v of lane l is row (v&3) + 8(v>>2) + 4h, column r
+#pragma unroll
+  for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int i = i0 + wi * 64 + ib * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const int k = k0 + wk * 64 + kb * 32 + r;
+        Cb[(long long)i * Np + k] = acc[ib][kb][v];
+      }
+}
+
+__global__ __launch_bounds__(256) void k_argmax_rows(const float* __restrict__ C, int rows, int n,
+                                                     int ldc, int* __restrict__ out,
+                                                     float* __restrict__ vmax) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* __restrict__ p = C + (long long)row * ldc;
+  float bv = -INFINITY;
+  int bi = INT_MAX;
+  for (int k = lane; k < n; k += 64) {
+    const float v = p[k];
+    if (bi == INT_MAX || v > bv) {
+      bv = v;
+      bi = k;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float ov = __shfl_xor(bv, off);
+    const int oi = __shfl_xor(bi, off);
+    if (oi != INT_MAX && (bi == INT_MAX || ov > bv || (ov == bv && oi < bi))) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    out[row] = bi;
+    if (vmax) vmax[row] = bv;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pbvi_gamma_a(Geom g, PlaneSet R,
+                                                      const float* __restrict__ G,
+                                                      long long gstride, int ld, int a,
+                                                      const int* __restrict__ kstar, int kstride,
+                                                      float* __restrict__ Ga) {
+  const int W = g.width, H = g.rows;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= H * W) return;
+  const int i = blockIdx.y, y = idx / W, x = idx - y * W;
+  float v = R.p[(long long)y * R.rs + (long long)a * R.ps + x];
+#pragma unroll
+  for (int o = 0; o < 16; ++o)
+    v = v + G[o * gstride + (long long)kstar[o * kstride + i] * ld + idx];
+  Ga[(long long)i * ld + idx] = v;
+}
+
+__global__ __launch_bounds__(256) void k_pbvi_select(const float* __restrict__ V,
+                                                     const float* __restrict__ Ga, int Sp, int ld,
+                                                     float* __restrict__ alpha_out,
+                                                     uint8_t* __restrict__ actions) {
+  const int i = blockIdx.y, x = blockIdx.x * 256 + threadIdx.x;
+  float opt = -FLT_MAX;
+  int oa = 0;
+  for (int a = 0; a < 9; ++a) {
+    const float v = V[a * Sp + i];
+    if (v > opt) {
+      opt = v;
+      oa = a;
+    }
+  }
+  if (x < ld) alpha_out[(long long)i * ld + x] = Ga[((long long)oa * Sp + i) * ld + x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) actions[i] = (uint8_t)oa;
+}
+
+__global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ C, int splits,
+                                                    long long sstride, int n,
+                                                    float* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  float v = C[e];
+  for (int s = 1; s < splits; ++s) v = v + C[s * sstride + e];
+  out[e] = v;
+}
+
+inline int cdiv(long long a, int b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+hipError_t launch_rows_seq(hipStream_t st, int mode, const float* A, int ld, int rows, int n,
+                           float* sums, float* cdf) {
+  if (rows <= 0) return hipSuccess;
+  if (mode == ROW_CDF)
+    hipLaunchKernelGGL(k_rows_seq<ROW_CDF>, dim3(cdiv(rows, 64)), dim3(64), 0, st, A, ld, rows,
+                       n, sums, cdf);
+  else
+    hipLaunchKernelGGL(k_rows_seq<ROW_SUM>, dim3(cdiv(rows, 64)), dim3(64), 0, st, A, ld, rows,
+                       n, sums, cdf);
+  return hipGetLastError();
+}
+
+hipError_t launch_rows_div(hipStream_t st, float* A, int ld, int rows, int n,
+                           const float* sums) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rows_div, dim3(cdiv(n, 256), rows), dim3(256), 0, st, A, ld, n, sums);
+  return hipGetLastError();
+}
+
+hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float* B, int ld,
+                           int rows, int n, float* out) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rows_dot, dim3(cdiv(rows, 64)), dim3(64), 0, st, A, amod, B, ld, rows, n,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, const float* B,
+                             int nb, int ld, int n, float* out, int ldo) {
+  if (na <= 0 || nb <= 0) return hipSuccess;
+  dim3 grid(cdiv(na, 64), cdiv(nb, 64));
+  if (op == PAIR_L1)
+    hipLaunchKernelGGL(k_pair_chain<PAIR_L1>, grid, dim3(256), 0, st, A, na, B, nb, ld, n, out,
+                       ldo);
+  else
+    hipLaunchKernelGGL(k_pair_chain<PAIR_DOT>, grid, dim3(256), 0, st, A, na, B, nb, ld, n, out,
+                       ldo);
+  return hipGetLastError();
+}
+
+hipError_t launch_pbvi_sample(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
+                              const float* cdf, int ld, int rows, const float* rnd,
+                              uint8_t* z_out, int* s_out) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pbvi_sample, dim3(cdiv(9LL * rows, 256)), dim3(256), 0, st, g, T, L, cdf,
+                     ld, rows, rnd, z_out, s_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pbvi_pick(hipStream_t st, const float* l1, int ldo, int n, int nset,
+                            float* best_l1, int* best_a) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pbvi_pick, dim3(cdiv(n, 256)), dim3(256), 0, st, l1, ldo, n, nset,
+                     best_l1, best_a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_nt(hipStream_t st, const float* A, const float* B, float* C, int Mp,
+                          int Np, int ld, int batch, long long bstride, long long cstride,
+                          int ksplit, long long sstride) {
+  if (Mp % GT || Np % GT || ld % GK || ksplit < 1) return hipErrorInvalidValue;
+  int kchunk = (ld + ksplit - 1) / ksplit;
+  kchunk = (kchunk + GK - 1) / GK * GK;
+  const long long blocks = (long long)(Mp / GT) * (Np / GT) * ksplit * batch;
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gemm_nt, dim3((unsigned)blocks), dim3(256), 0, st, A, B, C, Mp, Np, ld,
+                     bstride, cstride, ksplit, kchunk, sstride);
+  return hipGetLastError();
+}
+
+hipError_t launch_argmax_rows(hipStream_t st, const float* C, int rows, int n, int ldc, int* out,
+                              float* vmax) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_argmax_rows, dim3(cdiv(rows, 4)), dim3(256), 0, st, C, rows, n, ldc, out,
+                     vmax);
+  return hipGetLastError();
+}
+
+hipError_t launch_pbvi_gamma_a(hipStream_t st, const Geom& g, PlaneSet R, const float* G,
+                               long long gstride, int ld, int S, int a, const int* kstar,
+                               int kstride, float* Ga) {
+  if (S <= 0) return hipSuccess;
+  dim3 grid(cdiv((long long)g.rows * g.width, 256), S);
+  hipLaunchKernelGGL(k_pbvi_gamma_a, grid, dim3(256), 0, st, g, R, G, gstride, ld, a, kstar,
+                     kstride, Ga);
+  return hipGetLastError();
+}
+
+hipError_t launch_pbvi_select(hipStream_t st, const float* V, const float* Ga, int Sp, int S,
+                              int ld, float* alpha_out, uint8_t* actions) {
+  if (S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pbvi_select, dim3(cdiv(ld, 256), S), dim3(256), 0, st, V, Ga, Sp, ld,
+                     alpha_out, actions);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_splits(hipStream_t st, const float* C, int splits, long long sstride,
+                             int n, float* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sum_splits, dim3(cdiv(n, 256)), dim3(256), 0, st, C, splits, sstride, n,
+                     out);
+  return hipGetLastError();
+}
+
+}  // namespace pp2

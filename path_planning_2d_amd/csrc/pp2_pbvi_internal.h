@@ -1,0 +1,82 @@
+// pp2_pbvi_internal.h -- launchers of the PBVI kernels (private).
+//
+// Flat row layout: a belief / alpha vector is one row of `ld` floats (cell
+// idx = y*W + x, ld = hw rounded up to kPbviChunk, pad cells 0); a set of S
+// rows is padded to Sp = round_up(S, kGemmTile) rows, pad rows 0.
+//
+// Two translation units, split by whose arithmetic they restate:
+//   pp2_pbvi_dev.hip  (FTZ, like the reference's nvcc --use_fast_math device
+//                      code): the batched belief update and Gamma_ao;
+//   pp2_pbvi_host.hip (IEEE denormals, like the reference's x86 host code and
+//                      cuBLAS): sums, prefix sums, divisions, L1 distances,
+//                      inner products, the sampler and the MFMA GEMM.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pp2_internal.h"
+
+namespace pp2 {
+
+constexpr int kPbviChunk = 32;  // x-chunk of the row kernels and the GEMM (ld multiple)
+constexpr int kGemmTile = 128;  // GEMM tile rows / cols (Sp multiple)
+
+enum PairOp { PAIR_L1 = 0, PAIR_DOT = 1 };
+enum RowMode { ROW_SUM = 0, ROW_CDF = 1 };
+
+// ---- pp2_pbvi_dev.hip
+// out[c] = cudaBayesBeliefUpdate(src[src_row[c]], us[c], zs[c]) (unnormalised)
+hipError_t launch_pbvi_update(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
+                              const float* src, int ld, const int* src_row, const uint8_t* us,
+                              const uint8_t* zs, int n, float* out);
+// G[o][k][x] = cudaComputeGammaOA(a, o) of alpha k, for o < 16, k < S
+// (rows k >= S and cells x >= hw are left untouched).
+hipError_t launch_pbvi_gamma_ao(hipStream_t st, const Geom& g, float gamma, PlaneSet T,
+                                PlaneSet L, const float* alpha, int ld, int S, int a, float* G,
+                                long long ostride);
+
+// ---- pp2_pbvi_host.hip
+// ROW_SUM: sums[r] = ((A[r][0] + A[r][1]) + ...) over x < n (std::accumulate);
+// ROW_CDF: cdf[r][x] = the running sums (std::partial_sum), and sums[r].
+hipError_t launch_rows_seq(hipStream_t st, int mode, const float* A, int ld, int rows, int n,
+                           float* sums, float* cdf);
+// A[r][x] /= sums[r], x < n
+hipError_t launch_rows_div(hipStream_t st, float* A, int ld, int rows, int n,
+                           const float* sums);
+// out[r] = inner_product(A[r % amod], B[r]) (x-ordered, multiply then add)
+hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float* B, int ld,
+                           int rows, int n, float* out);
+// out[i*ldo + j] = x-ordered sum over x < n of |A[i][x] - B[j][x]| (PAIR_L1)
+// or A[i][x] * B[j][x] (PAIR_DOT, multiply then add), i < na, j < nb.
+hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, const float* B,
+                             int nb, int ld, int n, float* out, int ldo);
+// The three draws of generateBeliefSet per (belief i, action a): state from
+// cdf row i, next state from T[s][a][:], observation from L[ns][:].
+hipError_t launch_pbvi_sample(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
+                              const float* cdf, int ld, int rows, const float* rnd,
+                              uint8_t* z_out, int* s_out);
+// per belief i < n: m[a] = min_j l1[(9i+a)*ldo + j] (j < nset), best_a[i] =
+// first argmax of m, best_l1[i] = m[best_a]
+hipError_t launch_pbvi_pick(hipStream_t st, const float* l1, int ldo, int n, int nset,
+                            float* best_l1, int* best_a);
+// C[z][s][i][k] = x-ordered fmaf chain over the split-s range of x of
+// A[i][x] * B[z][k][x] (v_mfma_f32_32x32x2_f32); Mp, Np multiples of
+// kGemmTile, ld of kPbviChunk.  ksplit = 1: the chain over all x from 0.
+hipError_t launch_gemm_nt(hipStream_t st, const float* A, const float* B, float* C, int Mp,
+                          int Np, int ld, int batch, long long bstride, long long cstride,
+                          int ksplit, long long sstride);
+// out[r] = first argmax over k < n of C[r*ldc + k]
+hipError_t launch_argmax_rows(hipStream_t st, const float* C, int rows, int n, int ldc,
+                              int* out, float* vmax);
+// Gamma_a[i][x] = R[x][a] + G[0][k*[0][i]][x] + ... + G[15][k*[15][i]][x]
+hipError_t launch_pbvi_gamma_a(hipStream_t st, const Geom& g, PlaneSet R, const float* G,
+                               long long gstride, int ld, int S, int a, const int* kstar,
+                               int kstride, float* Ga);
+// action of belief i = first argmax_a V[a*Sp + i]; alpha_out[i] = Ga[action][i]
+hipError_t launch_pbvi_select(hipStream_t st, const float* V, const float* Ga, int Sp, int S,
+                              int ld, float* alpha_out, uint8_t* actions);
+// split-K partial sums C[s][r][k] -> out[r][k], s ascending
+hipError_t launch_sum_splits(hipStream_t st, const float* C, int splits, long long sstride,
+                             int n, float* out);
+
+}  // namespace pp2

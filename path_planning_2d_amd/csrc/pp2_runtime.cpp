@@ -279,6 +279,22 @@ int read_text(const std::string& path, std::vector<float>& v) {
   return PP2_OK;
 }
 
+int read_actions(const std::string& path, std::vector<uint8_t>& v) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return set_err(PP2_EIO, "cannot open %s: %s", path.c_str(), strerror(errno));
+  for (size_t i = 0; i < v.size(); ++i) {
+    unsigned a = 0;
+    if (fscanf(f, "%u", &a) != 1 || a > 8) {
+      fclose(f);
+      return set_err(PP2_EIO, "%s: data dimension is not set properly (action %zu)",
+                     path.c_str(), i);
+    }
+    v[i] = (uint8_t)a;
+  }
+  fclose(f);
+  return PP2_OK;
+}
+
 std::string join(const char* dir, const char* name) {
   std::string d = dir ? dir : ".";
   if (d.empty()) d = ".";
@@ -619,6 +635,7 @@ int pp2_destroy(pp2_ctx* c) {
   if (!c) return PP2_OK;
   DeviceGuard dg(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  pbvi_free(c);
   if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -927,6 +944,35 @@ int pp2_fib_set(pp2_ctx* c, const float* alphas) {
   if (!alphas) return set_err(PP2_EINVAL, "alphas is null");
   DeviceGuard dg(c->device);
   return upload_planes(c, c->fib[c->fcur], alphas);
+}
+
+// saveFibDataToFile / loadFibDataFromFile (fast_informed_bound_cuda.cu:343-394):
+// dir/fib_alphas holds one cell per line (9 "%15.8f" values), dir/fib_actions
+// the 9 actions {0..8} as "%10u" lines.
+int pp2_fib_save(pp2_ctx* c, const char* dir) {
+  CHECK(check_ctx(c));
+  std::vector<float> al(owned_cells(c) * 9);
+  CHECK(pp2_fib_get(c, al.data()));
+  CHECK(write_text(join(dir, "fib_alphas"), al, 9));
+  const std::string path = join(dir, "fib_actions");
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) return set_err(PP2_EIO, "cannot open %s for writing", path.c_str());
+  for (unsigned u = 0; u < 9; ++u) fprintf(f, "%10u\n", u);
+  if (fclose(f) != 0) return set_err(PP2_EIO, "write %s failed", path.c_str());
+  return PP2_OK;
+}
+
+int pp2_fib_load(pp2_ctx* c, const char* dir) {
+  CHECK(check_ctx(c));
+  std::vector<float> al(owned_cells(c) * 9);
+  CHECK(read_text(join(dir, "fib_alphas"), al));
+  std::vector<uint8_t> act(9);
+  CHECK(read_actions(join(dir, "fib_actions"), act));
+  for (int u = 0; u < 9; ++u)
+    if (act[u] != u)
+      return set_err(PP2_EIO, "fib_actions: alpha %d is labelled action %u (expected %d)", u,
+                     act[u], u);
+  return pp2_fib_set(c, al.data());
 }
 
 // ---------------------------------------------------------------- shards

@@ -22,40 +22,13 @@
 #include <rocrand/rocrand_xorwow.h>
 
 #include "pp2_ctx.h"
+#include "pp2_rand.h"
 
 using namespace pp2rt;
 
 namespace {
 
-// glibc random_r, TYPE_3 (x**31 + x**3 + 1), as srand(seed) / rand().
-struct GlibcRand {
-  int32_t r[31];
-  int f = 3, b = 0;
-  void seed(uint32_t s) {
-    int64_t word = (int32_t)(s == 0 ? 1 : s);
-    r[0] = (int32_t)word;
-    for (int i = 1; i < 31; ++i) {
-      const int64_t hi = word / 127773, lo = word % 127773;
-      word = 16807 * lo - 2836 * hi;
-      if (word < 0) word += 2147483647;
-      r[i] = (int32_t)word;
-    }
-    f = 3;
-    b = 0;
-    for (int i = 0; i < 310; ++i) (void)next();
-  }
-  int32_t next() {
-    const uint32_t val = (uint32_t)r[f] + (uint32_t)r[b];
-    r[f] = (int32_t)val;
-    if (++f >= 31) {
-      f = 0;
-      ++b;
-    } else if (++b >= 31) {
-      b = 0;
-    }
-    return (int32_t)(val >> 1);
-  }
-};
+using pp2rt::GlibcRand;
 
 // cuRAND XORWOW as curand_init(seed, subsequence, 0) seeds it (CUDA 8
 // curand_kernel.h: salted seed halves, then skipahead by subsequence * 2^67);
