@@ -250,10 +250,15 @@ typedef struct {
   int32_t max_search_tree_depth;  /* launch default 50 */
   int32_t max_online_iteration;   /* launch default 15 */
   int32_t lower_bound_mode;       /* 0: constant -5/(1-gamma), the reference's
-                                     fallback (search_tree_cuda.cu:382-383) */
+                                     commented fallback (search_tree_cuda.cu:382-383);
+                                     1: PBVI, evaluatePbviCpu (:379) over the
+                                     context's alpha vectors (pp2_pbvi_*) */
   uint32_t rand_seed;             /* glibc srand seed; reference never seeds: 1 */
   uint32_t sample_num;            /* observation samples per QNode (:176): 50 */
   uint64_t curand_seed;           /* curand_init seed (:90): 1234 */
+  uint64_t rand_skip;             /* rand() draws already taken from the stream
+                                     (the reference's generateBeliefSet runs
+                                     first: pp2_pbvi_solve's *rand_calls) */
 } pp2_planner_params;
 
 /* Snapshot of the root and its children, for inspection and parity tests. */

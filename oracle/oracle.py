@@ -83,6 +83,8 @@ def lib():
             "orc_planner_step": (I, [C.c_void_p, C.c_uint8, C.c_uint8, C.c_void_p,
                                      C.POINTER(C.c_uint8), C.POINTER(F)]),
             "orc_planner_reset": (None, [C.c_void_p]),
+            "orc_planner_set_pbvi": (None, [C.c_void_p, I, _f32p, _u8p]),
+            "orc_planner_skip_rand": (None, [C.c_void_p, C.c_uint64]),
             "orc_planner_info": (None, [C.c_void_p, C.c_void_p]),
             "orc_planner_destroy": (None, [C.c_void_p]),
         }
@@ -294,6 +296,15 @@ class Planner:
 
     def reset(self):
         lib().orc_planner_reset(self._h)
+
+    def set_pbvi(self, alphas, actions):
+        """Lower bounds from PBVI alpha vectors (evaluatePbviCpu)."""
+        self._pbvi = (np.ascontiguousarray(alphas, np.float32),
+                      np.ascontiguousarray(actions, np.uint8))
+        lib().orc_planner_set_pbvi(self._h, self._pbvi[0].shape[0], *self._pbvi)
+
+    def skip_rand(self, n):
+        lib().orc_planner_skip_rand(self._h, int(n))
 
     def info(self):
         t = TreeInfo()

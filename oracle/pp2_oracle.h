@@ -173,6 +173,11 @@ orc_planner* orc_planner_create(int H, int W, const float* T, const float* L,
 int orc_planner_step(orc_planner* p, uint8_t a, uint8_t z, const float* belief,
                      uint8_t* new_action, float* new_value);
 void orc_planner_reset(orc_planner* p);
+/* VNode lower bounds from PBVI alphas [S][hw] (evaluatePbviCpu,
+ * search_tree_cuda.cu:379) instead of the constant -5/(1-gamma); borrowed. */
+void orc_planner_set_pbvi(orc_planner* p, int S, const float* alphas, const uint8_t* actions);
+/* discard n rand() draws (the reference's generateBeliefSet runs first) */
+void orc_planner_skip_rand(orc_planner* p, uint64_t n);
 void orc_planner_info(orc_planner* p, orc_tree_info* info);
 void orc_planner_destroy(orc_planner* p);
 

@@ -55,6 +55,9 @@ struct orc_planner {
   float* u1;
   float* u2;
   orc_rand_state rng;
+  int pbvi_S;                 /* > 0: PBVI lower bounds (evaluatePbviCpu, :379) */
+  const float* pbvi_alphas;   /* [S][hw] */
+  const uint8_t* pbvi_actions;
   OV* root;
   uint32_t n_vnodes, n_qnodes, expansions;
 };
@@ -77,7 +80,22 @@ static OV* ov_new(orc_planner* p, const float* b, uint8_t z, float w, OQ* parent
   } else {
     orc_fib_eval(p->n, v->belief, p->alphas, &v->ub, &dummy);
   }
-  v->lb = p->lb_const;
+  if (p->pbvi_S > 0) {
+    if (p->accurate) {
+      float best = 0.0f;
+      for (int k = 0; k < p->pbvi_S; ++k) {
+        double d = 0.0;
+        const float* al = p->pbvi_alphas + (size_t)k * p->n;
+        for (size_t x = 0; x < p->n; ++x) d += (double)v->belief[x] * al[x];
+        if (k == 0 || best < (float)d) best = (float)d;
+      }
+      v->lb = best;
+    } else {
+      orc_pbvi_eval(p->n, v->belief, p->pbvi_S, p->pbvi_alphas, p->pbvi_actions, &v->lb, &dummy);
+    }
+  } else {
+    v->lb = p->lb_const;
+  }
   v->heuristic = v->ub - v->lb;
   v->vte = v;
   v->depth = 0;
@@ -286,6 +304,16 @@ orc_planner* orc_planner_create(int H, int W, const float* T, const float* L,
   }
   orc_rand_seed(&p->rng, rand_seed);
   return p;
+}
+
+void orc_planner_set_pbvi(orc_planner* p, int S, const float* alphas, const uint8_t* actions) {
+  p->pbvi_S = S;
+  p->pbvi_alphas = alphas;
+  p->pbvi_actions = actions;
+}
+
+void orc_planner_skip_rand(orc_planner* p, uint64_t n) {
+  for (uint64_t k = 0; k < n; ++k) (void)orc_rand_next(&p->rng);
 }
 
 void orc_planner_reset(orc_planner* p) {

@@ -164,6 +164,8 @@ int read_actions(const std::string& path, std::vector<uint8_t>& v);
 std::string join(const char* dir, const char* name);
 
 void pbvi_free(pp2_ctx* c);
+// The context's PBVI alpha vectors (device rows of ld floats, Sp rows); ESTATE if none.
+int pbvi_alphas(pp2_ctx* c, const float** alpha, int* S, int* Sp, int* ld);
 // d_dots[i*S + k] = inner_product(belief i, alpha k) for n device rows of ld floats
 int pbvi_eval_device(pp2_ctx* c, int n, const float* d_beliefs, int ld, float* d_dots);
 

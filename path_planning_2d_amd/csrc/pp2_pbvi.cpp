@@ -4,13 +4,15 @@
 // loop on the device and the model, belief set and alpha vectors resident in
 // HBM.  The reference's per-(a,o) round trips -- Gamma_ao to the host
 // (:406-427), back for the Sgemm (:497-503), the max-alpha gather on the host
-// (:531-540) and back again -- become five kernels per action and iteration:
+// (:531-540) and back again -- become six launches per iteration, each over
+// all 144 (a, o) pairs at once while their Gamma_ao fits the budget below:
 //
-//   Gamma_ao   k_pbvi_gamma_ao    G[o][k] for all 16 o and S alphas    (HBM-bound)
-//   Sgemm      k_gemm_nt          C[o][i][k] = <b_i, G[o][k]>          (MFMA f32)
-//   max        k_argmax_rows      k*[o][i] = first argmax_k C[o][i][k]
-//   Sgeam      k_pbvi_gamma_a     Gamma_a[i] = R_a + sum_o G[o][k*[o][i]]
-// and per iteration one inner-product chain over (a, i) and one selection.
+//   Gamma_ao   k_pbvi_gamma_ao    G[a,o][k] for every alpha k           (HBM-bound)
+//   Sgemm      k_gemm_nt          C[a,o][i][k] = <b_i, G[a,o][k]>       (MFMA f32)
+//   max        k_argmax_rows      k*[a,o][i] = first argmax_k C[a,o][i][k]
+//   Sgeam      k_pbvi_gamma_a     Gamma_a[i] = R_a + sum_o G[a,o][k*[a,o][i]]
+//   values     k_rows_chain       V[a][i] = inner_product(b_i, Gamma_a[i])
+//   select     k_pbvi_select      alpha_i = Gamma_a*[i], a* = first argmax_a V[a][i]
 // The belief-set expansion (:165-295) keeps the reference's glibc rand()
 // stream and arithmetic: the samples, the candidates' update and
 // normalisation, and every L1 distance are batched over all (belief, action)
@@ -38,10 +40,10 @@ struct PbviState {
   uint8_t* actions = nullptr;  // [Sp]
   bool has_set = false;
   // backup scratch
-  float* G = nullptr;    // [16][Sp][ld]
-  float* Ga = nullptr;   // [9][Sp][ld]
-  float* Cm = nullptr;   // [16][Sp][Sp]
-  int* kstar = nullptr;  // [16][Sp]
+  float* G = nullptr;    // [group*16][Sp][ld]  Gamma_ao of the actions in flight
+  float* Ga = nullptr;   // [9][Sp][ld]         Gamma_a
+  float* Cm = nullptr;   // [group*16][Sp][Sp]  <b_i, Gamma_ao_k>
+  int* kstar = nullptr;  // [group*16][Sp]
   float* V = nullptr;    // [9][Sp]
 };
 
@@ -235,28 +237,35 @@ int belief_set_impl(pp2_ctx* c, const float* b0, int S, uint32_t seed, uint64_t*
   return PP2_OK;
 }
 
+// Actions whose Gamma_ao slices are resident at once: all 9 (one GEMM
+// launch of 144 batches) when they fit kGaoBudget bytes, else fewer.
+constexpr size_t kGaoBudget = size_t(48) << 30;
+
 int backup_impl(pp2_ctx* c, int iterations) {
   PbviState* p = c->pbvi;
   if (!p || !p->has_set) return set_err(PP2_ESTATE, "no PBVI belief set");
   if (iterations <= 0)  // :440-441, in float like std::log(float) / std::ceil(float)
     iterations = (int)(uint32_t)std::ceil(std::log(1.0e-3f / 5.0f) / std::log(c->gamma));
   const int S = p->S, Sp = p->Sp, ld = p->ld, hw = p->hw;
-  CHECK(dalloc(&p->G, (size_t)16 * Sp * ld, c->stream));
-  CHECK(dalloc(&p->Ga, (size_t)9 * Sp * ld, c->stream));
-  CHECK(dalloc(&p->Cm, (size_t)16 * Sp * Sp, c->stream));
-  CHECK(dalloc(&p->kstar, (size_t)16 * Sp, c->stream));
-  CHECK(dalloc(&p->V, (size_t)9 * Sp, c->stream));
   const long long gstride = (long long)Sp * ld;
+  const size_t per_action = (size_t)16 * gstride * sizeof(float);
+  const int group = (int)std::max<size_t>(1, std::min<size_t>(9, kGaoBudget / per_action));
+  CHECK(dalloc(&p->G, (size_t)16 * group * gstride, c->stream));
+  CHECK(dalloc(&p->Ga, (size_t)9 * gstride, c->stream));
+  CHECK(dalloc(&p->Cm, (size_t)16 * group * Sp * Sp, c->stream));
+  CHECK(dalloc(&p->kstar, (size_t)16 * group * Sp, c->stream));
+  CHECK(dalloc(&p->V, (size_t)9 * Sp, c->stream));
   for (int it = 0; it < iterations; ++it) {
     const float* al = p->alpha[p->acur];
-    for (int a = 0; a < 9; ++a) {
-      HIPCHK(pp2::launch_pbvi_gamma_ao(c->stream, c->g, c->gamma, c->T.v, c->L.v, al, ld, S, a,
-                                       p->G, gstride));
-      HIPCHK(pp2::launch_gemm_nt(c->stream, p->bset, p->G, p->Cm, Sp, Sp, ld, 16, gstride,
+    for (int a0 = 0; a0 < 9; a0 += group) {
+      const int a1 = std::min(9, a0 + group), nb = 16 * (a1 - a0);
+      HIPCHK(pp2::launch_pbvi_gamma_ao(c->stream, c->g, c->gamma, c->T.v, c->L.v, al, ld, S, a0,
+                                       a1, p->G, gstride));
+      HIPCHK(pp2::launch_gemm_nt(c->stream, p->bset, p->G, p->Cm, Sp, Sp, ld, nb, gstride,
                                  (long long)Sp * Sp, 1, 0));
-      HIPCHK(pp2::launch_argmax_rows(c->stream, p->Cm, 16 * Sp, S, Sp, p->kstar, nullptr));
-      HIPCHK(pp2::launch_pbvi_gamma_a(c->stream, c->g, c->R.v, p->G, gstride, ld, S, a, p->kstar,
-                                      Sp, p->Ga + (size_t)a * gstride));
+      HIPCHK(pp2::launch_argmax_rows(c->stream, p->Cm, nb * Sp, S, Sp, p->kstar, nullptr));
+      HIPCHK(pp2::launch_pbvi_gamma_a(c->stream, c->g, c->R.v, p->G, gstride, ld, S, a0, a1,
+                                      p->kstar, Sp, p->Ga));
     }
     HIPCHK(pp2::launch_rows_dot(c->stream, p->bset, Sp, p->Ga, ld, 9 * Sp, hw, p->V));
     HIPCHK(pp2::launch_pbvi_select(c->stream, p->V, p->Ga, Sp, S, ld, p->alpha[p->acur ^ 1],
@@ -278,6 +287,16 @@ void pbvi_free(pp2_ctx* c) {
   free_scratch(p);
   delete p;
   c->pbvi = nullptr;
+}
+
+int pbvi_alphas(pp2_ctx* c, const float** alpha, int* S, int* Sp, int* ld) {
+  PbviState* p = c->pbvi;
+  if (!p || p->S <= 0) return set_err(PP2_ESTATE, "no PBVI alpha vectors");
+  *alpha = p->alpha[p->acur];
+  *S = p->S;
+  *Sp = p->Sp;
+  *ld = p->ld;
+  return PP2_OK;
 }
 
 int pbvi_eval_device(pp2_ctx* c, int n, const float* d_beliefs, int ld, float* d_dots) {

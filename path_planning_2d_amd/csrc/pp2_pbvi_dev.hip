@@ -45,8 +45,10 @@ __global__ __launch_bounds__(kThreads) void k_pbvi_update(
 // (it never holds -0), exactly as the reference's skipped terms.
 __global__ __launch_bounds__(kThreads) void k_pbvi_gamma_ao(
     Geom g, float gamma, PlaneSet T, PlaneSet L, const float* __restrict__ alpha, int ld, int S,
-    int a, float* __restrict__ G, long long ostride) {
+    int a0, float* __restrict__ G, long long ostride) {
   const int W = g.width, H = g.rows;
+  const int a = a0 + blockIdx.z;
+  G += (long long)blockIdx.z * 16 * ostride;
   const int idx = blockIdx.x * kThreads + threadIdx.x;
   if (idx >= H * W) return;
   const int y = idx / W, x = idx - y * W;
@@ -95,13 +97,13 @@ hipError_t launch_pbvi_update(hipStream_t st, const Geom& g, PlaneSet T, PlaneSe
 }
 
 hipError_t launch_pbvi_gamma_ao(hipStream_t st, const Geom& g, float gamma, PlaneSet T,
-                                PlaneSet L, const float* alpha, int ld, int S, int a, float* G,
-                                long long ostride) {
-  if (S <= 0) return hipSuccess;
+                                PlaneSet L, const float* alpha, int ld, int S, int a0, int a1,
+                                float* G, long long ostride) {
+  if (S <= 0 || a1 <= a0) return hipSuccess;
   const int hw = g.rows * g.width;
-  dim3 grid((hw + kThreads - 1) / kThreads, (S + kGaoRows - 1) / kGaoRows);
+  dim3 grid((hw + kThreads - 1) / kThreads, (S + kGaoRows - 1) / kGaoRows, a1 - a0);
   hipLaunchKernelGGL(k_pbvi_gamma_ao, grid, dim3(kThreads), 0, st, g, gamma, T, L, alpha, ld, S,
-                     a, G, ostride);
+                     a0, G, ostride);
   return hipGetLastError();
 }
 

@@ -2,10 +2,10 @@
 // IEEE, no FMA) and cuBLAS arithmetic.  Built WITHOUT denormal flushing; the
 // only fused multiply-adds are the MFMA's (the pinned Sgemm chain).
 //
-//   k_rows_seq      std::accumulate / std::partial_sum of rows
-//                   (normalizeProbDensity :135-145, sampleFromProbDensity :147-163)
+//   k_rows_chain    std::accumulate / std::partial_sum / std::inner_product of
+//                   rows (normalizeProbDensity :135-145, sampleFromProbDensity
+//                   :147-163, the action values :610-622)
 //   k_rows_div      x /= sum (:142-143)
-//   k_rows_dot      std::inner_product (:610-622, evaluatePbviCpu :678-699)
 //   k_pair_chain    the L1 distances of generateBeliefSet (:238-246) and
 //                   all-pairs inner products
 //   k_pbvi_sample   the three draws of generateBeliefSet (:212-222)
@@ -32,37 +32,115 @@ __device__ __forceinline__ int xcd_map(int b, int n) {
 }
 
 // ---------------------------------------------------------------- row chains
-// One wave walks 64 rows: 64x64 tiles staged through LDS with coalesced
-// loads, then lane r adds row r's values in x order.
+// One x-ordered chain per row (std::accumulate, partial_sum, inner_product).
+// A block owns kChainRows rows: all 256 threads stream kChainX-wide tiles of
+// them into LDS with coalesced loads (the next tile's loads in flight while
+// the current one is summed), and lane r of wave 0 walks row r of the tile.
+// Row stride kChainXP = kChainX + 4 keeps the per-lane float4 LDS reads on
+// distinct banks.
+constexpr int kChainRows = 16, kChainX = 256, kChainXP = kChainX + 4;
+constexpr int kChainVec = kChainRows * kChainX / 4 / 256;  // float4 per thread per tile
+
+enum { CH_SUM = 0, CH_CDF = 1, CH_DOT = 2 };
+
 template <int MODE>
-__global__ __launch_bounds__(64) void k_rows_seq(const float* __restrict__ A, int ld, int rows,
-                                                 int n, float* __restrict__ sums,
-                                                 float* __restrict__ cdf) {
-  __shared__ float t[64][65];
-  const int lane = threadIdx.x, r0 = blockIdx.x * 64;
+__global__ __launch_bounds__(256) void k_rows_chain(const float* __restrict__ A, int amod,
+                                                    const float* __restrict__ B, int ld, int rows,
+                                                    int n, float* __restrict__ sums,
+                                                    float* __restrict__ cdf) {
+  constexpr int NOP = MODE == CH_DOT ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) float t[2][NOP][kChainRows * kChainXP];
+  const int tid = threadIdx.x, r0 = blockIdx.x * kChainRows;
+  const int lrow = tid >> 4, lcol = tid & 15;  // staging: 16 threads per row
+  const int grow = r0 + lrow;
+  const bool rin = grow < rows;
+  const float* __restrict__ pa = A + (long long)(rin ? grow % amod : 0) * ld;
+  const float* __restrict__ pb = MODE == CH_DOT ? B + (long long)(rin ? grow : 0) * ld : nullptr;
+  f4 ra[kChainVec], rb[kChainVec];
+  auto gload = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < kChainVec; ++k) {
+      const int x = x0 + 4 * (lcol + 16 * k);
+      const bool in = rin && x < ld;
+      ra[k] = in ? *(const f4*)(pa + x) : f4{0, 0, 0, 0};
+      if (MODE == CH_DOT) rb[k] = in ? *(const f4*)(pb + x) : f4{0, 0, 0, 0};
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < kChainVec; ++k) {
+      *(f4*)&t[buf][0][lrow * kChainXP + 4 * (lcol + 16 * k)] = ra[k];
+      if (MODE == CH_DOT) *(f4*)&t[buf][NOP - 1][lrow * kChainXP + 4 * (lcol + 16 * k)] = rb[k];
+    }
+  };
   float acc = 0.0f;
-  for (int x0 = 0; x0 < n; x0 += 64) {
-    const int x = x0 + lane;
-    for (int rr = 0; rr < 64; ++rr) {
-      const int r = r0 + rr;
-      t[rr][lane] = (r < rows && x < n) ? A[(long long)r * ld + x] : 0.0f;
-    }
-    __syncthreads();
-    const int m = min(64, n - x0);
-    for (int j = 0; j < m; ++j) {
-      acc = acc + t[lane][j];
-      if (MODE == ROW_CDF) t[lane][j] = acc;
-    }
-    __syncthreads();
-    if (MODE == ROW_CDF) {
-      for (int rr = 0; rr < 64; ++rr) {
-        const int r = r0 + rr;
-        if (r < rows && x < n) cdf[(long long)r * ld + x] = t[rr][lane];
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  int buf = 0;
+  for (int x0 = 0; x0 < n; x0 += kChainX) {
+    const bool more = x0 + kChainX < n;
+    if (more) gload(x0 + kChainX);
+    if (tid < kChainRows) {
+      float* __restrict__ ta = &t[buf][0][tid * kChainXP];
+      const float* __restrict__ tb = &t[buf][NOP - 1][tid * kChainXP];
+      const int m = min(kChainX, n - x0);
+      int j = 0;
+      for (; j + 4 <= m; j += 4) {
+        f4 v = *(const f4*)(ta + j);
+        if (MODE == CH_DOT) {
+          const f4 w = *(const f4*)(tb + j);
+          acc = acc + v.x * w.x;
+          acc = acc + v.y * w.y;
+          acc = acc + v.z * w.z;
+          acc = acc + v.w * w.w;
+        } else {
+          acc = acc + v.x;
+          v.x = acc;
+          acc = acc + v.y;
+          v.y = acc;
+          acc = acc + v.z;
+          v.z = acc;
+          acc = acc + v.w;
+          v.w = acc;
+          if (MODE == CH_CDF) *(f4*)(ta + j) = v;
+        }
       }
-      __syncthreads();
+      for (; j < m; ++j) {
+        if (MODE == CH_DOT) {
+          acc = acc + ta[j] * tb[j];
+        } else {
+          acc = acc + ta[j];
+          if (MODE == CH_CDF) ta[j] = acc;
+        }
+      }
     }
+    __syncthreads();
+    if (MODE == CH_CDF && rin) {
+      float* __restrict__ pc = cdf + (long long)grow * ld;
+#pragma unroll
+      for (int k = 0; k < kChainVec; ++k) {
+        const int x = x0 + 4 * (lcol + 16 * k);
+        if (x < n) {
+          const f4 v = *(const f4*)&t[buf][0][lrow * kChainXP + 4 * (lcol + 16 * k)];
+          if (x + 4 <= n) {
+            *(f4*)(pc + x) = v;
+          } else {
+            for (int e = 0; e < n - x; ++e) pc[x + e] = v[e];
+          }
+        }
+      }
+    }
+    if (more) lstore(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
   }
-  if (sums && r0 + lane < rows) sums[r0 + lane] = acc;
+  if (tid < kChainRows && r0 + tid < rows) {
+    if (MODE == CH_DOT)
+      sums[r0 + tid] = acc;
+    else if (sums)
+      sums[r0 + tid] = acc;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_rows_div(float* __restrict__ A, int ld, int n,
@@ -71,29 +149,6 @@ __global__ __launch_bounds__(256) void k_rows_div(float* __restrict__ A, int ld,
   if (x >= n) return;
   float* p = A + (long long)blockIdx.y * ld + x;
   *p = *p / sums[blockIdx.y];
-}
-
-__global__ __launch_bounds__(64) void k_rows_dot(const float* __restrict__ A, int amod,
-                                                 const float* __restrict__ B, int ld, int rows,
-                                                 int n, float* __restrict__ out) {
-  __shared__ float ta[64][65];
-  __shared__ float tb[64][65];
-  const int lane = threadIdx.x, r0 = blockIdx.x * 64;
-  float acc = 0.0f;
-  for (int x0 = 0; x0 < n; x0 += 64) {
-    const int x = x0 + lane;
-    for (int rr = 0; rr < 64; ++rr) {
-      const int r = r0 + rr;
-      const bool in = r < rows && x < n;
-      ta[rr][lane] = in ? A[(long long)(r % amod) * ld + x] : 0.0f;
-      tb[rr][lane] = in ? B[(long long)r * ld + x] : 0.0f;
-    }
-    __syncthreads();
-    const int m = min(64, n - x0);
-    for (int j = 0; j < m; ++j) acc = acc + ta[lane][j] * tb[lane][j];
-    __syncthreads();
-  }
-  if (r0 + lane < rows) out[r0 + lane] = acc;
 }
 
 // ---------------------------------------------------------------- pair chains
@@ -108,21 +163,24 @@ __device__ __forceinline__ float pair_step(float acc, float a, float b) {
     return acc + a * b;
 }
 
+constexpr int kPairChunk = 32;
+
 template <int OP>
 __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A, int na,
                                                     const float* __restrict__ B, int nb, int ld,
                                                     int n, float* __restrict__ out, int ldo) {
-  __shared__ float sAT[kPbviChunk][64 + 1];
-  __shared__ __attribute__((aligned(16))) float sB[64][kPbviChunk + 4];
+  __shared__ float sAT[kPairChunk][64 + 1];
+  __shared__ __attribute__((aligned(16))) float sB[64][kPairChunk + 4];
   const int tid = threadIdx.x, la = tid & 63, jg = tid >> 6;
   const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
   float acc[16];
 #pragma unroll
   for (int m = 0; m < 16; ++m) acc[m] = 0.0f;
-  for (int x0 = 0; x0 < n; x0 += kPbviChunk) {
+  for (int x0 = 0; x0 < n; x0 += kPairChunk) {
+    constexpr int kRowVec = kPairChunk / 4;  // float4 per row of the chunk
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int e = tid + 256 * q, row = e >> 3, c4 = (e & 7) * 4;
+    for (int q = 0; q < 64 * kRowVec / 256; ++q) {
+      const int e = tid + 256 * q, row = e / kRowVec, c4 = (e % kRowVec) * 4;
       const int ia = i0 + row, jb = j0 + row;
       const f4 va = ia < na ? *(const f4*)(A + (long long)ia * ld + x0 + c4) : f4{0, 0, 0, 0};
       const f4 vb = jb < nb ? *(const f4*)(B + (long long)jb * ld + x0 + c4) : f4{0, 0, 0, 0};
@@ -133,7 +191,7 @@ __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A,
       *(f4*)&sB[row][c4] = vb;
     }
     __syncthreads();
-    const int m = min(kPbviChunk, n - x0);
+    const int m = min(kPairChunk, n - x0);
     int xx = 0;
     for (; xx + 4 <= m; xx += 4) {
       const float a0 = sAT[xx][la], a1 = sAT[xx + 1][la], a2 = sAT[xx + 2][la],
@@ -241,12 +299,17 @@ __global__ __launch_bounds__(256) void k_pbvi_pick(const float* __restrict__ l1,
 // C[i][k] = sum_x A[i][x] * B[k][x] with x in ascending order: each
 // v_mfma_f32_32x32x2_f32 step is fma(a[x+1], b[x+1], fma(a[x], b[x], c)),
 // lane half h holding x = 2t + h.  128x128 tiles, 4 waves of 64x64 (2x2
-// MFMA blocks), x-chunks of 32 staged through LDS with each row's 8-float
+// MFMA blocks), x-chunks of GK staged through LDS with each row's 8-float
 // groups stored as [h][s] (x = 8q + 2s + h -> 8q + 4h + s) so a lane reads
-// four consecutive steps with one ds_read_b128.
-constexpr int GT = kGemmTile, GK = kPbviChunk, GLD = 36;
+// four consecutive steps with one ds_read_b128; the next chunk's global loads
+// are in flight while the current one is multiplied.  146 VGPRs and 37 KB of
+// LDS keep three workgroups per CU: the 144-batch launch of a 500-belief set
+// (2304 tiles) is exactly three rounds of the 768 slots.
+constexpr int GT = kGemmTile, GK = 32, GLD = GK + 4;
+constexpr int GQ = GK / 8;               // 8-float groups per row chunk
+constexpr int GPAIRS = GT * GQ / 256;    // (row, group) pairs per thread per operand
 
-__global__ __launch_bounds__(256, 2) void k_gemm_nt(const float* __restrict__ A,
+__global__ __launch_bounds__(256, 3) void k_gemm_nt(const float* __restrict__ A,
                                                     const float* __restrict__ B,
                                                     float* __restrict__ C, int Mp, int Np, int ld,
                                                     long long bstride, long long cstride,
@@ -268,11 +331,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(const float* __restrict__ A,
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wi = w & 1, wk = w >> 1;
   const int r = lane & 31, h = lane >> 5;
 
-  f4 ra[2][2], rb[2][2];
+  f4 ra[GPAIRS][2], rb[GPAIRS][2];
   auto gload = [&](int x0) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = tid + 256 * q, row = p >> 2, c8 = (p & 3) * 8;
+    for (int q = 0; q < GPAIRS; ++q) {
+      const int p = tid + 256 * q, row = p / GQ, c8 = (p % GQ) * 8;
       const f4* pa = (const f4*)(Ab + (long long)row * ld + x0 + c8);
       const f4* pb = (const f4*)(Bb + (long long)row * ld + x0 + c8);
       ra[q][0] = pa[0];
@@ -283,8 +346,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(const float* __restrict__ A,
   };
   auto lstore = [&]() {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = tid + 256 * q, row = p >> 2, c8 = (p & 3) * 8;
+    for (int q = 0; q < GPAIRS; ++q) {
+      const int p = tid + 256 * q, row = p / GQ, c8 = (p % GQ) * 8;
       float* da = sA + row * GLD + c8;
       float* db = sB + row * GLD + c8;
       *(f4*)da = f4{ra[q][0].x, ra[q][0].z, ra[q][1].x, ra[q][1].z};
@@ -309,7 +372,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(const float* __restrict__ A,
     __syncthreads();
     if (x0 + GK < xe) gload(x0 + GK);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < GQ; ++q) {
       f4 a[2], b[2];
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib)
@@ -372,13 +435,17 @@ __global__ __launch_bounds__(256) void k_argmax_rows(const float* __restrict__ C
 
 __global__ __launch_bounds__(256) void k_pbvi_gamma_a(Geom g, PlaneSet R,
                                                       const float* __restrict__ G,
-                                                      long long gstride, int ld, int a,
+                                                      long long gstride, int ld, int a0,
                                                       const int* __restrict__ kstar, int kstride,
                                                       float* __restrict__ Ga) {
   const int W = g.width, H = g.rows;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= H * W) return;
   const int i = blockIdx.y, y = idx / W, x = idx - y * W;
+  const int a = a0 + blockIdx.z;
+  G += (long long)blockIdx.z * 16 * gstride;
+  kstar += blockIdx.z * 16 * kstride;
+  Ga += (long long)a * gstride;
   float v = R.p[(long long)y * R.rs + (long long)a * R.ps + x];
 #pragma unroll
   for (int o = 0; o < 16; ++o)
@@ -421,12 +488,13 @@ inline int cdiv(long long a, int b) { return (int)((a + b - 1) / b); }
 hipError_t launch_rows_seq(hipStream_t st, int mode, const float* A, int ld, int rows, int n,
                            float* sums, float* cdf) {
   if (rows <= 0) return hipSuccess;
+  const dim3 grid(cdiv(rows, kChainRows));
   if (mode == ROW_CDF)
-    hipLaunchKernelGGL(k_rows_seq<ROW_CDF>, dim3(cdiv(rows, 64)), dim3(64), 0, st, A, ld, rows,
+    hipLaunchKernelGGL(k_rows_chain<CH_CDF>, grid, dim3(256), 0, st, A, rows, nullptr, ld, rows,
                        n, sums, cdf);
   else
-    hipLaunchKernelGGL(k_rows_seq<ROW_SUM>, dim3(cdiv(rows, 64)), dim3(64), 0, st, A, ld, rows,
-                       n, sums, cdf);
+    hipLaunchKernelGGL(k_rows_chain<CH_SUM>, grid, dim3(256), 0, st, A, rows, nullptr, ld, rows,
+                       n, sums, nullptr);
   return hipGetLastError();
 }
 
@@ -440,8 +508,8 @@ hipError_t launch_rows_div(hipStream_t st, float* A, int ld, int rows, int n,
 hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float* B, int ld,
                            int rows, int n, float* out) {
   if (rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rows_dot, dim3(cdiv(rows, 64)), dim3(64), 0, st, A, amod, B, ld, rows, n,
-                     out);
+  hipLaunchKernelGGL(k_rows_chain<CH_DOT>, dim3(cdiv(rows, kChainRows)), dim3(256), 0, st, A,
+                     amod, B, ld, rows, n, out, nullptr);
   return hipGetLastError();
 }
 
@@ -497,11 +565,11 @@ hipError_t launch_argmax_rows(hipStream_t st, const float* C, int rows, int n, i
 }
 
 hipError_t launch_pbvi_gamma_a(hipStream_t st, const Geom& g, PlaneSet R, const float* G,
-                               long long gstride, int ld, int S, int a, const int* kstar,
-                               int kstride, float* Ga) {
-  if (S <= 0) return hipSuccess;
-  dim3 grid(cdiv((long long)g.rows * g.width, 256), S);
-  hipLaunchKernelGGL(k_pbvi_gamma_a, grid, dim3(256), 0, st, g, R, G, gstride, ld, a, kstar,
+                               long long gstride, int ld, int S, int a0, int a1,
+                               const int* kstar, int kstride, float* Ga) {
+  if (S <= 0 || a1 <= a0) return hipSuccess;
+  dim3 grid(cdiv((long long)g.rows * g.width, 256), S, a1 - a0);
+  hipLaunchKernelGGL(k_pbvi_gamma_a, grid, dim3(256), 0, st, g, R, G, gstride, ld, a0, kstar,
                      kstride, Ga);
   return hipGetLastError();
 }

@@ -18,7 +18,7 @@
 
 namespace pp2 {
 
-constexpr int kPbviChunk = 32;  // x-chunk of the row kernels and the GEMM (ld multiple)
+constexpr int kPbviChunk = 64;  // x-chunk of the pair kernel and the GEMM (ld multiple)
 constexpr int kGemmTile = 128;  // GEMM tile rows / cols (Sp multiple)
 
 enum PairOp { PAIR_L1 = 0, PAIR_DOT = 1 };
@@ -29,11 +29,12 @@ enum RowMode { ROW_SUM = 0, ROW_CDF = 1 };
 hipError_t launch_pbvi_update(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
                               const float* src, int ld, const int* src_row, const uint8_t* us,
                               const uint8_t* zs, int n, float* out);
-// G[o][k][x] = cudaComputeGammaOA(a, o) of alpha k, for o < 16, k < S
-// (rows k >= S and cells x >= hw are left untouched).
+// G[(a-a0)*16 + o][k][x] = cudaComputeGammaOA(a, o) of alpha k, for
+// a0 <= a < a1, o < 16, k < S (rows k >= S and cells x >= hw are left
+// untouched); ostride = floats between consecutive (a, o) slices.
 hipError_t launch_pbvi_gamma_ao(hipStream_t st, const Geom& g, float gamma, PlaneSet T,
-                                PlaneSet L, const float* alpha, int ld, int S, int a, float* G,
-                                long long ostride);
+                                PlaneSet L, const float* alpha, int ld, int S, int a0, int a1,
+                                float* G, long long ostride);
 
 // ---- pp2_pbvi_host.hip
 // ROW_SUM: sums[r] = ((A[r][0] + A[r][1]) + ...) over x < n (std::accumulate);
@@ -68,10 +69,12 @@ hipError_t launch_gemm_nt(hipStream_t st, const float* A, const float* B, float*
 // out[r] = first argmax over k < n of C[r*ldc + k]
 hipError_t launch_argmax_rows(hipStream_t st, const float* C, int rows, int n, int ldc,
                               int* out, float* vmax);
-// Gamma_a[i][x] = R[x][a] + G[0][k*[0][i]][x] + ... + G[15][k*[15][i]][x]
+// for a0 <= a < a1: Ga[a][i][x] = R[x][a] + G[(a-a0)16 + 0][k*][x] + ... +
+// G[(a-a0)16 + 15][k*][x], k* = kstar[((a-a0)16 + o) * kstride + i];
+// Ga's action slices are gstride floats apart, like G's (a, o) slices.
 hipError_t launch_pbvi_gamma_a(hipStream_t st, const Geom& g, PlaneSet R, const float* G,
-                               long long gstride, int ld, int S, int a, const int* kstar,
-                               int kstride, float* Ga);
+                               long long gstride, int ld, int S, int a0, int a1,
+                               const int* kstar, int kstride, float* Ga);
 // action of belief i = first argmax_a V[a*Sp + i]; alpha_out[i] = Ga[action][i]
 hipError_t launch_pbvi_select(hipStream_t st, const float* V, const float* Ga, int Sp, int S,
                               int ld, float* alpha_out, uint8_t* actions);

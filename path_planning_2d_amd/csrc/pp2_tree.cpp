@@ -22,6 +22,7 @@
 #include <rocrand/rocrand_xorwow.h>
 
 #include "pp2_ctx.h"
+#include "pp2_pbvi_internal.h"
 #include "pp2_rand.h"
 
 using namespace pp2rt;
@@ -115,6 +116,21 @@ struct pp2_planner {
   float* h_belief = nullptr;    // pinned normalised belief
   hipEvent_t ev_belief = nullptr;
 
+  // lower_bound_mode 1: PBVI leaf bounds (evaluatePbviCpu) of all 144
+  // (observation, action) children per expansion, as one split-x MFMA GEMM
+  // of the materialised children against the context's alpha vectors.
+  bool pbvi = false;
+  int lb_S = 0, lb_Sp = 0, lb_ld = 0, lb_split = 1;
+  float* d_parent = nullptr;    // [ld] the expanded belief, unnormalised
+  float* d_children = nullptr;  // [256][ld] its 144 children, row z*9 + a
+  float* d_lbpart = nullptr;    // [lb_split][256][Sp] split-x partial dots
+  float* d_lbdots = nullptr;    // [256][Sp]
+  int* d_lbidx = nullptr;
+  float* d_lbv = nullptr;
+  float* h_lbv = nullptr;       // pinned: max_k <row, alpha_k>
+  int* d_srow = nullptr;
+  uint8_t *d_us = nullptr, *d_zs = nullptr;
+
   VNode* root = nullptr;
   uint32_t n_vnodes = 0, n_qnodes = 0, expansions = 0;
 };
@@ -189,6 +205,27 @@ float fib_upper(const float* dots, float mass) {
     if (best < v) best = v;
   }
   return best;
+}
+
+// max_k <row r, alpha_k> for rows [0, nrows) of d_rows (ld floats each) into
+// h_lbv[r] (asynchronous; the caller synchronises the stream).
+int pbvi_row_max(pp2_planner* p, const float* d_rows, int nrows) {
+  pp2_ctx* c = p->ctx;
+  const float* al = nullptr;
+  int S = 0, Sp = 0, ld = 0;
+  CHECK(pbvi_alphas(c, &al, &S, &Sp, &ld));
+  if (S != p->lb_S || ld != p->lb_ld)
+    return set_err(PP2_ESTATE, "PBVI alpha vectors changed size since the planner was created");
+  const int Mp = (nrows + pp2::kGemmTile - 1) / pp2::kGemmTile * pp2::kGemmTile;
+  const long long sstride = (long long)Mp * Sp;
+  HIPCHK(pp2::launch_gemm_nt(c->stream, d_rows, al, p->d_lbpart, Mp, Sp, ld, 1, 0, 0,
+                             p->lb_split, sstride));
+  HIPCHK(pp2::launch_sum_splits(c->stream, p->d_lbpart, p->lb_split, sstride, (int)sstride,
+                                p->d_lbdots));
+  HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, nrows, S, Sp, p->d_lbidx, p->d_lbv));
+  HIPCHK(hipMemcpyAsync(p->h_lbv, p->d_lbv, nrows * sizeof(float), hipMemcpyDeviceToHost,
+                        c->stream));
+  return PP2_OK;
 }
 
 // QNode::update (search_tree_cuda.cu:251-286)
@@ -276,11 +313,16 @@ int make_root(pp2_planner* p, int s, uint8_t z, VNode** out) {
   HIPCHK(hipMemcpyAsync(p->h_out + kOutDots, p->d_out + kOutDots,
                         (kStatsPerChild + 1) * sizeof(float), hipMemcpyDeviceToHost,
                         c->stream));
+  if (p->pbvi) {
+    HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_children, nullptr));
+    CHECK(pbvi_row_max(p, p->d_children, 1));
+  }
   HIPCHK(hipStreamSynchronize(c->stream));
   VNode* v = new_vnode(p, z, 0.0f, nullptr);
   v->slot = s;
   v->upper_bound = fib_upper(p->h_out + kOutDots + 1, p->h_out[kOutMass]);
-  v->lower_bound = p->lb_const;
+  // evaluatePbviCpu on the normalised belief: max_k <b, alpha_k> / mass
+  v->lower_bound = p->pbvi ? p->h_lbv[0] / p->h_out[kOutMass] : p->lb_const;
   v->heuristic = v->upper_bound - v->lower_bound;
   *out = v;
   return PP2_OK;
@@ -353,6 +395,12 @@ int expand_vnode(pp2_planner* p, VNode* v) {
                         c->stream));
   HIPCHK(hipMemcpyAsync(p->h_out, p->d_out, kOutFloats * sizeof(float), hipMemcpyDeviceToHost,
                         c->stream));
+  if (p->pbvi) {
+    HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
+    HIPCHK(pp2::launch_pbvi_update(c->stream, c->g, c->T.v, c->L.v, p->d_parent, p->lb_ld,
+                                   p->d_srow, p->d_us, p->d_zs, 144, p->d_children));
+    CHECK(pbvi_row_max(p, p->d_children, 144));
+  }
   HIPCHK(hipEventSynchronize(p->ev_belief));
 
   std::vector<float> cdf(n);
@@ -382,7 +430,7 @@ int expand_vnode(pp2_planner* p, VNode* v) {
       const float* st = stats + ((size_t)z * 9 + a) * kStatsPerChild;
       VNode* cv = new_vnode(p, z, fq[a][k], q);
       cv->upper_bound = fib_upper(st + 1, st[0]);
-      cv->lower_bound = p->lb_const;
+      cv->lower_bound = p->pbvi ? p->h_lbv[z * 9 + a] / st[0] : p->lb_const;
       cv->heuristic = cv->upper_bound - cv->lower_bound;
       q->children.push_back(cv);
     }
@@ -465,6 +513,7 @@ int pp2_planner_default_params(pp2_planner_params* prm) {
   prm->max_online_iteration = 15;
   prm->lower_bound_mode = 0;
   prm->rand_seed = 1;
+  prm->rand_skip = 0;
   prm->sample_num = 50;
   prm->curand_seed = 1234;
   return PP2_OK;
@@ -491,9 +540,14 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   pp2_planner_params d;
   pp2_planner_default_params(&d);
   if (!prm) prm = &d;
-  if (prm->lower_bound_mode != 0)
-    return set_err(PP2_EINVAL, "lower_bound_mode %d not supported (0 = constant)",
+  if (prm->lower_bound_mode != 0 && prm->lower_bound_mode != 1)
+    return set_err(PP2_EINVAL, "lower_bound_mode %d not supported (0 = constant, 1 = PBVI)",
                    prm->lower_bound_mode);
+  const float* pal = nullptr;
+  int pS = 0, pSp = 0, pld = 0;
+  if (prm->lower_bound_mode == 1 && pbvi_alphas(c, &pal, &pS, &pSp, &pld) != PP2_OK)
+    return set_err(PP2_ESTATE, "lower_bound_mode 1 needs PBVI alpha vectors (pp2_pbvi_solve "
+                   "or pp2_pbvi_set)");
   if (prm->sample_num == 0) return set_err(PP2_EINVAL, "sample_num must be > 0");
   DeviceGuard dg(c->device);
   pp2_planner* p = new pp2_planner();
@@ -516,6 +570,7 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   p->u2.resize(prm->sample_num);
   pp2_curand_uniforms(prm->curand_seed, (int)prm->sample_num, p->u1.data(), p->u2.data());
   p->rng.seed(prm->rand_seed);
+  for (uint64_t k = 0; k < prm->rand_skip; ++k) (void)p->rng.next();
   const int tiles1 = pp2::cells_grid(c->g, 1);
   if ((s = alloc_planes(c, &p->P, 9))) return fail(s);
   if (hipMalloc(&p->d_rpart, (size_t)tiles1 * 9 * sizeof(float)) != hipSuccess ||
@@ -527,6 +582,40 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       hipHostMalloc(&p->h_belief, p->n * sizeof(float), hipHostMallocDefault) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_belief, hipEventDisableTiming) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "planner scratch allocation failed"));
+  if (prm->lower_bound_mode == 1) {
+    p->pbvi = true;
+    p->lb_S = pS;
+    p->lb_Sp = pSp;
+    p->lb_ld = pld;
+    // split x so that the 144-row product fills the chip (>= 768 workgroups)
+    const int tiles = (256 / pp2::kGemmTile) * (pSp / pp2::kGemmTile);
+    p->lb_split = std::max(1, std::min((768 + tiles - 1) / tiles, pld / 64));
+    const size_t rows = (size_t)256 * pld, dots = (size_t)256 * pSp;
+    std::vector<int> srow(144, 0);
+    std::vector<uint8_t> us(144), zs(144);
+    for (int k = 0; k < 144; ++k) {
+      us[k] = (uint8_t)(k % 9);
+      zs[k] = (uint8_t)(k / 9);
+    }
+    if (hipMalloc(&p->d_parent, (size_t)pld * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_children, rows * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_lbpart, (size_t)p->lb_split * dots * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_lbdots, dots * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_lbidx, 256 * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->d_lbv, 256 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_srow, 144 * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->d_us, 144) != hipSuccess || hipMalloc(&p->d_zs, 144) != hipSuccess ||
+        hipHostMalloc(&p->h_lbv, 256 * sizeof(float), hipHostMallocDefault) != hipSuccess)
+      return fail(set_err(PP2_ENOMEM, "planner PBVI scratch allocation failed"));
+    if (hipMemsetAsync(p->d_parent, 0, (size_t)pld * sizeof(float), c->stream) != hipSuccess ||
+        hipMemsetAsync(p->d_children, 0, rows * sizeof(float), c->stream) != hipSuccess ||
+        hipMemcpyAsync(p->d_srow, srow.data(), 144 * sizeof(int), hipMemcpyHostToDevice,
+                       c->stream) != hipSuccess ||
+        hipMemcpyAsync(p->d_us, us.data(), 144, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(p->d_zs, zs.data(), 144, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      return fail(set_err(PP2_EHIP, "planner PBVI scratch initialisation failed"));
+  }
   *out = p;
   return PP2_OK;
 }
@@ -548,8 +637,12 @@ int pp2_planner_destroy(pp2_planner* p) {
     if (s.mass) (void)hipFree(s.mass);
   }
   free_planes(&p->P);
-  for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_out, p->d_dense})
+  for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_out, p->d_dense, p->d_parent,
+                   p->d_children, p->d_lbpart, p->d_lbdots, p->d_lbv})
     if (d) (void)hipFree(d);
+  for (void* d : {(void*)p->d_lbidx, (void*)p->d_srow, (void*)p->d_us, (void*)p->d_zs})
+    if (d) (void)hipFree(d);
+  if (p->h_lbv) (void)hipHostFree(p->h_lbv);
   if (p->h_out) (void)hipHostFree(p->h_out);
   if (p->h_belief) (void)hipHostFree(p->h_belief);
   if (p->ev_belief) (void)hipEventDestroy(p->ev_belief);

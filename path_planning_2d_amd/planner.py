@@ -21,7 +21,8 @@ class PlannerParams(C.Structure):
                 ("lower_bound_mode", C.c_int32),
                 ("rand_seed", C.c_uint32),
                 ("sample_num", C.c_uint32),
-                ("curand_seed", C.c_uint64)]
+                ("curand_seed", C.c_uint64),
+                ("rand_skip", C.c_uint64)]
 
 
 class TreeInfo(C.Structure):

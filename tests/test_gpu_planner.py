@@ -121,3 +121,59 @@ def test_planner_256_plan_step(oracle):
                 compare(gpl.info(), opl.info(), f"256 step {k + 1}")
                 assert a_g == a_o
         opl.close()
+
+
+@pytest.mark.parametrize("name,S,max_depth,steps", [
+    ("map_10x10", 64, 50, 5),
+    ("sparse_map_100x40", 500, 5, 4),   # the reference node: S = 500, PBVI leaves
+])
+def test_planner_pbvi_lower_bound(oracle, name, S, max_depth, steps):
+    """lower_bound_mode 1: every VNode's lower bound is evaluatePbviCpu over
+    the context's PBVI alphas (search_tree_cuda.cu:379), and the tree's rand()
+    stream continues after generateBeliefSet's draws, as in the reference node
+    (PomdpPathPlanning2d::initialize runs PBVI before the first plan step)."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S_
+    grid = golden_map(name)
+    m = golden("model", name)
+    b0 = S_.uniform_belief(grid)
+    with P.GridContext(grid, tuple(m["goal"]), gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_solve()
+        alphas = ctx.fib_get()
+        calls = ctx.pbvi_solve(b0, S)
+        pal, pact = ctx.pbvi_get()
+        opl = oracle.Planner(grid, m["T"], m["L"], m["R"], alphas, max_depth=max_depth,
+                             max_iter=15, accurate=True)
+        opl.set_pbvi(pal, pact)
+        opl.skip_rand(calls)
+        with P.QVTreePlanner(ctx, max_search_tree_depth=max_depth, max_online_iteration=15,
+                             lower_bound_mode=1, rand_skip=calls) as gpl:
+            a_g, v_g = gpl.step(0, 0, b0)
+            a_o, v_o = opl.step(0, 0, b0)
+            gi = gpl.info()
+            compare(gi, opl.info(), f"{name} pbvi step 0")
+            assert a_g == a_o and rel_close(v_g, v_o)
+            # PBVI is a lower bound: nowhere above the FIB upper bound
+            assert gi["root_lower_bound"] <= gi["root_upper_bound"] + 1e-3
+            assert gi["root_lower_bound"] > -5.0 / (1.0 - 0.95)
+            _, zs, _ = S_.synth_trajectory(grid, steps, seed=11)
+            for k in range(steps):
+                a_g, v_g = gpl.step(a_o, int(zs[k]))
+                a_o, v_o = opl.step(a_o, int(zs[k]))
+                compare(gpl.info(), opl.info(), f"{name} pbvi step {k + 1}")
+                assert a_g == a_o and rel_close(v_g, v_o)
+    opl.close()
+
+
+def test_planner_pbvi_needs_alphas():
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S_
+    g = S_.synth_grid(12, 12, 2)
+    g[0, 0] = 0
+    with P.GridContext(g, (0, 0), gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        with pytest.raises(P.Pp2Error):
+            P.QVTreePlanner(ctx, lower_bound_mode=1)
+        with pytest.raises(P.Pp2Error):
+            P.QVTreePlanner(ctx, lower_bound_mode=2)
