@@ -43,6 +43,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFLOPS = 157.3     # dense f32-input MFMA peak (MI355X_MICROARCH.md, Matrix cores)
 BYTES_SWEEP = 369                # per cell: T 324 + C 36 + J 4 + J' 4 + A 1
 BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
 BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
@@ -74,6 +75,8 @@ def parse():
                     help="batched fp16 rollout copies (0 disables)")
     ap.add_argument("--rollout-depth", type=int, default=5)
     ap.add_argument("--rollout-size", type=int, default=512)
+    ap.add_argument("--pbvi-S", type=int, default=500, help="PBVI belief set size")
+    ap.add_argument("--no-pbvi", action="store_true", help="skip the PBVI leg")
     ap.add_argument("--dense", action="store_true",
                     help="time the dense-plane kernels as the main loop")
     ap.add_argument("--profile", action="store_true",
@@ -173,6 +176,42 @@ def cpu_baseline(grid, goal, us, zs, budget_s):
             "cpu": cpu_model(), "host_cpus": os.cpu_count()}
 
 
+def closed_loop(grid, b0, step_fn, max_steps, budget_s):
+    """Closed-loop plan steps: the planner's action moves a simulated robot
+    (T), whose observation (L) is the next message.  Returns the wall time of
+    each step in ms."""
+    from path_planning_2d_amd import synthetic as S
+    rng = S.SplitMix64(99)
+    x, y = S.start_cell(grid)
+    times = []
+    a, z, first = 0, 0, True
+    t_start = time.perf_counter()
+    for _ in range(max_steps):
+        t = time.perf_counter()
+        a, _ = step_fn(a, z, b0 if first else None)
+        times.append(time.perf_counter() - t)
+        first = False
+        tp = S.cell_transition(grid, x, y, a)
+        r, c, j = rng.u01(), 0.0, 4
+        for i in range(9):
+            c += float(tp[i])
+            if tp[i] > 0 and r < c:
+                j = i
+                break
+        x += j % 3 - 1
+        y += j // 3 - 1
+        lk = S.cell_likelihood(grid, x, y)
+        r, c, z = rng.u01(), 0.0, 15
+        for i in range(16):
+            c += float(lk[i])
+            if r < c:
+                z = i
+                break
+        if time.perf_counter() - t_start > budget_s:
+            break
+    return np.array(times) * 1e3
+
+
 def plan_step_bench(args, device, stream_handle, with_cpu):
     """BASELINE configs[1]: 256x256 synthetic grid, POMDP belief update +
     QV-tree with max_search_tree_depth 3 (FIB upper bound, constant lower
@@ -195,36 +234,7 @@ def plan_step_bench(args, device, stream_handle, with_cpu):
     b0 = S.uniform_belief(grid)
 
     def run(step_fn, max_steps, budget_s):
-        rng = S.SplitMix64(99)
-        x, y = S.start_cell(grid)
-        times = []
-        a, z, first = 0, 0, True
-        t_start = time.perf_counter()
-        for _ in range(max_steps):
-            t = time.perf_counter()
-            a, _ = step_fn(a, z, b0 if first else None)
-            times.append(time.perf_counter() - t)
-            first = False
-            tp = S.cell_transition(grid, x, y, a)
-            r, c, j = rng.u01(), 0.0, 4
-            for i in range(9):
-                c += float(tp[i])
-                if tp[i] > 0 and r < c:
-                    j = i
-                    break
-            x += j % 3 - 1
-            y += j // 3 - 1
-            lk = S.cell_likelihood(grid, x, y)
-            r, c, z = rng.u01(), 0.0, 15
-            for i in range(16):
-                c += float(lk[i])
-                if r < c:
-                    z = i
-                    break
-            if time.perf_counter() - t_start > budget_s:
-                break
-        ms = np.array(times) * 1e3
-        return ms
+        return closed_loop(grid, b0, step_fn, max_steps, budget_s)
 
     with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
                          max_online_iteration=15) as pl:
@@ -251,6 +261,95 @@ def plan_step_bench(args, device, stream_handle, with_cpu):
             "sample": f"{cms.size} closed-loop plan steps of the oracle's reference-semantics "
                       f"QV-tree (oracle/pp2_oracle_tree.c, every node holds a host belief), "
                       f"same grid/alphas"}
+    return out
+
+
+def pbvi_bench(args, device, stream_handle, with_cpu):
+    """PBVI lower bound (point_based_value_iteration_cuda.cu): the reference
+    node's configuration -- S = 500 beliefs on the 100x40 map, 167 backups
+    (gamma 0.95) -- end to end, and the same at 256x256 (BASELINE configs[1]'s
+    grid, which the reference cannot run), followed there by
+    closed-loop plan steps with PBVI leaf lower bounds.  `gemm_equiv_tflops` = the iteration's Sgemm flops (2 * 144 *
+    Sp^2 * ld) / the whole iteration's time: a lower bound on the MFMA GEMM
+    kernel's own rate (its rocprof time is in profiles/)."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden")
+    out = {}
+    cases = [("sparse_map_100x40 (reference node: S=500, 167 backups)",
+              np.load(os.path.join(gold, "maps", "sparse_map_100x40.npy"), allow_pickle=False),
+              (95, 34), 0)]
+    g256 = S.synth_grid(256, 256, seed=256)
+    cases.append((f"256x256 synthetic, S={args.pbvi_S}", g256, S.synth_goal(g256), 0))
+    for label, grid, goal, iters in cases:
+        with P.GridContext(grid, goal, gamma=GAMMA, device=device) as ctx:
+            ctx.set_stream(stream_handle)
+            ctx.model_generate()
+            b0 = S.uniform_belief(grid)
+            ctx.pbvi_belief_set(b0, 8)  # warm-up: code objects, allocations
+            ctx.pbvi_backup(1)
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            ctx.pbvi_belief_set(b0, args.pbvi_S)
+            ctx.synchronize()
+            t_set = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            ctx.pbvi_backup(iters)
+            ctx.synchronize()
+            t_bk = time.perf_counter() - t0
+            plan = None
+            if iters == 0 and grid.shape == (256, 256) and args.plan_steps > 0:
+                # BASELINE configs[1] with the reference node's PBVI leaf bounds
+                # (the reference itself falls back to -5/(1-gamma) there)
+                ctx.fib_solve()
+                with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
+                                     max_online_iteration=15, lower_bound_mode=1) as pl:
+                    closed_loop(grid, b0, pl.step, 3, 1e9)
+                    pl.reset()
+                    ms = closed_loop(grid, b0, pl.step, args.plan_steps, 1e9)
+                plan = {"config": f"256x256 synthetic grid, max_search_tree_depth {args.plan_depth}, "
+                                  f"max_online_iteration 15, FIB upper bound, PBVI lower bound "
+                                  f"(S={args.pbvi_S}, 167 backups)",
+                        "steps": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
+                        "p90_ms": float(np.percentile(ms, 90)), "mean_ms": float(ms.mean())}
+            n_it = iters if iters > 0 else int(np.ceil(np.log(np.float32(1e-3) / np.float32(5))
+                                                       / np.log(np.float32(GAMMA))))
+            Sp = (args.pbvi_S + 127) // 128 * 128
+            ld = (grid.size + 63) // 64 * 64
+            flop = 2.0 * 144 * Sp * Sp * ld
+            v, _ = ctx.pbvi_evaluate(b0[None, :])
+        key = "ref_100x40" if grid.shape == (40, 100) else "synth_256"
+        out[key] = {"config": label, "S": args.pbvi_S, "iterations": n_it,
+                    "belief_set_s": t_set, "backup_s": t_bk,
+                    "backup_iter_ms": 1e3 * t_bk / n_it,
+                    "gemm_equiv_tflops": flop * n_it / t_bk / 1e12,
+                    "mfma_f32_peak_tflops": MFMA_F32_PEAK_TFLOPS,
+                    "root_lower_bound": float(v[0])}
+        if plan is not None:
+            out[key]["plan_step_pbvi_lb"] = plan
+    if with_cpu:
+        from oracle import oracle as O
+        grid = cases[0][1]
+        H, W = grid.shape
+        T, L, R = O.model_pomdp(grid, (95, 34))
+        b0 = S.uniform_belief(grid)
+        t0 = time.perf_counter()
+        B, _ = O.pbvi_belief_set(H, W, T, L, b0, args.pbvi_S)
+        cs = time.perf_counter() - t0
+        s_small = 64
+        t0 = time.perf_counter()
+        O.pbvi_backup(H, W, GAMMA, T, L, R, B[:s_small], iterations=1)
+        cb = time.perf_counter() - t0
+        it_cpu = cb * (args.pbvi_S / s_small) ** 2
+        n_it = out["ref_100x40"]["iterations"]
+        out["cpu_baseline"] = {
+            "belief_set_s": cs, "backup_iter_s_extrapolated": it_cpu,
+            "total_s_extrapolated": cs + it_cpu * n_it, "cores": 1, "kind": "port",
+            "sample": f"oracle/pp2_oracle_pbvi.c on 100x40: generateBeliefSet at S={args.pbvi_S} "
+                      f"timed in full; one backup at S={s_small} timed and scaled by "
+                      f"(S/{s_small})^2 (the per-(a,o) Sgemm dominates)"}
+        out["speedup_vs_cpu"] = out["cpu_baseline"]["total_s_extrapolated"] / (
+            out["ref_100x40"]["belief_set_s"] + out["ref_100x40"]["backup_s"])
     return out
 
 
@@ -449,6 +548,9 @@ def main():
     if rank == 0 and ws == 1 and args.plan_steps > 0:
         plan = plan_step_bench(args, local, stream.cuda_stream,
                                with_cpu=not args.no_cpu_baseline)
+    pbvi = None
+    if rank == 0 and ws == 1 and not args.no_pbvi:
+        pbvi = pbvi_bench(args, local, stream.cuda_stream, with_cpu=not args.no_cpu_baseline)
     rollout = None
     if rank == 0 and ws == 1 and args.rollout_copies > 0:
         rollout = rollout_bench(args, local, stream)
@@ -515,6 +617,7 @@ def main():
             "belief_mass_ok": mass_ok,
             "plan_step": plan,
             "rollout": rollout,
+            "pbvi": pbvi,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result))

@@ -120,7 +120,7 @@ template <bool SPARSE>
 struct Layout {
   static constexpr int row = SPARSE ? kSpRow : kDictTC;
   static constexpr int blk = SPARSE ? 6 : 10;  // floats per action block
-  static constexpr int tu = SPARSE ? 4 : 9;    // raw T_u floats per entry (belief gather)
+  static constexpr int tu = tu_width(SPARSE);  // raw T_u floats per entry (belief gather)
 };
 
 // Global -> LDS copy of n floats with LDS-DMA (global_load_lds_dwordx4: no
@@ -484,7 +484,7 @@ void allow_lds(const void* fn, bool& done) {
 
 size_t coded_loop_lds_bytes(int E, bool sparse) {
   return ((size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) + lds_span(E) +
-          lds_span(E * (sparse ? 4 : 9))) * sizeof(float);
+          lds_span(E * tu_width(sparse))) * sizeof(float);
 }
 
 hipError_t launch_dict_hash(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,

@@ -125,6 +125,10 @@ constexpr int kDictMax = 400;  // coded_loop_lds_bytes(kDictMax, false) <= kDict
 // kSupN[a]) (base_kernel in pp2_kernels.hip; occupied neighbours and traps
 // only move mass to the centre, which is in every support), then C_a, then 0.
 constexpr int kSpRow = 54;  // 9 actions x 6 floats
+// Raw T_u floats per entry in the belief gather's LDS table: the support
+// cells (sparse, 4) or all 9, padded to an odd stride so that two codes land
+// on the same LDS bank only when they differ by a multiple of 64.
+constexpr int tu_width(bool sparse) { return sparse ? 5 : 9; }
 constexpr int kSupN[9] = {4, 4, 4, 4, 1, 4, 4, 4, 4};
 constexpr int kSup[9][4] = {{0, 1, 3, 4}, {0, 1, 2, 4}, {1, 2, 4, 5}, {0, 3, 4, 6}, {4, 0, 0, 0},
                             {2, 4, 5, 8}, {3, 4, 6, 7}, {4, 6, 7, 8}, {4, 5, 7, 8}};

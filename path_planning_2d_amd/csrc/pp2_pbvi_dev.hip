@@ -39,22 +39,25 @@ __global__ __launch_bounds__(kThreads) void k_pbvi_update(
   out[(long long)c * ld + idx] = p * L.p[(long long)y * L.rs + (long long)z * L.ps + x];
 }
 
-// One thread = one cell x and kGaoRows alpha vectors: the 16x9 products
-// T[x][a][s] * L[nbr_s(x)][o] stay in registers across the alpha rows.
+// One thread = one cell x, kGaoRows alpha vectors and 8 of the 16
+// observations: the 8x9 products T[x][a][s] * L[nbr_s(x)][o] stay in
+// registers across the alpha rows (blockIdx.z = 2 * action + half).
 // Off-grid neighbours enter as 0 * 0 terms, which leave the chain unchanged
-// (it never holds -0), exactly as the reference's skipped terms.
+// (it never holds -0), exactly as the reference's skipped terms.  The slices
+// are written once and read back by the GEMM after more than the Infinity
+// Cache has streamed by: non-temporal stores.
 __global__ __launch_bounds__(kThreads) void k_pbvi_gamma_ao(
     Geom g, float gamma, PlaneSet T, PlaneSet L, const float* __restrict__ alpha, int ld, int S,
     int a0, float* __restrict__ G, long long ostride) {
   const int W = g.width, H = g.rows;
-  const int a = a0 + blockIdx.z;
-  G += (long long)blockIdx.z * 16 * ostride;
+  const int a = a0 + (blockIdx.z >> 1), o0 = (blockIdx.z & 1) * 8;
+  G += ((long long)(blockIdx.z >> 1) * 16 + o0) * ostride;
   const int idx = blockIdx.x * kThreads + threadIdx.x;
   if (idx >= H * W) return;
   const int y = idx / W, x = idx - y * W;
   int off[9];
   bool ok[9];
-  float tm[16][9];
+  float tm[8][9];
 #pragma unroll
   for (int s = 0; s < 9; ++s) {
     const int sy = y + s / 3 - 1, sx = x + s % 3 - 1;
@@ -62,8 +65,8 @@ __global__ __launch_bounds__(kThreads) void k_pbvi_gamma_ao(
     off[s] = ok[s] ? sy * W + sx : idx;
     const float t = T.p[(long long)y * T.rs + (long long)(9 * a + s) * T.ps + x];
 #pragma unroll
-    for (int o = 0; o < 16; ++o)
-      tm[o][s] = ok[s] ? t * L.p[(long long)(ok[s] ? sy : y) * L.rs + (long long)o * L.ps +
+    for (int o = 0; o < 8; ++o)
+      tm[o][s] = ok[s] ? t * L.p[(long long)(ok[s] ? sy : y) * L.rs + (long long)(o0 + o) * L.ps +
                                  (ok[s] ? sx : x)]
                        : 0.0f;
   }
@@ -74,11 +77,11 @@ __global__ __launch_bounds__(kThreads) void k_pbvi_gamma_ao(
 #pragma unroll
     for (int s = 0; s < 9; ++s) av[s] = ok[s] ? al[off[s]] : 0.0f;
 #pragma unroll
-    for (int o = 0; o < 16; ++o) {
+    for (int o = 0; o < 8; ++o) {
       float acc = 0.0f;
 #pragma unroll
       for (int s = 0; s < 9; ++s) acc = fmaf(tm[o][s], av[s], acc);
-      G[o * ostride + (long long)k * ld + idx] = gamma * acc;
+      __builtin_nontemporal_store(gamma * acc, G + o * ostride + (long long)k * ld + idx);
     }
   }
 }
@@ -101,7 +104,7 @@ hipError_t launch_pbvi_gamma_ao(hipStream_t st, const Geom& g, float gamma, Plan
                                 float* G, long long ostride) {
   if (S <= 0 || a1 <= a0) return hipSuccess;
   const int hw = g.rows * g.width;
-  dim3 grid((hw + kThreads - 1) / kThreads, (S + kGaoRows - 1) / kGaoRows, a1 - a0);
+  dim3 grid((hw + kThreads - 1) / kThreads, (S + kGaoRows - 1) / kGaoRows, 2 * (a1 - a0));
   hipLaunchKernelGGL(k_pbvi_gamma_ao, grid, dim3(kThreads), 0, st, g, gamma, T, L, alpha, ld, S,
                      a0, G, ostride);
   return hipGetLastError();

@@ -301,21 +301,21 @@ __global__ __launch_bounds__(256) void k_pbvi_pick(const float* __restrict__ l1,
 // lane half h holding x = 2t + h.  128x128 tiles, 4 waves of 64x64 (2x2
 // MFMA blocks), x-chunks of GK staged through LDS with each row's 8-float
 // groups stored as [h][s] (x = 8q + 2s + h -> 8q + 4h + s) so a lane reads
-// four consecutive steps with one ds_read_b128; the next chunk's global loads
-// are in flight while the current one is multiplied.  146 VGPRs and 37 KB of
-// LDS keep three workgroups per CU: the 144-batch launch of a 500-belief set
-// (2304 tiles) is exactly three rounds of the 768 slots.
+// four consecutive steps with one ds_read_b128.  The next chunk's global
+// loads and LDS stores overlap the current chunk's MFMAs (double-buffered
+// LDS, one barrier per chunk), and each 4-step group's fragments are read
+// while the previous group multiplies.
 constexpr int GT = kGemmTile, GK = 32, GLD = GK + 4;
 constexpr int GQ = GK / 8;               // 8-float groups per row chunk
 constexpr int GPAIRS = GT * GQ / 256;    // (row, group) pairs per thread per operand
 
-__global__ __launch_bounds__(256, 3) void k_gemm_nt(const float* __restrict__ A,
+__global__ __launch_bounds__(256, 2) void k_gemm_nt(const float* __restrict__ A,
                                                     const float* __restrict__ B,
                                                     float* __restrict__ C, int Mp, int Np, int ld,
                                                     long long bstride, long long cstride,
                                                     int ksplit, int kchunk, long long sstride) {
-  __shared__ __attribute__((aligned(16))) float sA[GT * GLD];
-  __shared__ __attribute__((aligned(16))) float sB[GT * GLD];
+  __shared__ __attribute__((aligned(16))) float sA[2][GT * GLD];
+  __shared__ __attribute__((aligned(16))) float sB[2][GT * GLD];
   const int ti_n = Mp / GT, tk_n = Np / GT;
   const int L = xcd_map(blockIdx.x, gridDim.x);
   const int ti = L % ti_n;
@@ -344,12 +344,12 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(const float* __restrict__ A,
       rb[q][1] = pb[1];
     }
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < GPAIRS; ++q) {
       const int p = tid + 256 * q, row = p / GQ, c8 = (p % GQ) * 8;
-      float* da = sA + row * GLD + c8;
-      float* db = sB + row * GLD + c8;
+      float* da = sA[buf] + row * GLD + c8;
+      float* db = sB[buf] + row * GLD + c8;
       *(f4*)da = f4{ra[q][0].x, ra[q][0].z, ra[q][1].x, ra[q][1].z};
       *(f4*)(da + 4) = f4{ra[q][0].y, ra[q][0].w, ra[q][1].y, ra[q][1].w};
       *(f4*)db = f4{rb[q][0].x, rb[q][0].z, rb[q][1].x, rb[q][1].z};
@@ -365,21 +365,32 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(const float* __restrict__ A,
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[ib][kb][v] = 0.0f;
 
-  if (xb < xe) gload(xb);
+  // LDS double buffer: chunk c is multiplied from buffer c&1 while chunk c+1
+  // goes global -> registers -> buffer (c+1)&1; one barrier per chunk.
+  if (xb < xe) {
+    gload(xb);
+    lstore(0);
+  }
+  __syncthreads();
+  int buf = 0;
   for (int x0 = xb; x0 < xe; x0 += GK) {
-    __syncthreads();
-    lstore();
-    __syncthreads();
-    if (x0 + GK < xe) gload(x0 + GK);
+    const bool more = x0 + GK < xe;
+    if (more) gload(x0 + GK);
+    const float* __restrict__ pa = sA[buf] + (wi * 64 + r) * GLD + 4 * h;
+    const float* __restrict__ pb = sB[buf] + (wk * 64 + r) * GLD + 4 * h;
+    f4 a[2], b[2], an[2], bn[2];
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) a[ib] = *(const f4*)(pa + ib * 32 * GLD);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) b[kb] = *(const f4*)(pb + kb * 32 * GLD);
 #pragma unroll
     for (int q = 0; q < GQ; ++q) {
-      f4 a[2], b[2];
+      if (q + 1 < GQ) {  // next group's fragments in flight during this group's MFMAs
 #pragma unroll
-      for (int ib = 0; ib < 2; ++ib)
-        a[ib] = *(const f4*)(sA + (wi * 64 + ib * 32 + r) * GLD + 8 * q + 4 * h);
+        for (int ib = 0; ib < 2; ++ib) an[ib] = *(const f4*)(pa + ib * 32 * GLD + 8 * (q + 1));
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        b[kb] = *(const f4*)(sB + (wk * 64 + kb * 32 + r) * GLD + 8 * q + 4 * h);
+        for (int kb = 0; kb < 2; ++kb) bn[kb] = *(const f4*)(pb + kb * 32 * GLD + 8 * (q + 1));
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -388,7 +399,17 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(const float* __restrict__ A,
           for (int kb = 0; kb < 2; ++kb)
             acc[ib][kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ib][s], b[kb][s], acc[ib][kb],
                                                                0, 0, 0);
+      if (q + 1 < GQ) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          a[e] = an[e];
+          b[e] = bn[e];
+        }
+      }
     }
+    if (more) lstore(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
   }
   // C/D map of the 32x32 forms: register v of lane l is row (v&3) + 8(v>>2) + 4h, column r
 #pragma unroll

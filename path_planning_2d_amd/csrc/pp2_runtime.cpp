@@ -392,7 +392,7 @@ int build_model_dict(pp2_ctx* c) {
         if (!in && bits != 0) { sparse = false; break; }
       }
   const int rw = sparse ? pp2::kSpRow : pp2::kDictTC;
-  const int tw = sparse ? 4 : 9;
+  const int tw = pp2::tu_width(sparse);
   const int es = (E + 3) & ~3;  // L_z column stride (16-B aligned columns)
   std::vector<float> rows((size_t)E * rw + 4, 0.0f), dl((size_t)16 * es, 0.0f);
   const size_t tstride = ((size_t)E * tw + 3) & ~(size_t)3;  // 16-B aligned per action
@@ -529,7 +529,7 @@ int pp2rt::loop_launch(pp2_ctx* c, int e, uint8_t u, uint8_t z, const float* in_
   if (coded_active(c)) {
     HIPCHK(pp2::launch_loop_step_coded(c->stream, g, c->gamma, c->d_code - e * wp, c->d_rows,
                                        c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3),
-                                       c->d_tu + (size_t)u * (((size_t)c->dict_n * (c->dict_sparse ? 4 : 9) + 3) & ~(size_t)3),
+                                       c->d_tu + (size_t)u * (((size_t)c->dict_n * pp2::tu_width(c->dict_sparse) + 3) & ~(size_t)3),
                                        c->dict_n, c->dict_sparse, b_in, b_out, u, in_partials,
                                        in_n, in_sum, in_sum_out, c->pbuf[bn], J_in, J_out, A,
                                        e, e + c->g.rows, scale));
