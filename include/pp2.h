@@ -97,6 +97,10 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           halo exchange = halo rows exchanged, 1..8
  *                           (default: the most the smallest shard allows) */
 #define PP2_TUNE_HALO_DEPTH 4
+/*  PP2_TUNE_COMM_STREAM     0 (default): RCCL calls are issued on the context's
+ *                           stream; 1: on a dedicated stream entered and left
+ *                           through events */
+#define PP2_TUNE_COMM_STREAM 5
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
 /* ---------------------------------------------------------------- model

@@ -98,6 +98,7 @@ class GridContext:
     TUNE_NT_STREAMS = 2
     TUNE_CODED_MODEL = 3
     TUNE_HALO_DEPTH = 4
+    TUNE_COMM_STREAM = 5
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))

@@ -110,7 +110,8 @@ struct pp2_ctx {
 
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-  hipStream_t comm_stream = nullptr;  // every RCCL operation of the context, in issue order
+  hipStream_t comm_stream = nullptr;  // RCCL operations when use_comm_stream (PP2_TUNE_COMM_STREAM)
+  bool use_comm_stream = false;
   hipEvent_t ev_enter = nullptr, ev_leave = nullptr;
   pp2_shard_group* group = nullptr;  // single-process shard group, if any
   int grank = 0;                     // rank (row-block order) inside the group

@@ -87,16 +87,21 @@ const Planes& halo_planes(pp2_ctx* c, HaloKind k) {
   }
 }
 
-// Every RCCL operation of a context runs on its comm stream, in host issue
-// order (the same on every rank); comm_enter / comm_leave hand the work over
-// from / back to the compute stream.
+// Every RCCL operation of a context is issued in host order (the same on
+// every rank) on cst(c): by default the compute stream itself, so a block
+// start costs no cross-stream hand-off; with PP2_TUNE_COMM_STREAM 1 a
+// dedicated comm stream, entered and left through events.
+hipStream_t cst(const pp2_ctx* c) { return c->use_comm_stream ? c->comm_stream : c->stream; }
+
 int comm_enter(pp2_ctx* c) {
+  if (!c->use_comm_stream) return PP2_OK;
   HIPCHK(hipEventRecord(c->ev_enter, c->stream));
   HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_enter, 0));
   return PP2_OK;
 }
 
 int comm_leave(pp2_ctx* c) {
+  if (!c->use_comm_stream) return PP2_OK;
   HIPCHK(hipEventRecord(c->ev_leave, c->comm_stream));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_leave, 0));
   return PP2_OK;
@@ -121,14 +126,14 @@ int exchange_halos_k(pp2_ctx* c, std::initializer_list<HaloKind> kinds, int k) {
     const long long rs = P->v.rs;
     const size_t n = (size_t)k * rs;
     if (c->rank > 0) {
-      NCCLCHK(ncclSend(p, n, ncclFloat, c->rank - 1, c->comm, c->comm_stream));
-      NCCLCHK(ncclRecv(p - k * rs, n, ncclFloat, c->rank - 1, c->comm, c->comm_stream));
+      NCCLCHK(ncclSend(p, n, ncclFloat, c->rank - 1, c->comm, cst(c)));
+      NCCLCHK(ncclRecv(p - k * rs, n, ncclFloat, c->rank - 1, c->comm, cst(c)));
     }
     if (c->rank < c->nranks - 1) {
       NCCLCHK(ncclSend(p + (long long)(c->g.rows - k) * rs, n, ncclFloat, c->rank + 1, c->comm,
-                       c->comm_stream));
+                       cst(c)));
       NCCLCHK(ncclRecv(p + (long long)c->g.rows * rs, n, ncclFloat, c->rank + 1, c->comm,
-                       c->comm_stream));
+                       cst(c)));
     }
   }
   NCCLCHK(ncclGroupEnd());
@@ -142,7 +147,7 @@ int exchange_halos(pp2_ctx* c, std::initializer_list<HaloKind> kinds) {
 int allreduce_mass(pp2_ctx* c, float* d) {
   if (!c->comm) return PP2_OK;
   CHECK(comm_enter(c));
-  NCCLCHK(ncclAllReduce(d, d, 1, ncclFloat, ncclSum, c->comm, c->comm_stream));
+  NCCLCHK(ncclAllReduce(d, d, 1, ncclFloat, ncclSum, c->comm, cst(c)));
   return comm_leave(c);
 }
 
@@ -156,7 +161,7 @@ int absdiff_max(pp2_ctx* c, const Planes& cur, const Planes& snap, double* out) 
     HIPCHK(hipMemcpyAsync(c->rpartials, &m, sizeof(float), hipMemcpyHostToDevice, c->stream));
     CHECK(comm_enter(c));
     NCCLCHK(ncclAllReduce(c->rpartials, c->rpartials, 1, ncclFloat, ncclMax, c->comm,
-                          c->comm_stream));
+                          cst(c)));
     CHECK(comm_leave(c));
     HIPCHK(hipMemcpyAsync(&m, c->rpartials, sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -690,6 +695,11 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
     case PP2_TUNE_CODED_MODEL: c->use_coded = value != 0; return PP2_OK;
+    case PP2_TUNE_COMM_STREAM:
+      if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      c->use_comm_stream = value != 0;
+      return PP2_OK;
     case PP2_TUNE_HALO_DEPTH:
       if (value < 1 || value > c->kdepth_max)
         return set_err(PP2_EINVAL, "halo depth %d not in [1, %d]", value, c->kdepth_max);
@@ -1007,7 +1017,7 @@ int pp2_shard_comm_init(pp2_ctx* c, const uint8_t id[PP2_RCCL_ID_BYTES],
   HIPCHK(hipMalloc(&d, sizeof(int)));
   HIPCHK(hipMemcpyAsync(d, &rows, sizeof(int), hipMemcpyHostToDevice, c->stream));
   CHECK(comm_enter(c));
-  NCCLCHK(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, c->comm_stream));
+  NCCLCHK(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, cst(c)));
   CHECK(comm_leave(c));
   HIPCHK(hipMemcpyAsync(&rows, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));

@@ -18,7 +18,7 @@ def main():
     goal = S.synth_goal(grid)
     us, zs, _ = S.synth_trajectory(grid, reps, seed=42)
     stream = torch.cuda.Stream()
-    for mode in ("plain", "rccl1", "rccl1-depth1"):
+    for mode in ("plain", "rccl1", "rccl1-depth1", "rccl1-cs", "rccl1-cs-depth1"):
         kw = {} if mode == "plain" else {"rows": (0, N)}
         with P.GridContext(grid, goal, gamma=0.95, **kw) as ctx:
             ctx.set_stream(stream.cuda_stream)
@@ -26,6 +26,8 @@ def main():
                 ctx.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
                 if mode.endswith("depth1"):
                     ctx.set_tuning(ctx.TUNE_HALO_DEPTH, 1)
+                if "-cs" in mode:
+                    ctx.set_tuning(ctx.TUNE_COMM_STREAM, 1)
             ctx.model_generate()
             ctx.belief_set(S.uniform_belief(grid))
             ctx.mdp_reset()
