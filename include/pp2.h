@@ -101,6 +101,13 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           stream; 1: on a dedicated stream entered and left
  *                           through events */
 #define PP2_TUNE_COMM_STREAM 5
+/*  PP2_TUNE_NORM_BLOCK      unsharded pp2_loop_step: 1 = divide by the exact
+ *                           mass every step (bit-exact with per-step host
+ *                           normalisation); k = 2..16 (default 8) = divide by
+ *                           the exact mass times 2^64 at the first step of
+ *                           every k and by 1 in between (beliefs equal to
+ *                           rounding; values and actions unchanged) */
+#define PP2_TUNE_NORM_BLOCK 6
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
 /* ---------------------------------------------------------------- model
@@ -168,8 +175,10 @@ int pp2_mdp_get(pp2_ctx* ctx, float* J, uint8_t* A);
 
 /* ---------------------------------------------------------------- north star
  * One iteration of the benchmarked loop: one belief update (u, z) and one
- * Bellman sweep, with the belief normalisation folded into the sweep launch.
- * Sharded contexts also exchange halo rows and all-reduce the belief mass.
+ * Bellman sweep in one launch.  The stored belief is renormalised by its
+ * exact mass every PP2_TUNE_NORM_BLOCK steps (power-of-two scaled in
+ * between); reads always divide by the true mass.  Sharded contexts also
+ * exchange halo rows and all-reduce the belief mass at each block start.
  * Asynchronous. */
 int pp2_loop_step(pp2_ctx* ctx, uint8_t u, uint8_t z);
 int pp2_loop_run(pp2_ctx* ctx, int n, const uint8_t* us, const uint8_t* zs);

@@ -99,6 +99,7 @@ class GridContext:
     TUNE_CODED_MODEL = 3
     TUNE_HALO_DEPTH = 4
     TUNE_COMM_STREAM = 5
+    TUNE_NORM_BLOCK = 6
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))

@@ -106,7 +106,8 @@ struct pp2_ctx {
   // rows deep every kdepth loop steps; only a block's first step normalises.
   int kdepth = 1;          // loop halo depth in use
   int kdepth_max = 1;      // min(g.halo, the smallest shard's rows)
-  int kstep = 0;           // loop step within the current halo block
+  int kstep = 0;           // loop step within the current halo / normalisation block
+  int norm_block = 8;      // unsharded loop: steps per exact normalisation (PP2_TUNE_NORM_BLOCK)
 
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;

@@ -568,23 +568,26 @@ int pp2rt::loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass) {
   return PP2_OK;
 }
 
-// One loop step of an RCCL row shard.  Steps come in blocks
-// of kdepth.  A block starts by finalising the exact global mass of the
-// current belief (one all-reduce) and refreshing the halo rows of b and J
-// kdepth rows deep (one RCCL group); its first step divides by that mass
-// (times 2^64, exact) and the others by 1.  Step i computes a view
-// kdepth-1-i rows wider than the owned rows per side, so nothing crosses
-// ranks until the next block.
-static int sharded_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
+// One loop step in normalisation blocks.  Steps come in
+// blocks of `depth`.  A block starts by finalising the exact (global) mass of
+// the current belief; its first step divides by that mass times 2^64 (exact)
+// and the others by 1, so the in-kernel reduction of the previous step's
+// partials drops out of 7 in 8 steps.  RCCL shards also refresh their halo
+// rows of b and J `depth` rows deep at the block start (one RCCL group), and
+// step i computes a view depth-1-i rows wider than the owned rows per side,
+// so nothing crosses ranks until the next block.
+static int blocked_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  const bool shard = c->comm != nullptr;
+  const int depth = shard ? c->kdepth : c->norm_block;
   const int bc = c->bcur, bn = bc ^ 1, jn = c->jcur ^ 1;
   const bool start = c->kstep == 0;
   if (start) {
     CHECK(ensure_mass(c));
-    CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, c->kdepth));
+    if (shard) CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, depth));
   }
   int nparts = 0;
-  CHECK(loop_launch(c, c->kdepth - 1 - c->kstep, u, z, nullptr, 0,
+  CHECK(loop_launch(c, shard ? depth - 1 - c->kstep : 0, u, z, nullptr, 0,
                     start ? c->bsum + bc : nullptr, nullptr, &nparts,
                     start ? kBlockScale : 1.0f));
   c->pending[bc] = false;
@@ -592,7 +595,7 @@ static int sharded_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   c->pending[bn] = true;
   c->bcur = bn;
   c->jcur = jn;
-  c->kstep = (c->kstep + 1) % c->kdepth;
+  c->kstep = (c->kstep + 1) % depth;
   return PP2_OK;
 }
 
@@ -695,6 +698,12 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
     case PP2_TUNE_CODED_MODEL: c->use_coded = value != 0; return PP2_OK;
+    case PP2_TUNE_NORM_BLOCK:
+      if (value < 1 || value > 16)
+        return set_err(PP2_EINVAL, "normalisation block %d not in [1, 16]", value);
+      c->norm_block = value;
+      break_pipeline(c);
+      return PP2_OK;
     case PP2_TUNE_COMM_STREAM:
       if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
       HIPCHK(hipStreamSynchronize(c->stream));
@@ -893,7 +902,7 @@ int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   DeviceGuard dg(c->device);
   if (c->group)
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
-  if (c->comm) return sharded_loop_step(c, u, z);  // RCCL shard (any rank count)
+  if (c->comm || c->norm_block > 1) return blocked_loop_step(c, u, z);  // RCCL shard or blocks
   return loop_step_fused(c, u, z, false);
 }
 

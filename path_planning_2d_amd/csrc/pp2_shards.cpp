@@ -201,7 +201,7 @@ int pp2_shard_group_synchronize(pp2_shard_group* g) {
   return PP2_OK;
 }
 
-// The RCCL row-shard loop step (pp2_runtime.cpp sharded_loop_step) with
+// The RCCL row-shard loop step (pp2_runtime.cpp blocked_loop_step) with
 // device copies as the transport: a block starts by refreshing the halo rows
 // of b and J kdepth rows deep, and its first step divides by the global mass
 // (times 2^64) and the others by 1; step i computes a view kdepth-1-i rows

@@ -233,3 +233,65 @@ def test_errors_surface_as_exceptions(pp2):
             ctx.belief_update(9, 0)
         with pytest.raises(pp2.Pp2Error):
             ctx.model_load("/nonexistent-dir")
+
+
+@pytest.mark.parametrize("block", [1, 2, 8, 16])
+@pytest.mark.parametrize("cpt", [1, 4])
+def test_loop_normalisation_blocks(pp2, oracle, block, cpt):
+    """PP2_TUNE_NORM_BLOCK: the stored belief is divided by its exact mass
+    every `block` steps (x 2^64, exact) and by 1 in between.  Over the 64-step
+    golden trajectory every read belief matches the reference's per-step
+    normalised sequence to rel 1e-5 (FTZ floor), at every block phase; values
+    and actions are untouched (bit-exact).  block 1 is per-step division."""
+    name = "sparse_map_100x40"
+    grid = golden_map(name)
+    m = golden("model", name)
+    bt = golden("belief", name)
+    with make_ctx(pp2, grid, tuple(m["goal"]), cpt) as ctx:
+        ctx.set_tuning(ctx.TUNE_NORM_BLOCK, block)
+        ctx.belief_set(bt["b0"])
+        ctx.mdp_reset()
+        done = 0
+        for k in (1, 2, 4, 8, 16, 32, 64):
+            ctx.loop_run(bt["us"][done:k], bt["zs"][done:k])
+            done = k
+            assert_rel_close(ctx.belief_get(), bt[f"b{k}"], rel=1e-5, abs_floor=1e-30,
+                             msg=f"block {block}, step {k}")
+            if k == 8:
+                J, A = ctx.mdp_get()
+                g = golden("mdp", name)
+                Jr = np.zeros_like(J)
+                with make_ctx(pp2, grid, tuple(m["goal"]), cpt) as ref:
+                    ref.mdp_reset()
+                    ref.mdp_sweep(8)
+                    Jr, Ar = ref.mdp_get()
+                np.testing.assert_array_equal(J, Jr)
+                np.testing.assert_array_equal(A, Ar)
+                del g
+        with pytest.raises(pp2.Pp2Error):
+            ctx.set_tuning(ctx.TUNE_NORM_BLOCK, 17)
+
+
+def test_loop_blocks_equal_across_paths(pp2):
+    """Coded and dense loops under the default normalisation blocks stay
+    bit-identical (raw beliefs and masses) through block boundaries."""
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(96, 130, 4)
+    grid[0, 0] = 0
+    us, zs, _ = S.synth_trajectory(grid, 19, seed=5)
+    b0 = S.uniform_belief(grid)
+    a = pp2.GridContext(grid, (0, 0), gamma=float(GAMMA))
+    b = pp2.GridContext(grid, (0, 0), gamma=float(GAMMA))
+    with a, b:
+        for c in (a, b):
+            c.model_generate()
+            c.belief_set(b0)
+            c.mdp_reset()
+        b.set_tuning(b.TUNE_CODED_MODEL, 0)
+        for k in range(19):
+            a.loop_step(int(us[k]), int(zs[k]))
+            b.loop_step(int(us[k]), int(zs[k]))
+            ra, ma = a.belief_get_raw()
+            rb, mb = b.belief_get_raw()
+            np.testing.assert_array_equal(ra, rb, err_msg=f"step {k}")
+            assert np.float32(ma) == np.float32(mb)
