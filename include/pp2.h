@@ -103,8 +103,8 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
 #define PP2_TUNE_COMM_STREAM 5
 /*  PP2_TUNE_NORM_BLOCK      unsharded pp2_loop_step: 1 = divide by the exact
  *                           mass every step (bit-exact with per-step host
- *                           normalisation); k = 2..16 (default 8) = divide by
- *                           the exact mass times 2^64 at the first step of
+ *                           normalisation); k = 2..8 (default 8) = divide by
+ *                           the exact mass times 2^96 at the first step of
  *                           every k and by 1 in between (beliefs equal to
  *                           rounding; values and actions unchanged) */
 #define PP2_TUNE_NORM_BLOCK 6

@@ -42,11 +42,15 @@ int set_err(int code, const char* fmt, ...);
 
 constexpr int kGuard = 64;  // floats of guard before/after each plane set
 constexpr int kShardHalo = 8;  // halo rows allocated per side in row-sharded contexts
-// Row-shard loop blocks start by dividing the belief by its global mass and
-// multiplying by 2^64 (exact), then divide by 1: the stored belief stays far
-// above the flush-to-zero range while it decays by < kdepth observation
-// probabilities inside a block.  Reads divide by the true mass.
-constexpr float kBlockScale = 18446744073709551616.0f;  // 2^64
+// Loop normalisation blocks (row shards, and PP2_TUNE_NORM_BLOCK > 1) start
+// by dividing the belief by its exact (global) mass and multiplying by 2^96
+// (exact), then divide by 1: the stored belief decays by < 8 observation
+// probabilities inside a block, and 2^96 keeps cells far above the
+// flush-to-zero range (at P(z) >= 1e-3 per step, every normalised value above
+// FLT_MIN stays representable), while normalised cells <= 1 times 2^96 stay
+// far below FLT_MAX.  Reads divide by the true mass.
+constexpr float kBlockScale = 79228162514264337593543950336.0f;  // 2^96
+constexpr int kMaxNormBlock = 8;
 
 // A set of K planes over rows [-1, rows] (one halo row each side).
 struct Planes {

@@ -570,9 +570,9 @@ int pp2rt::loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass) {
 
 // One loop step in normalisation blocks.  Steps come in
 // blocks of `depth`.  A block starts by finalising the exact (global) mass of
-// the current belief; its first step divides by that mass times 2^64 (exact)
+// the current belief; its first step divides by that mass times 2^96 (exact)
 // and the others by 1, so the in-kernel reduction of the previous step's
-// partials drops out of 7 in 8 steps.  RCCL shards also refresh their halo
+// partials drops out of all but the first step of a block.  RCCL shards also refresh their halo
 // rows of b and J `depth` rows deep at the block start (one RCCL group), and
 // step i computes a view depth-1-i rows wider than the owned rows per side,
 // so nothing crosses ranks until the next block.
@@ -699,8 +699,8 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
     case PP2_TUNE_CODED_MODEL: c->use_coded = value != 0; return PP2_OK;
     case PP2_TUNE_NORM_BLOCK:
-      if (value < 1 || value > 16)
-        return set_err(PP2_EINVAL, "normalisation block %d not in [1, 16]", value);
+      if (value < 1 || value > kMaxNormBlock)
+        return set_err(PP2_EINVAL, "normalisation block %d not in [1, %d]", value, kMaxNormBlock);
       c->norm_block = value;
       break_pipeline(c);
       return PP2_OK;

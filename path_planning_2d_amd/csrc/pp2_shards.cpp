@@ -204,7 +204,7 @@ int pp2_shard_group_synchronize(pp2_shard_group* g) {
 // The RCCL row-shard loop step (pp2_runtime.cpp blocked_loop_step) with
 // device copies as the transport: a block starts by refreshing the halo rows
 // of b and J kdepth rows deep, and its first step divides by the global mass
-// (times 2^64) and the others by 1; step i computes a view kdepth-1-i rows
+// (times 2^96) and the others by 1; step i computes a view kdepth-1-i rows
 // wider per side.  (The group also combines the mass after every step, so a
 // shard's bsum always holds the global mass for reads.)
 int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z) {
