@@ -89,7 +89,9 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           CPT 4): -8 % time per loop step measured
  *  PP2_TUNE_CODED_MODEL     1 (default) = loop step and MDP sweep read the
  *                           dictionary-coded model (pp2_model_dict_info)
- *                           when one exists; 0 = always the dense planes */
+ *                           when one exists, and FIB sweeps skip the T
+ *                           entries the dictionary proved zero; 0 = always
+ *                           the dense planes and full sums */
 #define PP2_TUNE_CELLS_PER_LANE 1
 #define PP2_TUNE_NT_STREAMS 2
 #define PP2_TUNE_CODED_MODEL 3

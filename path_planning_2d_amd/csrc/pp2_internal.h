@@ -64,9 +64,11 @@ hipError_t launch_sum_finalize(hipStream_t st, const float* partials, int n,
                                float* out);
 // out = v[0] + v[1] + ... + v[n-1], in index order.
 hipError_t launch_sum_ordered(hipStream_t st, const float* v, int n, float* out);
+// sparse: every T row is +0.0 off its action's base-kernel support (the
+// dictionary build's check, pp2_ctx::dict_sparse) -- same alphas, bit for bit.
 hipError_t launch_fib_sweep(hipStream_t st, const Geom& g, float gamma,
                             PlaneSet T, PlaneSet L, PlaneSet R,
-                            PlaneSet a_in, PlaneSet a_out);
+                            PlaneSet a_in, PlaneSet a_out, bool sparse = false);
 hipError_t launch_absdiff_max(hipStream_t st, const Geom& g, int planes,
                               PlaneSet cur, PlaneSet snap, float* partials,
                               int* nparts);

@@ -518,12 +518,73 @@ __global__ __launch_bounds__(kBlock) void k_fib_sweep(
   }
 }
 
+// k_fib_sweep for models whose T rows are +0.0 off each action's base-kernel
+// support kSup[a] (every generated model; build_model_dict checks it): per
+// action, per observation, only the <= 4 support neighbours' T * L enter the
+// 9 next-action chains, so the likelihood loads drop from 144 to 4 per
+// (action, observation) and the flops by 2.2x.  Dropped terms are
+// fmaf(0 * L, alpha, s) == s (the chain starts at +0 and never holds -0), so
+// alphas are bit-identical to k_fib_sweep's full 9-term chains.
+__global__ __launch_bounds__(kBlock) void k_fib_sweep_sparse(
+    Geom g, float gamma, PlaneSet T, PlaneSet L, PlaneSet R, PlaneSet a_in,
+    PlaneSet a_out) {
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const int y = (int)(t / g.wp);
+  const int x = (int)(t % g.wp);
+  if (y >= g.rows) return;
+  float la[9][9];
+  bool ok[9];
+#pragma unroll
+  for (int sp = 0; sp < 9; ++sp) {
+    const int oy = sp / 3 - 1, nx = x + sp % 3 - 1;
+    ok[sp] = nx >= 0 && nx < g.wp;
+    const float* ap = a_in.p + (long long)(y + oy) * a_in.rs + nx;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) la[sp][q] = ok[sp] ? ap[(long long)q * a_in.ps] : 0.0f;
+  }
+#pragma unroll
+  for (int a = 0; a < 9; ++a) {
+    float ts[4];
+    const float* lp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int sp = kSup[a][j], oy = sp / 3 - 1, nx = x + sp % 3 - 1;
+      ts[j] = j < kSupN[a] ? T.p[(long long)y * T.rs + (long long)(9 * a + sp) * T.ps + x] : 0.0f;
+      lp[j] = L.p + (long long)(y + oy) * L.rs + (ok[sp] ? nx : x);
+    }
+    float rtg = 0.0f;
+#pragma unroll 2
+    for (int o = 0; o < 16; ++o) {
+      float tm[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        tm[j] = j < kSupN[a] ? ts[j] * (ok[kSup[a][j]] ? lp[j][(long long)o * L.ps] : 0.0f) : 0.0f;
+      float rtgo = -FLT_MAX;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        float sq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < kSupN[a]) sq = __builtin_fmaf(tm[j], la[kSup[a][j]][q], sq);
+        if (rtgo < sq) rtgo = sq;
+      }
+      rtg = rtg + rtgo;
+    }
+    a_out.p[(long long)y * a_out.rs + (long long)a * a_out.ps + x] =
+        __builtin_fmaf(gamma, rtg, R.p[(long long)y * R.rs + (long long)a * R.ps + x]);
+  }
+}
+
 hipError_t launch_fib_sweep(hipStream_t st, const Geom& g, float gamma,
                             PlaneSet T, PlaneSet L, PlaneSet R,
-                            PlaneSet a_in, PlaneSet a_out) {
+                            PlaneSet a_in, PlaneSet a_out, bool sparse) {
   const int grid = cells_grid(g, 1);
-  hipLaunchKernelGGL(k_fib_sweep, dim3(grid), dim3(kBlock), 0, st, g, gamma, T,
-                     L, R, a_in, a_out);
+  if (sparse)
+    hipLaunchKernelGGL(k_fib_sweep_sparse, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, L, R,
+                       a_in, a_out);
+  else
+    hipLaunchKernelGGL(k_fib_sweep, dim3(grid), dim3(kBlock), 0, st, g, gamma, T,
+                       L, R, a_in, a_out);
   return hipGetLastError();
 }
 

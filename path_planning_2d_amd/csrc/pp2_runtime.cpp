@@ -455,7 +455,8 @@ int mdp_sweep_once(pp2_ctx* c) {
 int fib_sweep_once(pp2_ctx* c) {
   const int fn = c->fcur ^ 1;
   HIPCHK(pp2::launch_fib_sweep(c->stream, c->g, c->gamma, c->T.v, c->L.v, c->R.v,
-                               c->fib[c->fcur].v, c->fib[fn].v));
+                               c->fib[c->fcur].v, c->fib[fn].v,
+                               c->use_coded && c->dict_n > 0 && c->dict_sparse));
   c->fcur = fn;
   return PP2_OK;
 }

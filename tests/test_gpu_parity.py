@@ -295,3 +295,22 @@ def test_loop_blocks_equal_across_paths(pp2):
             rb, mb = b.belief_get_raw()
             np.testing.assert_array_equal(ra, rb, err_msg=f"step {k}")
             assert np.float32(ma) == np.float32(mb)
+
+
+@pytest.mark.parametrize("name", ["map_10x10", "sparse_map_100x40", "tile64_sparse_map_100x40"])
+def test_fib_sparse_equals_dense(pp2, name):
+    """k_fib_sweep_sparse (support-only terms, observation-outer loads) gives
+    the dense k_fib_sweep's alphas bit for bit, sweep by sweep and solved."""
+    grid = golden_map(name)
+    m = golden("model", name)
+    with make_ctx(pp2, grid, tuple(m["goal"])) as a, make_ctx(pp2, grid, tuple(m["goal"])) as b:
+        b.set_tuning(b.TUNE_CODED_MODEL, 0)
+        for c in (a, b):
+            c.fib_reset()
+        for k in range(4):
+            a.fib_sweep(1)
+            b.fib_sweep(1)
+            np.testing.assert_array_equal(a.fib_get(), b.fib_get(), err_msg=f"sweep {k}")
+        ra, rb = a.fib_solve(), b.fib_solve()
+        assert ra == rb
+        np.testing.assert_array_equal(a.fib_get(), b.fib_get())
