@@ -14,7 +14,7 @@ What is frozen, and where it comes from:
   the default seed (the reference never seeds; search_tree_cuda.cu:332),
   captured through ctypes: pins the oracle's rand() restatement.
 * ``model_<map>.npz``, ``belief_<map>.npz``, ``mdp_<map>.npz``,
-  ``fib_<map>.npz`` -- outputs of the CPU oracle (oracle/pp2_oracle.c), the
+  ``fib_<map>.npz``, ``pbvi_<map>.npz`` -- outputs of the CPU oracle (oracle/pp2_oracle.c), the
   restatement of the reference kernels.  The reference itself cannot be built
   or run here, so these are "parity unpinned" vectors that
   freeze the oracle and feed the GPU tests (which may not read
@@ -126,5 +126,28 @@ def main():
     print("goals:", goals)
 
 
+def save_pbvi():
+    """PBVI (point_based_value_iteration_cuda.cu): generateBeliefSet from the
+    uniform belief with the reference's unseeded rand() (seed 1), then
+    backupAlphaVectors from zero alphas -- all 167 backups on 10x10 at
+    S = 32, 2 backups on 100x40 at S = 48.  Needs only the committed maps:
+    ``python tests/golden/make_golden.py pbvi``."""
+    for name, S_, iters in (("map_10x10", 32, 0), ("sparse_map_100x40", 48, 2)):
+        grid = np.load(os.path.join(HERE, "maps", name + ".npy"), allow_pickle=False)
+        goal = tuple(np.load(os.path.join(HERE, f"model_{name}.npz"))["goal"])
+        H, W = grid.shape
+        T, L, R = O.model_pomdp(grid, goal)
+        b0 = S.uniform_belief(grid)
+        B, _ = O.pbvi_belief_set(H, W, T, L, b0, S_)
+        al, act, n = O.pbvi_backup(H, W, GAMMA, T, L, R, B, iterations=iters)
+        np.savez_compressed(os.path.join(HERE, f"pbvi_{name}.npz"), beliefs=B, alphas=al,
+                            actions=act, iterations=np.int32(n))
+        print(f"{name}: PBVI S={S_}, {n} backups")
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["pbvi"]:
+        save_pbvi()
+    else:
+        main()
+        save_pbvi()

@@ -299,3 +299,20 @@ def test_pbvi_oracle_structure(oracle):
     al1, act1, _ = oracle.pbvi_backup(H, W, GAMMA, T, L, R, B, iterations=1)
     for i in range(len(B)):
         np.testing.assert_array_equal(al1[i], R[:, act1[i]])
+
+
+@pytest.mark.parametrize("name", ["map_10x10", "sparse_map_100x40"])
+def test_pbvi_oracle_matches_golden(oracle, name):
+    """The oracle's generateBeliefSet + backupAlphaVectors reproduce the
+    frozen PBVI fixtures bit for bit (tests/golden/make_golden.py pbvi)."""
+    from conftest import GAMMA, golden, golden_map
+    from path_planning_2d_amd import synthetic as S
+    g = golden_map(name)
+    p = golden("pbvi", name)
+    T, L, R = oracle.model_pomdp(g, tuple(golden("model", name)["goal"]))
+    H, W = g.shape
+    B, _ = oracle.pbvi_belief_set(H, W, T, L, S.uniform_belief(g), p["beliefs"].shape[0])
+    np.testing.assert_array_equal(B, p["beliefs"])
+    al, act, n = oracle.pbvi_backup(H, W, GAMMA, T, L, R, B, iterations=int(p["iterations"]))
+    np.testing.assert_array_equal(al, p["alphas"])
+    np.testing.assert_array_equal(act, p["actions"])
