@@ -1,6 +1,7 @@
 """CPU: the C-ABI library builds, loads and exports every symbol declared in
 include/pp2.h (no compute calls -- there is no GPU here)."""
 import ctypes
+import os
 import re
 
 import pytest
@@ -47,3 +48,22 @@ def test_errors_are_returned_not_fatal():
         _lib.call("pp2_create", ctypes.byref(ctypes.c_void_p()), 0, 0, 4,
                   g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 0, 0,
                   ctypes.c_float(0.95))
+
+
+def test_c_client_compiles_and_links(tmp_path):
+    """examples/pp2_node_demo.c -- the POMDP node's sequence in plain C99 --
+    compiles against include/pp2.h and links against the in-tree library."""
+    import shutil
+    import subprocess
+    cc = shutil.which("cc") or shutil.which("gcc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib_dir = os.path.join(root, "path_planning_2d_amd")
+    if not os.path.exists(os.path.join(lib_dir, "libpp2_hip.so")):
+        pytest.skip("library not built")
+    exe = tmp_path / "demo"
+    subprocess.run([cc, "-std=c99", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(root, "include"),
+                    "-o", str(exe), os.path.join(root, "examples", "pp2_node_demo.c"),
+                    "-L", lib_dir, "-lpp2_hip"], check=True)
+    assert exe.exists()

@@ -177,3 +177,20 @@ def test_planner_pbvi_needs_alphas():
             P.QVTreePlanner(ctx, lower_bound_mode=1)
         with pytest.raises(P.Pp2Error):
             P.QVTreePlanner(ctx, lower_bound_mode=2)
+
+
+def test_c_client_runs(tmp_path):
+    """The plain-C node sequence (examples/pp2_node_demo.c, built by the
+    csrc Makefile): planner with PBVI bounds, loop steps and the reference
+    text files, all through include/pp2.h."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "examples", "pp2_node_demo")
+    assert os.path.exists(exe), "build with make -C path_planning_2d_amd/csrc"
+    out = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "pp2_node_demo ok" in out.stdout
+    for f in ("model_data_trans_prob", "fib_alphas", "fib_actions", "pbvi_alphas",
+              "pbvi_actions"):
+        assert (tmp_path / f).exists(), f
