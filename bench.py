@@ -168,8 +168,26 @@ def cpu_baseline(grid, goal, us, zs, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s / 2 or msteps >= 100000:
             break
+    # the simulator's scatter-form CPU filter (dummy_simulator.cpp:671-773),
+    # belief steps only, single thread: the other CPU formulation of the step
+    gu8 = np.ascontiguousarray(grid, np.uint8)
+    b = b0.copy()
+    p = np.empty_like(b)
+    ssteps = 0
+    t0 = time.perf_counter()
+    while True:
+        lib.orc_sim_predict(H, W, gu8, b, int(us[ssteps % len(us)]), p)
+        lib.orc_sim_correct(H, W, gu8, p, int(zs[ssteps % len(zs)]), b)
+        ssteps += 1
+        el_s = time.perf_counter() - t0
+        if el_s >= min(3.0, budget_s / 4) or ssteps >= 10000:
+            break
+    scatter = {"value": H * W * ssteps / el_s, "unit": "cells/s (belief step only)", "cores": 1,
+               "sample": f"{ssteps} predict+correct steps, {el_s:.1f} s (orc_sim_predict/"
+                         f"orc_sim_correct, dummy_simulator.cpp:671-773)"}
     return {"value": H * W * msteps / el, "unit": "cells/s", "cores": nt,
             "kind": "port",
+            "scatter_filter": scatter,
             "sample": f"{msteps} loop steps on the same {H}x{W} grid ({el:.1f} s), rows split "
                       f"over {nt} threads (oracle/pp2_oracle.c orc_loop_run_mt, -O3 "
                       f"-march=native); single thread: {single['value']:.3g} cells/s "
@@ -534,6 +552,20 @@ def main():
                  "mdp_sweep_us": dsweep_ms * 1e3,
                  "mdp_sweep_frac": BYTES_SWEEP * cells_per_gpu / (dsweep_ms * 1e-3) / 1e9
                  / HBM_PEAK_GBS}
+    mdp_solve = None
+    if rank == 0 and ws == 1:
+        # BASELINE configs[2]: MDP value iteration to convergence on this grid
+        # (valueIteration, src/mdp/path_planning_2d.cu:207-269, no GUI)
+        ctx.mdp_reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_sw, nrm = ctx.mdp_solve()
+        torch.cuda.synchronize()
+        t_solve = time.perf_counter() - t0
+        mdp_solve = {"config": f"{N}x{N} MDP value iteration to convergence "
+                               f"(blocks of 100 sweeps, stop at inf-norm <= 1e-3*5/(1-gamma))",
+                     "sweeps": n_sw, "final_norm": nrm, "ms": t_solve * 1e3,
+                     "us_per_sweep": t_solve * 1e6 / max(1, n_sw)}
     ctx.close()
 
     bytes_loop = BYTES_LOOP_CODED if coded else BYTES_LOOP
@@ -631,6 +663,7 @@ def main():
                 "loop_frac": loop_gbs / HBM_PEAK_GBS,
             },
             "belief_mass_ok": mass_ok,
+            "mdp_solve": mdp_solve,
             "plan_step": plan,
             "rollout": rollout,
             "pbvi": pbvi,
