@@ -224,3 +224,40 @@ def test_pbvi_matches_golden(pp2, name):
         al, act = ctx.pbvi_get()
     np.testing.assert_array_equal(al, p["alphas"])
     np.testing.assert_array_equal(act, p["actions"])
+
+
+@pytest.mark.parametrize("case", ["map_3x3", "row_1x9", "col_7x1", "single_belief"])
+def test_pbvi_edge_shapes(pp2, oracle, case):
+    """Tiny and degenerate grids and S = 1: belief set and 5 backups equal the
+    oracle bit for bit; an empty evaluation batch is a no-op."""
+    from path_planning_2d_amd import synthetic as S
+    if case == "map_3x3":
+        g = golden_map("map_3x3")
+        goal = tuple(golden("model", "map_3x3")["goal"])
+        Sn = 20
+    elif case == "row_1x9":
+        g = np.zeros((1, 9), np.uint8)
+        g[0, 4] = 1
+        goal, Sn = (8, 0), 9
+    elif case == "col_7x1":
+        g = np.zeros((7, 1), np.uint8)
+        goal, Sn = (0, 6), 5
+    else:
+        g = golden_map("map_10x10")
+        goal = tuple(golden("model", "map_10x10")["goal"])
+        Sn = 1
+    H, W = g.shape
+    T, L, R = oracle.model_pomdp(g, goal)
+    b0 = S.uniform_belief(g)
+    Bo, _ = oracle.pbvi_belief_set(H, W, T, L, b0, Sn)
+    al_o, act_o, _ = oracle.pbvi_backup(H, W, GAMMA, T, L, R, Bo, iterations=5)
+    with pp2.GridContext(g, goal, gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.pbvi_belief_set(b0, Sn)
+        np.testing.assert_array_equal(ctx.pbvi_get_beliefs(), Bo)
+        ctx.pbvi_backup(5)
+        al, act = ctx.pbvi_get()
+        v, a = ctx.pbvi_evaluate(np.zeros((0, H * W), np.float32))
+        assert v.size == 0 and a.size == 0
+    np.testing.assert_array_equal(al, al_o)
+    np.testing.assert_array_equal(act, act_o)
