@@ -209,8 +209,8 @@ int pp2_fib_load(pp2_ctx* ctx, const char* dir);
  * their actions[S] (host_pbvi_alphas / host_pbvi_actions, :51-57).  The
  * reference's node uses S = 500 (src/pomdp/path_planning_2d.cu:122,140).
  *
- * generateBeliefSet (:165-295): S beliefs grown from b0 (hw floats, used as
- * given).  Three glibc rand() draws per (belief, action) and round from
+ * generateBeliefSet (:165-295): S beliefs (1..4096) grown from b0 (hw
+ * floats, used as given).  Three glibc rand() draws per (belief, action) and round from
  * srand(rand_seed) (the reference never seeds: 1); *rand_calls (may be NULL)
  * gets the number drawn, so a planner can continue the same stream.  Resets
  * the alphas to 0 (pointBasedValueIteration, :652-657). */

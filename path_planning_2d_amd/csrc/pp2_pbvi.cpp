@@ -68,6 +68,8 @@ void dfree(T** p) {
 
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
+constexpr int kMaxBeliefs = 4096;
+
 int check_pbvi_ctx(pp2_ctx* c) {
   CHECK(check_model(c));
   if (c->nranks > 1 || c->group || c->g.rows != c->g.grows)
@@ -86,7 +88,9 @@ void free_scratch(PbviState* p) {
 // (Re)size the state for S beliefs; alphas and actions are zeroed.
 int ensure_state(pp2_ctx* c, int S) {
   if (S < 1) return set_err(PP2_EINVAL, "belief set size must be >= 1");
-  if (S > 8192) return set_err(PP2_EINVAL, "belief set size %d > 8192", S);
+  // the expansion's 9 n candidates index grid.y of the update / division
+  // launches (< 65536); the reference node uses 500
+  if (S > kMaxBeliefs) return set_err(PP2_EINVAL, "belief set size %d > %d", S, kMaxBeliefs);
   PbviState*& p = c->pbvi;
   if (!p) p = new PbviState();
   const int hw = c->g.rows * c->g.width;

@@ -203,6 +203,8 @@ def test_pbvi_rejects_sharded_and_unset(pp2):
             ctx.pbvi_backup(1)  # no belief set
         with pytest.raises(pp2.Pp2Error):
             ctx.pbvi_belief_set(S.uniform_belief(g), 0)
+        with pytest.raises(pp2.Pp2Error):
+            ctx.pbvi_belief_set(S.uniform_belief(g), 4097)
     with pp2.GridContext(g, (0, 0), gamma=float(GAMMA), rows=(0, 8)) as sh:
         sh.model_generate()
         with pytest.raises(pp2.Pp2Error):
