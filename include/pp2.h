@@ -320,6 +320,7 @@ int pp2_curand_uniforms(uint64_t seed, int n, float* u1, float* u2);
  * Beliefs are stored as per-copy max-normalised fp16 (2 B per cell-copy),
  * arithmetic is fp32; expect ~1e-3 relative agreement with an fp32 rollout. */
 typedef struct pp2_rollout pp2_rollout;
+/* copies 1..131072, depth >= 1 */
 int pp2_rollout_create(pp2_rollout** out, pp2_ctx* ctx, int copies, int depth);
 int pp2_rollout_destroy(pp2_rollout* r);
 /* root belief (hw floats) copied into every copy */

@@ -55,6 +55,8 @@ int pp2_rollout_create(pp2_rollout** out, pp2_ctx* c, int copies, int depth) {
   *out = nullptr;
   CHECK(check_model(c));
   if (copies < 1 || depth < 1) return set_err(PP2_EINVAL, "copies and depth must be >= 1");
+  // chunks of >= 4 copies index grid.y of the step launch (< 65536)
+  if (copies > 131072) return set_err(PP2_EINVAL, "copies %d > 131072", copies);
   if (c->nranks > 1 || c->group || c->g.rows != c->g.grows)
     return set_err(PP2_EINVAL, "rollouts need an unsharded context");
   DeviceGuard dg(c->device);
