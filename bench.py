@@ -11,8 +11,9 @@ resident in HBM before the timed region.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size 1024]
 
 For N > 1 launch with torch.distributed.run: rank r owns rows
-[r*S, (r+1)*S) of an (N*S) x S grid (weak scaling), exchanging one halo row
-per step with its neighbours and all-reducing the belief mass over RCCL.
+[r*S, (r+1)*S) of an (N*S) x S grid (weak scaling); every 8 steps it
+exchanges 8 halo rows of belief and values with its neighbours and
+all-reduces the belief mass over RCCL.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant (and only)
 kernel of a step, timed live with HIP events around the timed steps on the
@@ -612,7 +613,9 @@ def main():
                             f"Bellman sweep per step (BASELINE.json configs[2] grid)",
                 "grid": [gh, gw],
                 "rows_per_gpu": N,
-                "parallelism": f"row-shard x{ws}, 1-row RCCL halo" if ws > 1 else "single GPU",
+                "parallelism": (f"row-shard x{ws}: {min(8, N)}-row RCCL halo exchange and one "
+                                f"1-float mass all-reduce every {min(8, N)} steps"
+                                if ws > 1 else "single GPU"),
                 "cells_per_lane": args.cpt,
                 "model": (f"dictionary-coded ({dict_entries} entries, uint16 code per cell)"
                           if coded else "dense fp32 planes"),
