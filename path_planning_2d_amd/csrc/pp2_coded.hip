@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void k_dict_verify(Geom g, PlaneSet T, Plan
 // ---------------------------------------------------------------- kernels
 // Two LDS row layouts per dictionary entry:
 //  * full   (kDictTC = 90 floats): [a][gT_a0..gT_a8, C_a];
-//  * sparse (kSpRow = 54 floats):  [a][gT_a at kSup[a][0..3], C_a, 0] -- only
+//  * sparse (kSpRow = 52 floats):  [a][gT_a at kSup[a][0..3]] | C[0..8] | pad -- only
 //    the base-kernel support of each action (at most 4 cells; the host checks
 //    every other T entry of every row is +0.0 before choosing it).
 // gT = fl(gamma * T), rounded once on the host exactly as the dense sweep
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kBlock) void k_dict_verify(Geom g, PlaneSet T, Plan
 template <bool SPARSE>
 struct Layout {
   static constexpr int row = SPARSE ? kSpRow : kDictTC;
-  static constexpr int blk = SPARSE ? 6 : 10;  // floats per action block
+  static constexpr int blk = SPARSE ? 4 : 10;  // floats per action block (sparse: T only)
   static constexpr int tu = tu_width(SPARSE);  // raw T_u floats per entry (belief gather)
 };
 
@@ -161,12 +161,15 @@ __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&
     for (int a = 0; a < 9; ++a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const f2a* row = reinterpret_cast<const f2a*>(sTC + cc[k] * kSpRow + a * 6);
-        const f2a t01 = row[0];
-        const f2a t23 = kSupN[a] > 2 ? row[1] : f2a{0.0f, 0.0f};
-        const f2a cz = row[2];
-        const float tv[4] = {t01[0], t01[1], t23[0], t23[1]};
-        float cost = cz[0];
+        const float* row = sTC + cc[k] * kSpRow;
+        float tv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (kSupN[a] > 2) {
+          const f4a t = *reinterpret_cast<const f4a*>(row + a * 4);  // one ds_read_b128
+          tv[0] = t[0]; tv[1] = t[1]; tv[2] = t[2]; tv[3] = t[3];
+        } else {
+          tv[0] = row[a * 4];
+        }
+        float cost = row[kSpC + a];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);

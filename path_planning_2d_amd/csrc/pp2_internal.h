@@ -126,7 +126,11 @@ constexpr int kDictMax = 400;  // coded_loop_lds_bytes(kDictMax, false) <= kDict
 // Sparse LDS rows: per action a, T at the base kernel's support kSup[a][0 ..
 // kSupN[a]) (base_kernel in pp2_kernels.hip; occupied neighbours and traps
 // only move mass to the centre, which is in every support), then C_a, then 0.
-constexpr int kSpRow = 54;  // 9 actions x 6 floats
+// Sparse row: [a][gT at kSup[a][0..3]] (9 x 4 floats, one 16-B quad per
+// action) | C[0..8] | pad: 52 floats = 13 quads, an odd count so that two
+// codes share a bank quad only when they differ by a multiple of 16.
+constexpr int kSpRow = 52;
+constexpr int kSpC = 36;  // offset of the C block
 // Raw T_u floats per entry in the belief gather's LDS table: the support
 // cells (sparse, 4) or all 9, padded to an odd stride so that two codes land
 // on the same LDS bank only when they differ by a multiple of 64.
