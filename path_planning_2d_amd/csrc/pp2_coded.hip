@@ -270,8 +270,18 @@ __device__ __forceinline__ void load_codes6(const uint16_t* __restrict__ code, i
   }
 }
 
-// The two halves of a coded fused step for one lane's 4 cells.
-template <bool SPARSE>
+// Support slot of T[.][u][i] in the sparse layout, or -1 (T == 0 there).
+__host__ __device__ constexpr int sup_slot(int u, int i) {
+  for (int j = 0; j < kSupN[u]; ++j)
+    if (kSup[u][j] == i) return j;
+  return -1;
+}
+
+// The two halves of a coded fused step for one lane's 4 cells.  U >= 0: the
+// action is known at compile time (sparse layout), so only its <= 4 support
+// terms are gathered -- the others are fmaf(+0, b, p) == p (b >= 0, p never
+// -0) -- in the same ascending-s order.
+template <bool SPARSE, int U = -1>
 __device__ __forceinline__ void belief_cells(const Geom& g, const float* sTu, const float* sL,
                                              const int (&slot)[9], float inv,
                                              const CodeWin6& cw, const Win6& win, int y, int x0,
@@ -283,7 +293,8 @@ __device__ __forceinline__ void belief_cells(const Geom& g, const float* sTu, co
 #pragma unroll
   for (int s = 0; s < 9; ++s) {
     const int oy = s / 3, ox = s % 3 - 1;
-    const int sl = slot[8 - s];
+    const int sl = U >= 0 ? sup_slot(U, 8 - s) : slot[8 - s];
+    if (U >= 0 && sl < 0) continue;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float tv = sl >= 0 ? sTu[cw.at(oy, k + 1 + ox) * LY::tu + sl] : 0.0f;
@@ -333,7 +344,7 @@ __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, flo
 // would not fit beside the belief's); no barrier follows the stores.
 //   rows: dictionary rows in the LDS layout (E x Layout::row floats)
 //   lz:   L_z column of the dictionary (E floats)
-template <bool SPARSE, int QPB, int MINB>
+template <bool SPARSE, int QPB, int MINB, int U = -1>
 __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
     const float* __restrict__ lz, const float* __restrict__ tu, int E,
@@ -394,7 +405,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     // kernel); unconditional compute with a guarded store spills heavily
     float local = 0.0f;
     if (ok) {
-      belief_cells<SPARSE>(g, sTu, sL, slot, inv, cw, bw, y, x0, b_out, local);
+      belief_cells<SPARSE, U>(g, sTu, sL, slot, inv, cw, bw, y, x0, b_out, local);
       const bool own = y >= own0 && y < own1;
       if (!own) local = 0.0f;
       PP2_PHASE(2);
@@ -415,7 +426,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       Win6 w2;
       load_codes6(code, g.wp, yy, xx, c2);
       load_win6(b_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
-      belief_cells<SPARSE>(g, sTu, sL, slot, inv, c2, w2, yy, xx, b_out, local);
+      belief_cells<SPARSE, U>(g, sTu, sL, slot, inv, c2, w2, yy, xx, b_out, local);
       const bool own = yy >= own0 && yy < own1;
       if (!own) local = 0.0f;
       load_win6(J_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
@@ -526,21 +537,36 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   float* J_out, uint8_t* A, int own0, int own1, float scale) {
   const size_t lds = coded_loop_lds_bytes(E, sparse);
   const int dense_blocks = cells_grid(g, 4);
-#define PP2_LOOPC(SP, Q, MB)                                                                    \
+#define PP2_LOOPC(SP, Q, MB, UU)                                                                \
   do {                                                                                          \
     if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                               \
     static bool attr = false;                                                                   \
-    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB>), attr);              \
+    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB, UU>), attr);          \
     const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                                \
-    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB>), dim3(grid), dim3(Q * kQuarter), lds, st,  \
+    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB, UU>), dim3(grid), dim3(Q * kQuarter), lds, \
+                       st,                                                                      \
                        g, gamma, code, rows, lz, tu, E, b_in, b_out, u, in_partials, in_n,      \
                        in_sum, in_sum_out, out_partials, dense_blocks, J_in, J_out, A, own0,    \
                        own1, scale);                                                            \
   } while (0)
   // sparse rows: two 512-thread workgroups per CU (~60 KB LDS each, <= 128
   // VGPRs, 4 waves per SIMD); full rows: one 1024-thread workgroup per CU
-  if (sparse) PP2_LOOPC(true, 2, 2);
-  else PP2_LOOPC(false, 4, 1);
+  // sparse rows: one kernel per action (its support terms only)
+  if (sparse) {
+    switch (u) {
+      case 0: PP2_LOOPC(true, 2, 2, 0); break;
+      case 1: PP2_LOOPC(true, 2, 2, 1); break;
+      case 2: PP2_LOOPC(true, 2, 2, 2); break;
+      case 3: PP2_LOOPC(true, 2, 2, 3); break;
+      case 4: PP2_LOOPC(true, 2, 2, 4); break;
+      case 5: PP2_LOOPC(true, 2, 2, 5); break;
+      case 6: PP2_LOOPC(true, 2, 2, 6); break;
+      case 7: PP2_LOOPC(true, 2, 2, 7); break;
+      default: PP2_LOOPC(true, 2, 2, 8); break;
+    }
+  } else {
+    PP2_LOOPC(false, 4, 1, -1);
+  }
 #undef PP2_LOOPC
   return hipGetLastError();
 }
