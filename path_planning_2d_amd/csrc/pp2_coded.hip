@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void k_dict_verify(Geom g, PlaneSet T, Plan
 // ---------------------------------------------------------------- kernels
 // Two LDS row layouts per dictionary entry:
 //  * full   (kDictTC = 90 floats): [a][gT_a0..gT_a8, C_a];
-//  * sparse (kSpRow = 52 floats):  [a][gT_a at kSup[a][0..3]] | C[0..8] | pad -- only
+//  * sparse (kSpRow = 44 floats):  gT at kSup[a][0..3] per move action | gT_4, C[0..8] -- only
 //    the base-kernel support of each action (at most 4 cells; the host checks
 //    every other T entry of every row is +0.0 before choosing it).
 // gT = fl(gamma * T), rounded once on the host exactly as the dense sweep
@@ -146,37 +146,38 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, int n,
 }
 
 // Bellman backup of 4 cells from their codes (k_mdp_sweep's arithmetic).
-// CELL_GRAIN: scheduling barrier after every cell (kernels capped at 64
-// VGPRs) instead of after every action.
-template <bool SPARSE, bool CELL_GRAIN>
+template <bool SPARSE>
 __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&cc)[4],
                                              const float (&jn)[9][4], float gamma,
                                              float (&best)[4], uint32_t (&arg)[4]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
   if constexpr (SPARSE) {
-    // fully unrolled (support positions index jn at compile time); the
-    // scheduling barrier keeps one cell's dictionary row live at a time
+    // cell-outer, fully unrolled (support positions index jn at compile
+    // time): a cell's 11 row quads are 11 ds_read_b128, the scheduling
+    // barrier keeps one cell's row live at a time.  Actions are still
+    // compared in ascending order, so best/arg are the dense kernel's.
 #pragma unroll
-    for (int a = 0; a < 9; ++a) {
+    for (int k = 0; k < 4; ++k) {
+      const float* row = sTC + cc[k] * kSpRow;
+      const f4a q8 = *reinterpret_cast<const f4a*>(row + 32);
+      const f4a q9 = *reinterpret_cast<const f4a*>(row + 36);
+      const f4a q10 = *reinterpret_cast<const f4a*>(row + 40);
+      const float cst[9] = {q8[1], q8[2], q8[3], q9[0], q9[1], q9[2], q9[3], q10[0], q10[1]};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float* row = sTC + cc[k] * kSpRow;
-        float tv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (kSupN[a] > 2) {
-          const f4a t = *reinterpret_cast<const f4a*>(row + a * 4);  // one ds_read_b128
+      for (int a = 0; a < 9; ++a) {
+        float tv[4] = {q8[0], 0.0f, 0.0f, 0.0f};
+        if (a != 4) {
+          const f4a t = *reinterpret_cast<const f4a*>(row + sp_t(a));
           tv[0] = t[0]; tv[1] = t[1]; tv[2] = t[2]; tv[3] = t[3];
-        } else {
-          tv[0] = row[a * 4];
         }
-        float cost = row[kSpC + a];
+        float cost = cst[a];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);
         if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
-        if (CELL_GRAIN) __builtin_amdgcn_sched_barrier(0);
       }
-      if (!CELL_GRAIN) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
     }
   } else {
     // one action at a time: 4 cells x 10 dictionary floats live (a fully
@@ -327,7 +328,7 @@ __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, flo
   const uint32_t cc[4] = {m0 & 0xffffu, m0 >> 16, m1 & 0xffffu, m1 >> 16};
   float best[4];
   uint32_t arg[4];
-  coded_sweep4<SPARSE, true>(sTC, cc, jn, gamma, best, arg);
+  coded_sweep4<SPARSE>(sTC, cc, jn, gamma, best, arg);
   const long long off = (long long)y * g.wp + x0;
   stv<4>(J_out + off, best);
   if (own)
@@ -466,7 +467,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
     load_jn(J_in, g.wp, y, x0, le, re, jn);
     float best[4];
     uint32_t arg[4];
-    coded_sweep4<SPARSE, true>(lds, cc, jn, gamma, best, arg);
+    coded_sweep4<SPARSE>(lds, cc, jn, gamma, best, arg);
     store_ja(J_out, A, off, best, arg);
   }
 }

@@ -126,11 +126,15 @@ constexpr int kDictMax = 400;  // coded_loop_lds_bytes(kDictMax, false) <= kDict
 // Sparse LDS rows: per action a, T at the base kernel's support kSup[a][0 ..
 // kSupN[a]) (base_kernel in pp2_kernels.hip; occupied neighbours and traps
 // only move mass to the centre, which is in every support), then C_a, then 0.
-// Sparse row: [a][gT at kSup[a][0..3]] (9 x 4 floats, one 16-B quad per
-// action) | C[0..8] | pad: 52 floats = 13 quads, an odd count so that two
-// codes share a bank quad only when they differ by a multiple of 16.
-constexpr int kSpRow = 52;
-constexpr int kSpC = 36;  // offset of the C block
+// Sparse row (44 floats = 11 quads, an odd count so that two codes share a
+// bank quad only when they differ by a multiple of 16):
+//   quads 0..7 : gT at kSup[a][0..3] of the 8 move actions (a != 4), one 16-B
+//                quad each (ds_read_b128)
+//   quads 8..10: gT_4 (the stay action's single support), C[0..8], 0, 0 --
+//                the 9 costs and the stay term in three quads.
+constexpr int kSpRow = 44;
+constexpr int kSpC = 33;  // offset of C[0]
+__host__ __device__ constexpr int sp_t(int a) { return a < 4 ? 4 * a : a == 4 ? 32 : 4 * (a - 1); }
 // Raw T_u floats per entry in the belief gather's LDS table: the support
 // cells (sparse, 4) or all 9, padded to an odd stride so that two codes land
 // on the same LDS bank only when they differ by a multiple of 64.

@@ -409,7 +409,8 @@ int build_model_dict(pp2_ctx* c) {
     for (int a = 0; a < 9; ++a) {
       // sweep rows hold fl(gamma * T) (the dense sweep's per-cell product)
       if (sparse) {
-        for (int j = 0; j < pp2::kSupN[a]; ++j) dst[a * 4 + j] = gam * src[a * 10 + pp2::kSup[a][j]];
+        for (int j = 0; j < pp2::kSupN[a]; ++j)
+          dst[pp2::sp_t(a) + j] = gam * src[a * 10 + pp2::kSup[a][j]];
         dst[pp2::kSpC + a] = src[a * 10 + 9];
       } else {
         for (int i = 0; i < 9; ++i) dst[a * 10 + i] = gam * src[a * 10 + i];
