@@ -23,7 +23,7 @@ A 1, the reference's fp32 tensor contract).
   * k_loop_step_coded (default; the model is dictionary-coded, see
     DESIGN.md §2.1) moves only 19 B per cell (code 2, b 4, b' 4, J 4, J' 4,
     A 1; `traffic`, `roofline_moved`), so its frac on the contract exceeds 1;
-    its binding resources are the per-launch latency chain and LDS (400 B of
+    its binding resources are the per-launch latency chain and LDS (196 B of
     dictionary reads per cell, `roofline_lds`);
   * k_loop_step (dense planes, `dense_path` leg, or --dense) moves the
     contract's 417 B.
@@ -52,7 +52,7 @@ BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
 BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
 BYTES_LOOP_CODED = 19            # per cell: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1
 BYTES_SWEEP_CODED = 11           # per cell: code 2 + J 4 + J' 4 + A 1
-LDS_BYTES_LOOP_CODED = 400       # per cell: T gather 9*4 + L_z 4 + sweep 9*(9+1)*4
+LDS_BYTES_LOOP_CODED = 196       # per cell (sparse rows): T_u gather 4*4 + L_z 4 + sweep 11*16
 LDS_PEAK_GBS = 150000.0          # ds_read_b64/b128 chip aggregate (MI355X_MICROARCH.md LDS)
 GAMMA = 0.95
 
