@@ -97,18 +97,25 @@ hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* ma
 
 // Batched fp16 rollouts (pp2_rollout.cpp).  Beliefs: fp16 [copy][rows+2][wp],
 // cstride halfs per copy, copy plane origin at row -1.  A chunk is a run of
-// copies (indices copies[first .. first+n)) sharing the step's action.
-int rollout_waves(const Geom& g);
-int rollout_chunk();      // copies per chunk (block) of the selected variant
+// rollout_chunk() copies (indices copies[first ..]) sharing the step's action.
+int rollout_waves(const Geom& g);       // partials per copy to allocate (>= both passes)
+int rollout_step_waves(const Geom& g);  // partials per copy of one step launch
+int rollout_leaf_waves(const Geom& g);  // partials per copy of the leaf pass
+int rollout_chunk();      // copies per chunk (workgroup) of the selected variant
 int rollout_min_chunk();  // smallest chunk of any variant (sizes chunk tables)
-// code/dict/E: the coded model (E > 0; pp2_coded.hip) or E = 0 for the planes
+// Model source: the coded model (E > 0: code plane, tu_all = the per-action
+// raw T tables [u][tstride] with tw floats per entry, sparse = support-only
+// rows; dl = L transposed [z][es]) or E = 0 for the T/L planes.  R is always
+// the R plane.  Writes bout, then stats_out[copy][3] (k_rollout_reduce).
 hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
-                               PlaneSet R, const uint16_t* code, const float* dict, int E,
-                               const void* bin, void* bout, long long cstride,
+                               PlaneSet R, const uint16_t* code, const float* tu_all,
+                               long long tstride, int tw, const float* dl, int es, int E,
+                               bool sparse, const void* bin, void* bout, long long cstride,
                                int nchunks, const int* chunk_u, const int* chunk_first,
-                               const int* chunk_n, const int* copies, const uint8_t* zs,
-                               const float* in_stats, float* partials, float* stats_out,
-                               int ncopies);
+                               const int* copies, const uint8_t* zs, const float* in_stats,
+                               float* partials, float* stats_out, int ncopies);
+hipError_t launch_rollout_reduce(hipStream_t st, const float* partials, int nwaves,
+                                 int ncopies, float* stats_out);
 hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const void* b,
                                long long cstride, int ncopies, float* partials, float* out);
 hipError_t launch_rollout_broadcast(hipStream_t st, const void* src, void* dst,

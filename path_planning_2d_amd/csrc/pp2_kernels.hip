@@ -863,19 +863,14 @@ hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* ma
 }
 
 // ============================================================================
-// Batched fp16 QV-tree rollouts (BASELINE configs[4]).  C copies of a belief
-// advance `depth` steps of the reference update (a2/a3), each copy with its
-// own (u, z) per step; every step scores the copy's QNode reward
-// <b, R[:,u]> (search_tree_cuda.cu:168-173), and the leaf is scored with the
-// FIB bound (fast_informed_bound_cuda.cu:278-297).
+// Batched fp16 QV-tree rollouts (BASELINE configs[4]): the per-copy
+// reduction of the step kernel's partials, the FIB leaf pass
+// (fast_informed_bound_cuda.cu:278-297) and the root broadcast.  The step
+// kernel itself (k_rollout_band) is in pp2_rollout_dev.hip.
 //  * beliefs live as fp16 planes [copy][row][x] (2 B per cell-copy), each
-//    copy max-normalised: the update of step k multiplies by 1/max_k, so the
-//    stored values stay O(1) and tiny probabilities keep fp16 precision;
-//  * the math is fp32 (the reference fma chain on fp16-decoded inputs);
-//  * copies are grouped by action: one block loads its T_u stencil rows once
-//    and reuses them for up to kRollChunk copies (T_u amortised over copies);
+//    copy max-normalised, math in fp32;
 //  * per (copy, wave) partial sums of {stored sum, stored max, reward dot} are
-//    reduced per copy by k_rollout_reduce.
+//    reduced per copy by k_rollout_reduce, in a fixed order.
 // ============================================================================
 
 template <bool ALIGNED>
@@ -886,188 +881,9 @@ __device__ __forceinline__ void ldh4(const _Float16* __restrict__ p, float (&v)[
   v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
 }
 
-struct RollRaw {  // one copy's raw stencil loads for one lane (4 cells)
-  h4 m[3];              // rows y-1, y, y+1 at x0..x0+3
-  uint32_t lw[3], rw[3];  // halves x0-2..x0-1 and x0+4..x0+5 of each row
-  float l[4];           // L_z at x0..x0+3
-};
-
-__device__ __forceinline__ _Float16 h2_lo(uint32_t w) {
-  return __builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu));
-}
-__device__ __forceinline__ _Float16 h2_hi(uint32_t w) {
-  return __builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
-}
-
-// b points at (row y, x0) of one copy; every address is dword aligned (x0 is
-// a multiple of 4) and lies inside the copy's halo rows or the guards.  The
-// L_z load is skipped on the coded path (L comes from the LDS dictionary).
-template <bool WITH_L>
-__device__ __forceinline__ void roll_load(RollRaw& q, const _Float16* __restrict__ b, int wp,
-                                          const float* __restrict__ lp) {
-#pragma unroll
-  for (int row = 0; row < 3; ++row) {
-    const _Float16* bp = b + (long long)(row - 1) * wp;
-    q.m[row] = *reinterpret_cast<const h4*>(bp);
-    q.lw[row] = *reinterpret_cast<const uint32_t*>(bp - 2);
-    q.rw[row] = *reinterpret_cast<const uint32_t*>(bp + 4);
-  }
-  if constexpr (WITH_L) {
-    const float4 l4 = *reinterpret_cast<const float4*>(lp);
-    q.l[0] = l4.x; q.l[1] = l4.y; q.l[2] = l4.z; q.l[3] = l4.w;
-  }
-}
-
 constexpr int kRollStats = 3;  // stored sum, stored max, reward dot
-constexpr int kRollIter = 8;   // 1024-cell slabs per block tile
-constexpr int kRollChunk = 8;  // copies per block (sharing one action)
-
-// A block owns kRollIter consecutive 1024-cell slabs (row-major over the
-// padded grid) for one chunk of <= kRollChunk copies that share the action:
-// the T_u stencil and R_u of a slab are loaded once for all copies, and each
-// copy's {sum, max, reward} stays in registers until one wave reduction per
-// copy at the end of the tile.
-// CODED: T_u and L come from the dictionary-coded model (pp2_coded.hip)
-// staged in LDS (the T_u column of the chunk's action, all 16 L columns)
-// instead of the dense planes; same values, so bit-identical results.
-template <int CH, int PF, bool CODED>
-__global__ __launch_bounds__(kBlock) void k_rollout_step(
-    Geom g, PlaneSet T, PlaneSet L, PlaneSet R, const uint16_t* __restrict__ code,
-    const float* __restrict__ dict, int E, const _Float16* __restrict__ bin,
-    _Float16* __restrict__ bout, long long cstride, const int* __restrict__ chunk_u,
-    const int* __restrict__ chunk_first, const int* __restrict__ copies,
-    const uint8_t* __restrict__ zs, const float* __restrict__ in_stats,
-    float* __restrict__ partials, int nwaves) {
-  // Chunks always hold CH entries (the host repeats a partial chunk's last
-  // copy; a repeat writes the same belief and partials as the original), and
-  // lanes past the grid end clamp to its last cell: the slab loop has no
-  // branches, so the compiler's vmcnt waits can follow the prefetch pipeline.
-  const int ch = blockIdx.y;
-  const int u = chunk_u[ch], first = chunk_first[ch];
-  const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  extern __shared__ float rlds[];
-  float* sT = rlds;           // [E][9]  T_u
-  float* sL = rlds + E * 9;   // [E][16] L
-  if constexpr (CODED) {
-    for (int i = threadIdx.x; i < E * 9; i += kBlock)
-      sT[i] = dict[(long long)(i / 9) * kDictRow + u * 10 + i % 9];
-    for (int i = threadIdx.x; i < E * 16; i += kBlock)
-      sL[i] = dict[(long long)(i / 16) * kDictRow + kDictL + i % 16];
-    __syncthreads();
-  }
-  const long long ncells = (long long)g.rows * g.wp;
-  const long long tile0 = (long long)blockIdx.x * kRollIter * (kBlock * 4);
-  const int iters = (int)min((long long)kRollIter, (ncells - tile0 + kBlock * 4 - 1) / (kBlock * 4));
-  long long cbase[CH];
-  int cid[CH], zc[CH];
-  float inv[CH], acc[CH][kRollStats];
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const int c = copies[first + j];
-    cid[j] = c;
-    cbase[j] = (long long)c * cstride;
-    zc[j] = zs[c];
-    inv[j] = 1.0f / in_stats[c * kRollStats + 1];  // 1 / stored max
-    acc[j][0] = acc[j][1] = acc[j][2] = 0.0f;
-  }
-  for (int it = 0; it < iters; ++it) {
-    const long long cell_raw = tile0 + (long long)it * (kBlock * 4) + threadIdx.x * 4;
-    const bool valid = cell_raw < ncells;
-    const long long cell = valid ? cell_raw : ncells - 4;
-    const int y = (int)(cell / g.wp), x0 = (int)(cell % g.wp);
-    const bool le = x0 == 0, re = x0 + 4 == g.wp;
-    float tv[9][4], rv[4];
-    uint32_t lc[4] = {0, 0, 0, 0};  // coded: L row offsets of the 4 cells
-    if constexpr (CODED) {
-      CodeWin w;
-      load_codes(code, g.wp, y, x0, w);
-#pragma unroll
-      for (int s = 0; s < 9; ++s) {
-        const int oy = s / 3 - 1, ox = s % 3 - 1;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) tv[s][k] = sT[w.c[oy + 1][k + 1 + ox] * 9 + 8 - s];
-        if (ox < 0 && le) tv[s][0] = 0.0f;
-        if (ox > 0 && re) tv[s][3] = 0.0f;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) lc[k] = w.c[1][k + 1] * 16;
-    } else {
-#pragma unroll
-      for (int s = 0; s < 9; ++s) {
-        const int oy = s / 3 - 1, ox = s % 3 - 1;
-        const float* tp = T.p + (long long)(y + oy) * T.rs + (long long)(9 * u + 8 - s) * T.ps + x0 + ox;
-        if (ox == 0) ldv<4, true>(tp, tv[s]);
-        else ldv<4, false>(tp, tv[s]);
-        if (ox < 0 && le) tv[s][0] = 0.0f;
-        if (ox > 0 && re) tv[s][3] = 0.0f;
-      }
-    }
-    ldv<4, true>(R.p + (long long)y * R.rs + (long long)u * R.ps + x0, rv);
-    const long long off = (long long)y * g.wp + x0;
-    const float* lrow = L.p + (long long)y * L.rs + x0;
-    // software pipeline over the chunk: copy j+PF's loads are in flight while
-    // copy j is computed (one copy at a time leaves too few bytes in flight
-    // per wave to cover HBM latency)
-    RollRaw q[PF + 1];
-#pragma unroll
-    for (int j = 0; j < PF; ++j)
-      roll_load<!CODED>(q[j], bin + cbase[j] + off, g.wp, lrow + (long long)zc[j] * L.ps);
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      if (j + PF < CH)
-        roll_load<!CODED>(q[(j + PF) % (PF + 1)], bin + cbase[j + PF] + off, g.wp,
-                  lrow + (long long)zc[j + PF] * L.ps);
-      const RollRaw& r = q[j % (PF + 1)];
-      float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bcen[4];
-#pragma unroll
-      for (int row = 0; row < 3; ++row) {
-        // x+-1 neighbours: aligned 8-byte centre load + the adjacent halves
-        // of the dwords either side (fp16 x+-1 loads are not dword aligned)
-        float w[6];
-        w[0] = le ? 0.0f : (float)h2_hi(r.lw[row]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[1 + k] = (float)r.m[row][k];
-        w[5] = re ? 0.0f : (float)h2_lo(r.rw[row]);
-        if (row == 1) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) bcen[k] = w[1 + k];
-        }
-#pragma unroll
-        for (int ox = -1; ox <= 1; ++ox) {
-          const int s = row * 3 + (ox + 1);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) p[k] = __builtin_fmaf(tv[s][k], w[k + 1 + ox], p[k]);
-        }
-      }
-      h4 o;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float lz;
-        if constexpr (CODED) lz = sL[lc[k] + zc[j]];
-        else lz = r.l[k];
-        const float v = (p[k] * lz) * inv[j];
-        o[k] = (_Float16)v;
-        const float vr = valid ? (float)o[k] : 0.0f;
-        acc[j][0] += vr;
-        acc[j][1] = fmaxf(acc[j][1], vr);
-        acc[j][2] = __builtin_fmaf(valid ? bcen[k] : 0.0f, rv[k], acc[j][2]);
-      }
-      __builtin_nontemporal_store(o, reinterpret_cast<h4*>(bout + cbase[j] + off));
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const float sm = wave_sum(acc[j][0]);
-    const float mx = wave_max(acc[j][1]);
-    const float rw = wave_sum(acc[j][2]);
-    if ((threadIdx.x & 63) == 0) {
-      float* pp = partials + ((long long)cid[j] * nwaves + wave) * kRollStats;
-      pp[0] = sm;
-      pp[1] = mx;
-      pp[2] = rw;
-    }
-  }
-}
+constexpr int kRollIter = 8;   // 1024-cell slabs per leaf-pass block tile
+constexpr int kRollChunk = 8;  // copies per leaf-pass block
 
 // per copy: out[c] = {sum, max, reward} over its nwaves partials (fixed order)
 __global__ __launch_bounds__(64) void k_rollout_reduce(const float* __restrict__ partials,
@@ -1093,13 +909,14 @@ __global__ __launch_bounds__(64) void k_rollout_reduce(const float* __restrict__
 }
 
 // Leaf FIB dots of every copy: partials[c][wave][10] = {sum, dot_0..dot_8};
-// same tiling as k_rollout_step, the alpha planes loaded once per slab.
+// 1024-cell slabs of kRollChunk copies per block, the alpha planes loaded
+// once per slab.
 __global__ __launch_bounds__(kBlock) void k_rollout_leaf(Geom g, PlaneSet F,
                                                          const _Float16* __restrict__ b,
                                                          long long cstride, int copies,
                                                          float* __restrict__ partials,
                                                          int nwaves) {
-  // branch-free like k_rollout_step: copies past the end repeat the last one
+  // branch-free like k_rollout_band: copies past the end repeat the last one
   // (identical partials), lanes past the grid end add nothing
   const int c0 = blockIdx.y * kRollChunk;
   const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
@@ -1179,60 +996,15 @@ int rollout_tiles(const Geom& g) {
   const long long per = (long long)kRollIter * kBlock * 4;
   return (int)((cells + per - 1) / per);
 }
-int rollout_waves(const Geom& g) { return rollout_tiles(g) * (kBlock / 64); }
-
-// (copies per chunk, prefetch distance) variants of k_rollout_step;
-// PP2_ROLLOUT_VARIANT selects one for A/B runs (tools/prof_rollout.py).
-namespace {
-struct RollVariant { int ch, pf; };
-constexpr RollVariant kRollVariants[] = {{8, 1}, {8, 2}, {4, 1}, {4, 2}, {16, 1}, {8, 3}};
-int roll_variant() {
-  static const int v = [] {
-    const char* e = getenv("PP2_ROLLOUT_VARIANT");
-    const int i = e ? atoi(e) : 0;
-    return (i >= 0 && i < (int)(sizeof(kRollVariants) / sizeof(kRollVariants[0]))) ? i : 0;
-  }();
-  return v;
+int rollout_leaf_waves(const Geom& g) { return rollout_tiles(g) * (kBlock / 64); }
+int rollout_waves(const Geom& g) {
+  const int a = rollout_leaf_waves(g), b = rollout_step_waves(g);
+  return a > b ? a : b;
 }
-}  // namespace
-int rollout_chunk() { return kRollVariants[roll_variant()].ch; }
-int rollout_min_chunk() { return 4; }
 
-hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
-                               PlaneSet R, const uint16_t* code, const float* dict, int E,
-                               const void* bin, void* bout, long long cstride,
-                               int nchunks, const int* chunk_u, const int* chunk_first,
-                               const int* chunk_n, const int* copies, const uint8_t* zs,
-                               const float* in_stats, float* partials, float* stats_out,
-                               int ncopies) {
-  const int tiles = rollout_tiles(g);
-  const int nw = rollout_waves(g);
-  // copy planes start at row -1: the kernels index rows from row 0
-  const dim3 grid(tiles, nchunks);
-  const _Float16* bi = (const _Float16*)bin + g.wp;
-  _Float16* bo = (_Float16*)bout + g.wp;
-#define PP2_ROLL(CH, PF)                                                                    \
-  do {                                                                                      \
-    if (E > 0)                                                                              \
-      hipLaunchKernelGGL((k_rollout_step<CH, PF, true>), grid, dim3(kBlock), lds, st, g, T,  \
-                         L, R, code, dict, E, bi, bo, cstride, chunk_u, chunk_first, copies, \
-                         zs, in_stats, partials, nw);                                       \
-    else                                                                                    \
-      hipLaunchKernelGGL((k_rollout_step<CH, PF, false>), grid, dim3(kBlock), 0, st, g, T,   \
-                         L, R, code, dict, 0, bi, bo, cstride, chunk_u, chunk_first, copies, \
-                         zs, in_stats, partials, nw);                                       \
-  } while (0)
-  const size_t lds = (size_t)E * 25 * sizeof(float);
-  switch (roll_variant()) {
-    case 1: PP2_ROLL(8, 2); break;
-    case 2: PP2_ROLL(4, 1); break;
-    case 3: PP2_ROLL(4, 2); break;
-    case 4: PP2_ROLL(16, 1); break;
-    case 5: PP2_ROLL(8, 3); break;
-    default: PP2_ROLL(8, 1); break;
-  }
-#undef PP2_ROLL
-  hipLaunchKernelGGL(k_rollout_reduce, dim3(ncopies), dim3(64), 0, st, partials, nw, ncopies,
+hipError_t launch_rollout_reduce(hipStream_t st, const float* partials, int nwaves,
+                                 int ncopies, float* stats_out) {
+  hipLaunchKernelGGL(k_rollout_reduce, dim3(ncopies), dim3(64), 0, st, partials, nwaves, ncopies,
                      stats_out);
   return hipGetLastError();
 }
@@ -1241,7 +1013,7 @@ hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const 
                                long long cstride, int ncopies, float* partials,
                                float* out) {
   const int tiles = rollout_tiles(g);
-  const int nw = rollout_waves(g);
+  const int nw = rollout_leaf_waves(g);
   const int gy = (ncopies + kRollChunk - 1) / kRollChunk;
   hipLaunchKernelGGL(k_rollout_leaf, dim3(tiles, gy), dim3(kBlock), 0, st, g, F,
                      (const _Float16*)b + g.wp, cstride, ncopies, partials, nw);

@@ -1,8 +1,9 @@
 // pp2_rollout.cpp -- batched fp16 QV-tree rollouts (C ABI pp2_rollout_*).
 //
-// Host driver of k_rollout_step / k_rollout_leaf (pp2_kernels.hip): groups the
-// copies of every step by action (chunks of <= kChunk copies sharing u, so a
-// block reuses its T_u stencil rows for all of them), chains the depth steps
+// Host driver of k_rollout_band (pp2_rollout_dev.hip) and k_rollout_leaf
+// (pp2_kernels.hip): groups the copies of every step by action (chunks of
+// rollout_chunk() copies sharing u, so a wave gathers its T_u stencil terms
+// once for all of them), chains the depth steps
 // on the context's stream, and turns the per-copy {stored sum, stored max,
 // reward dot} statistics into rewards, observation likelihoods and values.
 #include <algorithm>
@@ -168,11 +169,13 @@ int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs) {
   for (int k = 0; k < D; ++k) {
     const int* base = r->d_chunks + k * stride;
     const bool coded = coded_active(c);
+    const int E = coded ? c->dict_n : 0;
+    const int tw = pp2::tu_width(c->dict_sparse);
     HIPCHK(pp2::launch_rollout_step(c->stream, c->g, c->T.v, c->L.v, c->R.v, c->d_code,
-                                    c->d_dict, coded ? c->dict_n : 0, r->buf[k & 1],
+                                    c->d_tu, ((long long)E * tw + 3) & ~3LL, tw, c->d_dl,
+                                    (E + 3) & ~3, E, c->dict_sparse, r->buf[k & 1],
                                     r->buf[(k + 1) & 1], r->cstride, r->nchunks[k], base,
-                                    base + M, base + 2 * M, base + 3 * M,
-                                    r->d_zs + (size_t)k * C,
+                                    base + M, base + 3 * M, r->d_zs + (size_t)k * C,
                                     r->d_stats + (size_t)k * C * kRollStats, r->d_partials,
                                     r->d_stats + (size_t)(k + 1) * C * kRollStats, C));
   }

@@ -1,0 +1,544 @@
+// pp2_rollout_dev.hip -- the batched fp16 rollout step kernel (gfx950).
+//
+// BASELINE configs[4]: C copies of a belief, each advanced by the reference
+// update (a2/a3: point_based_value_iteration_cuda.cu:88-133 with the
+// renormalisation of search_tree_cuda.cu:225-229) under its own (u, z) per
+// step, scoring its QNode reward <b, R[:,u]> (search_tree_cuda.cu:168-173).
+// Beliefs are fp16 planes [copy][row -1 .. rows][wp], max-normalised per copy
+// (the update of step k multiplies by 1 / max_k); the math is fp32.
+//
+// The step is HBM-bound on 2 B read + 2 B written per cell-copy (measured
+// ceiling for this traffic on MI355X: a plain streaming copy runs 4.5-5.9
+// TB/s read+write, tools/micro/copy_bw.hip).  The kernel moves each belief
+// byte once:
+//  * a wave walks DOWN a band of kBandRows rows of one 256-column segment
+//    (64 lanes x 4 cells) and keeps each copy's rows y-1, y, y+1 in
+//    registers; row y+1 comes from an LDS ring that LDS-DMA
+//    (global_load_lds, no VGPRs) fills NS-1 rows ahead -- beliefs, codes,
+//    R_u and the segment-edge dwords of every copy -- with explicit vmcnt
+//    waits (the compiler's own would drain the ring at every LDS read);
+//  * the x-1 / x+4 neighbours come from the adjacent lanes by DPP wave
+//    shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1); lanes 0 and 63, which
+//    have no neighbour lane, keep the DPP's `old` operand: the edge dword;
+//  * the CH copies of a workgroup share the step's action, so the T_u
+//    coefficients of a row (from the coded model's LDS table, by the codes
+//    of the 3x3 neighbourhood, or from the dense T planes) are gathered once
+//    for all of them; on a sparse model only the action's <= 4 support terms
+//    are gathered (the others are fmaf(+0, b, p) == p exactly, b >= 0);
+//  * the fp16 -> fp32 decode folds into v_fma_mix_f32, the stored-sum
+//    statistic into v_dot2c_f32_f16, the output pack into v_cvt_pk_f16_f32;
+//  * each copy's {stored sum, stored max, reward dot} stays in registers for
+//    the band and is written as one partial per (copy, wave), reduced per
+//    copy by k_rollout_reduce (pp2_kernels.hip) in a fixed order.
+// Per cell the arithmetic is the dense update's: p = sum_s fmaf(T, b, p) in
+// ascending stencil order s, then p * fl(L_z / max).  The coded and dense
+// model sources give bit-identical beliefs and statistics.
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "pp2_device.h"
+
+namespace pp2 {
+namespace {
+
+constexpr int kSegCells = 256;  // columns of one wave (64 lanes x 4 cells)
+constexpr int kBandRows = 32;   // rows one wave walks
+constexpr int kRollStats = 3;   // stored sum, stored max, reward dot
+
+enum Src { kSparse = 0, kFull = 1, kDense = 2 };
+
+// Number of stencil terms and the stencil index s of term t (ascending s).
+// Sparse: the support of action U (kSup[U][.] ascending in i = 8 - s).
+template <int SRC, int U>
+__host__ __device__ constexpr int n_terms() { return SRC == kSparse ? kSupN[U] : 9; }
+template <int SRC, int U>
+__host__ __device__ constexpr int term_s(int t) {
+  return SRC == kSparse ? 8 - kSup[U][kSupN[U] - 1 - t] : t;
+}
+// Column of term t in a tu table row (sparse: support slot; full: i = 8 - s).
+template <int SRC, int U>
+__host__ __device__ constexpr int term_col(int t) {
+  return SRC == kSparse ? kSupN[U] - 1 - t : 8 - t;
+}
+
+// One row of a lane's window: cells x0..x0+3 as two fp16 (or uint16 code)
+// pairs, and the two dwords the DPP wave shifts deliver: l (high half =
+// cell x0-1) and r (low half = cell x0+4).  v_fma_mix_f32 reads either half
+// of a dword directly, so no unpacking is done.
+struct Row4 {
+  uint32_t lo, hi, l, r;
+};
+
+__device__ __forceinline__ uint32_t at(const Row4& w, int c) {
+  switch (c) {
+    case 0: return w.l >> 16;
+    case 1: return w.lo & 0xffffu;
+    case 2: return w.lo >> 16;
+    case 3: return w.hi & 0xffffu;
+    case 4: return w.hi >> 16;
+    default: return w.r & 0xffffu;
+  }
+}
+
+__device__ __forceinline__ float hf(uint32_t h) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)h);
+}
+
+// A row as read from the ring: the lane's 4 cells (8 B), and the edge dword
+// that lanes 0 / 63 use as the neighbour outside the segment (lane 0: the
+// dword ending at x0-1, lane 63: the dword starting at x0+4; zeros outside
+// the grid).
+struct Raw {
+  uint2 m;
+  uint32_t e;
+};
+
+__device__ __forceinline__ const char* cptr(const void* base, uint32_t off) {
+  return reinterpret_cast<const char*>(base) + off;
+}
+
+// Window row from a raw load: lane i gets lane i-1's high dword and lane
+// i+1's low dword by DPP wave shifts; a lane without a source lane (0 for
+// wave_shr, 63 for wave_shl) keeps the `old` operand, its loaded edge dword.
+__device__ __forceinline__ Row4 make_row(const Raw& q) {
+  Row4 w;
+  w.lo = q.m.x;
+  w.hi = q.m.y;
+  w.l = (uint32_t)__builtin_amdgcn_update_dpp((int)q.e, (int)q.m.y, 0x138, 0xf, 0xf, false);
+  w.r = (uint32_t)__builtin_amdgcn_update_dpp((int)q.e, (int)q.m.x, 0x130, 0xf, 0xf, false);
+  return w;
+}
+
+struct BandArgs {
+  Geom g;
+  PlaneSet T, L, R;
+  const uint16_t* code;  // code plane at row -1
+  const _Float16* bin;   // copy 0's plane at row -1
+  _Float16* bout;
+  long long cstride;
+  float* partials;
+  int nwaves;
+};
+
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+// LDS-DMA (global_load_lds): global -> LDS without VGPRs, so a wave keeps
+// NS-1 rows of loads in flight at no register cost.  The compiler does not
+// track these copies: band() waits for them with an explicit s_waitcnt.
+__device__ __forceinline__ void dma4(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((glb_void*)g, (lds_void*)l, 4, 0, 0);
+}
+__device__ __forceinline__ void dma16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((glb_void*)g, (lds_void*)l, 16, 0, 0);
+}
+
+// Ring slot of one row (bytes): CH belief rows of the segment (512 B each),
+// the code row (512), the R_u row (1 KB) and 64 edge dwords (lane l of the
+// edge copy writes dword l: 2j / 2j+1 = copy j's x-1 / x+256 dwords, 2CH /
+// 2CH+1 the code row's).
+template <int CH>
+struct Slot {
+  static constexpr int code = CH * 512, r = code + 512, edge = r + 1024, bytes = edge + 256;
+  static constexpr int groups = 2 * CH + 4;  // DMA instructions per row
+};
+
+// One wave's band: rows [ya, yb) of the segment starting at xs.
+// sTu: [E][TW] T_u table (coded); sLz: [CH][E] L_z * (1 / max) of each copy;
+// ring: this wave's NS slots.  Row r of a copy / code plane is at byte
+// offset 2 (r + 1) wp (row -1 = 0, the zero halo row that cells outside the
+// grid and lanes past the row end read instead).  Those lanes' outputs are
+// exactly 0 (zero beliefs; codes of the all-zero halo tuple, L = 0); they
+// store them into row -1 and add 0 to every statistic, so no lane is masked
+// (the dense source zeroes their L_z explicitly: its L plane is read at the
+// clamped cell).
+template <int CH, int NS, int SRC, int U>
+__device__ __forceinline__ void band(const BandArgs& a, const float* sTu, const float* sLz,
+                                     char* ring, int E, int ecid, const int (&cid)[CH],
+                                     const int (&zc)[CH], const float (&inv)[CH], int u, int ya,
+                                     int yb, int xs, int lane, float (&acc)[CH][kRollStats]) {
+  using SL_ = Slot<CH>;
+  constexpr int NT = n_terms<SRC, U>();
+  constexpr int TW = tu_width(SRC == kSparse);
+  constexpr int G = SL_::groups;
+  const Geom& g = a.g;
+  const int x0 = xs + 4 * lane;  // this lane's first cell (compute)
+  const bool xok = x0 < g.wp;
+  const int xc = xok ? x0 : g.wp - 4;
+  const uint32_t rowb = 2u * (uint32_t)g.wp;  // bytes per plane row
+  // DMA lanes: 2 cells per lane and copy instruction (h = 0, 1 halves)
+  const int dx0 = xs + 2 * lane, dx1 = dx0 + 128;
+  const bool d0ok = dx0 < g.wp, d1ok = dx1 < g.wp;
+  const uint32_t db0 = 2u * (uint32_t)dx0, db1 = 2u * (uint32_t)dx1;
+  // edge lanes: 2j / 2j+1 -> copy j's dword at xs-2 / xs+256, 2CH / 2CH+1 the
+  // code row's; outside the grid -> row -1 (zeros)
+  const int ej = lane >> 1, es_ = lane & 1;
+  const bool eside_ok = es_ == 0 ? xs > 0 : xs + 256 < g.wp;
+  const uint32_t ebyte = 2u * (uint32_t)(es_ == 0 ? xs - 2 : xs + 256);
+  const void* ebase = ej < CH ? (const void*)(a.bin + (long long)ecid * a.cstride)
+                              : (const void*)a.code;
+  const bool eok = eside_ok && ej <= CH;
+  const _Float16* bb[CH];
+  _Float16* ob[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    bb[j] = a.bin + (long long)cid[j] * a.cstride;
+    ob[j] = a.bout + (long long)cid[j] * a.cstride;
+  }
+  const float* rbase = a.R.p + (long long)u * a.R.ps + xs;
+  const bool rok = xs + 4 * lane < g.wp;  // R lane (4 floats)
+  // issue the DMA group of row r (beliefs, codes, edges, R_u) into a slot
+  auto issue = [&](int r, char* slot) {
+    const uint32_t ro = (uint32_t)(r + 1) * rowb;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      dma4(cptr(bb[j], d0ok ? ro + db0 : 0u), slot + j * 512);
+      dma4(cptr(bb[j], d1ok ? ro + db1 : 0u), slot + j * 512 + 256);
+    }
+    if constexpr (SRC != kDense) {
+      dma4(cptr(a.code, d0ok ? ro + db0 : 0u), slot + SL_::code);
+      dma4(cptr(a.code, d1ok ? ro + db1 : 0u), slot + SL_::code + 256);
+    } else {
+      dma4(cptr(bb[0], 0u), slot + SL_::code);  // keep G fixed (zeros)
+      dma4(cptr(bb[0], 0u), slot + SL_::code + 256);
+    }
+    const int rr = r < yb ? (r >= 0 ? r : 0) : yb - 1;  // R rows stay inside the grid
+    dma16(rbase + (rok ? (long long)rr * a.R.rs + 4 * lane : 0), slot + SL_::r);
+    dma4(cptr(ebase, eok ? ro + ebyte : 0u), slot + SL_::edge);
+  };
+  // wait until at most n VMEM ops are outstanding.  vmcnt counts loads,
+  // LDS-DMA copies and stores in issue order (gfx9 has no separate store
+  // counter), and every phase issues its DMA group, then its CH stores, in
+  // a fixed order (compiler barriers at the phase boundaries), so "row y+1
+  // has landed" is vmcnt <= (the ops issued after its group).
+  auto wait_n = [&](auto n) {
+    constexpr int N = decltype(n)::value;
+    static_assert(N < 64, "vmcnt is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  };
+  auto slot_of = [&](int r) { return ring + ((r - ya + 1) % NS) * SL_::bytes; };
+  const int e_own = lane == 0 ? 0 : 1;  // lane 0 -> the x-1 dword, lane 63 -> x+256
+  // Ring reads are inline asm: the compiler tracks LDS-DMA writes only
+  // coarsely and would put a vmcnt(0) -- a drain of every row in flight --
+  // before any LDS read it sees.  read_rows() issues a slot's reads, waits
+  // for them (lgkmcnt), and pins the results below that wait.
+  auto read_rows = [&](const char* slot, Raw (&q)[CH + 1]) {
+    const uint32_t rb = (uint32_t)(uintptr_t)(slot) + 8u * (uint32_t)lane;
+    const uint32_t eb2 = (uint32_t)(uintptr_t)(slot) + SL_::edge + 4u * (uint32_t)e_own;
+#pragma unroll
+    for (int j = 0; j <= CH; ++j) {
+      if (SRC == kDense && j == CH) break;
+      asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(q[j].m) : "v"(rb), "i"(j * 512));
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(q[j].e) : "v"(eb2), "i"(8 * j));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j <= CH; ++j) {
+      if (SRC == kDense && j == CH) break;
+      asm volatile("" : "+v"(q[j].m), "+v"(q[j].e));
+    }
+  };
+  auto read_r = [&](const char* slot, float (&r4)[4]) {
+    const uint32_t ab = (uint32_t)(uintptr_t)(slot) + SL_::r + 16u * (uint32_t)lane;
+    f4a t;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(ab) : "memory");
+    r4[0] = t[0]; r4[1] = t[1]; r4[2] = t[2]; r4[3] = t[3];
+  };
+  Row4 W[CH][3], CW[3];
+  // prologue: rows ya-1 .. ya+NS-2 in flight; rows ya-1, ya into window slots
+  // 0, 1 once their groups have landed
+#pragma unroll
+  for (int r = 0; r < NS; ++r) issue(ya - 1 + r <= yb ? ya - 1 + r : yb, ring + r * SL_::bytes);
+  wait_n(std::integral_constant<int, (NS - 2) * G>{});
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    Raw q[CH + 1];
+    read_rows(ring + r * SL_::bytes, q);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) W[j][r] = make_row(q[j]);
+    if constexpr (SRC != kDense) CW[r] = make_row(q[CH]);
+  }
+
+  auto step = [&](auto phase, int y) {
+    constexpr int P = decltype(phase)::value;
+    constexpr int S0 = P % 3, S1 = (P + 1) % 3, S2 = (P + 2) % 3;  // rows y-1, y, y+1
+    // refill the slot of row y-1 (fully consumed) with row y+NS-1, then
+    // wait for row y+1's group (NS-2 younger groups may stay in flight)
+    {
+      asm volatile("" ::: "memory");  // the slot's last reads stay above its refill
+      const int rn = y + NS - 1 <= yb ? y + NS - 1 : yb;
+      issue(rn, slot_of(y - 1));
+    }
+    // ops issued after row y+1's group: the NS-2 younger groups, plus the
+    // stores of the phases between (none yet in the band's first phase;
+    // one phase's in the second; NS-2 phases' from then on)
+    if (y >= ya + NS - 2) wait_n(std::integral_constant<int, (NS - 2) * (G + CH)>{});
+    else if (y == ya) wait_n(std::integral_constant<int, (NS - 2) * G>{});
+    else wait_n(std::integral_constant<int, (NS - 2) * G + CH>{});
+    const char* sn = slot_of(y + 1);
+    const char* sc = slot_of(y);
+    {
+      Raw q[CH + 1];
+      read_rows(sn, q);
+#pragma unroll
+      for (int j = 0; j < CH; ++j) W[j][S2] = make_row(q[j]);
+      if constexpr (SRC != kDense) CW[S2] = make_row(q[CH]);
+    }
+    float rcur[4];
+    read_r(sc, rcur);
+    constexpr int SL[3] = {S0, S1, S2};
+    // T_u coefficients of the row's NT stencil terms (shared by the copies)
+    float tv[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int s = term_s<SRC, U>(t);
+      const int oy = s / 3, ox = s % 3 - 1;
+      if constexpr (SRC == kDense) {
+        const float* tp = a.T.p + (long long)(y - 1 + oy) * a.T.rs +
+                          (long long)(9 * u + 8 - s) * a.T.ps + xc + ox;
+        if (ox == 0) ldv<4, true>(tp, tv[t]);
+        else ldv<4, false>(tp, tv[t]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          tv[t][k] = sTu[at(CW[SL[oy]], k + 1 + ox) * TW + term_col<SRC, U>(t)];
+      }
+    }
+    uint32_t lzo[4] = {0, 0, 0, 0};  // coded: the cells' own codes (L_z rows)
+    if constexpr (SRC != kDense) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lzo[k] = at(CW[S1], k + 1);
+    }
+    const uint32_t so = xok ? (uint32_t)(y + 1) * rowb + 2u * (uint32_t)x0 : 0u;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      float li[4];  // L_z * (1 / max) of the 4 cells
+      if constexpr (SRC == kDense) {
+        float lz[4];
+        ldv<4, true>(a.L.p + (long long)y * a.L.rs + (long long)zc[j] * a.L.ps + xc, lz);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) li[k] = xok ? lz[k] * inv[j] : 0.0f;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) li[k] = sLz[j * E + lzo[k]];
+      }
+      float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int s = term_s<SRC, U>(t);
+        const int oy = s / 3, ox = s % 3 - 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          p[k] = __builtin_fmaf(tv[t][k], hf(at(W[j][SL[oy]], k + 1 + ox)), p[k]);
+      }
+      float v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = p[k] * li[k];
+      // stored values; max(fp16(v)) == fp16(max(v)) (rounding is monotone),
+      // so the max is taken on v and rounded once per wave
+      const h2v h01 = {(_Float16)v[0], (_Float16)v[1]};
+      const h2v h23 = {(_Float16)v[2], (_Float16)v[3]};
+      const h2v one = {(_Float16)1.0f, (_Float16)1.0f};
+      acc[j][0] = __builtin_amdgcn_fdot2(h01, one, acc[j][0], false);
+      acc[j][0] = __builtin_amdgcn_fdot2(h23, one, acc[j][0], false);
+      acc[j][1] = fmaxf(fmaxf(acc[j][1], v[0]), v[1]);
+      acc[j][1] = fmaxf(fmaxf(acc[j][1], v[2]), v[3]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        acc[j][2] = __builtin_fmaf(hf(at(W[j][S1], k + 1)), rcur[k], acc[j][2]);
+      const u2v o = {__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23)};
+      __builtin_nontemporal_store(o, reinterpret_cast<u2v*>(reinterpret_cast<char*>(ob[j]) + so));
+    }
+  };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  using P2 = std::integral_constant<int, 2>;
+  // whole 3-row groups (every window slot returns to its register), then
+  // the tail
+  int y = ya;
+  for (; y + 3 <= yb; y += 3) {
+    step(P0{}, y);
+    step(P1{}, y + 1);
+    step(P2{}, y + 2);
+  }
+  if (y < yb) step(P0{}, y);
+  if (y + 1 < yb) step(P1{}, y + 1);
+  // drain: no DMA may still target this wave's ring when the slot memory
+  // is reused (by the next workgroup on the CU)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// grid: nchunks x gx workgroups of 4 waves (1-D, XCD-remapped so that the
+// waves of one chunk run on one XCD and share its L2 for the band halos).
+// Wave v of a chunk walks band v / nseg of segment v % nseg.
+template <int CH, int NS, int WPS, int SRC>
+__global__ __launch_bounds__(kBlock, WPS) void k_rollout_band(
+    BandArgs a, const float* __restrict__ tu_all, long long tstride,
+    const float* __restrict__ dl, int es, int E, int gx, int nseg, int nband,
+    const int* __restrict__ chunk_u, const int* __restrict__ chunk_first,
+    const int* __restrict__ copies, const uint8_t* __restrict__ zs,
+    const float* __restrict__ in_stats) {
+  constexpr int TW = tu_width(SRC == kSparse);
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int ch = lin / gx, bx = lin % gx;
+  const int u = chunk_u[ch], first = chunk_first[ch];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // the rings are their own LDS object, so the compiler's LDS-DMA tracking
+  // can tell them from the dictionary tables (sTu [E][TW], sLz [CH][E])
+  __shared__ __attribute__((aligned(16))) char rings[4 * NS * Slot<CH>::bytes];
+  extern __shared__ float rlds[];
+  char* ring = rings + w * NS * Slot<CH>::bytes;
+  float* sTu = rlds;
+  float* sLz = sTu + ((E * TW + 3) & ~3);
+  int cid[CH], zc[CH];
+  float inv[CH], acc[CH][kRollStats];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int c = copies[first + j];
+    cid[j] = c;
+    zc[j] = zs[c];
+    inv[j] = 1.0f / in_stats[c * kRollStats + 1];  // 1 / stored max
+    acc[j][0] = acc[j][1] = acc[j][2] = 0.0f;
+  }
+  if constexpr (SRC != kDense) {
+    const float* tu = tu_all + (long long)u * tstride;
+    for (int i = threadIdx.x; i < E * TW; i += kBlock) sTu[i] = tu[i];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const float* lz = dl + (long long)zc[j] * es;
+      for (int e = threadIdx.x; e < E; e += kBlock) sLz[j * E + e] = lz[e] * inv[j];
+    }
+    __syncthreads();
+  }
+  // the copy whose edge dwords this lane fetches (lanes 2j, 2j+1 -> copy j)
+  const int ecid = copies[first + ((lane >> 1) < CH ? (lane >> 1) : CH - 1)];
+  const int v = bx * 4 + w;
+  const int seg = v % nseg, bnd = v / nseg;
+  if (bnd < nband) {
+    const int ya = bnd * kBandRows;
+    const int yb = ya + kBandRows < a.g.rows ? ya + kBandRows : a.g.rows;
+    const int xs = seg * kSegCells;
+    if constexpr (SRC == kSparse) {
+      switch (u) {
+#define PP2_BAND_U(UU)                                                                         \
+  case UU:                                                                                     \
+    band<CH, NS, kSparse, UU>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc); \
+    break;
+        PP2_BAND_U(0) PP2_BAND_U(1) PP2_BAND_U(2) PP2_BAND_U(3) PP2_BAND_U(4)
+        PP2_BAND_U(5) PP2_BAND_U(6) PP2_BAND_U(7)
+        default:
+          band<CH, NS, kSparse, 8>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc);
+#undef PP2_BAND_U
+      }
+    } else {
+      band<CH, NS, SRC, 0>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc);
+    }
+  }
+  // one partial per (copy, wave); repeated copies of a partial chunk write
+  // identical values.  The max is of the unrounded values: round it here.
+  const int gw = bx * 4 + w;
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const float sm = wave_sum(acc[j][0]);
+    const float mx = (float)(_Float16)wave_max(acc[j][1]);
+    const float rw = wave_sum(acc[j][2]);
+    if (lane == 0) {
+      float* pp = a.partials + ((long long)cid[j] * a.nwaves + gw) * kRollStats;
+      pp[0] = sm;
+      pp[1] = mx;
+      pp[2] = rw;
+    }
+  }
+}
+
+int band_nseg(const Geom& g) { return (g.wp + kSegCells - 1) / kSegCells; }
+int band_nband(const Geom& g) { return (g.rows + kBandRows - 1) / kBandRows; }
+int band_gx(const Geom& g) { return (band_nseg(g) * band_nband(g) + 3) / 4; }
+
+// (copies per chunk, ring slots, waves per SIMD) variants of
+// k_rollout_band; PP2_ROLLOUT_VARIANT selects one for A/B runs
+struct BandVariant { int ch, ns, wps; };
+// (MI355X, 512^2 x 4096 copies x 5 steps: 6.01 / 6.21 / 6.25 / 6.36 / 6.20 ms)
+constexpr BandVariant kBandVariants[] = {{4, 4, 2}, {4, 3, 2}, {2, 4, 3}, {8, 3, 1}, {4, 4, 3}};
+int roll_variant() {
+  static const int v = [] {
+    const char* e = getenv("PP2_ROLLOUT_VARIANT");
+    const int i = e ? atoi(e) : 0;
+    return i >= 0 && i < (int)(sizeof(kBandVariants) / sizeof(kBandVariants[0])) ? i : 0;
+  }();
+  return v;
+}
+
+}  // namespace
+
+int rollout_chunk() { return kBandVariants[roll_variant()].ch; }
+int rollout_min_chunk() { return 2; }
+int rollout_step_waves(const Geom& g) { return band_gx(g) * 4; }
+
+hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
+                               PlaneSet R, const uint16_t* code, const float* tu_all,
+                               long long tstride, int tw, const float* dl, int es, int E,
+                               bool sparse, const void* bin, void* bout, long long cstride,
+                               int nchunks, const int* chunk_u, const int* chunk_first,
+                               const int* copies, const uint8_t* zs, const float* in_stats,
+                               float* partials, float* stats_out, int ncopies) {
+  const int gx = band_gx(g), nseg = band_nseg(g), nband = band_nband(g);
+  const int nw = gx * 4;
+  BandArgs a;
+  a.g = g;
+  a.T = T;
+  a.L = L;
+  a.R = R;
+  a.code = code ? code - g.wp : nullptr;  // row -1
+  a.bin = (const _Float16*)bin;            // copy planes start at row -1
+  a.bout = (_Float16*)bout;
+  a.cstride = cstride;
+  a.partials = partials;
+  a.nwaves = nw;
+  const long long nblocks = (long long)gx * nchunks;
+  if (nblocks <= 0) return hipSuccess;
+  const int CH = rollout_chunk();
+  const size_t lds = E > 0 ? (size_t)(((E * tw + 3) & ~3) + CH * E) * sizeof(float) : 0;
+#define PP2_BAND(CC, PP, WW)                                                                 \
+  do {                                                                                       \
+    static bool attr = false;                                                                \
+    if (!attr) {                                                                             \
+      for (const void* fn : {reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kSparse>), \
+                             reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kFull>),   \
+                             reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kDense>)}) \
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,           \
+                                  (int)kDictLdsMaxBytes);                                    \
+      (void)hipGetLastError();                                                               \
+      attr = true;                                                                           \
+    }                                                                                        \
+    if (src == kSparse)                                                                      \
+      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kSparse>), dim3((unsigned)nblocks),     \
+                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,     \
+                         nband, chunk_u, chunk_first, copies, zs, in_stats);                 \
+    else if (src == kFull)                                                                   \
+      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kFull>), dim3((unsigned)nblocks),       \
+                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,     \
+                         nband, chunk_u, chunk_first, copies, zs, in_stats);                 \
+    else                                                                                     \
+      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kDense>), dim3((unsigned)nblocks),      \
+                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,     \
+                         nband, chunk_u, chunk_first, copies, zs, in_stats);                 \
+  } while (0)
+  const int src = E <= 0 ? kDense : sparse ? kSparse : kFull;
+  switch (roll_variant()) {
+    case 1: PP2_BAND(4, 3, 2); break;
+    case 2: PP2_BAND(2, 4, 3); break;
+    case 3: PP2_BAND(8, 3, 1); break;
+    case 4: PP2_BAND(4, 4, 3); break;
+    default: PP2_BAND(4, 4, 2); break;
+  }
+#undef PP2_BAND
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_rollout_reduce(st, partials, nw, ncopies, stats_out);
+}
+
+}  // namespace pp2
