@@ -110,6 +110,13 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           every k and by 1 in between (beliefs equal to
  *                           rounding; values and actions unchanged) */
 #define PP2_TUNE_NORM_BLOCK 6
+/*  PP2_TUNE_STEP_PAIRS      1 (default): pp2_loop_run on an unsharded context
+ *                           with a sparse coded model runs two steps of a
+ *                           normalisation block per launch (the first over
+ *                           the tile plus a one-row halo, kept in LDS);
+ *                           0 = one launch per step.  Results are
+ *                           bit-identical either way. */
+#define PP2_TUNE_STEP_PAIRS 7
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
 /* ---------------------------------------------------------------- model

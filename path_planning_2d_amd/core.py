@@ -100,6 +100,7 @@ class GridContext:
     TUNE_HALO_DEPTH = 4
     TUNE_COMM_STREAM = 5
     TUNE_NORM_BLOCK = 6
+    TUNE_STEP_PAIRS = 7
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))

@@ -211,13 +211,6 @@ __device__ __forceinline__ void load_jn(const float* __restrict__ J_in, int wp, 
   }
 }
 
-__device__ __forceinline__ void store_ja(float* __restrict__ J_out, uint8_t* __restrict__ A,
-                                         long long off, const float (&best)[4],
-                                         const uint32_t (&arg)[4]) {
-  stv<4>(J_out + off, best);
-  *reinterpret_cast<uint32_t*>(A + off) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
-}
-
 // A lane's 3-row stencil window over its 4 cells: x0-1 .. x0+4 of rows
 // y-1, y, y+1 (one aligned 16-B load and two dword loads per row).  Values
 // outside the grid's x range are 0.
@@ -271,6 +264,23 @@ __device__ __forceinline__ void load_codes6(const uint16_t* __restrict__ code, i
   }
 }
 
+template <bool NT>
+__device__ __forceinline__ void store4(float* __restrict__ p, const float (&v)[4]) {
+  const f4a t = {v[0], v[1], v[2], v[3]};
+  if constexpr (NT) __builtin_nontemporal_store(t, reinterpret_cast<f4a*>(p));
+  else *reinterpret_cast<f4a*>(p) = t;
+}
+
+template <bool NT>
+__device__ __forceinline__ void store_ja(float* __restrict__ J_out, uint8_t* __restrict__ A,
+                                         long long off, const float (&best)[4],
+                                         const uint32_t (&arg)[4]) {
+  store4<NT>(J_out + off, best);
+  const uint32_t a4 = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+  if constexpr (NT) __builtin_nontemporal_store(a4, reinterpret_cast<uint32_t*>(A + off));
+  else *reinterpret_cast<uint32_t*>(A + off) = a4;
+}
+
 // Support slot of T[.][u][i] in the sparse layout, or -1 (T == 0 there).
 __host__ __device__ constexpr int sup_slot(int u, int i) {
   for (int j = 0; j < kSupN[u]; ++j)
@@ -283,14 +293,15 @@ __host__ __device__ constexpr int sup_slot(int u, int i) {
 // terms are gathered -- the others are fmaf(+0, b, p) == p (b >= 0, p never
 // -0) -- in the same ascending-s order.
 template <bool SPARSE, int U = -1>
-__device__ __forceinline__ void belief_cells(const Geom& g, const float* sTu, const float* sL,
-                                             const int (&slot)[9], float inv,
-                                             const CodeWin6& cw, const Win6& win, int y, int x0,
-                                             float* __restrict__ b_out, float& local) {
+__device__ __forceinline__ void belief_vals(const Geom& g, const float* sTu, const float* sL,
+                                            const int (&slot)[9], float inv,
+                                            const CodeWin6& cw, const Win6& win, int x0,
+                                            float (&p)[4], float& local) {
   using LY = Layout<SPARSE>;
   const bool lx = x0 == 0, rx = x0 + 4 == g.wp;
   // p = L_z * sum_s T[x+off_s][u][8-s] b(x+off_s), in s order
-  float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) p[k] = 0.0f;
 #pragma unroll
   for (int s = 0; s < 9; ++s) {
     const int oy = s / 3, ox = s % 3 - 1;
@@ -312,10 +323,19 @@ __device__ __forceinline__ void belief_cells(const Geom& g, const float* sTu, co
     p[k] = p[k] * inv;
     local += p[k];
   }
-  stv<4>(b_out + (long long)y * g.wp + x0, p);
 }
 
-template <bool SPARSE>
+template <bool SPARSE, int U = -1, bool NT = false>
+__device__ __forceinline__ void belief_cells(const Geom& g, const float* sTu, const float* sL,
+                                             const int (&slot)[9], float inv,
+                                             const CodeWin6& cw, const Win6& win, int y, int x0,
+                                             float* __restrict__ b_out, float& local) {
+  float p[4];
+  belief_vals<SPARSE, U>(g, sTu, sL, slot, inv, cw, win, x0, p, local);
+  store4<NT>(b_out + (long long)y * g.wp + x0, p);
+}
+
+template <bool SPARSE, bool NT = false>
 __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, float gamma,
                                             uint32_t m0, uint32_t m1, const Win6& win, int y,
                                             int x0, bool own, float* __restrict__ J_out,
@@ -330,9 +350,35 @@ __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, flo
   uint32_t arg[4];
   coded_sweep4<SPARSE>(sTC, cc, jn, gamma, best, arg);
   const long long off = (long long)y * g.wp + x0;
-  stv<4>(J_out + off, best);
-  if (own)
-    *reinterpret_cast<uint32_t*>(A + off) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+  if (own) {
+    store_ja<NT>(J_out, A, off, best, arg);
+  } else {
+    store4<NT>(J_out + off, best);
+  }
+}
+
+// J window of a lane from the workgroup's LDS copy of its tile's value rows
+// (sJ holds the plane from flat cell jb on, see k_loop_step_coded).
+__device__ __forceinline__ void lds_win6(const float* sJ, int wp, int y, int x0, long long jb,
+                                         bool le, bool re, Win6& w) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const float* p = sJ + ((long long)(y + r - 1) * wp + x0 - jb);
+    const f4a m = *reinterpret_cast<const f4a*>(p);
+    const float l = p[-1], rt = p[4];
+    w.v[r][0] = le ? 0.0f : l;
+    w.v[r][1] = m[0];
+    w.v[r][2] = m[1];
+    w.v[r][3] = m[2];
+    w.v[r][4] = m[3];
+    w.v[r][5] = re ? 0.0f : rt;
+  }
+}
+
+// Floats of the value rows one tile's sweep reads: its cells, one row and a
+// 16-B chunk on each side, rounded to whole 1-KiB DMA instructions.
+__host__ __device__ constexpr int jwin_floats(int tile_cells, int wp) {
+  return lds_span(tile_cells + 2 * wp + 8);
 }
 
 // Fused north-star step on the coded model (k_loop_step's semantics).  A
@@ -345,7 +391,10 @@ __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, flo
 // would not fit beside the belief's); no barrier follows the stores.
 //   rows: dictionary rows in the LDS layout (E x Layout::row floats)
 //   lz:   L_z column of the dictionary (E floats)
-template <bool SPARSE, int QPB, int MINB, int U = -1>
+// JPF: the first tile's value rows (jwin_floats) are DMA-staged into LDS with
+// the dictionary, so the sweep's J window is an LDS read instead of an HBM
+// round trip after the belief update.  NT: non-temporal b', J', A stores.
+template <bool SPARSE, int QPB, int MINB, int U = -1, bool JPF = false, bool NT = false>
 __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
     const float* __restrict__ lz, const float* __restrict__ tu, int E,
@@ -359,6 +408,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   float* sTC = lds;
   float* sL = lds + lds_span(E * LY::row);
   float* sTu = sL + lds_span(E);
+  float* sJ = sTu + lds_span(E * LY::tu);
   PP2_PHASE(0);
   const int q = threadIdx.x / kQuarter, tq = threadIdx.x % kQuarter;
   const int tpr = g.wp / 4;
@@ -379,6 +429,21 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   stage_rows(rows, E * LY::row, sTC);
   stage_rows(lz, E, sL);
   stage_rows(tu, E * LY::tu, sTu);
+  long long jb = 0;  // flat cell of sJ[0]
+  if constexpr (JPF) {
+    constexpr int kTileCells = QPB * kQuarter * 4;
+    jb = (long long)(tile0 < ntiles ? tile0 : 0) * kTileCells - g.wp - 4;
+    // 16-B chunks past the halo row below re-read its last chunk (their LDS
+    // words belong to lanes without a cell)
+    const long long hi = (long long)(g.rows + 1) * g.wp - 4;
+    const int n4 = jwin_floats(kTileCells, g.wp) >> 2;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int c = wave; c * 64 < n4; c += nw) {
+      long long f = jb + 4LL * (c * 64 + lane);
+      if (f > hi) f = hi;
+      __builtin_amdgcn_global_load_lds((glb_void*)(J_in + f), (lds_void*)(sJ + c * 256), 16, 0, 0);
+    }
+  }
   float S = 1.0f;
   if (in_partials) S = wave_reduce_partials(in_partials, in_n);
   else if (in_sum) S = *in_sum;
@@ -406,13 +471,14 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     // kernel); unconditional compute with a guarded store spills heavily
     float local = 0.0f;
     if (ok) {
-      belief_cells<SPARSE, U>(g, sTu, sL, slot, inv, cw, bw, y, x0, b_out, local);
+      belief_cells<SPARSE, U, NT>(g, sTu, sL, slot, inv, cw, bw, y, x0, b_out, local);
       const bool own = y >= own0 && y < own1;
       if (!own) local = 0.0f;
       PP2_PHASE(2);
       Win6 jw;
-      load_win6(J_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, jw);
-      sweep_cells<SPARSE>(g, sTC, gamma, cw.m0[1], cw.m1[1], jw, y, x0, own, J_out, A);
+      if constexpr (JPF) lds_win6(sJ, g.wp, y, x0, jb, x0 == 0, x0 + 4 == g.wp, jw);
+      else load_win6(J_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, jw);
+      sweep_cells<SPARSE, NT>(g, sTC, gamma, cw.m0[1], cw.m1[1], jw, y, x0, own, J_out, A);
       PP2_PHASE(3);
     }
     const int d = QPB * tile0 + q;
@@ -427,11 +493,11 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       Win6 w2;
       load_codes6(code, g.wp, yy, xx, c2);
       load_win6(b_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
-      belief_cells<SPARSE, U>(g, sTu, sL, slot, inv, c2, w2, yy, xx, b_out, local);
+      belief_cells<SPARSE, U, NT>(g, sTu, sL, slot, inv, c2, w2, yy, xx, b_out, local);
       const bool own = yy >= own0 && yy < own1;
       if (!own) local = 0.0f;
       load_win6(J_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
-      sweep_cells<SPARSE>(g, sTC, gamma, c2.m0[1], c2.m1[1], w2, yy, xx, own, J_out, A);
+      sweep_cells<SPARSE, NT>(g, sTC, gamma, c2.m0[1], c2.m1[1], w2, yy, xx, own, J_out, A);
     }
     const int d = QPB * tl + q;
     if (d < dense_blocks) write_wave_partial(local, out_partials, d);
@@ -440,7 +506,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   PP2_PHASE(4);
 }
 
-template <bool SPARSE, int QPB, int MINB>
+template <bool SPARSE, int QPB, int MINB, bool NTS>
 __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
     Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
     int E, const float* __restrict__ J_in, float* __restrict__ J_out,
@@ -468,7 +534,144 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
     float best[4];
     uint32_t arg[4];
     coded_sweep4<SPARSE>(lds, cc, jn, gamma, best, arg);
-    store_ja(J_out, A, off, best, arg);
+    store_ja<NTS>(J_out, A, off, best, arg);
+  }
+}
+
+
+// ---------------------------------------------------------------- step pairs
+// Two fused loop steps of one normalisation block in ONE launch, with no
+// communication between workgroups: a workgroup owns a 4096-cell tile (the
+// dense kernel's 4 blocks).  Step 1 is computed over the tile plus one row
+// and a quad on each side (tile + 2 wp + 8 cells) from HBM, into LDS; step 2
+// reads its b and J windows from LDS and writes the tile.  Each launch saves
+// one launch, one dictionary staging and one dependent HBM round trip per
+// two steps for 2 wp + 8 recomputed cells per tile (1.5x step-1 work at
+// 1024^2).  Step-1 cells outside rows [0, rows) are the zero halo.  Per cell
+// the arithmetic is k_loop_step_coded's; the intermediate belief, values and
+// actions are not stored (nobody reads them), the mass partials and actions
+// are step 2's, in the dense kernel's cell -> (block, wave) mapping.
+constexpr int kPQ = 4;                      // 256-thread quarters per workgroup
+constexpr int kPTile = kPQ * kQuarter * 4;  // cells per tile
+__host__ __device__ constexpr int pair_region(int wp) { return kPTile + 2 * wp + 8; }
+
+// J or b window of a lane from an LDS region holding the plane from flat cell
+// r0 on.
+__device__ __forceinline__ void region_win6(const float* sR, int wp, int y, int x0, long long r0,
+                                            bool le, bool re, Win6& w) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const float* p = sR + ((long long)(y + r - 1) * wp + x0 - r0);
+    const f4a m = *reinterpret_cast<const f4a*>(p);
+    const float l = p[-1], rt = p[4];
+    w.v[r][0] = le ? 0.0f : l;
+    w.v[r][1] = m[0];
+    w.v[r][2] = m[1];
+    w.v[r][3] = m[2];
+    w.v[r][4] = m[3];
+    w.v[r][5] = re ? 0.0f : rt;
+  }
+}
+
+__device__ __forceinline__ void belief_u(int u, const Geom& g, const float* sTu, const float* sL,
+                                         float inv, const CodeWin6& cw, const Win6& w, int x0,
+                                         float (&p)[4], float& local) {
+  const int slot[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // unused (U >= 0)
+  switch (u) {
+#define PP2_BV(UU) \
+  case UU: belief_vals<true, UU>(g, sTu, sL, slot, inv, cw, w, x0, p, local); break;
+    PP2_BV(0) PP2_BV(1) PP2_BV(2) PP2_BV(3) PP2_BV(4) PP2_BV(5) PP2_BV(6) PP2_BV(7)
+    default: belief_vals<true, 8>(g, sTu, sL, slot, inv, cw, w, x0, p, local);
+#undef PP2_BV
+  }
+}
+
+__device__ __forceinline__ void sweep_vals(const float* sTC, float gamma, const CodeWin6& cw,
+                                           const Win6& w, float (&best)[4], uint32_t (&arg)[4]) {
+  float jn[9][4];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) jn[i][k] = w.v[i / 3][k + i % 3];
+  const uint32_t cc[4] = {cw.m0[1] & 0xffffu, cw.m0[1] >> 16, cw.m1[1] & 0xffffu, cw.m1[1] >> 16};
+  coded_sweep4<true>(sTC, cc, jn, gamma, best, arg);
+}
+
+__global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
+    Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
+    const float* __restrict__ lz1, const float* __restrict__ lz2, const float* __restrict__ tu1,
+    const float* __restrict__ tu2, int E, int u1, int u2, const float* __restrict__ b_in,
+    float* __restrict__ b_out, const float* __restrict__ J_in, float* __restrict__ J_out,
+    uint8_t* __restrict__ A, float* __restrict__ out_partials, const float* __restrict__ in_sum,
+    float scale0, int dense_blocks) {
+  using LY = Layout<true>;
+  extern __shared__ float lds[];
+  const int nreg = pair_region(g.wp);
+  float* sTC = lds;
+  float* sL1 = sTC + lds_span(E * LY::row);
+  float* sL2 = sL1 + lds_span(E);
+  float* sT1 = sL2 + lds_span(E);
+  float* sT2 = sT1 + lds_span(E * LY::tu);
+  float* sB = sT2 + lds_span(E * LY::tu);  // step-1 belief over the region
+  float* sJ = sB + lds_span(nreg);         // step-1 values over the region
+  const int q = threadIdx.x / kQuarter;
+  const int ntiles = (dense_blocks + kPQ - 1) / kPQ;
+  stage_rows(rows, E * LY::row, sTC);
+  stage_rows(lz1, E, sL1);
+  stage_rows(lz2, E, sL2);
+  stage_rows(tu1, E * LY::tu, sT1);
+  stage_rows(tu2, E * LY::tu, sT2);
+  const float inv0 = in_sum ? (1.0f / *in_sum) * scale0 : scale0;
+  __syncthreads();
+  for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
+    const long long c0 = (long long)tile * kPTile;
+    const long long r0 = c0 - g.wp - 4;  // flat cell of sB[0] / sJ[0] (a quad boundary)
+    // ---- step 1 over the region: quads of 4 cells, rows outside [0, rows) are 0
+    for (int qd = threadIdx.x; 4 * qd < nreg; qd += kPQ * kQuarter) {
+      const long long f = r0 + 4LL * qd;
+      const int y = (int)((f + 2LL * g.wp) / g.wp) - 2;
+      const int x0 = (int)(f - (long long)y * g.wp);
+      float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, best[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (y >= 0 && y < g.rows) {
+        const bool le = x0 == 0, re = x0 + 4 == g.wp;
+        CodeWin6 cw;
+        Win6 w;
+        load_codes6(code, g.wp, y, x0, cw);
+        load_win6(b_in, g.wp, y, x0, le, re, w);
+        float local;
+        belief_u(u1, g, sT1, sL1, inv0, cw, w, x0, p, local);
+        load_win6(J_in, g.wp, y, x0, le, re, w);
+        uint32_t arg[4];
+        sweep_vals(sTC, gamma, cw, w, best, arg);
+      }
+      *reinterpret_cast<f4a*>(sB + 4 * qd) = f4a{p[0], p[1], p[2], p[3]};
+      *reinterpret_cast<f4a*>(sJ + 4 * qd) = f4a{best[0], best[1], best[2], best[3]};
+    }
+    __syncthreads();
+    // ---- step 2 over the tile (k_loop_step_coded's lane -> cell mapping)
+    const long long t_ = (long long)(kPQ * tile) * kQuarter + threadIdx.x;
+    const int y = (int)(t_ / (g.wp / 4));
+    const int x0 = (int)(t_ % (g.wp / 4)) * 4;
+    float local = 0.0f;
+    if (y < g.rows) {
+      const bool le = x0 == 0, re = x0 + 4 == g.wp;
+      CodeWin6 cw;
+      Win6 w;
+      load_codes6(code, g.wp, y, x0, cw);
+      region_win6(sB, g.wp, y, x0, r0, le, re, w);
+      float p[4];
+      belief_u(u2, g, sT2, sL2, 1.0f, cw, w, x0, p, local);
+      const long long off = (long long)y * g.wp + x0;
+      store4<true>(b_out + off, p);
+      region_win6(sJ, g.wp, y, x0, r0, le, re, w);
+      float best[4];
+      uint32_t arg[4];
+      sweep_vals(sTC, gamma, cw, w, best, arg);
+      store_ja<true>(J_out, A, off, best, arg);
+    }
+    const int d = kPQ * tile + q;
+    if (d < dense_blocks) write_wave_partial(local, out_partials, d);
+    __syncthreads();  // the region is rewritten by the next tile
   }
 }
 
@@ -493,6 +696,24 @@ void allow_lds(const void* fn, bool& done) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDictLdsMaxBytes);
   (void)hipGetLastError();
   done = true;
+}
+
+// Loop-kernel variant bits (A/B runs; PP2_LOOP_VARIANT, default 2): 1 =
+// value-row prefetch into LDS, 2 = non-temporal stores, 4 = one 1024-thread workgroup
+// per CU (non-temporal stores, no prefetch), 8 = non-temporal stores in the
+// MDP sweep kernel.  MI355X, 1024^2
+// loop step (two interleaved runs): 0: 9.90 / 9.75 us, 1: 10.57 / 10.44,
+// 2: 9.25 / 9.34, 3: 9.95 / 10.09; later 0: 9.94 / 9.99, 2: 9.45 / 9.53,
+// 6: 9.51 / 9.46 (2048^2: 27.4-28.2 for all three).  The prefetch makes every workgroup's
+// barrier wait for an HBM round trip that the register path overlaps with
+// the belief update; non-temporal stores skip the L2 write-back at the end
+// of the launch.
+int loop_variant() {
+  static const int v = [] {
+    const char* e = getenv("PP2_LOOP_VARIANT");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -536,39 +757,89 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   const float* in_partials, int in_n, const float* in_sum,
                                   float* in_sum_out, float* out_partials, const float* J_in,
                                   float* J_out, uint8_t* A, int own0, int own1, float scale) {
-  const size_t lds = coded_loop_lds_bytes(E, sparse);
+  const size_t lds0 = coded_loop_lds_bytes(E, sparse);
   const int dense_blocks = cells_grid(g, 4);
-#define PP2_LOOPC(SP, Q, MB, UU)                                                                \
+  // value-row prefetch when both workgroups' LDS still fit a CU (sparse rows)
+  const size_t jlds = (size_t)jwin_floats(2 * kQuarter * 4, g.wp) * sizeof(float);  // QPB 2
+  const int var = loop_variant();
+  const bool jpf = sparse && (var & 5) == 1 && (lds0 + jlds) * 2 <= kDictLdsMaxBytes;
+  const bool nt = (var & 2) != 0;
+  const size_t lds = lds0 + (jpf ? jlds : 0);
+#define PP2_LOOPC(SP, Q, MB, UU, JP, N)                                                          \
   do {                                                                                          \
     if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                               \
     static bool attr = false;                                                                   \
-    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB, UU>), attr);          \
+    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB, UU, JP, N>), attr);   \
     const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                                \
-    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB, UU>), dim3(grid), dim3(Q * kQuarter), lds, \
-                       st,                                                                      \
+    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB, UU, JP, N>), dim3(grid), dim3(Q * kQuarter), \
+                       lds, st,                                                                 \
                        g, gamma, code, rows, lz, tu, E, b_in, b_out, u, in_partials, in_n,      \
                        in_sum, in_sum_out, out_partials, dense_blocks, J_in, J_out, A, own0,    \
                        own1, scale);                                                            \
   } while (0)
-  // sparse rows: two 512-thread workgroups per CU (~60 KB LDS each, <= 128
-  // VGPRs, 4 waves per SIMD); full rows: one 1024-thread workgroup per CU
-  // sparse rows: one kernel per action (its support terms only)
+#define PP2_LOOPV(UU)                                                  \
+  do {                                                                 \
+    if (var & 4) PP2_LOOPC(true, 4, 1, UU, false, true);               \
+    else if (jpf && nt) PP2_LOOPC(true, 2, 2, UU, true, true);         \
+    else if (jpf) PP2_LOOPC(true, 2, 2, UU, true, false);              \
+    else if (nt) PP2_LOOPC(true, 2, 2, UU, false, true);               \
+    else PP2_LOOPC(true, 2, 2, UU, false, false);                      \
+  } while (0)
+  // sparse rows: two 512-thread workgroups per CU (~60-76 KB LDS each, <= 128
+  // VGPRs, 4 waves per SIMD), one kernel per action (its support terms
+  // only); full rows: one 1024-thread workgroup per CU
   if (sparse) {
     switch (u) {
-      case 0: PP2_LOOPC(true, 2, 2, 0); break;
-      case 1: PP2_LOOPC(true, 2, 2, 1); break;
-      case 2: PP2_LOOPC(true, 2, 2, 2); break;
-      case 3: PP2_LOOPC(true, 2, 2, 3); break;
-      case 4: PP2_LOOPC(true, 2, 2, 4); break;
-      case 5: PP2_LOOPC(true, 2, 2, 5); break;
-      case 6: PP2_LOOPC(true, 2, 2, 6); break;
-      case 7: PP2_LOOPC(true, 2, 2, 7); break;
-      default: PP2_LOOPC(true, 2, 2, 8); break;
+      case 0: PP2_LOOPV(0); break;
+      case 1: PP2_LOOPV(1); break;
+      case 2: PP2_LOOPV(2); break;
+      case 3: PP2_LOOPV(3); break;
+      case 4: PP2_LOOPV(4); break;
+      case 5: PP2_LOOPV(5); break;
+      case 6: PP2_LOOPV(6); break;
+      case 7: PP2_LOOPV(7); break;
+      default: PP2_LOOPV(8); break;
     }
   } else {
-    PP2_LOOPC(false, 4, 1, -1);
+    PP2_LOOPC(false, 4, 1, -1, false, false);
   }
+#undef PP2_LOOPV
 #undef PP2_LOOPC
+  return hipGetLastError();
+}
+
+size_t loop_pair_lds_bytes(int E, int wp) {
+  return ((size_t)lds_span(E * kSpRow) + 2 * lds_span(E) + 2 * lds_span(E * tu_width(true)) +
+          2 * lds_span(pair_region(wp))) * sizeof(float);
+}
+
+bool loop_pair_fits(const Geom& g, int E, bool sparse) {
+  // Sparse rows, LDS for one 1024-thread workgroup, at most 1.6x recomputed
+  // step-1 cells, and a tile for every CU: on fewer tiles the per-step
+  // kernel's 2048-cell workgroups keep more CUs busy (MI355X, 512^2: 6.1
+  // us/step per-step vs 7.4 paired; 1024^2: 9.45 vs 9.0).
+  (void)coded_grid(1, 1);  // sets g_num_cus
+  return sparse && E > 0 && loop_pair_lds_bytes(E, g.wp) <= kDictLdsMaxBytes &&
+         5 * (2 * g.wp + 8) <= 3 * kPTile &&
+         (cells_grid(g, 4) + kPQ - 1) / kPQ >= g_num_cus;
+}
+
+hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
+                                  const uint16_t* code, const float* rows, const float* lz1,
+                                  const float* lz2, const float* tu1, const float* tu2, int E,
+                                  int u1, int u2, const float* b_in, float* b_out,
+                                  const float* J_in, float* J_out, uint8_t* A,
+                                  float* out_partials, const float* in_sum, float scale) {
+  if (!loop_pair_fits(g, E, true) || u1 < 0 || u1 > 8 || u2 < 0 || u2 > 8)
+    return hipErrorInvalidValue;
+  const size_t lds = loop_pair_lds_bytes(E, g.wp);
+  static bool attr = false;
+  allow_lds(reinterpret_cast<const void*>(&k_loop_pair_coded), attr);
+  const int dense_blocks = cells_grid(g, 4);
+  const int grid = coded_grid((dense_blocks + kPQ - 1) / kPQ, 1);
+  hipLaunchKernelGGL(k_loop_pair_coded, dim3(grid), dim3(kPQ * kQuarter), lds, st, g, gamma,
+                     code, rows, lz1, lz2, tu1, tu2, E, u1, u2, b_in, b_out, J_in, J_out, A,
+                     out_partials, in_sum, scale, dense_blocks);
   return hipGetLastError();
 }
 
@@ -577,18 +848,24 @@ hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const float* J_in, float* J_out, uint8_t* A) {
   const size_t lds = (size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) * sizeof(float);
   const long long nthreads = (long long)g.rows * (g.wp / 4);
-#define PP2_SWEEPC(SP, Q, MB)                                                                  \
+#define PP2_SWEEPC(SP, Q, MB, N)                                                               \
   do {                                                                                         \
     if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                              \
     static bool attr = false;                                                                  \
-    allow_lds(reinterpret_cast<const void*>(&k_mdp_sweep_coded<SP, Q, MB>), attr);             \
+    allow_lds(reinterpret_cast<const void*>(&k_mdp_sweep_coded<SP, Q, MB, N>), attr);          \
     const int nt = Q * kQuarter;                                                               \
     const int grid = coded_grid((int)((nthreads + nt - 1) / nt), MB);                          \
-    hipLaunchKernelGGL((k_mdp_sweep_coded<SP, Q, MB>), dim3(grid), dim3(nt), lds, st, g, gamma, \
-                       code, rows, E, J_in, J_out, A);                                         \
+    hipLaunchKernelGGL((k_mdp_sweep_coded<SP, Q, MB, N>), dim3(grid), dim3(nt), lds, st, g,     \
+                       gamma, code, rows, E, J_in, J_out, A);                                  \
   } while (0)
-  if (sparse) PP2_SWEEPC(true, 4, 2);
-  else PP2_SWEEPC(false, 4, 1);
+  const bool ntst = (loop_variant() & 8) != 0;  // measured slower (8.8 -> 9.9 us at 1024^2)
+  if (sparse) {
+    if (ntst) PP2_SWEEPC(true, 4, 2, true);
+    else PP2_SWEEPC(true, 4, 2, false);
+  } else {
+    if (ntst) PP2_SWEEPC(false, 4, 1, true);
+    else PP2_SWEEPC(false, 4, 1, false);
+  }
 #undef PP2_SWEEPC
   return hipGetLastError();
 }
@@ -600,4 +877,5 @@ extern "C" int pp2_debug_phase_trace(unsigned long long* out, int nblocks) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(pp2::g_phase),
                              sizeof(unsigned long long) * 8 * nblocks) == hipSuccess ? 0 : 2;
 }
+
 #endif

@@ -40,7 +40,7 @@ int set_err(int code, const char* fmt, ...);
     if (s_ != PP2_OK) return s_;    \
   } while (0)
 
-constexpr int kGuard = 64;  // floats of guard before/after each plane set
+constexpr int kGuard = pp2::kPlaneGuard;  // floats of guard before/after each plane set
 constexpr int kShardHalo = 8;  // halo rows allocated per side in row-sharded contexts
 // Loop normalisation blocks (row shards, and PP2_TUNE_NORM_BLOCK > 1) start
 // by dividing the belief by its exact (global) mass and multiplying by 2^96
@@ -112,6 +112,10 @@ struct pp2_ctx {
   int kdepth_max = 1;      // min(g.halo, the smallest shard's rows)
   int kstep = 0;           // loop step within the current halo / normalisation block
   int norm_block = 8;      // unsharded loop: steps per exact normalisation (PP2_TUNE_NORM_BLOCK)
+
+  // pp2_loop_run on an unsharded sparse-coded context fuses the steps of a
+  // normalisation block in pairs (pp2::launch_loop_pair_coded)
+  int step_pairs = 1;              // PP2_TUNE_STEP_PAIRS
 
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;

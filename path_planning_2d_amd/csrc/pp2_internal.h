@@ -167,6 +167,19 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   const float* in_sum, float* in_sum_out, float* out_partials,
                                   const float* J_in, float* J_out, uint8_t* A, int own0,
                                   int own1, float scale = 1.0f);
+// Two fused loop steps in one launch (pp2_coded.hip, sparse rows,
+// unsharded): step 1 (u1, L_z1 column lz1, T_u1 table tu1) divides by
+// *in_sum (if given) times scale, step 2 (u2, lz2, tu2) by 1.  Reads b_in /
+// J_in, writes b_out / J_out / A and step 2's mass partials.  Returns
+// hipErrorInvalidValue when loop_pair_fits is false.
+constexpr int kPlaneGuard = 64;  // floats of guard before/after every plane allocation
+bool loop_pair_fits(const Geom& g, int entries, bool sparse);
+hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
+                                  const uint16_t* code, const float* rows, const float* lz1,
+                                  const float* lz2, const float* tu1, const float* tu2,
+                                  int entries, int u1, int u2, const float* b_in, float* b_out,
+                                  const float* J_in, float* J_out, uint8_t* A,
+                                  float* out_partials, const float* in_sum, float scale);
 hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int entries,
                                   bool sparse, const float* J_in, float* J_out, uint8_t* A);

@@ -601,6 +601,40 @@ static int blocked_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   return PP2_OK;
 }
 
+// Two steps of the current normalisation block in one launch
+// (k_loop_pair_coded): the same state transitions as two blocked_loop_step
+// calls.  Applies to an unsharded context with a sparse coded model when the
+// block has two steps left.
+static bool can_pair(pp2_ctx* c) {
+  return c->step_pairs && !c->group && !c->comm && c->norm_block >= 2 &&
+         c->kstep + 2 <= c->norm_block && coded_active(c) && c->dict_sparse &&
+         pp2::loop_pair_fits(c->g, c->dict_n, true);
+}
+
+static int loop_pair(pp2_ctx* c, uint8_t u1, uint8_t z1, uint8_t u2, uint8_t z2) {
+  for (int i = 0; i < 2; ++i) {
+    const uint8_t u = i ? u2 : u1, z = i ? z2 : z1;
+    if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  }
+  const int bc = c->bcur, bn = bc ^ 1, jc = c->jcur;
+  const bool start = c->kstep == 0;
+  if (start) CHECK(ensure_mass(c));
+  const size_t es = (size_t)((c->dict_n + 3) & ~3);
+  const size_t ts = ((size_t)c->dict_n * pp2::tu_width(true) + 3) & ~(size_t)3;
+  HIPCHK(pp2::launch_loop_pair_coded(
+      c->stream, c->g, c->gamma, c->d_code, c->d_rows, c->d_dl + z1 * es, c->d_dl + z2 * es,
+      c->d_tu + u1 * ts, c->d_tu + u2 * ts, c->dict_n, u1, u2, c->b[bc].v.p, c->b[bn].v.p,
+      c->J[jc].v.p, c->J[jc ^ 1].v.p, c->A, c->pbuf[bn], start ? c->bsum + bc : nullptr,
+      start ? kBlockScale : 1.0f));
+  c->pending[bc] = false;
+  c->pcount[bn] = pp2::mass_partials(c->g, 4);
+  c->pending[bn] = true;
+  c->bcur = bn;
+  c->jcur = jc ^ 1;
+  c->kstep = (c->kstep + 2) % c->norm_block;
+  return PP2_OK;
+}
+
 // =========================================================================== C ABI
 extern "C" {
 
@@ -700,6 +734,7 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
     case PP2_TUNE_CODED_MODEL: c->use_coded = value != 0; return PP2_OK;
+    case PP2_TUNE_STEP_PAIRS: c->step_pairs = value != 0; return PP2_OK;
     case PP2_TUNE_NORM_BLOCK:
       if (value < 1 || value > kMaxNormBlock)
         return set_err(PP2_EINVAL, "normalisation block %d not in [1, %d]", value, kMaxNormBlock);
@@ -911,7 +946,16 @@ int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
 int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
   CHECK(check_model(c));
   if (n < 0 || (n > 0 && (!us || !zs))) return set_err(PP2_EINVAL, "bad trajectory");
-  for (int i = 0; i < n; ++i) CHECK(pp2_loop_step(c, us[i], zs[i]));
+  DeviceGuard dg(c->device);
+  for (int i = 0; i < n;) {
+    if (i + 1 < n && can_pair(c)) {
+      CHECK(loop_pair(c, us[i], zs[i], us[i + 1], zs[i + 1]));
+      i += 2;
+    } else {
+      CHECK(pp2_loop_step(c, us[i], zs[i]));
+      ++i;
+    }
+  }
   return PP2_OK;
 }
 

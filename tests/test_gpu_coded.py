@@ -227,3 +227,41 @@ def test_off_support_model_uses_full_rows(pp2):
         a.mdp_sweep(9)
         b.mdp_sweep(9)
         np.testing.assert_array_equal(a.mdp_get()[0], b.mdp_get()[0])
+
+
+@pytest.mark.parametrize("block", [8, 5, 3])
+@pytest.mark.parametrize("H,W", [(1024, 1024), (1000, 1100)])
+def test_step_pairs_equal_single_steps(pp2, H, W, block):
+    """pp2_loop_run fuses two steps of a normalisation block per launch
+    (k_loop_pair_coded: step 1 over the tile plus a one-row halo in LDS) on
+    grids with a 4096-cell tile per CU.  Raw beliefs, masses, values and
+    actions equal the one-launch-per-step path bit for bit, across odd chunk
+    lengths and block boundaries."""
+    from path_planning_2d_amd import synthetic as S
+    wp = (W + 3) // 4 * 4
+    assert 5 * (2 * wp + 8) <= 3 * 4096 and (-(-H * wp // 1024) + 3) // 4 >= 256
+    grid = S.synth_grid(H, W, H + W)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 13, seed=3)
+    b0 = S.uniform_belief(grid)
+    a = pp2.GridContext(grid, goal, gamma=float(GAMMA))
+    b = pp2.GridContext(grid, goal, gamma=float(GAMMA))
+    with a, b:
+        b.set_tuning(b.TUNE_STEP_PAIRS, 0)
+        for c in (a, b):
+            c.model_generate()
+            assert c.model_dict_info()[1]
+            c.set_tuning(c.TUNE_NORM_BLOCK, block)
+            c.belief_set(b0)
+            c.mdp_reset()
+        for lo, hi in ((0, 3), (3, 4), (4, 13)):
+            a.loop_run(us[lo:hi], zs[lo:hi])
+            b.loop_run(us[lo:hi], zs[lo:hi])
+            ra, ma = a.belief_get_raw()
+            rb, mb = b.belief_get_raw()
+            np.testing.assert_array_equal(ra, rb, err_msg=f"raw belief after {hi} steps")
+            assert np.float32(ma) == np.float32(mb), (hi, ma, mb)
+            Ja, Aa = a.mdp_get()
+            Jb, Ab = b.mdp_get()
+            np.testing.assert_array_equal(Ja, Jb, err_msg=f"J after {hi} steps")
+            np.testing.assert_array_equal(Aa, Ab, err_msg=f"A after {hi} steps")

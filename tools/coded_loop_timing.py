@@ -17,6 +17,7 @@ def main():
     stream = torch.cuda.Stream()
     with P.GridContext(grid, goal, gamma=0.95) as ctx:
         ctx.set_stream(stream.cuda_stream)
+        ctx.set_tuning(ctx.TUNE_STEP_PAIRS, int(os.environ.get("PP2_PAIRS", "1")))
         ctx.model_generate()
         ctx.belief_set(S.uniform_belief(grid))
         ctx.mdp_reset()

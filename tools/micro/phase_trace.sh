@@ -7,7 +7,5 @@ HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$(cd "$HERE/../.." && pwd)
 CS=$ROOT/path_planning_2d_amd/csrc
 mkdir -p "$HERE/_trace"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fgpu-flush-denormals-to-zero \
-  -ffp-contract=off -DPP2_PHASE_TRACE -I"$ROOT/include" -I"$CS" -shared \
-  -o "$HERE/_trace/libpp2_trace.so" "$CS/pp2_kernels.hip" "$CS/pp2_coded.hip" \
-  "$CS/pp2_runtime.cpp" "$CS/pp2_tree.cpp" "$CS/pp2_shards.cpp" "$CS/pp2_rollout.cpp" -lrccl
+make -C "$CS" -j8 OUT="$HERE/_trace/libpp2_trace.so" OBJDIR="$HERE/_trace/obj" \
+  EXTRA_FLAGS=-DPP2_PHASE_TRACE "$HERE/_trace/libpp2_trace.so"
