@@ -20,11 +20,13 @@ kernel of a step, timed live with HIP events around the timed steps on the
 stream it runs on, with SURVEY.md §8(d)'s algorithmic bytes: 417 per cell
 (belief: T_u 36 + L_z 4 + b 4 + b' 4; sweep: T 324 + C 36 + J 4 + J' 4 +
 A 1, the reference's fp32 tensor contract).
-  * k_loop_step_coded (default; the model is dictionary-coded, see
-    DESIGN.md §2.1) moves only 19 B per cell (code 2, b 4, b' 4, J 4, J' 4,
-    A 1; `traffic`, `roofline_moved`), so its frac on the contract exceeds 1;
-    its binding resources are the per-launch latency chain and LDS (196 B of
-    dictionary reads per cell, `roofline_lds`);
+  * k_loop_pair_coded (default at 1024^2: two steps per launch, the first
+    over the tile plus a one-row halo kept in LDS) and k_loop_step_coded (one
+    step per launch; the model is dictionary-coded) move
+    only 19 B per cell and launch (code 2, b 4, b' 4, J 4, J' 4, A 1;
+    `traffic`, `roofline_moved`), so their frac on the contract exceeds 1;
+    the binding resources are the per-launch latency chain and LDS (196 B
+    of dictionary reads per cell-step, `roofline_lds`);
   * k_loop_step (dense planes, `dense_path` leg, or --dense) moves the
     contract's 417 B.
 Both give bit-identical beliefs, values and actions (tests/test_gpu_coded.py).
@@ -474,6 +476,7 @@ def main():
     if args.dense:
         ctx.set_tuning(ctx.TUNE_CODED_MODEL, 0)
     dict_entries, coded = ctx.model_dict_info()
+    steps_per_launch = ctx.loop_steps_per_launch()
     ctx.belief_set(b0[r0 * gw:r1 * gw])
     ctx.mdp_reset()
     ctx.synchronize()
@@ -571,13 +574,17 @@ def main():
 
     bytes_loop = BYTES_LOOP_CODED if coded else BYTES_LOOP
     bytes_sweep = BYTES_SWEEP_CODED if coded else BYTES_SWEEP
-    loop_kernel = "k_loop_step_coded" if coded else "k_loop_step"
+    loop_kernel = ("k_loop_pair_coded" if steps_per_launch == 2 else "k_loop_step_coded") \
+        if coded else "k_loop_step"
+    spl = steps_per_launch
     sweep_gbs = bytes_sweep * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
     belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
     loop_gbs = bytes_loop * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
     contract_gbs = BYTES_LOOP * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
+    # PMC bytes per launch; a pair launch covers two steps (per step: / spl)
     traffic, traffic_src = pmc_traffic(loop_kernel, cells_per_gpu,
                                        exclude=None if coded else "coded")
+    bytes_launch_moved = BYTES_LOOP_CODED if spl == 2 else bytes_loop * spl
 
     result = None
     plan = None
@@ -624,8 +631,13 @@ def main():
             # the reference's fp32 tensor contract (T, L, C are inputs read per
             # cell).  The dictionary-coded kernel moves 19 B/cell (`traffic`,
             # `roofline_moved`), so its frac on the contract exceeds 1.
+            # avg_launch_us: the events' time per step x steps per launch
+            # (it includes the one k_sum_finalize launch per 8 steps; the
+            # kernel's own rocprof average is in profiles/).
             "roofline": {
-                "kernel": f"{loop_kernel} (fused belief update + MDP Bellman sweep)",
+                "kernel": (f"{loop_kernel} (two fused loop steps per launch: belief update + "
+                           f"MDP Bellman sweep, twice)" if spl == 2 else
+                           f"{loop_kernel} (fused belief update + MDP Bellman sweep)"),
                 "bound": "hbm",
                 "achieved": contract_gbs,
                 "peak": HBM_PEAK_GBS,
@@ -633,16 +645,20 @@ def main():
                 "frac": contract_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "steps_per_launch": spl,
                 "algorithmic_bytes_per_cell": BYTES_LOOP,
-                "algorithmic_bytes_per_launch": BYTES_LOOP * cells_per_gpu,
-                "avg_launch_us": loop_ms_events * 1e3,
+                "algorithmic_bytes_per_launch": BYTES_LOOP * cells_per_gpu * spl,
+                "avg_launch_us": loop_ms_events * 1e3 * spl,
             },
             "roofline_moved": {
-                "bytes_per_cell": bytes_loop,
-                "achieved": loop_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": loop_gbs / HBM_PEAK_GBS,
-                "note": ("bytes the coded kernel must move (code 2, b 4, b' 4, J 4, J' 4, "
-                         "A 1); latency- and LDS-bound, see roofline_lds"
+                "bytes_per_cell_per_launch": bytes_launch_moved,
+                "achieved": bytes_launch_moved * cells_per_gpu / (spl * loop_ms_events * 1e-3) / 1e9,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": bytes_launch_moved * cells_per_gpu / (spl * loop_ms_events * 1e-3) / 1e9
+                / HBM_PEAK_GBS,
+                "note": ("bytes the coded kernel must move per launch (code 2, b 4, b' 4, J 4, "
+                         "J' 4, A 1; a pair launch keeps the intermediate step in LDS); "
+                         "latency- and LDS-bound, see roofline_lds"
                          if coded else "dense planes: equal to the contract"),
             },
             "roofline_lds": ({

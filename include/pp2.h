@@ -146,6 +146,12 @@ int pp2_model_load(pp2_ctx* ctx, const char* dir);
  * bit-identical either way. */
 int pp2_model_dict_info(pp2_ctx* ctx, int* entries, int* active);
 
+/* Loop steps pp2_loop_run fuses into one kernel launch on this context: 2
+ * when it runs the steps of a normalisation block in pairs
+ * (PP2_TUNE_STEP_PAIRS on an unsharded context with a sparse coded model
+ * whose grid has a 4096-cell tile per CU), else 1. */
+int pp2_loop_steps_per_launch(pp2_ctx* ctx, int* steps);
+
 /* ---------------------------------------------------------------- belief
  * The belief lives on the device with deferred normalisation: each update
  * applies the previous step's 1/sum and records its own sum on the device,

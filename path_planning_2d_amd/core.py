@@ -115,6 +115,12 @@ class GridContext:
         call("pp2_model_dict_info", self._h, C.byref(e), C.byref(a))
         return e.value, bool(a.value)
 
+    def loop_steps_per_launch(self) -> int:
+        """Loop steps one kernel launch of pp2_loop_run covers (1 or 2)."""
+        n = C.c_int(0)
+        call("pp2_loop_steps_per_launch", self._h, C.byref(n))
+        return n.value
+
     def model_download(self):
         n = self.cells
         T = np.empty((n, 9, 9), np.float32)

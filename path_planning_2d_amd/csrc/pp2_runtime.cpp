@@ -605,11 +605,11 @@ static int blocked_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
 // (k_loop_pair_coded): the same state transitions as two blocked_loop_step
 // calls.  Applies to an unsharded context with a sparse coded model when the
 // block has two steps left.
-static bool can_pair(pp2_ctx* c) {
-  return c->step_pairs && !c->group && !c->comm && c->norm_block >= 2 &&
-         c->kstep + 2 <= c->norm_block && coded_active(c) && c->dict_sparse &&
-         pp2::loop_pair_fits(c->g, c->dict_n, true);
+static bool pairs_apply(pp2_ctx* c) {
+  return c->step_pairs && !c->group && !c->comm && c->norm_block >= 2 && coded_active(c) &&
+         c->dict_sparse && pp2::loop_pair_fits(c->g, c->dict_n, true);
 }
+static bool can_pair(pp2_ctx* c) { return c->kstep + 2 <= c->norm_block && pairs_apply(c); }
 
 static int loop_pair(pp2_ctx* c, uint8_t u1, uint8_t z1, uint8_t u2, uint8_t z2) {
   for (int i = 0; i < 2; ++i) {
@@ -941,6 +941,14 @@ int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
   if (c->comm || c->norm_block > 1) return blocked_loop_step(c, u, z);  // RCCL shard or blocks
   return loop_step_fused(c, u, z, false);
+}
+
+int pp2_loop_steps_per_launch(pp2_ctx* c, int* steps) {
+  CHECK(check_ctx(c));
+  if (!steps) return set_err(PP2_EINVAL, "steps is null");
+  DeviceGuard dg(c->device);
+  *steps = pairs_apply(c) ? 2 : 1;
+  return PP2_OK;
 }
 
 int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {

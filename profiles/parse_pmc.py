@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 # algorithmic HBM bytes per cell (bench.py docstring / DESIGN.md)
 ALGO = {"k_mdp_sweep": 369, "k_belief_update": 48, "k_loop_step": 417,
-        "k_loop_step_coded": 19, "k_mdp_sweep_coded": 11}
+        "k_loop_step_coded": 19, "k_mdp_sweep_coded": 11,
+        "k_loop_pair_coded": 19}  # two steps per launch, intermediate in LDS
 
 
 def short(name):
