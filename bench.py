@@ -8,30 +8,36 @@ on a 1024 x 1024 synthetic grid per GPU (BASELINE.json configs[2]; the metric
 "grid cells/sec for belief-update+Bellman loop, 1024x1024").  Inputs are
 resident in HBM before the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 1024]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 1024] [--grid G]
 
-For N > 1 launch with torch.distributed.run: rank r owns rows
-[r*S, (r+1)*S) of an (N*S) x S grid (weak scaling); every 8 steps it
-exchanges 8 halo rows of belief and values with its neighbours and
-all-reduces the belief mass over RCCL.
+For N > 1 launch with torch.distributed.run.  Default (weak scaling): rank r
+owns rows [r*S, (r+1)*S) of an (N*S) x S grid.  --grid G (strong scaling):
+one fixed G x G grid, rows split as evenly as possible over the N ranks.
+Every 8 steps a rank exchanges 8 halo rows of belief and values with its
+neighbours and all-reduces the belief mass over RCCL.
+
+Every run also reports `config4` (BASELINE.json configs[3]): the 2048 x 2048
+grid row-sharded over all N ranks (strong scaling), its cells/s, the same
+grid unsharded on rank 0's GPU in the same job (speedup), and a parity gate:
+the sharded J / A gathered to rank 0 equal the unsharded run bit for bit and
+the belief agrees to rel 1e-5.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant (and only)
 kernel of a step, timed live with HIP events around the timed steps on the
-stream it runs on, with SURVEY.md §8(d)'s algorithmic bytes: 417 per cell
-(belief: T_u 36 + L_z 4 + b 4 + b' 4; sweep: T 324 + C 36 + J 4 + J' 4 +
-A 1, the reference's fp32 tensor contract).
-  * k_loop_pair_coded (default at 1024^2: two steps per launch, the first
-    over the tile plus a one-row halo kept in LDS) and k_loop_step_coded (one
-    step per launch; the model is dictionary-coded) move
-    only 19 B per cell and launch (code 2, b 4, b' 4, J 4, J' 4, A 1;
-    `traffic`, `roofline_moved`), so their frac on the contract exceeds 1;
-    the binding resources are the per-launch latency chain and LDS (196 B
-    of dictionary reads per cell-step, `roofline_lds`);
-  * k_loop_step (dense planes, `dense_path` leg, or --dense) moves the
-    contract's 417 B.
-Both give bit-identical beliefs, values and actions (tests/test_gpu_coded.py).
-`cpu_baseline` is the C restatement of the reference (oracle/) timed on this
-host on a bounded sample of the same workload.
+stream it runs on: k_loop_pair_coded (default at 1024^2: two steps per
+launch, the first over the tile plus a one-row halo kept in LDS) or
+k_loop_step_coded (one step per launch) on the dictionary-coded model
+(DESIGN.md §2.1).  Its algorithmic bytes are the ones the kernel must move
+per cell and launch: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1 = 19 B (the
+intermediate step of a pair stays in LDS); `traffic` is the PMC-measured HBM
+bytes per launch from profiles/pmc_*.json.  `contract_equivalent` states the
+same throughput on SURVEY.md §8(d)'s 417 B/cell fp32 tensor contract of the
+reference (T 324 + C 36 + T_u 36 + L_z 4 + b/b'/J/J' 16 + A 1), which the coded
+kernel does not move; the `dense_path` leg runs the dense-plane kernel that
+does (k_loop_step, or --dense).  Both give bit-identical beliefs, values and
+actions (tests/test_gpu_coded.py).  `cpu_baseline` is the C restatement of
+the reference (oracle/) timed on this host on a bounded sample of the same
+workload.
 """
 from __future__ import annotations
 
@@ -64,7 +70,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--size", type=int, default=1024, help="grid side per GPU")
+    ap.add_argument("--size", type=int, default=1024, help="grid side per GPU (weak scaling)")
+    ap.add_argument("--grid", type=int, default=0,
+                    help="strong scaling: one G x G grid row-sharded over the ranks")
+    ap.add_argument("--c4-size", type=int, default=2048,
+                    help="config4 leg: grid side (0 disables)")
+    ap.add_argument("--c4-steps", type=int, default=200)
+    ap.add_argument("--c4-warmup", type=int, default=16)
     ap.add_argument("--cpt", type=int, default=4, help="cells per lane")
     ap.add_argument("--kernel-reps", type=int, default=100,
                     help="launches per kernel in the per-kernel timing segment")
@@ -421,6 +433,118 @@ def rollout_bench(args, device, stream):
             "mean_value": float(res["value"].mean())}
 
 
+def _gather_rows(arr, r0, r1, G, W, ws, torch, dist):
+    """Rows [r0, r1) (flat, row-major) of a G x W array from every rank,
+    assembled in row order on every rank (all_gather over RCCL)."""
+    maxr = -(-G // ws)
+    t = torch.zeros((maxr * W,), dtype=torch.from_numpy(arr[:1]).dtype, device="cuda")
+    t[: (r1 - r0) * W] = torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+    parts = [torch.empty_like(t) for _ in range(ws)]
+    dist.all_gather(parts, t)
+    out = []
+    for r in range(ws):
+        a, b = r * G // ws, (r + 1) * G // ws
+        out.append(parts[r][: (b - a) * W].cpu().numpy())
+    return np.concatenate(out)
+
+
+def config4_leg(args, ws, rank, local, stream):
+    """BASELINE.json configs[3]: the G x G (2048^2) grid, belief stencil +
+    Bellman sweep row-sharded over the ws ranks (strong scaling, RCCL halo
+    every 8 steps), and the same grid unsharded on rank 0's GPU in the same
+    job: cells/s of both, the speedup, and the parity gate (sharded J / A ==
+    unsharded bit for bit, belief rel 1e-5 above a 1e-30 floor; the reference
+    loop is single-GPU, src/mdp/path_planning_2d.cu:226-237)."""
+    import torch
+    import torch.distributed as dist
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    G = args.c4_size
+    grid = S.synth_grid(G, G, seed=G)
+    goal = S.synth_goal(grid)
+    w, k = args.c4_warmup, args.c4_steps
+    us, zs, _ = S.synth_trajectory(grid, w + k, seed=42)
+    b0 = S.uniform_belief(grid)
+    r0, r1 = rank * G // ws, (rank + 1) * G // ws
+
+    def run(ctx, sharded):
+        ctx.loop_run(us[:w], zs[:w])
+        torch.cuda.synchronize()
+        if sharded:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.loop_run(us[w:], zs[w:])
+        torch.cuda.synchronize()
+        if sharded:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if sharded:
+            t = torch.tensor([el], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    out = None
+    if ws > 1:
+        ctx = P.GridContext(grid, goal, gamma=GAMMA, device=local, rows=(r0, r1))
+        ctx.set_stream(stream.cuda_stream)
+        uid = torch.zeros(P._lib.RCCL_ID_BYTES, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(P.GridContext.rccl_unique_id()),
+                                       dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        ctx.shard_comm_init(bytes(uid.cpu().numpy().tobytes()), ws, rank)
+        ctx.model_generate()
+        ctx.belief_set(b0[r0 * G:r1 * G])
+        ctx.mdp_reset()
+        ctx.synchronize()
+        el = run(ctx, True)
+        b = ctx.belief_get()  # collective: global mass all-reduce
+        J, A = ctx.mdp_get()
+        ctx.close()
+        bg = _gather_rows(b, r0, r1, G, G, ws, torch, dist)
+        Jg = _gather_rows(J, r0, r1, G, G, ws, torch, dist)
+        Ag = _gather_rows(A, r0, r1, G, G, ws, torch, dist)
+    if rank == 0:
+        with P.GridContext(grid, goal, gamma=GAMMA, device=local) as c1:
+            c1.set_stream(stream.cuda_stream)
+            c1.model_generate()
+            c1.belief_set(b0)
+            c1.mdp_reset()
+            c1.synchronize()
+            el1 = run(c1, False)
+            b1 = c1.belief_get()
+            J1, A1 = c1.mdp_get()
+        v1 = G * G * k / el1
+        out = {"workload": f"{G}x{G} grid (BASELINE.json configs[3]), {k} timed loop steps "
+                           f"after {w} warm-up, rows split over {ws} rank(s)",
+               "n_gpus": ws, "scaling": "strong",
+               "unsharded_1gpu": {"cells_per_s": v1, "ms_per_step": 1e3 * el1 / k}}
+        if ws > 1:
+            v = G * G * k / el
+            j_ok = bool(np.array_equal(Jg.view(np.uint32), J1.view(np.uint32)))
+            a_ok = bool(np.array_equal(Ag, A1))
+            err = np.abs(bg.astype(np.float64) - b1) / np.maximum(np.abs(b1.astype(np.float64)),
+                                                                   1e-300)
+            bmask = np.abs(b1) > 1e-30
+            b_rel = float(err[bmask].max()) if bmask.any() else 0.0
+            b_ok = b_rel <= 1e-5 and bool(np.all(np.abs(bg[~bmask]) <= 1e-30))
+            out.update({"cells_per_s": v, "ms_per_step": 1e3 * el / k,
+                        "speedup_vs_unsharded_1gpu": v / v1,
+                        "parity": {"J_bit_exact": j_ok, "A_bit_exact": a_ok,
+                                   "belief_max_rel_err": b_rel, "belief_ok": b_ok,
+                                   "pass": j_ok and a_ok and b_ok}})
+        else:
+            out.update({"cells_per_s": v1, "ms_per_step": 1e3 * el1 / k,
+                        "speedup_vs_unsharded_1gpu": 1.0,
+                        "parity": "single rank: nothing to gather"})
+    if ws > 1:
+        dist.barrier()
+    return out
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -446,17 +570,24 @@ def main():
     if ws > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    N = args.size
-    gh, gw = N * ws, N
+    strong = args.grid > 0
+    if strong:
+        gh = gw = args.grid
+        r0, r1 = rank * gh // ws, (rank + 1) * gh // ws
+    else:
+        N = args.size
+        gh, gw = N * ws, N
+        r0, r1 = rank * N, (rank + 1) * N
     grid = S.synth_grid(gh, gw, seed=gh)
     goal = S.synth_goal(grid)
     total = args.warmup + args.steps
-    us, zs, _ = S.synth_trajectory(grid, min(total, 4096), seed=42)
-    us = np.resize(us, total)
-    zs = np.resize(zs, total)
+    # long enough for the timed steps and for the per-kernel timing segment
+    ntraj = max(total, args.kernel_reps)
+    us, zs, _ = S.synth_trajectory(grid, min(ntraj, 4096), seed=42)
+    us = np.resize(us, ntraj)
+    zs = np.resize(zs, ntraj)
     b0 = S.uniform_belief(grid)
 
-    r0, r1 = rank * N, (rank + 1) * N
     ctx = P.GridContext(grid, goal, gamma=GAMMA, device=local,
                         rows=(r0, r1) if ws > 1 else None)
     ctx.set_cells_per_lane(args.cpt)
@@ -493,7 +624,7 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    ctx.loop_run(us[args.warmup:], zs[args.warmup:])
+    ctx.loop_run(us[args.warmup:total], zs[args.warmup:total])
     enqueue_s = time.perf_counter() - t0
     ev1.record(stream)
     torch.cuda.synchronize()
@@ -507,8 +638,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    cells_per_gpu = N * N
-    value = cells_per_gpu * ws * args.steps / elapsed
+    cells_per_gpu = (r1 - r0) * gw  # this rank's cells
+    value = gh * gw * args.steps / elapsed
     # sanity: the belief is still a distribution (checks the timed work ran)
     mass_ok = None
     if rank == 0 and ws == 1:
@@ -566,7 +697,7 @@ def main():
         n_sw, nrm = ctx.mdp_solve()
         torch.cuda.synchronize()
         t_solve = time.perf_counter() - t0
-        mdp_solve = {"config": f"{N}x{N} MDP value iteration to convergence "
+        mdp_solve = {"config": f"{gh}x{gw} MDP value iteration to convergence "
                                f"(blocks of 100 sweeps, stop at inf-norm <= 1e-3*5/(1-gamma))",
                      "sweeps": n_sw, "final_norm": nrm, "ms": t_solve * 1e3,
                      "us_per_sweep": t_solve * 1e6 / max(1, n_sw)}
@@ -579,12 +710,17 @@ def main():
     spl = steps_per_launch
     sweep_gbs = bytes_sweep * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
     belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
-    loop_gbs = bytes_loop * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
+    # one launch = spl steps; its average duration from the timed region's events
+    launch_s = loop_ms_events * 1e-3 * spl
+    algo_launch = bytes_loop * cells_per_gpu  # bytes the kernel must move per launch
+    loop_gbs = algo_launch / launch_s / 1e9
     contract_gbs = BYTES_LOOP * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
-    # PMC bytes per launch; a pair launch covers two steps (per step: / spl)
     traffic, traffic_src = pmc_traffic(loop_kernel, cells_per_gpu,
                                        exclude=None if coded else "coded")
-    bytes_launch_moved = BYTES_LOOP_CODED if spl == 2 else bytes_loop * spl
+
+    c4 = None
+    if args.c4_size > 0:
+        c4 = config4_leg(args, ws, rank, local, stream)
 
     result = None
     plan = None
@@ -610,56 +746,54 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic: splitmix64 occupancy grid (p_occ=0.2, seed=H), "
                     "uniform initial belief, seeded simulated (u,z) trajectory",
             "config": {
-                "workload": f"{N}x{N} cells per GPU: 1 belief update + 1 MDP "
-                            f"Bellman sweep per step (BASELINE.json configs[2] grid)",
+                "workload": (f"{gh}x{gw} grid row-sharded over {ws} GPU(s): 1 belief update + "
+                             f"1 MDP Bellman sweep per step" if strong else
+                             f"{args.size}x{args.size} cells per GPU: 1 belief update + 1 MDP "
+                             f"Bellman sweep per step (BASELINE.json configs[2] grid)"),
                 "grid": [gh, gw],
-                "rows_per_gpu": N,
-                "parallelism": (f"row-shard x{ws}: {min(8, N)}-row RCCL halo exchange and one "
-                                f"1-float mass all-reduce every {min(8, N)} steps"
+                "rows_per_gpu": r1 - r0,
+                "parallelism": (f"row-shard x{ws}: 8-row RCCL halo exchange and one "
+                                f"1-float mass all-reduce every 8 steps"
                                 if ws > 1 else "single GPU"),
                 "cells_per_lane": args.cpt,
                 "model": (f"dictionary-coded ({dict_entries} entries, uint16 code per cell)"
                           if coded else "dense fp32 planes"),
             },
-            # the loop's algorithmic bytes are 417 per cell on
-            # the reference's fp32 tensor contract (T, L, C are inputs read per
-            # cell).  The dictionary-coded kernel moves 19 B/cell (`traffic`,
-            # `roofline_moved`), so its frac on the contract exceeds 1.
-            # avg_launch_us: the events' time per step x steps per launch
-            # (it includes the one k_sum_finalize launch per 8 steps; the
-            # kernel's own rocprof average is in profiles/).
             "roofline": {
                 "kernel": (f"{loop_kernel} (two fused loop steps per launch: belief update + "
                            f"MDP Bellman sweep, twice)" if spl == 2 else
                            f"{loop_kernel} (fused belief update + MDP Bellman sweep)"),
                 "bound": "hbm",
-                "achieved": contract_gbs,
+                "achieved": loop_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": contract_gbs / HBM_PEAK_GBS,
+                "frac": loop_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "steps_per_launch": spl,
-                "algorithmic_bytes_per_cell": BYTES_LOOP,
-                "algorithmic_bytes_per_launch": BYTES_LOOP * cells_per_gpu * spl,
-                "avg_launch_us": loop_ms_events * 1e3 * spl,
+                "algorithmic_bytes_per_cell_per_launch": bytes_loop,
+                "algorithmic_bytes_per_launch": algo_launch,
+                "avg_launch_us": launch_s * 1e6,
+                "note": ("bytes the coded kernel must move per launch: code 2, b 4, b' 4, J 4, "
+                         "J' 4, A 1 per cell (a pair launch keeps its intermediate step in "
+                         "LDS); launch-latency and LDS bound, see roofline_lds"
+                         if coded else "dense planes: SURVEY.md §8(d) fp32 tensor contract"),
             },
-            "roofline_moved": {
-                "bytes_per_cell_per_launch": bytes_launch_moved,
-                "achieved": bytes_launch_moved * cells_per_gpu / (spl * loop_ms_events * 1e-3) / 1e9,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": bytes_launch_moved * cells_per_gpu / (spl * loop_ms_events * 1e-3) / 1e9
-                / HBM_PEAK_GBS,
-                "note": ("bytes the coded kernel must move per launch (code 2, b 4, b' 4, J 4, "
-                         "J' 4, A 1; a pair launch keeps the intermediate step in LDS); "
-                         "latency- and LDS-bound, see roofline_lds"
-                         if coded else "dense planes: equal to the contract"),
+            "contract_equivalent": {
+                "bytes_per_cell_step": BYTES_LOOP,
+                "GBps": contract_gbs,
+                "frac_of_hbm_peak": contract_gbs / HBM_PEAK_GBS,
+                "note": ("the loop's throughput priced on the reference's fp32 tensor contract "
+                         "(SURVEY.md §8(d): T, C, T_u, L_z read per cell, 417 B/cell-step); the "
+                         "coded kernel does not move these bytes, so this can exceed 1 and is "
+                         "not a roofline fraction -- the 11.5 G cells/s target of BASELINE.md "
+                         "is 60 % of 8 TB/s / 417 B"),
             },
             "roofline_lds": ({
                 "achieved": LDS_BYTES_LOOP_CODED * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9,
@@ -668,6 +802,7 @@ def main():
                 / LDS_PEAK_GBS,
                 "bytes_per_cell": LDS_BYTES_LOOP_CODED} if coded else None),
             "dense_path": dense,
+            "config4": c4,
             "kernels": {
                 "mdp_sweep_kernel": "k_mdp_sweep_coded" if coded else "k_mdp_sweep",
                 "mdp_sweep_us": sweep_ms * 1e3,

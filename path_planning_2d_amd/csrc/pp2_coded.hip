@@ -18,8 +18,6 @@
 // the dense kernels' (same operands, same fmaf order), and the belief partial
 // sums use the dense kernels' cell->block mapping and reduction tree, so the
 // coded and dense paths give bit-identical beliefs, masses, values and actions.
-#include <stdlib.h>
-
 #include "pp2_device.h"
 
 namespace pp2 {
@@ -357,30 +355,6 @@ __device__ __forceinline__ void sweep_cells(const Geom& g, const float* sTC, flo
   }
 }
 
-// J window of a lane from the workgroup's LDS copy of its tile's value rows
-// (sJ holds the plane from flat cell jb on, see k_loop_step_coded).
-__device__ __forceinline__ void lds_win6(const float* sJ, int wp, int y, int x0, long long jb,
-                                         bool le, bool re, Win6& w) {
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    const float* p = sJ + ((long long)(y + r - 1) * wp + x0 - jb);
-    const f4a m = *reinterpret_cast<const f4a*>(p);
-    const float l = p[-1], rt = p[4];
-    w.v[r][0] = le ? 0.0f : l;
-    w.v[r][1] = m[0];
-    w.v[r][2] = m[1];
-    w.v[r][3] = m[2];
-    w.v[r][4] = m[3];
-    w.v[r][5] = re ? 0.0f : rt;
-  }
-}
-
-// Floats of the value rows one tile's sweep reads: its cells, one row and a
-// 16-B chunk on each side, rounded to whole 1-KiB DMA instructions.
-__host__ __device__ constexpr int jwin_floats(int tile_cells, int wp) {
-  return lds_span(tile_cells + 2 * wp + 8);
-}
-
 // Fused north-star step on the coded model (k_loop_step's semantics).  A
 // workgroup of QPB x 256 threads covers QPB dense-kernel blocks per tile:
 // lane (q, t) of tile tl is the dense kernel's thread t of block QPB*tl + q,
@@ -391,10 +365,12 @@ __host__ __device__ constexpr int jwin_floats(int tile_cells, int wp) {
 // would not fit beside the belief's); no barrier follows the stores.
 //   rows: dictionary rows in the LDS layout (E x Layout::row floats)
 //   lz:   L_z column of the dictionary (E floats)
-// JPF: the first tile's value rows (jwin_floats) are DMA-staged into LDS with
-// the dictionary, so the sweep's J window is an LDS read instead of an HBM
-// round trip after the belief update.  NT: non-temporal b', J', A stores.
-template <bool SPARSE, int QPB, int MINB, int U = -1, bool JPF = false, bool NT = false>
+// NT: non-temporal b', J', A stores (they skip the L2 write-back at the end
+// of the launch).  A value-row prefetch into LDS (the sweep's J window staged
+// with the dictionary) measured slower: every workgroup's barrier then waits
+// for an HBM round trip that the register path overlaps with the belief
+// update (MI355X, 1024^2: 10.5 vs 9.3 us per step).
+template <bool SPARSE, int QPB, int MINB, int U = -1, bool NT = false>
 __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
     const float* __restrict__ lz, const float* __restrict__ tu, int E,
@@ -408,7 +384,6 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   float* sTC = lds;
   float* sL = lds + lds_span(E * LY::row);
   float* sTu = sL + lds_span(E);
-  float* sJ = sTu + lds_span(E * LY::tu);
   PP2_PHASE(0);
   const int q = threadIdx.x / kQuarter, tq = threadIdx.x % kQuarter;
   const int tpr = g.wp / 4;
@@ -429,26 +404,18 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   stage_rows(rows, E * LY::row, sTC);
   stage_rows(lz, E, sL);
   stage_rows(tu, E * LY::tu, sTu);
-  long long jb = 0;  // flat cell of sJ[0]
-  if constexpr (JPF) {
-    constexpr int kTileCells = QPB * kQuarter * 4;
-    jb = (long long)(tile0 < ntiles ? tile0 : 0) * kTileCells - g.wp - 4;
-    // 16-B chunks past the halo row below re-read its last chunk (their LDS
-    // words belong to lanes without a cell)
-    const long long hi = (long long)(g.rows + 1) * g.wp - 4;
-    const int n4 = jwin_floats(kTileCells, g.wp) >> 2;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int c = wave; c * 64 < n4; c += nw) {
-      long long f = jb + 4LL * (c * 64 + lane);
-      if (f > hi) f = hi;
-      __builtin_amdgcn_global_load_lds((glb_void*)(J_in + f), (lds_void*)(sJ + c * 256), 16, 0, 0);
+  // pending input mass: wave 0 reduces the partials (k_sum_finalize's tree)
+  // while the dictionary stages, and hands the sum over through LDS
+  float* sS = sTu + lds_span(E * LY::tu);
+  if (in_partials && threadIdx.x < 64) {
+    const float S = wave_reduce_partials(in_partials, in_n);
+    if (threadIdx.x == 0) {
+      sS[0] = S;
+      if (in_sum_out && blockIdx.x == 0) *in_sum_out = S;
     }
+  } else if (!in_partials && in_sum_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    *in_sum_out = in_sum ? *in_sum : 1.0f;
   }
-  float S = 1.0f;
-  if (in_partials) S = wave_reduce_partials(in_partials, in_n);
-  else if (in_sum) S = *in_sum;
-  if (in_sum_out && blockIdx.x == 0 && threadIdx.x == 0) *in_sum_out = S;
-  const float inv = (1.0f / S) * scale;  // scale: a power of two (1 unsharded)
   // belief gather: LDS slot of T[.][u][i] inside the action-u block, or -1
   // when i is outside u's support on the sparse layout (T == 0 there)
   int slot[9];
@@ -464,6 +431,8 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
     }
   }
   __syncthreads();
+  const float S = in_partials ? sS[0] : in_sum ? *in_sum : 1.0f;
+  const float inv = (1.0f / S) * scale;  // scale: a power of two (1 unsharded)
   PP2_PHASE(1);
   if (tile0 >= ntiles) return;
   {
@@ -476,8 +445,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       if (!own) local = 0.0f;
       PP2_PHASE(2);
       Win6 jw;
-      if constexpr (JPF) lds_win6(sJ, g.wp, y, x0, jb, x0 == 0, x0 + 4 == g.wp, jw);
-      else load_win6(J_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, jw);
+      load_win6(J_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, jw);
       sweep_cells<SPARSE, NT>(g, sTC, gamma, cw.m0[1], cw.m1[1], jw, y, x0, own, J_out, A);
       PP2_PHASE(3);
     }
@@ -602,8 +570,9 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
     const float* __restrict__ lz1, const float* __restrict__ lz2, const float* __restrict__ tu1,
     const float* __restrict__ tu2, int E, int u1, int u2, const float* __restrict__ b_in,
     float* __restrict__ b_out, const float* __restrict__ J_in, float* __restrict__ J_out,
-    uint8_t* __restrict__ A, float* __restrict__ out_partials, const float* __restrict__ in_sum,
-    float scale0, int dense_blocks) {
+    uint8_t* __restrict__ A, float* __restrict__ out_partials, const float* __restrict__ in_partials,
+    int in_n, float* __restrict__ in_sum_out, const float* __restrict__ in_sum, float scale0,
+    int dense_blocks) {
   using LY = Layout<true>;
   extern __shared__ float lds[];
   const int nreg = pair_region(g.wp);
@@ -614,6 +583,7 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
   float* sT2 = sT1 + lds_span(E * LY::tu);
   float* sB = sT2 + lds_span(E * LY::tu);  // step-1 belief over the region
   float* sJ = sB + lds_span(nreg);         // step-1 values over the region
+  float* sS = sJ + lds_span(nreg);         // the input mass (block-start launch)
   const int q = threadIdx.x / kQuarter;
   const int ntiles = (dense_blocks + kPQ - 1) / kPQ;
   stage_rows(rows, E * LY::row, sTC);
@@ -621,8 +591,19 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
   stage_rows(lz2, E, sL2);
   stage_rows(tu1, E * LY::tu, sT1);
   stage_rows(tu2, E * LY::tu, sT2);
-  const float inv0 = in_sum ? (1.0f / *in_sum) * scale0 : scale0;
+  // block-start launch with the previous launch's mass still pending: wave 0
+  // reduces its partials (k_sum_finalize's tree, so the mass is bit-identical
+  // to a separately finalised one) while the dictionary stages
+  if (in_partials && threadIdx.x < 64) {
+    const float S = wave_reduce_partials(in_partials, in_n);
+    if (threadIdx.x == 0) {
+      sS[0] = S;
+      if (blockIdx.x == 0 && in_sum_out) *in_sum_out = S;
+    }
+  }
   __syncthreads();
+  const float inv0 = in_partials ? (1.0f / sS[0]) * scale0
+                                 : in_sum ? (1.0f / *in_sum) * scale0 : scale0;
   for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
     const long long c0 = (long long)tile * kPTile;
     const long long r0 = c0 - g.wp - 4;  // flat cell of sB[0] / sJ[0] (a quad boundary)
@@ -675,52 +656,47 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
   }
 }
 
-int g_num_cus = 0;
+// Per-device launch facts: the CU count (grid caps, loop_pair_fits) and which
+// kernels were opted into the large dynamic LDS on that device.  A process may
+// drive several devices (a shard group, several contexts).
+constexpr int kMaxDevices = 64;
+int g_num_cus[kMaxDevices];
+
+int device_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+  if (g_num_cus[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    g_num_cus[dev] = n;
+  }
+  return g_num_cus[dev];
+}
 
 int coded_grid(int ntiles, int per_cu) {
-  if (g_num_cus == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      g_num_cus = n;
-    if (g_num_cus <= 0) g_num_cus = 256;
-  }
-  const int cap = g_num_cus * per_cu;
+  const int cap = device_cus() * per_cu;
   return ntiles < cap ? ntiles : cap;
-}
-
-// Opt a kernel into more than the default dynamic LDS once per process.  A
-// refusal is not fatal here: the launch itself reports an oversized request.
-void allow_lds(const void* fn, bool& done) {
-  if (done) return;
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDictLdsMaxBytes);
-  (void)hipGetLastError();
-  done = true;
-}
-
-// Loop-kernel variant bits (A/B runs; PP2_LOOP_VARIANT, default 2): 1 =
-// value-row prefetch into LDS, 2 = non-temporal stores, 4 = one 1024-thread workgroup
-// per CU (non-temporal stores, no prefetch), 8 = non-temporal stores in the
-// MDP sweep kernel.  MI355X, 1024^2
-// loop step (two interleaved runs): 0: 9.90 / 9.75 us, 1: 10.57 / 10.44,
-// 2: 9.25 / 9.34, 3: 9.95 / 10.09; later 0: 9.94 / 9.99, 2: 9.45 / 9.53,
-// 6: 9.51 / 9.46 (2048^2: 27.4-28.2 for all three).  The prefetch makes every workgroup's
-// barrier wait for an HBM round trip that the register path overlaps with
-// the belief update; non-temporal stores skip the L2 write-back at the end
-// of the launch.
-int loop_variant() {
-  static const int v = [] {
-    const char* e = getenv("PP2_LOOP_VARIANT");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
 }
 
 }  // namespace
 
+// Opt a kernel into more than the default dynamic LDS once per device (bit d
+// of `done`).  A refusal is not fatal here: the launch itself reports an
+// oversized request.
+void allow_lds(const void* fn, unsigned long long& done) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+  if (done >> dev & 1ull) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDictLdsMaxBytes);
+  (void)hipGetLastError();
+  done |= 1ull << dev;
+}
+
 size_t coded_loop_lds_bytes(int E, bool sparse) {
   return ((size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) + lds_span(E) +
-          lds_span(E * tu_width(sparse))) * sizeof(float);
+          lds_span(E * tu_width(sparse)) + 4) * sizeof(float);
 }
 
 hipError_t launch_dict_hash(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
@@ -757,34 +733,21 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   const float* in_partials, int in_n, const float* in_sum,
                                   float* in_sum_out, float* out_partials, const float* J_in,
                                   float* J_out, uint8_t* A, int own0, int own1, float scale) {
-  const size_t lds0 = coded_loop_lds_bytes(E, sparse);
+  const size_t lds = coded_loop_lds_bytes(E, sparse);
   const int dense_blocks = cells_grid(g, 4);
-  // value-row prefetch when both workgroups' LDS still fit a CU (sparse rows)
-  const size_t jlds = (size_t)jwin_floats(2 * kQuarter * 4, g.wp) * sizeof(float);  // QPB 2
-  const int var = loop_variant();
-  const bool jpf = sparse && (var & 5) == 1 && (lds0 + jlds) * 2 <= kDictLdsMaxBytes;
-  const bool nt = (var & 2) != 0;
-  const size_t lds = lds0 + (jpf ? jlds : 0);
-#define PP2_LOOPC(SP, Q, MB, UU, JP, N)                                                          \
+#define PP2_LOOPC(SP, Q, MB, UU, N)                                                              \
   do {                                                                                          \
     if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                               \
-    static bool attr = false;                                                                   \
-    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB, UU, JP, N>), attr);   \
+    static unsigned long long attr = 0;                                                         \
+    allow_lds(reinterpret_cast<const void*>(&k_loop_step_coded<SP, Q, MB, UU, N>), attr);       \
     const int grid = coded_grid((dense_blocks + Q - 1) / Q, MB);                                \
-    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB, UU, JP, N>), dim3(grid), dim3(Q * kQuarter), \
+    hipLaunchKernelGGL((k_loop_step_coded<SP, Q, MB, UU, N>), dim3(grid), dim3(Q * kQuarter),   \
                        lds, st,                                                                 \
                        g, gamma, code, rows, lz, tu, E, b_in, b_out, u, in_partials, in_n,      \
                        in_sum, in_sum_out, out_partials, dense_blocks, J_in, J_out, A, own0,    \
                        own1, scale);                                                            \
   } while (0)
-#define PP2_LOOPV(UU)                                                  \
-  do {                                                                 \
-    if (var & 4) PP2_LOOPC(true, 4, 1, UU, false, true);               \
-    else if (jpf && nt) PP2_LOOPC(true, 2, 2, UU, true, true);         \
-    else if (jpf) PP2_LOOPC(true, 2, 2, UU, true, false);              \
-    else if (nt) PP2_LOOPC(true, 2, 2, UU, false, true);               \
-    else PP2_LOOPC(true, 2, 2, UU, false, false);                      \
-  } while (0)
+#define PP2_LOOPV(UU) PP2_LOOPC(true, 2, 2, UU, true)
   // sparse rows: two 512-thread workgroups per CU (~60-76 KB LDS each, <= 128
   // VGPRs, 4 waves per SIMD), one kernel per action (its support terms
   // only); full rows: one 1024-thread workgroup per CU
@@ -801,7 +764,7 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
       default: PP2_LOOPV(8); break;
     }
   } else {
-    PP2_LOOPC(false, 4, 1, -1, false, false);
+    PP2_LOOPC(false, 4, 1, -1, false);
   }
 #undef PP2_LOOPV
 #undef PP2_LOOPC
@@ -810,7 +773,7 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
 
 size_t loop_pair_lds_bytes(int E, int wp) {
   return ((size_t)lds_span(E * kSpRow) + 2 * lds_span(E) + 2 * lds_span(E * tu_width(true)) +
-          2 * lds_span(pair_region(wp))) * sizeof(float);
+          2 * lds_span(pair_region(wp)) + 4) * sizeof(float);
 }
 
 bool loop_pair_fits(const Geom& g, int E, bool sparse) {
@@ -818,10 +781,9 @@ bool loop_pair_fits(const Geom& g, int E, bool sparse) {
   // step-1 cells, and a tile for every CU: on fewer tiles the per-step
   // kernel's 2048-cell workgroups keep more CUs busy (MI355X, 512^2: 6.1
   // us/step per-step vs 7.4 paired; 1024^2: 9.45 vs 9.0).
-  (void)coded_grid(1, 1);  // sets g_num_cus
   return sparse && E > 0 && loop_pair_lds_bytes(E, g.wp) <= kDictLdsMaxBytes &&
          5 * (2 * g.wp + 8) <= 3 * kPTile &&
-         (cells_grid(g, 4) + kPQ - 1) / kPQ >= g_num_cus;
+         (cells_grid(g, 4) + kPQ - 1) / kPQ >= device_cus();
 }
 
 hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
@@ -829,17 +791,18 @@ hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
                                   const float* lz2, const float* tu1, const float* tu2, int E,
                                   int u1, int u2, const float* b_in, float* b_out,
                                   const float* J_in, float* J_out, uint8_t* A,
-                                  float* out_partials, const float* in_sum, float scale) {
+                                  float* out_partials, const float* in_partials, int in_n,
+                                  float* in_sum_out, const float* in_sum, float scale) {
   if (!loop_pair_fits(g, E, true) || u1 < 0 || u1 > 8 || u2 < 0 || u2 > 8)
     return hipErrorInvalidValue;
   const size_t lds = loop_pair_lds_bytes(E, g.wp);
-  static bool attr = false;
+  static unsigned long long attr = 0;
   allow_lds(reinterpret_cast<const void*>(&k_loop_pair_coded), attr);
   const int dense_blocks = cells_grid(g, 4);
   const int grid = coded_grid((dense_blocks + kPQ - 1) / kPQ, 1);
   hipLaunchKernelGGL(k_loop_pair_coded, dim3(grid), dim3(kPQ * kQuarter), lds, st, g, gamma,
                      code, rows, lz1, lz2, tu1, tu2, E, u1, u2, b_in, b_out, J_in, J_out, A,
-                     out_partials, in_sum, scale, dense_blocks);
+                     out_partials, in_partials, in_n, in_sum_out, in_sum, scale, dense_blocks);
   return hipGetLastError();
 }
 
@@ -848,24 +811,19 @@ hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const float* J_in, float* J_out, uint8_t* A) {
   const size_t lds = (size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) * sizeof(float);
   const long long nthreads = (long long)g.rows * (g.wp / 4);
-#define PP2_SWEEPC(SP, Q, MB, N)                                                               \
+// Plain stores: non-temporal ones measured slower here (1024^2: 8.8 -> 9.9 us).
+#define PP2_SWEEPC(SP, Q, MB)                                                                  \
   do {                                                                                         \
     if (lds * MB > kDictLdsMaxBytes) return hipErrorInvalidValue;                              \
-    static bool attr = false;                                                                  \
-    allow_lds(reinterpret_cast<const void*>(&k_mdp_sweep_coded<SP, Q, MB, N>), attr);          \
+    static unsigned long long attr = 0;                                                        \
+    allow_lds(reinterpret_cast<const void*>(&k_mdp_sweep_coded<SP, Q, MB, false>), attr);      \
     const int nt = Q * kQuarter;                                                               \
     const int grid = coded_grid((int)((nthreads + nt - 1) / nt), MB);                          \
-    hipLaunchKernelGGL((k_mdp_sweep_coded<SP, Q, MB, N>), dim3(grid), dim3(nt), lds, st, g,     \
+    hipLaunchKernelGGL((k_mdp_sweep_coded<SP, Q, MB, false>), dim3(grid), dim3(nt), lds, st, g, \
                        gamma, code, rows, E, J_in, J_out, A);                                  \
   } while (0)
-  const bool ntst = (loop_variant() & 8) != 0;  // measured slower (8.8 -> 9.9 us at 1024^2)
-  if (sparse) {
-    if (ntst) PP2_SWEEPC(true, 4, 2, true);
-    else PP2_SWEEPC(true, 4, 2, false);
-  } else {
-    if (ntst) PP2_SWEEPC(false, 4, 1, true);
-    else PP2_SWEEPC(false, 4, 1, false);
-  }
+  if (sparse) PP2_SWEEPC(true, 4, 2);
+  else PP2_SWEEPC(false, 4, 1);
 #undef PP2_SWEEPC
   return hipGetLastError();
 }

@@ -102,6 +102,9 @@ struct pp2_ctx {
   float* d_tu = nullptr;           // raw T per action: [u][entry][4 sparse | 9 full]
   int dict_n = 0;                  // entries; 0 = no dictionary (dense path only)
   bool dict_sparse = false;        // every T row is zero off the base-kernel support
+  // the sparse rows' T == 0 skip needs finite, non-negative beliefs (not -0):
+  // false after a pp2_belief_set that breaks that, until the next one
+  bool belief_sparse_ok = true;
   bool use_coded = true;           // PP2_TUNE_CODED_MODEL
   void* staging = nullptr;     // dense host-layout staging buffer
   size_t staging_bytes = 0;

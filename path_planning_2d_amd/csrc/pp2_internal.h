@@ -150,6 +150,9 @@ constexpr int kSupN[9] = {4, 4, 4, 4, 1, 4, 4, 4, 4};
 constexpr int kSup[9][4] = {{0, 1, 3, 4}, {0, 1, 2, 4}, {1, 2, 4, 5}, {0, 3, 4, 6}, {4, 0, 0, 0},
                             {2, 4, 5, 8}, {3, 4, 6, 7}, {4, 6, 7, 8}, {4, 5, 7, 8}};
 size_t coded_loop_lds_bytes(int entries, bool sparse);
+// Opt kernel `fn` into kDictLdsMaxBytes of dynamic LDS on the current device,
+// once per device (bit d of `done`).
+void allow_lds(const void* fn, unsigned long long& done);
 hipError_t launch_dict_hash(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
                             PlaneSet L, uint64_t* out);
 hipError_t launch_dict_gather(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
@@ -168,8 +171,10 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
                                   const float* J_in, float* J_out, uint8_t* A, int own0,
                                   int own1, float scale = 1.0f);
 // Two fused loop steps in one launch (pp2_coded.hip, sparse rows,
-// unsharded): step 1 (u1, L_z1 column lz1, T_u1 table tu1) divides by
-// *in_sum (if given) times scale, step 2 (u2, lz2, tu2) by 1.  Reads b_in /
+// unsharded): step 1 (u1, L_z1 column lz1, T_u1 table tu1) divides by the
+// input mass times scale, step 2 (u2, lz2, tu2) by 1.  The input mass is the
+// reduction of in_n pending partials in_partials (k_sum_finalize's tree,
+// also stored to *in_sum_out when given), else *in_sum, else 1.  Reads b_in /
 // J_in, writes b_out / J_out / A and step 2's mass partials.  Returns
 // hipErrorInvalidValue when loop_pair_fits is false.
 constexpr int kPlaneGuard = 64;  // floats of guard before/after every plane allocation
@@ -179,7 +184,8 @@ hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
                                   const float* lz2, const float* tu1, const float* tu2,
                                   int entries, int u1, int u2, const float* b_in, float* b_out,
                                   const float* J_in, float* J_out, uint8_t* A,
-                                  float* out_partials, const float* in_sum, float scale);
+                                  float* out_partials, const float* in_partials, int in_n,
+                                  float* in_sum_out, const float* in_sum, float scale);
 hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int entries,
                                   bool sparse, const float* J_in, float* J_out, uint8_t* A);

@@ -33,7 +33,6 @@
 // Per cell the arithmetic is the dense update's: p = sum_s fmaf(T, b, p) in
 // ascending stencil order s, then p * fl(L_z / max).  The coded and dense
 // model sources give bit-identical beliefs and statistics.
-#include <stdlib.h>
 
 #include <type_traits>
 
@@ -458,23 +457,14 @@ int band_nseg(const Geom& g) { return (g.wp + kSegCells - 1) / kSegCells; }
 int band_nband(const Geom& g) { return (g.rows + kBandRows - 1) / kBandRows; }
 int band_gx(const Geom& g) { return (band_nseg(g) * band_nband(g) + 3) / 4; }
 
-// (copies per chunk, ring slots, waves per SIMD) variants of
-// k_rollout_band; PP2_ROLLOUT_VARIANT selects one for A/B runs
-struct BandVariant { int ch, ns, wps; };
-// (MI355X, 512^2 x 4096 copies x 5 steps: 6.01 / 6.21 / 6.25 / 6.36 / 6.20 ms)
-constexpr BandVariant kBandVariants[] = {{4, 4, 2}, {4, 3, 2}, {2, 4, 3}, {8, 3, 1}, {4, 4, 3}};
-int roll_variant() {
-  static const int v = [] {
-    const char* e = getenv("PP2_ROLLOUT_VARIANT");
-    const int i = e ? atoi(e) : 0;
-    return i >= 0 && i < (int)(sizeof(kBandVariants) / sizeof(kBandVariants[0])) ? i : 0;
-  }();
-  return v;
-}
+// Band shape: 4 copies per chunk, 4 LDS ring slots, 2 waves per SIMD.  The
+// other shapes measured (MI355X, 512^2 x 4096 copies x 5 steps): (4,4,2) 6.01
+// ms, (4,3,2) 6.21, (2,4,3) 6.25, (8,3,1) 6.36, (4,4,3) 6.20.
+constexpr int kBandCopies = 4, kBandSlots = 4, kBandWaves = 2;
 
 }  // namespace
 
-int rollout_chunk() { return kBandVariants[roll_variant()].ch; }
+int rollout_chunk() { return kBandCopies; }
 int rollout_min_chunk() { return 2; }
 int rollout_step_waves(const Geom& g) { return band_gx(g) * 4; }
 
@@ -504,16 +494,10 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
   const size_t lds = E > 0 ? (size_t)(((E * tw + 3) & ~3) + CH * E) * sizeof(float) : 0;
 #define PP2_BAND(CC, PP, WW)                                                                 \
   do {                                                                                       \
-    static bool attr = false;                                                                \
-    if (!attr) {                                                                             \
-      for (const void* fn : {reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kSparse>), \
-                             reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kFull>),   \
-                             reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kDense>)}) \
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,           \
-                                  (int)kDictLdsMaxBytes);                                    \
-      (void)hipGetLastError();                                                               \
-      attr = true;                                                                           \
-    }                                                                                        \
+    static unsigned long long attr[3] = {0, 0, 0};                                           \
+    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kSparse>), attr[0]); \
+    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kFull>), attr[1]);   \
+    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kDense>), attr[2]);  \
     if (src == kSparse)                                                                      \
       hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kSparse>), dim3((unsigned)nblocks),     \
                          dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,     \
@@ -528,13 +512,7 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
                          nband, chunk_u, chunk_first, copies, zs, in_stats);                 \
   } while (0)
   const int src = E <= 0 ? kDense : sparse ? kSparse : kFull;
-  switch (roll_variant()) {
-    case 1: PP2_BAND(4, 3, 2); break;
-    case 2: PP2_BAND(2, 4, 3); break;
-    case 3: PP2_BAND(8, 3, 1); break;
-    case 4: PP2_BAND(4, 4, 3); break;
-    default: PP2_BAND(4, 4, 2); break;
-  }
+  PP2_BAND(kBandCopies, kBandSlots, kBandWaves);
 #undef PP2_BAND
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

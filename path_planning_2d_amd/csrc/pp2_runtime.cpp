@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -307,7 +308,16 @@ std::string join(const char* dir, const char* name) {
   return d + name;
 }
 
-bool coded_active(const pp2_ctx* c) { return c->use_coded && c->dict_n > 0 && c->cpt == 4; }
+bool coded_active(const pp2_ctx* c) {
+  return c->use_coded && c->dict_n > 0 && c->cpt == 4 && (!c->dict_sparse || c->belief_sparse_ok);
+}
+
+// +0 <= v < +inf (sign bit clear, not inf or NaN)
+static bool finite_nonneg(float v) {
+  uint32_t bits;
+  std::memcpy(&bits, &v, 4);
+  return bits < 0x7f800000u;
+}
 
 // Dictionary of the distinct per-cell model tuples (T, C, L) over rows
 // [-1, rows]: GPU hash per cell, first-appearance numbering on the host, GPU
@@ -386,7 +396,21 @@ int build_model_dict(pp2_ctx* c) {
   if (bad) return PP2_OK;
   // LDS-layout rows: sparse when every T entry off the base-kernel support is
   // +0.0 (always so for generated models), else the full [a][T..,C] rows
-  bool sparse = true;
+  // They also drop the T == 0 terms of the Bellman backup, which equals the
+  // dense fmaf chain only while every partial cost stays finite and never -0:
+  // every dictionary C finite and >= +0 (J then starts at +0 and stays finite
+  // below max C / (1 - gamma)), 0 <= gamma < 1.  Otherwise the full rows
+  // (no term dropped) keep coded == dense bit for bit.
+  const float gam = c->gamma;
+  bool sparse = gam >= 0.0f && gam < 1.0f;
+  double cmax = 0.0;
+  for (int e = 0; e < E && sparse; ++e)
+    for (int a = 0; a < 9; ++a) {
+      const float cv = dh[(size_t)e * pp2::kDictRow + a * 10 + 9];
+      if (!finite_nonneg(cv)) { sparse = false; break; }
+      cmax = std::max(cmax, (double)cv);
+    }
+  if (sparse && cmax / (1.0 - (double)gam) >= 0.5 * (double)FLT_MAX) sparse = false;
   for (int e = 0; e < E && sparse; ++e)
     for (int a = 0; a < 9 && sparse; ++a)
       for (int i = 0; i < 9; ++i) {
@@ -402,7 +426,6 @@ int build_model_dict(pp2_ctx* c) {
   std::vector<float> rows((size_t)E * rw + 4, 0.0f), dl((size_t)16 * es, 0.0f);
   const size_t tstride = ((size_t)E * tw + 3) & ~(size_t)3;  // 16-B aligned per action
   std::vector<float> tu(9 * tstride, 0.0f);
-  const float gam = c->gamma;
   for (int e = 0; e < E; ++e) {
     const float* src = &dh[(size_t)e * pp2::kDictRow];
     float* dst = &rows[(size_t)e * rw];
@@ -584,14 +607,17 @@ static int blocked_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   const int depth = shard ? c->kdepth : c->norm_block;
   const int bc = c->bcur, bn = bc ^ 1, jn = c->jcur ^ 1;
   const bool start = c->kstep == 0;
-  if (start) {
+  // unsharded coded context: a pending mass is reduced inside the block-start
+  // launch (stored to bsum[bc]) instead of by a separate k_sum_finalize
+  const bool fold = start && !shard && c->pending[bc] && coded_active(c);
+  if (start && !fold) {
     CHECK(ensure_mass(c));
     if (shard) CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, depth));
   }
   int nparts = 0;
-  CHECK(loop_launch(c, shard ? depth - 1 - c->kstep : 0, u, z, nullptr, 0,
-                    start ? c->bsum + bc : nullptr, nullptr, &nparts,
-                    start ? kBlockScale : 1.0f));
+  CHECK(loop_launch(c, shard ? depth - 1 - c->kstep : 0, u, z, fold ? c->pbuf[bc] : nullptr,
+                    fold ? c->pcount[bc] : 0, start && !fold ? c->bsum + bc : nullptr,
+                    fold ? c->bsum + bc : nullptr, &nparts, start ? kBlockScale : 1.0f));
   c->pending[bc] = false;
   c->pcount[bn] = nparts;
   c->pending[bn] = true;
@@ -618,14 +644,17 @@ static int loop_pair(pp2_ctx* c, uint8_t u1, uint8_t z1, uint8_t u2, uint8_t z2)
   }
   const int bc = c->bcur, bn = bc ^ 1, jc = c->jcur;
   const bool start = c->kstep == 0;
-  if (start) CHECK(ensure_mass(c));
+  // a block start with the mass still pending reduces it inside the launch
+  // (and stores it to bsum[bc]) instead of a separate k_sum_finalize
+  const bool fold = start && c->pending[bc];
   const size_t es = (size_t)((c->dict_n + 3) & ~3);
   const size_t ts = ((size_t)c->dict_n * pp2::tu_width(true) + 3) & ~(size_t)3;
   HIPCHK(pp2::launch_loop_pair_coded(
       c->stream, c->g, c->gamma, c->d_code, c->d_rows, c->d_dl + z1 * es, c->d_dl + z2 * es,
       c->d_tu + u1 * ts, c->d_tu + u2 * ts, c->dict_n, u1, u2, c->b[bc].v.p, c->b[bn].v.p,
-      c->J[jc].v.p, c->J[jc ^ 1].v.p, c->A, c->pbuf[bn], start ? c->bsum + bc : nullptr,
-      start ? kBlockScale : 1.0f));
+      c->J[jc].v.p, c->J[jc ^ 1].v.p, c->A, c->pbuf[bn], fold ? c->pbuf[bc] : nullptr,
+      fold ? c->pcount[bc] : 0, fold ? c->bsum + bc : nullptr,
+      start && !fold ? c->bsum + bc : nullptr, start ? kBlockScale : 1.0f));
   c->pending[bc] = false;
   c->pcount[bn] = pp2::mass_partials(c->g, 4);
   c->pending[bn] = true;
@@ -837,6 +866,9 @@ int pp2_belief_set(pp2_ctx* c, const float* b) {
   DeviceGuard dg(c->device);
   break_pipeline(c);
   CHECK(upload_planes(c, c->b[c->bcur], b));
+  bool ok = true;
+  for (size_t i = 0; i < (size_t)c->g.rows * c->g.width && ok; ++i) ok = finite_nonneg(b[i]);
+  c->belief_sparse_ok = ok;
   c->pending[c->bcur] = false;
   const float one = 1.0f;
   HIPCHK(hipMemcpyAsync(c->bsum + c->bcur, &one, sizeof one, hipMemcpyHostToDevice, c->stream));

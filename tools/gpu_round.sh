@@ -8,10 +8,10 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
 STEP=${1:-all}
-run_tests() { timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1; }
+run_tests() { timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1; }
 run_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; }
-run_bench() { timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err; }
-run_prof()  { timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --profile --steps 100 --warmup 10 > $OUT/prof.log 2>&1; }
+run_bench() { timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; }
+run_prof()  { timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --profile --steps 100 --warmup 10 > $OUT/prof.log 2>&1; }
 case $STEP in
   all)   run_tests && run_smoke && run_bench && run_prof ;;
   tests) run_tests ;;
