@@ -1,5 +1,5 @@
 // MdpPathPlanning2d on libpp2_hip.so: replaces src/mdp/path_planning_2d.cu of
-// the reference (class body :60-487) in the catkin package.  Header
+// the reference (class body :59-487) in the catkin package.  Header
 // (include/path_planning_2d/mdp_path_planning_2d.h), node main, launch files,
 // parameters and topics are unchanged.  The model and value iteration run in
 // one pp2_ctx; valueIteration keeps the reference's stopping rule (blocks of

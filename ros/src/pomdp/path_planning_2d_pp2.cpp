@@ -1,5 +1,5 @@
 // PomdpPathPlanning2d on libpp2_hip.so: replaces src/pomdp/path_planning_2d.cu
-// of the reference (class body :44-283) in the catkin package.  The node
+// of the reference (class body :61-282) in the catkin package.  The node
 // main (src/pomdp/path_planning_2d_node.cpp), launch files, parameters,
 // topics ("belief" in, "control" out) and services ("save_data",
 // "reset_search_tree") are unchanged; every CUDA call is a pp2.h call.
