@@ -277,13 +277,26 @@ def plan_step_bench(args, device, stream_handle, with_cpu):
         pl.reset()
         ms = run(pl.step, args.plan_steps, 1e9)
         info = pl.info()
+    # reference_order: the same plan steps with every grid-wide sum as the
+    # reference's x-ordered fp32 chain (bit-exact with its arithmetic)
+    with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
+                         max_online_iteration=15, reference_order=1) as pl:
+        run(pl.step, 2, 1e9)
+        pl.reset()
+        ms_ref = run(pl.step, min(args.plan_steps, 50), 1e9)
     ctx.close()
     out = {"config": f"{N}x{N} synthetic grid, max_search_tree_depth {args.plan_depth}, "
                      f"max_online_iteration 15, FIB upper bound ({fib_sweeps} sweeps, "
                      f"{fib_s * 1e3:.1f} ms on GPU), lower bound -5/(1-gamma)",
            "steps": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
            "p90_ms": float(np.percentile(ms, 90)), "mean_ms": float(ms.mean()),
-           "first_ms": float(ms[0]), "final_tree_vnodes": int(info["total_vnodes"])}
+           "first_ms": float(ms[0]), "final_tree_vnodes": int(info["total_vnodes"]),
+           "reference_order": {"steps": int(ms_ref.size),
+                               "p50_ms": float(np.percentile(ms_ref, 50)),
+                               "p90_ms": float(np.percentile(ms_ref, 90)),
+                               "note": "planner reference_order=1: rewards, renormalisations "
+                                       "and leaf bounds as x-ordered fp32 chains, bit-exact "
+                                       "with the reference arithmetic"}}
     if with_cpu:
         from oracle import oracle as O
         T, L, R = O.model_pomdp(grid, goal)

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PP2_ABI_VERSION 1
+#define PP2_ABI_VERSION 2
 
 typedef enum {
   PP2_OK = 0,
@@ -287,6 +287,23 @@ typedef struct {
   uint64_t rand_skip;             /* rand() draws already taken from the stream
                                      (the reference's generateBeliefSet runs
                                      first: pp2_pbvi_solve's *rand_calls) */
+  int32_t reference_order;        /* 0 (default): grid-wide sums as parallel
+                                     trees (fp64 where the reference's fp32
+                                     chains lose digits); 1: every sum the
+                                     reference runs on its host -- the QNode
+                                     reward inner_product and the child
+                                     renormalisation accumulate
+                                     (search_tree_cuda.cu:168-173, :225-229),
+                                     evaluateFibCpu / evaluatePbviCpu
+                                     (fast_informed_bound_cuda.cu:278-297,
+                                     point_based_value_iteration_cuda.cu:
+                                     678-699) -- as one x-ordered fp32 chain
+                                     on the device (multiply, then add; IEEE
+                                     division), so bounds, rewards, weights
+                                     and the tree equal the reference's
+                                     arithmetic bit for bit.  Slower: each
+                                     expansion is a few dependent chains of
+                                     H*W adds. */
 } pp2_planner_params;
 
 /* Snapshot of the root and its children, for inspection and parity tests. */

@@ -131,6 +131,17 @@ struct pp2_planner {
   int* d_srow = nullptr;
   uint8_t *d_us = nullptr, *d_zs = nullptr;
 
+  // reference_order: node beliefs are stored normalised (mass 1) exactly as
+  // the reference's host normalises them, and every grid-wide sum is one
+  // x-ordered fp32 chain (pp2_pbvi_host.hip k_rows_chain / k_pair_chain).
+  bool ref = false;
+  int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
+  float* d_rrows = nullptr;     // [9][ld] R[.][a]
+  float* d_frows = nullptr;     // [9][ld] FIB alphas[.][i]
+  float* d_rsum = nullptr;      // [256] row sums
+  float* d_rout = nullptr;      // [9 rewards | 256 x 9 FIB dots]
+  float* h_rout = nullptr;      // pinned mirror of d_rout
+
   VNode* root = nullptr;
   uint32_t n_vnodes = 0, n_qnodes = 0, expansions = 0;
 };
@@ -278,6 +289,69 @@ void vnode_update(VNode* v) {
     }
 }
 
+// ---------------------------------------------------------------- reference order
+constexpr int kRefOutFloats = 9 + 256 * 9;
+
+// K planes of `src` -> K dense rows of p->ref_ld floats (zero tails stay 0).
+int pack_rows(pp2_planner* p, pp2::PlaneSet src, int K, float* dst) {
+  pp2_ctx* c = p->ctx;
+  for (int k = 0; k < K; ++k) {
+    pp2::PlaneSet v = src;
+    v.p += (long long)k * src.ps;
+    HIPCHK(pp2::launch_pack(c->stream, c->g, 1, v, dst + (size_t)k * p->ref_ld, nullptr));
+  }
+  return PP2_OK;
+}
+
+// Normalise the raw belief in slot s as the reference's host does
+// (search_tree_cuda.cu:225-229): sum = accumulate(b) in x order, then
+// b[x] /= sum (IEEE); the slot's mass becomes 1.
+int ref_normalize_slot(pp2_planner* p, int s) {
+  pp2_ctx* c = p->ctx;
+  const Slot& sl = p->slots[s];
+  const int n = (int)p->n, ld = p->ref_ld;
+  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
+  HIPCHK(pp2::launch_rows_seq(c->stream, pp2::ROW_SUM, p->d_parent, ld, 1, n, p->d_rsum,
+                              nullptr));
+  HIPCHK(pp2::launch_rows_div(c->stream, p->d_parent, ld, 1, n, p->d_rsum));
+  HIPCHK(pp2::launch_unpack(c->stream, c->g, 1, p->d_parent, sl.b.v));
+  const float one = 1.0f;
+  HIPCHK(hipMemcpyAsync(sl.mass, &one, sizeof one, hipMemcpyHostToDevice, c->stream));
+  return PP2_OK;
+}
+
+// evaluateFibCpu (first maximum of the 9 x-ordered dots) and evaluatePbviCpu
+// (first maximum over the alphas) of `rows` dense normalised beliefs: FIB dots
+// into d_rout[9 + 9 r + i], PBVI maxima into h_lbv[r].  Asynchronous.
+int ref_leaf_bounds(pp2_planner* p, const float* d_rows, int rows) {
+  pp2_ctx* c = p->ctx;
+  const int n = (int)p->n, ld = p->ref_ld;
+  CHECK(pack_rows(p, c->fib[c->fcur].v, 9, p->d_frows));
+  HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, p->d_frows, 9, ld, n,
+                                p->d_rout + 9, 9));
+  if (p->pbvi) {
+    const float* al = nullptr;
+    int S = 0, Sp = 0, ald = 0;
+    CHECK(pbvi_alphas(c, &al, &S, &Sp, &ald));
+    if (S != p->lb_S || ald != ld)
+      return set_err(PP2_ESTATE, "PBVI alpha vectors changed size since the planner was created");
+    HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, al, S, ld, n,
+                                  p->d_lbdots, S));
+    HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, rows, S, S, p->d_lbidx, p->d_lbv));
+    HIPCHK(hipMemcpyAsync(p->h_lbv, p->d_lbv, rows * sizeof(float), hipMemcpyDeviceToHost,
+                          c->stream));
+  }
+  return PP2_OK;
+}
+
+// std::max_element of evaluateFibCpu's 9 values (first maximum).
+float first_max9(const float* v) {
+  float best = v[0];
+  for (int i = 1; i < 9; ++i)
+    if (best < v[i]) best = v[i];
+  return best;
+}
+
 // Device copy of a VNode's belief, recomputed from its parent VNode's
 // (always materialised: it was expanded) as the QNode constructor's update:
 // cudaBayesBeliefUpdate + renormalisation (search_tree_cuda.cu:213-231).
@@ -298,6 +372,7 @@ int materialize(pp2_planner* p, VNode* v) {
   HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
                                   ns.mass));
   v->slot = s;
+  if (p->ref) CHECK(ref_normalize_slot(p, s));
   return PP2_OK;
 }
 
@@ -306,6 +381,21 @@ int materialize(pp2_planner* p, VNode* v) {
 int make_root(pp2_planner* p, int s, uint8_t z, VNode** out) {
   pp2_ctx* c = p->ctx;
   const Slot& sl = p->slots[s];
+  if (p->ref) {
+    // the slot holds the normalised belief (mass 1)
+    HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
+    CHECK(ref_leaf_bounds(p, p->d_parent, 1));
+    HIPCHK(hipMemcpyAsync(p->h_rout + 9, p->d_rout + 9, 9 * sizeof(float),
+                          hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    VNode* v = new_vnode(p, z, 0.0f, nullptr);
+    v->slot = s;
+    v->upper_bound = first_max9(p->h_rout + 9);
+    v->lower_bound = p->pbvi ? p->h_lbv[0] : p->lb_const;
+    v->heuristic = v->upper_bound - v->lower_bound;
+    *out = v;
+    return PP2_OK;
+  }
   HIPCHK(pp2::launch_belief_dots(c->stream, c->g, c->cpt, sl.b.v.p, c->fib[c->fcur].v,
                                  p->d_bpart, p->d_out + kOutDots));
   HIPCHK(hipMemcpyAsync(p->d_out + kOutMass, sl.mass, sizeof(float),
@@ -377,7 +467,10 @@ void sample_observations(pp2_planner* p, const std::vector<float>& cdf, uint8_t 
 
 // VNode::expand (search_tree_cuda.cu:437-450) with the 9 QNode constructors
 // (:161-242) batched.
+int expand_vnode_ref(pp2_planner* p, VNode* v);
+
 int expand_vnode(pp2_planner* p, VNode* v) {
+  if (p->ref) return expand_vnode_ref(p, v);
   pp2_ctx* c = p->ctx;
   CHECK(materialize(p, v));
   const Slot& sl = p->slots[v->slot];
@@ -442,6 +535,71 @@ int expand_vnode(pp2_planner* p, VNode* v) {
   return PP2_OK;
 }
 
+// VNode::expand in reference order: the 9 QNode rewards are inner_product(b,
+// R[.][a]) chains; the 144 children are cudaBayesBeliefUpdate of b
+// (k_pbvi_update), each renormalised by its own accumulate chain and IEEE
+// division; their FIB / PBVI bounds are evaluateFibCpu / evaluatePbviCpu
+// chains.  Only the children the samples select are kept, as in the
+// reference; they are re-derived (materialize) when expanded.
+int expand_vnode_ref(pp2_planner* p, VNode* v) {
+  pp2_ctx* c = p->ctx;
+  CHECK(materialize(p, v));
+  const Slot& sl = p->slots[v->slot];
+  const size_t n = p->n;
+  const int ld = p->ref_ld;
+  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
+  HIPCHK(hipMemcpyAsync(p->h_belief, p->d_parent, n * sizeof(float), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipEventRecord(p->ev_belief, c->stream));
+  HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, p->d_parent, 1, p->d_rrows, 9, ld,
+                                (int)n, p->d_rout, 9));
+  HIPCHK(pp2::launch_pbvi_update(c->stream, c->g, c->T.v, c->L.v, p->d_parent, ld, p->d_srow,
+                                 p->d_us, p->d_zs, 144, p->d_children));
+  HIPCHK(pp2::launch_rows_seq(c->stream, pp2::ROW_SUM, p->d_children, ld, 144, (int)n,
+                              p->d_rsum, nullptr));
+  HIPCHK(pp2::launch_rows_div(c->stream, p->d_children, ld, 144, (int)n, p->d_rsum));
+  CHECK(ref_leaf_bounds(p, p->d_children, 144));
+  HIPCHK(hipMemcpyAsync(p->h_rout, p->d_rout, kRefOutFloats * sizeof(float),
+                        hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipEventSynchronize(p->ev_belief));
+
+  std::vector<float> cdf(n);
+  float acc = 0.0f;
+  for (size_t i = 0; i < n; ++i) {
+    acc = acc + p->h_belief[i];
+    cdf[i] = acc;
+  }
+  std::vector<uint8_t> zs[9];
+  std::vector<float> fq[9];
+  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, cdf, a, zs[a], fq[a]);
+  HIPCHK(hipStreamSynchronize(c->stream));
+
+  for (QNode* q : v->children)
+    if (q) delete_subtree(p, q);
+  v->children.assign(9, nullptr);
+  for (uint8_t a = 0; a < 9; ++a) {
+    QNode* q = new QNode();
+    ++p->n_qnodes;
+    q->action = a;
+    q->parent = v;
+    q->reward = p->h_rout[a];
+    for (size_t k = 0; k < zs[a].size(); ++k) {
+      const uint8_t z = zs[a][k];
+      const int row = z * 9 + a;
+      VNode* cv = new_vnode(p, z, fq[a][k], q);
+      cv->upper_bound = first_max9(p->h_rout + 9 + 9 * row);
+      cv->lower_bound = p->pbvi ? p->h_lbv[row] : p->lb_const;
+      cv->heuristic = cv->upper_bound - cv->lower_bound;
+      q->children.push_back(cv);
+    }
+    qnode_update(p, q);
+    v->children[a] = q;
+  }
+  vnode_update(v);
+  ++p->expansions;
+  return PP2_OK;
+}
+
 // SearchTree::expand (search_tree_cuda.cu:490-508)
 int tree_expand(pp2_planner* p) {
   VNode* vte = p->root->vnode_to_expand;
@@ -495,6 +653,7 @@ int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
                                    ns.b.v.p, a, z, os.mass, p->d_bpart));
   HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
                                   ns.mass));
+  if (p->ref) CHECK(ref_normalize_slot(p, s));
   VNode* nv = nullptr;
   CHECK(make_root(p, s, 0, &nv));
   if (root_q) delete_qnode_only(p, root_q);
@@ -516,6 +675,7 @@ int pp2_planner_default_params(pp2_planner_params* prm) {
   prm->rand_skip = 0;
   prm->sample_num = 50;
   prm->curand_seed = 1234;
+  prm->reference_order = 0;
   return PP2_OK;
 }
 
@@ -549,6 +709,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
     return set_err(PP2_ESTATE, "lower_bound_mode 1 needs PBVI alpha vectors (pp2_pbvi_solve "
                    "or pp2_pbvi_set)");
   if (prm->sample_num == 0) return set_err(PP2_EINVAL, "sample_num must be > 0");
+  if (prm->reference_order != 0 && prm->reference_order != 1)
+    return set_err(PP2_EINVAL, "reference_order must be 0 or 1");
   DeviceGuard dg(c->device);
   pp2_planner* p = new pp2_planner();
   p->ctx = c;
@@ -582,6 +744,11 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       hipHostMalloc(&p->h_belief, p->n * sizeof(float), hipHostMallocDefault) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_belief, hipEventDisableTiming) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "planner scratch allocation failed"));
+  p->ref = prm->reference_order == 1;
+  // dense rows of the children / PBVI / reference-order passes: the PBVI
+  // alphas' row length, else the cells rounded up to 64
+  const int row_ld = prm->lower_bound_mode == 1 ? pld : (int)((p->n + 63) / 64 * 64);
+  p->ref_ld = row_ld;
   if (prm->lower_bound_mode == 1) {
     p->pbvi = true;
     p->lb_S = pS;
@@ -616,6 +783,41 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         hipStreamSynchronize(c->stream) != hipSuccess)
       return fail(set_err(PP2_EHIP, "planner PBVI scratch initialisation failed"));
   }
+  if (p->ref) {
+    const size_t rows = (size_t)256 * row_ld;
+    if ((!p->d_parent && hipMalloc(&p->d_parent, (size_t)row_ld * sizeof(float)) != hipSuccess) ||
+        (!p->d_children && hipMalloc(&p->d_children, rows * sizeof(float)) != hipSuccess) ||
+        (!p->d_srow && hipMalloc(&p->d_srow, 144 * sizeof(int)) != hipSuccess) ||
+        (!p->d_us && hipMalloc(&p->d_us, 144) != hipSuccess) ||
+        (!p->d_zs && hipMalloc(&p->d_zs, 144) != hipSuccess) ||
+        hipMalloc(&p->d_rrows, (size_t)9 * row_ld * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_frows, (size_t)9 * row_ld * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_rsum, 256 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_rout, kRefOutFloats * sizeof(float)) != hipSuccess ||
+        hipHostMalloc(&p->h_rout, kRefOutFloats * sizeof(float), hipHostMallocDefault) !=
+            hipSuccess)
+      return fail(set_err(PP2_ENOMEM, "planner reference-order scratch allocation failed"));
+    std::vector<int> srow(144, 0);
+    std::vector<uint8_t> us(144), zs(144);
+    for (int k = 0; k < 144; ++k) {
+      us[k] = (uint8_t)(k % 9);
+      zs[k] = (uint8_t)(k / 9);
+    }
+    if (hipMemsetAsync(p->d_parent, 0, (size_t)row_ld * sizeof(float), c->stream) != hipSuccess ||
+        hipMemsetAsync(p->d_children, 0, rows * sizeof(float), c->stream) != hipSuccess ||
+        hipMemsetAsync(p->d_rrows, 0, (size_t)9 * row_ld * sizeof(float), c->stream) !=
+            hipSuccess ||
+        hipMemsetAsync(p->d_frows, 0, (size_t)9 * row_ld * sizeof(float), c->stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(p->d_srow, srow.data(), 144 * sizeof(int), hipMemcpyHostToDevice,
+                       c->stream) != hipSuccess ||
+        hipMemcpyAsync(p->d_us, us.data(), 144, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(p->d_zs, zs.data(), 144, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+      return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
+    if ((s = pack_rows(p, c->R.v, 9, p->d_rrows))) return fail(s);
+    if (hipStreamSynchronize(c->stream) != hipSuccess)
+      return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
+  }
   *out = p;
   return PP2_OK;
 }
@@ -638,8 +840,10 @@ int pp2_planner_destroy(pp2_planner* p) {
   }
   free_planes(&p->P);
   for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_out, p->d_dense, p->d_parent,
-                   p->d_children, p->d_lbpart, p->d_lbdots, p->d_lbv})
+                   p->d_children, p->d_lbpart, p->d_lbdots, p->d_lbv, p->d_rrows, p->d_frows,
+                   p->d_rsum, p->d_rout})
     if (d) (void)hipFree(d);
+  if (p->h_rout) (void)hipHostFree(p->h_rout);
   for (void* d : {(void*)p->d_lbidx, (void*)p->d_srow, (void*)p->d_us, (void*)p->d_zs})
     if (d) (void)hipFree(d);
   if (p->h_lbv) (void)hipHostFree(p->h_lbv);

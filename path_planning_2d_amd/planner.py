@@ -22,7 +22,8 @@ class PlannerParams(C.Structure):
                 ("rand_seed", C.c_uint32),
                 ("sample_num", C.c_uint32),
                 ("curand_seed", C.c_uint64),
-                ("rand_skip", C.c_uint64)]
+                ("rand_skip", C.c_uint64),
+                ("reference_order", C.c_int32)]
 
 
 class TreeInfo(C.Structure):

@@ -10,10 +10,11 @@ whole grid: against the oracle in fp64-accumulation mode they must agree to
 rel 1e-5 at every step (and the trees stay identical).  Against the
 reference-arithmetic oracle (sequential fp32 sums, whose own error is
 ~sqrt(hw)*eps*|value|) the fresh, shallow (<= 2 expansions) tree of the
-first step must have the same shape and values within rel 1e-4; deeper trees
-and later steps are not compared with it, since
-that fp32 noise alone can flip a near-tied expansion choice and the two trees
-then legitimately grow apart."""
+first step must have the same shape and values within rel 1e-4: that fp32
+noise alone can flip a near-tied expansion choice deeper in.  The planner's
+reference_order mode runs those sums as the reference's own x-ordered fp32
+chains, and is held to the reference-arithmetic oracle bit for bit at every
+step (test_planner_reference_order_bit_exact)."""
 import numpy as np
 import pytest
 
@@ -164,6 +165,95 @@ def test_planner_pbvi_lower_bound(oracle, name, S, max_depth, steps):
                 compare(gpl.info(), opl.info(), f"{name} pbvi step {k + 1}")
                 assert a_g == a_o and rel_close(v_g, v_o)
     opl.close()
+
+
+def compare_exact(gi, oi, where):
+    """Every field of the two tree snapshots equal (floats bit for bit)."""
+    for k in gi:
+        a, b = np.asarray(gi[k]), np.asarray(oi[k])
+        if a.dtype.kind == "f":
+            a32 = np.atleast_1d(a.astype(np.float32))
+            b32 = np.atleast_1d(b.astype(np.float32))
+            assert np.array_equal(a32.view(np.uint32), b32.view(np.uint32)), \
+                f"{where}: {k} {a} != {b}"
+        else:
+            assert np.array_equal(a, b), f"{where}: {k} {a} != {b}"
+
+
+@pytest.mark.parametrize("name,max_depth,lb,S,steps", [
+    ("map_10x10", 50, 0, 0, 8),
+    ("sparse_map_100x40", 50, 0, 0, 6),
+    ("sparse_map_100x40", 5, 1, 500, 5),    # the reference node: PBVI leaves, S = 500
+    ("tile64_sparse_map_100x40", 8, 1, 64, 6),
+])
+def test_planner_reference_order_bit_exact(oracle, name, max_depth, lb, S, steps):
+    """reference_order = 1: rewards, renormalisations and leaf bounds run as
+    the reference's own x-ordered fp32 chains (inner_product / accumulate,
+    search_tree_cuda.cu:168-173, :225-229; evaluateFibCpu, evaluatePbviCpu),
+    so the tree equals the reference-arithmetic oracle at EVERY plan step:
+    shape, observations, weights, bounds, rewards, heuristics bit for bit, and
+    the chosen action and its value exactly -- deep trees included, where the
+    fp64-accumulating mode may legitimately pick another near-tied node."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S_
+    grid = golden_map(name)
+    m = golden("model", name)
+    b0 = S_.uniform_belief(grid)
+    with P.GridContext(grid, tuple(m["goal"]), gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_solve()
+        alphas = ctx.fib_get()
+        calls = 0
+        rpl = oracle.Planner(grid, m["T"], m["L"], m["R"], alphas, max_depth=max_depth,
+                             max_iter=15)
+        if lb:
+            calls = ctx.pbvi_solve(b0, S)
+            pal, pact = ctx.pbvi_get()
+            rpl.set_pbvi(pal, pact)
+            rpl.skip_rand(calls)
+        with P.QVTreePlanner(ctx, max_search_tree_depth=max_depth, max_online_iteration=15,
+                             lower_bound_mode=lb, rand_skip=calls, reference_order=1) as gpl:
+            a_g, v_g = gpl.step(0, 0, b0)
+            a_r, v_r = rpl.step(0, 0, b0)
+            compare_exact(gpl.info(), rpl.info(), f"{name} ref step 0")
+            assert a_g == a_r and np.float32(v_g) == np.float32(v_r)
+            _, zs, _ = S_.synth_trajectory(grid, steps, seed=5)
+            for k in range(steps):
+                a_g, v_g = gpl.step(a_r, int(zs[k]))
+                a_r, v_r = rpl.step(a_r, int(zs[k]))
+                compare_exact(gpl.info(), rpl.info(), f"{name} ref step {k + 1}")
+                assert a_g == a_r, f"{name} step {k + 1}: action {a_g} != {a_r}"
+                assert np.float32(v_g) == np.float32(v_r)
+    rpl.close()
+
+
+def test_planner_reference_order_256(oracle):
+    """BASELINE configs[1] (256x256, max_search_tree_depth 3) in reference
+    order: bit-exact with the reference-arithmetic oracle at every step."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S_
+    grid = S_.synth_grid(256, 256, 256)
+    goal = S_.synth_goal(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_solve(max_sweeps=40)
+        alphas = ctx.fib_get()
+        T, L, R = oracle.model_pomdp(grid, goal)
+        rpl = oracle.Planner(grid, T, L, R, alphas, max_depth=3, max_iter=15)
+        with P.QVTreePlanner(ctx, max_search_tree_depth=3, max_online_iteration=15,
+                             reference_order=1) as gpl:
+            b0 = S_.uniform_belief(grid)
+            a_g, _ = gpl.step(0, 0, b0)
+            a_r, _ = rpl.step(0, 0, b0)
+            compare_exact(gpl.info(), rpl.info(), "256 ref step 0")
+            assert a_g == a_r
+            _, zs, _ = S_.synth_trajectory(grid, 3, seed=3)
+            for k in range(3):
+                a_g, _ = gpl.step(a_r, int(zs[k]))
+                a_r, _ = rpl.step(a_r, int(zs[k]))
+                compare_exact(gpl.info(), rpl.info(), f"256 ref step {k + 1}")
+                assert a_g == a_r
+        rpl.close()
 
 
 def test_planner_pbvi_needs_alphas():
