@@ -103,21 +103,21 @@ __global__ __launch_bounds__(kBlock) void k_dict_verify(Geom g, PlaneSet T, Plan
 }
 
 // ---------------------------------------------------------------- kernels
-// Two LDS row layouts per dictionary entry:
-//  * full   (kDictTC = 90 floats): [a][gT_a0..gT_a8, C_a];
-//  * sparse (kSpRow = 44 floats):  gT at kSup[a][0..3] per move action | gT_4, C[0..8] -- only
-//    the base-kernel support of each action (at most 4 cells; the host checks
-//    every other T entry of every row is +0.0 before choosing it).
+// Two LDS layouts of the sweep rows:
+//  * full     (kDictTC = 90 floats per entry): [a][gT_a0..gT_a8, C_a];
+//  * factored (sparse; pp2_internal.h): per-action tables of the distinct
+//    (gT support quad, C_a) pairs and one 16-B record of byte offsets per
+//    entry -- only the base-kernel support of each action (at most 4 cells;
+//    the host checks every other T entry of every row is +0.0).
 // gT = fl(gamma * T), rounded once on the host exactly as the dense sweep
 // rounds gamma * T per cell (one fp32 multiply, round to nearest).  The belief
-// gather reads raw T from a per-action table (tu: E x 4 sparse / E x 9 full).
-// Sparse Bellman rows skip the T == 0 terms: fmaf(gamma*0, J, cost) == cost
-// for the finite, non-negative J and cost of the MDP (J starts at 0, C >= 0),
-// so values and actions stay bit-identical to the dense kernel.
+// gather reads raw T from a per-action table (tu: E x 5 sparse / E x 9 full).
+// Sparse backups skip the T == 0 terms: fmaf(gamma*0, J, cost) == cost for
+// the finite, non-negative J and cost of the MDP (J starts at 0, C >= +0,
+// checked on the host), so values and actions stay bit-identical to the
+// dense kernel.
 template <bool SPARSE>
 struct Layout {
-  static constexpr int row = SPARSE ? kSpRow : kDictTC;
-  static constexpr int blk = SPARSE ? 4 : 10;  // floats per action block (sparse: T only)
   static constexpr int tu = tu_width(SPARSE);  // raw T_u floats per entry (belief gather)
 };
 
@@ -152,24 +152,28 @@ __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&
   for (int k = 0; k < 4; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
   if constexpr (SPARSE) {
     // cell-outer, fully unrolled (support positions index jn at compile
-    // time): a cell's 11 row quads are 11 ds_read_b128, the scheduling
-    // barrier keeps one cell's row live at a time.  Actions are still
-    // compared in ascending order, so best/arg are the dense kernel's.
+    // time): one IW record, then per action a quad from QT (a float for the
+    // one-cell stay support) and the cost from CT at the same byte offset.
+    // The scheduling barrier keeps one cell's loads live at a time.  Actions
+    // are compared in ascending order, so best/arg are the dense kernel's.
+    const char* qt = reinterpret_cast<const char*>(sTC + kFactQT);
+    const char* ct = reinterpret_cast<const char*>(sTC + kFactCT);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float* row = sTC + cc[k] * kSpRow;
-      const f4a q8 = *reinterpret_cast<const f4a*>(row + 32);
-      const f4a q9 = *reinterpret_cast<const f4a*>(row + 36);
-      const f4a q10 = *reinterpret_cast<const f4a*>(row + 40);
-      const float cst[9] = {q8[1], q8[2], q8[3], q9[0], q9[1], q9[2], q9[3], q10[0], q10[1]};
+      const uint4 iw = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * cc[k]);
 #pragma unroll
       for (int a = 0; a < 9; ++a) {
-        float tv[4] = {q8[0], 0.0f, 0.0f, 0.0f};
-        if (a != 4) {
-          const f4a t = *reinterpret_cast<const f4a*>(row + sp_t(a));
+        const uint32_t w = a < 4 ? iw.x : a < 8 ? iw.y : iw.z;
+        const uint32_t off = __builtin_amdgcn_ubfe(w, 8 * (a % 4), 8);
+        const int tab = a * kFactK * 16;  // byte offset of action a's table
+        float tv[4];
+        if (kSupN[a] == 1) {
+          tv[0] = *reinterpret_cast<const float*>(qt + tab + off);
+        } else {
+          const f4a t = *reinterpret_cast<const f4a*>(qt + tab + off);
           tv[0] = t[0]; tv[1] = t[1]; tv[2] = t[2]; tv[3] = t[3];
         }
-        float cost = cst[a];
+        float cost = *reinterpret_cast<const float*>(ct + tab + off);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);
@@ -382,7 +386,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   using LY = Layout<SPARSE>;
   extern __shared__ float lds[];
   float* sTC = lds;
-  float* sL = lds + lds_span(E * LY::row);
+  float* sL = lds + lds_span(rows_floats(E, SPARSE));
   float* sTu = sL + lds_span(E);
   PP2_PHASE(0);
   const int q = threadIdx.x / kQuarter, tq = threadIdx.x % kQuarter;
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
   Win6 bw;
   load_codes6(code, g.wp, y, x0, cw);
   load_win6(b_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, bw);
-  stage_rows(rows, E * LY::row, sTC);
+  stage_rows(rows, rows_floats(E, SPARSE), sTC);
   stage_rows(lz, E, sL);
   stage_rows(tu, E * LY::tu, sTu);
   // pending input mass: wave 0 reduces the partials (k_sum_finalize's tree)
@@ -479,14 +483,13 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
     Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
     int E, const float* __restrict__ J_in, float* __restrict__ J_out,
     uint8_t* __restrict__ A) {
-  using LY = Layout<SPARSE>;
   constexpr int NT = QPB * kQuarter;
   extern __shared__ float lds[];
   const int tpr = g.wp / 4;
   const long long nthreads = (long long)g.rows * tpr;
   const int ntiles = (int)((nthreads + NT - 1) / NT);
   int tile = xcd_remap(blockIdx.x, gridDim.x);
-  stage_rows(rows, E * LY::row, lds);
+  stage_rows(rows, rows_floats(E, SPARSE), lds);
   __syncthreads();
   for (; tile < ntiles; tile += gridDim.x) {
     const long long t = (long long)tile * NT + threadIdx.x;
@@ -575,9 +578,10 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
     int dense_blocks) {
   using LY = Layout<true>;
   extern __shared__ float lds[];
+  PP2_PHASE(0);
   const int nreg = pair_region(g.wp);
   float* sTC = lds;
-  float* sL1 = sTC + lds_span(E * LY::row);
+  float* sL1 = sTC + lds_span(rows_floats(E, true));
   float* sL2 = sL1 + lds_span(E);
   float* sT1 = sL2 + lds_span(E);
   float* sT2 = sT1 + lds_span(E * LY::tu);
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
   float* sS = sJ + lds_span(nreg);         // the input mass (block-start launch)
   const int q = threadIdx.x / kQuarter;
   const int ntiles = (dense_blocks + kPQ - 1) / kPQ;
-  stage_rows(rows, E * LY::row, sTC);
+  stage_rows(rows, rows_floats(E, true), sTC);
   stage_rows(lz1, E, sL1);
   stage_rows(lz2, E, sL2);
   stage_rows(tu1, E * LY::tu, sT1);
@@ -604,6 +608,7 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
   __syncthreads();
   const float inv0 = in_partials ? (1.0f / sS[0]) * scale0
                                  : in_sum ? (1.0f / *in_sum) * scale0 : scale0;
+  PP2_PHASE(1);
   for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
     const long long c0 = (long long)tile * kPTile;
     const long long r0 = c0 - g.wp - 4;  // flat cell of sB[0] / sJ[0] (a quad boundary)
@@ -627,8 +632,11 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
       }
       *reinterpret_cast<f4a*>(sB + 4 * qd) = f4a{p[0], p[1], p[2], p[3]};
       *reinterpret_cast<f4a*>(sJ + 4 * qd) = f4a{best[0], best[1], best[2], best[3]};
+      if (qd == threadIdx.x) PP2_PHASE(2);
     }
+    PP2_PHASE(3);
     __syncthreads();
+    PP2_PHASE(4);
     // ---- step 2 over the tile (k_loop_step_coded's lane -> cell mapping)
     const long long t_ = (long long)(kPQ * tile) * kQuarter + threadIdx.x;
     const int y = (int)(t_ / (g.wp / 4));
@@ -650,10 +658,12 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
       sweep_vals(sTC, gamma, cw, w, best, arg);
       store_ja<true>(J_out, A, off, best, arg);
     }
+    PP2_PHASE(5);
     const int d = kPQ * tile + q;
     if (d < dense_blocks) write_wave_partial(local, out_partials, d);
     __syncthreads();  // the region is rewritten by the next tile
   }
+  PP2_PHASE(6);
 }
 
 // Per-device launch facts: the CU count (grid caps, loop_pair_fits) and which
@@ -695,7 +705,7 @@ void allow_lds(const void* fn, unsigned long long& done) {
 }
 
 size_t coded_loop_lds_bytes(int E, bool sparse) {
-  return ((size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) + lds_span(E) +
+  return ((size_t)lds_span(rows_floats(E, sparse)) + lds_span(E) +
           lds_span(E * tu_width(sparse)) + 4) * sizeof(float);
 }
 
@@ -772,8 +782,8 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
 }
 
 size_t loop_pair_lds_bytes(int E, int wp) {
-  return ((size_t)lds_span(E * kSpRow) + 2 * lds_span(E) + 2 * lds_span(E * tu_width(true)) +
-          2 * lds_span(pair_region(wp)) + 4) * sizeof(float);
+  return ((size_t)lds_span(rows_floats(E, true)) + 2 * lds_span(E) +
+          2 * lds_span(E * tu_width(true)) + 2 * lds_span(pair_region(wp)) + 4) * sizeof(float);
 }
 
 bool loop_pair_fits(const Geom& g, int E, bool sparse) {
@@ -809,7 +819,7 @@ hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
 hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int E, bool sparse,
                                   const float* J_in, float* J_out, uint8_t* A) {
-  const size_t lds = (size_t)lds_span(E * (sparse ? kSpRow : kDictTC)) * sizeof(float);
+  const size_t lds = (size_t)lds_span(rows_floats(E, sparse)) * sizeof(float);
   const long long nthreads = (long long)g.rows * (g.wp / 4);
 // Plain stores: non-temporal ones measured slower here (1024^2: 8.8 -> 9.9 us).
 #define PP2_SWEEPC(SP, Q, MB)                                                                  \

@@ -97,7 +97,7 @@ struct pp2_ctx {
   uint16_t* code_alloc = nullptr;  // code plane allocation (guards + rows -1..rows)
   uint16_t* d_code = nullptr;      // code plane at (row 0, x 0)
   float* d_dict = nullptr;         // kDictMax * kDictRow floats
-  float* d_rows = nullptr;         // LDS-layout rows, gamma*T (sparse: kSpRow, else kDictTC)
+  float* d_rows = nullptr;         // LDS-layout rows, gamma*T (rows_floats: factored or kDictTC)
   float* d_dl = nullptr;           // L transposed: [z][entry]
   float* d_tu = nullptr;           // raw T per action: [u][entry][4 sparse | 9 full]
   int dict_n = 0;                  // entries; 0 = no dictionary (dense path only)

@@ -130,18 +130,27 @@ constexpr int kDictTuple = 106;  // floats compared per cell
 constexpr int kDictRow = 108;
 constexpr size_t kDictLdsMaxBytes = 160 * 1024;
 constexpr int kDictMax = 400;  // coded_loop_lds_bytes(kDictMax, false) <= kDictLdsMaxBytes
-// Sparse LDS rows: per action a, T at the base kernel's support kSup[a][0 ..
-// kSupN[a]) (base_kernel in pp2_kernels.hip; occupied neighbours and traps
-// only move mass to the centre, which is in every support), then C_a, then 0.
-// Sparse row (44 floats = 11 quads, an odd count so that two codes share a
-// bank quad only when they differ by a multiple of 16):
-//   quads 0..7 : gT at kSup[a][0..3] of the 8 move actions (a != 4), one 16-B
-//                quad each (ds_read_b128)
-//   quads 8..10: gT_4 (the stay action's single support), C[0..8], 0, 0 --
-//                the 9 costs and the stay term in three quads.
-constexpr int kSpRow = 44;
-constexpr int kSpC = 33;  // offset of C[0]
-__host__ __device__ constexpr int sp_t(int a) { return a < 4 ? 4 * a : a == 4 ? 32 : 4 * (a - 1); }
+// Factored sweep rows (the "sparse" layout; generated models always qualify).
+// Every T entry off action a's base-kernel support kSup[a][0 .. kSupN[a]) is
+// +0.0 (occupied neighbours and traps only move mass to the centre, which is
+// in every support), and across the dictionary action a takes at most kFactK
+// distinct (gT support quad, C_a) pairs -- 9 on generated models: the 8
+// occupancy patterns of its 3 non-centre support cells, and the goal.  The
+// LDS image is
+//   QT [9][kFactK] quads: gT = fl(gamma * T) at kSup[a][0..3] (zero-padded)
+//   CT [9][kFactK] x 4 floats: C_a of the pair at .x (16-B stride, so that
+//      one byte offset addresses both tables)
+//   IW [E] x 4 uint32: byte a of the 16 = 16 * (pair index of action a)
+// so a cell's backup reads one 16-B IW record, then per action one quad and
+// one cost from 256-B tables whose 16 entries sit on 16 distinct bank quads
+// (conflict-free gathers).  More than kFactK pairs for any action: full rows.
+constexpr int kFactK = 16;
+constexpr int kFactQT = 0;
+constexpr int kFactCT = 9 * kFactK * 4;
+constexpr int kFactIW = 2 * 9 * kFactK * 4;
+__host__ __device__ constexpr int rows_floats(int entries, bool sparse) {
+  return sparse ? kFactIW + 4 * entries : entries * kDictTC;
+}
 // Raw T_u floats per entry in the belief gather's LDS table: the support
 // cells (sparse, 4) or all 9, padded to an odd stride so that two codes land
 // on the same LDS bank only when they differ by a multiple of 64.
@@ -160,7 +169,7 @@ hipError_t launch_dict_gather(hipStream_t st, const Geom& g, PlaneSet T, PlaneSe
 hipError_t launch_dict_verify(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet C, PlaneSet R,
                               PlaneSet L, const uint16_t* code_all, const float* dict, int* bad);
 // code = code plane at (row 0, x 0); rows = LDS-layout dictionary rows (E x
-// kSpRow if sparse else E x kDictTC, T entries pre-multiplied by gamma); lz =
+// factored if sparse else E x kDictTC, T entries pre-multiplied by gamma); lz =
 // the L_z column (E floats); tu = raw T of action u per entry (E x 4 sparse,
 // E x 9 full).  Same contract as launch_loop_step (cpt 4).
 hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cfloat>
 #include <cerrno>
 #include <cmath>
@@ -420,22 +421,46 @@ int build_model_dict(pp2_ctx* c) {
         std::memcpy(&bits, &dh[(size_t)e * pp2::kDictRow + a * 10 + i], 4);
         if (!in && bits != 0) { sparse = false; break; }
       }
-  const int rw = sparse ? pp2::kSpRow : pp2::kDictTC;
+  // Factored sweep rows (pp2_internal.h): per action the distinct (gT support
+  // quad, C_a) pairs, at most kFactK of them, else the full rows.
+  std::vector<uint32_t> fact_iw((size_t)E * 4, 0u);
+  std::vector<float> fact_qt(9 * pp2::kFactK * 4, 0.0f), fact_ct(9 * pp2::kFactK * 4, 0.0f);
+  for (int a = 0; a < 9 && sparse; ++a) {
+    std::vector<std::array<uint32_t, 5>> pairs;
+    for (int e = 0; e < E && sparse; ++e) {
+      const float* src = &dh[(size_t)e * pp2::kDictRow];
+      float q[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int j = 0; j < pp2::kSupN[a]; ++j) q[j] = gam * src[a * 10 + pp2::kSup[a][j]];
+      std::array<uint32_t, 5> key;
+      std::memcpy(key.data(), q, 16);
+      std::memcpy(&key[4], &src[a * 10 + 9], 4);
+      size_t k = std::find(pairs.begin(), pairs.end(), key) - pairs.begin();
+      if (k == pairs.size()) {
+        if ((int)k >= pp2::kFactK) { sparse = false; break; }
+        pairs.push_back(key);
+        std::memcpy(&fact_qt[(a * pp2::kFactK + k) * 4], q, 16);
+        std::memcpy(&fact_ct[(a * pp2::kFactK + k) * 4], &key[4], 4);
+      }
+      fact_iw[(size_t)e * 4 + a / 4] |= (uint32_t)(16 * k) << (8 * (a % 4));
+    }
+  }
   const int tw = pp2::tu_width(sparse);
   const int es = (E + 3) & ~3;  // L_z column stride (16-B aligned columns)
-  std::vector<float> rows((size_t)E * rw + 4, 0.0f), dl((size_t)16 * es, 0.0f);
+  std::vector<float> rows((size_t)pp2::rows_floats(E, sparse) + 4, 0.0f),
+      dl((size_t)16 * es, 0.0f);
+  if (sparse) {
+    std::memcpy(&rows[pp2::kFactQT], fact_qt.data(), fact_qt.size() * sizeof(float));
+    std::memcpy(&rows[pp2::kFactCT], fact_ct.data(), fact_ct.size() * sizeof(float));
+    std::memcpy(&rows[pp2::kFactIW], fact_iw.data(), fact_iw.size() * sizeof(uint32_t));
+  }
   const size_t tstride = ((size_t)E * tw + 3) & ~(size_t)3;  // 16-B aligned per action
   std::vector<float> tu(9 * tstride, 0.0f);
   for (int e = 0; e < E; ++e) {
     const float* src = &dh[(size_t)e * pp2::kDictRow];
-    float* dst = &rows[(size_t)e * rw];
     for (int a = 0; a < 9; ++a) {
-      // sweep rows hold fl(gamma * T) (the dense sweep's per-cell product)
-      if (sparse) {
-        for (int j = 0; j < pp2::kSupN[a]; ++j)
-          dst[pp2::sp_t(a) + j] = gam * src[a * 10 + pp2::kSup[a][j]];
-        dst[pp2::kSpC + a] = src[a * 10 + 9];
-      } else {
+      // full sweep rows hold fl(gamma * T) (the dense sweep's per-cell product)
+      if (!sparse) {
+        float* dst = &rows[(size_t)e * pp2::kDictTC];
         for (int i = 0; i < 9; ++i) dst[a * 10 + i] = gam * src[a * 10 + i];
         dst[a * 10 + 9] = src[a * 10 + 9];
       }

@@ -22,6 +22,7 @@ def main():
         ctx.belief_set(S.uniform_belief(grid))
         ctx.mdp_reset()
         ctx.loop_run(us[:10], zs[:10])
+        print(f"N={N} steps/launch={ctx.loop_steps_per_launch()}", flush=True)
         for what in ("loop", "sweep"):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
