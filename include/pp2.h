@@ -110,10 +110,13 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           every k and by 1 in between (beliefs equal to
  *                           rounding; values and actions unchanged) */
 #define PP2_TUNE_NORM_BLOCK 6
-/*  PP2_TUNE_STEP_PAIRS      1 (default): pp2_loop_run on an unsharded context
- *                           with a sparse coded model runs two steps of a
- *                           normalisation block per launch (the first over
- *                           the tile plus a one-row halo, kept in LDS);
+/*  PP2_TUNE_STEP_PAIRS      1 (default): pp2_loop_run (and
+ *                           pp2_shard_group_loop_run) on a context with a
+ *                           sparse coded model runs two steps of a
+ *                           normalisation / halo block per launch (the first
+ *                           over the tile plus a one-row halo, kept in LDS)
+ *                           where the grid has a 4096-cell tile per CU;
+ *                           2 = pairs on any fitting grid (tests);
  *                           0 = one launch per step.  Results are
  *                           bit-identical either way. */
 #define PP2_TUNE_STEP_PAIRS 7
@@ -147,9 +150,9 @@ int pp2_model_load(pp2_ctx* ctx, const char* dir);
 int pp2_model_dict_info(pp2_ctx* ctx, int* entries, int* active);
 
 /* Loop steps pp2_loop_run fuses into one kernel launch on this context: 2
- * when it runs the steps of a normalisation block in pairs
- * (PP2_TUNE_STEP_PAIRS on an unsharded context with a sparse coded model
- * whose grid has a 4096-cell tile per CU), else 1. */
+ * when it runs the steps of a normalisation / halo block in pairs
+ * (PP2_TUNE_STEP_PAIRS with a sparse coded model whose grid has a 4096-cell
+ * tile per CU; unsharded, RCCL row shard or shard-group member), else 1. */
 int pp2_loop_steps_per_launch(pp2_ctx* ctx, int* steps);
 
 /* ---------------------------------------------------------------- belief
@@ -377,6 +380,9 @@ typedef struct pp2_shard_group pp2_shard_group;
 int pp2_shard_group_create(pp2_shard_group** out, pp2_ctx* const* ctxs, int n);
 int pp2_shard_group_destroy(pp2_shard_group* g);
 int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z);
+/* n loop steps (pp2_loop_run's contract): pairs of steps of a halo block per
+ * launch on every shard where PP2_TUNE_STEP_PAIRS applies, else single steps. */
+int pp2_shard_group_loop_run(pp2_shard_group* g, int n, const uint8_t* us, const uint8_t* zs);
 int pp2_shard_group_belief_update(pp2_shard_group* g, uint8_t u, uint8_t z);
 int pp2_shard_group_mdp_sweep(pp2_shard_group* g, int n);
 int pp2_shard_group_mdp_solve(pp2_shard_group* g, int max_sweeps, int* sweeps,

@@ -103,6 +103,7 @@ SIGNATURES = {
     "pp2_shard_group_create": [C.POINTER(_vp), C.POINTER(_vp), C.c_int],
     "pp2_shard_group_destroy": [_vp],
     "pp2_shard_group_loop_step": [_vp, C.c_uint8, C.c_uint8],
+    "pp2_shard_group_loop_run": [_vp, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)],
     "pp2_shard_group_belief_update": [_vp, C.c_uint8, C.c_uint8],
     "pp2_shard_group_mdp_sweep": [_vp, C.c_int],
     "pp2_shard_group_mdp_solve": [_vp, C.c_int, _i32p, _f64p],

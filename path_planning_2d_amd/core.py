@@ -369,6 +369,18 @@ class ShardGroup:
     def loop_step(self, u, z):
         call("pp2_shard_group_loop_step", self._h, int(u), int(z))
 
+    def loop_run(self, us, zs):
+        us = np.ascontiguousarray(us, np.uint8)
+        zs = np.ascontiguousarray(zs, np.uint8)
+        call("pp2_shard_group_loop_run", self._h, int(us.size), _u8(us), _u8(zs))
+
+    def set_tuning(self, key: int, value: int):
+        for s in self.shards:
+            s.set_tuning(key, value)
+
+    def loop_steps_per_launch(self):
+        return [s.loop_steps_per_launch() for s in self.shards]
+
     def belief_update(self, u, z):
         call("pp2_shard_group_belief_update", self._h, int(u), int(z))
 

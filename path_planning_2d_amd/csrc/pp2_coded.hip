@@ -522,6 +522,10 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
 // the arithmetic is k_loop_step_coded's; the intermediate belief, values and
 // actions are not stored (nobody reads them), the mass partials and actions
 // are step 2's, in the dense kernel's cell -> (block, wave) mapping.
+// Row shards launch it on a view extended by halo rows (pp2_runtime.cpp
+// loop_pair): step 1 then also covers view rows -1 and rows (s1lo/s1hi,
+// real neighbour rows read from the deep halo), and only the owned rows
+// [own0, own1) store actions and add to the mass.
 constexpr int kPQ = 4;                      // 256-thread quarters per workgroup
 constexpr int kPTile = kPQ * kQuarter * 4;  // cells per tile
 __host__ __device__ constexpr int pair_region(int wp) { return kPTile + 2 * wp + 8; }
@@ -575,7 +579,7 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
     float* __restrict__ b_out, const float* __restrict__ J_in, float* __restrict__ J_out,
     uint8_t* __restrict__ A, float* __restrict__ out_partials, const float* __restrict__ in_partials,
     int in_n, float* __restrict__ in_sum_out, const float* __restrict__ in_sum, float scale0,
-    int dense_blocks) {
+    int dense_blocks, int own0, int own1, int s1lo, int s1hi) {
   using LY = Layout<true>;
   extern __shared__ float lds[];
   PP2_PHASE(0);
@@ -612,13 +616,13 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
   for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
     const long long c0 = (long long)tile * kPTile;
     const long long r0 = c0 - g.wp - 4;  // flat cell of sB[0] / sJ[0] (a quad boundary)
-    // ---- step 1 over the region: quads of 4 cells, rows outside [0, rows) are 0
+    // ---- step 1 over the region: quads of 4 cells, rows outside [s1lo, s1hi) are 0
     for (int qd = threadIdx.x; 4 * qd < nreg; qd += kPQ * kQuarter) {
       const long long f = r0 + 4LL * qd;
       const int y = (int)((f + 2LL * g.wp) / g.wp) - 2;
       const int x0 = (int)(f - (long long)y * g.wp);
       float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, best[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (y >= 0 && y < g.rows) {
+      if (y >= s1lo && y < s1hi) {
         const bool le = x0 == 0, re = x0 + 4 == g.wp;
         CodeWin6 cw;
         Win6 w;
@@ -656,7 +660,12 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
       float best[4];
       uint32_t arg[4];
       sweep_vals(sTC, gamma, cw, w, best, arg);
-      store_ja<true>(J_out, A, off, best, arg);
+      if (y >= own0 && y < own1) {
+        store_ja<true>(J_out, A, off, best, arg);
+      } else {  // a recomputed halo row of a row shard: no actions, no mass
+        store4<true>(J_out + off, best);
+        local = 0.0f;
+      }
     }
     PP2_PHASE(5);
     const int d = kPQ * tile + q;
@@ -788,12 +797,16 @@ size_t loop_pair_lds_bytes(int E, int wp) {
 
 bool loop_pair_fits(const Geom& g, int E, bool sparse) {
   // Sparse rows, LDS for one 1024-thread workgroup, at most 1.6x recomputed
-  // step-1 cells, and a tile for every CU: on fewer tiles the per-step
-  // kernel's 2048-cell workgroups keep more CUs busy (MI355X, 512^2: 6.1
-  // us/step per-step vs 7.4 paired; 1024^2: 9.45 vs 9.0).
+  // step-1 cells (and at most two step-1 quads per lane)
   return sparse && E > 0 && loop_pair_lds_bytes(E, g.wp) <= kDictLdsMaxBytes &&
-         5 * (2 * g.wp + 8) <= 3 * kPTile &&
-         (cells_grid(g, 4) + kPQ - 1) / kPQ >= device_cus();
+         5 * (2 * g.wp + 8) <= 3 * kPTile;
+}
+
+bool loop_pair_pays(const Geom& g) {
+  // a tile for every CU: on fewer tiles the per-step kernel's 2048-cell
+  // workgroups keep more CUs busy (MI355X, 512^2: 6.1 us/step per-step vs 7.4
+  // paired; 1024^2: 8.6 vs 7.7)
+  return (cells_grid(g, 4) + kPQ - 1) / kPQ >= device_cus();
 }
 
 hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
@@ -802,9 +815,14 @@ hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
                                   int u1, int u2, const float* b_in, float* b_out,
                                   const float* J_in, float* J_out, uint8_t* A,
                                   float* out_partials, const float* in_partials, int in_n,
-                                  float* in_sum_out, const float* in_sum, float scale) {
-  if (!loop_pair_fits(g, E, true) || u1 < 0 || u1 > 8 || u2 < 0 || u2 > 8)
+                                  float* in_sum_out, const float* in_sum, float scale,
+                                  int own0, int own1, bool halo_step1) {
+  if (!loop_pair_fits(g, E, true) || u1 < 0 || u1 > 8 || u2 < 0 || u2 > 8 ||
+      (halo_step1 && g.halo < 2))
     return hipErrorInvalidValue;
+  // step-1 rows: the view plus one row per side read from the deep halo, or
+  // the view alone with a zero halo (the grid boundary)
+  const int s1lo = halo_step1 ? -1 : 0, s1hi = halo_step1 ? g.rows + 1 : g.rows;
   const size_t lds = loop_pair_lds_bytes(E, g.wp);
   static unsigned long long attr = 0;
   allow_lds(reinterpret_cast<const void*>(&k_loop_pair_coded), attr);
@@ -812,7 +830,8 @@ hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
   const int grid = coded_grid((dense_blocks + kPQ - 1) / kPQ, 1);
   hipLaunchKernelGGL(k_loop_pair_coded, dim3(grid), dim3(kPQ * kQuarter), lds, st, g, gamma,
                      code, rows, lz1, lz2, tu1, tu2, E, u1, u2, b_in, b_out, J_in, J_out, A,
-                     out_partials, in_partials, in_n, in_sum_out, in_sum, scale, dense_blocks);
+                     out_partials, in_partials, in_n, in_sum_out, in_sum, scale, dense_blocks,
+                     own0, own1, s1lo, s1hi);
   return hipGetLastError();
 }
 

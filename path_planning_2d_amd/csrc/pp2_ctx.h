@@ -162,6 +162,14 @@ int loop_launch(pp2_ctx* c, int e, uint8_t u, uint8_t z, const float* in_partial
 int mdp_sweep_once(pp2_ctx* c);
 int build_model_dict(pp2_ctx* c);
 bool coded_active(const pp2_ctx* c);
+// Step pairs (k_loop_pair_coded) on this context: sparse coded model, a
+// block depth >= 2, a fitting geometry and (unless PP2_TUNE_STEP_PAIRS = 2
+// forces it) a tile per CU.
+bool pairs_apply(pp2_ctx* c);
+// One pair launch on the view extended by e rows per side (pp2_runtime.cpp).
+int pair_launch(pp2_ctx* c, int e, bool shard, uint8_t u1, uint8_t z1, uint8_t u2, uint8_t z2,
+                const float* in_partials, int in_n, float* in_sum_out, const float* in_sum,
+                float scale, int* nparts);
 int fib_sweep_once(pp2_ctx* c);
 int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* out);
 

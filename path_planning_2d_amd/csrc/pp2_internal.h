@@ -183,18 +183,24 @@ hipError_t launch_loop_step_coded(hipStream_t st, const Geom& g, float gamma,
 // unsharded): step 1 (u1, L_z1 column lz1, T_u1 table tu1) divides by the
 // input mass times scale, step 2 (u2, lz2, tu2) by 1.  The input mass is the
 // reduction of in_n pending partials in_partials (k_sum_finalize's tree,
-// also stored to *in_sum_out when given), else *in_sum, else 1.  Reads b_in /
+// also stored to *in_sum_out when given), else *in_sum, else 1.  Only rows
+// [own0, own1) store actions and add to the mass; halo_step1 (row shards on
+// an extended view, g.halo >= 2) computes step 1 on view rows -1 and rows from
+// the halo instead of taking them as zero.  Reads b_in /
 // J_in, writes b_out / J_out / A and step 2's mass partials.  Returns
 // hipErrorInvalidValue when loop_pair_fits is false.
 constexpr int kPlaneGuard = 64;  // floats of guard before/after every plane allocation
 bool loop_pair_fits(const Geom& g, int entries, bool sparse);
+// Whether pairing is faster than single steps on this geometry (a tile per CU).
+bool loop_pair_pays(const Geom& g);
 hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, const float* lz1,
                                   const float* lz2, const float* tu1, const float* tu2,
                                   int entries, int u1, int u2, const float* b_in, float* b_out,
                                   const float* J_in, float* J_out, uint8_t* A,
                                   float* out_partials, const float* in_partials, int in_n,
-                                  float* in_sum_out, const float* in_sum, float scale);
+                                  float* in_sum_out, const float* in_sum, float scale,
+                                  int own0, int own1, bool halo_step1);
 hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int entries,
                                   bool sparse, const float* J_in, float* J_out, uint8_t* A);

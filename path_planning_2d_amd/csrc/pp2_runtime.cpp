@@ -652,40 +652,80 @@ static int blocked_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   return PP2_OK;
 }
 
-// Two steps of the current normalisation block in one launch
+// Two steps of the current normalisation / halo block in one launch
 // (k_loop_pair_coded): the same state transitions as two blocked_loop_step
-// calls.  Applies to an unsharded context with a sparse coded model when the
-// block has two steps left.
-static bool pairs_apply(pp2_ctx* c) {
-  return c->step_pairs && !c->group && !c->comm && c->norm_block >= 2 && coded_active(c) &&
-         c->dict_sparse && pp2::loop_pair_fits(c->g, c->dict_n, true);
+// calls.  Applies to a context with a sparse coded model when the block has
+// two steps left: unsharded, or an RCCL row shard, whose launch covers step
+// 2's extended view (depth - 2 - kstep rows per side) and computes step 1
+// one row deeper from the halo.
+bool pp2rt::pairs_apply(pp2_ctx* c) {
+  const int depth = (c->comm || c->group) ? c->kdepth : c->norm_block;
+  return c->step_pairs && depth >= 2 && coded_active(c) && c->dict_sparse &&
+         pp2::loop_pair_fits(c->g, c->dict_n, true) &&
+         (c->step_pairs == 2 || pp2::loop_pair_pays(c->g));
 }
-static bool can_pair(pp2_ctx* c) { return c->kstep + 2 <= c->norm_block && pairs_apply(c); }
+static bool can_pair(pp2_ctx* c) {
+  const int depth = c->comm ? c->kdepth : c->norm_block;
+  return !c->group && c->kstep + 2 <= depth && pairs_apply(c);
+}
 
+// One k_loop_pair_coded launch for steps kstep, kstep + 1 of a block.  Row
+// shards (e >= 0 rows of view extension: step 2's view, step 1 one row
+// deeper from the halo) store actions and mass only for their own rows.
+int pp2rt::pair_launch(pp2_ctx* c, int e, bool shard, uint8_t u1, uint8_t z1, uint8_t u2,
+                       uint8_t z2, const float* in_partials, int in_n, float* in_sum_out,
+                       const float* in_sum, float scale, int* nparts) {
+  const int bc = c->bcur, bn = bc ^ 1, jc = c->jcur;
+  Geom g = c->g;
+  g.rows += 2 * e;
+  g.row0 -= e;
+  g.halo -= e;
+  const long long sh = (long long)e * g.wp;
+  const size_t es = (size_t)((c->dict_n + 3) & ~3);
+  const size_t ts = ((size_t)c->dict_n * pp2::tu_width(true) + 3) & ~(size_t)3;
+  HIPCHK(pp2::launch_loop_pair_coded(
+      c->stream, g, c->gamma, c->d_code - sh, c->d_rows, c->d_dl + z1 * es, c->d_dl + z2 * es,
+      c->d_tu + u1 * ts, c->d_tu + u2 * ts, c->dict_n, u1, u2, c->b[bc].v.p - sh,
+      c->b[bn].v.p - sh, c->J[jc].v.p - sh, c->J[jc ^ 1].v.p - sh, c->A - sh, c->pbuf[bn],
+      in_partials, in_n, in_sum_out, in_sum, scale, e, e + c->g.rows, shard));
+  *nparts = pp2::mass_partials(g, 4);
+  return PP2_OK;
+}
+
+// Two steps of the current normalisation / halo block in one launch
+// (k_loop_pair_coded): the same state transitions as two blocked_loop_step
+// calls.  Applies to a context with a sparse coded model when the block has
+// two steps left: unsharded, or an RCCL row shard, whose launch covers step
+// 2's extended view (depth - 2 - kstep rows per side) and computes step 1
+// one row deeper from the halo.
 static int loop_pair(pp2_ctx* c, uint8_t u1, uint8_t z1, uint8_t u2, uint8_t z2) {
   for (int i = 0; i < 2; ++i) {
     const uint8_t u = i ? u2 : u1, z = i ? z2 : z1;
     if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
   }
-  const int bc = c->bcur, bn = bc ^ 1, jc = c->jcur;
+  const bool shard = c->comm != nullptr;
+  const int depth = shard ? c->kdepth : c->norm_block;
+  const int bc = c->bcur, bn = bc ^ 1;
   const bool start = c->kstep == 0;
-  // a block start with the mass still pending reduces it inside the launch
-  // (and stores it to bsum[bc]) instead of a separate k_sum_finalize
-  const bool fold = start && c->pending[bc];
-  const size_t es = (size_t)((c->dict_n + 3) & ~3);
-  const size_t ts = ((size_t)c->dict_n * pp2::tu_width(true) + 3) & ~(size_t)3;
-  HIPCHK(pp2::launch_loop_pair_coded(
-      c->stream, c->g, c->gamma, c->d_code, c->d_rows, c->d_dl + z1 * es, c->d_dl + z2 * es,
-      c->d_tu + u1 * ts, c->d_tu + u2 * ts, c->dict_n, u1, u2, c->b[bc].v.p, c->b[bn].v.p,
-      c->J[jc].v.p, c->J[jc ^ 1].v.p, c->A, c->pbuf[bn], fold ? c->pbuf[bc] : nullptr,
-      fold ? c->pcount[bc] : 0, fold ? c->bsum + bc : nullptr,
-      start && !fold ? c->bsum + bc : nullptr, start ? kBlockScale : 1.0f));
+  // unsharded: a block start with the mass still pending reduces it inside
+  // the launch (and stores it to bsum[bc]) instead of a separate
+  // k_sum_finalize; shards finalise the global mass and refresh the halo
+  const bool fold = start && !shard && c->pending[bc];
+  if (start && shard) {
+    CHECK(ensure_mass(c));
+    CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, depth));
+  }
+  int nparts = 0;
+  CHECK(pair_launch(c, shard ? depth - 2 - c->kstep : 0, shard, u1, z1, u2, z2,
+                    fold ? c->pbuf[bc] : nullptr, fold ? c->pcount[bc] : 0,
+                    fold ? c->bsum + bc : nullptr, start && !fold ? c->bsum + bc : nullptr,
+                    start ? kBlockScale : 1.0f, &nparts));
   c->pending[bc] = false;
-  c->pcount[bn] = pp2::mass_partials(c->g, 4);
+  c->pcount[bn] = nparts;
   c->pending[bn] = true;
   c->bcur = bn;
-  c->jcur = jc ^ 1;
-  c->kstep = (c->kstep + 2) % c->norm_block;
+  c->jcur ^= 1;
+  c->kstep = (c->kstep + 2) % depth;
   return PP2_OK;
 }
 
@@ -788,7 +828,10 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
     case PP2_TUNE_CODED_MODEL: c->use_coded = value != 0; return PP2_OK;
-    case PP2_TUNE_STEP_PAIRS: c->step_pairs = value != 0; return PP2_OK;
+    case PP2_TUNE_STEP_PAIRS:
+      if (value < 0 || value > 2) return set_err(PP2_EINVAL, "step pairs %d not in [0, 2]", value);
+      c->step_pairs = value;
+      return PP2_OK;
     case PP2_TUNE_NORM_BLOCK:
       if (value < 1 || value > kMaxNormBlock)
         return set_err(PP2_EINVAL, "normalisation block %d not in [1, %d]", value, kMaxNormBlock);

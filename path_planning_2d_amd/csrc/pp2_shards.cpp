@@ -234,6 +234,53 @@ int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z) {
   return mark_done(g);
 }
 
+// Two loop steps of a halo block on every shard in one launch each
+// (pp2rt::pair_launch on the view of step kstep + 1; step kstep is computed
+// one row deeper from the halo), the mass combined after the pair.
+static int group_loop_pair(pp2_shard_group* g, uint8_t u1, uint8_t z1, uint8_t u2, uint8_t z2) {
+  pp2_ctx* c0 = g->ctx[0];
+  const int K = c0->kdepth;
+  CHECK(wait_neighbours(g));
+  const bool start = c0->kstep == 0;
+  if (start) CHECK(exchange_local(g, {HALO_BELIEF, HALO_VALUE}, K));
+  for (pp2_ctx* c : g->ctx) {
+    DeviceGuard dg(c->device);
+    const int bc = c->bcur, bn = bc ^ 1;
+    int nparts = 0;
+    CHECK(pair_launch(c, K - 2 - c->kstep, true, u1, z1, u2, z2, nullptr, 0, nullptr,
+                      start ? c->bsum + bc : nullptr, start ? kBlockScale : 1.0f, &nparts));
+    HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bn], nparts, c->bsum + bn));
+    c->pending[bc] = c->pending[bn] = false;
+    c->bcur = bn;
+    c->jcur ^= 1;
+    c->kstep = (c->kstep + 2) % K;
+  }
+  CHECK(combine_mass(g));
+  return mark_done(g);
+}
+
+int pp2_shard_group_loop_run(pp2_shard_group* g, int n, const uint8_t* us, const uint8_t* zs) {
+  CHECK(check_group(g));
+  if (n < 0 || (n > 0 && (!us || !zs))) return set_err(PP2_EINVAL, "bad trajectory");
+  for (int i = 0; i < n;) {
+    pp2_ctx* c0 = g->ctx[0];
+    bool pair = i + 1 < n && c0->kstep + 2 <= c0->kdepth;
+    for (pp2_ctx* c : g->ctx) pair = pair && pairs_apply(c);
+    if (pair) {
+      for (int k = 0; k < 2; ++k)
+        if (us[i + k] > 8 || zs[i + k] > 15)
+          return set_err(PP2_EINVAL, "action %u / observation %u out of range", us[i + k],
+                         zs[i + k]);
+      CHECK(group_loop_pair(g, us[i], zs[i], us[i + 1], zs[i + 1]));
+      i += 2;
+    } else {
+      CHECK(pp2_shard_group_loop_step(g, us[i], zs[i]));
+      ++i;
+    }
+  }
+  return PP2_OK;
+}
+
 int pp2_shard_group_belief_update(pp2_shard_group* g, uint8_t u, uint8_t z) {
   CHECK(check_group(g));
   CHECK(wait_neighbours(g));

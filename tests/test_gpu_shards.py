@@ -191,3 +191,70 @@ def test_rccl_single_rank_pipeline():
             sh.mdp_sweep(3)
         assert ref.mdp_solve() == sh.mdp_solve()
         np.testing.assert_array_equal(sh.mdp_get()[0], ref.mdp_get()[0])
+
+
+@pytest.mark.parametrize("bounds,depth", [((0, 512, 1024), 8), ((0, 300, 777, 1024), 8),
+                                          ((0, 512, 1024), 3), ((0, 400, 1024), 5)])
+def test_shard_group_step_pairs(bounds, depth):
+    """Two loop steps of a halo block per launch on row shards
+    (k_loop_pair_coded on step 2's extended view, step 1 one row deeper from
+    the halo rows of the neighbour shards; pp2_shard_group_loop_run), forced
+    with PP2_TUNE_STEP_PAIRS = 2 on these small shards: values and actions
+    bit-exact with the unsharded grid, beliefs rel 1e-5, across block
+    boundaries, odd chunks and halo depths whose blocks end on a single step."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    N = 1024
+    grid = S.synth_grid(N, N, N)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 23, seed=9)
+    b0 = S.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            P.ShardGroup(grid, goal, bounds, gamma=float(GAMMA)) as grp:
+        ref.model_generate()
+        grp.model_generate()
+        grp.set_halo_depth(depth)
+        grp.set_tuning(P.GridContext.TUNE_STEP_PAIRS, 2)
+        assert grp.loop_steps_per_launch() == [2] * (len(bounds) - 1)
+        for c in (ref, grp):
+            c.belief_set(b0)
+            c.mdp_reset()
+        for lo, hi in ((0, 5), (5, 6), (6, 23)):
+            ref.loop_run(us[lo:hi], zs[lo:hi])
+            grp.loop_run(us[lo:hi], zs[lo:hi])
+            Jr, Ar = ref.mdp_get()
+            Jg, Ag = grp.mdp_get()
+            np.testing.assert_array_equal(Jg.view(np.uint32), Jr.view(np.uint32),
+                                          err_msg=f"J after {hi} steps")
+            np.testing.assert_array_equal(Ag, Ar, err_msg=f"A after {hi} steps")
+            assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
+                             msg=f"belief after {hi} steps")
+
+
+def test_rccl_single_rank_step_pairs():
+    """The RCCL shard path with step pairs at the bench size (1024^2, a tile
+    per CU): a full-grid shard with a 1-rank communicator runs pp2_loop_run in
+    pair launches over its 8-deep halo blocks; equals the unsharded grid."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    N = 1024
+    grid = S.synth_grid(N, N, N)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 21, seed=4)
+    b0 = S.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            P.GridContext(grid, goal, gamma=float(GAMMA), rows=(0, N)) as sh:
+        sh.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
+        for c in (ref, sh):
+            c.model_generate()
+            c.belief_set(b0)
+            c.mdp_reset()
+        assert sh.loop_steps_per_launch() == 2
+        for lo, hi in ((0, 7), (7, 21)):
+            ref.loop_run(us[lo:hi], zs[lo:hi])
+            sh.loop_run(us[lo:hi], zs[lo:hi])
+            np.testing.assert_array_equal(sh.mdp_get()[0].view(np.uint32),
+                                          ref.mdp_get()[0].view(np.uint32))
+            np.testing.assert_array_equal(sh.mdp_get()[1], ref.mdp_get()[1])
+            assert_rel_close(sh.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
+                             msg=f"belief after {hi} steps")
