@@ -526,9 +526,16 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_mdp_sweep_coded(
 // loop_pair): step 1 then also covers view rows -1 and rows (s1lo/s1hi,
 // real neighbour rows read from the deep halo), and only the owned rows
 // [own0, own1) store actions and add to the mass.
-constexpr int kPQ = 4;                      // 256-thread quarters per workgroup
+// 256-thread quarters per workgroup.  Two (2048-cell tiles, two workgroups
+// per CU) measured slower: 1024^2 8.5 us/step against 7.7.
+constexpr int kPQ = 4;
 constexpr int kPTile = kPQ * kQuarter * 4;  // cells per tile
-__host__ __device__ constexpr int pair_region(int wp) { return kPTile + 2 * wp + 8; }
+// step-1 region: the tile plus a row per side, plus a quad per side unless
+// tiles are whole rows (then the x +- 1 neighbours at the tile ends are the
+// zero grid edge)
+__host__ __device__ constexpr int pair_region(int wp) {
+  return kPTile + 2 * wp + (kPTile % wp == 0 ? 0 : 8);
+}
 
 // J or b window of a lane from an LDS region holding the plane from flat cell
 // r0 on.
@@ -572,7 +579,7 @@ __device__ __forceinline__ void sweep_vals(const float* sTC, float gamma, const 
   coded_sweep4<true>(sTC, cc, jn, gamma, best, arg);
 }
 
-__global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
+__global__ __launch_bounds__(kPQ * kQuarter, 4) void k_loop_pair_coded(
     Geom g, float gamma, const uint16_t* __restrict__ code, const float* __restrict__ rows,
     const float* __restrict__ lz1, const float* __restrict__ lz2, const float* __restrict__ tu1,
     const float* __restrict__ tu2, int E, int u1, int u2, const float* __restrict__ b_in,
@@ -615,7 +622,8 @@ __global__ __launch_bounds__(kPQ * kQuarter, kPQ) void k_loop_pair_coded(
   PP2_PHASE(1);
   for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
     const long long c0 = (long long)tile * kPTile;
-    const long long r0 = c0 - g.wp - 4;  // flat cell of sB[0] / sJ[0] (a quad boundary)
+    // flat cell of sB[0] / sJ[0] (a quad boundary)
+    const long long r0 = c0 - g.wp - (kPTile % g.wp == 0 ? 0 : 4);
     // ---- step 1 over the region: quads of 4 cells, rows outside [s1lo, s1hi) are 0
     for (int qd = threadIdx.x; 4 * qd < nreg; qd += kPQ * kQuarter) {
       const long long f = r0 + 4LL * qd;
@@ -796,17 +804,18 @@ size_t loop_pair_lds_bytes(int E, int wp) {
 }
 
 bool loop_pair_fits(const Geom& g, int E, bool sparse) {
-  // Sparse rows, LDS for one 1024-thread workgroup, at most 1.6x recomputed
-  // step-1 cells (and at most two step-1 quads per lane)
+  // Sparse rows, LDS for one 1024-thread workgroup, step 1 over at most 1.6x
+  // the tile's cells (MI355X, 2048^2: pairs at 2.0x ran 31.4 us/step against
+  // 24.2 for single steps)
   return sparse && E > 0 && loop_pair_lds_bytes(E, g.wp) <= kDictLdsMaxBytes &&
-         5 * (2 * g.wp + 8) <= 3 * kPTile;
+         5 * pair_region(g.wp) <= 8 * kPTile;
 }
 
 bool loop_pair_pays(const Geom& g) {
   // a tile for every CU: on fewer tiles the per-step kernel's 2048-cell
   // workgroups keep more CUs busy (MI355X, 512^2: 6.1 us/step per-step vs 7.4
   // paired; 1024^2: 8.6 vs 7.7)
-  return (cells_grid(g, 4) + kPQ - 1) / kPQ >= device_cus();
+  return (cells_grid(g, 4) + kPQ - 1) / kPQ >= device_cus() * (4 / kPQ);
 }
 
 hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
@@ -827,7 +836,7 @@ hipError_t launch_loop_pair_coded(hipStream_t st, const Geom& g, float gamma,
   static unsigned long long attr = 0;
   allow_lds(reinterpret_cast<const void*>(&k_loop_pair_coded), attr);
   const int dense_blocks = cells_grid(g, 4);
-  const int grid = coded_grid((dense_blocks + kPQ - 1) / kPQ, 1);
+  const int grid = coded_grid((dense_blocks + kPQ - 1) / kPQ, 4 / kPQ);
   hipLaunchKernelGGL(k_loop_pair_coded, dim3(grid), dim3(kPQ * kQuarter), lds, st, g, gamma,
                      code, rows, lz1, lz2, tu1, tu2, E, u1, u2, b_in, b_out, J_in, J_out, A,
                      out_partials, in_partials, in_n, in_sum_out, in_sum, scale, dense_blocks,

@@ -18,14 +18,15 @@ def main():
     goal = S.synth_goal(grid)
     us, zs, _ = S.synth_trajectory(grid, reps, seed=42)
     stream = torch.cuda.Stream()
-    for mode in ("plain", "rccl1", "rccl1-depth1", "rccl1-cs", "rccl1-cs-depth1"):
+    modes = os.environ.get("PP2_MODES", "plain,rccl1,rccl1-depth2,rccl1-depth1,rccl1-cs").split(",")
+    for mode in modes:
         kw = {} if mode == "plain" else {"rows": (0, N)}
         with P.GridContext(grid, goal, gamma=0.95, **kw) as ctx:
             ctx.set_stream(stream.cuda_stream)
             if mode != "plain":
                 ctx.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
-                if mode.endswith("depth1"):
-                    ctx.set_tuning(ctx.TUNE_HALO_DEPTH, 1)
+                if "-depth" in mode:
+                    ctx.set_tuning(ctx.TUNE_HALO_DEPTH, int(mode.split("-depth")[1]))
                 if "-cs" in mode:
                     ctx.set_tuning(ctx.TUNE_COMM_STREAM, 1)
             ctx.model_generate()
