@@ -60,7 +60,7 @@ BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
 BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
 BYTES_LOOP_CODED = 19            # per cell: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1
 BYTES_SWEEP_CODED = 11           # per cell: code 2 + J 4 + J' 4 + A 1
-LDS_BYTES_LOOP_CODED = 196       # per cell (sparse rows): T_u gather 4*4 + L_z 4 + sweep 11*16
+LDS_BYTES_LOOP_CODED = 204       # per cell-step (factored rows): T_u gather 4*4 + L_z 4 + backup record 16 + quads 8*16 + stay 4 + costs 9*4
 LDS_PEAK_GBS = 150000.0          # ds_read_b64/b128 chip aggregate (MI355X_MICROARCH.md LDS)
 GAMMA = 0.95
 
