@@ -61,6 +61,8 @@ BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
 BYTES_LOOP_CODED = 19            # per cell: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1
 BYTES_SWEEP_CODED = 11           # per cell: code 2 + J 4 + J' 4 + A 1
 LDS_BYTES_LOOP_CODED = 204       # per cell-step (factored rows): T_u gather 4*4 + L_z 4 + backup record 16 + quads 8*16 + stay 4 + costs 9*4
+LDS_BYTES_LOOP_RESIDENT = 248    # + the b / J window rows read from LDS (2 planes x 3 rows x 24 B per quad = 36) + b', J' stored (8)
+RESIDENT_STEPS = 2048            # pp2_loop_steps_per_launch of the tile-resident loop
 LDS_PEAK_GBS = 150000.0          # ds_read_b64/b128 chip aggregate (MI355X_MICROARCH.md LDS)
 GAMMA = 0.95
 
@@ -684,6 +686,12 @@ def main():
         ctx.loop_run(us[:reps], zs[:reps])
 
     sweep_ms = timed(lambda: ctx.mdp_sweep(reps))  # coded when active
+    pairs_ms = None
+    if coded and steps_per_launch >= RESIDENT_STEPS:
+        # the launch-per-pair path beside the resident loop (same steps)
+        ctx.set_tuning(ctx.TUNE_RESIDENT, 0)
+        pairs_ms = timed(loop_reps)
+        ctx.set_tuning(ctx.TUNE_RESIDENT, 1)
     belief_ms = timed(lambda: [ctx.belief_update(int(us[k]), int(zs[k])) for k in range(reps)])
     dense = None
     if coded:
@@ -718,9 +726,13 @@ def main():
 
     bytes_loop = BYTES_LOOP_CODED if coded else BYTES_LOOP
     bytes_sweep = BYTES_SWEEP_CODED if coded else BYTES_SWEEP
-    loop_kernel = ("k_loop_pair_coded" if steps_per_launch == 2 else "k_loop_step_coded") \
+    resident = steps_per_launch >= RESIDENT_STEPS
+    loop_kernel = ("k_loop_resident" if resident else
+                   "k_loop_pair_coded" if steps_per_launch == 2 else "k_loop_step_coded") \
         if coded else "k_loop_step"
-    spl = steps_per_launch
+    # the resident loop runs the whole timed trajectory in ceil(steps / 2048) launches
+    spl = (args.steps / -(-args.steps // RESIDENT_STEPS)) if resident else steps_per_launch
+    lds_bytes = LDS_BYTES_LOOP_RESIDENT if resident else LDS_BYTES_LOOP_CODED
     sweep_gbs = bytes_sweep * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
     belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
     # one launch = spl steps; its average duration from the timed region's events
@@ -779,7 +791,10 @@ def main():
                           if coded else "dense fp32 planes"),
             },
             "roofline": {
-                "kernel": (f"{loop_kernel} (two fused loop steps per launch: belief update + "
+                "kernel": (f"{loop_kernel} (the whole timed trajectory, {args.steps} fused loop "
+                           f"steps, in one launch: one tile of rows per CU resident in LDS)"
+                           if resident else
+                           f"{loop_kernel} (two fused loop steps per launch: belief update + "
                            f"MDP Bellman sweep, twice)" if spl == 2 else
                            f"{loop_kernel} (fused belief update + MDP Bellman sweep)"),
                 "bound": "hbm",
@@ -793,7 +808,13 @@ def main():
                 "algorithmic_bytes_per_cell_per_launch": bytes_loop,
                 "algorithmic_bytes_per_launch": algo_launch,
                 "avg_launch_us": launch_s * 1e6,
-                "note": ("bytes the coded kernel must move per launch: code 2, b 4, b' 4, J 4, "
+                "note": ("bytes the resident kernel must move per launch: code 2, b 4, J 4 in, "
+                         "b' 4, J' 4, A 1 out per cell; every intermediate step stays in LDS "
+                         "(the tiles' edge rows cross CUs through L2/MALL), so HBM is not the "
+                         "binding resource: LDS (roofline_lds) and VALU issue are, plus the "
+                         "per-step edge-row hand-off chain (DESIGN.md §3.2)"
+                         if resident and coded else
+                         "bytes the coded kernel must move per launch: code 2, b 4, b' 4, J 4, "
                          "J' 4, A 1 per cell (a pair launch keeps its intermediate step in "
                          "LDS); launch-latency and LDS bound, see roofline_lds"
                          if coded else "dense planes: SURVEY.md §8(d) fp32 tensor contract"),
@@ -809,11 +830,11 @@ def main():
                          "is 60 % of 8 TB/s / 417 B"),
             },
             "roofline_lds": ({
-                "achieved": LDS_BYTES_LOOP_CODED * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9,
+                "achieved": lds_bytes * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9,
                 "peak": LDS_PEAK_GBS, "unit": "GB/s",
-                "frac": LDS_BYTES_LOOP_CODED * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
+                "frac": lds_bytes * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
                 / LDS_PEAK_GBS,
-                "bytes_per_cell": LDS_BYTES_LOOP_CODED} if coded else None),
+                "bytes_per_cell": lds_bytes} if coded else None),
             "dense_path": dense,
             "config4": c4,
             "kernels": {
@@ -825,6 +846,7 @@ def main():
                 "belief_update_gbs": belief_gbs,
                 "belief_update_frac": belief_gbs / HBM_PEAK_GBS,
                 "loop_step_us_events": loop_ms_events * 1e3,
+                "loop_step_us_step_pairs": (pairs_ms * 1e3 if pairs_ms else None),
                 "loop_enqueue_us_per_step": 1e6 * enqueue_s / args.steps,
                 "loop_gbs": loop_gbs,
                 "loop_frac": loop_gbs / HBM_PEAK_GBS,

@@ -120,6 +120,18 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           0 = one launch per step.  Results are
  *                           bit-identical either way. */
 #define PP2_TUNE_STEP_PAIRS 7
+/*  PP2_TUNE_RESIDENT        1 (default): pp2_loop_run on an unsharded context
+ *                           with a sparse coded model whose grid fits one
+ *                           tile of whole rows per CU (width padded to a
+ *                           multiple of 256, rows * width <= 4096 * CUs, the
+ *                           dictionary in LDS) runs the whole trajectory in
+ *                           one launch (the tile-resident loop, up to 2048
+ *                           steps per launch); 0 = step pairs / single steps.
+ *                           Results are bit-identical either way.  A resident
+ *                           launch that cannot get every tile onto the GPU
+ *                           at once ends with an error that pp2_synchronize
+ *                           reports (PP2_EHIP); the context then falls back. */
+#define PP2_TUNE_RESIDENT 8
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
 /* ---------------------------------------------------------------- model
@@ -149,10 +161,11 @@ int pp2_model_load(pp2_ctx* ctx, const char* dir);
  * bit-identical either way. */
 int pp2_model_dict_info(pp2_ctx* ctx, int* entries, int* active);
 
-/* Loop steps pp2_loop_run fuses into one kernel launch on this context: 2
- * when it runs the steps of a normalisation / halo block in pairs
- * (PP2_TUNE_STEP_PAIRS with a sparse coded model whose grid has a 4096-cell
- * tile per CU; unsharded, RCCL row shard or shard-group member), else 1. */
+/* Loop steps pp2_loop_run fuses into one kernel launch on this context: 2048
+ * for the tile-resident loop (PP2_TUNE_RESIDENT), 2 when it runs the steps
+ * of a normalisation / halo block in pairs (PP2_TUNE_STEP_PAIRS with a sparse
+ * coded model whose grid has a 4096-cell tile per CU; unsharded, RCCL row
+ * shard or shard-group member), else 1. */
 int pp2_loop_steps_per_launch(pp2_ctx* ctx, int* steps);
 
 /* ---------------------------------------------------------------- belief

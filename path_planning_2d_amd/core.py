@@ -101,6 +101,7 @@ class GridContext:
     TUNE_COMM_STREAM = 5
     TUNE_NORM_BLOCK = 6
     TUNE_STEP_PAIRS = 7
+    TUNE_RESIDENT = 8
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))

@@ -102,6 +102,7 @@ struct pp2_ctx {
   float* d_tu = nullptr;           // raw T per action: [u][entry][4 sparse | 9 full]
   int dict_n = 0;                  // entries; 0 = no dictionary (dense path only)
   bool dict_sparse = false;        // every T row is zero off the base-kernel support
+  bool dict_t_finite = false;      // every dictionary T entry is finite
   // the sparse rows' T == 0 skip needs finite, non-negative beliefs (not -0):
   // false after a pp2_belief_set that breaks that, until the next one
   bool belief_sparse_ok = true;
@@ -119,6 +120,18 @@ struct pp2_ctx {
   // pp2_loop_run on an unsharded sparse-coded context fuses the steps of a
   // normalisation block in pairs (pp2::launch_loop_pair_coded)
   int step_pairs = 1;              // PP2_TUNE_STEP_PAIRS
+
+  // pp2_loop_run's tile-resident loop (pp2_resident.hip), PP2_TUNE_RESIDENT
+  int resident = 1;
+  int ncus = 0;                    // CUs of the device
+  int res_plan_e = -1;             // dictionary size the plan below was made for
+  bool res_ok = false;
+  pp2::ResidentPlan res_plan{};
+  unsigned* res_sync = nullptr;    // sync words (flags, counters, error)
+  float* res_ring = nullptr;       // kResidentRing slots of mass partials
+  float* res_xch = nullptr;        // exchange rows
+  unsigned res_epoch = 0, res_arrive = 0, res_read = 0;  // epoch-tagged counters
+  bool res_used = false;           // a resident launch since the last error check
 
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;

@@ -205,4 +205,53 @@ hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int entries,
                                   bool sparse, const float* J_in, float* J_out, uint8_t* A);
 
+// Tile-resident loop (pp2_resident.hip): n fused loop steps of an unsharded
+// sparse-coded context in one launch, one tile of rt whole rows per CU kept
+// in LDS, neighbour rows handed over by per-wave flags, block-start masses
+// behind an arrival counter.  Needs wp % 256 == 0, rt * wp / 4 <= 1024 lanes,
+// a tile per CU and the whole dictionary in LDS (resident_plan).
+constexpr int kResidentMaxSteps = 2048;  // steps per launch (kernel-argument trajectory)
+constexpr int kResidentRing = 16;        // partial-mass slots (>= block depth + 2)
+constexpr int kResidentSyncArrive = 0;   // sync words: block-start arrivals,
+constexpr int kResidentSyncRead = 1;     //   in_partials readers done,
+constexpr int kResidentSyncErr = 2;      //   sticky timeout flag,
+constexpr int kResidentSyncFlags = 16;   //   then [tile][top, bottom][wave of row] flags
+struct ResidentPlan {
+  int rt = 0, ntiles = 0, threads = 0, flag_words = 0;
+  size_t lds = 0;
+};
+struct ResidentRun {
+  Geom g;
+  float gamma;
+  int E, es, ts;             // entries; L_z column stride (dl[z*es]); T_u table stride (tu[u*ts])
+  const uint16_t* code;      // code plane (row 0, x 0)
+  const float* rows;         // factored sweep rows
+  const float* dl;           // L transposed [16][es]
+  const float* tu;           // raw T per action [9][ts]
+  const float* b_in;         // step 0's input belief / value planes (row 0)
+  const float* j_in;
+  float* b_out;              // the last step's output planes
+  float* j_out;
+  float* xch;                // exchange rows, resident_xch_floats(): [step & 1][b, J][tile][top, bottom][4 zero + wp]
+  uint8_t* A;
+  int n, kstep0, depth, rt, ntiles, nparts;
+  float bscale;              // block-start scale (2^96, or 1 for depth 1)
+  const float* in_partials;  // step 0's pending input mass (block start), or null
+  int in_n;
+  float* in_sum_out;         // receives that mass (tile 0)
+  const float* in_sum;       // step 0's finalised input mass when in_partials is null
+  float* ring;               // kResidentRing x nparts partial slots
+  float* out_partials;       // the last step's partials (the context's pending buffer)
+  unsigned* sync;            // sync words (kResidentSyncFlags + flag_words)
+  unsigned epoch, arrive_base, read_base;  // epoch-tagged counters of earlier launches
+  int final_wait_read;       // out_partials == in_partials: the last step waits for readers
+  uint8_t uz[kResidentMaxSteps];  // u | z << 4 per step
+};
+size_t resident_lds_bytes(const Geom& g, int E, int es, int ts, int rt);
+inline size_t resident_xch_floats(const Geom& g, int ntiles) {
+  return (size_t)8 * ntiles * (g.wp + 4) + 8;  // rows of 4 zero + wp floats, slack at the end
+}
+bool resident_plan(const Geom& g, int E, int es, int ts, int ncus, ResidentPlan* p);
+hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a);
+
 }  // namespace pp2

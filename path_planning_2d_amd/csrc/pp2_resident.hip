@@ -1,0 +1,444 @@
+// pp2_resident.hip -- the tile-resident loop (gfx950): a run of n north-star
+// steps (belief update + MDP Bellman sweep, k_loop_step's semantics) in ONE
+// launch, for the unsharded sparse-coded context.
+//
+// Per launch of the one-step / step-pair kernels the grid pays a dependent
+// kernel boundary, a dictionary staging, an HBM round trip of b and J and a
+// lock-stepped load -> gather -> backup -> store chain with nothing to overlap
+// it (pairs also recompute a one-row halo: 1.5x step-1 work at 1024^2).  Here
+// every CU keeps ONE tile of rt whole rows resident for the whole run:
+//   * the tile's b and J live in LDS (ping-pong buffers with zero pads at
+//     the x edges); the dictionary (factored sweep rows, T_u of all 9
+//     actions, L_z of all 16 observations) is staged once per launch;
+//   * a lane owns one quad of 4 cells and keeps its code window in registers;
+//   * only the tile's first and last rows cross CUs.  Their waves take the
+//     neighbours' rows of step t-1 first (poll the <= 3 flags of the
+//     neighbour waves over their columns, then sc1 loads), compute with issue
+//     priority, store their own row write-through (sc1) into an exchange slot
+//     (step & 1), drain, and raise one flag per wave (MI355X_MICROARCH.md
+//     § visibility, table row 1 with one storing wave).  A producer rewrites
+//     a slot only after the consumer's flag of the following step, i.e.
+//     after the consumer's loads of it have returned.  Interior waves never
+//     touch global memory;
+//   * a normalisation block start needs the exact mass of the previous belief:
+//     every tile adds to an arrival counter after its step's wave partials are
+//     drained, and wave 0 of each tile reduces all partials (k_sum_finalize's
+//     tree, sc1 loads) once the counter is full.  The partials of step t go to
+//     ring slot t % kResidentRing (no tile runs more than one block ahead of
+//     the slowest, so a slot is never rewritten while a block start reads it);
+//   * the last step stores b, J and A for the whole grid (non-temporal) and its
+//     partials to the context's pending buffer.
+// Per cell the arithmetic is k_loop_step_coded's (same operands, same fmaf
+// order; off-grid neighbours are +0 from the pads, and fmaf(T, +0, p) == p
+// for the finite T resident_plan's caller checks), the partials use the dense
+// kernels' cell -> (block, wave) map, and normalisation follows
+// blocked_loop_step exactly, so b, masses, J and A equal the
+// one-launch-per-step path bit for bit.
+//
+// Flags and counters are epoch-tagged (values grow monotonically over the
+// context's launches), so no per-launch reset is needed.  Every wait is
+// bounded: after kSpinTicks of the 100 MHz clock it raises the sticky error
+// word and returns, so a grid that is not fully resident ends with an error
+// instead of hanging (pp2_synchronize reports it).
+#include "pp2_coded_dev.h"
+
+namespace pp2 {
+
+#ifdef PP2_RES_TRACE
+// Diagnostic build only (tools/micro/resident_trace.py): s_memrealtime
+// (100 MHz) per step of tiles 0..15 for wave 0 (the first row) and wave 5
+// (an interior row at 1024^2): step top, neighbour rows in hand, computed
+// and published, after the step barrier.
+__device__ unsigned long long g_rtrace[16][64][2][4];
+#define PP2_RT(ph)                                                                    \
+  if (tile < 16 && t < 64 && lane == 0 && (wave == 0 || wave == 5))                   \
+  g_rtrace[tile][t][wave == 5][ph] = __builtin_amdgcn_s_memrealtime()
+#else
+#define PP2_RT(ph) (void)0
+#endif
+
+namespace {
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;                              // buffer aux bit: sc1
+constexpr unsigned long long kSpinTicks = 25000000ull;  // 0.25 s at 100 MHz
+
+__device__ __forceinline__ Rsrc make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ f4a ld4_sc1(Rsrc r, int off) {
+  return __builtin_bit_cast(f4a, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1));
+}
+__device__ __forceinline__ float ld1_sc1(Rsrc r, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kSc1));
+}
+__device__ __forceinline__ void st4_sc1(Rsrc r, int off, const float (&v)[4]) {
+  const f4a t = {v[0], v[1], v[2], v[3]};
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, t), r, off, 0, kSc1);
+}
+__device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool reached(unsigned v, unsigned target) {
+  return (int)(v - target) >= 0;  // epoch arithmetic, wrap-safe
+}
+
+// The calling wave waits until flag[idx(i)] has reached target for every lane
+// i < nf (lane i polls one word; relaxed sc1 loads, s_sleep between polls).
+// Bounded: gives up after kSpinTicks (or at once when the error word is
+// already raised), raising it.  The wavefront acquire only keeps the compiler
+// from moving the caller's later (sc1) loads above the poll.
+__device__ __forceinline__ bool wave_wait(const unsigned* f0, int nf, unsigned target, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long t0 = wall_clock64();
+  for (int spin = 0;; ++spin) {
+    const unsigned v = lane < nf ? ld_flag(f0 + lane) : target;
+    if (__all(reached(v, target))) break;
+    if ((spin & 7) == 7) {
+      if (ld_flag(err) != 0u || wall_clock64() - t0 > kSpinTicks) {
+        if (lane == 0) st_flag(err, 1u);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return true;
+}
+
+// wave_reduce_partials (pp2_device.h) with sc1 loads: the partials were
+// stored by other CUs inside this launch.  Same association, bit for bit.
+__device__ __forceinline__ float wave_reduce_partials_sc1(const float* p, int n) {
+  const Rsrc r = make_rsrc(p);
+  const int lane = threadIdx.x & 63;
+  const int nq = n >> 2;
+  float s = 0.0f;
+  for (int base = lane; base < nq; base += 64 * 8) {
+    f4a w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + 64 * j;
+      w[j] = ld4_sc1(r, 16 * (i < nq ? i : base));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (base + 64 * j < nq) s += ((w[j][0] + w[j][1]) + w[j][2]) + w[j][3];
+  }
+  return wave_sum(s);
+}
+
+// The coded belief gather of action U for a lane's quad (belief_vals'
+// arithmetic) on a window whose off-grid cells are 0: the resident kernel's
+// LDS rows and exchange rows carry zero pads, so instead of zeroing T at the
+// x edges it multiplies the edge code's (finite, resident_plan checks) T by
+// b = +0, and fmaf(T, +0, p) == p for the non-negative partial sums.
+template <int U>
+__device__ __forceinline__ void belief_quad(const float* sTu, const float* sL, float inv,
+                                            const CodeWin6& cw, const Win6& win, float (&p)[4],
+                                            float& local) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) p[k] = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const int oy = s / 3, ox = s % 3 - 1;
+    constexpr int kTu = tu_width(true);
+    const int sl = sup_slot(U, 8 - s);
+    if (sl < 0) continue;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      p[k] = __builtin_fmaf(sTu[cw.at(oy, k + 1 + ox) * kTu + sl], win.v[oy][k + 1 + ox], p[k]);
+    __builtin_amdgcn_sched_barrier(0);  // <= 4 gathers in flight
+  }
+  local = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    p[k] = p[k] * sL[cw.at(1, k + 1)];
+    p[k] = p[k] * inv;
+    local += p[k];
+  }
+}
+
+__device__ __forceinline__ void belief_any(int u, const float* sTu, const float* sL, float inv,
+                                           const CodeWin6& cw, const Win6& w, float (&p)[4],
+                                           float& local) {
+  switch (u) {
+#define PP2_BQ(UU) \
+  case UU: belief_quad<UU>(sTu, sL, inv, cw, w, p, local); break;
+    PP2_BQ(0) PP2_BQ(1) PP2_BQ(2) PP2_BQ(3) PP2_BQ(4) PP2_BQ(5) PP2_BQ(6) PP2_BQ(7)
+    default: belief_quad<8>(sTu, sL, inv, cw, w, p, local);
+#undef PP2_BQ
+  }
+}
+
+// One window row (x0 - 1 .. x0 + 4) from a zero-padded LDS row.
+__device__ __forceinline__ void row_lds(const float* row, int x0, float (&v)[6]) {
+  const float* p = row + x0;
+  const f4a m = *reinterpret_cast<const f4a*>(p);
+  v[0] = p[-1]; v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3]; v[5] = p[4];
+}
+__device__ __forceinline__ void row_zero(float (&v)[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[i] = 0.0f;
+}
+
+// One window row from a zero-padded exchange row (sc1: handed over in-launch).
+__device__ __forceinline__ void row_sc1(Rsrc r, int off, float (&v)[6]) {
+  const f4a m = ld4_sc1(r, off);
+  v[0] = ld1_sc1(r, off - 4); v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3];
+  v[5] = ld1_sc1(r, off + 16);
+}
+
+__global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int wp = a.g.wp, rows = a.g.rows, tpr = wp >> 2, wpr = wp >> 8;
+  const int xs = wp + 4;                // padded row stride (LDS and exchange rows)
+  const int bufn = 4 + a.rt * xs;       // one padded tile buffer
+  float* sTC = lds;
+  float* sL = sTC + lds_span(rows_floats(a.E, true));
+  float* sTu = sL + lds_span(16 * a.es);
+  float* sB0 = sTu + lds_span(9 * a.ts);  // b buffers 0, 1, then J buffers 0, 1
+  float* sS = sB0 + 4 * bufn;
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave-uniform: a row holds wpr whole waves (wp % 256 == 0)
+  const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x / tpr);
+  const int wj = __builtin_amdgcn_readfirstlane((threadIdx.x % tpr) >> 6);
+  const int x0 = (threadIdx.x % tpr) * 4;
+  const int y = tile * a.rt + ty;
+  const bool valid = y < rows;
+  // the tile's first row reads the row above from tile - 1 and publishes
+  // itself for it; its last row likewise with tile + 1
+  const bool nb_up = valid && ty == 0 && tile > 0;
+  const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
+  unsigned* const flags = a.sync + kResidentSyncFlags;
+  unsigned* const err = a.sync + kResidentSyncErr;
+  // lanes 0..nfl-1 poll the flags of the neighbour row's waves j-1 .. j+1
+  const int fj = max(wj - 1, 0);
+  const int nfl = min(wj + 1, wpr - 1) - fj + 1;
+  const Rsrc rx = make_rsrc(a.xch);
+  // byte offset of x0 in exchange row [slot][k][tl][side] (4 zero floats
+  // before every row)
+  auto xoff = [&](int slot, int k, int tl, int side) {
+    return (int)(((((((long long)slot * 2 + k) * a.ntiles + tl) * 2 + side) * xs + 4) + x0) * 4);
+  };
+  auto sbuf = [&](int k, int slot) { return sB0 + (2 * k + slot) * bufn + 4; };
+  // the boundary waves' hand-off: store the quad's b and J write-through into
+  // exchange slot `slot`, drain, raise the wave's flag(s) to `tag`
+  auto publish = [&](int slot, const float (&b)[4], const float (&j)[4], unsigned tag) {
+    if (nb_up) {
+      st4_sc1(rx, xoff(slot, 0, tile, 0), b);
+      st4_sc1(rx, xoff(slot, 1, tile, 0), j);
+    }
+    if (nb_dn) {
+      st4_sc1(rx, xoff(slot, 0, tile, 1), b);
+      st4_sc1(rx, xoff(slot, 1, tile, 1), j);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      if (nb_up) st_flag(flags + (tile * 2) * wpr + wj, tag);
+      if (nb_dn) st_flag(flags + (tile * 2 + 1) * wpr + wj, tag);
+    }
+  };
+  // ... and wait until the neighbours' flags over this wave's columns reach
+  // `tag` (their rows are then read with sc1 loads)
+  auto await_rows = [&](unsigned tag) {
+    if (nb_up) wave_wait(flags + ((tile - 1) * 2 + 1) * wpr + fj, nfl, tag, err);
+    if (nb_dn) wave_wait(flags + ((tile + 1) * 2) * wpr + fj, nfl, tag, err);
+  };
+
+  // ---- prologue: dictionary, zero pads, codes, the tile's b / J into LDS
+  // buffer 0, boundary rows into exchange slot 1 (as if step -1's output),
+  // then the neighbours' rows for step 0
+  stage_rows(a.rows, rows_floats(a.E, true), sTC);
+  stage_rows(a.dl, 16 * a.es, sL);
+  stage_rows(a.tu, 9 * a.ts, sTu);
+  for (int i = threadIdx.x; i < 4 * (a.rt + 1); i += blockDim.x) {
+    const int buf = i / (a.rt + 1), r = i % (a.rt + 1);
+    *reinterpret_cast<f4a*>(sB0 + buf * bufn + r * xs) = f4a{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  CodeWin6 cw;
+  if (valid) {
+    load_codes6(a.code, wp, y, x0, cw);
+    const long long off = (long long)y * wp + x0;
+    const f4a b = *reinterpret_cast<const f4a*>(a.b_in + off);
+    const f4a j = *reinterpret_cast<const f4a*>(a.j_in + off);
+    *reinterpret_cast<f4a*>(sbuf(0, 0) + ty * xs + x0) = b;
+    *reinterpret_cast<f4a*>(sbuf(1, 0) + ty * xs + x0) = j;
+    if (nb_up || nb_dn) {
+      const float bv[4] = {b[0], b[1], b[2], b[3]}, jv[4] = {j[0], j[1], j[2], j[3]};
+      publish(1, bv, jv, a.epoch + 1);
+    }
+  }
+  // step 0's input mass (a block start with the previous launch's partials
+  // still pending: wave 0 reduces them, k_sum_finalize's tree)
+  const bool start0 = a.kstep0 % a.depth == 0;
+  if (start0 && a.in_partials && wave == 0) {
+    const float S = wave_reduce_partials(a.in_partials, a.in_n);
+    if (threadIdx.x == 0) {
+      sS[0] = S;
+      if (tile == 0 && a.in_sum_out) *a.in_sum_out = S;
+    }
+  }
+  __syncthreads();
+  if (start0 && a.in_partials && a.final_wait_read && threadIdx.x == 0)
+    __hip_atomic_fetch_add(a.sync + kResidentSyncRead, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  float inv = 1.0f;
+  if (start0)
+    inv = (1.0f / (a.in_partials ? sS[0] : a.in_sum ? *a.in_sum : 1.0f)) * a.bscale;
+
+  const int wave_part0 = (int)(((long long)tile * a.rt * tpr) >> 6);  // dense wave of wave 0
+  const int pi = wave_part0 + wave;
+  unsigned arrivals = a.arrive_base;
+  float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, best[4] = {0.0f, 0.0f, 0.0f, 0.0f}, local = 0.0f;
+  uint32_t arg[4] = {0u, 0u, 0u, 0u};
+
+  for (int t = 0; t < a.n; ++t) {
+    const int u = a.uz[t] & 15, z = a.uz[t] >> 4;
+    const int ci = t & 1, co = ci ^ 1;
+    const bool last = t == a.n - 1;
+    // ---- a block start inside the run: the exact mass of step t-1's belief
+    if (t > 0 && (a.kstep0 + t) % a.depth != 0) {
+      inv = 1.0f;
+    } else if (t > 0) {
+      if (wave == 0) {
+        arrivals += a.ntiles;
+        wave_wait(a.sync + kResidentSyncArrive, 1, arrivals, err);
+        const float S = wave_reduce_partials_sc1(
+            a.ring + (size_t)((t - 1) % kResidentRing) * a.nparts, a.nparts);
+        if (threadIdx.x == 0) sS[0] = S;
+      }
+      __syncthreads();
+      inv = (1.0f / sS[0]) * a.bscale;
+    }
+    PP2_RT(0);
+    local = 0.0f;
+    const bool bnd = nb_up || nb_dn;
+    // one quad of step t: window rows from LDS (step t-1), the neighbour rows
+    // taken at the end of step t-1, or 0 off the grid
+    auto step_quad = [&]() {
+      Win6 wb, wj;
+      if (ty > 0) {
+        row_lds(sbuf(0, ci) + (ty - 1) * xs, x0, wb.v[0]);
+        row_lds(sbuf(1, ci) + (ty - 1) * xs, x0, wj.v[0]);
+      } else if (nb_up) {  // the tile above's last row (its flags checked by the caller)
+        row_sc1(rx, xoff(co, 0, tile - 1, 1), wb.v[0]);
+        row_sc1(rx, xoff(co, 1, tile - 1, 1), wj.v[0]);
+      } else {
+        row_zero(wb.v[0]);
+        row_zero(wj.v[0]);
+      }
+      row_lds(sbuf(0, ci) + ty * xs, x0, wb.v[1]);
+      row_lds(sbuf(1, ci) + ty * xs, x0, wj.v[1]);
+      if (ty + 1 < a.rt && y + 1 < rows) {
+        row_lds(sbuf(0, ci) + (ty + 1) * xs, x0, wb.v[2]);
+        row_lds(sbuf(1, ci) + (ty + 1) * xs, x0, wj.v[2]);
+      } else if (nb_dn) {  // the tile below's first row
+        row_sc1(rx, xoff(co, 0, tile + 1, 0), wb.v[2]);
+        row_sc1(rx, xoff(co, 1, tile + 1, 0), wj.v[2]);
+      } else {
+        row_zero(wb.v[2]);
+        row_zero(wj.v[2]);
+      }
+      belief_any(u, sTu + u * a.ts, sL + z * a.es, inv, cw, wb, p, local);
+      sweep_vals(sTC, a.gamma, cw, wj, best, arg);
+      *reinterpret_cast<f4a*>(sbuf(0, co) + ty * xs + x0) = f4a{p[0], p[1], p[2], p[3]};
+      *reinterpret_cast<f4a*>(sbuf(1, co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
+    };
+    if (valid) {
+      // the boundary waves: the neighbours' step t-1 rows (published at the
+      // end of their step t-1), then the quad with issue priority, then
+      // publish -- the neighbours' next inputs
+      if (bnd) {
+        __builtin_amdgcn_s_setprio(2);  // 6.0 vs 7.4 us/step at 1024^2 without
+        await_rows(a.epoch + t + 1);
+      }
+      step_quad();
+      if (bnd) {
+        if (!last) publish(ci, p, best, a.epoch + t + 2);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      PP2_RT(1);
+    }
+    if (last) break;  // the last step's outputs are stored after the loop
+    // ---- mass partials of step t (dense map), sc1 into the ring
+    {
+      const float v = wave_sum(local);
+      if (lane == 0 && pi < a.nparts)
+        st_flag(reinterpret_cast<unsigned*>(a.ring + (size_t)(t % kResidentRing) * a.nparts + pi),
+                __float_as_uint(v));
+    }
+    // ---- arrive for the next step's block start (every wave drained first)
+    const bool arrive = (a.kstep0 + t + 1) % a.depth == 0;
+    if (arrive) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // also: this step's LDS writes before the next step's reads
+    if (arrive && threadIdx.x == 0)
+      __hip_atomic_fetch_add(a.sync + kResidentSyncArrive, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    PP2_RT(3);
+  }
+
+  // ---- the last step: b, J, A of the whole grid and its mass partials
+  if (valid) {
+    const long long off = (long long)y * wp + x0;
+    store4<true>(a.b_out + off, p);
+    store_ja<true>(a.j_out, a.A, off, best, arg);
+  }
+  if (a.final_wait_read && pi < a.nparts)
+    wave_wait(a.sync + kResidentSyncRead, 1, a.read_base + a.ntiles, err);
+  const float v = wave_sum(local);
+  if (lane == 0 && pi < a.nparts) a.out_partials[pi] = v;
+}
+
+}  // namespace
+
+size_t resident_lds_bytes(const Geom& g, int E, int es, int ts, int rt) {
+  return ((size_t)lds_span(rows_floats(E, true)) + lds_span(16 * es) + lds_span(9 * ts) +
+          4 * (4 + (size_t)rt * (g.wp + 4)) + 16) * sizeof(float);
+}
+
+bool resident_plan(const Geom& g, int E, int es, int ts, int ncus, ResidentPlan* p) {
+  if (E <= 0 || g.rows <= 0 || g.wp % 256 != 0 || ncus <= 0) return false;
+  const int rt = (g.rows + ncus - 1) / ncus;
+  const long long threads = (long long)rt * (g.wp / 4);
+  if (threads > 1024) return false;
+  const size_t lds = resident_lds_bytes(g, E, es, ts, rt);
+  if (lds > kDictLdsMaxBytes) return false;
+  static unsigned long long attr = 0;
+  allow_lds(reinterpret_cast<const void*>(&k_loop_resident), attr);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_loop_resident, (int)threads, lds) !=
+          hipSuccess ||
+      nb < 1) {
+    (void)hipGetLastError();
+    return false;
+  }
+  p->rt = rt;
+  p->ntiles = (g.rows + rt - 1) / rt;
+  p->threads = (int)threads;
+  p->lds = lds;
+  p->flag_words = 2 * p->ntiles * (g.wp / 256);
+  return p->ntiles <= ncus;
+}
+
+hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a) {
+  if (a.n < 1 || a.n > kResidentMaxSteps || a.ntiles != p.ntiles || a.rt != p.rt ||
+      a.depth < 1 || a.depth > kResidentRing - 2)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_loop_resident, dim3(p.ntiles), dim3(p.threads), p.lds, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace pp2
+
+#ifdef PP2_RES_TRACE
+extern "C" int pp2_debug_resident_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pp2::g_rtrace), sizeof(pp2::g_rtrace)) == hipSuccess
+             ? 0 : 2;
+}
+#endif

@@ -16,6 +16,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -207,6 +208,8 @@ int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(PP2_EHIP, "hipStreamCreate failed"));
   c->stream = c->own_stream;
+  if (hipDeviceGetAttribute(&c->ncus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    c->ncus = 0;
 
   const size_t map_bytes = (size_t)grows * width;
   if (hipMalloc(&c->d_map, map_bytes) != hipSuccess)
@@ -395,6 +398,11 @@ int build_model_dict(pp2_ctx* c) {
                         c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (bad) return PP2_OK;
+  bool t_finite = true;
+  for (int e = 0; e < E && t_finite; ++e)
+    for (int a = 0; a < 9; ++a)
+      for (int i = 0; i < 9; ++i)
+        if (!std::isfinite(dh[(size_t)e * pp2::kDictRow + a * 10 + i])) t_finite = false;
   // LDS-layout rows: sparse when every T entry off the base-kernel support is
   // +0.0 (always so for generated models), else the full [a][T..,C] rows
   // They also drop the T == 0 terms of the Bellman backup, which equals the
@@ -481,6 +489,7 @@ int build_model_dict(pp2_ctx* c) {
                         c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->dict_sparse = sparse;
+  c->dict_t_finite = t_finite;
   c->dict_n = E;
   return PP2_OK;
 }
@@ -729,6 +738,136 @@ static int loop_pair(pp2_ctx* c, uint8_t u1, uint8_t z1, uint8_t u2, uint8_t z2)
   return PP2_OK;
 }
 
+// ---------------------------------------------------------------- resident loop
+static void resident_free(pp2_ctx* c) {
+  for (void* p : {(void*)c->res_sync, (void*)c->res_ring, (void*)c->res_xch})
+    if (p) (void)hipFree(p);
+  c->res_sync = nullptr;
+  c->res_ring = nullptr;
+  c->res_xch = nullptr;
+  c->res_ok = false;
+  c->res_plan_e = -1;
+}
+
+// Whether pp2_loop_run takes the tile-resident loop (pp2_resident.hip): an
+// unsharded context with a sparse coded model (finite T: the kernel's zero
+// padded edges multiply T by +0), a normalisation block that fits the
+// partial ring, and a geometry resident_plan accepts.  (Re)allocates the
+// plan's sync words, partial ring and exchange rows when the dictionary
+// changes size.
+static bool resident_ready(pp2_ctx* c) {
+  if (!c->resident || c->comm || c->group || !coded_active(c) || !c->dict_sparse ||
+      !c->dict_t_finite || c->norm_block > pp2::kResidentRing - 2 || c->ncus <= 0)
+    return false;
+  if (c->res_plan_e == c->dict_n) return c->res_ok;
+  resident_free(c);
+  c->res_plan_e = c->dict_n;
+  const int es = (c->dict_n + 3) & ~3;
+  const int ts = (c->dict_n * pp2::tu_width(true) + 3) & ~3;
+  pp2::ResidentPlan p;
+  if (!pp2::resident_plan(c->g, c->dict_n, es, ts, c->ncus, &p)) return false;
+  const size_t sync_b = (size_t)(pp2::kResidentSyncFlags + p.flag_words) * sizeof(unsigned);
+  const size_t ring_b = (size_t)pp2::kResidentRing * pp2::mass_partials(c->g, 4) * sizeof(float);
+  const size_t xch_b = pp2::resident_xch_floats(c->g, p.ntiles) * sizeof(float);
+  if (hipMalloc(&c->res_sync, sync_b) != hipSuccess || hipMalloc(&c->res_ring, ring_b) != hipSuccess ||
+      hipMalloc(&c->res_xch, xch_b) != hipSuccess ||
+      hipMemsetAsync(c->res_sync, 0, sync_b, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->res_ring, 0, ring_b, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->res_xch, 0, xch_b, c->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    resident_free(c);
+    c->res_plan_e = c->dict_n;
+    return false;
+  }
+  c->res_epoch = c->res_arrive = c->res_read = 0;
+  c->res_plan = p;
+  c->res_ok = true;
+  return true;
+}
+
+// n loop steps in ceil(n / kResidentMaxSteps) resident launches, with the
+// state transitions of n blocked_loop_step calls (bcur, jcur, kstep, the
+// pending mass of the final belief).
+static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
+  for (int i = 0; i < n; ++i)
+    if (us[i] > 8 || zs[i] > 15)
+      return set_err(PP2_EINVAL, "action %u / observation %u out of range", us[i], zs[i]);
+  const pp2::ResidentPlan& p = c->res_plan;
+  const int depth = c->norm_block;
+  const int nparts = pp2::mass_partials(c->g, 4);
+  std::unique_ptr<pp2::ResidentRun> run(new pp2::ResidentRun());
+  pp2::ResidentRun& a = *run;
+  for (int i = 0; i < n;) {
+    const int m = std::min(n - i, pp2::kResidentMaxSteps);
+    const int bc = c->bcur, jc = c->jcur, bf = (bc + m) & 1, jf = (jc + m) & 1;
+    const bool start0 = c->kstep == 0;
+    const bool fold = start0 && c->pending[bc];
+    a.g = c->g;
+    a.gamma = c->gamma;
+    a.E = c->dict_n;
+    a.es = (c->dict_n + 3) & ~3;
+    a.ts = (c->dict_n * pp2::tu_width(true) + 3) & ~3;
+    a.code = c->d_code;
+    a.rows = c->d_rows;
+    a.dl = c->d_dl;
+    a.tu = c->d_tu;
+    a.b_in = c->b[bc].v.p;
+    a.j_in = c->J[jc].v.p;
+    a.b_out = c->b[bf].v.p;  // == b_in for even m: each lane reads its cells first
+    a.j_out = c->J[jf].v.p;
+    a.xch = c->res_xch;
+    a.A = c->A;
+    a.n = m;
+    a.kstep0 = c->kstep;
+    a.depth = depth;
+    a.rt = p.rt;
+    a.ntiles = p.ntiles;
+    a.nparts = nparts;
+    a.bscale = depth == 1 ? 1.0f : kBlockScale;
+    a.in_partials = fold ? c->pbuf[bc] : nullptr;
+    a.in_n = c->pcount[bc];
+    a.in_sum_out = fold ? c->bsum + bc : nullptr;
+    a.in_sum = start0 && !fold ? c->bsum + bc : nullptr;
+    a.ring = c->res_ring;
+    a.out_partials = c->pbuf[bf];
+    a.sync = c->res_sync;
+    a.epoch = c->res_epoch;
+    a.arrive_base = c->res_arrive;
+    a.read_base = c->res_read;
+    a.final_wait_read = fold && bf == bc;
+    for (int k = 0; k < m; ++k) a.uz[k] = (uint8_t)(us[i + k] | (zs[i + k] << 4));
+    HIPCHK(pp2::launch_loop_resident(c->stream, p, a));
+    int arrivals = 0;
+    for (int t = 0; t + 1 < m; ++t) arrivals += (c->kstep + t + 1) % depth == 0;
+    c->res_epoch += (unsigned)m + 1u;
+    c->res_arrive += (unsigned)(arrivals * p.ntiles);
+    if (a.final_wait_read) c->res_read += (unsigned)p.ntiles;
+    c->res_used = true;
+    c->pending[bf ^ 1] = false;
+    c->pending[bf] = true;
+    c->pcount[bf] = nparts;
+    c->bcur = bf;
+    c->jcur = jf;
+    c->kstep = (c->kstep + m) % depth;
+    i += m;
+  }
+  return PP2_OK;
+}
+
+// After a stream sync: a resident launch that timed out (a tile never got a
+// CU) left garbage; report it and fall back to the launch-per-step paths.
+static int resident_check(pp2_ctx* c) {
+  if (!c->res_used || !c->res_sync) return PP2_OK;
+  c->res_used = false;
+  unsigned e = 0;
+  HIPCHK(hipMemcpy(&e, c->res_sync + pp2::kResidentSyncErr, sizeof(e), hipMemcpyDeviceToHost));
+  if (!e) return PP2_OK;
+  resident_free(c);
+  c->resident = 0;
+  return set_err(PP2_EHIP, "resident loop: a workgroup wait timed out (grid not co-resident); "
+                 "results of that run are invalid, the context now uses per-step launches");
+}
+
 // =========================================================================== C ABI
 extern "C" {
 
@@ -791,6 +930,7 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->rpartials) (void)hipFree(c->rpartials);
   if (c->staging) (void)hipFree(c->staging);
   if (c->code_alloc) (void)hipFree(c->code_alloc);
+  resident_free(c);
   for (float* p : {c->d_dict, c->d_rows, c->d_dl, c->d_tu})
     if (p) (void)hipFree(p);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -809,7 +949,7 @@ int pp2_synchronize(pp2_ctx* c) {
   DeviceGuard dg(c->device);
   if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  return PP2_OK;
+  return resident_check(c);
 }
 
 int pp2_get_geometry(pp2_ctx* c, uint32_t* rows, uint32_t* width,
@@ -828,6 +968,10 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
     case PP2_TUNE_CODED_MODEL: c->use_coded = value != 0; return PP2_OK;
+    case PP2_TUNE_RESIDENT:
+      if (value < 0 || value > 1) return set_err(PP2_EINVAL, "resident %d not in [0, 1]", value);
+      c->resident = value;
+      return PP2_OK;
     case PP2_TUNE_STEP_PAIRS:
       if (value < 0 || value > 2) return set_err(PP2_EINVAL, "step pairs %d not in [0, 2]", value);
       c->step_pairs = value;
@@ -1047,7 +1191,7 @@ int pp2_loop_steps_per_launch(pp2_ctx* c, int* steps) {
   CHECK(check_ctx(c));
   if (!steps) return set_err(PP2_EINVAL, "steps is null");
   DeviceGuard dg(c->device);
-  *steps = pairs_apply(c) ? 2 : 1;
+  *steps = resident_ready(c) ? pp2::kResidentMaxSteps : pairs_apply(c) ? 2 : 1;
   return PP2_OK;
 }
 
@@ -1055,6 +1199,7 @@ int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
   CHECK(check_model(c));
   if (n < 0 || (n > 0 && (!us || !zs))) return set_err(PP2_EINVAL, "bad trajectory");
   DeviceGuard dg(c->device);
+  if (n >= 2 && resident_ready(c)) return loop_resident(c, n, us, zs);
   for (int i = 0; i < n;) {
     if (i + 1 < n && can_pair(c)) {
       CHECK(loop_pair(c, us[i], zs[i], us[i + 1], zs[i + 1]));

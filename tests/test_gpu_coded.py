@@ -249,6 +249,7 @@ def test_step_pairs_equal_single_steps(pp2, H, W, block):
     with a, b:
         b.set_tuning(b.TUNE_STEP_PAIRS, 0)
         for c in (a, b):
+            c.set_tuning(c.TUNE_RESIDENT, 0)  # pairs, not the resident loop (test_gpu_resident.py)
             c.model_generate()
             assert c.model_dict_info()[1]
             c.set_tuning(c.TUNE_NORM_BLOCK, block)

@@ -1,0 +1,154 @@
+"""GPU: the tile-resident loop (pp2_resident.hip) -- pp2_loop_run's whole
+trajectory in one launch, one tile of whole rows per CU kept in LDS,
+neighbour rows handed over by per-wave flags, block-start masses behind an
+arrival counter.
+
+The bar is bit equality with the one-launch-per-step path (which equals the
+dense path and the oracle: test_gpu_coded.py, test_gpu_parity.py): raw
+beliefs, masses, values and actions after every run, across runs of odd and
+even length (the last step's partials land in the input's buffer on even
+runs with a pending mass), block boundaries inside and across launches,
+normalisation blocks 1..8, partial last tiles, padded widths and runs longer
+than one launch (2048 steps).
+"""
+import numpy as np
+import pytest
+
+from conftest import GAMMA
+
+pytestmark = pytest.mark.gpu
+
+RESIDENT_STEPS = 2048
+
+
+@pytest.fixture(scope="module")
+def pp2():
+    import path_planning_2d_amd as P
+    assert P.device_count() >= 1, "no GPU visible"
+    return P
+
+
+def _pair(pp2, H, W, block, seed):
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(H, W, seed)
+    goal = S.synth_goal(grid)
+    a = pp2.GridContext(grid, goal, gamma=float(GAMMA))
+    b = pp2.GridContext(grid, goal, gamma=float(GAMMA))
+    b.set_tuning(b.TUNE_RESIDENT, 0)
+    b.set_tuning(b.TUNE_STEP_PAIRS, 0)
+    b0 = S.uniform_belief(grid)
+    for c in (a, b):
+        c.model_generate()
+        assert c.model_dict_info()[1]
+        c.set_tuning(c.TUNE_NORM_BLOCK, block)
+        c.belief_set(b0)
+        c.mdp_reset()
+    return grid, a, b
+
+
+def _same(a, b, what):
+    ra, ma = a.belief_get_raw()
+    rb, mb = b.belief_get_raw()
+    np.testing.assert_array_equal(ra.view(np.uint32), rb.view(np.uint32),
+                                  err_msg=f"raw belief {what}")
+    assert np.float32(ma).view(np.uint32) == np.float32(mb).view(np.uint32), (what, ma, mb)
+    Ja, Aa = a.mdp_get()
+    Jb, Ab = b.mdp_get()
+    np.testing.assert_array_equal(Ja.view(np.uint32), Jb.view(np.uint32), err_msg=f"J {what}")
+    np.testing.assert_array_equal(Aa, Ab, err_msg=f"A {what}")
+
+
+# (H, W): the 1024^2 bench grid (4 rows per tile), 2-row and 1-row tiles, a
+# partial last tile (700 rows over 256 CUs: 3-row tiles), a padded width
+GEOMS = [(1024, 1024), (512, 512), (256, 1024), (700, 768), (1024, 1022), (300, 256)]
+
+
+@pytest.mark.parametrize("block", [8, 5, 1])
+@pytest.mark.parametrize("H,W", GEOMS)
+def test_resident_equals_single_steps(pp2, H, W, block):
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, H, W, block, H * 7 + W)
+    with a, b:
+        assert a.loop_steps_per_launch() == RESIDENT_STEPS, "resident loop not selected"
+        assert b.loop_steps_per_launch() == 1
+        us, zs, _ = S.synth_trajectory(grid, 40, seed=5)
+        # chunks: even and odd lengths, starting on and off block boundaries
+        for lo, hi in ((0, 2), (2, 5), (5, 6), (6, 16), (16, 40)):
+            a.loop_run(us[lo:hi], zs[lo:hi])
+            b.loop_run(us[lo:hi], zs[lo:hi])
+            a.synchronize()
+            _same(a, b, f"after {hi} steps")
+
+
+def test_resident_interleaved_with_other_ops(pp2):
+    """Single loop steps, belief-only updates, sweeps and a belief_set between
+    resident runs: the context's pipeline state (pending masses, block phase,
+    ping-pong parities) stays consistent."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 1024, 1024, 8, 11)
+    with a, b:
+        us, zs, _ = S.synth_trajectory(grid, 40, seed=9)
+        for c in (a, b):
+            c.loop_run(us[:7], zs[:7])
+            c.loop_step(int(us[7]), int(zs[7]))
+            c.loop_run(us[8:12], zs[8:12])
+            c.belief_update(int(us[12]), int(zs[12]))
+            c.loop_run(us[13:20], zs[13:20])
+            c.mdp_sweep(3)
+            c.loop_run(us[20:30], zs[20:30])
+        _same(a, b, "after mixed ops")
+        b0 = S.uniform_belief(grid)
+        for c in (a, b):
+            c.belief_set(b0)
+            c.loop_run(us[30:40], zs[30:40])
+        _same(a, b, "after belief_set")
+
+
+def test_resident_multi_launch(pp2):
+    """A run longer than one launch (2048 steps): three launches, the epoch
+    counters carried over, equal to 4100 single-step launches."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 256, 256, 8, 3)
+    with a, b:
+        us, zs, _ = S.synth_trajectory(grid, 4100, seed=2)
+        a.loop_run(us, zs)
+        b.loop_run(us, zs)
+        a.synchronize()
+        _same(a, b, "after 4100 steps")
+        a.loop_run(us[:33], zs[:33])
+        b.loop_run(us[:33], zs[:33])
+        _same(a, b, "after a further 33 steps")
+
+
+def test_resident_matches_oracle_1024(pp2, oracle):
+    """The 1024^2 bench grid: 16 resident steps against the oracle's
+    fp64-normalised loop (J/A bit-exact, belief rel 1e-5 above a 1e-30 floor:
+    cells the FTZ build drops may keep ~1e-36-scale values here)."""
+    from path_planning_2d_amd import synthetic as S
+    O = oracle
+    H = W = 1024
+    grid = S.synth_grid(H, W, H)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 16, seed=42)
+    T, L, R = O.model_pomdp(grid, goal)
+    _, C = O.model_mdp(grid, goal)
+    bo = S.uniform_belief(grid)
+    J = np.zeros(H * W, np.float32)
+    for k in range(16):
+        bo = O.belief_step(H, W, T, L, bo, us[k], zs[k], mode="f64")
+        J, A = O.mdp_sweep(H, W, GAMMA, T, C, J)
+    with pp2.GridContext(grid, goal, gamma=float(GAMMA)) as c:
+        c.model_generate()
+        c.belief_set(S.uniform_belief(grid))
+        c.mdp_reset()
+        assert c.loop_steps_per_launch() == RESIDENT_STEPS
+        c.loop_run(us, zs)
+        c.synchronize()
+        Jd, Ad = c.mdp_get()
+        bd = c.belief_get()
+    np.testing.assert_array_equal(Jd.reshape(-1), J.reshape(-1))
+    np.testing.assert_array_equal(Ad.reshape(-1), A.reshape(-1))
+    bo = np.asarray(bo, np.float32).reshape(-1)
+    bd = bd.reshape(-1)
+    big = np.abs(bo) > 1e-30
+    np.testing.assert_allclose(bd[big], bo[big], rtol=1e-5, atol=0)

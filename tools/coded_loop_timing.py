@@ -9,7 +9,15 @@ def main():
     import torch
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S
-    N = int(os.environ.get("PP2_N", "1024"))
+    for N in [int(v) for v in os.environ.get("PP2_NS", os.environ.get("PP2_N", "1024")).split(",")]:
+        for res in [int(v) for v in os.environ.get("PP2_RESIDENT", "1,0").split(",")]:
+            one(N, res)
+
+
+def one(N, resident):
+    import torch
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
     reps = int(os.environ.get("PP2_REPS", "100"))
     grid = S.synth_grid(N, N, seed=N)
     goal = S.synth_goal(grid)
@@ -18,11 +26,13 @@ def main():
     with P.GridContext(grid, goal, gamma=0.95) as ctx:
         ctx.set_stream(stream.cuda_stream)
         ctx.set_tuning(ctx.TUNE_STEP_PAIRS, int(os.environ.get("PP2_PAIRS", "1")))
+        ctx.set_tuning(ctx.TUNE_RESIDENT, resident)
         ctx.model_generate()
         ctx.belief_set(S.uniform_belief(grid))
         ctx.mdp_reset()
         ctx.loop_run(us[:10], zs[:10])
-        print(f"N={N} steps/launch={ctx.loop_steps_per_launch()}", flush=True)
+        ctx.synchronize()
+        print(f"N={N} resident={resident} steps/launch={ctx.loop_steps_per_launch()}", flush=True)
         for what in ("loop", "sweep"):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -33,6 +43,7 @@ def main():
                 ctx.mdp_sweep(reps)
             e1.record(stream)
             torch.cuda.synchronize()
+            ctx.synchronize()
             print(f"{what}: {e0.elapsed_time(e1) / reps * 1e3:.2f} us/step", flush=True)
 
 
