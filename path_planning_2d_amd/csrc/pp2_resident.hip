@@ -174,11 +174,24 @@ __device__ __forceinline__ void belief_any(int u, const float* sTu, const float*
   }
 }
 
-// One window row (x0 - 1 .. x0 + 4) from a zero-padded LDS row.
+// One window row (x0 - 1 .. x0 + 4) from a zero-padded LDS row: the lane's
+// aligned 16 B, and x0 - 1 / x0 + 4 from the neighbouring lanes' quads by DPP
+// wave shifts (wave_shr:1 / wave_shl:1; a wave holds 64 consecutive quads of
+// one row).  Lanes 0 and 63 have no source lane and keep the DPP's `old`
+// operand, the edge dword they read themselves (one 2-lane ds_read_b32 --
+// every lane reading its own edge dwords, at a 16-B lane stride, costs a
+// 4-way bank conflict per read).
 __device__ __forceinline__ void row_lds(const float* row, int x0, float (&v)[6]) {
   const float* p = row + x0;
   const f4a m = *reinterpret_cast<const f4a*>(p);
-  v[0] = p[-1]; v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3]; v[5] = p[4];
+  const int lane = threadIdx.x & 63;
+  float e = 0.0f;
+  if (lane == 0 || lane == 63) e = p[lane == 0 ? -1 : 4];
+  v[0] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(e), __float_as_int(m[3]),
+                                                    0x138, 0xf, 0xf, false));
+  v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3];
+  v[5] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(e), __float_as_int(m[0]),
+                                                    0x130, 0xf, 0xf, false));
 }
 __device__ __forceinline__ void row_zero(float (&v)[6]) {
 #pragma unroll
