@@ -343,7 +343,7 @@ __global__ __launch_bounds__(kPQ * kQuarter, 4) void k_loop_pair_coded(
         belief_u(u1, g, sT1, sL1, inv0, cw, w, x0, p, local);
         load_win6(J_in, g.wp, y, x0, le, re, w);
         uint32_t arg[4];
-        sweep_vals(sTC, gamma, cw, w, best, arg);
+        sweep_vals<false>(sTC, gamma, cw, w, best, arg);  // step 1 stores no actions
       }
       *reinterpret_cast<f4a*>(sB + 4 * qd) = f4a{p[0], p[1], p[2], p[3]};
       *reinterpret_cast<f4a*>(sJ + 4 * qd) = f4a{best[0], best[1], best[2], best[3]};

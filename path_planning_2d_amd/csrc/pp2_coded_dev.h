@@ -51,7 +51,12 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, int n,
 }
 
 // Bellman backup of 4 cells from their codes (k_mdp_sweep's arithmetic).
-template <bool SPARSE>
+// ARG = false: values only (the resident loop's intermediate steps store no
+// actions), best = minnum over the actions -- the same value as the strict-<
+// scan, since every cost is an fmaf result (canonical, flushed, never -0 or
+// NaN under the sparse rows' preconditions); one v_min per action instead of
+// a compare and two selects.
+template <bool SPARSE, bool ARG = true>
 __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&cc)[4],
                                              const float (&jn)[9][4], float gamma,
                                              float (&best)[4], uint32_t (&arg)[4]) {
@@ -84,7 +89,11 @@ __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);
-        if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
+        if constexpr (ARG) {
+          if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
+        } else {
+          best[k] = __builtin_fminf(best[k], cost);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -297,6 +306,7 @@ __device__ __forceinline__ void belief_u(int u, const Geom& g, const float* sTu,
   }
 }
 
+template <bool ARG = true>
 __device__ __forceinline__ void sweep_vals(const float* sTC, float gamma, const CodeWin6& cw,
                                            const Win6& w, float (&best)[4], uint32_t (&arg)[4]) {
   float jn[9][4];
@@ -305,7 +315,7 @@ __device__ __forceinline__ void sweep_vals(const float* sTC, float gamma, const 
 #pragma unroll
     for (int k = 0; k < 4; ++k) jn[i][k] = w.v[i / 3][k + i % 3];
   const uint32_t cc[4] = {cw.m0[1] & 0xffffu, cw.m0[1] >> 16, cw.m1[1] & 0xffffu, cw.m1[1] >> 16};
-  coded_sweep4<true>(sTC, cc, jn, gamma, best, arg);
+  coded_sweep4<true, ARG>(sTC, cc, jn, gamma, best, arg);
 }
 
 }  // namespace

@@ -359,7 +359,8 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
         row_zero(wj.v[2]);
       }
       belief_any(u, sTu + u * a.ts, sL + z * a.es, inv, cw, wb, p, local);
-      sweep_vals(sTC, a.gamma, cw, wj, best, arg);
+      if (last) sweep_vals<true>(sTC, a.gamma, cw, wj, best, arg);  // actions: last step only
+      else sweep_vals<false>(sTC, a.gamma, cw, wj, best, arg);
       *reinterpret_cast<f4a*>(sbuf(0, co) + ty * xs + x0) = f4a{p[0], p[1], p[2], p[3]};
       *reinterpret_cast<f4a*>(sbuf(1, co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
     };
