@@ -167,6 +167,10 @@ int pp2_model_dict_info(pp2_ctx* ctx, int* entries, int* active);
  * coded model whose grid has a 4096-cell tile per CU; unsharded, RCCL row
  * shard or shard-group member), else 1. */
 int pp2_loop_steps_per_launch(pp2_ctx* ctx, int* steps);
+/* Diagnostics: resident launches so far on this context -- tile-resident loop
+ * launches (pp2_loop_run) and resident MDP-solve launches (pp2_mdp_solve);
+ * either pointer may be NULL.  No reference counterpart. */
+int pp2_resident_launches(pp2_ctx* ctx, int* loop_launches, int* solve_launches);
 
 /* ---------------------------------------------------------------- belief
  * The belief lives on the device with deferred normalisation: each update

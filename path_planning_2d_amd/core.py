@@ -116,6 +116,13 @@ class GridContext:
         call("pp2_model_dict_info", self._h, C.byref(e), C.byref(a))
         return e.value, bool(a.value)
 
+    def resident_launches(self):
+        """(tile-resident loop launches, resident MDP-solve launches) so far."""
+        lo = C.c_int()
+        so = C.c_int()
+        call("pp2_resident_launches", self._h, C.byref(lo), C.byref(so))
+        return lo.value, so.value
+
     def loop_steps_per_launch(self) -> int:
         """Loop steps one kernel launch of pp2_loop_run covers (1 or 2)."""
         n = C.c_int(0)

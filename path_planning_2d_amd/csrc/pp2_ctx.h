@@ -132,6 +132,13 @@ struct pp2_ctx {
   float* res_xch = nullptr;        // exchange rows
   unsigned res_epoch = 0, res_arrive = 0, res_read = 0;  // epoch-tagged counters
   bool res_used = false;           // a resident launch since the last error check
+  int sol_plan_e = -1;             // resident MDP solve (k_sweep_resident): plan for dict_n
+  bool sol_ok = false;
+  pp2::ResidentPlan sol_plan{};
+  int res_ntiles = 0;              // tiles the sync words / exchange rows were sized for
+  float* res_tmax = nullptr;       // 2 x ntiles per-tile convergence maxima
+  int* res_out = nullptr;          // {sweeps, norm bits} of a resident solve launch
+  int res_launches = 0, sol_launches = 0;  // pp2_resident_launches
 
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;

@@ -247,7 +247,31 @@ struct ResidentRun {
   int final_wait_read;       // out_partials == in_partials: the last step waits for readers
   uint8_t uz[kResidentMaxSteps];  // u | z << 4 per step
 };
+// Resident MDP solve (pp2_mdp_solve): sweeps in blocks of kSolveBlock, a
+// convergence check after each, at most max_blocks per launch.
+constexpr int kSolveBlock = 100;
+struct SweepRun {
+  Geom g;
+  float gamma;
+  int E;
+  const uint16_t* code;
+  const float* rows;
+  float *j0, *j1;      // sweep s reads J(s & 1 ? j1 : j0); the last J goes to the other
+  float* snap;         // convergence snapshot (read at start, written at the end)
+  uint8_t* A;
+  float* xch;
+  unsigned* sync;
+  float* tile_max;     // 2 x ntiles per-tile maxima
+  int* res;            // {sweeps done, norm bits}
+  unsigned epoch, arrive_base;
+  int rt, ntiles;
+  int max_blocks;      // blocks per launch
+  int cap_blocks;      // stop after this many blocks (0: no cap)
+  double thresh;       // stop when norm <= thresh
+};
 size_t resident_lds_bytes(const Geom& g, int E, int es, int ts, int rt);
+bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p);
+hipError_t launch_sweep_resident(hipStream_t st, const ResidentPlan& p, const SweepRun& a);
 inline size_t resident_xch_floats(const Geom& g, int ntiles) {
   return (size_t)8 * ntiles * (g.wp + 4) + 8;  // rows of 4 zero + wp floats, slack at the end
 }

@@ -409,6 +409,167 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   if (lane == 0 && pi < a.nparts) a.out_partials[pi] = v;
 }
 
+// ---------------------------------------------------------------- MDP solve
+// pp2_mdp_solve's value iteration (valueIteration, src/mdp/path_planning_2d.cu:
+// 207-269) as resident sweeps: the tiles of k_loop_resident carry J only (two
+// LDS buffers and the convergence snapshot), the edge rows of J cross CUs by
+// the same flags (exchange plane k = 1), and after every block of 100 sweeps
+// each tile publishes max |J - snapshot| over its cells; once the arrival
+// counter is full every tile reads all of them (the max is exact in any
+// order) and takes the same decision: stop when the norm is <= thresh or the
+// block cap is reached, else go on.  Actions are computed (and stored) on
+// each block's last sweep only; the last block's J, A and snapshot are
+// stored, and tile 0 writes {sweeps, norm bits} to res.
+__global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int wp = a.g.wp, rows = a.g.rows, tpr = wp >> 2, wpr = wp >> 8;
+  const int xs = wp + 4;
+  const int bufn = 4 + a.rt * xs;
+  float* sTC = lds;
+  float* sJ0 = sTC + lds_span(rows_floats(a.E, true));  // J buffers 0, 1, snapshot
+  float* sM = sJ0 + 3 * bufn;                              // per-wave maxima, decision
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x / tpr);
+  const int wj = __builtin_amdgcn_readfirstlane((threadIdx.x % tpr) >> 6);
+  const int x0 = (threadIdx.x % tpr) * 4;
+  const int y = tile * a.rt + ty;
+  const bool valid = y < rows;
+  const bool nb_up = valid && ty == 0 && tile > 0;
+  const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
+  unsigned* const flags = a.sync + kResidentSyncFlags;
+  unsigned* const err = a.sync + kResidentSyncErr;
+  const int fj = max(wj - 1, 0);
+  const int nfl = min(wj + 1, wpr - 1) - fj + 1;
+  const Rsrc rx = make_rsrc(a.xch);
+  auto xoff = [&](int slot, int tl, int side) {  // J rows: exchange plane k = 1
+    return (int)(((((((long long)slot * 2 + 1) * a.ntiles + tl) * 2 + side) * xs + 4) + x0) * 4);
+  };
+  auto sbuf = [&](int i) { return sJ0 + i * bufn + 4; };
+  auto publish = [&](int slot, const float (&j)[4], unsigned tag) {
+    if (nb_up) st4_sc1(rx, xoff(slot, tile, 0), j);
+    if (nb_dn) st4_sc1(rx, xoff(slot, tile, 1), j);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      if (nb_up) st_flag(flags + (tile * 2) * wpr + wj, tag);
+      if (nb_dn) st_flag(flags + (tile * 2 + 1) * wpr + wj, tag);
+    }
+  };
+
+  stage_rows(a.rows, rows_floats(a.E, true), sTC);
+  for (int i = threadIdx.x; i < 3 * (a.rt + 1); i += blockDim.x) {
+    const int buf = i / (a.rt + 1), r = i % (a.rt + 1);
+    *reinterpret_cast<f4a*>(sJ0 + buf * bufn + r * xs) = f4a{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  uint32_t c0 = 0, c1 = 0;  // the quad's codes
+  const long long goff = (long long)y * wp + x0;
+  if (valid) {
+    const uint2 m = *reinterpret_cast<const uint2*>(a.code + goff);
+    c0 = m.x;
+    c1 = m.y;
+    const f4a j = *reinterpret_cast<const f4a*>(a.j0 + goff);
+    *reinterpret_cast<f4a*>(sbuf(0) + ty * xs + x0) = j;
+    *reinterpret_cast<f4a*>(sbuf(2) + ty * xs + x0) = *reinterpret_cast<const f4a*>(a.snap + goff);
+    if (nb_up || nb_dn) {
+      const float jv[4] = {j[0], j[1], j[2], j[3]};
+      publish(1, jv, a.epoch + 1);
+    }
+  }
+  __syncthreads();
+
+  unsigned arrivals = a.arrive_base;
+  float best[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t arg[4] = {0u, 0u, 0u, 0u};
+  int s = 0, blk = 0;
+  float norm = 0.0f;
+  for (;; ++s) {
+    const int ci = s & 1, co = ci ^ 1;
+    const bool check = s % kSolveBlock == kSolveBlock - 1;
+    if (valid) {
+      if (nb_up || nb_dn) {
+        __builtin_amdgcn_s_setprio(2);
+        if (nb_up) wave_wait(flags + ((tile - 1) * 2 + 1) * wpr + fj, nfl, a.epoch + s + 1, err);
+        if (nb_dn) wave_wait(flags + ((tile + 1) * 2) * wpr + fj, nfl, a.epoch + s + 1, err);
+      }
+      Win6 w;
+      if (ty > 0) row_lds(sbuf(ci) + (ty - 1) * xs, x0, w.v[0]);
+      else if (nb_up) row_sc1(rx, xoff(co, tile - 1, 1), w.v[0]);
+      else row_zero(w.v[0]);
+      row_lds(sbuf(ci) + ty * xs, x0, w.v[1]);
+      if (ty + 1 < a.rt && y + 1 < rows) row_lds(sbuf(ci) + (ty + 1) * xs, x0, w.v[2]);
+      else if (nb_dn) row_sc1(rx, xoff(co, tile + 1, 0), w.v[2]);
+      else row_zero(w.v[2]);
+      float jn[9][4];
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) jn[i][k] = w.v[i / 3][k + i % 3];
+      const uint32_t cc[4] = {c0 & 0xffffu, c0 >> 16, c1 & 0xffffu, c1 >> 16};
+      if (check) coded_sweep4<true, true>(sTC, cc, jn, a.gamma, best, arg);
+      else coded_sweep4<true, false>(sTC, cc, jn, a.gamma, best, arg);
+      *reinterpret_cast<f4a*>(sbuf(co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
+      if (nb_up || nb_dn) {
+        publish(ci, best, a.epoch + s + 2);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    if (!check) {
+      __syncthreads();
+      continue;
+    }
+    // ---- end of a block: max |J - snapshot| over the tile, snapshot := J
+    float m = 0.0f;
+    if (valid) {
+      float* sn = sbuf(2) + ty * xs + x0;
+      const f4a old = *reinterpret_cast<const f4a*>(sn);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m = fmaxf(m, fabsf(old[k] - best[k]));
+      *reinterpret_cast<f4a*>(sn) = f4a{best[0], best[1], best[2], best[3]};
+    }
+    m = wave_max(m);
+    if (lane == 0) sM[wave] = m;
+    __syncthreads();
+    if (wave == 0) {
+      float tm = lane < (int)(blockDim.x >> 6) ? sM[lane] : 0.0f;
+      tm = wave_max(tm);
+      if (lane == 0)
+        st_flag(reinterpret_cast<unsigned*>(a.tile_max + (blk & 1) * a.ntiles + tile),
+                __float_as_uint(tm));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_fetch_add(a.sync + kResidentSyncArrive, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      arrivals += a.ntiles;
+      wave_wait(a.sync + kResidentSyncArrive, 1, arrivals, err);
+      const Rsrc rm = make_rsrc(a.tile_max + (blk & 1) * a.ntiles);
+      float g = 0.0f;
+      for (int i = lane; i < a.ntiles; i += 64) g = fmaxf(g, ld1_sc1(rm, 4 * i));
+      g = wave_max(g);
+      if (lane == 0) sM[16] = g;
+    }
+    __syncthreads();
+    norm = sM[16];
+    ++blk;
+    if (!((double)norm > a.thresh) || (a.cap_blocks > 0 && blk >= a.cap_blocks) ||
+        blk >= a.max_blocks)
+      break;
+  }
+  // ---- J, A and the snapshot of the last block; the result
+  const int done = s + 1;
+  if (valid) {
+    float* jo = (done & 1) ? a.j1 : a.j0;
+    store4<false>(jo + goff, best);
+    const uint32_t a4 = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    *reinterpret_cast<uint32_t*>(a.A + goff) = a4;
+    *reinterpret_cast<f4a*>(a.snap + goff) = f4a{best[0], best[1], best[2], best[3]};
+  }
+  if (tile == 0 && threadIdx.x == 0) {
+    a.res[0] = done;
+    a.res[1] = (int)__float_as_uint(norm);
+  }
+}
+
 }  // namespace
 
 size_t resident_lds_bytes(const Geom& g, int E, int es, int ts, int rt) {
@@ -445,6 +606,41 @@ hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const Res
       a.depth < 1 || a.depth > kResidentRing - 2)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_loop_resident, dim3(p.ntiles), dim3(p.threads), p.lds, st, a);
+  return hipGetLastError();
+}
+
+size_t solve_lds_bytes(const Geom& g, int E, int rt) {
+  return ((size_t)lds_span(rows_floats(E, true)) + 3 * (4 + (size_t)rt * (g.wp + 4)) + 32) *
+         sizeof(float);
+}
+
+bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p) {
+  if (E <= 0 || g.rows <= 0 || g.wp % 256 != 0 || ncus <= 0) return false;
+  const int rt = (g.rows + ncus - 1) / ncus;
+  const long long threads = (long long)rt * (g.wp / 4);
+  if (threads > 1024) return false;
+  const size_t lds = solve_lds_bytes(g, E, rt);
+  if (lds > kDictLdsMaxBytes) return false;
+  static unsigned long long attr = 0;
+  allow_lds(reinterpret_cast<const void*>(&k_sweep_resident), attr);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sweep_resident, (int)threads, lds) !=
+          hipSuccess ||
+      nb < 1) {
+    (void)hipGetLastError();
+    return false;
+  }
+  p->rt = rt;
+  p->ntiles = (g.rows + rt - 1) / rt;
+  p->threads = (int)threads;
+  p->lds = lds;
+  p->flag_words = 2 * p->ntiles * (g.wp / 256);
+  return p->ntiles <= ncus;
+}
+
+hipError_t launch_sweep_resident(hipStream_t st, const ResidentPlan& p, const SweepRun& a) {
+  if (a.max_blocks < 1 || a.ntiles != p.ntiles || a.rt != p.rt) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_sweep_resident, dim3(p.ntiles), dim3(p.threads), p.lds, st, a);
   return hipGetLastError();
 }
 

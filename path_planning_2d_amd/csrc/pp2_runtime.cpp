@@ -739,14 +739,63 @@ static int loop_pair(pp2_ctx* c, uint8_t u1, uint8_t z1, uint8_t u2, uint8_t z2)
 }
 
 // ---------------------------------------------------------------- resident loop
-static void resident_free(pp2_ctx* c) {
-  for (void* p : {(void*)c->res_sync, (void*)c->res_ring, (void*)c->res_xch})
+static void resident_free_buffers(pp2_ctx* c) {
+  for (void* p : {(void*)c->res_sync, (void*)c->res_ring, (void*)c->res_xch, (void*)c->res_tmax,
+                  (void*)c->res_out})
     if (p) (void)hipFree(p);
   c->res_sync = nullptr;
   c->res_ring = nullptr;
   c->res_xch = nullptr;
+  c->res_tmax = nullptr;
+  c->res_out = nullptr;
+  c->res_ntiles = 0;
+}
+
+static void resident_free(pp2_ctx* c) {
+  resident_free_buffers(c);
   c->res_ok = false;
   c->res_plan_e = -1;
+  c->sol_ok = false;
+  c->sol_plan_e = -1;
+}
+
+// Sync words, partial ring, exchange rows and solve scratch for plan p (both
+// resident kernels share them and the epoch counters; a plan with another
+// tile count reallocates and restarts the epochs).
+static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
+  if (c->res_sync && c->res_ntiles == p.ntiles) return true;
+  resident_free_buffers(c);
+  const size_t sync_b = (size_t)(pp2::kResidentSyncFlags + p.flag_words) * sizeof(unsigned);
+  const size_t ring_b = (size_t)pp2::kResidentRing * pp2::mass_partials(c->g, 4) * sizeof(float);
+  const size_t xch_b = pp2::resident_xch_floats(c->g, p.ntiles) * sizeof(float);
+  const size_t tmax_b = (size_t)2 * p.ntiles * sizeof(float);
+  if (hipMalloc(&c->res_sync, sync_b) != hipSuccess || hipMalloc(&c->res_ring, ring_b) != hipSuccess ||
+      hipMalloc(&c->res_xch, xch_b) != hipSuccess || hipMalloc(&c->res_tmax, tmax_b) != hipSuccess ||
+      hipMalloc(&c->res_out, 4 * sizeof(int)) != hipSuccess ||
+      hipMemsetAsync(c->res_sync, 0, sync_b, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->res_ring, 0, ring_b, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->res_xch, 0, xch_b, c->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    resident_free_buffers(c);
+    return false;
+  }
+  c->res_ntiles = p.ntiles;
+  c->res_epoch = c->res_arrive = c->res_read = 0;
+  return true;
+}
+
+// After a stream sync: a resident launch that timed out (a tile never got a
+// CU) left garbage; report it and fall back to the launch-per-step paths.
+static int resident_check(pp2_ctx* c) {
+  if (!c->res_used || !c->res_sync) return PP2_OK;
+  c->res_used = false;
+  unsigned e = 0;
+  HIPCHK(hipMemcpy(&e, c->res_sync + pp2::kResidentSyncErr, sizeof(e), hipMemcpyDeviceToHost));
+  if (!e) return PP2_OK;
+  resident_free(c);
+  c->resident = 0;
+  return set_err(PP2_EHIP, "resident loop: a workgroup wait timed out (grid not co-resident); "
+                 "results of that run are invalid, the context now uses per-step launches");
 }
 
 // Whether pp2_loop_run takes the tile-resident loop (pp2_resident.hip): an
@@ -759,30 +808,90 @@ static bool resident_ready(pp2_ctx* c) {
   if (!c->resident || c->comm || c->group || !coded_active(c) || !c->dict_sparse ||
       !c->dict_t_finite || c->norm_block > pp2::kResidentRing - 2 || c->ncus <= 0)
     return false;
-  if (c->res_plan_e == c->dict_n) return c->res_ok;
-  resident_free(c);
-  c->res_plan_e = c->dict_n;
-  const int es = (c->dict_n + 3) & ~3;
-  const int ts = (c->dict_n * pp2::tu_width(true) + 3) & ~3;
-  pp2::ResidentPlan p;
-  if (!pp2::resident_plan(c->g, c->dict_n, es, ts, c->ncus, &p)) return false;
-  const size_t sync_b = (size_t)(pp2::kResidentSyncFlags + p.flag_words) * sizeof(unsigned);
-  const size_t ring_b = (size_t)pp2::kResidentRing * pp2::mass_partials(c->g, 4) * sizeof(float);
-  const size_t xch_b = pp2::resident_xch_floats(c->g, p.ntiles) * sizeof(float);
-  if (hipMalloc(&c->res_sync, sync_b) != hipSuccess || hipMalloc(&c->res_ring, ring_b) != hipSuccess ||
-      hipMalloc(&c->res_xch, xch_b) != hipSuccess ||
-      hipMemsetAsync(c->res_sync, 0, sync_b, c->stream) != hipSuccess ||
-      hipMemsetAsync(c->res_ring, 0, ring_b, c->stream) != hipSuccess ||
-      hipMemsetAsync(c->res_xch, 0, xch_b, c->stream) != hipSuccess) {
-    (void)hipGetLastError();
-    resident_free(c);
+  if (c->res_plan_e != c->dict_n) {
     c->res_plan_e = c->dict_n;
-    return false;
+    c->res_ok = false;
+    const int es = (c->dict_n + 3) & ~3;
+    const int ts = (c->dict_n * pp2::tu_width(true) + 3) & ~3;
+    pp2::ResidentPlan p;
+    if (!pp2::resident_plan(c->g, c->dict_n, es, ts, c->ncus, &p)) return false;
+    c->res_plan = p;
+    c->res_ok = true;
   }
-  c->res_epoch = c->res_arrive = c->res_read = 0;
-  c->res_plan = p;
-  c->res_ok = true;
-  return true;
+  return c->res_ok && resident_buffers(c, c->res_plan);
+}
+
+// Whether pp2_mdp_solve runs as resident sweeps (k_sweep_resident): the
+// resident loop's conditions minus the belief's, and a plan for J alone.
+static bool solve_ready(pp2_ctx* c) {
+  if (!c->resident || c->comm || c->group || !coded_active(c) || !c->dict_sparse ||
+      c->ncus <= 0)
+    return false;
+  if (c->sol_plan_e != c->dict_n) {
+    c->sol_plan_e = c->dict_n;
+    c->sol_ok = false;
+    pp2::ResidentPlan p;
+    if (!pp2::solve_plan(c->g, c->dict_n, c->ncus, &p)) return false;
+    c->sol_plan = p;
+    c->sol_ok = true;
+  }
+  return c->sol_ok && resident_buffers(c, c->sol_plan);
+}
+
+// pp2_mdp_solve's driver (reset, then blocks of 100 sweeps until the
+// inf-norm change of a block is <= max_cost * 1e-3 or max_sweeps is reached)
+// on resident sweeps: <= 20 blocks per launch, the decision taken in-kernel;
+// one host read of {sweeps, norm} per launch.
+static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps,
+                          double* final_norm) {
+  const pp2::ResidentPlan& p = c->sol_plan;
+  const int cap_total = max_sweeps > 0 ? (max_sweeps + pp2::kSolveBlock - 1) / pp2::kSolveBlock : 0;
+  int blocks = 0, total = 0;
+  float norm = 0.0f;
+  for (;;) {
+    pp2::SweepRun a{};
+    a.g = c->g;
+    a.gamma = c->gamma;
+    a.E = c->dict_n;
+    a.code = c->d_code;
+    a.rows = c->d_rows;
+    a.j0 = c->J[c->jcur].v.p;
+    a.j1 = c->J[c->jcur ^ 1].v.p;
+    a.snap = c->Jsnap.v.p;
+    a.A = c->A;
+    a.xch = c->res_xch;
+    a.sync = c->res_sync;
+    a.tile_max = c->res_tmax;
+    a.res = c->res_out;
+    a.epoch = c->res_epoch;
+    a.arrive_base = c->res_arrive;
+    a.rt = p.rt;
+    a.ntiles = p.ntiles;
+    a.max_blocks = 20;
+    a.cap_blocks = cap_total ? cap_total - blocks : 0;
+    a.thresh = thresh;
+    HIPCHK(pp2::launch_sweep_resident(c->stream, p, a));
+    ++c->sol_launches;
+    int res[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(res, c->res_out, sizeof(res), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->res_used = true;
+    CHECK(resident_check(c));
+    const int done = res[0];
+    if (done <= 0 || done % pp2::kSolveBlock != 0)
+      return set_err(PP2_EHIP, "resident MDP solve returned %d sweeps", done);
+    std::memcpy(&norm, &res[1], sizeof(float));
+    total += done;
+    blocks += done / pp2::kSolveBlock;
+    c->res_epoch += (unsigned)done + 1u;
+    c->res_arrive += (unsigned)(done / pp2::kSolveBlock * p.ntiles);
+    c->jcur = (c->jcur + done) & 1;
+    if (cap_total && blocks >= cap_total) break;
+    if (!((double)norm > thresh)) break;
+  }
+  if (sweeps) *sweeps = total;
+  if (final_norm) *final_norm = (double)norm;
+  return PP2_OK;
 }
 
 // n loop steps in ceil(n / kResidentMaxSteps) resident launches, with the
@@ -837,6 +946,7 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
     a.final_wait_read = fold && bf == bc;
     for (int k = 0; k < m; ++k) a.uz[k] = (uint8_t)(us[i + k] | (zs[i + k] << 4));
     HIPCHK(pp2::launch_loop_resident(c->stream, p, a));
+    ++c->res_launches;
     int arrivals = 0;
     for (int t = 0; t + 1 < m; ++t) arrivals += (c->kstep + t + 1) % depth == 0;
     c->res_epoch += (unsigned)m + 1u;
@@ -852,20 +962,6 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
     i += m;
   }
   return PP2_OK;
-}
-
-// After a stream sync: a resident launch that timed out (a tile never got a
-// CU) left garbage; report it and fall back to the launch-per-step paths.
-static int resident_check(pp2_ctx* c) {
-  if (!c->res_used || !c->res_sync) return PP2_OK;
-  c->res_used = false;
-  unsigned e = 0;
-  HIPCHK(hipMemcpy(&e, c->res_sync + pp2::kResidentSyncErr, sizeof(e), hipMemcpyDeviceToHost));
-  if (!e) return PP2_OK;
-  resident_free(c);
-  c->resident = 0;
-  return set_err(PP2_EHIP, "resident loop: a workgroup wait timed out (grid not co-resident); "
-                 "results of that run are invalid, the context now uses per-step launches");
 }
 
 // =========================================================================== C ABI
@@ -1150,6 +1246,10 @@ int pp2_mdp_solve(pp2_ctx* c, int max_sweeps, int* sweeps, double* final_norm) {
   CHECK(pp2_mdp_reset(c));
   // double max_optimal_cost = 5.0/(1.0-discount_factor) (path_planning_2d.cu:221)
   const double max_cost = 5.0 / (1.0 - (double)c->gamma);
+  if (solve_ready(c)) {
+    break_pipeline(c);  // J changes: the loop's deep halo rows are stale
+    return solve_resident(c, max_sweeps, max_cost * 1e-3, sweeps, final_norm);
+  }
   int total = 0;
   double norm = 0.0;
   do {
@@ -1192,6 +1292,13 @@ int pp2_loop_steps_per_launch(pp2_ctx* c, int* steps) {
   if (!steps) return set_err(PP2_EINVAL, "steps is null");
   DeviceGuard dg(c->device);
   *steps = resident_ready(c) ? pp2::kResidentMaxSteps : pairs_apply(c) ? 2 : 1;
+  return PP2_OK;
+}
+
+int pp2_resident_launches(pp2_ctx* c, int* loop_launches, int* solve_launches) {
+  CHECK(check_ctx(c));
+  if (loop_launches) *loop_launches = c->res_launches;
+  if (solve_launches) *solve_launches = c->sol_launches;
   return PP2_OK;
 }
 

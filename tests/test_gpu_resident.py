@@ -73,10 +73,13 @@ def test_resident_equals_single_steps(pp2, H, W, block):
         assert b.loop_steps_per_launch() == 1
         us, zs, _ = S.synth_trajectory(grid, 40, seed=5)
         # chunks: even and odd lengths, starting on and off block boundaries
+        launches = 0
         for lo, hi in ((0, 2), (2, 5), (5, 6), (6, 16), (16, 40)):
             a.loop_run(us[lo:hi], zs[lo:hi])
             b.loop_run(us[lo:hi], zs[lo:hi])
             a.synchronize()
+            launches += hi - lo >= 2  # a one-step run takes the single-step launch
+            assert a.resident_launches()[0] == launches and b.resident_launches() == (0, 0)
             _same(a, b, f"after {hi} steps")
 
 
@@ -96,6 +99,7 @@ def test_resident_interleaved_with_other_ops(pp2):
             c.loop_run(us[13:20], zs[13:20])
             c.mdp_sweep(3)
             c.loop_run(us[20:30], zs[20:30])
+        assert a.resident_launches()[0] == 4 and b.resident_launches()[0] == 0
         _same(a, b, "after mixed ops")
         b0 = S.uniform_belief(grid)
         for c in (a, b):
@@ -114,6 +118,7 @@ def test_resident_multi_launch(pp2):
         a.loop_run(us, zs)
         b.loop_run(us, zs)
         a.synchronize()
+        assert a.resident_launches()[0] == 3
         _same(a, b, "after 4100 steps")
         a.loop_run(us[:33], zs[:33])
         b.loop_run(us[:33], zs[:33])
@@ -144,6 +149,7 @@ def test_resident_matches_oracle_1024(pp2, oracle):
         assert c.loop_steps_per_launch() == RESIDENT_STEPS
         c.loop_run(us, zs)
         c.synchronize()
+        assert c.resident_launches()[0] == 1
         Jd, Ad = c.mdp_get()
         bd = c.belief_get()
     np.testing.assert_array_equal(Jd.reshape(-1), J.reshape(-1))
@@ -152,3 +158,29 @@ def test_resident_matches_oracle_1024(pp2, oracle):
     bd = bd.reshape(-1)
     big = np.abs(bo) > 1e-30
     np.testing.assert_allclose(bd[big], bo[big], rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("max_sweeps", [0, 150, 300])
+@pytest.mark.parametrize("H,W", [(1024, 1024), (512, 512), (700, 768)])
+def test_resident_mdp_solve_equals_per_sweep(pp2, H, W, max_sweeps):
+    """pp2_mdp_solve as resident sweeps (k_sweep_resident: blocks of 100,
+    the convergence decision in-kernel) equals the launch-per-sweep driver:
+    same sweep count, same final norm, J and A bit for bit."""
+    grid, a, b = _pair(pp2, H, W, 8, H + 3 * W)
+    with a, b:
+        ra = a.mdp_solve(max_sweeps)
+        rb = b.mdp_solve(max_sweeps)
+        assert a.resident_launches()[1] >= 1 and b.resident_launches()[1] == 0
+        assert ra[0] == rb[0] and ra[0] % 100 == 0, (ra, rb)
+        assert np.float32(ra[1]) == np.float32(rb[1]), (ra, rb)
+        Ja, Aa = a.mdp_get()
+        Jb, Ab = b.mdp_get()
+        np.testing.assert_array_equal(Ja.view(np.uint32), Jb.view(np.uint32))
+        np.testing.assert_array_equal(Aa, Ab)
+        # the loop afterwards starts from the solved values on both paths
+        from path_planning_2d_amd import synthetic as S
+        us, zs, _ = S.synth_trajectory(grid, 10, seed=1)
+        a.loop_run(us, zs)
+        b.loop_run(us, zs)
+        assert a.resident_launches()[0] == 1
+        _same(a, b, "loop after the solve")

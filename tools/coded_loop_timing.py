@@ -45,6 +45,14 @@ def one(N, resident):
             torch.cuda.synchronize()
             ctx.synchronize()
             print(f"{what}: {e0.elapsed_time(e1) / reps * 1e3:.2f} us/step", flush=True)
+        import time
+        ctx.mdp_reset()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        n_sw, nrm = ctx.mdp_solve()
+        ctx.synchronize()
+        print(f"mdp_solve: {n_sw} sweeps, norm {nrm:.6g}, {1e3 * (time.perf_counter() - t0):.3f} ms",
+              flush=True)
 
 
 if __name__ == "__main__":
