@@ -268,6 +268,7 @@ struct SweepRun {
   int max_blocks;      // blocks per launch
   int cap_blocks;      // stop after this many blocks (0: no cap)
   double thresh;       // stop when norm <= thresh
+  int nsweeps;         // > 0: exactly this many sweeps, no convergence checks
 };
 size_t resident_lds_bytes(const Geom& g, int E, int es, int ts, int rt);
 bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p);

@@ -419,7 +419,8 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
 // order) and takes the same decision: stop when the norm is <= thresh or the
 // block cap is reached, else go on.  Actions are computed (and stored) on
 // each block's last sweep only; the last block's J, A and snapshot are
-// stored, and tile 0 writes {sweeps, norm bits} to res.
+// stored, and tile 0 writes {sweeps, norm bits} to res.  nsweeps > 0 runs
+// exactly that many sweeps instead, with no checks (pp2_mdp_sweep).
 __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wp = a.g.wp, rows = a.g.rows, tpr = wp >> 2, wpr = wp >> 8;
@@ -485,7 +486,9 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
   float norm = 0.0f;
   for (;; ++s) {
     const int ci = s & 1, co = ci ^ 1;
-    const bool check = s % kSolveBlock == kSolveBlock - 1;
+    // a block's last sweep (convergence check), or the last of a fixed count
+    const bool fin = a.nsweeps > 0 && s == a.nsweeps - 1;
+    const bool check = a.nsweeps == 0 && s % kSolveBlock == kSolveBlock - 1;
     if (valid) {
       if (nb_up || nb_dn) {
         __builtin_amdgcn_s_setprio(2);
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) jn[i][k] = w.v[i / 3][k + i % 3];
       const uint32_t cc[4] = {c0 & 0xffffu, c0 >> 16, c1 & 0xffffu, c1 >> 16};
-      if (check) coded_sweep4<true, true>(sTC, cc, jn, a.gamma, best, arg);
+      if (check || fin) coded_sweep4<true, true>(sTC, cc, jn, a.gamma, best, arg);
       else coded_sweep4<true, false>(sTC, cc, jn, a.gamma, best, arg);
       *reinterpret_cast<f4a*>(sbuf(co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
       if (nb_up || nb_dn) {
@@ -514,6 +517,7 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
         __builtin_amdgcn_s_setprio(0);
       }
     }
+    if (fin) break;
     if (!check) {
       __syncthreads();
       continue;
@@ -562,7 +566,8 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
     store4<false>(jo + goff, best);
     const uint32_t a4 = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
     *reinterpret_cast<uint32_t*>(a.A + goff) = a4;
-    *reinterpret_cast<f4a*>(a.snap + goff) = f4a{best[0], best[1], best[2], best[3]};
+    if (a.nsweeps == 0)  // the solve's snapshot (pp2_mdp_sweep leaves it alone)
+      *reinterpret_cast<f4a*>(a.snap + goff) = f4a{best[0], best[1], best[2], best[3]};
   }
   if (tile == 0 && threadIdx.x == 0) {
     a.res[0] = done;
@@ -639,7 +644,9 @@ bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p) {
 }
 
 hipError_t launch_sweep_resident(hipStream_t st, const ResidentPlan& p, const SweepRun& a) {
-  if (a.max_blocks < 1 || a.ntiles != p.ntiles || a.rt != p.rt) return hipErrorInvalidValue;
+  if ((a.nsweeps == 0 && a.max_blocks < 1) || a.nsweeps < 0 || a.ntiles != p.ntiles ||
+      a.rt != p.rt)
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_sweep_resident, dim3(p.ntiles), dim3(p.threads), p.lds, st, a);
   return hipGetLastError();
 }

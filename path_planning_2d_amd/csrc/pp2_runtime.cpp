@@ -870,6 +870,7 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
     a.max_blocks = 20;
     a.cap_blocks = cap_total ? cap_total - blocks : 0;
     a.thresh = thresh;
+    a.nsweeps = 0;
     HIPCHK(pp2::launch_sweep_resident(c->stream, p, a));
     ++c->sol_launches;
     int res[2] = {0, 0};
@@ -961,6 +962,38 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
     c->kstep = (c->kstep + m) % depth;
     i += m;
   }
+  return PP2_OK;
+}
+
+// pp2_mdp_sweep(n) on resident sweeps: n sweeps in one launch (no checks),
+// the J of the last sweep in J[(jcur + n) & 1], A of the last sweep.
+static int sweeps_resident(pp2_ctx* c, int n) {
+  const pp2::ResidentPlan& p = c->sol_plan;
+  pp2::SweepRun a{};
+  a.g = c->g;
+  a.gamma = c->gamma;
+  a.E = c->dict_n;
+  a.code = c->d_code;
+  a.rows = c->d_rows;
+  a.j0 = c->J[c->jcur].v.p;
+  a.j1 = c->J[c->jcur ^ 1].v.p;
+  a.snap = c->Jsnap.v.p;  // read and written back unchanged (no checks)
+  a.A = c->A;
+  a.xch = c->res_xch;
+  a.sync = c->res_sync;
+  a.tile_max = c->res_tmax;
+  a.res = c->res_out;
+  a.epoch = c->res_epoch;
+  a.arrive_base = c->res_arrive;
+  a.rt = p.rt;
+  a.ntiles = p.ntiles;
+  a.max_blocks = 1;
+  a.nsweeps = n;
+  HIPCHK(pp2::launch_sweep_resident(c->stream, p, a));
+  ++c->sol_launches;
+  c->res_used = true;
+  c->res_epoch += (unsigned)n + 1u;
+  c->jcur = (c->jcur + n) & 1;
   return PP2_OK;
 }
 
@@ -1233,6 +1266,10 @@ int pp2_mdp_sweep(pp2_ctx* c, int n) {
   CHECK(check_model(c));
   if (n < 0) return set_err(PP2_EINVAL, "negative sweep count");
   DeviceGuard dg(c->device);
+  if (n >= 2 && solve_ready(c)) {
+    break_pipeline(c);  // the loop's deep halo rows of J are stale after sweeps
+    return sweeps_resident(c, n);
+  }
   for (int i = 0; i < n; ++i) {
     CHECK(exchange_halos(c, {HALO_VALUE}));
     CHECK(mdp_sweep_once(c));

@@ -184,3 +184,21 @@ def test_resident_mdp_solve_equals_per_sweep(pp2, H, W, max_sweeps):
         b.loop_run(us, zs)
         assert a.resident_launches()[0] == 1
         _same(a, b, "loop after the solve")
+
+
+@pytest.mark.parametrize("n", [2, 7, 100, 301])
+def test_resident_mdp_sweeps_equal_per_sweep(pp2, n):
+    """pp2_mdp_sweep(n >= 2) as one resident launch equals n sweep launches
+    (J, A bit for bit), also mid-solve and followed by a solve."""
+    grid, a, b = _pair(pp2, 1024, 1024, 8, 77)
+    with a, b:
+        for c in (a, b):
+            c.mdp_sweep(n)
+        assert a.resident_launches()[1] == 1 and b.resident_launches()[1] == 0
+        Ja, Aa = a.mdp_get()
+        Jb, Ab = b.mdp_get()
+        np.testing.assert_array_equal(Ja.view(np.uint32), Jb.view(np.uint32))
+        np.testing.assert_array_equal(Aa, Ab)
+        ra, rb = a.mdp_solve(200), b.mdp_solve(200)
+        assert ra[0] == rb[0] and np.float32(ra[1]) == np.float32(rb[1])
+        np.testing.assert_array_equal(a.mdp_get()[0].view(np.uint32), b.mdp_get()[0].view(np.uint32))
