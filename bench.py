@@ -838,7 +838,10 @@ def main():
             "dense_path": dense,
             "config4": c4,
             "kernels": {
-                "mdp_sweep_kernel": "k_mdp_sweep_coded" if coded else "k_mdp_sweep",
+                "mdp_sweep_kernel": (("k_sweep_resident (the 100 sweeps in one launch; gbs/frac "
+                                      "count its 11 B/cell once per sweep)")
+                                     if coded and resident else
+                                     "k_mdp_sweep_coded" if coded else "k_mdp_sweep"),
                 "mdp_sweep_us": sweep_ms * 1e3,
                 "mdp_sweep_gbs": sweep_gbs,
                 "mdp_sweep_frac": sweep_gbs / HBM_PEAK_GBS,
