@@ -525,32 +525,61 @@ __global__ __launch_bounds__(kBlock) void k_fib_sweep(
 // (action, observation) and the flops by 2.2x.  Dropped terms are
 // fmaf(0 * L, alpha, s) == s (the chain starts at +0 and never holds -0), so
 // alphas are bit-identical to k_fib_sweep's full 9-term chains.
-__global__ __launch_bounds__(kBlock) void k_fib_sweep_sparse(
+//
+// The 9 next-action chains of an (action, observation) run as packed pairs:
+// q = 0..7 in four v_pk_fma_f32 pairs (each element the same IEEE fma, in the
+// same j order, as the scalar chain) and q = 8 alone, and the max over q is a
+// v_max3 chain (fmaxf: the chains are fma results, never NaN, and the max is
+// the same value as the strict-< scan).  Neighbour alphas and likelihoods are
+// buffer loads: 32-bit lane offsets, the plane offsets in SGPRs, and +0.0
+// for off-grid neighbours from an out-of-range offset.  <= 128 VGPRs (4 waves
+// per SIMD) against 158 for the scalar chains.
+typedef float f2v __attribute__((ext_vector_type(2)));
+constexpr int kOffRange = 0x7ffffff0;  // num_records of the FIB resources: loads at or past it return 0
+
+__global__ __launch_bounds__(kBlock, 4) void k_fib_sweep_sparse(
     Geom g, float gamma, PlaneSet T, PlaneSet L, PlaneSet R, PlaneSet a_in,
     PlaneSet a_out) {
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const int y = (int)(t / g.wp);
   const int x = (int)(t % g.wp);
   if (y >= g.rows) return;
-  float la[9][9];
+  const int ars = (int)a_in.rs, aps = (int)a_in.ps, lrs = (int)L.rs, lps = (int)L.ps;
+  // buffer resources at row -1 of plane 0: per-lane row/column offsets in
+  // VGPRs, the plane offsets (q * aps, o * lps) uniform in SGPRs
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(a_in.p - ars, 0, kOffRange, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc(L.p - lrs, 0, kOffRange, 0x00020000);
+  auto ldb = [](__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  };
+  f2v lap[9][4];  // alpha_q of neighbour sp, q = 0..7 in pairs
+  float la8[9];   // alpha_8 of neighbour sp
   bool ok[9];
 #pragma unroll
   for (int sp = 0; sp < 9; ++sp) {
     const int oy = sp / 3 - 1, nx = x + sp % 3 - 1;
     ok[sp] = nx >= 0 && nx < g.wp;
-    const float* ap = a_in.p + (long long)(y + oy) * a_in.rs + nx;
+    // off-grid neighbours: an offset past the resource's range, which a
+    // buffer load answers with +0.0 (no select)
+    const int vo = ok[sp] ? ((y + oy + 1) * ars + nx) * 4 : kOffRange;
 #pragma unroll
-    for (int q = 0; q < 9; ++q) la[sp][q] = ok[sp] ? ap[(long long)q * a_in.ps] : 0.0f;
+    for (int p = 0; p < 4; ++p) {
+      lap[sp][p].x = ldb(ra, vo, (2 * p) * aps * 4);
+      lap[sp][p].y = ldb(ra, vo, (2 * p + 1) * aps * 4);
+    }
+    la8[sp] = ldb(ra, vo, 8 * aps * 4);
   }
 #pragma unroll
   for (int a = 0; a < 9; ++a) {
     float ts[4];
-    const float* lp[4];
+    int lo[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int sp = kSup[a][j], oy = sp / 3 - 1, nx = x + sp % 3 - 1;
       ts[j] = j < kSupN[a] ? T.p[(long long)y * T.rs + (long long)(9 * a + sp) * T.ps + x] : 0.0f;
-      lp[j] = L.p + (long long)(y + oy) * L.rs + (ok[sp] ? nx : x);
+      lo[j] = ok[sp] ? ((y + oy + 1) * lrs + nx) * 4 : kOffRange;
     }
     float rtg = 0.0f;
 #pragma unroll 2
@@ -558,16 +587,21 @@ __global__ __launch_bounds__(kBlock) void k_fib_sweep_sparse(
       float tm[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        tm[j] = j < kSupN[a] ? ts[j] * (ok[kSup[a][j]] ? lp[j][(long long)o * L.ps] : 0.0f) : 0.0f;
-      float rtgo = -FLT_MAX;
+        tm[j] = j < kSupN[a] ? ts[j] * ldb(rl, lo[j], o * lps * 4) : 0.0f;
+      f2v sq[4] = {f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}};
+      float sq8 = 0.0f;
 #pragma unroll
-      for (int q = 0; q < 9; ++q) {
-        float sq = 0.0f;
+      for (int j = 0; j < 4; ++j) {
+        if (j >= kSupN[a]) continue;
+        const f2v tj = {tm[j], tm[j]};
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (j < kSupN[a]) sq = __builtin_fmaf(tm[j], la[kSup[a][j]][q], sq);
-        if (rtgo < sq) rtgo = sq;
+        for (int p = 0; p < 4; ++p) sq[p] = __builtin_elementwise_fma(tj, lap[kSup[a][j]][p], sq[p]);
+        sq8 = __builtin_fmaf(tm[j], la8[kSup[a][j]], sq8);
       }
+      float rtgo = fmaxf(fmaxf(-FLT_MAX, sq[0].x), sq[0].y);
+#pragma unroll
+      for (int p = 1; p < 4; ++p) rtgo = fmaxf(fmaxf(rtgo, sq[p].x), sq[p].y);
+      rtgo = fmaxf(rtgo, sq8);
       rtg = rtg + rtgo;
     }
     a_out.p[(long long)y * a_out.rs + (long long)a * a_out.ps + x] =
