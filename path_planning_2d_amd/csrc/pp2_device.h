@@ -65,16 +65,41 @@ __device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[N]) 
 
 // ---- deterministic reductions (fixed association order) --------------------
 // xor-butterfly: partners always add the same two operands, so every lane of
-// the wave ends with the bit-identical total.
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+// the wave ends with the bit-identical total.  Stages xor 32, 16, 8, 4, 2, 1
+// (the association of a __shfl_xor loop from 32 down), without the LDS
+// crossbar: xor 32 / 16 by v_permlane32_swap / v_permlane16_swap (a pair of
+// half-swapped copies whose sum is v_i + v_{i^m} in every lane), xor 8 as
+// row_mirror then row_half_mirror (i ^ 15 ^ 7), xor 4 as row_half_mirror then
+// quad_perm [3,2,1,0] (i ^ 7 ^ 3), xor 2 / 1 as quad_perm -- 10 VALU
+// instructions against 6 ds_bpermute_b32 round trips and 6 adds.
+template <typename OP>
+__device__ __forceinline__ float wave_butterfly(float v, OP op) {
+  const uint32_t u = __float_as_uint(v);
+  const auto h32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  v = op(__uint_as_float(h32[0]), __uint_as_float(h32[1]));
+  const uint32_t u16 = __float_as_uint(v);
+  const auto h16 = __builtin_amdgcn_permlane16_swap(u16, u16, false, false);
+  v = op(__uint_as_float(h16[0]), __uint_as_float(h16[1]));
+  auto dpp = [](float x, int ctrl) -> float {
+    switch (ctrl) {  // the DPP control must be a constant
+      case 0x140: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xf, 0xf, false));
+      case 0x141: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
+      case 0x1b: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x1b, 0xf, 0xf, false));
+      case 0x4e: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4e, 0xf, 0xf, false));
+      default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xb1, 0xf, 0xf, false));
+    }
+  };
+  v = op(v, dpp(dpp(v, 0x140), 0x141));  // xor 8
+  v = op(v, dpp(dpp(v, 0x141), 0x1b));   // xor 4
+  v = op(v, dpp(v, 0x4e));               // xor 2
+  v = op(v, dpp(v, 0xb1));               // xor 1
   return v;
 }
+__device__ __forceinline__ float wave_sum(float v) {
+  return wave_butterfly(v, [](float a, float b) { return a + b; });
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
+  return wave_butterfly(v, [](float a, float b) { return fmaxf(a, b); });
 }
 
 // Sum over a 256-thread block; result valid in thread 0.
