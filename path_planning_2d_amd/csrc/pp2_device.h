@@ -98,6 +98,65 @@ __device__ __forceinline__ float wave_butterfly(float v, OP op) {
 __device__ __forceinline__ float wave_sum(float v) {
   return wave_butterfly(v, [](float a, float b) { return a + b; });
 }
+
+// 128 per-lane values summed across the wave as a reduce-scatter: each
+// butterfly stage (xor 32, 16, 8, 4, 2, 1) halves the values a lane carries
+// -- it keeps the half its xor-group owns and adds the partner's copy of it --
+// so the wave exchanges 126 values instead of 6 x 128, and lane l ends with
+// the totals of values 2l and 2l + 1 in out[0], out[1].  Every total is
+// v_i + v_{i^m} stage by stage from 32 down, i.e. wave_sum's association,
+// bit for bit.  xor 32 / 16: one v_permlane32/16_swap of the kept pair (x =
+// low half, y = high half) leaves x' + y' = the lane's own sum in every lane;
+// xor 8 .. 1: send the half the partner keeps by DPP and add it to the kept
+// half.
+__device__ __forceinline__ void wave_sum_scatter128(const float (&lo)[64], const float (&hi)[64],
+                                                   float (&out)[2]) {
+  const int lane = threadIdx.x & 63;
+  float v1[64], v2[32], v3[16], v4[8], v5[4], v6[2];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo[j]), __float_as_uint(hi[j]),
+                                                    false, false);
+    v1[j] = __uint_as_float(h[0]) + __uint_as_float(h[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const auto h = __builtin_amdgcn_permlane16_swap(__float_as_uint(v1[j]),
+                                                    __float_as_uint(v1[32 + j]), false, false);
+    v2[j] = __uint_as_float(h[0]) + __uint_as_float(h[1]);
+  }
+  auto x8 = [](float x) {
+    const float m = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m), 0x141, 0xf, 0xf, false));
+  };
+  auto x4 = [](float x) {
+    const float m = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m), 0x1b, 0xf, 0xf, false));
+  };
+  auto x2 = [](float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4e, 0xf, 0xf, false));
+  };
+  auto x1 = [](float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xb1, 0xf, 0xf, false));
+  };
+  // keep the half this lane's xor-group owns, add the partner's copy of it
+#define PP2_HALVE(SRC, DST, N, D, XF)                                  \
+  {                                                                    \
+    const bool h_ = lane & (D);                                        \
+    _Pragma("unroll") for (int j = 0; j < (N); ++j) {                  \
+      const float keep = h_ ? SRC[(N) + j] : SRC[j];                   \
+      const float send = h_ ? SRC[j] : SRC[(N) + j];                   \
+      DST[j] = keep + XF(send);                                        \
+    }                                                                  \
+  }
+  PP2_HALVE(v2, v3, 16, 8, x8)
+  PP2_HALVE(v3, v4, 8, 4, x4)
+  PP2_HALVE(v4, v5, 4, 2, x2)
+  PP2_HALVE(v5, v6, 2, 1, x1)
+#undef PP2_HALVE
+  out[0] = v6[0];
+  out[1] = v6[1];
+}
 __device__ __forceinline__ float wave_max(float v) {
   return wave_butterfly(v, [](float a, float b) { return fmaxf(a, b); });
 }

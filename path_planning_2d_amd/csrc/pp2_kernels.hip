@@ -761,11 +761,12 @@ __global__ __launch_bounds__(kBlock) void k_expand_stats(
   const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
   const int y = (int)(t / tpr);
   const int x0 = (int)(t % tpr) * CPT;
-  float acc[9][kStats];
+  // [a * kStats + i] as two 64-float halves, zero-padded to 128 for
+  // wave_sum_scatter128
+  float acl[64], ach[64];
 #pragma unroll
-  for (int a = 0; a < 9; ++a)
-#pragma unroll
-    for (int i = 0; i < kStats; ++i) acc[a][i] = 0.0f;
+  for (int j = 0; j < 64; ++j) acl[j] = ach[j] = 0.0f;
+#define PP2_ACC(m) (*((m) < 64 ? &acl[(m) & 63] : &ach[(m) & 63]))
   if (y < g.rows) {
     float lv[CPT], fv[9][CPT];
     ldv<CPT, true>(L.p + (long long)y * L.rs + (long long)z * L.ps + x0, lv);
@@ -779,20 +780,24 @@ __global__ __launch_bounds__(kBlock) void k_expand_stats(
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const float c = pv[k] * lv[k];  // the reference kernel's child value
-        acc[a][0] += c;
+        PP2_ACC(a * kStats) += c;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) acc[a][1 + i] = __builtin_fmaf(c, fv[i][k], acc[a][1 + i]);
+        for (int i = 0; i < 9; ++i)
+          PP2_ACC(a * kStats + 1 + i) = __builtin_fmaf(c, fv[i][k], PP2_ACC(a * kStats + 1 + i));
       }
     }
   }
   const int w = threadIdx.x >> 6;
-#pragma unroll
-  for (int a = 0; a < 9; ++a)
-#pragma unroll
-    for (int i = 0; i < kStats; ++i) {
-      const float v = wave_sum(acc[a][i]);
-      if ((threadIdx.x & 63) == 0) red[w][a * kStats + i] = v;
-    }
+  // the 90 wave totals by one reduce-scatter (wave_sum's association): lane l
+  // gets totals 2l, 2l + 1
+#undef PP2_ACC
+  float tot[2];
+  wave_sum_scatter128(acl, ach, tot);
+  {
+    const int l = threadIdx.x & 63;
+    if (2 * l < 9 * kStats) red[w][2 * l] = tot[0];
+    if (2 * l + 1 < 9 * kStats) red[w][2 * l + 1] = tot[1];
+  }
   __syncthreads();
   if (threadIdx.x < 9 * kStats) {
     const int j = threadIdx.x;
@@ -843,8 +848,18 @@ __global__ __launch_bounds__(kBlock) void k_reduce_columns(const float* __restri
                                                            int rows, int cols, float* __restrict__ out) {
   const int j = blockIdx.x * kBlock + threadIdx.x;
   if (j >= cols) return;
+  // 16 loads in flight ahead of the in-order adds (one L2 round trip per 16
+  // rows instead of per row)
   float s = 0.0f;
-  for (int r = 0; r < rows; ++r) s += partials[(long long)r * cols + j];
+  int r = 0;
+  for (; r + 16 <= rows; r += 16) {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = partials[(long long)(r + i) * cols + j];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += v[i];
+  }
+  for (; r < rows; ++r) s += partials[(long long)r * cols + j];
   out[j] = s;
 }
 
