@@ -712,16 +712,23 @@ def main():
     if rank == 0 and ws == 1:
         # BASELINE configs[2]: MDP value iteration to convergence on this grid
         # (valueIteration, src/mdp/path_planning_2d.cu:207-269, no GUI)
-        ctx.mdp_reset()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        n_sw, nrm = ctx.mdp_solve()
-        torch.cuda.synchronize()
-        t_solve = time.perf_counter() - t0
+        # the first solve on a context also pays its one-time setup (the
+        # resident solve's plan); the steady-state solve is timed after it
+        solve_ms = []
+        for _ in range(2):
+            ctx.mdp_reset()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n_sw, nrm = ctx.mdp_solve()
+            torch.cuda.synchronize()
+            solve_ms.append((time.perf_counter() - t0) * 1e3)
         mdp_solve = {"config": f"{gh}x{gw} MDP value iteration to convergence "
                                f"(blocks of 100 sweeps, stop at inf-norm <= 1e-3*5/(1-gamma))",
-                     "sweeps": n_sw, "final_norm": nrm, "ms": t_solve * 1e3,
-                     "us_per_sweep": t_solve * 1e6 / max(1, n_sw)}
+                     "sweeps": n_sw, "final_norm": nrm, "ms": solve_ms[1],
+                     "first_call_ms": solve_ms[0],
+                     "us_per_sweep": solve_ms[1] * 1e3 / max(1, n_sw),
+                     "kernel": ("k_sweep_resident" if coded and steps_per_launch >= RESIDENT_STEPS
+                                else "k_mdp_sweep_coded" if coded else "k_mdp_sweep")}
     ctx.close()
 
     bytes_loop = BYTES_LOOP_CODED if coded else BYTES_LOOP

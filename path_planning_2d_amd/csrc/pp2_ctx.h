@@ -138,6 +138,7 @@ struct pp2_ctx {
   int res_ntiles = 0;              // tiles the sync words / exchange rows were sized for
   float* res_tmax = nullptr;       // 2 x ntiles per-tile convergence maxima
   int* res_out = nullptr;          // {sweeps, norm bits} of a resident solve launch
+  unsigned* res_host = nullptr;    // pinned: {sweeps, norm bits, error word} read back
   int res_launches = 0, sol_launches = 0;  // pp2_resident_launches
 
   ncclComm_t comm = nullptr;

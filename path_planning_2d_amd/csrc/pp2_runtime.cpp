@@ -743,6 +743,8 @@ static void resident_free_buffers(pp2_ctx* c) {
   for (void* p : {(void*)c->res_sync, (void*)c->res_ring, (void*)c->res_xch, (void*)c->res_tmax,
                   (void*)c->res_out})
     if (p) (void)hipFree(p);
+  if (c->res_host) (void)hipHostFree(c->res_host);
+  c->res_host = nullptr;
   c->res_sync = nullptr;
   c->res_ring = nullptr;
   c->res_xch = nullptr;
@@ -772,6 +774,7 @@ static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
   if (hipMalloc(&c->res_sync, sync_b) != hipSuccess || hipMalloc(&c->res_ring, ring_b) != hipSuccess ||
       hipMalloc(&c->res_xch, xch_b) != hipSuccess || hipMalloc(&c->res_tmax, tmax_b) != hipSuccess ||
       hipMalloc(&c->res_out, 4 * sizeof(int)) != hipSuccess ||
+      hipHostMalloc(&c->res_host, 4 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
       hipMemsetAsync(c->res_sync, 0, sync_b, c->stream) != hipSuccess ||
       hipMemsetAsync(c->res_ring, 0, ring_b, c->stream) != hipSuccess ||
       hipMemsetAsync(c->res_xch, 0, xch_b, c->stream) != hipSuccess) {
@@ -789,9 +792,10 @@ static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
 static int resident_check(pp2_ctx* c) {
   if (!c->res_used || !c->res_sync) return PP2_OK;
   c->res_used = false;
-  unsigned e = 0;
-  HIPCHK(hipMemcpy(&e, c->res_sync + pp2::kResidentSyncErr, sizeof(e), hipMemcpyDeviceToHost));
-  if (!e) return PP2_OK;
+  HIPCHK(hipMemcpyAsync(c->res_host + 2, c->res_sync + pp2::kResidentSyncErr, sizeof(unsigned),
+                        hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (!c->res_host[2]) return PP2_OK;
   resident_free(c);
   c->resident = 0;
   return set_err(PP2_EHIP, "resident loop: a workgroup wait timed out (grid not co-resident); "
@@ -873,11 +877,12 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
     a.nsweeps = 0;
     HIPCHK(pp2::launch_sweep_resident(c->stream, p, a));
     ++c->sol_launches;
-    int res[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(res, c->res_out, sizeof(res), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpyAsync(c->res_host, c->res_out, 2 * sizeof(int), hipMemcpyDeviceToHost,
+                          c->stream));
     c->res_used = true;
-    CHECK(resident_check(c));
+    CHECK(resident_check(c));  // one stream sync for the result and the error word
+    int res[2];
+    std::memcpy(res, c->res_host, sizeof(res));
     const int done = res[0];
     if (done <= 0 || done % pp2::kSolveBlock != 0)
       return set_err(PP2_EHIP, "resident MDP solve returned %d sweeps", done);
