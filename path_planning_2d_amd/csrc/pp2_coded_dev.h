@@ -50,6 +50,50 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, int n,
   }
 }
 
+// Factored-row Bellman backup of N cells from their codes (k_mdp_sweep's
+// arithmetic): cell-outer, fully unrolled (support positions index jn at
+// compile time): one IW record, then per action a quad from QT (a float for
+// the one-cell stay support) and the cost from CT at the same byte offset.
+// The scheduling barrier keeps one cell's loads live at a time.  Actions are
+// compared in ascending order, so best/arg are the dense kernel's.  ARG =
+// false: values only, best = minnum over the actions (see coded_sweep4).
+template <int N, bool ARG>
+__device__ __forceinline__ void coded_sweep_sparse(const float* sTC, const uint32_t (&cc)[N],
+                                                   const float (&jn)[9][N], float (&best)[N],
+                                                   uint32_t (&arg)[N]) {
+  const char* qt = reinterpret_cast<const char*>(sTC + kFactQT);
+  const char* ct = reinterpret_cast<const char*>(sTC + kFactCT);
+#pragma unroll
+  for (int k = 0; k < N; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const uint4 iw = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * cc[k]);
+#pragma unroll
+    for (int a = 0; a < 9; ++a) {
+      const uint32_t w = a < 4 ? iw.x : a < 8 ? iw.y : iw.z;
+      const uint32_t off = __builtin_amdgcn_ubfe(w, 8 * (a % 4), 8);
+      const int tab = a * kFactK * 16;  // byte offset of action a's table
+      float tv[4];
+      if (kSupN[a] == 1) {
+        tv[0] = *reinterpret_cast<const float*>(qt + tab + off);
+      } else {
+        const f4a t = *reinterpret_cast<const f4a*>(qt + tab + off);
+        tv[0] = t[0]; tv[1] = t[1]; tv[2] = t[2]; tv[3] = t[3];
+      }
+      float cost = *reinterpret_cast<const float*>(ct + tab + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);
+      if constexpr (ARG) {
+        if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
+      } else {
+        best[k] = __builtin_fminf(best[k], cost);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Bellman backup of 4 cells from their codes (k_mdp_sweep's arithmetic).
 // ARG = false: values only (the resident loop's intermediate steps store no
 // actions), best = minnum over the actions -- the same value as the strict-<
@@ -63,40 +107,7 @@ __device__ __forceinline__ void coded_sweep4(const float* sTC, const uint32_t (&
 #pragma unroll
   for (int k = 0; k < 4; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
   if constexpr (SPARSE) {
-    // cell-outer, fully unrolled (support positions index jn at compile
-    // time): one IW record, then per action a quad from QT (a float for the
-    // one-cell stay support) and the cost from CT at the same byte offset.
-    // The scheduling barrier keeps one cell's loads live at a time.  Actions
-    // are compared in ascending order, so best/arg are the dense kernel's.
-    const char* qt = reinterpret_cast<const char*>(sTC + kFactQT);
-    const char* ct = reinterpret_cast<const char*>(sTC + kFactCT);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 iw = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * cc[k]);
-#pragma unroll
-      for (int a = 0; a < 9; ++a) {
-        const uint32_t w = a < 4 ? iw.x : a < 8 ? iw.y : iw.z;
-        const uint32_t off = __builtin_amdgcn_ubfe(w, 8 * (a % 4), 8);
-        const int tab = a * kFactK * 16;  // byte offset of action a's table
-        float tv[4];
-        if (kSupN[a] == 1) {
-          tv[0] = *reinterpret_cast<const float*>(qt + tab + off);
-        } else {
-          const f4a t = *reinterpret_cast<const f4a*>(qt + tab + off);
-          tv[0] = t[0]; tv[1] = t[1]; tv[2] = t[2]; tv[3] = t[3];
-        }
-        float cost = *reinterpret_cast<const float*>(ct + tab + off);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);
-        if constexpr (ARG) {
-          if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
-        } else {
-          best[k] = __builtin_fminf(best[k], cost);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    coded_sweep_sparse<4, ARG>(sTC, cc, jn, best, arg);
   } else {
     // one action at a time: 4 cells x 10 dictionary floats live (a fully
     // unrolled action loop hoists all 360 LDS reads and spills)
