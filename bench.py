@@ -110,7 +110,8 @@ def dist_env():
     return ws, rank, local
 
 
-def pmc_traffic(kernel_substr: str, cells: int, exclude: str | None = None):
+def pmc_traffic(kernel_substr: str, cells: int, exclude: str | None = None,
+                steps: int | None = None):
     """HBM bytes per launch of the dominant kernel from the newest committed
     rocprofv3 PMC summary (profiles/pmc_*.json, written by
     profiles/collect_pmc.py), or None."""
@@ -123,7 +124,8 @@ def pmc_traffic(kernel_substr: str, cells: int, exclude: str | None = None):
         k = d.get("kernels", {})
         for name, v in k.items():
             if (kernel_substr in name and v.get("cells") == cells
-                    and not (exclude and exclude in name)):
+                    and not (exclude and exclude in name)
+                    and v.get("steps_per_launch") == steps):
                 return v.get("hbm_bytes_per_launch"), os.path.basename(f)
     return None, None
 
@@ -748,7 +750,8 @@ def main():
     loop_gbs = algo_launch / launch_s / 1e9
     contract_gbs = BYTES_LOOP * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(loop_kernel, cells_per_gpu,
-                                       exclude=None if coded else "coded")
+                                       exclude=None if coded else "coded",
+                                       steps=round(spl) if resident else None)
 
     c4 = None
     if args.c4_size > 0:

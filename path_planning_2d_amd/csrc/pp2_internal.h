@@ -207,17 +207,17 @@ hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
 
 // Tile-resident loop (pp2_resident.hip): n fused loop steps of an unsharded
 // sparse-coded context in one launch, one tile of rt whole rows per CU kept
-// in LDS, neighbour rows handed over by per-wave flags, block-start masses
+// in LDS, neighbour rows handed over as data-tagged granules, block-start masses
 // behind an arrival counter.  Needs wp % 256 == 0, rt * wp / 4 <= 1024 lanes,
 // a tile per CU and the whole dictionary in LDS (resident_plan).
 constexpr int kResidentMaxSteps = 2048;  // steps per launch (kernel-argument trajectory)
 constexpr int kResidentRing = 16;        // partial-mass slots (>= block depth + 2)
 constexpr int kResidentSyncArrive = 0;   // sync words: block-start arrivals,
 constexpr int kResidentSyncRead = 1;     //   in_partials readers done,
-constexpr int kResidentSyncErr = 2;      //   sticky timeout flag,
-constexpr int kResidentSyncFlags = 16;   //   then [tile][top, bottom][wave of row] flags
+constexpr int kResidentSyncErr = 2;      //   sticky timeout flag
+constexpr int kResidentSyncWords = 16;
 struct ResidentPlan {
-  int rt = 0, ntiles = 0, threads = 0, flag_words = 0;
+  int rt = 0, ntiles = 0, threads = 0;
   size_t lds = 0;
 };
 struct ResidentRun {
@@ -232,7 +232,7 @@ struct ResidentRun {
   const float* j_in;
   float* b_out;              // the last step's output planes
   float* j_out;
-  float* xch;                // exchange rows, resident_xch_floats(): [step & 1][b, J][tile][top, bottom][4 zero + wp]
+  float* xch;                // exchange granules, resident_xch_floats(): [step & 1][tile][top, bottom][wave][3][lane] x 16 B
   uint8_t* A;
   int n, kstep0, depth, rt, ntiles, nparts;
   float bscale;              // block-start scale (2^96, or 1 for depth 1)
@@ -242,7 +242,7 @@ struct ResidentRun {
   const float* in_sum;       // step 0's finalised input mass when in_partials is null
   float* ring;               // kResidentRing x nparts partial slots
   float* out_partials;       // the last step's partials (the context's pending buffer)
-  unsigned* sync;            // sync words (kResidentSyncFlags + flag_words)
+  unsigned* sync;            // kResidentSyncWords sync words
   unsigned epoch, arrive_base, read_base;  // epoch-tagged counters of earlier launches
   int final_wait_read;       // out_partials == in_partials: the last step waits for readers
   uint8_t uz[kResidentMaxSteps];  // u | z << 4 per step
@@ -274,7 +274,8 @@ size_t resident_lds_bytes(const Geom& g, int E, int es, int ts, int rt);
 bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p);
 hipError_t launch_sweep_resident(hipStream_t st, const ResidentPlan& p, const SweepRun& a);
 inline size_t resident_xch_floats(const Geom& g, int ntiles) {
-  return (size_t)8 * ntiles * (g.wp + 4) + 8;  // rows of 4 zero + wp floats, slack at the end
+  // [step & 1][tile][top, bottom][wave of row][3][lane] 16-B granules
+  return (size_t)2 * ntiles * 2 * (g.wp / 256) * 3 * 64 * 4;
 }
 bool resident_plan(const Geom& g, int E, int es, int ts, int ncus, ResidentPlan* p);
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a);

@@ -12,14 +12,15 @@
 //     actions, L_z of all 16 observations) is staged once per launch;
 //   * a lane owns one quad of 4 cells and keeps its code window in registers;
 //   * only the tile's first and last rows cross CUs.  Their waves take the
-//     neighbours' rows of step t-1 first (poll the <= 3 flags of the
-//     neighbour waves over their columns, then sc1 loads), compute with issue
-//     priority, store their own row write-through (sc1) into an exchange slot
-//     (step & 1), drain, and raise one flag per wave (MI355X_MICROARCH.md
-//     § visibility, table row 1 with one storing wave).  A producer rewrites
-//     a slot only after the consumer's flag of the following step, i.e.
-//     after the consumer's loads of it have returned.  Interior waves never
-//     touch global memory;
+//     neighbours' rows of step t-1 first (poll the data-tagged granules of
+//     the neighbour waves over their columns with sc1 loads until every tag
+//     matches), compute with issue priority and store their own row as
+//     granules (one sc1 store each) into an exchange slot (step & 1): the
+//     data is the flag, so no drain and no separate flag (MI355X_MICROARCH.md
+//     § visibility, handoff-1to1).  A producer rewrites a slot only after it
+//     took the consumer's granules of the following step, i.e. after the
+//     consumer's loads of it have returned.  Interior waves never touch
+//     global memory;
 //   * a normalisation block start needs the exact mass of the previous belief:
 //     every tile adds to an arrival counter after its step's wave partials are
 //     drained, and wave 0 of each tile reduces all partials (k_sum_finalize's
@@ -35,8 +36,8 @@
 // blocked_loop_step exactly, so b, masses, J and A equal the
 // one-launch-per-step path bit for bit.
 //
-// Flags and counters are epoch-tagged (values grow monotonically over the
-// context's launches), so no per-launch reset is needed.  Every wait is
+// Granule tags and counters are epoch-tagged (values grow monotonically over
+// the context's launches), so no per-launch reset is needed.  Every wait is
 // bounded: after kSpinTicks of the 100 MHz clock it raises the sticky error
 // word and returns, so a grid that is not fully resident ends with an error
 // instead of hanging (pp2_synchronize reports it).
@@ -72,10 +73,6 @@ __device__ __forceinline__ f4a ld4_sc1(Rsrc r, int off) {
 }
 __device__ __forceinline__ float ld1_sc1(Rsrc r, int off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kSc1));
-}
-__device__ __forceinline__ void st4_sc1(Rsrc r, int off, const float (&v)[4]) {
-  const f4a t = {v[0], v[1], v[2], v[3]};
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, t), r, off, 0, kSc1);
 }
 __device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -198,17 +195,72 @@ __device__ __forceinline__ void row_zero(float (&v)[6]) {
   for (int i = 0; i < 6; ++i) v[i] = 0.0f;
 }
 
-// One window row from a zero-padded exchange row (sc1: handed over in-launch).
-__device__ __forceinline__ void row_sc1(Rsrc r, int off, float (&v)[6]) {
-  const f4a m = ld4_sc1(r, off);
-  v[0] = ld1_sc1(r, off - 4); v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3];
-  v[5] = ld1_sc1(r, off + 16);
+// Edge-row hand-off by data-tagged granules (MI355X_MICROARCH.md
+// § visibility, handoff-1to1: the data is the flag).  A granule is 16 B,
+// three values and the tag in .w, written by ONE sc1 (write-through) store;
+// the consumer polls the granules themselves with sc1 loads until every tag
+// matches -- no drain, no flag, one fabric round trip per hand-off.  Layout:
+// [step & 1][tile][top, bottom][wave of the row][granule k < 3][lane], so a
+// wave's k-th store and load cover 1 KiB contiguously.  Every granule slot of
+// the buffer holds a tag in .w in both resident kernels (the sweep uses
+// k < 2), and tags grow monotonically over the context's launches, so a
+// stale granule never matches.
+__device__ __forceinline__ int xch_gran(int ntiles, int wpr, int slot, int tl, int side, int w,
+                                        int k, int ln) {
+  return (((((slot * ntiles + tl) * 2 + side) * wpr + w) * 3 + k) * 64 + ln) * 16;
+}
+__device__ __forceinline__ void st_gran(Rsrc r, int off, float x, float y, float z, unsigned tag) {
+  const u4v t = {__float_as_uint(x), __float_as_uint(y), __float_as_uint(z), tag};
+  __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, kSc1);
+}
+// The wave polls granules g[k] at o + 1 KiB * k and (edge lanes) e[k] at
+// eo + 1 KiB * k until all carry `tag`.  Bounded like wave_wait; the empty
+// asm keeps the loads inside the loop.
+template <int NG, int NE>
+__device__ __forceinline__ void take_granules(Rsrc r, int o, bool edge, int eo, unsigned tag,
+                                              u4v (&g)[NG], u4v (&e)[NE], unsigned* err) {
+  const unsigned long long t0 = wall_clock64();
+#pragma unroll
+  for (int k = 0; k < NE; ++k) e[k] = u4v{0u, 0u, 0u, tag};
+  for (int spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      g[k] = __builtin_amdgcn_raw_buffer_load_b128(r, o + 1024 * k, 0, kSc1);
+    }
+    if (edge) {
+#pragma unroll
+      for (int k = 0; k < NE; ++k) e[k] = __builtin_amdgcn_raw_buffer_load_b128(r, eo + 1024 * k, 0, kSc1);
+    }
+#pragma unroll
+    for (int k = 0; k < NG; ++k) ok = ok && g[k][3] == tag;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) ok = ok && e[k][3] == tag;
+    if (__all(ok)) break;
+    if ((spin & 7) == 7) {
+      if (ld_flag(err) != 0u || wall_clock64() - t0 > kSpinTicks) {
+        if ((threadIdx.x & 63) == 0) st_flag(err, 1u);
+        return;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  }
+}
+// One window row from the lane's aligned quad m and the edge dword e of the
+// lane's wave-edge neighbour (lanes 0 / 63), the others by DPP wave shifts.
+__device__ __forceinline__ void row_quad(const float (&m)[4], float e, float (&v)[6]) {
+  v[0] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(e), __float_as_int(m[3]),
+                                                    0x138, 0xf, 0xf, false));
+  v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3];
+  v[5] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(e), __float_as_int(m[0]),
+                                                    0x130, 0xf, 0xf, false));
 }
 
 __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wp = a.g.wp, rows = a.g.rows, tpr = wp >> 2, wpr = wp >> 8;
-  const int xs = wp + 4;                // padded row stride (LDS and exchange rows)
+  const int xs = wp + 4;                // padded LDS row stride
   const int bufn = 4 + a.rt * xs;       // one padded tile buffer
   float* sTC = lds;
   float* sL = sTC + lds_span(rows_floats(a.E, true));
@@ -228,40 +280,39 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   // itself for it; its last row likewise with tile + 1
   const bool nb_up = valid && ty == 0 && tile > 0;
   const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
-  unsigned* const flags = a.sync + kResidentSyncFlags;
   unsigned* const err = a.sync + kResidentSyncErr;
-  // lanes 0..nfl-1 poll the flags of the neighbour row's waves j-1 .. j+1
-  const int fj = max(wj - 1, 0);
-  const int nfl = min(wj + 1, wpr - 1) - fj + 1;
   const Rsrc rx = make_rsrc(a.xch);
-  // byte offset of x0 in exchange row [slot][k][tl][side] (4 zero floats
-  // before every row)
-  auto xoff = [&](int slot, int k, int tl, int side) {
-    return (int)(((((((long long)slot * 2 + k) * a.ntiles + tl) * 2 + side) * xs + 4) + x0) * 4);
-  };
   auto sbuf = [&](int k, int slot) { return sB0 + (2 * k + slot) * bufn + 4; };
-  // the boundary waves' hand-off: store the quad's b and J write-through into
-  // exchange slot `slot`, drain, raise the wave's flag(s) to `tag`
+  // the boundary waves' hand-off: b and J of the lane's quad as three
+  // granules {b0 b1 b2}, {b3 j0 j1}, {j2 j3 0} in exchange slot `slot`
   auto publish = [&](int slot, const float (&b)[4], const float (&j)[4], unsigned tag) {
-    if (nb_up) {
-      st4_sc1(rx, xoff(slot, 0, tile, 0), b);
-      st4_sc1(rx, xoff(slot, 1, tile, 0), j);
-    }
-    if (nb_dn) {
-      st4_sc1(rx, xoff(slot, 0, tile, 1), b);
-      st4_sc1(rx, xoff(slot, 1, tile, 1), j);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      if (nb_up) st_flag(flags + (tile * 2) * wpr + wj, tag);
-      if (nb_dn) st_flag(flags + (tile * 2 + 1) * wpr + wj, tag);
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      if (side == 0 ? !nb_up : !nb_dn) continue;
+      const int o = xch_gran(a.ntiles, wpr, slot, tile, side, wj, 0, lane);
+      st_gran(rx, o, b[0], b[1], b[2], tag);
+      st_gran(rx, o + 1024, b[3], j[0], j[1], tag);
+      st_gran(rx, o + 2048, j[2], j[3], 0.0f, tag);
     }
   };
-  // ... and wait until the neighbours' flags over this wave's columns reach
-  // `tag` (their rows are then read with sc1 loads)
-  auto await_rows = [&](unsigned tag) {
-    if (nb_up) wave_wait(flags + ((tile - 1) * 2 + 1) * wpr + fj, nfl, tag, err);
-    if (nb_dn) wave_wait(flags + ((tile + 1) * 2) * wpr + fj, nfl, tag, err);
+  // ... and the neighbour's row (tile tl, side) of the step tagged `tag`:
+  // poll its granules over this wave's columns (lanes 0 / 63 also the
+  // neighbour waves' edge cells) until every tag matches
+  auto take = [&](int slot, int tl, int side, unsigned tag, float (&vb)[6], float (&vj)[6]) {
+    const bool el = lane == 0 && wj > 0, er = lane == 63 && wj + 1 < wpr;
+    const int o = xch_gran(a.ntiles, wpr, slot, tl, side, wj, 0, lane);
+    const int eo = el ? xch_gran(a.ntiles, wpr, slot, tl, side, wj - 1, 1, 63)
+                      : xch_gran(a.ntiles, wpr, slot, tl, side, wj + 1, 0, 0);
+    u4v g[3], e[2];
+    take_granules(rx, o, el || er, eo, tag, g, e, err);
+    const float mb[4] = {__uint_as_float(g[0][0]), __uint_as_float(g[0][1]),
+                         __uint_as_float(g[0][2]), __uint_as_float(g[1][0])};
+    const float mj[4] = {__uint_as_float(g[1][1]), __uint_as_float(g[1][2]),
+                         __uint_as_float(g[2][0]), __uint_as_float(g[2][1])};
+    // lane 0: b3 / j3 of wave wj-1's lane 63 (granules 1, 2: .x, .y); lane 63:
+    // b0 / j0 of wave wj+1's lane 0 (granules 0, 1: .x, .y); 0 off the grid
+    row_quad(mb, __uint_as_float(e[0][0]), vb);
+    row_quad(mj, __uint_as_float(e[1][1]), vj);
   };
 
   // ---- prologue: dictionary, zero pads, codes, the tile's b / J into LDS
@@ -333,15 +384,14 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
     local = 0.0f;
     const bool bnd = nb_up || nb_dn;
     // one quad of step t: window rows from LDS (step t-1), the neighbour rows
-    // taken at the end of step t-1, or 0 off the grid
+    // of step t-1, or 0 off the grid
     auto step_quad = [&]() {
       Win6 wb, wj;
       if (ty > 0) {
         row_lds(sbuf(0, ci) + (ty - 1) * xs, x0, wb.v[0]);
         row_lds(sbuf(1, ci) + (ty - 1) * xs, x0, wj.v[0]);
-      } else if (nb_up) {  // the tile above's last row (its flags checked by the caller)
-        row_sc1(rx, xoff(co, 0, tile - 1, 1), wb.v[0]);
-        row_sc1(rx, xoff(co, 1, tile - 1, 1), wj.v[0]);
+      } else if (nb_up) {  // the tile above's last row
+        take(co, tile - 1, 1, a.epoch + t + 1, wb.v[0], wj.v[0]);
       } else {
         row_zero(wb.v[0]);
         row_zero(wj.v[0]);
@@ -352,8 +402,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
         row_lds(sbuf(0, ci) + (ty + 1) * xs, x0, wb.v[2]);
         row_lds(sbuf(1, ci) + (ty + 1) * xs, x0, wj.v[2]);
       } else if (nb_dn) {  // the tile below's first row
-        row_sc1(rx, xoff(co, 0, tile + 1, 0), wb.v[2]);
-        row_sc1(rx, xoff(co, 1, tile + 1, 0), wj.v[2]);
+        take(co, tile + 1, 0, a.epoch + t + 1, wb.v[2], wj.v[2]);
       } else {
         row_zero(wb.v[2]);
         row_zero(wj.v[2]);
@@ -365,13 +414,10 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
       *reinterpret_cast<f4a*>(sbuf(1, co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
     };
     if (valid) {
-      // the boundary waves: the neighbours' step t-1 rows (published at the
-      // end of their step t-1), then the quad with issue priority, then
-      // publish -- the neighbours' next inputs
-      if (bnd) {
-        __builtin_amdgcn_s_setprio(2);  // 6.0 vs 7.4 us/step at 1024^2 without
-        await_rows(a.epoch + t + 1);
-      }
+      // the boundary waves take the neighbours' step t-1 rows (published at
+      // the end of their step t-1), compute with issue priority and publish
+      // -- the neighbours' next inputs
+      if (bnd) __builtin_amdgcn_s_setprio(2);  // 6.0 vs 7.4 us/step at 1024^2 without
       step_quad();
       if (bnd) {
         if (!last) publish(ci, p, best, a.epoch + t + 2);
@@ -413,7 +459,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
 // pp2_mdp_solve's value iteration (valueIteration, src/mdp/path_planning_2d.cu:
 // 207-269) as resident sweeps: the tiles of k_loop_resident carry J only (two
 // LDS buffers and the convergence snapshot), the edge rows of J cross CUs by
-// the same flags (exchange plane k = 1), and after every block of 100 sweeps
+// the same granules (J alone: granules 0, 1), and after every block of 100 sweeps
 // each tile publishes max |J - snapshot| over its cells; once the arrival
 // counter is full every tile reads all of them (the max is exact in any
 // order) and takes the same decision: stop when the norm is <= thresh or the
@@ -439,23 +485,31 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
   const bool valid = y < rows;
   const bool nb_up = valid && ty == 0 && tile > 0;
   const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
-  unsigned* const flags = a.sync + kResidentSyncFlags;
   unsigned* const err = a.sync + kResidentSyncErr;
-  const int fj = max(wj - 1, 0);
-  const int nfl = min(wj + 1, wpr - 1) - fj + 1;
   const Rsrc rx = make_rsrc(a.xch);
-  auto xoff = [&](int slot, int tl, int side) {  // J rows: exchange plane k = 1
-    return (int)(((((((long long)slot * 2 + 1) * a.ntiles + tl) * 2 + side) * xs + 4) + x0) * 4);
-  };
   auto sbuf = [&](int i) { return sJ0 + i * bufn + 4; };
+  // k_loop_resident's hand-off with J alone: granules {j0 j1 j2}, {j3 0 0}
   auto publish = [&](int slot, const float (&j)[4], unsigned tag) {
-    if (nb_up) st4_sc1(rx, xoff(slot, tile, 0), j);
-    if (nb_dn) st4_sc1(rx, xoff(slot, tile, 1), j);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      if (nb_up) st_flag(flags + (tile * 2) * wpr + wj, tag);
-      if (nb_dn) st_flag(flags + (tile * 2 + 1) * wpr + wj, tag);
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      if (side == 0 ? !nb_up : !nb_dn) continue;
+      const int o = xch_gran(a.ntiles, wpr, slot, tile, side, wj, 0, lane);
+      st_gran(rx, o, j[0], j[1], j[2], tag);
+      st_gran(rx, o + 1024, j[3], 0.0f, 0.0f, tag);
     }
+  };
+  auto take = [&](int slot, int tl, int side, unsigned tag, float (&v)[6]) {
+    const bool el = lane == 0 && wj > 0, er = lane == 63 && wj + 1 < wpr;
+    const int o = xch_gran(a.ntiles, wpr, slot, tl, side, wj, 0, lane);
+    // lane 0: j3 of wave wj-1's lane 63 (granule 1 .x); lane 63: j0 of wave
+    // wj+1's lane 0 (granule 0 .x)
+    const int eo = el ? xch_gran(a.ntiles, wpr, slot, tl, side, wj - 1, 1, 63)
+                      : xch_gran(a.ntiles, wpr, slot, tl, side, wj + 1, 0, 0);
+    u4v g[2], e[1];
+    take_granules(rx, o, el || er, eo, tag, g, e, err);
+    const float m[4] = {__uint_as_float(g[0][0]), __uint_as_float(g[0][1]),
+                        __uint_as_float(g[0][2]), __uint_as_float(g[1][0])};
+    row_quad(m, __uint_as_float(e[0][0]), v);
   };
 
   stage_rows(a.rows, rows_floats(a.E, true), sTC);
@@ -490,18 +544,14 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
     const bool fin = a.nsweeps > 0 && s == a.nsweeps - 1;
     const bool check = a.nsweeps == 0 && s % kSolveBlock == kSolveBlock - 1;
     if (valid) {
-      if (nb_up || nb_dn) {
-        __builtin_amdgcn_s_setprio(2);
-        if (nb_up) wave_wait(flags + ((tile - 1) * 2 + 1) * wpr + fj, nfl, a.epoch + s + 1, err);
-        if (nb_dn) wave_wait(flags + ((tile + 1) * 2) * wpr + fj, nfl, a.epoch + s + 1, err);
-      }
+      if (nb_up || nb_dn) __builtin_amdgcn_s_setprio(2);
       Win6 w;
       if (ty > 0) row_lds(sbuf(ci) + (ty - 1) * xs, x0, w.v[0]);
-      else if (nb_up) row_sc1(rx, xoff(co, tile - 1, 1), w.v[0]);
+      else if (nb_up) take(co, tile - 1, 1, a.epoch + s + 1, w.v[0]);
       else row_zero(w.v[0]);
       row_lds(sbuf(ci) + ty * xs, x0, w.v[1]);
       if (ty + 1 < a.rt && y + 1 < rows) row_lds(sbuf(ci) + (ty + 1) * xs, x0, w.v[2]);
-      else if (nb_dn) row_sc1(rx, xoff(co, tile + 1, 0), w.v[2]);
+      else if (nb_dn) take(co, tile + 1, 0, a.epoch + s + 1, w.v[2]);
       else row_zero(w.v[2]);
       float jn[9][4];
 #pragma unroll
@@ -602,7 +652,6 @@ bool resident_plan(const Geom& g, int E, int es, int ts, int ncus, ResidentPlan*
   p->ntiles = (g.rows + rt - 1) / rt;
   p->threads = (int)threads;
   p->lds = lds;
-  p->flag_words = 2 * p->ntiles * (g.wp / 256);
   return p->ntiles <= ncus;
 }
 
@@ -639,7 +688,6 @@ bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p) {
   p->ntiles = (g.rows + rt - 1) / rt;
   p->threads = (int)threads;
   p->lds = lds;
-  p->flag_words = 2 * p->ntiles * (g.wp / 256);
   return p->ntiles <= ncus;
 }
 

@@ -767,11 +767,7 @@ static void resident_free(pp2_ctx* c) {
 static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
   if (c->res_sync && c->res_ntiles == p.ntiles) return true;
   resident_free_buffers(c);
-  // flag words for the finest layout any resident kernel uses (one per
-  // 128-column wave and tile side), whichever plan allocates first
-  const size_t flag_words = (size_t)2 * p.ntiles * (c->g.wp / 128);
-  const size_t sync_b = (pp2::kResidentSyncFlags + std::max(flag_words, (size_t)p.flag_words)) *
-                        sizeof(unsigned);
+  const size_t sync_b = (size_t)pp2::kResidentSyncWords * sizeof(unsigned);
   const size_t ring_b = (size_t)pp2::kResidentRing * pp2::mass_partials(c->g, 4) * sizeof(float);
   const size_t xch_b = pp2::resident_xch_floats(c->g, p.ntiles) * sizeof(float);
   const size_t tmax_b = (size_t)2 * p.ntiles * sizeof(float);

@@ -9,7 +9,7 @@ WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of
 a wide (16 B/lane) coalesced streaming read, so it is doubled; WRITE_SIZE is
 exact for 16-B-per-lane streaming stores.
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
-Usage: python profiles/parse_pmc.py <tag> [cells]
+Usage: python profiles/parse_pmc.py <tag> [cells] [steps per resident launch]
 """
 import csv
 import json
@@ -22,7 +22,8 @@ OUT = os.path.join(ROOT, "gpurun_out")
 # algorithmic HBM bytes per cell (bench.py docstring / DESIGN.md)
 ALGO = {"k_mdp_sweep": 369, "k_belief_update": 48, "k_loop_step": 417,
         "k_loop_step_coded": 19, "k_mdp_sweep_coded": 11,
-        "k_loop_pair_coded": 19}  # two steps per launch, intermediate in LDS
+        "k_loop_pair_coded": 19,  # two steps per launch, intermediate in LDS
+        "k_loop_resident": 19}  # the whole trajectory per launch, tiles in LDS
 
 
 def short(name):
@@ -40,6 +41,7 @@ def counter(path):
 def main():
     tag = sys.argv[1]
     cells = int(sys.argv[2]) if len(sys.argv) > 2 else 1024 * 1024
+    spl = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     stats = {}
     for r in csv.DictReader(open(os.path.join(OUT, "prof", "run_kernel_stats.csv"))):
         stats[short(r["Name"])] = r
@@ -59,6 +61,8 @@ def main():
             d["hbm_bytes_per_launch"] = (2 * f + w) * 1024
         if base in ALGO:
             d["cells"] = cells
+            if base == "k_loop_resident":
+                d["steps_per_launch"] = spl
             d["algorithmic_bytes_per_launch"] = ALGO[base] * cells
             d["algorithmic_GBps"] = ALGO[base] * cells / (d["avg_us"] * 1e-6) / 1e9
             if "hbm_bytes_per_launch" in d:
