@@ -50,46 +50,68 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, int n,
   }
 }
 
-// Factored-row Bellman backup of N cells from their codes (k_mdp_sweep's
-// arithmetic): cell-outer, fully unrolled (support positions index jn at
-// compile time): one IW record, then per action a quad from QT (a float for
-// the one-cell stay support) and the cost from CT at the same byte offset.
-// The scheduling barrier keeps one cell's loads live at a time.  Actions are
-// compared in ascending order, so best/arg are the dense kernel's.  ARG =
-// false: values only, best = minnum over the actions (see coded_sweep4).
+// Factored-row Bellman backup of cell k of N (k_mdp_sweep's arithmetic) from
+// its IW record {w0, w1, w2}: per action a quad from QT (a float for the
+// one-cell stay support) and the cost from CT at the same byte offset; the
+// support positions index jn at compile time.  Actions are compared in
+// ascending order, so best/arg are the dense kernel's.  ARG = false: values
+// only, best = minnum over the actions (see coded_sweep4).
+template <int N, bool ARG>
+__device__ __forceinline__ void sweep_cell_fact(const float* sTC, uint32_t w0, uint32_t w1,
+                                                uint32_t w2, const float (&jn)[9][N], int k,
+                                                float& best, uint32_t& arg) {
+  const char* qt = reinterpret_cast<const char*>(sTC + kFactQT);
+  const char* ct = reinterpret_cast<const char*>(sTC + kFactCT);
+#pragma unroll
+  for (int a = 0; a < 9; ++a) {
+    const uint32_t w = a < 4 ? w0 : a < 8 ? w1 : w2;
+    const uint32_t off = __builtin_amdgcn_ubfe(w, 8 * (a % 4), 8);
+    const int tab = a * kFactK * 16;  // byte offset of action a's table
+    float tv[4];
+    if (kSupN[a] == 1) {
+      tv[0] = *reinterpret_cast<const float*>(qt + tab + off);
+    } else {
+      const f4a t = *reinterpret_cast<const f4a*>(qt + tab + off);
+      tv[0] = t[0]; tv[1] = t[1]; tv[2] = t[2]; tv[3] = t[3];
+    }
+    float cost = *reinterpret_cast<const float*>(ct + tab + off);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);
+    if constexpr (ARG) {
+      if (cost < best) { best = cost; arg = (uint32_t)a; }
+    } else {
+      best = __builtin_fminf(best, cost);
+    }
+  }
+}
+
+// The backup of N cells from their codes: cell-outer, one IW record per cell,
+// the scheduling barrier keeps one cell's loads live at a time.
 template <int N, bool ARG>
 __device__ __forceinline__ void coded_sweep_sparse(const float* sTC, const uint32_t (&cc)[N],
                                                    const float (&jn)[9][N], float (&best)[N],
                                                    uint32_t (&arg)[N]) {
-  const char* qt = reinterpret_cast<const char*>(sTC + kFactQT);
-  const char* ct = reinterpret_cast<const char*>(sTC + kFactCT);
 #pragma unroll
   for (int k = 0; k < N; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     const uint4 iw = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * cc[k]);
+    sweep_cell_fact<N, ARG>(sTC, iw.x, iw.y, iw.z, jn, k, best[k], arg[k]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The same with the cells' IW records held in registers (the resident loop).
+template <int N, bool ARG>
+__device__ __forceinline__ void coded_sweep_iw(const float* sTC, const uint32_t (&iw)[N][3],
+                                               const float (&jn)[9][N], float (&best)[N],
+                                               uint32_t (&arg)[N]) {
 #pragma unroll
-    for (int a = 0; a < 9; ++a) {
-      const uint32_t w = a < 4 ? iw.x : a < 8 ? iw.y : iw.z;
-      const uint32_t off = __builtin_amdgcn_ubfe(w, 8 * (a % 4), 8);
-      const int tab = a * kFactK * 16;  // byte offset of action a's table
-      float tv[4];
-      if (kSupN[a] == 1) {
-        tv[0] = *reinterpret_cast<const float*>(qt + tab + off);
-      } else {
-        const f4a t = *reinterpret_cast<const f4a*>(qt + tab + off);
-        tv[0] = t[0]; tv[1] = t[1]; tv[2] = t[2]; tv[3] = t[3];
-      }
-      float cost = *reinterpret_cast<const float*>(ct + tab + off);
+  for (int k = 0; k < N; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j < kSupN[a]) cost = __builtin_fmaf(tv[j], jn[kSup[a][j]][k], cost);
-      if constexpr (ARG) {
-        if (cost < best[k]) { best[k] = cost; arg[k] = (uint32_t)a; }
-      } else {
-        best[k] = __builtin_fminf(best[k], cost);
-      }
-    }
+  for (int k = 0; k < N; ++k) {
+    sweep_cell_fact<N, ARG>(sTC, iw[k][0], iw[k][1], iw[k][2], jn, k, best[k], arg[k]);
     __builtin_amdgcn_sched_barrier(0);
   }
 }

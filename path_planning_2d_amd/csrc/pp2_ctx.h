@@ -100,9 +100,11 @@ struct pp2_ctx {
   float* d_rows = nullptr;         // LDS-layout rows, gamma*T (rows_floats: factored or kDictTC)
   float* d_dl = nullptr;           // L transposed: [z][entry]
   float* d_tu = nullptr;           // raw T per action: [u][entry][4 sparse | 9 full]
+  float* d_rfact = nullptr;        // resident class tables (pp2_internal.h kRes*)
   int dict_n = 0;                  // entries; 0 = no dictionary (dense path only)
   bool dict_sparse = false;        // every T row is zero off the base-kernel support
   bool dict_t_finite = false;      // every dictionary T entry is finite
+  bool dict_rfact = false;         // d_rfact valid: raw T and L by class (<= 16 each)
   // the sparse rows' T == 0 skip needs finite, non-negative beliefs (not -0):
   // false after a pp2_belief_set that breaks that, until the next one
   bool belief_sparse_ok = true;

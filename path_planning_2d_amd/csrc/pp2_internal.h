@@ -145,6 +145,20 @@ constexpr int kDictMax = 400;  // coded_loop_lds_bytes(kDictMax, false) <= kDict
 // one cost from 256-B tables whose 16 entries sit on 16 distinct bank quads
 // (conflict-free gathers).  More than kFactK pairs for any action: full rows.
 constexpr int kFactK = 16;
+// Class tables of the tile-resident loop (pp2_resident.hip), one image at the
+// start of its LDS: the pair classes above also fix the raw T support quad
+// (the host keys them on it too), and the dictionary's L columns (16 values
+// per entry, one per z) take at most kResLK distinct vectors (16 on the grid
+// of a generated model, plus the zero vector of the halo rows and pads).
+//   QR  [9][kFactK] quads: raw T at kSup[a][0..3] of the class (belief gather,
+//       addressed by the same 16 * class byte offsets as QT / CT)
+//   LT  [16 z][kResLK]: L_z of the L class
+//   LX  [E] bytes (global only): 4 * L class of the entry
+constexpr int kResLK = 32;
+constexpr int kResQR = 0;
+constexpr int kResLT = 9 * kFactK * 4;
+constexpr int kResTab = kResLT + 16 * kResLK;  // floats of the LDS image
+constexpr int kResLX = kResTab;                // byte table after it (global)
 constexpr int kFactQT = 0;
 constexpr int kFactCT = 9 * kFactK * 4;
 constexpr int kFactIW = 2 * 9 * kFactK * 4;
@@ -223,11 +237,10 @@ struct ResidentPlan {
 struct ResidentRun {
   Geom g;
   float gamma;
-  int E, es, ts;             // entries; L_z column stride (dl[z*es]); T_u table stride (tu[u*ts])
+  int E;                     // dictionary entries
   const uint16_t* code;      // code plane (row 0, x 0)
   const float* rows;         // factored sweep rows
-  const float* dl;           // L transposed [16][es]
-  const float* tu;           // raw T per action [9][ts]
+  const float* rfact;        // class tables: kResTab floats (QR, LT), then the LX bytes
   const float* b_in;         // step 0's input belief / value planes (row 0)
   const float* j_in;
   float* b_out;              // the last step's output planes
@@ -270,14 +283,14 @@ struct SweepRun {
   double thresh;       // stop when norm <= thresh
   int nsweeps;         // > 0: exactly this many sweeps, no convergence checks
 };
-size_t resident_lds_bytes(const Geom& g, int E, int es, int ts, int rt);
+size_t resident_lds_bytes(const Geom& g, int E, int rt);
 bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p);
 hipError_t launch_sweep_resident(hipStream_t st, const ResidentPlan& p, const SweepRun& a);
 inline size_t resident_xch_floats(const Geom& g, int ntiles) {
   // [step & 1][tile][top, bottom][wave of row][3][lane] 16-B granules
   return (size_t)2 * ntiles * 2 * (g.wp / 256) * 3 * 64 * 4;
 }
-bool resident_plan(const Geom& g, int E, int es, int ts, int ncus, ResidentPlan* p);
+bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p);
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a);
 
 }  // namespace pp2

@@ -129,44 +129,82 @@ __device__ __forceinline__ float wave_reduce_partials_sc1(const float* p, int n)
 }
 
 // The coded belief gather of action U for a lane's quad (belief_vals'
-// arithmetic) on a window whose off-grid cells are 0: the resident kernel's
-// LDS rows and exchange rows carry zero pads, so instead of zeroing T at the
-// x edges it multiplies the edge code's (finite, resident_plan checks) T by
-// b = +0, and fmaf(T, +0, p) == p for the non-negative partial sums.
+// arithmetic, the same fmaf order) by classes: the raw T of a source cell x'
+// for action U is QR[U][class of x' for U][slot], the class byte offset (16 *
+// class) read from the tile's plane of action U (rows ty-1 .. ty+1 at plane
+// rows ty .. ty+2; x0-1 / x0+4 from the neighbour lanes' dwords by DPP wave
+// shifts, lanes 0 / 63 read those dwords themselves), and L_z of the cell is
+// LT[z][L class] with the 4 * class bytes of the lane's cells in lx4.  Every
+// table read hits a <= 16-entry table (no bank conflicts), where code-indexed
+// reads of 274-entry tables collide.  The window's off-grid cells are 0: the
+// LDS rows carry zero pads and off-grid plane bytes are class 0, whose
+// (finite, the host checks) T multiplies b = +0, and fmaf(T, +0, p) == p for
+// the non-negative partial sums.
+constexpr bool belief_row_used(int U, int oy) {
+  for (int s = 3 * oy; s < 3 * oy + 3; ++s)
+    if (sup_slot(U, 8 - s) >= 0) return true;
+  return false;
+}
 template <int U>
-__device__ __forceinline__ void belief_quad(const float* sTu, const float* sL, float inv,
-                                            const CodeWin6& cw, const Win6& win, float (&p)[4],
+__device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0, uint32_t lx4,
+                                            int z, float inv, const Win6& win, float (&p)[4],
                                             float& local) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const char* qr = reinterpret_cast<const char*>(lds + kResQR) + U * kFactK * 16;
+  const char* lt = reinterpret_cast<const char*>(lds + kResLT) + z * (kResLK * 4);
+  const int lane = threadIdx.x & 63;
+  // per window row: the class bytes of x0-1 .. x0+4
+  uint32_t cb[3][6];
+#pragma unroll
+  for (int oy = 0; oy < 3; ++oy) {
+    if (!belief_row_used(U, oy)) continue;
+    const uint8_t* r = prow + oy * ps + 4 + x0;
+    const uint32_t m = *reinterpret_cast<const uint32_t*>(r);
+    uint32_t e = 0u;
+    if (lane == 0 || lane == 63) e = *reinterpret_cast<const uint32_t*>(r + (lane == 0 ? -4 : 4));
+    const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp((int)e, (int)m, 0x138, 0xf, 0xf, false);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp((int)e, (int)m, 0x130, 0xf, 0xf, false);
+    cb[oy][0] = l >> 24;
+    cb[oy][1] = m & 0xffu;
+    cb[oy][2] = __builtin_amdgcn_ubfe(m, 8, 8);
+    cb[oy][3] = __builtin_amdgcn_ubfe(m, 16, 8);
+    cb[oy][4] = m >> 24;
+    cb[oy][5] = h & 0xffu;
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) p[k] = 0.0f;
 #pragma unroll
   for (int s = 0; s < 9; ++s) {
     const int oy = s / 3, ox = s % 3 - 1;
-    constexpr int kTu = tu_width(true);
     const int sl = sup_slot(U, 8 - s);
     if (sl < 0) continue;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      p[k] = __builtin_fmaf(sTu[cw.at(oy, k + 1 + ox) * kTu + sl], win.v[oy][k + 1 + ox], p[k]);
+      p[k] = __builtin_fmaf(*reinterpret_cast<const float*>(qr + 4 * sl + cb[oy][k + 1 + ox]),
+                            win.v[oy][k + 1 + ox], p[k]);
     __builtin_amdgcn_sched_barrier(0);  // <= 4 gathers in flight
   }
   local = 0.0f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    p[k] = p[k] * sL[cw.at(1, k + 1)];
+    p[k] = p[k] * *reinterpret_cast<const float*>(lt + __builtin_amdgcn_ubfe(lx4, 8 * k, 8));
     p[k] = p[k] * inv;
     local += p[k];
   }
 }
 
-__device__ __forceinline__ void belief_any(int u, const float* sTu, const float* sL, float inv,
-                                           const CodeWin6& cw, const Win6& w, float (&p)[4],
-                                           float& local) {
+// sP: the tile's class planes [9][rt + 2][ps] (ps = wp + 8 bytes: 4 pad
+// bytes on each side); this lane's rows start at plane row ty.
+__device__ __forceinline__ void belief_any(int u, const uint8_t* sP, int prows, int ps, int ty,
+                                           int x0, uint32_t lx4, int z, float inv, const Win6& w,
+                                           float (&p)[4], float& local) {
   switch (u) {
-#define PP2_BQ(UU) \
-  case UU: belief_quad<UU>(sTu, sL, inv, cw, w, p, local); break;
+#define PP2_BQ(UU)                                                                       \
+  case UU:                                                                               \
+    belief_fact<UU>(sP + (UU * prows + ty) * ps, ps, x0, lx4, z, inv, w, p, local); \
+    break;
     PP2_BQ(0) PP2_BQ(1) PP2_BQ(2) PP2_BQ(3) PP2_BQ(4) PP2_BQ(5) PP2_BQ(6) PP2_BQ(7)
-    default: belief_quad<8>(sTu, sL, inv, cw, w, p, local);
+    default: belief_fact<8>(sP + (8 * prows + ty) * ps, ps, x0, lx4, z, inv, w, p, local);
 #undef PP2_BQ
   }
 }
@@ -262,10 +300,12 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   const int wp = a.g.wp, rows = a.g.rows, tpr = wp >> 2, wpr = wp >> 8;
   const int xs = wp + 4;                // padded LDS row stride
   const int bufn = 4 + a.rt * xs;       // one padded tile buffer
-  float* sTC = lds;
-  float* sL = sTC + lds_span(rows_floats(a.E, true));
-  float* sTu = sL + lds_span(16 * a.es);
-  float* sB0 = sTu + lds_span(9 * a.ts);  // b buffers 0, 1, then J buffers 0, 1
+  // LDS: class tables (QR, LT: constant offsets), factored sweep rows (QT, CT:
+  // constant offsets; IW), class planes, b buffers 0, 1, J buffers 0, 1
+  const int prows = a.rt + 2, ps = wp + 8;
+  float* sTC = lds + lds_span(kResTab);  // (stage_rows writes up to the span)
+  uint8_t* sP = reinterpret_cast<uint8_t*>(sTC + lds_span(rows_floats(a.E, true)));
+  float* sB0 = reinterpret_cast<float*>(sP) + lds_span(9 * prows * ps / 4);
   float* sS = sB0 + 4 * bufn;
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -318,16 +358,55 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   // ---- prologue: dictionary, zero pads, codes, the tile's b / J into LDS
   // buffer 0, boundary rows into exchange slot 1 (as if step -1's output),
   // then the neighbours' rows for step 0
+  stage_rows(a.rfact, kResTab, lds);
   stage_rows(a.rows, rows_floats(a.E, true), sTC);
-  stage_rows(a.dl, 16 * a.es, sL);
-  stage_rows(a.tu, 9 * a.ts, sTu);
   for (int i = threadIdx.x; i < 4 * (a.rt + 1); i += blockDim.x) {
     const int buf = i / (a.rt + 1), r = i % (a.rt + 1);
     *reinterpret_cast<f4a*>(sB0 + buf * bufn + r * xs) = f4a{0.0f, 0.0f, 0.0f, 0.0f};
   }
-  CodeWin6 cw;
+  // the lane's cells: codes, their IW records (registers for the whole run)
+  // and L class bytes
+  uint32_t cc[4] = {0u, 0u, 0u, 0u}, iwr[4][3], lx4 = 0u;
   if (valid) {
-    load_codes6(a.code, wp, y, x0, cw);
+    const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)y * wp + x0);
+    cc[0] = m.x & 0xffffu; cc[1] = m.x >> 16; cc[2] = m.y & 0xffffu; cc[3] = m.y >> 16;
+    const uint8_t* lx = reinterpret_cast<const uint8_t*>(a.rfact + kResLX);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lx4 |= (uint32_t)lx[cc[k]] << (8 * k);
+  }
+  __syncthreads();  // the staged tables
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 w = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * cc[k]);
+    iwr[k][0] = w.x; iwr[k][1] = w.y; iwr[k][2] = w.z;
+  }
+  // class planes of rows tile*rt-1 .. tile*rt+rt: byte x+4 of plane a, row r
+  // = 16 * class of cell (y, x) for action a (0 off the grid and in the pads)
+  for (int i = threadIdx.x; i < prows * tpr; i += blockDim.x) {
+    const int r = i / tpr, xq = (i % tpr) * 4, yy = tile * a.rt + r - 1;
+    uint32_t pl[9] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (yy >= 0 && yy < rows) {
+      const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)yy * wp + xq);
+      const uint32_t c4[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 w = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * c4[k]);
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+          const uint32_t wq = q < 4 ? w.x : q < 8 ? w.y : w.z;
+          pl[q] |= __builtin_amdgcn_ubfe(wq, 8 * (q % 4), 8) << (8 * k);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+      *reinterpret_cast<uint32_t*>(sP + (q * prows + r) * ps + 4 + xq) = pl[q];
+  }
+  for (int i = threadIdx.x; i < 9 * prows; i += blockDim.x) {
+    *reinterpret_cast<uint32_t*>(sP + i * ps) = 0u;
+    *reinterpret_cast<uint32_t*>(sP + i * ps + 4 + wp) = 0u;
+  }
+  if (valid) {
     const long long off = (long long)y * wp + x0;
     const f4a b = *reinterpret_cast<const f4a*>(a.b_in + off);
     const f4a j = *reinterpret_cast<const f4a*>(a.j_in + off);
@@ -407,9 +486,15 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
         row_zero(wb.v[2]);
         row_zero(wj.v[2]);
       }
-      belief_any(u, sTu + u * a.ts, sL + z * a.es, inv, cw, wb, p, local);
-      if (last) sweep_vals<true>(sTC, a.gamma, cw, wj, best, arg);  // actions: last step only
-      else sweep_vals<false>(sTC, a.gamma, cw, wj, best, arg);
+      PP2_RT(1);
+      belief_any(u, sP, prows, ps, ty, x0, lx4, z, inv, wb, p, local);
+      float jn[9][4];
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) jn[i][k] = wj.v[i / 3][k + i % 3];
+      if (last) coded_sweep_iw<4, true>(sTC, iwr, jn, best, arg);  // actions: last step only
+      else coded_sweep_iw<4, false>(sTC, iwr, jn, best, arg);
       *reinterpret_cast<f4a*>(sbuf(0, co) + ty * xs + x0) = f4a{p[0], p[1], p[2], p[3]};
       *reinterpret_cast<f4a*>(sbuf(1, co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
     };
@@ -423,7 +508,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
         if (!last) publish(ci, p, best, a.epoch + t + 2);
         __builtin_amdgcn_s_setprio(0);
       }
-      PP2_RT(1);
+      PP2_RT(2);
     }
     if (last) break;  // the last step's outputs are stored after the loop
     // ---- mass partials of step t (dense map), sc1 into the ring
@@ -627,17 +712,18 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
 
 }  // namespace
 
-size_t resident_lds_bytes(const Geom& g, int E, int es, int ts, int rt) {
-  return ((size_t)lds_span(rows_floats(E, true)) + lds_span(16 * es) + lds_span(9 * ts) +
-          4 * (4 + (size_t)rt * (g.wp + 4)) + 16) * sizeof(float);
+size_t resident_lds_bytes(const Geom& g, int E, int rt) {
+  return ((size_t)lds_span(kResTab) + lds_span(rows_floats(E, true)) +
+          lds_span(9 * (rt + 2) * (g.wp + 8) / 4) + 4 * (4 + (size_t)rt * (g.wp + 4)) + 16) *
+         sizeof(float);
 }
 
-bool resident_plan(const Geom& g, int E, int es, int ts, int ncus, ResidentPlan* p) {
+bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p) {
   if (E <= 0 || g.rows <= 0 || g.wp % 256 != 0 || ncus <= 0) return false;
   const int rt = (g.rows + ncus - 1) / ncus;
   const long long threads = (long long)rt * (g.wp / 4);
   if (threads > 1024) return false;
-  const size_t lds = resident_lds_bytes(g, E, es, ts, rt);
+  const size_t lds = resident_lds_bytes(g, E, rt);
   if (lds > kDictLdsMaxBytes) return false;
   static unsigned long long attr = 0;
   allow_lds(reinterpret_cast<const void*>(&k_loop_resident), attr);

@@ -337,7 +337,9 @@ int build_model_dict(pp2_ctx* c) {
         hipMalloc(&c->d_dict, (size_t)pp2::kDictMax * pp2::kDictRow * sizeof(float)) != hipSuccess ||
         hipMalloc(&c->d_rows, ((size_t)pp2::kDictMax * pp2::kDictTC + 4) * sizeof(float)) != hipSuccess ||
         hipMalloc(&c->d_dl, (size_t)pp2::kDictMax * 16 * sizeof(float)) != hipSuccess ||
-        hipMalloc(&c->d_tu, ((size_t)9 * pp2::kDictMax * 9 + 4) * sizeof(float)) != hipSuccess)
+        hipMalloc(&c->d_tu, ((size_t)9 * pp2::kDictMax * 9 + 4) * sizeof(float)) != hipSuccess ||
+        hipMalloc(&c->d_rfact, ((size_t)pp2::kResTab + pp2::kDictMax / 4 + 4) * sizeof(float)) !=
+            hipSuccess)
       return set_err(PP2_ENOMEM, "hipMalloc model dictionary");
     HIPCHK(hipMemsetAsync(c->code_alloc, 0, (size_t)(n + 2 * kGuard) * sizeof(uint16_t), c->stream));
     c->d_code = c->code_alloc + kGuard + (long long)c->g.halo * c->g.wp;
@@ -430,26 +432,53 @@ int build_model_dict(pp2_ctx* c) {
         if (!in && bits != 0) { sparse = false; break; }
       }
   // Factored sweep rows (pp2_internal.h): per action the distinct (gT support
-  // quad, C_a) pairs, at most kFactK of them, else the full rows.
+  // quad, C_a) pairs, at most kFactK of them, else the full rows.  The classes
+  // are keyed on the raw T quad as well, so that a class also fixes the belief
+  // gather's T (the resident loop's QR table; gT = fl(gamma * T) does not
+  // determine T in general).
   std::vector<uint32_t> fact_iw((size_t)E * 4, 0u);
   std::vector<float> fact_qt(9 * pp2::kFactK * 4, 0.0f), fact_ct(9 * pp2::kFactK * 4, 0.0f);
+  std::vector<float> rfact((size_t)pp2::kResTab + pp2::kDictMax / 4 + 4, 0.0f);
   for (int a = 0; a < 9 && sparse; ++a) {
-    std::vector<std::array<uint32_t, 5>> pairs;
+    std::vector<std::array<uint32_t, 9>> pairs;
     for (int e = 0; e < E && sparse; ++e) {
       const float* src = &dh[(size_t)e * pp2::kDictRow];
-      float q[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      for (int j = 0; j < pp2::kSupN[a]; ++j) q[j] = gam * src[a * 10 + pp2::kSup[a][j]];
-      std::array<uint32_t, 5> key;
+      float q[4] = {0.0f, 0.0f, 0.0f, 0.0f}, r[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int j = 0; j < pp2::kSupN[a]; ++j) {
+        r[j] = src[a * 10 + pp2::kSup[a][j]];
+        q[j] = gam * r[j];
+      }
+      std::array<uint32_t, 9> key;
       std::memcpy(key.data(), q, 16);
       std::memcpy(&key[4], &src[a * 10 + 9], 4);
+      std::memcpy(&key[5], r, 16);
       size_t k = std::find(pairs.begin(), pairs.end(), key) - pairs.begin();
       if (k == pairs.size()) {
         if ((int)k >= pp2::kFactK) { sparse = false; break; }
         pairs.push_back(key);
         std::memcpy(&fact_qt[(a * pp2::kFactK + k) * 4], q, 16);
         std::memcpy(&fact_ct[(a * pp2::kFactK + k) * 4], &key[4], 4);
+        std::memcpy(&rfact[pp2::kResQR + (a * pp2::kFactK + k) * 4], r, 16);
       }
       fact_iw[(size_t)e * 4 + a / 4] |= (uint32_t)(16 * k) << (8 * (a % 4));
+    }
+  }
+  // L classes: the distinct 16-vectors (L_0..L_15 bits) of the entries
+  bool rfact_ok = sparse;
+  {
+    std::vector<std::array<uint32_t, 16>> lcls;
+    uint8_t* lx = reinterpret_cast<uint8_t*>(&rfact[pp2::kResLX]);
+    for (int e = 0; e < E && rfact_ok; ++e) {
+      std::array<uint32_t, 16> key;
+      std::memcpy(key.data(), &dh[(size_t)e * pp2::kDictRow + pp2::kDictL], 64);
+      size_t k = std::find(lcls.begin(), lcls.end(), key) - lcls.begin();
+      if (k == lcls.size()) {
+        if ((int)k >= pp2::kResLK) { rfact_ok = false; break; }
+        lcls.push_back(key);
+        for (int z = 0; z < 16; ++z)
+          std::memcpy(&rfact[pp2::kResLT + z * pp2::kResLK + k], &key[z], 4);
+      }
+      lx[e] = (uint8_t)(4 * k);
     }
   }
   const int tw = pp2::tu_width(sparse);
@@ -487,9 +516,12 @@ int build_model_dict(pp2_ctx* c) {
                         c->stream));
   HIPCHK(hipMemcpyAsync(c->d_tu, tu.data(), tu.size() * sizeof(float), hipMemcpyHostToDevice,
                         c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_rfact, rfact.data(), rfact.size() * sizeof(float),
+                        hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->dict_sparse = sparse;
   c->dict_t_finite = t_finite;
+  c->dict_rfact = rfact_ok;
   c->dict_n = E;
   return PP2_OK;
 }
@@ -810,15 +842,14 @@ static int resident_check(pp2_ctx* c) {
 // changes size.
 static bool resident_ready(pp2_ctx* c) {
   if (!c->resident || c->comm || c->group || !coded_active(c) || !c->dict_sparse ||
-      !c->dict_t_finite || c->norm_block > pp2::kResidentRing - 2 || c->ncus <= 0)
+      !c->dict_t_finite || !c->dict_rfact || c->norm_block > pp2::kResidentRing - 2 ||
+      c->ncus <= 0)
     return false;
   if (c->res_plan_e != c->dict_n) {
     c->res_plan_e = c->dict_n;
     c->res_ok = false;
-    const int es = (c->dict_n + 3) & ~3;
-    const int ts = (c->dict_n * pp2::tu_width(true) + 3) & ~3;
     pp2::ResidentPlan p;
-    if (!pp2::resident_plan(c->g, c->dict_n, es, ts, c->ncus, &p)) return false;
+    if (!pp2::resident_plan(c->g, c->dict_n, c->ncus, &p)) return false;
     c->res_plan = p;
     c->res_ok = true;
   }
@@ -920,12 +951,9 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
     a.g = c->g;
     a.gamma = c->gamma;
     a.E = c->dict_n;
-    a.es = (c->dict_n + 3) & ~3;
-    a.ts = (c->dict_n * pp2::tu_width(true) + 3) & ~3;
     a.code = c->d_code;
     a.rows = c->d_rows;
-    a.dl = c->d_dl;
-    a.tu = c->d_tu;
+    a.rfact = c->d_rfact;
     a.b_in = c->b[bc].v.p;
     a.j_in = c->J[jc].v.p;
     a.b_out = c->b[bf].v.p;  // == b_in for even m: each lane reads its cells first
@@ -1065,7 +1093,7 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->staging) (void)hipFree(c->staging);
   if (c->code_alloc) (void)hipFree(c->code_alloc);
   resident_free(c);
-  for (float* p : {c->d_dict, c->d_rows, c->d_dl, c->d_tu})
+  for (float* p : {c->d_dict, c->d_rows, c->d_dl, c->d_tu, c->d_rfact})
     if (p) (void)hipFree(p);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
