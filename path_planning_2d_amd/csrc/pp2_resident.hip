@@ -247,9 +247,32 @@ __device__ __forceinline__ int xch_gran(int ntiles, int wpr, int slot, int tl, i
                                         int k, int ln) {
   return (((((slot * ntiles + tl) * 2 + side) * wpr + w) * 3 + k) * 64 + ln) * 16;
 }
+template <int AUX>
 __device__ __forceinline__ void st_gran(Rsrc r, int off, float x, float y, float z, unsigned tag) {
   const u4v t = {__float_as_uint(x), __float_as_uint(y), __float_as_uint(z), tag};
-  __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, kSc1);
+  __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, AUX);
+}
+// Whether tile `nb` runs on the same XCD as this workgroup: blocks are dealt
+// round-robin over the 8 XCDs (MI355X_MICROARCH.md: blocks b and b + 8 share
+// one) and xcd_remap gives each class b % 8 a contiguous run of tiles.  A
+// granule for a same-XCD consumer is stored plain: it stays in the shared L2,
+// where the consumer's sc1 loads find it (an sc1 store drops the line and
+// the reader fetches it at the cross-XCD rate).  Should the observation not
+// hold, the consumer's bounded wait times out and reports the error -- a tag
+// is never matched by stale data.
+__device__ __forceinline__ bool same_xcd(int nb) {
+  const int n = gridDim.x, q = n / 8, r = n % 8, x = blockIdx.x % 8;
+  const int first = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return nb >= first && nb < first + q + (x < r);
+}
+// One granule store of a hand-off: plain for a same-XCD consumer, else sc1.
+__device__ __forceinline__ void st_gran_to(bool same, Rsrc r, int off, float x, float y, float z,
+                                           unsigned tag) {
+#ifndef PP2_GRAN_ALL_SC1  // A/B builds only
+  if (same) st_gran<0>(r, off, x, y, z, tag);
+  else
+#endif
+  st_gran<kSc1>(r, off, x, y, z, tag);
 }
 // The wave polls granules g[k] at o + 1 KiB * k and (edge lanes) e[k] at
 // eo + 1 KiB * k until all carry `tag`.  Bounded like wave_wait; the empty
@@ -320,6 +343,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   // itself for it; its last row likewise with tile + 1
   const bool nb_up = valid && ty == 0 && tile > 0;
   const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
+  const bool same_up = same_xcd(tile - 1), same_dn = same_xcd(tile + 1);
   unsigned* const err = a.sync + kResidentSyncErr;
   const Rsrc rx = make_rsrc(a.xch);
   auto sbuf = [&](int k, int slot) { return sB0 + (2 * k + slot) * bufn + 4; };
@@ -330,9 +354,10 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
     for (int side = 0; side < 2; ++side) {
       if (side == 0 ? !nb_up : !nb_dn) continue;
       const int o = xch_gran(a.ntiles, wpr, slot, tile, side, wj, 0, lane);
-      st_gran(rx, o, b[0], b[1], b[2], tag);
-      st_gran(rx, o + 1024, b[3], j[0], j[1], tag);
-      st_gran(rx, o + 2048, j[2], j[3], 0.0f, tag);
+      const bool same = side == 0 ? same_up : same_dn;
+      st_gran_to(same, rx, o, b[0], b[1], b[2], tag);
+      st_gran_to(same, rx, o + 1024, b[3], j[0], j[1], tag);
+      st_gran_to(same, rx, o + 2048, j[2], j[3], 0.0f, tag);
     }
   };
   // ... and the neighbour's row (tile tl, side) of the step tagged `tag`:
@@ -570,6 +595,7 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
   const bool valid = y < rows;
   const bool nb_up = valid && ty == 0 && tile > 0;
   const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
+  const bool same_up = same_xcd(tile - 1), same_dn = same_xcd(tile + 1);
   unsigned* const err = a.sync + kResidentSyncErr;
   const Rsrc rx = make_rsrc(a.xch);
   auto sbuf = [&](int i) { return sJ0 + i * bufn + 4; };
@@ -579,8 +605,9 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
     for (int side = 0; side < 2; ++side) {
       if (side == 0 ? !nb_up : !nb_dn) continue;
       const int o = xch_gran(a.ntiles, wpr, slot, tile, side, wj, 0, lane);
-      st_gran(rx, o, j[0], j[1], j[2], tag);
-      st_gran(rx, o + 1024, j[3], 0.0f, 0.0f, tag);
+      const bool same = side == 0 ? same_up : same_dn;
+      st_gran_to(same, rx, o, j[0], j[1], j[2], tag);
+      st_gran_to(same, rx, o + 1024, j[3], 0.0f, 0.0f, tag);
     }
   };
   auto take = [&](int slot, int tl, int side, unsigned tag, float (&v)[6]) {
