@@ -36,7 +36,7 @@ def main():
     tot = (b[1:, 56, 0, 0] - b[1:, 8, 0, 0]) / 100.0 / 48
     print(f"N={N} prio={os.environ.get('PP2_RES_PRIO', '1')}: us/step (tiles 1..15, steps 8..56, "
           f"block starts included) median {np.median(tot):.2f}")
-    names = ["top->A", "A->B", "B->barrier", "barrier->top"]
+    names = ["top->rows", "rows->done", "done->barrier", "barrier->top"]
     for w, role in ((0, "first-row wave"), (1, "interior wave")):
         x = b[1:, 8:63, w, :] / 100.0
         nxt = b[1:, 9:64, w, 0] / 100.0

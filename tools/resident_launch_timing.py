@@ -24,14 +24,17 @@ def main():
     with P.GridContext(grid, goal, gamma=0.95) as ctx:
         ctx.set_stream(stream.cuda_stream)
         ctx.model_generate()
+        if os.environ.get("PP2_NORM_BLOCK"):
+            ctx.set_tuning(ctx.TUNE_NORM_BLOCK, int(os.environ["PP2_NORM_BLOCK"]))
         ctx.belief_set(S.uniform_belief(grid))
         ctx.mdp_reset()
         ctx.loop_run(us[:10], zs[:10])
         ctx.synchronize()
-        print(f"N={N} steps/launch={ctx.loop_steps_per_launch()}", flush=True)
+        print(f"N={N} steps/launch={ctx.loop_steps_per_launch()} "
+              f"norm block {os.environ.get('PP2_NORM_BLOCK', 'default')}", flush=True)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
-        for n in (2, 4, 8, 20, 50, 100, 400, 2000):
+        for n in [int(v) for v in os.environ.get("PP2_NS", "2,4,8,20,50,100,400,2000").split(",")]:
             enq, gpu, wall = [], [], []
             for r in range(reps):
                 torch.cuda.synchronize()
