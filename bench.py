@@ -61,7 +61,7 @@ BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
 BYTES_LOOP_CODED = 19            # per cell: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1
 BYTES_SWEEP_CODED = 11           # per cell: code 2 + J 4 + J' 4 + A 1
 LDS_BYTES_LOOP_CODED = 204       # per cell-step (factored rows): T_u gather 4*4 + L_z 4 + backup record 16 + quads 8*16 + stay 4 + costs 9*4
-LDS_BYTES_LOOP_RESIDENT = 248    # + the b / J window rows read from LDS (2 planes x 3 rows x 24 B per quad = 36) + b', J' stored (8)
+LDS_BYTES_LOOP_RESIDENT = 235    # - the backup record (registers) + class-plane rows (<= 3 dwords per quad = 3) + the b / J window rows (2 planes x 3 rows x 24 B per quad = 36) + b', J' stored (8)
 RESIDENT_STEPS = 2048            # pp2_loop_steps_per_launch of the tile-resident loop
 LDS_PEAK_GBS = 150000.0          # ds_read_b64/b128 chip aggregate (MI355X_MICROARCH.md LDS)
 GAMMA = 0.95
@@ -687,6 +687,20 @@ def main():
     def loop_reps():
         ctx.loop_run(us[:reps], zs[:reps])
 
+    # the resident kernel's duration per launch for the roofline: launches of
+    # the timed region's length back to back, so the host enqueue of one
+    # overlaps the previous (the timed region's events also hold its single
+    # enqueue; rocprof's per-dispatch average is the comparable figure)
+    res_launch_us = None
+    if coded and steps_per_launch >= RESIDENT_STEPS:
+        n_l = -(-args.steps // -(-args.steps // RESIDENT_STEPS))
+        n_rep = 10
+        e0.record(stream)
+        for _ in range(n_rep):
+            ctx.loop_run(us[:n_l], zs[:n_l])
+        e1.record(stream)
+        torch.cuda.synchronize()
+        res_launch_us = e0.elapsed_time(e1) / n_rep * 1e3
     sweep_ms = timed(lambda: ctx.mdp_sweep(reps))  # coded when active
     pairs_ms = None
     if coded and steps_per_launch >= RESIDENT_STEPS:
@@ -744,8 +758,9 @@ def main():
     lds_bytes = LDS_BYTES_LOOP_RESIDENT if resident else LDS_BYTES_LOOP_CODED
     sweep_gbs = bytes_sweep * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
     belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
-    # one launch = spl steps; its average duration from the timed region's events
-    launch_s = loop_ms_events * 1e-3 * spl
+    # one launch = spl steps; its average duration: back-to-back resident
+    # launches (above), else the timed region's events
+    launch_s = res_launch_us * 1e-6 if res_launch_us else loop_ms_events * 1e-3 * spl
     algo_launch = bytes_loop * cells_per_gpu  # bytes the kernel must move per launch
     loop_gbs = algo_launch / launch_s / 1e9
     contract_gbs = BYTES_LOOP * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
