@@ -644,6 +644,16 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
     }
   }
   __syncthreads();
+  // the quad's IW records in registers for the whole run (k_loop_resident)
+  uint32_t iwr[4][3];
+  {
+    const uint32_t cc[4] = {c0 & 0xffffu, c0 >> 16, c1 & 0xffffu, c1 >> 16};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 w = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * cc[k]);
+      iwr[k][0] = w.x; iwr[k][1] = w.y; iwr[k][2] = w.z;
+    }
+  }
 
   unsigned arrivals = a.arrive_base;
   float best[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -670,9 +680,8 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
       for (int i = 0; i < 9; ++i)
 #pragma unroll
         for (int k = 0; k < 4; ++k) jn[i][k] = w.v[i / 3][k + i % 3];
-      const uint32_t cc[4] = {c0 & 0xffffu, c0 >> 16, c1 & 0xffffu, c1 >> 16};
-      if (check || fin) coded_sweep4<true, true>(sTC, cc, jn, a.gamma, best, arg);
-      else coded_sweep4<true, false>(sTC, cc, jn, a.gamma, best, arg);
+      if (check || fin) coded_sweep_iw<4, true>(sTC, iwr, jn, best, arg);
+      else coded_sweep_iw<4, false>(sTC, iwr, jn, best, arg);
       *reinterpret_cast<f4a*>(sbuf(co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
       if (nb_up || nb_dn) {
         publish(ci, best, a.epoch + s + 2);
