@@ -252,18 +252,16 @@ __device__ __forceinline__ void st_gran(Rsrc r, int off, float x, float y, float
   const u4v t = {__float_as_uint(x), __float_as_uint(y), __float_as_uint(z), tag};
   __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, AUX);
 }
-// Whether tile `nb` runs on the same XCD as this workgroup: blocks are dealt
-// round-robin over the 8 XCDs (MI355X_MICROARCH.md: blocks b and b + 8 share
-// one) and xcd_remap gives each class b % 8 a contiguous run of tiles.  A
-// granule for a same-XCD consumer is stored plain: it stays in the shared L2,
-// where the consumer's sc1 loads find it (an sc1 store drops the line and
-// the reader fetches it at the cross-XCD rate).  Should the observation not
-// hold, the consumer's bounded wait times out and reports the error -- a tag
-// is never matched by stale data.
-__device__ __forceinline__ bool same_xcd(int nb) {
-  const int n = gridDim.x, q = n / 8, r = n % 8, x = blockIdx.x % 8;
-  const int first = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-  return nb >= first && nb < first + q + (x < r);
+// The XCD this workgroup runs on.  Each publish carries it in a spare
+// granule slot, so an edge wave learns its neighbour's XCD from the first
+// granules it takes (the prologue's, stored sc1) and from then on stores its
+// own granules for a same-XCD neighbour plain: they stay in the shared L2,
+// where the consumer's sc1 loads find them (an sc1 store drops the line and
+// the reader fetches it at the cross-XCD rate).  No placement is assumed.
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned id;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(id));
+  return id & 0xfu;
 }
 // One granule store of a hand-off: plain for a same-XCD consumer, else sc1.
 __device__ __forceinline__ void st_gran_to(bool same, Rsrc r, int off, float x, float y, float z,
@@ -343,12 +341,13 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   // itself for it; its last row likewise with tile + 1
   const bool nb_up = valid && ty == 0 && tile > 0;
   const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
-  const bool same_up = same_xcd(tile - 1), same_dn = same_xcd(tile + 1);
+  const unsigned my_xcc = xcc_id();
+  bool same_up = false, same_dn = false;  // learnt from the neighbours' granules
   unsigned* const err = a.sync + kResidentSyncErr;
   const Rsrc rx = make_rsrc(a.xch);
   auto sbuf = [&](int k, int slot) { return sB0 + (2 * k + slot) * bufn + 4; };
   // the boundary waves' hand-off: b and J of the lane's quad as three
-  // granules {b0 b1 b2}, {b3 j0 j1}, {j2 j3 0} in exchange slot `slot`
+  // granules {b0 b1 b2}, {b3 j0 j1}, {j2 j3 xcc} in exchange slot `slot`
   auto publish = [&](int slot, const float (&b)[4], const float (&j)[4], unsigned tag) {
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
@@ -357,7 +356,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
       const bool same = side == 0 ? same_up : same_dn;
       st_gran_to(same, rx, o, b[0], b[1], b[2], tag);
       st_gran_to(same, rx, o + 1024, b[3], j[0], j[1], tag);
-      st_gran_to(same, rx, o + 2048, j[2], j[3], 0.0f, tag);
+      st_gran_to(same, rx, o + 2048, j[2], j[3], __uint_as_float(my_xcc), tag);
     }
   };
   // ... and the neighbour's row (tile tl, side) of the step tagged `tag`:
@@ -370,6 +369,9 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
                       : xch_gran(a.ntiles, wpr, slot, tl, side, wj + 1, 0, 0);
     u4v g[3], e[2];
     take_granules(rx, o, el || er, eo, tag, g, e, err);
+    const bool same = __builtin_amdgcn_readfirstlane(g[2][2]) == my_xcc;
+    if (tl < tile) same_up = same;
+    else same_dn = same;
     const float mb[4] = {__uint_as_float(g[0][0]), __uint_as_float(g[0][1]),
                          __uint_as_float(g[0][2]), __uint_as_float(g[1][0])};
     const float mj[4] = {__uint_as_float(g[1][1]), __uint_as_float(g[1][2]),
@@ -595,11 +597,12 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
   const bool valid = y < rows;
   const bool nb_up = valid && ty == 0 && tile > 0;
   const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
-  const bool same_up = same_xcd(tile - 1), same_dn = same_xcd(tile + 1);
+  const unsigned my_xcc = xcc_id();
+  bool same_up = false, same_dn = false;  // learnt from the neighbours' granules
   unsigned* const err = a.sync + kResidentSyncErr;
   const Rsrc rx = make_rsrc(a.xch);
   auto sbuf = [&](int i) { return sJ0 + i * bufn + 4; };
-  // k_loop_resident's hand-off with J alone: granules {j0 j1 j2}, {j3 0 0}
+  // k_loop_resident's hand-off with J alone: granules {j0 j1 j2}, {j3 xcc 0}
   auto publish = [&](int slot, const float (&j)[4], unsigned tag) {
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
@@ -607,7 +610,7 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
       const int o = xch_gran(a.ntiles, wpr, slot, tile, side, wj, 0, lane);
       const bool same = side == 0 ? same_up : same_dn;
       st_gran_to(same, rx, o, j[0], j[1], j[2], tag);
-      st_gran_to(same, rx, o + 1024, j[3], 0.0f, 0.0f, tag);
+      st_gran_to(same, rx, o + 1024, j[3], __uint_as_float(my_xcc), 0.0f, tag);
     }
   };
   auto take = [&](int slot, int tl, int side, unsigned tag, float (&v)[6]) {
@@ -619,6 +622,9 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
                       : xch_gran(a.ntiles, wpr, slot, tl, side, wj + 1, 0, 0);
     u4v g[2], e[1];
     take_granules(rx, o, el || er, eo, tag, g, e, err);
+    const bool same = __builtin_amdgcn_readfirstlane(g[1][1]) == my_xcc;
+    if (tl < tile) same_up = same;
+    else same_dn = same;
     const float m[4] = {__uint_as_float(g[0][0]), __uint_as_float(g[0][1]),
                         __uint_as_float(g[0][2]), __uint_as_float(g[1][0])};
     row_quad(m, __uint_as_float(e[0][0]), v);
