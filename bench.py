@@ -645,9 +645,9 @@ def main():
     enqueue_s = time.perf_counter() - t0
     ev1.record(stream)
     torch.cuda.synchronize()
-    if ws > 1:
+    if ws > 1:  # (one rank: the synchronize above already closes the region)
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     loop_ms_events = ev0.elapsed_time(ev1) / args.steps
     if ws > 1:
