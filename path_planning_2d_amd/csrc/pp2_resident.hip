@@ -182,7 +182,6 @@ __device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0,
     for (int k = 0; k < 4; ++k)
       p[k] = __builtin_fmaf(*reinterpret_cast<const float*>(qr + 4 * sl + cb[oy][k + 1 + ox]),
                             win.v[oy][k + 1 + ox], p[k]);
-    __builtin_amdgcn_sched_barrier(0);  // <= 4 gathers in flight
   }
   local = 0.0f;
 #pragma unroll
