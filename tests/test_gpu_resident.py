@@ -202,3 +202,31 @@ def test_resident_mdp_sweeps_equal_per_sweep(pp2, n):
         ra, rb = a.mdp_solve(200), b.mdp_solve(200)
         assert ra[0] == rb[0] and np.float32(ra[1]) == np.float32(rb[1])
         np.testing.assert_array_equal(a.mdp_get()[0].view(np.uint32), b.mdp_get()[0].view(np.uint32))
+
+
+def test_resident_beside_other_work(pp2):
+    """Resident runs while another context keeps the GPU busy on its own
+    stream (a queue of launch-per-step loop kernels and sweeps): the resident
+    workgroups start as CUs free up, on XCDs no placement rule predicts, and
+    each edge wave learns its neighbours' XCDs from their granules.  Results
+    stay bit-equal to the single-step path."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 1024, 1024, 8, 19)
+    g2 = S.synth_grid(512, 512, 512)
+    other = pp2.GridContext(g2, S.synth_goal(g2), gamma=float(GAMMA))
+    with a, b, other:
+        other.model_generate()
+        other.set_tuning(other.TUNE_RESIDENT, 0)
+        other.belief_set(S.uniform_belief(g2))
+        other.mdp_reset()
+        us, zs, _ = S.synth_trajectory(grid, 60, seed=4)
+        u2, z2, _ = S.synth_trajectory(g2, 400, seed=8)
+        for lo, hi in ((0, 20), (20, 41), (41, 60)):
+            other.loop_run(u2, z2)  # ~400 queued launches on its stream
+            other.mdp_sweep(1)
+            a.loop_run(us[lo:hi], zs[lo:hi])
+            b.loop_run(us[lo:hi], zs[lo:hi])
+        a.synchronize()
+        other.synchronize()
+        assert a.resident_launches()[0] == 3
+        _same(a, b, "beside other work")
