@@ -127,10 +127,14 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           dictionary in LDS) runs the whole trajectory in
  *                           one launch (the tile-resident loop, up to 2048
  *                           steps per launch); 0 = step pairs / single steps.
+ *                           pp2_mdp_solve and pp2_mdp_sweep(n >= 2) run as
+ *                           resident sweeps under the same conditions.
  *                           Results are bit-identical either way.  A resident
- *                           launch that cannot get every tile onto the GPU
- *                           at once ends with an error that pp2_synchronize
- *                           reports (PP2_EHIP); the context then falls back. */
+ *                           launch occupies every CU; work queued on other
+ *                           streams delays its start, and one that cannot get
+ *                           every tile onto the GPU within 0.25 s ends with an
+ *                           error that pp2_synchronize reports (PP2_EHIP); the
+ *                           context then falls back. */
 #define PP2_TUNE_RESIDENT 8
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
