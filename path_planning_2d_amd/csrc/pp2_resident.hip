@@ -47,13 +47,14 @@ namespace pp2 {
 
 #ifdef PP2_RES_TRACE
 // Diagnostic build only (tools/micro/resident_trace.py): s_memrealtime
-// (100 MHz) per step of tiles 0..15 for wave 0 (the first row) and wave 5
-// (an interior row at 1024^2): step top, neighbour rows in hand, computed
-// and published, after the step barrier.
-__device__ unsigned long long g_rtrace[16][64][2][4];
+// (100 MHz) per step of tiles 0..15 for waves 0, 5, 9 and 12 (rows 0..3 at
+// 1024^2): step top, window rows in hand, computed and published, after the
+// step barrier.
+__device__ unsigned long long g_rtrace[16][64][4][4];
 #define PP2_RT(ph)                                                                    \
-  if (tile < 16 && t < 64 && lane == 0 && (wave == 0 || wave == 5))                   \
-  g_rtrace[tile][t][wave == 5][ph] = __builtin_amdgcn_s_memrealtime()
+  if (tile < 16 && t < 64 && lane == 0 && (wave == 0 || wave == 5 || wave == 9 || wave == 12)) \
+  g_rtrace[tile][t][wave == 0 ? 0 : wave == 5 ? 1 : wave == 9 ? 2 : 3][ph] =          \
+      __builtin_amdgcn_s_memrealtime()
 #else
 #define PP2_RT(ph) (void)0
 #endif

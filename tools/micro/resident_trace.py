@@ -30,14 +30,15 @@ def main():
         ctx.mdp_reset()
         ctx.loop_run(us, zs)
         ctx.synchronize()
-        buf = np.zeros((16, 64, 2, 4), np.uint64)
+        buf = np.zeros((16, 64, 4, 4), np.uint64)
         assert fn(buf.ctypes.data) == 0
     b = buf.astype(np.int64)
     tot = (b[1:, 56, 0, 0] - b[1:, 8, 0, 0]) / 100.0 / 48
     print(f"N={N} prio={os.environ.get('PP2_RES_PRIO', '1')}: us/step (tiles 1..15, steps 8..56, "
           f"block starts included) median {np.median(tot):.2f}")
     names = ["top->rows", "rows->done", "done->barrier", "barrier->top"]
-    for w, role in ((0, "first-row wave"), (1, "interior wave")):
+    for w, role in ((0, "row 0 (top edge) wave 0"), (1, "row 1 (interior) wave 5"),
+                    (2, "row 2 (interior) wave 9"), (3, "row 3 (bottom edge) wave 12")):
         x = b[1:, 8:63, w, :] / 100.0
         nxt = b[1:, 9:64, w, 0] / 100.0
         d = [x[..., 1] - x[..., 0], x[..., 2] - x[..., 1], x[..., 3] - x[..., 2], nxt - x[..., 3]]
