@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PP2_ABI_VERSION 2
+#define PP2_ABI_VERSION 3
 
 typedef enum {
   PP2_OK = 0,
@@ -66,8 +66,10 @@ int pp2_create(pp2_ctx** out, int device, uint32_t height, uint32_t width,
                const uint8_t* map, int32_t goal_x, int32_t goal_y, float gamma);
 /* Row shard [row_begin, row_end) of a global_height x width grid (no
  * reference counterpart: the reference is single-GPU).  `global_map` is the
- * whole grid.  Shards exchange one halo row per step over RCCL once
- * pp2_shard_comm_init has been called on every shard. */
+ * whole grid.  Once pp2_shard_comm_init has been called on every shard,
+ * shards exchange halo rows over RCCL: loop steps k rows deep every k steps
+ * (PP2_TUNE_HALO_DEPTH, or e rows per resident launch of up to e steps,
+ * PP2_TUNE_RESIDENT_HALO), sweeps and belief-only updates one row per step. */
 int pp2_create_shard(pp2_ctx** out, int device, uint32_t global_height,
                      uint32_t width, uint32_t row_begin, uint32_t row_end,
                      const uint8_t* global_map, int32_t goal_x, int32_t goal_y,
@@ -95,9 +97,10 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
 #define PP2_TUNE_CELLS_PER_LANE 1
 #define PP2_TUNE_NT_STREAMS 2
 #define PP2_TUNE_CODED_MODEL 3
-/*  PP2_TUNE_HALO_DEPTH      row shards (RCCL or shard group): loop steps per
- *                           halo exchange = halo rows exchanged, 1..8
- *                           (default: the most the smallest shard allows) */
+/*  PP2_TUNE_HALO_DEPTH      row shards (RCCL or shard group), launch-per-step
+ *                           loop: steps per halo exchange = halo rows
+ *                           exchanged, 1..8 (default: the most the smallest
+ *                           shard allows) */
 #define PP2_TUNE_HALO_DEPTH 4
 /*  PP2_TUNE_COMM_STREAM     0 (default): RCCL calls are issued on the context's
  *                           stream; 1: on a dedicated stream entered and left
@@ -129,13 +132,39 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           steps per launch); 0 = step pairs / single steps.
  *                           pp2_mdp_solve and pp2_mdp_sweep(n >= 2) run as
  *                           resident sweeps under the same conditions.
- *                           Results are bit-identical either way.  A resident
- *                           launch occupies every CU; work queued on other
- *                           streams delays its start, and one that cannot get
- *                           every tile onto the GPU within 0.25 s ends with an
- *                           error that pp2_synchronize reports (PP2_EHIP); the
- *                           context then falls back. */
+ *                           Results are bit-identical either way.  A plan
+ *                           whose tiles cannot all be resident at once is
+ *                           never launched.  Resident launches of this
+ *                           process run one at a time per device.  A launch
+ *                           that still cannot get every tile onto the GPU
+ *                           within 0.25 s (another process holding CUs) ends
+ *                           early, leaves its inputs intact, and the next
+ *                           call on the context re-runs it on per-step
+ *                           launches before reading anything (same bits; the
+ *                           context then stays on them: pp2_resident_status).
+ *                           Consequence: a call after a resident launch
+ *                           first waits for that launch to finish. */
 #define PP2_TUNE_RESIDENT 8
+/*  PP2_TUNE_RESIDENT_HALO   row shards: the loop runs on the resident kernel
+ *                           when a view of the owned rows plus e halo rows
+ *                           per side fits one tile per CU; a run of n steps
+ *                           is ceil(n / e) launches of up to e steps, each
+ *                           after one exchange of e halo rows and one
+ *                           {mass, shift} all-reduce.  Value
+ *                           = the largest e to use (0, default: the most the
+ *                           halo allocation of 128 rows, the smallest shard
+ *                           and the CUs allow).  Values and actions are
+ *                           bit-identical to the unsharded grid either way. */
+#define PP2_TUNE_RESIDENT_HALO 9
+/*  Diagnostics (tests):
+ *  PP2_TUNE_RESIDENT_CUS    plan resident launches for at most this many CUs
+ *                           (0: all); a grid whose tiles do not fit falls
+ *                           back before launching
+ *  PP2_TUNE_RESIDENT_STALL  tile index that returns at once (-1: none): the
+ *                           other tiles' waits time out, exercising the
+ *                           re-run of a failed resident launch */
+#define PP2_TUNE_RESIDENT_CUS 10
+#define PP2_TUNE_RESIDENT_STALL 11
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
 
 /* ---------------------------------------------------------------- model
@@ -166,15 +195,20 @@ int pp2_model_load(pp2_ctx* ctx, const char* dir);
 int pp2_model_dict_info(pp2_ctx* ctx, int* entries, int* active);
 
 /* Loop steps pp2_loop_run fuses into one kernel launch on this context: 2048
- * for the tile-resident loop (PP2_TUNE_RESIDENT), 2 when it runs the steps
- * of a normalisation / halo block in pairs (PP2_TUNE_STEP_PAIRS with a sparse
- * coded model whose grid has a 4096-cell tile per CU; unsharded, RCCL row
- * shard or shard-group member), else 1. */
+ * for the tile-resident loop (PP2_TUNE_RESIDENT) on an unsharded grid, the
+ * resident halo depth e on a row shard (PP2_TUNE_RESIDENT_HALO), 2 when it
+ * runs the steps of a normalisation / halo block in pairs
+ * (PP2_TUNE_STEP_PAIRS with a sparse coded model whose grid has a 4096-cell
+ * tile per CU; unsharded, RCCL row shard or shard-group member), else 1.
+ * A query: allocates nothing. */
 int pp2_loop_steps_per_launch(pp2_ctx* ctx, int* steps);
 /* Diagnostics: resident launches so far on this context -- tile-resident loop
  * launches (pp2_loop_run) and resident MDP-solve launches (pp2_mdp_solve);
  * either pointer may be NULL.  No reference counterpart. */
 int pp2_resident_launches(pp2_ctx* ctx, int* loop_launches, int* solve_launches);
+/* Resident launches re-run on per-step launches after a timeout, and whether
+ * the resident kernels are still enabled on the context (either may be NULL). */
+int pp2_resident_status(pp2_ctx* ctx, int* fallbacks, int* enabled);
 
 /* ---------------------------------------------------------------- belief
  * The belief lives on the device with deferred normalisation: each update

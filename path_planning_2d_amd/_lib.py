@@ -59,6 +59,7 @@ SIGNATURES = {
     "pp2_model_dict_info": [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pp2_loop_steps_per_launch": [_vp, C.POINTER(C.c_int)],
     "pp2_resident_launches": [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "pp2_resident_status": [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pp2_belief_set": [_vp, _f32p],
     "pp2_belief_get": [_vp, _f32p],
     "pp2_belief_update": [_vp, C.c_uint8, C.c_uint8],

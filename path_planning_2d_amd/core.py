@@ -102,6 +102,9 @@ class GridContext:
     TUNE_NORM_BLOCK = 6
     TUNE_STEP_PAIRS = 7
     TUNE_RESIDENT = 8
+    TUNE_RESIDENT_HALO = 9
+    TUNE_RESIDENT_CUS = 10
+    TUNE_RESIDENT_STALL = 11
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))
@@ -123,8 +126,16 @@ class GridContext:
         call("pp2_resident_launches", self._h, C.byref(lo), C.byref(so))
         return lo.value, so.value
 
+    def resident_status(self):
+        """(resident launches re-run after a timeout, resident kernels enabled)."""
+        f = C.c_int()
+        e = C.c_int()
+        call("pp2_resident_status", self._h, C.byref(f), C.byref(e))
+        return f.value, bool(e.value)
+
     def loop_steps_per_launch(self) -> int:
-        """Loop steps one kernel launch of pp2_loop_run covers (1 or 2)."""
+        """Loop steps one kernel launch of pp2_loop_run covers (2048 resident,
+        the resident halo depth on a shard, 2 for step pairs, else 1)."""
         n = C.c_int(0)
         call("pp2_loop_steps_per_launch", self._h, C.byref(n))
         return n.value

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <initializer_list>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -41,7 +42,10 @@ int set_err(int code, const char* fmt, ...);
   } while (0)
 
 constexpr int kGuard = pp2::kPlaneGuard;  // floats of guard before/after each plane set
-constexpr int kShardHalo = 8;  // halo rows allocated per side in row-sharded contexts
+// Halo rows allocated per side in row-sharded contexts: the per-step paths
+// exchange up to kMaxNormBlock of them per block, the resident shard runs up
+// to all (one exchange per up to kShardHalo steps).
+constexpr int kShardHalo = 128;
 // Loop normalisation blocks (row shards, and PP2_TUNE_NORM_BLOCK > 1) start
 // by dividing the belief by its exact (global) mass and multiplying by 2^96
 // (exact), then divide by 1: the stored belief decays by < 8 observation
@@ -132,16 +136,41 @@ struct pp2_ctx {
   unsigned* res_sync = nullptr;    // sync words (flags, counters, error)
   float* res_ring = nullptr;       // kResidentRing slots of mass partials
   float* res_xch = nullptr;        // exchange rows
-  unsigned res_epoch = 0, res_arrive = 0, res_read = 0;  // epoch-tagged counters
-  bool res_used = false;           // a resident launch since the last error check
+  unsigned res_epoch = 0, res_arrive = 0;  // epoch-tagged counters
   int sol_plan_e = -1;             // resident MDP solve (k_sweep_resident): plan for dict_n
   bool sol_ok = false;
   pp2::ResidentPlan sol_plan{};
   int res_ntiles = 0;              // tiles the sync words / exchange rows were sized for
   float* res_tmax = nullptr;       // 2 x ntiles per-tile convergence maxima
   int* res_out = nullptr;          // {sweeps, norm bits} of a resident solve launch
-  unsigned* res_host = nullptr;    // pinned: {sweeps, norm bits, error word} read back
+  unsigned* res_host = nullptr;    // pinned: {sweeps, norm bits, error word} written by the kernels
   int res_launches = 0, sol_launches = 0;  // pp2_resident_launches
+  // Every resident launch is journalled until verified (resident_settle): its
+  // inputs stay intact (outputs go to the other ping-pong buffers), so a
+  // launch whose waits timed out is re-run from them with per-step launches
+  // before anything reads its outputs.
+  struct ResidentJournal {
+    int kind = 0;                  // 0 none, 1 loop run, 2 sweeps
+    int n = 0;
+    int bcur = 0, jcur = 0, kstep = 0, pcount[2] = {0, 0};
+    bool pending[2] = {false, false};
+    std::vector<uint8_t> us, zs;
+  } journal;
+  hipEvent_t res_done = nullptr;   // recorded after the journalled launch
+  int res_fallbacks = 0;           // launches re-run after a timeout (pp2_resident_status)
+  int res_stall_tile = -1;         // PP2_TUNE_RESIDENT_STALL (tests)
+  int res_cus = 0;                 // PP2_TUNE_RESIDENT_CUS: CUs the plans may use (0: all)
+  // row shards on the resident loop: halo depth per resident
+  // launch, the run's power-of-two shift and the {mass, shift} rank vector
+  int res_halo = 0;                // PP2_TUNE_RESIDENT_HALO (0: the most the shards allow)
+  int min_shard_rows = 0;          // smallest shard of the grid (comm init / group create)
+  int res_view_e = -1;             // view extension the plan below was made for
+  int res_e = 0, res_e_dict = -1;  // shard_resident_e's answer and the dictionary it is for
+  int* d_shift = nullptr;          // int: the last shard-resident run's shift
+  float* d_vec = nullptr;          // 2 x nranks floats
+  bool shift_pending = false;      // the pending mass comes with *d_shift (rebase owed)
+  // a shard-resident run timed out: belief / values unusable until set again
+  bool lost_belief = false, lost_values = false;
 
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -150,6 +179,7 @@ struct pp2_ctx {
   hipEvent_t ev_enter = nullptr, ev_leave = nullptr;
   pp2_shard_group* group = nullptr;  // single-process shard group, if any
   int grank = 0;                     // rank (row-block order) inside the group
+  int group_size = 0;                // shards in the group
 
   pp2rt::PbviState* pbvi = nullptr;  // PBVI belief set / alpha vectors (pp2_pbvi.cpp)
 };
@@ -170,7 +200,8 @@ struct DeviceGuard {
 int alloc_planes(pp2_ctx* c, Planes* P, int K);
 void free_planes(Planes* P);
 int ensure_staging(pp2_ctx* c, size_t bytes);
-int check_ctx(pp2_ctx* c);
+int check_ctx(pp2_ctx* c);          // null check, resident_settle, lost shard state
+int check_ctx_settled(pp2_ctx* c);  // null check, resident_settle
 int check_model(pp2_ctx* c);
 size_t owned_cells(const pp2_ctx* c);
 int download_planes(pp2_ctx* c, const Planes& P, float* host, const float* divide_by);
@@ -195,6 +226,20 @@ int pair_launch(pp2_ctx* c, int e, bool shard, uint8_t u1, uint8_t z1, uint8_t u
                 float scale, int* nparts);
 int fib_sweep_once(pp2_ctx* c);
 int absdiff_local_max(pp2_ctx* c, const Planes& cur, const Planes& snap, float* out);
+
+// Resident launches (pp2_runtime.cpp): verify the journalled launch, re-run
+// it on per-step launches if it timed out (every entry point, via check_ctx).
+int resident_settle(pp2_ctx* c);
+// Row shards on the resident loop: the view extension of the
+// shard's runs (0: not eligible), its plan and buffers, the {mass, shift}
+// post into d_vec's slot `rank`, the rebase of rows [r0, r1) once d_vec holds
+// every shard's slot, and one launch of m <= e steps.
+int shard_resident_e(pp2_ctx* c);
+bool shard_resident_ready(pp2_ctx* c, int e);
+int shard_post_mass(pp2_ctx* c, int nranks, int rank);
+int shard_rebase(pp2_ctx* c, int nranks, int rank, int r0, int r1);
+int shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, const uint8_t* zs);
+int loop_run_launches(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs);
 
 // Halo-exchanged state of a shard.
 enum HaloKind { HALO_BELIEF, HALO_VALUE, HALO_FIB };

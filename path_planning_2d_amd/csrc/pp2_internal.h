@@ -219,45 +219,55 @@ hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
                                   const uint16_t* code, const float* rows, int entries,
                                   bool sparse, const float* J_in, float* J_out, uint8_t* A);
 
-// Tile-resident loop (pp2_resident.hip): n fused loop steps of an unsharded
-// sparse-coded context in one launch, one tile of rt whole rows per CU kept
-// in LDS, neighbour rows handed over as data-tagged granules, block-start masses
+// Tile-resident loop (pp2_resident.hip): n fused loop steps of a sparse-coded
+// context in one launch, one tile of rt whole rows per CU kept in LDS,
+// neighbour rows handed over as data-tagged granules, block-start masses
 // behind an arrival counter.  Needs wp % 256 == 0, rt * wp / 4 <= 1024 lanes,
-// a tile per CU and the whole dictionary in LDS (resident_plan).
+// a tile per CU and the whole dictionary in LDS (resident_plan).  A row
+// shard runs it on a *view*: its owned rows extended by e halo rows per side
+// (DESIGN.md §6).
 constexpr int kResidentMaxSteps = 2048;  // steps per launch (kernel-argument trajectory)
 constexpr int kResidentRing = 16;        // partial-mass slots (>= block depth + 2)
 constexpr int kResidentSyncArrive = 0;   // sync words: block-start arrivals,
-constexpr int kResidentSyncRead = 1;     //   in_partials readers done,
 constexpr int kResidentSyncErr = 2;      //   sticky timeout flag
 constexpr int kResidentSyncWords = 16;
+// Exchange granules per lane and side: 16 B each, {v0, tag, v1, tag} -- a
+// tag in every 8-B half (MI355X_MICROARCH.md: 16-B sc1 stores are observed
+// untorn per 8-B half only).  The loop hands over b and J (4 + 4 floats).
+constexpr int kResidentGranules = 4;
 struct ResidentPlan {
   int rt = 0, ntiles = 0, threads = 0;
   size_t lds = 0;
 };
 struct ResidentRun {
-  Geom g;
+  Geom g;                    // the launch's rows: the grid, or a shard's view
   float gamma;
   int E;                     // dictionary entries
-  const uint16_t* code;      // code plane (row 0, x 0)
+  const uint16_t* code;      // code plane (view row 0, x 0)
   const float* rows;         // factored sweep rows
   const float* rfact;        // class tables: kResTab floats (QR, LT), then the LX bytes
-  const float* b_in;         // step 0's input belief / value planes (row 0)
+  const float* b_in;         // step 0's input belief / value planes (view row 0)
   const float* j_in;
-  float* b_out;              // the last step's output planes
-  float* j_out;
-  float* xch;                // exchange granules, resident_xch_floats(): [step & 1][tile][top, bottom][wave][3][lane] x 16 B
-  uint8_t* A;
+  float* b_out;              // the last step's output planes (never b_in / j_in:
+  float* j_out;              //   a run that fails leaves its inputs intact)
+  float* xch;                // exchange granules, resident_xch_floats(): [step & 1][tile][top, bottom][wave][kResidentGranules][lane] x 16 B
+  uint8_t* A;                // actions (view row 0; owned rows stored)
   int n, kstep0, depth, rt, ntiles, nparts;
+  int own0, own1;            // owned view rows: only they store b', J', A and add to the mass
+  int shard;                 // 1: block starts inside the run scale by 2^k from the owned
+                             //   mass (no cross-rank reduction), k summed into *scale_out
   float bscale;              // block-start scale (2^96, or 1 for depth 1)
   const float* in_partials;  // step 0's pending input mass (block start), or null
   int in_n;
   float* in_sum_out;         // receives that mass (tile 0)
   const float* in_sum;       // step 0's finalised input mass when in_partials is null
   float* ring;               // kResidentRing x nparts partial slots
-  float* out_partials;       // the last step's partials (the context's pending buffer)
+  float* out_partials;       // the last step's partials (never in_partials)
   unsigned* sync;            // kResidentSyncWords sync words
-  unsigned epoch, arrive_base, read_base;  // epoch-tagged counters of earlier launches
-  int final_wait_read;       // out_partials == in_partials: the last step waits for readers
+  unsigned* err_host;        // pinned host word: set with the sticky error word
+  int* scale_out;            // shard: the run's total power-of-two shift (tile 0)
+  unsigned epoch, arrive_base;  // epoch-tagged counters of earlier launches
+  int stall_tile;            // diagnostic (tests): this tile returns at once, -1 none
   uint8_t uz[kResidentMaxSteps];  // u | z << 4 per step
 };
 // Resident MDP solve (pp2_mdp_solve): sweeps in blocks of kSolveBlock, a
@@ -269,11 +279,13 @@ struct SweepRun {
   int E;
   const uint16_t* code;
   const float* rows;
-  float *j0, *j1;      // sweep s reads J(s & 1 ? j1 : j0); the last J goes to the other
+  const float* j_in;   // the input values
+  float* j_out;        // the last sweep's values (never j_in)
   float* snap;         // convergence snapshot (read at start, written at the end)
   uint8_t* A;
   float* xch;
   unsigned* sync;
+  unsigned* err_host;  // pinned host word, set with the sticky error word
   float* tile_max;     // 2 x ntiles per-tile maxima
   int* res;            // {sweeps done, norm bits}
   unsigned epoch, arrive_base;
@@ -282,15 +294,30 @@ struct SweepRun {
   int cap_blocks;      // stop after this many blocks (0: no cap)
   double thresh;       // stop when norm <= thresh
   int nsweeps;         // > 0: exactly this many sweeps, no convergence checks
+  int stall_tile;      // diagnostic (tests): this tile returns at once, -1 none
 };
 size_t resident_lds_bytes(const Geom& g, int E, int rt);
+// Plans fail (the caller falls back BEFORE launching) unless every tile can
+// be resident at once: occupancy per CU x ncus >= tiles (one 1024-lane
+// workgroup per CU at these LDS sizes).
 bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p);
 hipError_t launch_sweep_resident(hipStream_t st, const ResidentPlan& p, const SweepRun& a);
 inline size_t resident_xch_floats(const Geom& g, int ntiles) {
-  // [step & 1][tile][top, bottom][wave of row][3][lane] 16-B granules
-  return (size_t)2 * ntiles * 2 * (g.wp / 256) * 3 * 64 * 4;
+  // [step & 1][tile][top, bottom][wave of row][granule][lane] 16-B granules
+  return (size_t)2 * ntiles * 2 * (g.wp / 256) * kResidentGranules * 64 * 4;
 }
 bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p);
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a);
+// Row-shard boundary kernels (pp2_resident.hip).
+// vec[2 * nranks] := 0 except vec[2 * rank] = mass of the n partials (k_sum_finalize's
+// tree), vec[2 * rank + 1] = (float) *shift (0 if shift is null).
+hipError_t launch_shard_mass_vec(hipStream_t st, const float* partials, int n, const int* shift,
+                                 float* vec, int nranks, int rank);
+// After the all-reduce of vec: C = min over ranks of the shifts; rows [r0, r1)
+// of plane b (row stride wp) are scaled by 2^(C - shift_q), q = the rank the
+// row came from (rank - 1 above row 0, rank + 1 at rows >= own_rows), and
+// *mass_out = sum over q in rank order of ldexp(m_q, C - shift_q).
+hipError_t launch_shard_rebase(hipStream_t st, const float* vec, int nranks, int rank,
+                               float* b, int wp, int r0, int r1, int own_rows, float* mass_out);
 
 }  // namespace pp2

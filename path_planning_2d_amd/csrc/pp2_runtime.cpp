@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -68,8 +69,21 @@ int ensure_staging(pp2_ctx* c, size_t bytes) {
   return PP2_OK;
 }
 
-int check_ctx(pp2_ctx* c) {
+// Every entry point: a null check, then the journalled resident launch is
+// verified (and re-run if it timed out) before the call reads or builds on
+// its outputs; a shard whose resident run was lost refuses until its state
+// is set again.
+int check_ctx_settled(pp2_ctx* c) {
   if (!c) return set_err(PP2_EINVAL, "null context");
+  return resident_settle(c);
+}
+int check_ctx(pp2_ctx* c) {
+  CHECK(check_ctx_settled(c));
+  if (c->lost_belief || c->lost_values)
+    return set_err(PP2_ESTATE, "a resident shard run of this context timed out: set the %s again",
+                   c->lost_belief && c->lost_values ? "belief and values (pp2_belief_set, "
+                   "pp2_mdp_reset)" : c->lost_belief ? "belief (pp2_belief_set)" :
+                   "values (pp2_mdp_reset)");
   return PP2_OK;
 }
 
@@ -330,6 +344,7 @@ static bool finite_nonneg(float v) {
 // collision) leaves dict_n = 0, i.e. the dense kernels.
 int build_model_dict(pp2_ctx* c) {
   c->dict_n = 0;
+  c->res_e_dict = -1;  // shard_resident_e: recomputed (collectively) on the next run
   const long long n = (long long)(c->g.rows + 2 * c->g.halo) * c->g.wp;
   break_pipeline(c);
   if (!c->code_alloc) {
@@ -573,6 +588,13 @@ using namespace pp2rt;
 int pp2rt::ensure_mass(pp2_ctx* c) {
   const int bc = c->bcur;
   if (!c->pending[bc]) return PP2_OK;
+  if (c->shift_pending && c->comm) {  // a shard-resident run's mass: rebase as well
+    CHECK(shard_post_mass(c, c->nranks, c->rank));
+    CHECK(comm_enter(c));
+    NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, 2 * c->nranks, ncclFloat, ncclSum, c->comm, cst(c)));
+    CHECK(comm_leave(c));
+    return shard_rebase(c, c->nranks, c->rank, 0, c->g.rows);
+  }
   HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bc], c->pcount[bc], c->bsum + bc));
   c->pending[bc] = false;
   return allreduce_mass(c, c->bsum + bc);  // global mass (RCCL shards)
@@ -775,8 +797,6 @@ static void resident_free_buffers(pp2_ctx* c) {
   for (void* p : {(void*)c->res_sync, (void*)c->res_ring, (void*)c->res_xch, (void*)c->res_tmax,
                   (void*)c->res_out})
     if (p) (void)hipFree(p);
-  if (c->res_host) (void)hipHostFree(c->res_host);
-  c->res_host = nullptr;
   c->res_sync = nullptr;
   c->res_ring = nullptr;
   c->res_xch = nullptr;
@@ -789,24 +809,45 @@ static void resident_free(pp2_ctx* c) {
   resident_free_buffers(c);
   c->res_ok = false;
   c->res_plan_e = -1;
+  c->res_view_e = -1;
   c->sol_ok = false;
   c->sol_plan_e = -1;
 }
 
+// The pinned words the kernels write ({sweeps, norm bits, error word}) and the
+// completion event of the journalled launch; kept across plan changes.
+static bool resident_host_words(pp2_ctx* c) {
+  if (!c->res_host) {
+    if (hipHostMalloc(&c->res_host, 4 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
+      c->res_host = nullptr;
+      return false;
+    }
+    std::memset(c->res_host, 0, 4 * sizeof(unsigned));
+  }
+  if (!c->res_done && hipEventCreateWithFlags(&c->res_done, hipEventDisableTiming) != hipSuccess) {
+    c->res_done = nullptr;
+    return false;
+  }
+  return true;
+}
+
 // Sync words, partial ring, exchange rows and solve scratch for plan p (both
 // resident kernels share them and the epoch counters; a plan with another
-// tile count reallocates and restarts the epochs).
+// tile count reallocates and restarts the epochs).  The ring holds the
+// partials of the largest view a shard can launch.
 static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
+  if (!resident_host_words(c)) return false;
   if (c->res_sync && c->res_ntiles == p.ntiles) return true;
   resident_free_buffers(c);
+  Geom gext = c->g;
+  gext.rows += 2 * gext.halo;
   const size_t sync_b = (size_t)pp2::kResidentSyncWords * sizeof(unsigned);
-  const size_t ring_b = (size_t)pp2::kResidentRing * pp2::mass_partials(c->g, 4) * sizeof(float);
+  const size_t ring_b = (size_t)pp2::kResidentRing * pp2::mass_partials(gext, 4) * sizeof(float);
   const size_t xch_b = pp2::resident_xch_floats(c->g, p.ntiles) * sizeof(float);
   const size_t tmax_b = (size_t)2 * p.ntiles * sizeof(float);
   if (hipMalloc(&c->res_sync, sync_b) != hipSuccess || hipMalloc(&c->res_ring, ring_b) != hipSuccess ||
       hipMalloc(&c->res_xch, xch_b) != hipSuccess || hipMalloc(&c->res_tmax, tmax_b) != hipSuccess ||
       hipMalloc(&c->res_out, 4 * sizeof(int)) != hipSuccess ||
-      hipHostMalloc(&c->res_host, 4 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
       hipMemsetAsync(c->res_sync, 0, sync_b, c->stream) != hipSuccess ||
       hipMemsetAsync(c->res_ring, 0, ring_b, c->stream) != hipSuccess ||
       hipMemsetAsync(c->res_xch, 0, xch_b, c->stream) != hipSuccess) {
@@ -815,50 +856,58 @@ static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
     return false;
   }
   c->res_ntiles = p.ntiles;
-  c->res_epoch = c->res_arrive = c->res_read = 0;
+  c->res_epoch = c->res_arrive = 0;
   return true;
 }
 
-// After a stream sync: a resident launch that timed out (a tile never got a
-// CU) left garbage; report it and fall back to the launch-per-step paths.
-static int resident_check(pp2_ctx* c) {
-  if (!c->res_used || !c->res_sync) return PP2_OK;
-  c->res_used = false;
-  HIPCHK(hipMemcpyAsync(c->res_host + 2, c->res_sync + pp2::kResidentSyncErr, sizeof(unsigned),
-                        hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  if (!c->res_host[2]) return PP2_OK;
-  resident_free(c);
-  c->resident = 0;
-  return set_err(PP2_EHIP, "resident loop: a workgroup wait timed out (grid not co-resident); "
-                 "results of that run are invalid, the context now uses per-step launches");
+// CUs the resident plans may use (PP2_TUNE_RESIDENT_CUS narrows it: tests of
+// the fall-back-before-launch path).
+static int resident_cus(const pp2_ctx* c) {
+  return c->res_cus > 0 ? std::min(c->res_cus, c->ncus) : c->ncus;
 }
 
-// Whether pp2_loop_run takes the tile-resident loop (pp2_resident.hip): an
-// unsharded context with a sparse coded model (finite T: the kernel's zero
-// padded edges multiply T by +0), a normalisation block that fits the
-// partial ring, and a geometry resident_plan accepts.  (Re)allocates the
-// plan's sync words, partial ring and exchange rows when the dictionary
-// changes size.
-static bool resident_ready(pp2_ctx* c) {
-  if (!c->resident || c->comm || c->group || !coded_active(c) || !c->dict_sparse ||
-      !c->dict_t_finite || !c->dict_rfact || c->norm_block > pp2::kResidentRing - 2 ||
-      c->ncus <= 0)
-    return false;
-  if (c->res_plan_e != c->dict_n) {
+// A shard's view: its owned rows extended by e rows per side.
+static Geom view_geom(const pp2_ctx* c, int e) {
+  Geom g = c->g;
+  g.rows += 2 * e;
+  g.row0 -= e;
+  g.halo -= e;
+  return g;
+}
+
+// The model conditions of the resident kernels: a sparse coded model with
+// finite T (the kernel's zero-padded edges multiply T by +0) and the class
+// tables.
+static bool resident_model_ok(const pp2_ctx* c) {
+  return c->resident && coded_active(c) && c->dict_sparse && c->dict_t_finite && c->dict_rfact &&
+         c->norm_block <= pp2::kResidentRing - 2 && c->ncus > 0;
+}
+
+// Whether a loop plan exists for view extension e (0: an unsharded grid),
+// with no allocation: the eligibility query of pp2_loop_steps_per_launch.
+static bool resident_plan_for(pp2_ctx* c, int e) {
+  if (c->res_plan_e != c->dict_n || c->res_view_e != e) {
     c->res_plan_e = c->dict_n;
+    c->res_view_e = e;
     c->res_ok = false;
     pp2::ResidentPlan p;
-    if (!pp2::resident_plan(c->g, c->dict_n, c->ncus, &p)) return false;
+    if (!pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p)) return false;
     c->res_plan = p;
     c->res_ok = true;
   }
-  return c->res_ok && resident_buffers(c, c->res_plan);
+  return c->res_ok;
+}
+
+// Whether pp2_loop_run takes the tile-resident loop (pp2_resident.hip) on an
+// unsharded context, allocating the plan's buffers.
+static bool resident_ready(pp2_ctx* c) {
+  if (c->comm || c->group || !resident_model_ok(c)) return false;
+  return resident_plan_for(c, 0) && resident_buffers(c, c->res_plan);
 }
 
 // Whether pp2_mdp_solve runs as resident sweeps (k_sweep_resident): the
 // resident loop's conditions minus the belief's, and a plan for J alone.
-static bool solve_ready(pp2_ctx* c) {
+static bool solve_plan_ok(pp2_ctx* c) {
   if (!c->resident || c->comm || c->group || !coded_active(c) || !c->dict_sparse ||
       c->ncus <= 0)
     return false;
@@ -866,17 +915,105 @@ static bool solve_ready(pp2_ctx* c) {
     c->sol_plan_e = c->dict_n;
     c->sol_ok = false;
     pp2::ResidentPlan p;
-    if (!pp2::solve_plan(c->g, c->dict_n, c->ncus, &p)) return false;
+    if (!pp2::solve_plan(c->g, c->dict_n, resident_cus(c), &p)) return false;
     c->sol_plan = p;
     c->sol_ok = true;
   }
-  return c->sol_ok && resident_buffers(c, c->sol_plan);
+  return c->sol_ok;
+}
+static bool solve_ready(pp2_ctx* c) { return solve_plan_ok(c) && resident_buffers(c, c->sol_plan); }
+
+// Resident launches of all contexts of this process on one device run one at
+// a time: each is ordered after the previous one (any stream) by an event, so
+// two contexts never hold part of the CUs each and wait for the rest.  (Work
+// of other processes can still delay tiles: the kernels' bounded waits and
+// resident_settle cover that.)
+struct ResidentGate {
+  std::mutex m;
+  hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;
+  bool any = false;
+};
+static ResidentGate& resident_gate(int device) {
+  static ResidentGate gates[64];
+  return gates[device & 63];
+}
+
+template <class F>
+static int gated_launch(pp2_ctx* c, F launch) {
+  ResidentGate& g = resident_gate(c->device);
+  std::lock_guard<std::mutex> lk(g.m);
+  if (!g.ev) HIPCHK(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming));
+  if (g.any && g.last != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, g.ev, 0));
+  HIPCHK(launch());
+  HIPCHK(hipEventRecord(g.ev, c->stream));
+  g.last = c->stream;
+  g.any = true;
+  HIPCHK(hipEventRecord(c->res_done, c->stream));
+  return PP2_OK;
+}
+
+static void journal(pp2_ctx* c, int kind, int n, const uint8_t* us, const uint8_t* zs) {
+  auto& j = c->journal;
+  j.kind = kind;
+  j.n = n;
+  j.bcur = c->bcur;
+  j.jcur = c->jcur;
+  j.kstep = c->kstep;
+  for (int i = 0; i < 2; ++i) {
+    j.pending[i] = c->pending[i];
+    j.pcount[i] = c->pcount[i];
+  }
+  if (us) j.us.assign(us, us + n);
+  if (zs) j.zs.assign(zs, zs + n);
+}
+
+
+// Verify the journalled resident launch before anything reads its outputs
+// (every C-ABI entry point calls this through check_ctx).  If one of its
+// waits timed out (a tile never got a CU), its outputs are garbage but its
+// inputs are intact (b, J went to the other buffers): restore the state
+// before the launch and re-run it with the launch-per-step kernels, which
+// give the same bits; the context stays on them (PP2_TUNE_RESIDENT 1
+// re-enables the resident kernels).  A row shard cannot re-run alone (its
+// RCCL partners have moved on): it reports the loss instead, and its belief
+// and values stay unusable until pp2_belief_set / pp2_mdp_reset.
+int pp2rt::resident_settle(pp2_ctx* c) {
+  if (c->journal.kind == 0) return PP2_OK;
+  DeviceGuard dg(c->device);
+  const int kind = c->journal.kind;
+  c->journal.kind = 0;
+  HIPCHK(hipEventSynchronize(c->res_done));
+  volatile unsigned* eh = c->res_host + 2;
+  if (*eh == 0u) return PP2_OK;
+  *eh = 0u;
+  ++c->res_fallbacks;
+  resident_free(c);  // the failed run's epochs and counters are inconsistent
+  c->resident = 0;
+  const auto& j = c->journal;
+  c->bcur = j.bcur;
+  c->jcur = j.jcur;
+  c->kstep = j.kstep;
+  for (int i = 0; i < 2; ++i) {
+    c->pending[i] = j.pending[i];
+    c->pcount[i] = j.pcount[i];
+  }
+  if (kind == 1) return loop_run_launches(c, j.n, j.us.data(), j.zs.data());
+  if (kind == 2) {
+    for (int i = 0; i < j.n; ++i) CHECK(mdp_sweep_once(c));
+    return PP2_OK;
+  }
+  c->lost_belief = c->lost_values = true;
+  return set_err(PP2_EHIP, "resident shard run: a workgroup wait timed out (the GPU was shared "
+                 "with another process?); this shard's belief and values are lost -- set them "
+                 "again (pp2_belief_set, pp2_mdp_reset); the context now uses per-step launches");
 }
 
 // pp2_mdp_solve's driver (reset, then blocks of 100 sweeps until the
 // inf-norm change of a block is <= max_cost * 1e-3 or max_sweeps is reached)
 // on resident sweeps: <= 20 blocks per launch, the decision taken in-kernel;
-// one host read of {sweeps, norm} per launch.
+// one host read of {sweeps, norm} per launch.  Returns 1 (not an error) when
+// a launch timed out: the caller solves again on per-sweep launches.
 static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps,
                           double* final_norm) {
   const pp2::ResidentPlan& p = c->sol_plan;
@@ -890,12 +1027,13 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
     a.E = c->dict_n;
     a.code = c->d_code;
     a.rows = c->d_rows;
-    a.j0 = c->J[c->jcur].v.p;
-    a.j1 = c->J[c->jcur ^ 1].v.p;
+    a.j_in = c->J[c->jcur].v.p;
+    a.j_out = c->J[c->jcur ^ 1].v.p;
     a.snap = c->Jsnap.v.p;
     a.A = c->A;
     a.xch = c->res_xch;
     a.sync = c->res_sync;
+    a.err_host = c->res_host + 2;
     a.tile_max = c->res_tmax;
     a.res = c->res_out;
     a.epoch = c->res_epoch;
@@ -906,12 +1044,20 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
     a.cap_blocks = cap_total ? cap_total - blocks : 0;
     a.thresh = thresh;
     a.nsweeps = 0;
-    HIPCHK(pp2::launch_sweep_resident(c->stream, p, a));
+    a.stall_tile = c->res_stall_tile;
+    CHECK(gated_launch(c, [&] { return pp2::launch_sweep_resident(c->stream, p, a); }));
     ++c->sol_launches;
     HIPCHK(hipMemcpyAsync(c->res_host, c->res_out, 2 * sizeof(int), hipMemcpyDeviceToHost,
                           c->stream));
-    c->res_used = true;
-    CHECK(resident_check(c));  // one stream sync for the result and the error word
+    HIPCHK(hipStreamSynchronize(c->stream));  // one sync for the result and the error word
+    volatile unsigned* eh = c->res_host + 2;
+    if (*eh != 0u) {
+      *eh = 0u;
+      ++c->res_fallbacks;
+      resident_free(c);
+      c->resident = 0;
+      return 1;
+    }
     int res[2];
     std::memcpy(res, c->res_host, sizeof(res));
     const int done = res[0];
@@ -922,7 +1068,7 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
     blocks += done / pp2::kSolveBlock;
     c->res_epoch += (unsigned)done + 1u;
     c->res_arrive += (unsigned)(done / pp2::kSolveBlock * p.ntiles);
-    c->jcur = (c->jcur + done) & 1;
+    c->jcur ^= 1;
     if (cap_total && blocks >= cap_total) break;
     if (!((double)norm > thresh)) break;
   }
@@ -931,67 +1077,81 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
   return PP2_OK;
 }
 
+// The fields of a loop run shared by the unsharded and shard launches.
+static void run_common(pp2_ctx* c, const pp2::ResidentPlan& p, pp2::ResidentRun& a) {
+  a.gamma = c->gamma;
+  a.E = c->dict_n;
+  a.rows = c->d_rows;
+  a.rfact = c->d_rfact;
+  a.xch = c->res_xch;
+  a.rt = p.rt;
+  a.ntiles = p.ntiles;
+  a.ring = c->res_ring;
+  a.sync = c->res_sync;
+  a.err_host = c->res_host + 2;
+  a.epoch = c->res_epoch;
+  a.arrive_base = c->res_arrive;
+  a.stall_tile = c->res_stall_tile;
+}
+
 // n loop steps in ceil(n / kResidentMaxSteps) resident launches, with the
-// state transitions of n blocked_loop_step calls (bcur, jcur, kstep, the
-// pending mass of the final belief).
+// state transitions of n blocked_loop_step calls (the pending mass of the
+// final belief, kstep) -- except that b and J end in the other ping-pong
+// buffer of their inputs whatever the parity of n.
 static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
   for (int i = 0; i < n; ++i)
     if (us[i] > 8 || zs[i] > 15)
       return set_err(PP2_EINVAL, "action %u / observation %u out of range", us[i], zs[i]);
-  const pp2::ResidentPlan& p = c->res_plan;
   const int depth = c->norm_block;
   const int nparts = pp2::mass_partials(c->g, 4);
   std::unique_ptr<pp2::ResidentRun> run(new pp2::ResidentRun());
   pp2::ResidentRun& a = *run;
   for (int i = 0; i < n;) {
+    if (i > 0) {
+      // the next launch reads this one's outputs
+      CHECK(resident_settle(c));
+      if (!resident_ready(c)) return loop_run_launches(c, n - i, us + i, zs + i);
+    }
+    const pp2::ResidentPlan& p = c->res_plan;
     const int m = std::min(n - i, pp2::kResidentMaxSteps);
-    const int bc = c->bcur, jc = c->jcur, bf = (bc + m) & 1, jf = (jc + m) & 1;
+    const int bc = c->bcur, jc = c->jcur;
     const bool start0 = c->kstep == 0;
     const bool fold = start0 && c->pending[bc];
+    run_common(c, p, a);
     a.g = c->g;
-    a.gamma = c->gamma;
-    a.E = c->dict_n;
     a.code = c->d_code;
-    a.rows = c->d_rows;
-    a.rfact = c->d_rfact;
     a.b_in = c->b[bc].v.p;
     a.j_in = c->J[jc].v.p;
-    a.b_out = c->b[bf].v.p;  // == b_in for even m: each lane reads its cells first
-    a.j_out = c->J[jf].v.p;
-    a.xch = c->res_xch;
+    a.b_out = c->b[bc ^ 1].v.p;
+    a.j_out = c->J[jc ^ 1].v.p;
     a.A = c->A;
     a.n = m;
     a.kstep0 = c->kstep;
     a.depth = depth;
-    a.rt = p.rt;
-    a.ntiles = p.ntiles;
     a.nparts = nparts;
+    a.own0 = 0;
+    a.own1 = c->g.rows;
+    a.shard = 0;
     a.bscale = depth == 1 ? 1.0f : kBlockScale;
     a.in_partials = fold ? c->pbuf[bc] : nullptr;
     a.in_n = c->pcount[bc];
     a.in_sum_out = fold ? c->bsum + bc : nullptr;
     a.in_sum = start0 && !fold ? c->bsum + bc : nullptr;
-    a.ring = c->res_ring;
-    a.out_partials = c->pbuf[bf];
-    a.sync = c->res_sync;
-    a.epoch = c->res_epoch;
-    a.arrive_base = c->res_arrive;
-    a.read_base = c->res_read;
-    a.final_wait_read = fold && bf == bc;
+    a.out_partials = c->pbuf[bc ^ 1];
+    a.scale_out = nullptr;
     for (int k = 0; k < m; ++k) a.uz[k] = (uint8_t)(us[i + k] | (zs[i + k] << 4));
-    HIPCHK(pp2::launch_loop_resident(c->stream, p, a));
+    journal(c, 1, m, us + i, zs + i);
+    CHECK(gated_launch(c, [&] { return pp2::launch_loop_resident(c->stream, p, a); }));
     ++c->res_launches;
     int arrivals = 0;
     for (int t = 0; t + 1 < m; ++t) arrivals += (c->kstep + t + 1) % depth == 0;
     c->res_epoch += (unsigned)m + 1u;
     c->res_arrive += (unsigned)(arrivals * p.ntiles);
-    if (a.final_wait_read) c->res_read += (unsigned)p.ntiles;
-    c->res_used = true;
-    c->pending[bf ^ 1] = false;
-    c->pending[bf] = true;
-    c->pcount[bf] = nparts;
-    c->bcur = bf;
-    c->jcur = jf;
+    c->pending[bc] = false;
+    c->pending[bc ^ 1] = true;
+    c->pcount[bc ^ 1] = nparts;
+    c->bcur = bc ^ 1;
+    c->jcur = jc ^ 1;
     c->kstep = (c->kstep + m) % depth;
     i += m;
   }
@@ -999,7 +1159,7 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
 }
 
 // pp2_mdp_sweep(n) on resident sweeps: n sweeps in one launch (no checks),
-// the J of the last sweep in J[(jcur + n) & 1], A of the last sweep.
+// the J of the last sweep in J[jcur ^ 1], A of the last sweep.
 static int sweeps_resident(pp2_ctx* c, int n) {
   const pp2::ResidentPlan& p = c->sol_plan;
   pp2::SweepRun a{};
@@ -1008,12 +1168,13 @@ static int sweeps_resident(pp2_ctx* c, int n) {
   a.E = c->dict_n;
   a.code = c->d_code;
   a.rows = c->d_rows;
-  a.j0 = c->J[c->jcur].v.p;
-  a.j1 = c->J[c->jcur ^ 1].v.p;
-  a.snap = c->Jsnap.v.p;  // read and written back unchanged (no checks)
+  a.j_in = c->J[c->jcur].v.p;
+  a.j_out = c->J[c->jcur ^ 1].v.p;
+  a.snap = c->Jsnap.v.p;  // read, not written (no checks)
   a.A = c->A;
   a.xch = c->res_xch;
   a.sync = c->res_sync;
+  a.err_host = c->res_host + 2;
   a.tile_max = c->res_tmax;
   a.res = c->res_out;
   a.epoch = c->res_epoch;
@@ -1022,11 +1183,198 @@ static int sweeps_resident(pp2_ctx* c, int n) {
   a.ntiles = p.ntiles;
   a.max_blocks = 1;
   a.nsweeps = n;
-  HIPCHK(pp2::launch_sweep_resident(c->stream, p, a));
+  a.stall_tile = c->res_stall_tile;
+  journal(c, 2, n, nullptr, nullptr);
+  CHECK(gated_launch(c, [&] { return pp2::launch_sweep_resident(c->stream, p, a); }));
   ++c->sol_launches;
-  c->res_used = true;
   c->res_epoch += (unsigned)n + 1u;
-  c->jcur = (c->jcur + n) & 1;
+  c->jcur ^= 1;
+  return PP2_OK;
+}
+
+// ------------------------------------------------ row shards on the resident loop
+// DESIGN.md §6.  A pp2_loop_run of n steps on a row shard runs in blocks of
+// m <= the resident halo depth: each block refreshes m halo rows of b and J
+// from the neighbours, then ONE resident launch runs the m steps on the view
+// extended by m rows per side.  Its first step divides by the global mass
+// (times 2^96); its later block starts scale by powers of two from the
+// shard's own mass; the next exchange rebases every shard to a common power
+// of two, where the global mass is known again.  The call ends rebased, with
+// the global mass finalised (the state of the per-step paths), and the halo
+// pipeline restarted.
+
+// Deepest resident halo this shard may use: the halo allocation, the smallest
+// shard (rows come from the immediate neighbour), PP2_TUNE_RESIDENT_HALO.
+static int shard_resident_depth(const pp2_ctx* c) {
+  int k = std::min(c->g.halo, std::max(1, c->min_shard_rows));
+  if (c->res_halo > 0) k = std::min(k, c->res_halo);
+  return k;
+}
+
+// The view extension e of this shard's resident runs (0: none fits): the
+// deepest halo whose view still has a co-resident plan.  Every launch of a
+// run uses this view and exchanges e halo rows, whatever its step count m <=
+// e (the rows beyond m go stale without reaching the owned rows), so the plan
+// and its buffers stay fixed across calls.
+int pp2rt::shard_resident_e(pp2_ctx* c) {
+  if (!(c->comm || c->group) || !resident_model_ok(c)) return 0;
+  if (c->res_e_dict == c->dict_n) return c->res_e;
+  int e = shard_resident_depth(c);
+  for (; e >= 1; --e) {
+    pp2::ResidentPlan p;
+    if (pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p)) break;
+  }
+  c->res_e_dict = c->dict_n;
+  c->res_e = e;
+  return e;
+}
+
+bool pp2rt::shard_resident_ready(pp2_ctx* c, int e) {
+  if (e < 1 || e > shard_resident_e(c)) return false;
+  if (!resident_plan_for(c, e) || !resident_buffers(c, c->res_plan)) return false;
+  if (!c->d_shift) {
+    if (hipMalloc(&c->d_shift, sizeof(int)) != hipSuccess) {
+      c->d_shift = nullptr;
+      return false;
+    }
+  }
+  if (!c->d_vec) {
+    const int nr = c->group ? c->group_size : c->nranks;
+    if (hipMalloc(&c->d_vec, (size_t)2 * nr * sizeof(float)) != hipSuccess) {
+      c->d_vec = nullptr;
+      return false;
+    }
+  }
+  return true;
+}
+
+// {mass, shift} of this shard's pending belief into its slot of d_vec.
+int pp2rt::shard_post_mass(pp2_ctx* c, int nranks, int rank) {
+  const int bc = c->bcur;
+  HIPCHK(pp2::launch_shard_mass_vec(c->stream, c->pbuf[bc], c->pcount[bc],
+                                    c->shift_pending ? c->d_shift : nullptr, c->d_vec, nranks,
+                                    rank));
+  return PP2_OK;
+}
+
+// Rebase rows [r0, r1) of the current belief after the vector is complete and
+// take the global mass: the state of a finalised, common-scale belief.
+int pp2rt::shard_rebase(pp2_ctx* c, int nranks, int rank, int r0, int r1) {
+  const int bc = c->bcur;
+  HIPCHK(pp2::launch_shard_rebase(c->stream, c->d_vec, nranks, rank, c->b[bc].v.p, c->g.wp, r0,
+                                  r1, c->g.rows, c->bsum + bc));
+  c->pending[bc] = false;
+  c->shift_pending = false;
+  return PP2_OK;
+}
+
+// One resident launch of m <= e steps on the view extended by e rows (the
+// halo rows e deep and the global mass are in place).
+int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, const uint8_t* zs) {
+  if (m < 1 || m > e || !shard_resident_ready(c, e))
+    return set_err(PP2_ESTATE, "shard resident plan lost");
+  const pp2::ResidentPlan& p = c->res_plan;
+  const Geom gv = view_geom(c, e);
+  const long long sh = (long long)e * c->g.wp;
+  const int bc = c->bcur, jc = c->jcur;
+  const int nparts = pp2::mass_partials(gv, 4);
+  const int depth = std::min(c->norm_block, pp2::kResidentRing - 2);
+  std::unique_ptr<pp2::ResidentRun> run(new pp2::ResidentRun());
+  pp2::ResidentRun& a = *run;
+  run_common(c, p, a);
+  a.g = gv;
+  a.code = c->d_code - sh;
+  a.b_in = c->b[bc].v.p - sh;
+  a.j_in = c->J[jc].v.p - sh;
+  a.b_out = c->b[bc ^ 1].v.p - sh;
+  a.j_out = c->J[jc ^ 1].v.p - sh;
+  a.A = c->A - sh;  // only owned rows are stored
+  a.n = m;
+  a.kstep0 = 0;
+  a.depth = depth;
+  a.nparts = nparts;
+  a.own0 = e;
+  a.own1 = e + c->g.rows;
+  a.shard = 1;
+  a.bscale = kBlockScale;
+  a.in_partials = nullptr;
+  a.in_n = 0;
+  a.in_sum_out = nullptr;
+  a.in_sum = c->bsum + bc;
+  a.out_partials = c->pbuf[bc ^ 1];
+  a.scale_out = c->d_shift;
+  for (int k = 0; k < m; ++k) a.uz[k] = (uint8_t)(us[k] | (zs[k] << 4));
+  journal(c, 3, m, nullptr, nullptr);
+  CHECK(gated_launch(c, [&] { return pp2::launch_loop_resident(c->stream, p, a); }));
+  ++c->res_launches;
+  int arrivals = 0;
+  for (int t = 0; t + 1 < m; ++t) arrivals += (t + 1) % depth == 0;
+  c->res_epoch += (unsigned)m + 1u;
+  c->res_arrive += (unsigned)(arrivals * p.ntiles);
+  c->pending[bc] = false;
+  c->pending[bc ^ 1] = true;
+  c->pcount[bc ^ 1] = nparts;
+  c->shift_pending = true;
+  c->bcur = bc ^ 1;
+  c->jcur = jc ^ 1;
+  c->kstep = 0;
+  return PP2_OK;
+}
+
+// The RCCL shard's resident run: blocks of m <= e steps, each after an
+// exchange of e halo rows (and, with a pending mass, the {mass, shift}
+// all-reduce and the rebase), then the closing all-reduce and rebase.
+static int shard_allreduce_vec(pp2_ctx* c) {
+  CHECK(comm_enter(c));
+  NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, 2 * c->nranks, ncclFloat, ncclSum, c->comm, cst(c)));
+  return comm_leave(c);
+}
+
+static int shard_loop_resident(pp2_ctx* c, int e, int n, const uint8_t* us, const uint8_t* zs) {
+  for (int i = 0; i < n; ++i)
+    if (us[i] > 8 || zs[i] > 15)
+      return set_err(PP2_EINVAL, "action %u / observation %u out of range", us[i], zs[i]);
+  break_pipeline(c);
+  // (no settle between blocks: a shard cannot re-run alone, and a timed-out
+  // block leaves the sticky error words set for the settle after the call)
+  for (int i = 0; i < n;) {
+    const int m = std::min(e, n - i);
+    if (c->pending[c->bcur]) {
+      CHECK(shard_post_mass(c, c->nranks, c->rank));
+      CHECK(shard_allreduce_vec(c));
+      CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, e));
+      CHECK(shard_rebase(c, c->nranks, c->rank, -e, c->g.rows + e));
+    } else {
+      CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, e));
+    }
+    CHECK(shard_resident_launch(c, e, m, us + i, zs + i));
+    i += m;
+  }
+  // close: the global mass at a common scale, the state of the per-step paths
+  CHECK(shard_post_mass(c, c->nranks, c->rank));
+  CHECK(shard_allreduce_vec(c));
+  CHECK(shard_rebase(c, c->nranks, c->rank, 0, c->g.rows));
+  break_pipeline(c);
+  return PP2_OK;
+}
+
+static int loop_step_impl(pp2_ctx* c, uint8_t u, uint8_t z) {
+  if (c->comm || c->norm_block > 1) return blocked_loop_step(c, u, z);  // RCCL shard or blocks
+  return loop_step_fused(c, u, z, false);
+}
+
+// The launch-per-step (or per-pair) body of pp2_loop_run; also re-runs a
+// resident launch that timed out (resident_settle).
+int pp2rt::loop_run_launches(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
+  for (int i = 0; i < n;) {
+    if (i + 1 < n && can_pair(c)) {
+      CHECK(loop_pair(c, us[i], zs[i], us[i + 1], zs[i + 1]));
+      i += 2;
+    } else {
+      CHECK(loop_step_impl(c, us[i], zs[i]));
+      ++i;
+    }
+  }
   return PP2_OK;
 }
 
@@ -1093,6 +1441,10 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->staging) (void)hipFree(c->staging);
   if (c->code_alloc) (void)hipFree(c->code_alloc);
   resident_free(c);
+  if (c->res_host) (void)hipHostFree(c->res_host);
+  if (c->res_done) (void)hipEventDestroy(c->res_done);
+  if (c->d_shift) (void)hipFree(c->d_shift);
+  if (c->d_vec) (void)hipFree(c->d_vec);
   for (float* p : {c->d_dict, c->d_rows, c->d_dl, c->d_tu, c->d_rfact})
     if (p) (void)hipFree(p);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -1101,17 +1453,17 @@ int pp2_destroy(pp2_ctx* c) {
 }
 
 int pp2_set_stream(pp2_ctx* c, void* s) {
-  CHECK(check_ctx(c));
+  CHECK(check_ctx_settled(c));
   c->stream = s ? (hipStream_t)s : c->own_stream;
   return PP2_OK;
 }
 
 int pp2_synchronize(pp2_ctx* c) {
-  CHECK(check_ctx(c));
+  CHECK(check_ctx_settled(c));
   DeviceGuard dg(c->device);
   if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  return resident_check(c);
+  return PP2_OK;
 }
 
 int pp2_get_geometry(pp2_ctx* c, uint32_t* rows, uint32_t* width,
@@ -1125,7 +1477,7 @@ int pp2_get_geometry(pp2_ctx* c, uint32_t* rows, uint32_t* width,
 }
 
 int pp2_set_tuning(pp2_ctx* c, int key, int value) {
-  CHECK(check_ctx(c));
+  CHECK(check_ctx_settled(c));
   switch (key) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
@@ -1133,6 +1485,22 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
     case PP2_TUNE_RESIDENT:
       if (value < 0 || value > 1) return set_err(PP2_EINVAL, "resident %d not in [0, 1]", value);
       c->resident = value;
+      c->res_e_dict = -1;
+      return PP2_OK;
+    case PP2_TUNE_RESIDENT_STALL:
+      if (value < -1) return set_err(PP2_EINVAL, "stall tile %d < -1", value);
+      c->res_stall_tile = value;
+      return PP2_OK;
+    case PP2_TUNE_RESIDENT_CUS:
+      if (value < 0) return set_err(PP2_EINVAL, "resident CUs %d < 0", value);
+      c->res_cus = value;
+      c->res_plan_e = c->sol_plan_e = c->res_e_dict = -1;
+      return PP2_OK;
+    case PP2_TUNE_RESIDENT_HALO:
+      if (value < 0 || value > c->g.halo)
+        return set_err(PP2_EINVAL, "resident halo %d not in [0, %d]", value, c->g.halo);
+      c->res_halo = value;
+      c->res_e_dict = -1;
       return PP2_OK;
     case PP2_TUNE_STEP_PAIRS:
       if (value < 0 || value > 2) return set_err(PP2_EINVAL, "step pairs %d not in [0, 2]", value);
@@ -1235,7 +1603,8 @@ int pp2_model_load(pp2_ctx* c, const char* dir) {
 
 // ---------------------------------------------------------------- belief
 int pp2_belief_set(pp2_ctx* c, const float* b) {
-  CHECK(check_ctx(c));
+  CHECK(check_ctx_settled(c));
+  c->lost_belief = false;
   if (!b) return set_err(PP2_EINVAL, "belief is null");
   DeviceGuard dg(c->device);
   break_pipeline(c);
@@ -1285,7 +1654,8 @@ int pp2_belief_update(pp2_ctx* c, uint8_t u, uint8_t z) {
 
 // ---------------------------------------------------------------- MDP
 int pp2_mdp_reset(pp2_ctx* c) {
-  CHECK(check_ctx(c));
+  CHECK(check_ctx_settled(c));
+  c->lost_values = false;
   DeviceGuard dg(c->device);
   for (Planes* P : {&c->J[0], &c->J[1], &c->Jsnap})
     HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
@@ -1318,7 +1688,11 @@ int pp2_mdp_solve(pp2_ctx* c, int max_sweeps, int* sweeps, double* final_norm) {
   const double max_cost = 5.0 / (1.0 - (double)c->gamma);
   if (solve_ready(c)) {
     break_pipeline(c);  // J changes: the loop's deep halo rows are stale
-    return solve_resident(c, max_sweeps, max_cost * 1e-3, sweeps, final_norm);
+    const int s = solve_resident(c, max_sweeps, max_cost * 1e-3, sweeps, final_norm);
+    if (s != 1) return s;
+    // a launch timed out (resident_settle's case): solve again from J = 0 on
+    // per-sweep launches
+    CHECK(pp2_mdp_reset(c));
   }
   int total = 0;
   double norm = 0.0;
@@ -1353,22 +1727,50 @@ int pp2_loop_step(pp2_ctx* c, uint8_t u, uint8_t z) {
   DeviceGuard dg(c->device);
   if (c->group)
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
-  if (c->comm || c->norm_block > 1) return blocked_loop_step(c, u, z);  // RCCL shard or blocks
-  return loop_step_fused(c, u, z, false);
+  return loop_step_impl(c, u, z);
 }
 
+// A query: plans (host arithmetic and the occupancy API), allocates nothing.
 int pp2_loop_steps_per_launch(pp2_ctx* c, int* steps) {
   CHECK(check_ctx(c));
   if (!steps) return set_err(PP2_EINVAL, "steps is null");
   DeviceGuard dg(c->device);
-  *steps = resident_ready(c) ? pp2::kResidentMaxSteps : pairs_apply(c) ? 2 : 1;
+  if (c->comm || c->group) {
+    const int e = shard_resident_e(c);
+    *steps = e > 0 ? e : pairs_apply(c) ? 2 : 1;
+  } else {
+    *steps = resident_model_ok(c) && resident_plan_for(c, 0) ? pp2::kResidentMaxSteps
+             : pairs_apply(c) ? 2 : 1;
+  }
+  return PP2_OK;
+}
+
+int pp2_resident_status(pp2_ctx* c, int* fallbacks, int* enabled) {
+  CHECK(check_ctx_settled(c));
+  if (fallbacks) *fallbacks = c->res_fallbacks;
+  if (enabled) *enabled = c->resident;
   return PP2_OK;
 }
 
 int pp2_resident_launches(pp2_ctx* c, int* loop_launches, int* solve_launches) {
-  CHECK(check_ctx(c));
+  CHECK(check_ctx_settled(c));
   if (loop_launches) *loop_launches = c->res_launches;
   if (solve_launches) *solve_launches = c->sol_launches;
+  return PP2_OK;
+}
+
+// The ranks' smallest v (a blocking 1-int all-reduce): RCCL shards agree on
+// their communication pattern before a run takes the resident path, since
+// eligibility (the model, the belief's sign pattern, allocations) is local.
+static int agree_min(pp2_ctx* c, int* v) {
+  if (c->nranks <= 1) return PP2_OK;
+  int* d = reinterpret_cast<int*>(c->rpartials);
+  HIPCHK(hipMemcpyAsync(d, v, sizeof(int), hipMemcpyHostToDevice, c->stream));
+  CHECK(comm_enter(c));
+  NCCLCHK(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, cst(c)));
+  CHECK(comm_leave(c));
+  HIPCHK(hipMemcpyAsync(v, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   return PP2_OK;
 }
 
@@ -1376,17 +1778,20 @@ int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
   CHECK(check_model(c));
   if (n < 0 || (n > 0 && (!us || !zs))) return set_err(PP2_EINVAL, "bad trajectory");
   DeviceGuard dg(c->device);
-  if (n >= 2 && resident_ready(c)) return loop_resident(c, n, us, zs);
-  for (int i = 0; i < n;) {
-    if (i + 1 < n && can_pair(c)) {
-      CHECK(loop_pair(c, us[i], zs[i], us[i + 1], zs[i + 1]));
-      i += 2;
-    } else {
-      CHECK(pp2_loop_step(c, us[i], zs[i]));
-      ++i;
+  if (c->group)
+    return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
+  if (n >= 2 && c->comm) {
+    int e = shard_resident_e(c);
+    if (e > 0 && !shard_resident_ready(c, e)) e = 0;
+    CHECK(agree_min(c, &e));
+    if (e > 0) {
+      if (!shard_resident_ready(c, e))
+        return set_err(PP2_ENOMEM, "resident shard buffers for a %d-row halo", e);
+      return shard_loop_resident(c, e, n, us, zs);
     }
   }
-  return PP2_OK;
+  if (n >= 2 && resident_ready(c)) return loop_resident(c, n, us, zs);
+  return loop_run_launches(c, n, us, zs);
 }
 
 // ---------------------------------------------------------------- FIB
@@ -1507,8 +1912,10 @@ int pp2_shard_comm_init(pp2_ctx* c, const uint8_t id[PP2_RCCL_ID_BYTES],
   HIPCHK(hipMemcpyAsync(&rows, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipFree(d));
-  c->kdepth_max = std::max(1, std::min(c->g.halo, rows));
+  c->min_shard_rows = rows;
+  c->kdepth_max = std::max(1, std::min(std::min(c->g.halo, kMaxNormBlock), rows));
   c->kdepth = c->kdepth_max;
+  c->res_e_dict = -1;
   break_pipeline(c);
   return PP2_OK;
 }

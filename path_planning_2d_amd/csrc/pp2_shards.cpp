@@ -158,7 +158,7 @@ int pp2_shard_group_create(pp2_shard_group** out, pp2_ctx* const* ctxs, int n) {
   {
     DeviceGuard dg(ctxs[0]->device);
     if (hipEventCreateWithFlags(&g->ev_total, hipEventDisableTiming) != hipSuccess ||
-        hipMalloc(&g->d_gather, (n + 1) * sizeof(float)) != hipSuccess)
+        hipMalloc(&g->d_gather, (2 * n + 1) * sizeof(float)) != hipSuccess)
       return fail(set_err(PP2_ENOMEM, "shard group scratch"));
   }
   int min_rows = ctxs[0]->g.rows;
@@ -166,8 +166,11 @@ int pp2_shard_group_create(pp2_shard_group** out, pp2_ctx* const* ctxs, int n) {
   for (int r = 0; r < n; ++r) {
     ctxs[r]->group = g;
     ctxs[r]->grank = r;
-    ctxs[r]->kdepth_max = std::max(1, std::min(ctxs[r]->g.halo, min_rows));
+    ctxs[r]->group_size = n;
+    ctxs[r]->min_shard_rows = min_rows;
+    ctxs[r]->kdepth_max = std::max(1, std::min(std::min(ctxs[r]->g.halo, kMaxNormBlock), min_rows));
     ctxs[r]->kdepth = ctxs[r]->kdepth_max;
+    ctxs[r]->res_e_dict = -1;
     break_pipeline(ctxs[r]);
   }
   *out = g;
@@ -181,7 +184,13 @@ int pp2_shard_group_destroy(pp2_shard_group* g) {
     DeviceGuard dg(g->ctx[r]->device);
     if (g->ev_done[r]) (void)hipEventDestroy(g->ev_done[r]);
     if (g->ev_local[r]) (void)hipEventDestroy(g->ev_local[r]);
-    if (g->ctx[r]->group == g) g->ctx[r]->group = nullptr;
+    if (g->ctx[r]->group == g) {
+      g->ctx[r]->group = nullptr;
+      g->ctx[r]->group_size = 0;
+      g->ctx[r]->res_e_dict = -1;
+      if (g->ctx[r]->d_vec) (void)hipFree(g->ctx[r]->d_vec);
+      g->ctx[r]->d_vec = nullptr;
+    }
   }
   if (!g->ctx.empty()) {
     DeviceGuard dg(g->ctx[0]->device);
@@ -198,6 +207,7 @@ int pp2_shard_group_synchronize(pp2_shard_group* g) {
     DeviceGuard dg(c->device);
     HIPCHK(hipStreamSynchronize(c->stream));
   }
+  for (pp2_ctx* c : g->ctx) CHECK(check_ctx_settled(c));
   return PP2_OK;
 }
 
@@ -207,13 +217,21 @@ int pp2_shard_group_synchronize(pp2_shard_group* g) {
 // (times 2^96) and the others by 1; step i computes a view kdepth-1-i rows
 // wider per side.  (The group also combines the mass after every step, so a
 // shard's bsum always holds the global mass for reads.)
-int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z) {
-  CHECK(check_group(g));
-  if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+// Every shard of the group at the same halo depth and block phase (a
+// per-shard PP2_TUNE_HALO_DEPTH or pipeline restart breaks that).
+static int check_in_step(pp2_shard_group* g) {
   pp2_ctx* c0 = g->ctx[0];
   for (pp2_ctx* c : g->ctx)
     if (c->kdepth != c0->kdepth || c->kstep != c0->kstep)
       return set_err(PP2_ESTATE, "shards of the group are out of step (halo depth differs?)");
+  return PP2_OK;
+}
+
+int pp2_shard_group_loop_step(pp2_shard_group* g, uint8_t u, uint8_t z) {
+  CHECK(check_group(g));
+  if (u > 8 || z > 15) return set_err(PP2_EINVAL, "action %u / observation %u out of range", u, z);
+  CHECK(check_in_step(g));
+  pp2_ctx* c0 = g->ctx[0];
   const int K = c0->kdepth;
   CHECK(wait_neighbours(g));
   const bool start = c0->kstep == 0;
@@ -259,9 +277,89 @@ static int group_loop_pair(pp2_shard_group* g, uint8_t u1, uint8_t z1, uint8_t u
   return mark_done(g);
 }
 
+// {mass, shift} of every shard into every shard's d_vec: each posts its slot,
+// shard 0's stream gathers the slots in rank order, every shard copies the
+// whole vector back (the RCCL path's all-reduce).
+static int group_share_vec(pp2_shard_group* g) {
+  const int n = (int)g->ctx.size();
+  for (int r = 0; r < n; ++r) {
+    pp2_ctx* c = g->ctx[r];
+    DeviceGuard dg(c->device);
+    CHECK(shard_post_mass(c, n, r));
+    HIPCHK(hipEventRecord(g->ev_local[r], c->stream));
+  }
+  pp2_ctx* c0 = g->ctx[0];
+  {
+    DeviceGuard dg(c0->device);
+    for (int r = 0; r < n; ++r) {
+      HIPCHK(hipStreamWaitEvent(c0->stream, g->ev_local[r], 0));
+      HIPCHK(hipMemcpyAsync(g->d_gather + 2 * r, g->ctx[r]->d_vec + 2 * r, 2 * sizeof(float),
+                            hipMemcpyDefault, c0->stream));
+    }
+    HIPCHK(hipEventRecord(g->ev_total, c0->stream));
+  }
+  for (int r = 0; r < n; ++r) {
+    pp2_ctx* c = g->ctx[r];
+    DeviceGuard dg(c->device);
+    HIPCHK(hipStreamWaitEvent(c->stream, g->ev_total, 0));
+    HIPCHK(hipMemcpyAsync(c->d_vec, g->d_gather, 2 * n * sizeof(float), hipMemcpyDefault,
+                          c->stream));
+  }
+  return PP2_OK;
+}
+
+// pp2_loop_run's resident shard path for a group (pp2_runtime.cpp
+// shard_loop_resident with device copies as the transport): blocks of m <= e
+// steps, each after the {mass, shift} exchange + rebase and e halo rows, then
+// the closing exchange + rebase.  Resident launches of the shards run one at
+// a time per device (the runtime's gate), each on the whole GPU.
+static int group_loop_resident(pp2_shard_group* g, int e, int n, const uint8_t* us,
+                               const uint8_t* zs) {
+  for (int i = 0; i < n; ++i)
+    if (us[i] > 8 || zs[i] > 15)
+      return set_err(PP2_EINVAL, "action %u / observation %u out of range", us[i], zs[i]);
+  const int ns = (int)g->ctx.size();
+  for (pp2_ctx* c : g->ctx) break_pipeline(c);
+  for (int i = 0; i < n;) {
+    const int m = std::min(e, n - i);
+    CHECK(wait_neighbours(g));
+    const bool pend = g->ctx[0]->pending[g->ctx[0]->bcur];
+    if (pend) CHECK(group_share_vec(g));
+    CHECK(exchange_local(g, {HALO_BELIEF, HALO_VALUE}, e));
+    if (pend) {  // the neighbours have copied our rows before we rebase them
+      CHECK(mark_done(g));
+      CHECK(wait_neighbours(g));
+    }
+    for (int r = 0; r < ns; ++r) {
+      pp2_ctx* c = g->ctx[r];
+      DeviceGuard dg(c->device);
+      if (pend) CHECK(shard_rebase(c, ns, r, -e, c->g.rows + e));
+      CHECK(shard_resident_launch(c, e, m, us + i, zs + i));
+    }
+    CHECK(mark_done(g));
+    i += m;
+  }
+  CHECK(group_share_vec(g));
+  for (int r = 0; r < ns; ++r) {
+    pp2_ctx* c = g->ctx[r];
+    DeviceGuard dg(c->device);
+    CHECK(shard_rebase(c, ns, r, 0, c->g.rows));
+    break_pipeline(c);
+  }
+  return mark_done(g);
+}
+
 int pp2_shard_group_loop_run(pp2_shard_group* g, int n, const uint8_t* us, const uint8_t* zs) {
   CHECK(check_group(g));
   if (n < 0 || (n > 0 && (!us || !zs))) return set_err(PP2_EINVAL, "bad trajectory");
+  CHECK(check_in_step(g));
+  if (n >= 2) {
+    int e = 1 << 30;  // the deepest halo every shard can run
+    for (pp2_ctx* c : g->ctx) e = std::min(e, shard_resident_e(c));
+    bool ok = e > 0;
+    for (pp2_ctx* c : g->ctx) ok = ok && shard_resident_ready(c, e);
+    if (ok) return group_loop_resident(g, e, n, us, zs);
+  }
   for (int i = 0; i < n;) {
     pp2_ctx* c0 = g->ctx[0];
     bool pair = i + 1 < n && c0->kstep + 2 <= c0->kdepth;

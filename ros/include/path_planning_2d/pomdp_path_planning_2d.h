@@ -4,8 +4,8 @@
 // (class at :37-87).  Same public interface, parameters, topics and services;
 // the online tree (SearchTree* search_tree, :80) and the model/FIB/PBVI device
 // globals become one pp2_ctx (the grid's device state) and one pp2_planner
-// (the QV-tree), both owned by the node.  Not compiled in this repository
-// (no ROS in the build image); see ros/README.md.
+// (the QV-tree), both owned by the node.  Syntax-checked with both adapters
+// (tests/test_ros_adapters.py); see ros/README.md.
 #ifndef POMDP_PATH_PLANNING_2D_H
 #define POMDP_PATH_PLANNING_2D_H
 

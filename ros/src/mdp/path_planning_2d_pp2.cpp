@@ -7,7 +7,8 @@
 // :207-269) without its OpenCV windows, then the optimal cost and action are
 // downloaded once for the table-lookup beliefCallback.
 //
-// Not compiled in this repository (no ROS / OpenCV in the build image).
+// Syntax-checked here (tests/test_ros_adapters.py, stand-in ROS / OpenCV
+// headers in tests/ros_stubs/); no ROS / OpenCV in the image to link it.
 #include <cstdio>
 #include <cstdlib>
 

@@ -4,9 +4,11 @@
 // topics ("belief" in, "control" out) and services ("save_data",
 // "reset_search_tree") are unchanged; every CUDA call is a pp2.h call.
 //
-// Not compiled in this repository: the build image has no ROS, OpenCV or
-// Boost.  tests/test_abi.py compiles the same pp2.h call sequence in plain C
-// (examples/pp2_node_demo.c) and tests/test_gpu_planner.py runs it.
+// Syntax-checked here (tests/test_ros_adapters.py: g++ -fsyntax-only -Werror
+// against the stand-in ROS / OpenCV headers of tests/ros_stubs/); the image
+// has no ROS, OpenCV or Boost to link it.  tests/test_abi.py compiles the same
+// pp2.h call sequence in plain C (examples/pp2_node_demo.c) and
+// tests/test_gpu_planner.py runs it.
 #include <cstdio>
 #include <vector>
 

@@ -1,0 +1,12 @@
+// stub (syntax check only): std_srvs/Trigger
+#pragma once
+#include <string>
+namespace std_srvs {
+struct Trigger {
+  struct Request {};
+  struct Response {
+    bool success = false;
+    std::string message;
+  };
+};
+}  // namespace std_srvs

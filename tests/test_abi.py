@@ -32,7 +32,7 @@ def test_binding_covers_header():
 
 def test_version_and_status_strings():
     lib = _lib.load()
-    assert lib.pp2_abi_version() == 2
+    assert lib.pp2_abi_version() == 3
     assert lib.pp2_status_string(0) == b"ok"
     assert lib.pp2_status_string(6) == b"RCCL error"
 

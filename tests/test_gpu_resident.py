@@ -230,3 +230,93 @@ def test_resident_beside_other_work(pp2):
         other.synchronize()
         assert a.resident_launches()[0] == 3
         _same(a, b, "beside other work")
+
+
+# ---------------------------------------------------------------- safety
+def test_resident_not_coresident_falls_back_before_launch(pp2):
+    """A plan whose tiles cannot all hold a CU at once is never launched:
+    with the plans limited to 128 CUs the 1024^2 grid (256 tiles) runs on
+    per-step launches -- no resident launch, no fallback, same bits."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 1024, 1024, 8, 23)
+    with a, b:
+        a.set_tuning(a.TUNE_RESIDENT_CUS, 128)
+        assert a.loop_steps_per_launch() != RESIDENT_STEPS
+        us, zs, _ = S.synth_trajectory(grid, 12, seed=6)
+        a.loop_run(us, zs)
+        b.loop_run(us, zs)
+        a.mdp_sweep(5)
+        b.mdp_sweep(5)
+        assert a.resident_launches() == (0, 0)
+        assert a.resident_status() == (0, True)
+        _same(a, b, "co-residency check")
+        a.set_tuning(a.TUNE_RESIDENT_CUS, 0)  # all CUs: resident again
+        a.loop_run(us, zs)
+        b.loop_run(us, zs)
+        assert a.resident_launches()[0] == 1
+        _same(a, b, "after lifting the limit")
+
+
+@pytest.mark.parametrize("what", ["loop", "sweeps", "solve"])
+def test_resident_timeout_reruns_from_intact_inputs(pp2, what):
+    """A resident launch whose waits time out (one tile held back, as if
+    another process kept its CU) writes only the OTHER ping-pong buffers, so
+    the next call re-runs it from its intact inputs on per-step launches:
+    the readback is correct, the fallback is counted and the context stays
+    on per-step launches."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 1024, 1024, 8, 31)
+    with a, b:
+        us, zs, _ = S.synth_trajectory(grid, 30, seed=12)
+        for c in (a, b):
+            c.loop_run(us[:10], zs[:10])  # a pending mass and a mid-block phase
+        a.synchronize()
+        a.set_tuning(a.TUNE_RESIDENT_STALL, 100)
+        if what == "loop":
+            for c in (a, b):
+                c.loop_run(us[10:30], zs[10:30])
+        elif what == "sweeps":
+            for c in (a, b):
+                c.mdp_sweep(7)
+        else:
+            ra, rb = a.mdp_solve(), b.mdp_solve()
+            assert ra == rb, (ra, rb)
+        _same(a, b, f"after a timed-out resident {what}")
+        assert a.resident_status() == (1, False)
+        # still correct afterwards, and the resident kernels can be re-enabled
+        a.set_tuning(a.TUNE_RESIDENT_STALL, -1)
+        a.set_tuning(a.TUNE_RESIDENT, 1)
+        for c in (a, b):
+            c.loop_run(us[:9], zs[:9])
+        _same(a, b, "after re-enabling")
+        assert a.resident_status() == (1, True)
+
+
+def test_two_resident_contexts_on_separate_streams(pp2):
+    """Two contexts whose resident launches are queued on different streams
+    at the same time: launches of one process run one at a time per device
+    (the runtime's gate), so neither holds part of the CUs waiting for the
+    rest -- no timeout, both equal their per-step twins."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 1024, 1024, 8, 41)
+    g2 = S.synth_grid(512, 1024, 5)
+    c2 = pp2.GridContext(g2, S.synth_goal(g2), gamma=float(GAMMA))
+    d2 = pp2.GridContext(g2, S.synth_goal(g2), gamma=float(GAMMA))
+    with a, b, c2, d2:  # (every context runs on a stream of its own)
+        d2.set_tuning(d2.TUNE_RESIDENT, 0)
+        d2.set_tuning(d2.TUNE_STEP_PAIRS, 0)
+        for c in (c2, d2):
+            c.model_generate()
+            c.belief_set(S.uniform_belief(g2))
+            c.mdp_reset()
+        us, zs, _ = S.synth_trajectory(grid, 300, seed=3)
+        u2, z2, _ = S.synth_trajectory(g2, 300, seed=4)
+        for lo, hi in ((0, 100), (100, 300)):
+            a.loop_run(us[lo:hi], zs[lo:hi])   # queued on a's stream ...
+            c2.loop_run(u2[lo:hi], z2[lo:hi])  # ... and on c2's before a's finishes
+            b.loop_run(us[lo:hi], zs[lo:hi])
+            d2.loop_run(u2[lo:hi], z2[lo:hi])
+        assert a.resident_status() == (0, True) and c2.resident_status() == (0, True)
+        assert a.resident_launches()[0] == 2 and c2.resident_launches()[0] == 2
+        _same(a, b, "context 1")
+        _same(c2, d2, "context 2")

@@ -214,6 +214,7 @@ def test_shard_group_step_pairs(bounds, depth):
         ref.model_generate()
         grp.model_generate()
         grp.set_halo_depth(depth)
+        grp.set_tuning(P.GridContext.TUNE_RESIDENT, 0)  # (these shards fit resident views)
         grp.set_tuning(P.GridContext.TUNE_STEP_PAIRS, 2)
         assert grp.loop_steps_per_launch() == [2] * (len(bounds) - 1)
         for c in (ref, grp):
@@ -258,3 +259,111 @@ def test_rccl_single_rank_step_pairs():
             np.testing.assert_array_equal(sh.mdp_get()[1], ref.mdp_get()[1])
             assert_rel_close(sh.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
                              msg=f"belief after {hi} steps")
+
+
+# ------------------------------------------------- row shards on the resident loop
+def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True):
+    """pp2_shard_group_loop_run on the resident kernel (one launch per halo
+    block of up to e steps on the view of the owned rows plus e halo rows per
+    side, power-of-two rescaling inside, rebased at each exchange) against
+    the unsharded grid: values and actions bit-exact, beliefs rel 1e-5."""
+    from path_planning_2d_amd import synthetic as S
+    steps = chunks[-1][1]
+    us, zs, _ = S.synth_trajectory(grid, steps + 1, seed=21)
+    b0 = S.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            P.ShardGroup(grid, goal, bounds, gamma=float(GAMMA)) as grp:
+        ref.model_generate()
+        grp.model_generate()
+        if halo:
+            grp.set_tuning(P.GridContext.TUNE_RESIDENT_HALO, halo)
+        e = grp.loop_steps_per_launch()
+        assert len(set(e)) == 1 and e[0] >= 2, e
+        for c in (ref, grp):
+            c.belief_set(b0)
+            c.mdp_reset()
+        launches = 0
+        for lo, hi in chunks:
+            ref.loop_run(us[lo:hi], zs[lo:hi])
+            grp.loop_run(us[lo:hi], zs[lo:hi])
+            launches += -(-(hi - lo) // e[0])
+            assert grp.shards[0].resident_launches()[0] == launches
+            Jr, Ar = ref.mdp_get()
+            Jg, Ag = grp.mdp_get()
+            np.testing.assert_array_equal(Jg.view(np.uint32), Jr.view(np.uint32),
+                                          err_msg=f"J after {hi} steps")
+            np.testing.assert_array_equal(Ag, Ar, err_msg=f"A after {hi} steps")
+            assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
+                             msg=f"belief after {hi} steps")
+        if mixed:  # per-step drivers after resident runs: the state is theirs
+            ref.belief_update(us[steps], zs[steps])
+            grp.belief_update(us[steps], zs[steps])
+            assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
+                             msg="belief update after resident runs")
+            ref.mdp_sweep(2)
+            grp.mdp_sweep(2)
+            np.testing.assert_array_equal(grp.mdp_get()[0], ref.mdp_get()[0])
+            ref.loop_run(us[:3], zs[:3])
+            grp.loop_run(us[:3], zs[:3])
+            np.testing.assert_array_equal(grp.mdp_get()[1], ref.mdp_get()[1])
+            assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
+                             msg="loop after the per-step drivers")
+        return e[0]
+
+
+def test_shard_group_resident_config4():
+    """BASELINE configs[3]'s per-rank geometry: the 2048^2 grid in 8 row shards
+    of 256 rows (one device here), each shard's run on the resident kernel
+    (view 256 + 2e rows, e = 128: 256 tiles of 2 x 2048 cells)."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    N = 2048
+    grid = S.synth_grid(N, N, N)
+    e = _resident_shard_run(P, grid, S.synth_goal(grid), tuple(range(0, N + 1, N // 8)),
+                            ((0, 30), (30, 41)), mixed=False)
+    assert e == 128
+
+
+@pytest.mark.parametrize("bounds,halo", [((0, 256, 512), 0), ((0, 200, 512), 6),
+                                         ((0, 128, 300, 512), 9)])
+def test_shard_group_resident_blocks(bounds, halo):
+    """Uneven shards, several halo blocks per call (e = 6, 9: in-kernel
+    power-of-two block starts every 8 steps, rebases at every exchange),
+    calls ending mid-block, then per-step drivers on the same state."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(512, 1024, 7)
+    e = _resident_shard_run(P, grid, S.synth_goal(grid), bounds,
+                            ((0, 2), (2, 19), (19, 40)), halo=halo)
+    assert e == (halo or 128)
+
+
+def test_rccl_single_rank_resident_256x2048():
+    """The RCCL path of a 256 x 2048 shard -- the per-rank share of the
+    2048^2 grid at 8 ranks -- with a 1-rank communicator: pp2_loop_run takes
+    the resident shard path (e = 128: 512-row view, exchanges, {mass, shift}
+    all-reduce, rebase) and equals the unsharded grid."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(256, 2048, 256)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 300, seed=8)
+    b0 = S.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            P.GridContext(grid, goal, gamma=float(GAMMA), rows=(0, 256)) as sh:
+        sh.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
+        for c in (ref, sh):
+            c.model_generate()
+            c.belief_set(b0)
+            c.mdp_reset()
+        assert sh.loop_steps_per_launch() == 128
+        for lo, hi in ((0, 17), (17, 300)):
+            ref.loop_run(us[lo:hi], zs[lo:hi])
+            sh.loop_run(us[lo:hi], zs[lo:hi])
+            np.testing.assert_array_equal(sh.mdp_get()[0].view(np.uint32),
+                                          ref.mdp_get()[0].view(np.uint32))
+            np.testing.assert_array_equal(sh.mdp_get()[1], ref.mdp_get()[1])
+            assert_rel_close(sh.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
+                             msg=f"belief after {hi} steps")
+        assert sh.resident_launches()[0] == 1 + 3
+        assert abs(float(sh.belief_get().astype(np.float64).sum()) - 1.0) < 1e-4
