@@ -54,10 +54,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_COPY_GBS = 6290.0            # measured float4 copy rate, the achievable ceiling (same table)
 MFMA_F32_PEAK_TFLOPS = 157.3     # dense f32-input MFMA peak (MI355X_MICROARCH.md, Matrix cores)
 BYTES_SWEEP = 369                # per cell: T 324 + C 36 + J 4 + J' 4 + A 1
 BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
-BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF
+BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF   # SURVEY.md §8(d) contract (T counted twice)
+BYTES_LOOP_DENSE = 381           # k_loop_step: T 324 read ONCE for gather and sweep + C 36 + L_z 4 + b 4 + b' 4 + J 4 + J' 4 + A 1
 BYTES_LOOP_CODED = 19            # per cell: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1
 BYTES_SWEEP_CODED = 11           # per cell: code 2 + J 4 + J' 4 + A 1
 LDS_BYTES_LOOP_CODED = 204       # per cell-step (factored rows): T_u gather 4*4 + L_z 4 + backup record 16 + quads 8*16 + stay 4 + costs 9*4
@@ -65,6 +67,7 @@ LDS_BYTES_LOOP_RESIDENT = 235    # - the backup record (registers) + class-plane
 RESIDENT_STEPS = 2048            # pp2_loop_steps_per_launch of the tile-resident loop
 LDS_PEAK_GBS = 150000.0          # ds_read_b64/b128 chip aggregate (MI355X_MICROARCH.md LDS)
 GAMMA = 0.95
+RCCL_ROUND_US = (10.0, 30.0)     # assumed RCCL small-message round trip over xGMI (not measurable on 1 GPU)
 
 
 def parse():
@@ -504,6 +507,9 @@ def config4_leg(args, ws, rank, local, stream):
         return el
 
     out = None
+    rank_share = None
+    if ws == 1:
+        rank_share = config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run)
     if ws > 1:
         ctx = P.GridContext(grid, goal, gamma=GAMMA, device=local, rows=(r0, r1))
         ctx.set_stream(stream.cuda_stream)
@@ -557,9 +563,75 @@ def config4_leg(args, ws, rank, local, stream):
             out.update({"cells_per_s": v1, "ms_per_step": 1e3 * el1 / k,
                         "speedup_vs_unsharded_1gpu": 1.0,
                         "parity": "single rank: nothing to gather"})
+            if rank_share is not None:
+                t1 = 1e6 * el1 / k
+                proj = rank_share["projection_8_ranks"]
+                proj["unsharded_1gpu_us_per_step"] = t1
+                proj["speedup_vs_unsharded_1gpu"] = [t1 / proj["us_per_step"][1],
+                                                     t1 / proj["us_per_step"][0]]
+                out["rank_share_8"] = rank_share
     if ws > 1:
         dist.barrier()
     return out
+
+
+def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
+    """config4's per-rank work at 8 ranks, measured on this GPU: rank 3's
+    256 x 2048 shard of the 2048^2 grid as an RCCL shard with a 1-rank
+    communicator, so pp2_loop_run takes the resident shard path exactly as
+    a rank of the 8-GPU job does (views of 256 + 2e rows, one launch per e
+    steps, the {mass, shift} all-reduce, halo exchanges and rebases) -- with
+    every RCCL call a 1-rank no-op.  The 8-GPU time is then projected as this
+    measured step plus the RCCL rounds the real job adds per call (2 per block
+    + the agreement and the closing all-reduce) at an ASSUMED xGMI round trip
+    (RCCL_ROUND_US; multi-GPU RCCL cannot run on one GPU)."""
+    import torch
+    import path_planning_2d_amd as P
+    G = args.c4_size
+    R = 8
+    r0, r1 = 3 * G // R, 4 * G // R
+    w, k = args.c4_warmup, args.c4_steps
+    ctx = P.GridContext(grid, goal, gamma=GAMMA, device=local, rows=(r0, r1))
+    ctx.set_stream(stream.cuda_stream)
+    ctx.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
+    ctx.model_generate()
+    ctx.belief_set(b0[r0 * G:r1 * G])
+    ctx.mdp_reset()
+    ctx.synchronize()
+    e = ctx.loop_steps_per_launch()
+    l0 = ctx.resident_launches()[0]
+    el = run(ctx, False)
+    launches = ctx.resident_launches()[0] - l0
+    ctx.close()
+    t = 1e6 * el / k
+    nblk = -(-k // e)
+    rounds = 2 * nblk + 1
+    lo, hi = (t + rounds * r / k for r in RCCL_ROUND_US)
+    return {"shard": f"rows [{r0}, {r1}) x {G} of the {G}^2 grid (rank 3 of 8), 1-rank RCCL "
+                     f"communicator",
+            "steps_per_launch": e, "resident_launches_in_run": launches,
+            "measured_us_per_step": t,
+            "projection_8_ranks": {
+                "assumed_rccl_round_us": list(RCCL_ROUND_US),
+                "rccl_rounds_per_call": rounds,
+                "us_per_step": [lo, hi],
+                "note": "measured per-rank step + rounds x assumed RCCL round trip / steps; "
+                        "a projection, not a measurement (one GPU)"}}
+
+
+def sq_counters():
+    """LDS / VALU busy fractions of k_loop_resident from the newest committed
+    SQ-counter summary (profiles/r*/resident_sq.json, tools/collect_lds_pmc.sh
+    + tools/sq_summary.py), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "resident_sq.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        d["source"] = os.path.relpath(f, ROOT)
+        return d
+    return None
 
 
 def cpu_model():
@@ -715,12 +787,15 @@ def main():
         dloop_ms = timed(loop_reps)
         dsweep_ms = timed(lambda: ctx.mdp_sweep(reps))
         ctx.set_tuning(ctx.TUNE_CODED_MODEL, 1)
-        dloop_gbs = BYTES_LOOP * cells_per_gpu / (dloop_ms * 1e-3) / 1e9
+        dloop_gbs = BYTES_LOOP_DENSE * cells_per_gpu / (dloop_ms * 1e-3) / 1e9
+        dtraffic, dsrc = pmc_traffic("k_loop_step", cells_per_gpu, exclude="coded")
         dense = {"kernel": "k_loop_step (dense model planes)",
                  "loop_step_us": dloop_ms * 1e3,
                  "cells_per_s": cells_per_gpu / (dloop_ms * 1e-3),
                  "loop_gbs": dloop_gbs, "loop_frac": dloop_gbs / HBM_PEAK_GBS,
-                 "algorithmic_bytes_per_cell": BYTES_LOOP,
+                 "loop_frac_of_measured_copy_rate": dloop_gbs / HBM_COPY_GBS,
+                 "algorithmic_bytes_per_cell": BYTES_LOOP_DENSE,
+                 "traffic_per_launch": dtraffic, "traffic_source": dsrc,
                  "mdp_sweep_us": dsweep_ms * 1e3,
                  "mdp_sweep_frac": BYTES_SWEEP * cells_per_gpu / (dsweep_ms * 1e-3) / 1e9
                  / HBM_PEAK_GBS}
@@ -756,7 +831,9 @@ def main():
     # the resident loop runs the whole timed trajectory in ceil(steps / 2048) launches
     spl = (args.steps / -(-args.steps // RESIDENT_STEPS)) if resident else steps_per_launch
     lds_bytes = LDS_BYTES_LOOP_RESIDENT if resident else LDS_BYTES_LOOP_CODED
-    sweep_gbs = bytes_sweep * cells_per_gpu / (sweep_ms * 1e-3) / 1e9
+    # a resident sweep launch moves its 11 B/cell once for all `reps` sweeps
+    sweep_res = coded and resident
+    sweep_gbs = bytes_sweep * cells_per_gpu / ((sweep_ms * (reps if sweep_res else 1)) * 1e-3) / 1e9
     belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
     # one launch = spl steps; its average duration: back-to-back resident
     # launches (above), else the timed region's events
@@ -822,7 +899,12 @@ def main():
                            f"{loop_kernel} (two fused loop steps per launch: belief update + "
                            f"MDP Bellman sweep, twice)" if spl == 2 else
                            f"{loop_kernel} (fused belief update + MDP Bellman sweep)"),
-                "bound": "hbm",
+                # the resident kernel moves its bytes once per launch: its
+                # period is the per-step hand-off latency chain, with HBM, LDS
+                # and VALU all below saturation (sq_counters); the others are
+                # HBM-priced
+                "bound": "latency" if resident and coded else "hbm",
+                "sq_counters": sq_counters() if resident and coded else None,
                 "achieved": loop_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -863,8 +945,8 @@ def main():
             "dense_path": dense,
             "config4": c4,
             "kernels": {
-                "mdp_sweep_kernel": (("k_sweep_resident (the 100 sweeps in one launch; gbs/frac "
-                                      "count its 11 B/cell once per sweep)")
+                "mdp_sweep_kernel": (("k_sweep_resident (all the timed sweeps in one launch; "
+                                      "gbs/frac count its 11 B/cell once per launch)")
                                      if coded and resident else
                                      "k_mdp_sweep_coded" if coded else "k_mdp_sweep"),
                 "mdp_sweep_us": sweep_ms * 1e3,

@@ -92,6 +92,7 @@ struct pp2_ctx {
   uint8_t* A = nullptr;      // rows * wp actions
   Planes fib[2], fibsnap;    // FIB alphas (9 planes)
   int fcur = 0;
+  unsigned fib_version = 1;  // bumped whenever the current alphas change (planner caches)
   float* pbuf[2] = {nullptr, nullptr};  // per-block partial masses of b[0], b[1]
   bool pending[2] = {false, false};     // mass of b[i] still in pbuf[i]
   int pcount[2] = {0, 0};               // number of partials in pbuf[i]
@@ -136,7 +137,9 @@ struct pp2_ctx {
   unsigned* res_sync = nullptr;    // sync words (flags, counters, error)
   float* res_ring = nullptr;       // kResidentRing slots of mass partials
   float* res_xch = nullptr;        // exchange rows
-  unsigned res_epoch = 0, res_arrive = 0;  // epoch-tagged counters
+  unsigned res_slot[4] = {0, 0, 0, 0};  // uses of the exchange slots 0 / 1 (tag bits):
+                                        // loop kernel's region, then the sweep kernel's
+  unsigned res_arrive = 0;         // arrival counter (epoch-tagged)
   int sol_plan_e = -1;             // resident MDP solve (k_sweep_resident): plan for dict_n
   bool sol_ok = false;
   pp2::ResidentPlan sol_plan{};

@@ -231,10 +231,10 @@ constexpr int kResidentRing = 16;        // partial-mass slots (>= block depth +
 constexpr int kResidentSyncArrive = 0;   // sync words: block-start arrivals,
 constexpr int kResidentSyncErr = 2;      //   sticky timeout flag
 constexpr int kResidentSyncWords = 16;
-// Exchange granules per lane and side: 16 B each, {v0, tag, v1, tag} -- a
-// tag in every 8-B half (MI355X_MICROARCH.md: 16-B sc1 stores are observed
-// untorn per 8-B half only).  The loop hands over b and J (4 + 4 floats).
-constexpr int kResidentGranules = 4;
+// Exchange granules per lane and side: 16 B each, four values whose bit 31
+// carries the slot use's tag bit (every handed-over value is finite and
+// >= +0), so every 4-B word validates itself.  The loop hands over b and J.
+constexpr int kResidentGranules = 2;
 struct ResidentPlan {
   int rt = 0, ntiles = 0, threads = 0;
   size_t lds = 0;
@@ -266,7 +266,8 @@ struct ResidentRun {
   unsigned* sync;            // kResidentSyncWords sync words
   unsigned* err_host;        // pinned host word: set with the sticky error word
   int* scale_out;            // shard: the run's total power-of-two shift (tile 0)
-  unsigned epoch, arrive_base;  // epoch-tagged counters of earlier launches
+  unsigned arrive_base;      // arrival counter of earlier launches (epoch-tagged)
+  unsigned slot_use[2];      // uses of exchange slots 0 / 1 by earlier launches
   int stall_tile;            // diagnostic (tests): this tile returns at once, -1 none
   uint8_t uz[kResidentMaxSteps];  // u | z << 4 per step
 };
@@ -288,7 +289,8 @@ struct SweepRun {
   unsigned* err_host;  // pinned host word, set with the sticky error word
   float* tile_max;     // 2 x ntiles per-tile maxima
   int* res;            // {sweeps done, norm bits}
-  unsigned epoch, arrive_base;
+  unsigned arrive_base;
+  unsigned slot_use[2];  // uses of exchange slots 0 / 1 by earlier launches
   int rt, ntiles;
   int max_blocks;      // blocks per launch
   int cap_blocks;      // stop after this many blocks (0: no cap)

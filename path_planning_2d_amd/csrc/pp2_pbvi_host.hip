@@ -16,6 +16,8 @@
 //   k_pbvi_select   the best action per belief and its alpha (:610-626)
 #include <hip/hip_runtime.h>
 #include <float.h>
+
+#include <algorithm>
 #include <limits.h>
 
 #include "pp2_pbvi_internal.h"
@@ -140,6 +142,123 @@ __global__ __launch_bounds__(256) void k_rows_chain(const float* __restrict__ A,
       sums[r0 + tid] = acc;
     else if (sums)
       sums[r0 + tid] = acc;
+  }
+}
+
+// ---------------------------------------------------------------- lane chains
+// The same x-ordered chains when there are few of them (the reference-order
+// planner: 144 child renormalisations, 144 x 9 FIB dots, 9 rewards per
+// expansion).  Each chain is a dependent fp32 add per element, so its floor
+// is the add latency (~4 cycles, 65536 cells: ~0.11 ms); k_rows_chain's
+// load -> barrier -> sum per 256-x tile runs it at ~0.8 ms, k_pair_chain's
+// 32-x tiles at ~7 ms.  Here one wave per block owns a few chains, one per
+// lane (chain (r, i) = A row r, B row i), and streams its NROW rows through
+// an LDS ring by LDS-DMA (global_load_lds, one 1-KiB wave instruction per row
+// and chunk) up to three chunks ahead of the adds, waiting on its own vmcnt
+// only -- no barrier.  One wave's LDS-DMA lands ~16 KiB per 0.65 us
+// (MI355X_MICROARCH.md ldsdma-fill), so a block stages at most ~8 rows: a
+// 256-x chunk of adds takes ~0.43 us.  Lanes that share a row read the same
+// LDS address (a broadcast); rows sit 16 B apart in bank space.  Per element:
+// the product (DOT) first, then the add (x86 std::inner_product).
+constexpr int kLaneCH = 256;            // floats per row and chunk
+constexpr int kLaneRowF = kLaneCH + 4;  // LDS row stride (16-B bank skew)
+constexpr int kLaneSlots = 4;           // ring slots: 3 chunks in flight + 1 summed
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+// Block (bx, by): A rows [bx * ra, + ra), B rows [by * rb, + rb) (DOT), NROW
+// = ra + rb staged rows (fewer real ones at the grid's edge: the DMA repeats
+// row 0, so the vmcnt arithmetic stays fixed).
+template <int MODE, int NROW>
+__global__ __launch_bounds__(64) void k_lane_chains(const float* __restrict__ A, int na, int ra,
+                                                    const float* __restrict__ B, int nb, int rb,
+                                                    int ld, int n, float* __restrict__ out,
+                                                    int ldo) {
+  __shared__ __attribute__((aligned(16))) float ring[kLaneSlots][NROW][kLaneRowF];
+  const int lane = threadIdx.x;
+  const int r0 = blockIdx.x * ra, i0 = blockIdx.y * rb;
+  const int nra = min(ra, na - r0);
+  const int nrb = MODE == CH_DOT ? min(rb, nb - i0) : 0;
+  const int nrow = nra + (MODE == CH_DOT ? rb : 0);  // staged row j: A row j < ra.. (see src)
+  const int nch = (n + kLaneCH - 1) / kLaneCH;
+  // chunk c of every staged row into slot c % kLaneSlots
+  auto issue = [&](int c) {
+    const int x = c * kLaneCH + 4 * lane;
+    const int xs = x + 4 <= ld ? x : 0;  // past the row: an in-bounds address, never summed
+#pragma unroll
+    for (int j = 0; j < NROW; ++j) {
+      const float* src;
+      if (MODE == CH_DOT && j >= ra) {
+        const int ib = i0 + (j - ra < nrb ? j - ra : 0);
+        src = B + (long long)ib * ld;
+      } else {
+        src = A + (long long)(r0 + (j < nra ? j : 0)) * ld;
+      }
+      __builtin_amdgcn_global_load_lds((glb_void_t*)(src + xs),
+                                       (lds_void_t*)&ring[c % kLaneSlots][j][0], 16, 0, 0);
+    }
+  };
+  (void)nrow;
+  const int r = MODE == CH_DOT ? lane / rb : lane;
+  const int i = MODE == CH_DOT ? lane - r * rb : 0;
+  const bool active = MODE == CH_DOT ? (r < nra && i < nrb) : lane < nra;
+  const int ra_ = active ? r : 0, rb_ = MODE == CH_DOT && active ? ra + i : 0;
+  float acc = 0.0f;
+  for (int c = 0; c < 3 && c < nch; ++c) issue(c);
+  for (int c = 0; c < nch; ++c) {
+    // chunk c has landed once at most the younger chunks' loads are pending
+    if (c + 2 < nch) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NROW) : "memory");
+    else if (c + 1 < nch) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NROW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const float* pa = &ring[c % kLaneSlots][ra_][0];
+    const float* pb = &ring[c % kLaneSlots][rb_][0];
+    const int m = min(kLaneCH, n - c * kLaneCH);
+    if (m == kLaneCH) {
+      // groups of 8 elements, reads issued two groups ahead of the dependent
+      // adds (12 LDS reads in flight at most: lgkmcnt counts to 15)
+      constexpr int G = 8, NG = kLaneCH / G;
+      f4 ga[3][2], gb[3][2];
+      auto rd = [&](int g) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          ga[g % 3][q] = *(const f4*)(pa + G * g + 4 * q);
+          if (MODE == CH_DOT) gb[g % 3][q] = *(const f4*)(pb + G * g + 4 * q);
+        }
+      };
+      rd(0);
+      rd(1);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if (g + 2 < NG) rd(g + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (MODE == CH_DOT) {
+            const f4 pr = ga[g % 3][q] * gb[g % 3][q];  // the products, then the chain
+            acc = acc + pr.x;
+            acc = acc + pr.y;
+            acc = acc + pr.z;
+            acc = acc + pr.w;
+          } else {
+            acc = acc + ga[g % 3][q].x;
+            acc = acc + ga[g % 3][q].y;
+            acc = acc + ga[g % 3][q].z;
+            acc = acc + ga[g % 3][q].w;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      for (int j = 0; j < m; ++j) acc = MODE == CH_DOT ? acc + pa[j] * pb[j] : acc + pa[j];
+    }
+    // slot c % kLaneSlots is read (the LDS reads above returned: the adds
+    // consumed them); chunk c + 3 reuses the slot of chunk c - 1
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (c + 3 < nch) issue(c + 3);
+  }
+  if (active) {
+    if (MODE == CH_DOT) out[(long long)(r0 + r) * ldo + i0 + i] = acc;
+    else out[r0 + r] = acc;
   }
 }
 
@@ -516,6 +635,29 @@ hipError_t launch_rows_seq(hipStream_t st, int mode, const float* A, int ld, int
   else
     hipLaunchKernelGGL(k_rows_chain<CH_SUM>, grid, dim3(256), 0, st, A, rows, nullptr, ld, rows,
                        n, sums, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_lane_sums(hipStream_t st, const float* A, int ld, int rows, int n,
+                            float* sums) {
+  if (rows <= 0) return hipSuccess;
+  if (ld % 4 != 0) return hipErrorInvalidValue;
+  if (rows == 1)
+    hipLaunchKernelGGL((k_lane_chains<CH_SUM, 1>), dim3(1), dim3(64), 0, st, A, rows, 1, nullptr,
+                       0, 1, ld, n, sums, 1);
+  else  // 4 rows per block: ~0.16 us of LDS-DMA per 0.43-us chunk of adds
+    hipLaunchKernelGGL((k_lane_chains<CH_SUM, 4>), dim3(cdiv(rows, 4)), dim3(64), 0, st, A, rows,
+                       4, nullptr, 0, 1, ld, n, sums, 1);
+  return hipGetLastError();
+}
+
+hipError_t launch_lane_dots(hipStream_t st, const float* A, int na, const float* B, int nb,
+                            int ld, int n, float* out, int ldo) {
+  if (na <= 0 || nb <= 0) return hipSuccess;
+  if (ld % 4 != 0) return hipErrorInvalidValue;
+  // 3 A rows x 3 B rows per block: 9 chains, 6 rows staged per chunk
+  hipLaunchKernelGGL((k_lane_chains<CH_DOT, 6>), dim3(cdiv(na, 3), cdiv(nb, 3)), dim3(64), 0, st,
+                     A, na, 3, B, nb, 3, ld, n, out, ldo);
   return hipGetLastError();
 }
 

@@ -41,6 +41,13 @@ hipError_t launch_pbvi_gamma_ao(hipStream_t st, const Geom& g, float gamma, Plan
 // ROW_CDF: cdf[r][x] = the running sums (std::partial_sum), and sums[r].
 hipError_t launch_rows_seq(hipStream_t st, int mode, const float* A, int ld, int rows, int n,
                            float* sums, float* cdf);
+// The same sums and dots for few chains (<= a few thousand): one chain per
+// lane, rows streamed through an LDS ring (k_lane_chains), ~7x faster at hw
+// 65536 when the chains, not the bytes, are the limit.  Bit-identical results.
+// launch_lane_dots: out[i*ldo + j] = inner_product(A[i], B[j]), nb < 16.
+hipError_t launch_lane_sums(hipStream_t st, const float* A, int ld, int rows, int n, float* sums);
+hipError_t launch_lane_dots(hipStream_t st, const float* A, int na, const float* B, int nb,
+                            int ld, int n, float* out, int ldo);
 // A[r][x] /= sums[r], x < n
 hipError_t launch_rows_div(hipStream_t st, float* A, int ld, int rows, int n,
                            const float* sums);

@@ -563,6 +563,7 @@ int fib_sweep_once(pp2_ctx* c) {
                                c->fib[c->fcur].v, c->fib[fn].v,
                                c->use_coded && c->dict_n > 0 && c->dict_sparse));
   c->fcur = fn;
+  ++c->fib_version;
   return PP2_OK;
 }
 
@@ -843,7 +844,10 @@ static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
   gext.rows += 2 * gext.halo;
   const size_t sync_b = (size_t)pp2::kResidentSyncWords * sizeof(unsigned);
   const size_t ring_b = (size_t)pp2::kResidentRing * pp2::mass_partials(gext, 4) * sizeof(float);
-  const size_t xch_b = pp2::resident_xch_floats(c->g, p.ntiles) * sizeof(float);
+  // two exchange regions: the loop kernel's (b and J granules) and the
+  // sweep kernel's (J alone), each with its own slot-use counts, so that a
+  // granule's stale content is always the previous use of its own slot
+  const size_t xch_b = 2 * pp2::resident_xch_floats(c->g, p.ntiles) * sizeof(float);
   const size_t tmax_b = (size_t)2 * p.ntiles * sizeof(float);
   if (hipMalloc(&c->res_sync, sync_b) != hipSuccess || hipMalloc(&c->res_ring, ring_b) != hipSuccess ||
       hipMalloc(&c->res_xch, xch_b) != hipSuccess || hipMalloc(&c->res_tmax, tmax_b) != hipSuccess ||
@@ -856,7 +860,8 @@ static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
     return false;
   }
   c->res_ntiles = p.ntiles;
-  c->res_epoch = c->res_arrive = 0;
+  c->res_slot[0] = c->res_slot[1] = c->res_slot[2] = c->res_slot[3] = 0;
+  c->res_arrive = 0;
   return true;
 }
 
@@ -953,6 +958,17 @@ static int gated_launch(pp2_ctx* c, F launch) {
   return PP2_OK;
 }
 
+// Exchange-slot uses of a launch: the prologue's publish into slot 1, then
+// one per published step t (slot t & 1) for t < published.  region 0: the
+// loop kernel's exchange rows, 1: the sweep kernel's.
+static void count_slot_uses(pp2_ctx* c, int region, int published) {
+  c->res_slot[2 * region + 1] += 1u + (unsigned)(published / 2);
+  c->res_slot[2 * region] += (unsigned)((published + 1) / 2);
+}
+static float* sweep_xch(pp2_ctx* c) {
+  return c->res_xch + pp2::resident_xch_floats(c->g, c->res_ntiles);
+}
+
 static void journal(pp2_ctx* c, int kind, int n, const uint8_t* us, const uint8_t* zs) {
   auto& j = c->journal;
   j.kind = kind;
@@ -1031,12 +1047,13 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
     a.j_out = c->J[c->jcur ^ 1].v.p;
     a.snap = c->Jsnap.v.p;
     a.A = c->A;
-    a.xch = c->res_xch;
+    a.xch = sweep_xch(c);
     a.sync = c->res_sync;
     a.err_host = c->res_host + 2;
     a.tile_max = c->res_tmax;
     a.res = c->res_out;
-    a.epoch = c->res_epoch;
+    a.slot_use[0] = c->res_slot[2];
+    a.slot_use[1] = c->res_slot[3];
     a.arrive_base = c->res_arrive;
     a.rt = p.rt;
     a.ntiles = p.ntiles;
@@ -1066,7 +1083,7 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
     std::memcpy(&norm, &res[1], sizeof(float));
     total += done;
     blocks += done / pp2::kSolveBlock;
-    c->res_epoch += (unsigned)done + 1u;
+    count_slot_uses(c, 1, done);  // every sweep publishes
     c->res_arrive += (unsigned)(done / pp2::kSolveBlock * p.ntiles);
     c->jcur ^= 1;
     if (cap_total && blocks >= cap_total) break;
@@ -1089,7 +1106,8 @@ static void run_common(pp2_ctx* c, const pp2::ResidentPlan& p, pp2::ResidentRun&
   a.ring = c->res_ring;
   a.sync = c->res_sync;
   a.err_host = c->res_host + 2;
-  a.epoch = c->res_epoch;
+  a.slot_use[0] = c->res_slot[0];
+  a.slot_use[1] = c->res_slot[1];
   a.arrive_base = c->res_arrive;
   a.stall_tile = c->res_stall_tile;
 }
@@ -1145,7 +1163,7 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
     ++c->res_launches;
     int arrivals = 0;
     for (int t = 0; t + 1 < m; ++t) arrivals += (c->kstep + t + 1) % depth == 0;
-    c->res_epoch += (unsigned)m + 1u;
+    count_slot_uses(c, 0, m - 1);  // the last step publishes nothing
     c->res_arrive += (unsigned)(arrivals * p.ntiles);
     c->pending[bc] = false;
     c->pending[bc ^ 1] = true;
@@ -1172,12 +1190,13 @@ static int sweeps_resident(pp2_ctx* c, int n) {
   a.j_out = c->J[c->jcur ^ 1].v.p;
   a.snap = c->Jsnap.v.p;  // read, not written (no checks)
   a.A = c->A;
-  a.xch = c->res_xch;
+  a.xch = sweep_xch(c);
   a.sync = c->res_sync;
   a.err_host = c->res_host + 2;
   a.tile_max = c->res_tmax;
   a.res = c->res_out;
-  a.epoch = c->res_epoch;
+  a.slot_use[0] = c->res_slot[2];
+  a.slot_use[1] = c->res_slot[3];
   a.arrive_base = c->res_arrive;
   a.rt = p.rt;
   a.ntiles = p.ntiles;
@@ -1187,7 +1206,7 @@ static int sweeps_resident(pp2_ctx* c, int n) {
   journal(c, 2, n, nullptr, nullptr);
   CHECK(gated_launch(c, [&] { return pp2::launch_sweep_resident(c->stream, p, a); }));
   ++c->sol_launches;
-  c->res_epoch += (unsigned)n + 1u;
+  count_slot_uses(c, 1, n);
   c->jcur ^= 1;
   return PP2_OK;
 }
@@ -1309,7 +1328,7 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
   ++c->res_launches;
   int arrivals = 0;
   for (int t = 0; t + 1 < m; ++t) arrivals += (t + 1) % depth == 0;
-  c->res_epoch += (unsigned)m + 1u;
+  count_slot_uses(c, 0, m - 1);
   c->res_arrive += (unsigned)(arrivals * p.ntiles);
   c->pending[bc] = false;
   c->pending[bc ^ 1] = true;
@@ -1801,6 +1820,7 @@ int pp2_fib_reset(pp2_ctx* c) {
   for (Planes* P : {&c->fib[0], &c->fib[1], &c->fibsnap})
     HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
   c->fcur = 0;
+  ++c->fib_version;
   return PP2_OK;
 }
 
@@ -1843,6 +1863,7 @@ int pp2_fib_set(pp2_ctx* c, const float* alphas) {
   CHECK(check_ctx(c));
   if (!alphas) return set_err(PP2_EINVAL, "alphas is null");
   DeviceGuard dg(c->device);
+  ++c->fib_version;
   return upload_planes(c, c->fib[c->fcur], alphas);
 }
 

@@ -138,6 +138,9 @@ struct pp2_planner {
   int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
   float* d_rrows = nullptr;     // [9][ld] R[.][a]
   float* d_frows = nullptr;     // [9][ld] FIB alphas[.][i]
+  unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
+  hipStream_t side = nullptr;   // reward chains beside the child chains
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   float* d_rsum = nullptr;      // [256] row sums
   float* d_rout = nullptr;      // [9 rewards | 256 x 9 FIB dots]
   float* h_rout = nullptr;      // pinned mirror of d_rout
@@ -311,8 +314,7 @@ int ref_normalize_slot(pp2_planner* p, int s) {
   const Slot& sl = p->slots[s];
   const int n = (int)p->n, ld = p->ref_ld;
   HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
-  HIPCHK(pp2::launch_rows_seq(c->stream, pp2::ROW_SUM, p->d_parent, ld, 1, n, p->d_rsum,
-                              nullptr));
+  HIPCHK(pp2::launch_lane_sums(c->stream, p->d_parent, ld, 1, n, p->d_rsum));
   HIPCHK(pp2::launch_rows_div(c->stream, p->d_parent, ld, 1, n, p->d_rsum));
   HIPCHK(pp2::launch_unpack(c->stream, c->g, 1, p->d_parent, sl.b.v));
   const float one = 1.0f;
@@ -326,9 +328,11 @@ int ref_normalize_slot(pp2_planner* p, int s) {
 int ref_leaf_bounds(pp2_planner* p, const float* d_rows, int rows) {
   pp2_ctx* c = p->ctx;
   const int n = (int)p->n, ld = p->ref_ld;
-  CHECK(pack_rows(p, c->fib[c->fcur].v, 9, p->d_frows));
-  HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, p->d_frows, 9, ld, n,
-                                p->d_rout + 9, 9));
+  if (p->frows_version != c->fib_version) {  // the alphas changed since the last pack
+    CHECK(pack_rows(p, c->fib[c->fcur].v, 9, p->d_frows));
+    p->frows_version = c->fib_version;
+  }
+  HIPCHK(pp2::launch_lane_dots(c->stream, d_rows, rows, p->d_frows, 9, ld, n, p->d_rout + 9, 9));
   if (p->pbvi) {
     const float* al = nullptr;
     int S = 0, Sp = 0, ald = 0;
@@ -551,14 +555,19 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   HIPCHK(hipMemcpyAsync(p->h_belief, p->d_parent, n * sizeof(float), hipMemcpyDeviceToHost,
                         c->stream));
   HIPCHK(hipEventRecord(p->ev_belief, c->stream));
-  HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, p->d_parent, 1, p->d_rrows, 9, ld,
-                                (int)n, p->d_rout, 9));
+  // the 9 reward chains need only the parent: on the side stream, beside
+  // the children's update and renormalisation chains
+  HIPCHK(hipEventRecord(p->ev_fork, c->stream));
+  HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
+  HIPCHK(pp2::launch_lane_dots(p->side, p->d_parent, 1, p->d_rrows, 9, ld, (int)n, p->d_rout,
+                                9));
+  HIPCHK(hipEventRecord(p->ev_join, p->side));
   HIPCHK(pp2::launch_pbvi_update(c->stream, c->g, c->T.v, c->L.v, p->d_parent, ld, p->d_srow,
                                  p->d_us, p->d_zs, 144, p->d_children));
-  HIPCHK(pp2::launch_rows_seq(c->stream, pp2::ROW_SUM, p->d_children, ld, 144, (int)n,
-                              p->d_rsum, nullptr));
+  HIPCHK(pp2::launch_lane_sums(c->stream, p->d_children, ld, 144, (int)n, p->d_rsum));
   HIPCHK(pp2::launch_rows_div(c->stream, p->d_children, ld, 144, (int)n, p->d_rsum));
   CHECK(ref_leaf_bounds(p, p->d_children, 144));
+  HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipMemcpyAsync(p->h_rout, p->d_rout, kRefOutFloats * sizeof(float),
                         hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipEventSynchronize(p->ev_belief));
@@ -742,7 +751,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       hipMalloc(&p->d_dense, p->n * sizeof(float)) != hipSuccess ||
       hipHostMalloc(&p->h_out, kOutFloats * sizeof(float), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&p->h_belief, p->n * sizeof(float), hipHostMallocDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&p->ev_belief, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&p->ev_belief, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "planner scratch allocation failed"));
   p->ref = prm->reference_order == 1;
   // dense rows of the children / PBVI / reference-order passes: the PBVI
@@ -850,6 +862,12 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (p->h_out) (void)hipHostFree(p->h_out);
   if (p->h_belief) (void)hipHostFree(p->h_belief);
   if (p->ev_belief) (void)hipEventDestroy(p->ev_belief);
+  for (hipEvent_t e : {p->ev_fork, p->ev_join})
+    if (e) (void)hipEventDestroy(e);
+  if (p->side) {
+    (void)hipStreamSynchronize(p->side);
+    (void)hipStreamDestroy(p->side);
+  }
   delete p;
   return PP2_OK;
 }

@@ -21,14 +21,16 @@ def main():
     ctx.model_generate()
     ctx.fib_solve()
     b0 = S.uniform_belief(grid)
-    with P.QVTreePlanner(ctx, max_search_tree_depth=3, max_online_iteration=15) as pl:
+    ref = int(os.environ.get("PP2_REF", "0"))  # 1: reference_order planner
+    with P.QVTreePlanner(ctx, max_search_tree_depth=3, max_online_iteration=15,
+                         reference_order=ref) as pl:
         bench.closed_loop(grid, b0, pl.step, 3, 1e9)
         pl.reset()
         t0 = time.perf_counter()
         ms = bench.closed_loop(grid, b0, pl.step, steps, 1e9)
         el = time.perf_counter() - t0
     ctx.close()
-    print(f"{steps} plan steps: p50 {np.percentile(ms, 50):.3f} ms, mean {ms.mean():.3f} ms, "
+    print(f"reference_order={ref}: {steps} plan steps: p50 {np.percentile(ms, 50):.3f} ms, mean {ms.mean():.3f} ms, "
           f"wall {el * 1e3:.1f} ms", flush=True)
 
 
