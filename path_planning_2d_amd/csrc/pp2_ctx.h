@@ -109,6 +109,7 @@ struct pp2_ctx {
   int dict_n = 0;                  // entries; 0 = no dictionary (dense path only)
   bool dict_sparse = false;        // every T row is zero off the base-kernel support
   bool dict_t_finite = false;      // every dictionary T entry is finite
+  bool dict_tl_nonneg = false;     // every dictionary T and L entry finite and >= +0
   bool dict_rfact = false;         // d_rfact valid: raw T and L by class (<= 16 each)
   // the sparse rows' T == 0 skip needs finite, non-negative beliefs (not -0):
   // false after a pp2_belief_set that breaks that, until the next one

@@ -41,8 +41,9 @@
 // plus e halo rows per side, refreshed e deep before the launch, for n <= e
 // steps (the rows outside the view read as 0, so the view's outer rows go
 // stale one row per step and never reach the owned ones).  Only owned rows
-// add to the mass and store b', J', A.  Block starts inside the run scale the
-// belief by a power of two chosen from the shard's own mass, summed into
+// store b', J', A and give the final mass partials.  Block starts inside the
+// run scale the belief by a power of two chosen from the mass of the whole
+// view (every cell is <= it, so no halo row can overflow), summed into
 // *scale_out; the host rebases every shard to a common power of two at the
 // next halo exchange (launch_shard_rebase), where the global mass is known.
 //
@@ -507,7 +508,9 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
     const int ci = t & 1, co = ci ^ 1;
     const bool last = t == a.n - 1;
     // ---- a block start inside the run: the exact mass of step t-1's belief
-    // (a shard: its owned mass, for a power-of-two scale)
+    // (a shard: the mass of its whole view -- every cell is <= it, so the
+    // power-of-two scale cannot overflow a halo row that holds more mass than
+    // the owned ones)
     if (t > 0 && (a.kstep0 + t) % a.depth != 0) {
       inv = 1.0f;
     } else if (t > 0) {
@@ -576,7 +579,6 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
         if (!last) publish(ci, p, best, (use[ci] + 1u) & 1u);
         __builtin_amdgcn_s_setprio(0);
       }
-      if (!own) local = 0.0f;  // a shard's halo rows carry no mass
       PP2_RT(2);
     }
     if (last) break;  // the last step's outputs are stored after the loop
@@ -598,13 +600,14 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
     PP2_RT(3);
   }
 
-  // ---- the last step: b, J, A of the (owned) rows and its mass partials
+  // ---- the last step: b, J, A of the (owned) rows and the owned mass
+  // partials (a shard's halo rows are its neighbours' rows)
   if (own) {
     const long long off = (long long)y * wp + x0;
     store4<true>(a.b_out + off, p);
     store_ja<true>(a.j_out, a.A, off, best, arg);
   }
-  const float v = wave_sum(local);
+  const float v = wave_sum(own ? local : 0.0f);
   if (lane == 0 && pi < a.nparts) a.out_partials[pi] = v;
   if (a.scale_out && tile == 0 && threadIdx.x == 0) *a.scale_out = shift;
 }

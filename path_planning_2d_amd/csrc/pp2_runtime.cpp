@@ -420,6 +420,17 @@ int build_model_dict(pp2_ctx* c) {
     for (int a = 0; a < 9; ++a)
       for (int i = 0; i < 9; ++i)
         if (!std::isfinite(dh[(size_t)e * pp2::kDictRow + a * 10 + i])) t_finite = false;
+  // the resident kernels hand over beliefs and values with a tag bit in the
+  // sign bit: every T and L entry finite and >= +0 keeps every belief so
+  // (values: C >= +0, the sparse rows' precondition below)
+  bool tl_nonneg = true;
+  for (int e = 0; e < E && tl_nonneg; ++e) {
+    for (int a = 0; a < 9; ++a)
+      for (int i = 0; i < 9; ++i)
+        if (!finite_nonneg(dh[(size_t)e * pp2::kDictRow + a * 10 + i])) tl_nonneg = false;
+    for (int z = 0; z < 16; ++z)
+      if (!finite_nonneg(dh[(size_t)e * pp2::kDictRow + pp2::kDictL + z])) tl_nonneg = false;
+  }
   // LDS-layout rows: sparse when every T entry off the base-kernel support is
   // +0.0 (always so for generated models), else the full [a][T..,C] rows
   // They also drop the T == 0 terms of the Bellman backup, which equals the
@@ -536,6 +547,7 @@ int build_model_dict(pp2_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   c->dict_sparse = sparse;
   c->dict_t_finite = t_finite;
+  c->dict_tl_nonneg = tl_nonneg;
   c->dict_rfact = rfact_ok;
   c->dict_n = E;
   return PP2_OK;
@@ -884,7 +896,8 @@ static Geom view_geom(const pp2_ctx* c, int e) {
 // finite T (the kernel's zero-padded edges multiply T by +0) and the class
 // tables.
 static bool resident_model_ok(const pp2_ctx* c) {
-  return c->resident && coded_active(c) && c->dict_sparse && c->dict_t_finite && c->dict_rfact &&
+  return c->resident && coded_active(c) && c->dict_sparse && c->dict_t_finite &&
+         c->dict_tl_nonneg && c->dict_rfact &&
          c->norm_block <= pp2::kResidentRing - 2 && c->ncus > 0;
 }
 
@@ -914,7 +927,7 @@ static bool resident_ready(pp2_ctx* c) {
 // resident loop's conditions minus the belief's, and a plan for J alone.
 static bool solve_plan_ok(pp2_ctx* c) {
   if (!c->resident || c->comm || c->group || !coded_active(c) || !c->dict_sparse ||
-      c->ncus <= 0)
+      c->ncus <= 0)  // (values >= +0 finite: the sparse rows' precondition)
     return false;
   if (c->sol_plan_e != c->dict_n) {
     c->sol_plan_e = c->dict_n;
