@@ -147,20 +147,29 @@ struct pp2_ctx {
   int res_ntiles = 0;              // tiles the sync words / exchange rows were sized for
   float* res_tmax = nullptr;       // 2 x ntiles per-tile convergence maxima
   int* res_out = nullptr;          // {sweeps, norm bits} of a resident solve launch
-  unsigned* res_host = nullptr;    // pinned: {sweeps, norm bits, error word} written by the kernels
+  // pinned words the kernels write: {sweeps, norm bits, solve error word, -},
+  // then one error word per journalled launch
+  unsigned* res_host = nullptr;
   int res_launches = 0, sol_launches = 0;  // pp2_resident_launches
   // Every resident launch is journalled until verified (resident_settle): its
-  // inputs stay intact (outputs go to the other ping-pong buffers), so a
-  // launch whose waits timed out is re-run from them with per-step launches
-  // before anything reads its outputs.
+  // inputs stay intact (outputs go to the other ping-pong buffers), and a
+  // launch queued behind an unverified one exits at once if an earlier one
+  // timed out (the device error word is sticky), so the first failed launch
+  // and all later ones are re-run from the failed one's inputs with per-step
+  // launches before anything reads their outputs.  Resident loop runs and
+  // sweeps queue up to kResidentChain launches this way (no host sync between
+  // back-to-back calls); every other entry point verifies first.
   struct ResidentJournal {
-    int kind = 0;                  // 0 none, 1 loop run, 2 sweeps
+    int kind = 0;                  // 1 loop run, 2 sweeps, 3 shard loop run
     int n = 0;
     int bcur = 0, jcur = 0, kstep = 0, pcount[2] = {0, 0};
     bool pending[2] = {false, false};
     std::vector<uint8_t> us, zs;
-  } journal;
-  hipEvent_t res_done = nullptr;   // recorded after the journalled launch
+  };
+  static constexpr int kResidentChain = 16;
+  static constexpr int kResHostChain = 4;  // res_host index of launch 0's error word
+  std::vector<ResidentJournal> journal;    // unverified launches, oldest first
+  hipEvent_t res_done = nullptr;   // recorded after every journalled launch
   int res_fallbacks = 0;           // launches re-run after a timeout (pp2_resident_status)
   int res_stall_tile = -1;         // PP2_TUNE_RESIDENT_STALL (tests)
   int res_cus = 0;                 // PP2_TUNE_RESIDENT_CUS: CUs the plans may use (0: all)

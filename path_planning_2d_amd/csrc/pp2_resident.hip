@@ -58,7 +58,9 @@
 // 100 MHz clock it raises the sticky error word (and the pinned host word)
 // and returns, so a grid that is not fully resident ends with an error
 // instead of hanging; the host then re-runs the launch from its intact inputs
-// with the launch-per-step kernels (pp2_runtime.cpp resident_settle).
+// with the launch-per-step kernels (pp2_runtime.cpp resident_settle).  A
+// launch queued behind an unverified one reads the error word first and
+// exits before any global store if it is raised (the host re-runs it too).
 #include <algorithm>
 
 #include "pp2_coded_dev.h"
@@ -75,8 +77,14 @@ __device__ unsigned long long g_rtrace[16][64][4][4];
   if (tile < 16 && t < 64 && lane == 0 && (wave == 0 || wave == 5 || wave == 9 || wave == 12)) \
   g_rtrace[tile][t][wave == 0 ? 0 : wave == 5 ? 1 : wave == 9 ? 2 : 3][ph] =          \
       __builtin_amdgcn_s_memrealtime()
+// prologue / epilogue of every tile (wave 0): entry, tables staged, loop top,
+// outputs stored
+__device__ unsigned long long g_rtrace_pro[1024][4];
+#define PP2_RP(ph) \
+  if (tile < 1024 && threadIdx.x == 0) g_rtrace_pro[tile][ph] = __builtin_amdgcn_s_memrealtime()
 #else
 #define PP2_RT(ph) (void)0
+#define PP2_RP(ph) (void)0
 #endif
 
 namespace {
@@ -371,6 +379,10 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   if (tile == a.stall_tile) return;  // diagnostic: a tile that never arrives
+  PP2_RP(0);
+  // a chained launch after one that timed out does nothing: its inputs are
+  // that launch's garbage outputs (resident_settle re-runs both)
+  const unsigned prior_err = ld_flag(a.sync + kResidentSyncErr);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // wave-uniform: a row holds wpr whole waves (wp % 256 == 0)
   const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x / tpr);
@@ -436,6 +448,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
     for (int k = 0; k < 4; ++k) lx4 |= (uint32_t)lx[cc[k]] << (8 * k);
   }
   __syncthreads();  // the staged tables
+  PP2_RP(1);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint4 w = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * cc[k]);
@@ -467,6 +480,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
     *reinterpret_cast<uint32_t*>(sP + i * ps) = 0u;
     *reinterpret_cast<uint32_t*>(sP + i * ps + 4 + wp) = 0u;
   }
+  if (prior_err != 0u) return;  // (uniform: before any global store)
   if (valid) {
     const long long off = (long long)y * wp + x0;
     const f4a b = *reinterpret_cast<const f4a*>(a.b_in + off);
@@ -502,6 +516,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   int shift = 0;  // shard runs: the power-of-two shifts of the block starts so far
   float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, best[4] = {0.0f, 0.0f, 0.0f, 0.0f}, local = 0.0f;
   uint32_t arg[4] = {0u, 0u, 0u, 0u};
+  PP2_RP(2);
 
   for (int t = 0; t < a.n; ++t) {
     const int u = a.uz[t] & 15, z = a.uz[t] >> 4;
@@ -610,6 +625,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   const float v = wave_sum(own ? local : 0.0f);
   if (lane == 0 && pi < a.nparts) a.out_partials[pi] = v;
   if (a.scale_out && tile == 0 && threadIdx.x == 0) *a.scale_out = shift;
+  PP2_RP(3);
 }
 
 // ---------------------------------------------------------------- MDP solve
@@ -635,6 +651,8 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   if (tile == a.stall_tile) return;  // diagnostic: a tile that never arrives
+  // a chained launch after one that timed out does nothing (resident_settle)
+  const unsigned prior_err = ld_flag(a.sync + kResidentSyncErr);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x / tpr);
   const int wj = __builtin_amdgcn_readfirstlane((threadIdx.x % tpr) >> 6);
@@ -675,6 +693,7 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
   }
   uint32_t c0 = 0, c1 = 0;  // the quad's codes
   const long long goff = (long long)y * wp + x0;
+  if (prior_err != 0u) return;  // (uniform: before any global store)
   if (valid) {
     const uint2 m = *reinterpret_cast<const uint2*>(a.code + goff);
     c0 = m.x;
@@ -956,5 +975,9 @@ hipError_t launch_shard_rebase(hipStream_t st, const float* vec, int nranks, int
 extern "C" int pp2_debug_resident_trace(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(pp2::g_rtrace), sizeof(pp2::g_rtrace)) == hipSuccess
              ? 0 : 2;
+}
+extern "C" int pp2_debug_resident_prologue(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pp2::g_rtrace_pro), sizeof(pp2::g_rtrace_pro)) ==
+                 hipSuccess ? 0 : 2;
 }
 #endif

@@ -827,15 +827,17 @@ static void resident_free(pp2_ctx* c) {
   c->sol_plan_e = -1;
 }
 
-// The pinned words the kernels write ({sweeps, norm bits, error word}) and the
-// completion event of the journalled launch; kept across plan changes.
+// The pinned words the kernels write ({sweeps, norm bits, error word}, then
+// the journalled launches' error words) and the completion event of the
+// journalled launches; kept across plan changes.
 static bool resident_host_words(pp2_ctx* c) {
   if (!c->res_host) {
-    if (hipHostMalloc(&c->res_host, 4 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
+    const size_t b = (pp2_ctx::kResHostChain + pp2_ctx::kResidentChain) * sizeof(unsigned);
+    if (hipHostMalloc(&c->res_host, b, hipHostMallocDefault) != hipSuccess) {
       c->res_host = nullptr;
       return false;
     }
-    std::memset(c->res_host, 0, 4 * sizeof(unsigned));
+    std::memset(c->res_host, 0, b);
   }
   if (!c->res_done && hipEventCreateWithFlags(&c->res_done, hipEventDisableTiming) != hipSuccess) {
     c->res_done = nullptr;
@@ -964,10 +966,11 @@ static int gated_launch(pp2_ctx* c, F launch) {
   if (!g.ev) HIPCHK(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming));
   if (g.any && g.last != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, g.ev, 0));
   HIPCHK(launch());
-  HIPCHK(hipEventRecord(g.ev, c->stream));
+  static const int ab = getenv("PP2_AB_EV") ? atoi(getenv("PP2_AB_EV")) : 0;  // TEMP A/B
+  if (!(ab & 1)) HIPCHK(hipEventRecord(g.ev, c->stream));
   g.last = c->stream;
   g.any = true;
-  HIPCHK(hipEventRecord(c->res_done, c->stream));
+  if (!(ab & 2)) HIPCHK(hipEventRecord(c->res_done, c->stream));
   return PP2_OK;
 }
 
@@ -982,8 +985,11 @@ static float* sweep_xch(pp2_ctx* c) {
   return c->res_xch + pp2::resident_xch_floats(c->g, c->res_ntiles);
 }
 
-static void journal(pp2_ctx* c, int kind, int n, const uint8_t* us, const uint8_t* zs) {
-  auto& j = c->journal;
+// Journal a resident launch about to be enqueued; returns its pinned error
+// word (the caller settles first when kResidentChain launches are queued).
+static unsigned* journal(pp2_ctx* c, int kind, int n, const uint8_t* us, const uint8_t* zs) {
+  c->journal.emplace_back();
+  auto& j = c->journal.back();
   j.kind = kind;
   j.n = n;
   j.bcur = c->bcur;
@@ -995,31 +1001,40 @@ static void journal(pp2_ctx* c, int kind, int n, const uint8_t* us, const uint8_
   }
   if (us) j.us.assign(us, us + n);
   if (zs) j.zs.assign(zs, zs + n);
+  unsigned* eh = c->res_host + pp2_ctx::kResHostChain + (c->journal.size() - 1);
+  *eh = 0u;
+  return eh;
 }
 
 
-// Verify the journalled resident launch before anything reads its outputs
-// (every C-ABI entry point calls this through check_ctx).  If one of its
-// waits timed out (a tile never got a CU), its outputs are garbage but its
-// inputs are intact (b, J went to the other buffers): restore the state
-// before the launch and re-run it with the launch-per-step kernels, which
-// give the same bits; the context stays on them (PP2_TUNE_RESIDENT 1
-// re-enables the resident kernels).  A row shard cannot re-run alone (its
-// RCCL partners have moved on): it reports the loss instead, and its belief
-// and values stay unusable until pp2_belief_set / pp2_mdp_reset.
+// Verify the journalled resident launches before anything reads their
+// outputs (every C-ABI entry point calls this through check_ctx, except the
+// resident runs that queue behind them).  If a launch's waits timed out (a
+// tile never got a CU), its outputs are garbage but its inputs are intact
+// (b, J went to the other buffers), and the launches queued behind it exited
+// without a store: restore the state before the failed launch and re-run it
+// and every later one with the launch-per-step kernels, which give the same
+// bits; the context stays on them (PP2_TUNE_RESIDENT 1 re-enables the
+// resident kernels).  A row shard cannot re-run alone (its RCCL partners
+// have moved on): it reports the loss instead, and its belief and values
+// stay unusable until pp2_belief_set / pp2_mdp_reset.
 int pp2rt::resident_settle(pp2_ctx* c) {
-  if (c->journal.kind == 0) return PP2_OK;
+  if (c->journal.empty()) return PP2_OK;
   DeviceGuard dg(c->device);
-  const int kind = c->journal.kind;
-  c->journal.kind = 0;
+  std::vector<pp2_ctx::ResidentJournal> q;
+  q.swap(c->journal);
   HIPCHK(hipEventSynchronize(c->res_done));
-  volatile unsigned* eh = c->res_host + 2;
-  if (*eh == 0u) return PP2_OK;
-  *eh = 0u;
+  volatile unsigned* eh = c->res_host + pp2_ctx::kResHostChain;
+  size_t bad = q.size();
+  for (size_t i = 0; i < q.size(); ++i) {
+    if (eh[i] != 0u && bad == q.size()) bad = i;
+    eh[i] = 0u;
+  }
+  if (bad == q.size()) return PP2_OK;
   ++c->res_fallbacks;
   resident_free(c);  // the failed run's epochs and counters are inconsistent
   c->resident = 0;
-  const auto& j = c->journal;
+  const auto& j = q[bad];
   c->bcur = j.bcur;
   c->jcur = j.jcur;
   c->kstep = j.kstep;
@@ -1027,15 +1042,33 @@ int pp2rt::resident_settle(pp2_ctx* c) {
     c->pending[i] = j.pending[i];
     c->pcount[i] = j.pcount[i];
   }
-  if (kind == 1) return loop_run_launches(c, j.n, j.us.data(), j.zs.data());
-  if (kind == 2) {
-    for (int i = 0; i < j.n; ++i) CHECK(mdp_sweep_once(c));
-    return PP2_OK;
+  for (size_t i = bad; i < q.size(); ++i) {
+    const auto& e = q[i];
+    if (e.kind == 1) {
+      CHECK(loop_run_launches(c, e.n, e.us.data(), e.zs.data()));
+    } else if (e.kind == 2) {
+      for (int k = 0; k < e.n; ++k) CHECK(mdp_sweep_once(c));
+    } else {
+      c->lost_belief = c->lost_values = true;
+      return set_err(PP2_EHIP, "resident shard run: a workgroup wait timed out (the GPU was "
+                     "shared with another process?); this shard's belief and values are lost -- "
+                     "set them again (pp2_belief_set, pp2_mdp_reset); the context now uses "
+                     "per-step launches");
+    }
   }
-  c->lost_belief = c->lost_values = true;
-  return set_err(PP2_EHIP, "resident shard run: a workgroup wait timed out (the GPU was shared "
-                 "with another process?); this shard's belief and values are lost -- set them "
-                 "again (pp2_belief_set, pp2_mdp_reset); the context now uses per-step launches");
+  return PP2_OK;
+}
+
+// Whether a resident loop run (kind 1) or sweeps (kind 2) can be enqueued
+// behind the unverified launches without touching the resident buffers
+// (no plan change, no allocation): the chained entry points' test.
+static bool resident_chainable(pp2_ctx* c, int kind) {
+  if (c->journal.empty() || (int)c->journal.size() >= pp2_ctx::kResidentChain || c->comm ||
+      c->group || !c->model_ready || !c->res_sync)
+    return false;
+  if (kind == 1)
+    return resident_model_ok(c) && resident_plan_for(c, 0) && c->res_ntiles == c->res_plan.ntiles;
+  return solve_plan_ok(c) && c->res_ntiles == c->sol_plan.ntiles;
 }
 
 // pp2_mdp_solve's driver (reset, then blocks of 100 sweeps until the
@@ -1118,7 +1151,6 @@ static void run_common(pp2_ctx* c, const pp2::ResidentPlan& p, pp2::ResidentRun&
   a.ntiles = p.ntiles;
   a.ring = c->res_ring;
   a.sync = c->res_sync;
-  a.err_host = c->res_host + 2;
   a.slot_use[0] = c->res_slot[0];
   a.slot_use[1] = c->res_slot[1];
   a.arrive_base = c->res_arrive;
@@ -1138,8 +1170,7 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
   std::unique_ptr<pp2::ResidentRun> run(new pp2::ResidentRun());
   pp2::ResidentRun& a = *run;
   for (int i = 0; i < n;) {
-    if (i > 0) {
-      // the next launch reads this one's outputs
+    if ((int)c->journal.size() >= pp2_ctx::kResidentChain) {
       CHECK(resident_settle(c));
       if (!resident_ready(c)) return loop_run_launches(c, n - i, us + i, zs + i);
     }
@@ -1171,7 +1202,7 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
     a.out_partials = c->pbuf[bc ^ 1];
     a.scale_out = nullptr;
     for (int k = 0; k < m; ++k) a.uz[k] = (uint8_t)(us[i + k] | (zs[i + k] << 4));
-    journal(c, 1, m, us + i, zs + i);
+    a.err_host = journal(c, 1, m, us + i, zs + i);
     CHECK(gated_launch(c, [&] { return pp2::launch_loop_resident(c->stream, p, a); }));
     ++c->res_launches;
     int arrivals = 0;
@@ -1192,6 +1223,13 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
 // pp2_mdp_sweep(n) on resident sweeps: n sweeps in one launch (no checks),
 // the J of the last sweep in J[jcur ^ 1], A of the last sweep.
 static int sweeps_resident(pp2_ctx* c, int n) {
+  if ((int)c->journal.size() >= pp2_ctx::kResidentChain) {
+    CHECK(resident_settle(c));
+    if (!solve_ready(c)) {
+      for (int i = 0; i < n; ++i) CHECK(mdp_sweep_once(c));
+      return PP2_OK;
+    }
+  }
   const pp2::ResidentPlan& p = c->sol_plan;
   pp2::SweepRun a{};
   a.g = c->g;
@@ -1205,7 +1243,6 @@ static int sweeps_resident(pp2_ctx* c, int n) {
   a.A = c->A;
   a.xch = sweep_xch(c);
   a.sync = c->res_sync;
-  a.err_host = c->res_host + 2;
   a.tile_max = c->res_tmax;
   a.res = c->res_out;
   a.slot_use[0] = c->res_slot[2];
@@ -1216,7 +1253,7 @@ static int sweeps_resident(pp2_ctx* c, int n) {
   a.max_blocks = 1;
   a.nsweeps = n;
   a.stall_tile = c->res_stall_tile;
-  journal(c, 2, n, nullptr, nullptr);
+  a.err_host = journal(c, 2, n, nullptr, nullptr);
   CHECK(gated_launch(c, [&] { return pp2::launch_sweep_resident(c->stream, p, a); }));
   ++c->sol_launches;
   count_slot_uses(c, 1, n);
@@ -1303,6 +1340,7 @@ int pp2rt::shard_rebase(pp2_ctx* c, int nranks, int rank, int r0, int r1) {
 // One resident launch of m <= e steps on the view extended by e rows (the
 // halo rows e deep and the global mass are in place).
 int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, const uint8_t* zs) {
+  if ((int)c->journal.size() >= pp2_ctx::kResidentChain) CHECK(resident_settle(c));
   if (m < 1 || m > e || !shard_resident_ready(c, e))
     return set_err(PP2_ESTATE, "shard resident plan lost");
   const pp2::ResidentPlan& p = c->res_plan;
@@ -1336,7 +1374,7 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
   a.out_partials = c->pbuf[bc ^ 1];
   a.scale_out = c->d_shift;
   for (int k = 0; k < m; ++k) a.uz[k] = (uint8_t)(us[k] | (zs[k] << 4));
-  journal(c, 3, m, nullptr, nullptr);
+  a.err_host = journal(c, 3, m, nullptr, nullptr);
   CHECK(gated_launch(c, [&] { return pp2::launch_loop_resident(c->stream, p, a); }));
   ++c->res_launches;
   int arrivals = 0;
@@ -1698,9 +1736,15 @@ int pp2_mdp_reset(pp2_ctx* c) {
 }
 
 int pp2_mdp_sweep(pp2_ctx* c, int n) {
-  CHECK(check_model(c));
+  if (!c) return set_err(PP2_EINVAL, "null context");
   if (n < 0) return set_err(PP2_EINVAL, "negative sweep count");
   DeviceGuard dg(c->device);
+  // resident sweeps queue behind unverified resident launches (resident_settle)
+  if (n >= 2 && resident_chainable(c, 2)) {
+    break_pipeline(c);
+    return sweeps_resident(c, n);
+  }
+  CHECK(check_model(c));
   if (n >= 2 && solve_ready(c)) {
     break_pipeline(c);  // the loop's deep halo rows of J are stale after sweeps
     return sweeps_resident(c, n);
@@ -1807,9 +1851,13 @@ static int agree_min(pp2_ctx* c, int* v) {
 }
 
 int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
-  CHECK(check_model(c));
+  if (!c) return set_err(PP2_EINVAL, "null context");
   if (n < 0 || (n > 0 && (!us || !zs))) return set_err(PP2_EINVAL, "bad trajectory");
   DeviceGuard dg(c->device);
+  // a resident run queues behind unverified resident launches (no host sync
+  // between back-to-back runs; resident_settle verifies them all)
+  if (n >= 2 && resident_chainable(c, 1)) return loop_resident(c, n, us, zs);
+  CHECK(check_model(c));
   if (c->group)
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
   if (n >= 2 && c->comm) {

@@ -292,6 +292,44 @@ def test_resident_timeout_reruns_from_intact_inputs(pp2, what):
         assert a.resident_status() == (1, True)
 
 
+def test_resident_chain_equals_single_steps(pp2):
+    """Back-to-back resident runs and sweeps queue behind each other without
+    a host sync (more calls than the 16-launch chain, so the queue is verified
+    and restarted mid-way) and give the per-step bits."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 512, 512, 5, 77)
+    with a, b:
+        us, zs, _ = S.synth_trajectory(grid, 120, seed=8)
+        for k in range(40):
+            for c in (a, b):
+                c.loop_run(us[3 * k:3 * k + 3], zs[3 * k:3 * k + 3])
+                if k % 7 == 6:
+                    c.mdp_sweep(4)
+        assert a.resident_launches()[0] == 40
+        assert a.resident_status() == (0, True)
+        _same(a, b, "after 40 chained runs")
+
+
+def test_resident_chain_timeout_reruns_every_queued_launch(pp2):
+    """A chain whose first launch times out: the launches queued behind it
+    see the sticky error word and store nothing, so the next readback re-runs
+    the failed launch and every later one from the failed launch's inputs."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 1024, 1024, 8, 57)
+    with a, b:
+        us, zs, _ = S.synth_trajectory(grid, 40, seed=13)
+        for c in (a, b):
+            c.loop_run(us[:10], zs[:10])
+        a.synchronize()
+        a.set_tuning(a.TUNE_RESIDENT_STALL, 100)
+        for c in (a, b):
+            c.loop_run(us[10:20], zs[10:20])  # times out ...
+            c.mdp_sweep(6)                    # ... these queue behind it
+            c.loop_run(us[20:40], zs[20:40])
+        _same(a, b, "after a timed-out chain")
+        assert a.resident_status() == (1, False)
+
+
 def test_two_resident_contexts_on_separate_streams(pp2):
     """Two contexts whose resident launches are queued on different streams
     at the same time: launches of one process run one at a time per device

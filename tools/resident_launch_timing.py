@@ -53,6 +53,27 @@ def main():
             print(f"n={n:5d}: enqueue {m(enq):7.1f} us  events {m(gpu):8.1f} us "
                   f"({m(gpu) / n:5.2f}/step)  wall {m(wall):8.1f} us ({m(wall) / n:5.2f}/step)",
                   flush=True)
+        # back-to-back calls (a controller issuing runs of n steps): K runs
+        # queued without a host sync between them (the resident chain), one
+        # event span and one host wall time over all of them
+        K = int(os.environ.get("PP2_CHAIN", "12"))
+        for n in [int(v) for v in os.environ.get("PP2_NS", "2,4,8,20,50,100,400,2000").split(",")]:
+            gpu, wall = [], []
+            for r in range(max(3, reps // 3)):
+                ctx.synchronize()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                e0.record(stream)
+                for k in range(K):
+                    ctx.loop_run(us[:n], zs[:n])
+                e1.record(stream)
+                stream.synchronize()
+                ctx.synchronize()
+                wall.append((time.perf_counter() - t0) * 1e6)
+                gpu.append(e0.elapsed_time(e1) * 1e3)
+            m = statistics.median
+            print(f"chained x{K} n={n:5d}: events {m(gpu) / (K * n):5.2f} us/step  "
+                  f"wall {m(wall) / (K * n):5.2f} us/step", flush=True)
         enq = []
         for r in range(reps):
             torch.cuda.synchronize()
