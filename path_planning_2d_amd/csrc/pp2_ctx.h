@@ -169,7 +169,6 @@ struct pp2_ctx {
   static constexpr int kResidentChain = 16;
   static constexpr int kResHostChain = 4;  // res_host index of launch 0's error word
   std::vector<ResidentJournal> journal;    // unverified launches, oldest first
-  hipEvent_t res_done = nullptr;   // recorded after every journalled launch
   int res_fallbacks = 0;           // launches re-run after a timeout (pp2_resident_status)
   int res_stall_tile = -1;         // PP2_TUNE_RESIDENT_STALL (tests)
   int res_cus = 0;                 // PP2_TUNE_RESIDENT_CUS: CUs the plans may use (0: all)

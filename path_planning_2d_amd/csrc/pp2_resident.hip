@@ -78,8 +78,8 @@ __device__ unsigned long long g_rtrace[16][64][4][4];
   g_rtrace[tile][t][wave == 0 ? 0 : wave == 5 ? 1 : wave == 9 ? 2 : 3][ph] =          \
       __builtin_amdgcn_s_memrealtime()
 // prologue / epilogue of every tile (wave 0): entry, tables staged, loop top,
-// outputs stored
-__device__ unsigned long long g_rtrace_pro[1024][4];
+// outputs stored; class planes built, tile loaded + published, mass reduced
+__device__ unsigned long long g_rtrace_pro[1024][8];
 #define PP2_RP(ph) \
   if (tile < 1024 && threadIdx.x == 0) g_rtrace_pro[tile][ph] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -93,6 +93,7 @@ typedef __amdgpu_buffer_rsrc_t Rsrc;
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 constexpr int kSc1 = 16;                              // buffer aux bit: sc1
 constexpr unsigned long long kSpinTicks = 25000000ull;  // 0.25 s at 100 MHz
+constexpr int kPrologueParts = 4096;  // pending partials reduced from registers
 
 __device__ __forceinline__ Rsrc make_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
@@ -430,7 +431,24 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
 
   // ---- prologue: dictionary, zero pads, codes, the tile's b / J into LDS
   // buffer 0, boundary rows into exchange slot 1 (as if step -1's output),
-  // then the neighbours' rows for step 0
+  // then the neighbours' rows for step 0.
+  // Step 0's input mass, when a block starts with the previous launch's
+  // partials pending: wave 0 issues all its loads of them first (<= 16 quads
+  // per lane at <= 4096 partials, the resident grids' most), so that they
+  // land while the tables stage; reduced below in wave_reduce_partials' order
+  const bool start0 = a.kstep0 % a.depth == 0;
+  const bool red0 = start0 && a.in_partials && wave == 0;
+  const bool red0_regs = red0 && a.in_n <= kPrologueParts;
+  f4a pq[kPrologueParts / 256];
+  if (red0_regs) {
+    const f4a* q = reinterpret_cast<const f4a*>(a.in_partials);
+    const int nq = a.in_n >> 2;
+#pragma unroll
+    for (int j = 0; j < kPrologueParts / 256; ++j) {
+      const int i = lane + 64 * j;
+      pq[j] = q[i < nq ? i : 0];
+    }
+  }
   stage_rows(a.rfact, kResTab, lds);
   stage_rows(a.rows, rows_floats(a.E, true), sTC);
   for (int i = threadIdx.x; i < 4 * (a.rt + 1); i += blockDim.x) {
@@ -480,6 +498,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
     *reinterpret_cast<uint32_t*>(sP + i * ps) = 0u;
     *reinterpret_cast<uint32_t*>(sP + i * ps + 4 + wp) = 0u;
   }
+  PP2_RP(4);
   if (prior_err != 0u) return;  // (uniform: before any global store)
   if (valid) {
     const long long off = (long long)y * wp + x0;
@@ -495,11 +514,21 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   // uses of exchange slots 0 / 1 so far (every tile counts every use, whether
   // or not its rows cross a tile edge)
   unsigned use[2] = {a.slot_use[0], a.slot_use[1] + 1u};
-  // step 0's input mass (a block start with the previous launch's partials
-  // still pending: wave 0 reduces them, k_sum_finalize's tree)
-  const bool start0 = a.kstep0 % a.depth == 0;
-  if (start0 && a.in_partials && wave == 0) {
-    const float S = wave_reduce_partials(a.in_partials, a.in_n);
+  PP2_RP(5);
+  // step 0's input mass (k_sum_finalize's tree: lane-strided quads in
+  // ascending order, then the butterfly)
+  if (red0) {
+    float S;
+    if (red0_regs) {
+      const int nq = a.in_n >> 2;
+      float sl = 0.0f;
+#pragma unroll
+      for (int j = 0; j < kPrologueParts / 256; ++j)
+        if (lane + 64 * j < nq) sl += ((pq[j][0] + pq[j][1]) + pq[j][2]) + pq[j][3];
+      S = wave_sum(sl);
+    } else {
+      S = wave_reduce_partials(a.in_partials, a.in_n);
+    }
     if (threadIdx.x == 0) {
       sS[0] = S;
       if (tile == 0 && a.in_sum_out) *a.in_sum_out = S;

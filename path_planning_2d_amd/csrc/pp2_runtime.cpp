@@ -828,8 +828,7 @@ static void resident_free(pp2_ctx* c) {
 }
 
 // The pinned words the kernels write ({sweeps, norm bits, error word}, then
-// the journalled launches' error words) and the completion event of the
-// journalled launches; kept across plan changes.
+// the journalled launches' error words); kept across plan changes.
 static bool resident_host_words(pp2_ctx* c) {
   if (!c->res_host) {
     const size_t b = (pp2_ctx::kResHostChain + pp2_ctx::kResidentChain) * sizeof(unsigned);
@@ -838,10 +837,6 @@ static bool resident_host_words(pp2_ctx* c) {
       return false;
     }
     std::memset(c->res_host, 0, b);
-  }
-  if (!c->res_done && hipEventCreateWithFlags(&c->res_done, hipEventDisableTiming) != hipSuccess) {
-    c->res_done = nullptr;
-    return false;
   }
   return true;
 }
@@ -944,15 +939,16 @@ static bool solve_plan_ok(pp2_ctx* c) {
 static bool solve_ready(pp2_ctx* c) { return solve_plan_ok(c) && resident_buffers(c, c->sol_plan); }
 
 // Resident launches of all contexts of this process on one device run one at
-// a time: each is ordered after the previous one (any stream) by an event, so
-// two contexts never hold part of the CUs each and wait for the rest.  (Work
-// of other processes can still delay tiles: the kernels' bounded waits and
-// resident_settle cover that.)
+// a time: a launch on another stream than the previous one is ordered after
+// everything queued so far on that stream (an event recorded there at this
+// point), so two contexts never hold part of the CUs each and wait for the
+// rest.  No event per launch: two per launch cost ~8 us of GPU time each
+// (profiles/r03/resident_launch_events.txt).  (Work of other processes can
+// still delay tiles: the kernels' bounded waits and resident_settle cover it.)
 struct ResidentGate {
   std::mutex m;
   hipEvent_t ev = nullptr;
-  hipStream_t last = nullptr;
-  bool any = false;
+  hipStream_t last = nullptr;  // stream of the last resident launch, null: none pending
 };
 static ResidentGate& resident_gate(int device) {
   static ResidentGate gates[64];
@@ -963,15 +959,25 @@ template <class F>
 static int gated_launch(pp2_ctx* c, F launch) {
   ResidentGate& g = resident_gate(c->device);
   std::lock_guard<std::mutex> lk(g.m);
-  if (!g.ev) HIPCHK(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming));
-  if (g.any && g.last != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, g.ev, 0));
+  if (g.last && g.last != c->stream) {
+    if (!g.ev) HIPCHK(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(g.ev, g.last));
+    HIPCHK(hipStreamWaitEvent(c->stream, g.ev, 0));
+  }
   HIPCHK(launch());
-  static const int ab = getenv("PP2_AB_EV") ? atoi(getenv("PP2_AB_EV")) : 0;  // TEMP A/B
-  if (!(ab & 1)) HIPCHK(hipEventRecord(g.ev, c->stream));
   g.last = c->stream;
-  g.any = true;
-  if (!(ab & 2)) HIPCHK(hipEventRecord(c->res_done, c->stream));
   return PP2_OK;
+}
+
+// A stream leaves the gate (the context is destroyed or moves to another
+// stream): drained first, so nothing queued on it needs ordering any more.
+static void resident_gate_forget(pp2_ctx* c, hipStream_t s) {
+  ResidentGate& g = resident_gate(c->device);
+  std::lock_guard<std::mutex> lk(g.m);
+  if (g.last == s) {
+    (void)hipStreamSynchronize(s);
+    g.last = nullptr;
+  }
 }
 
 // Exchange-slot uses of a launch: the prologue's publish into slot 1, then
@@ -1023,7 +1029,7 @@ int pp2rt::resident_settle(pp2_ctx* c) {
   DeviceGuard dg(c->device);
   std::vector<pp2_ctx::ResidentJournal> q;
   q.swap(c->journal);
-  HIPCHK(hipEventSynchronize(c->res_done));
+  HIPCHK(hipStreamSynchronize(c->stream));
   volatile unsigned* eh = c->res_host + pp2_ctx::kResHostChain;
   size_t bad = q.size();
   for (size_t i = 0; i < q.size(); ++i) {
@@ -1494,6 +1500,8 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   pbvi_free(c);
   if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+  resident_gate_forget(c, c->stream);
+  if (c->own_stream) resident_gate_forget(c, c->own_stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (hipEvent_t e : {c->ev_enter, c->ev_leave})
@@ -1512,7 +1520,6 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->code_alloc) (void)hipFree(c->code_alloc);
   resident_free(c);
   if (c->res_host) (void)hipHostFree(c->res_host);
-  if (c->res_done) (void)hipEventDestroy(c->res_done);
   if (c->d_shift) (void)hipFree(c->d_shift);
   if (c->d_vec) (void)hipFree(c->d_vec);
   for (float* p : {c->d_dict, c->d_rows, c->d_dl, c->d_tu, c->d_rfact})
@@ -1524,6 +1531,8 @@ int pp2_destroy(pp2_ctx* c) {
 
 int pp2_set_stream(pp2_ctx* c, void* s) {
   CHECK(check_ctx_settled(c));
+  DeviceGuard dg(c->device);
+  resident_gate_forget(c, c->stream);
   c->stream = s ? (hipStream_t)s : c->own_stream;
   return PP2_OK;
 }

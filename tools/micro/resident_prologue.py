@@ -11,6 +11,10 @@ os.environ["PP2_LIBRARY"] = os.path.join(HERE, "_rtrace", "libpp2_rtrace.so")
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 
+def ctx_kstep(ctx):
+    return "?"
+
+
 def main():
     import numpy as np
     import path_planning_2d_amd as P
@@ -30,11 +34,11 @@ def main():
         ctx.loop_run(us[:10], zs[:10])
         ctx.synchronize()
         nt = None
-        for n in (2, 20, 200):
+        for n in (2, 20, 20, 200):
             for rep in range(3):
                 ctx.loop_run(us[:n], zs[:n])
                 ctx.synchronize()
-            buf = np.zeros((1024, 4), np.uint64)
+            buf = np.zeros((1024, 8), np.uint64)
             assert fn(buf.ctypes.data) == 0
             b = buf.astype(np.int64)
             if nt is None:
@@ -42,9 +46,11 @@ def main():
             b = b[:nt]
             t0 = b[:, 0].min()
             x = (b - t0) / 100.0
-            print(f"n={n:4d} tiles {nt}: entry spread {x[:, 0].max():6.2f} us  staged {np.median(x[:, 1] - x[:, 0]):5.2f}"
-                  f"  ->loop {np.median(x[:, 2] - x[:, 1]):5.2f}  loop+store {np.median(x[:, 3] - x[:, 2]):8.2f}"
-                  f" ({np.median(x[:, 3] - x[:, 2]) / n:5.2f}/step)  last end {x[:, 3].max():8.2f} us", flush=True)
+            md = lambda v: np.median(v)  # noqa: E731
+            print(f"n={n:4d} kstep0 {ctx_kstep(ctx)} tiles {nt}: entry spread {x[:, 0].max():6.2f} us  staged {md(x[:, 1] - x[:, 0]):5.2f}"
+                  f"  planes {md(x[:, 4] - x[:, 1]):5.2f}  tile+publish {md(x[:, 5] - x[:, 4]):5.2f}"
+                  f"  mass+sync {md(x[:, 2] - x[:, 5]):5.2f}  loop+store {md(x[:, 3] - x[:, 2]):8.2f}"
+                  f" ({md(x[:, 3] - x[:, 2]) / n:5.2f}/step)  last end {x[:, 3].max():8.2f} us", flush=True)
 
 
 if __name__ == "__main__":
