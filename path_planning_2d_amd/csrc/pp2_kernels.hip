@@ -609,11 +609,143 @@ __global__ __launch_bounds__(kBlock, 4) void k_fib_sweep_sparse(
   }
 }
 
+// k_fib_sweep_sparse with the block's likelihood rows staged in LDS: a block
+// of 2 rows x 256 cells first copies L of rows y0-1 .. y0+2, columns
+// x0-1 .. x0+256, all 16 observations (66.5 KB) by LDS-DMA (buffer loads
+// straight into LDS, no VGPRs; offsets past the resource read +0.0, like
+// the sparse kernel's off-grid loads), so each neighbour likelihood comes
+// from L2 / HBM once per block instead of once per action that reaches it
+// (4 of 9 on average) and the (action, observation) loop reads LDS
+// (consecutive lanes, consecutive words) instead of issuing 464
+// vector-memory loads per cell.  The alpha loads go out before the staging
+// and overlap it; each action's T support and R are loaded one action ahead.
+// Same values, same arithmetic: the alphas are k_fib_sweep_sparse's bit for
+// bit.  2 blocks (16 waves) per CU.
+constexpr int kFibCols = 256, kFibRows = 2, kFibLs = kFibCols + 4;
+constexpr int kFibPlane = (kFibRows + 2) * kFibLs;  // observation plane stride in LDS
+typedef __attribute__((address_space(3))) void fib_lds_void;
+
+__global__ __launch_bounds__(kFibCols * kFibRows, 4) void k_fib_sweep_lds(
+    Geom g, float gamma, PlaneSet T, PlaneSet L, PlaneSet R, PlaneSet a_in,
+    PlaneSet a_out) {
+  __shared__ __attribute__((aligned(16))) float sL[16 * kFibPlane];
+  const int tx = threadIdx.x % kFibCols, ty = threadIdx.x / kFibCols;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int x0 = blockIdx.x * kFibCols, y0 = blockIdx.y * kFibRows;
+  const int x = x0 + tx, y = y0 + ty;
+  const bool cell = y < g.rows && x < g.wp;
+  const int xc = cell ? x : 0, yc = cell ? y : 0;  // (lanes past the grid compute cell (0, 0), unstored)
+  const int ars = (int)a_in.rs, aps = (int)a_in.ps;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(a_in.p - ars, 0, kOffRange, 0x00020000);
+  auto ldb = [](__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  };
+  // 1. the neighbours' alphas (registers for the whole kernel)
+  f2v lap[9][4];  // alpha_q of neighbour sp, q = 0..7 in pairs
+  float la8[9];   // alpha_8 of neighbour sp
+#pragma unroll
+  for (int sp = 0; sp < 9; ++sp) {
+    const int oy = sp / 3 - 1, nx = xc + sp % 3 - 1;
+    const bool ok = nx >= 0 && nx < g.wp;
+    const int vo = ok ? ((yc + oy + 1) * ars + nx) * 4 : kOffRange;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      lap[sp][p].x = ldb(ra, vo, (2 * p) * aps * 4);
+      lap[sp][p].y = ldb(ra, vo, (2 * p + 1) * aps * 4);
+    }
+    la8[sp] = ldb(ra, vo, 8 * aps * 4);
+  }
+  // 2. L rows by LDS-DMA: per (o, r) row five wave copies of 64 columns, at
+  //    c = 0, 64, 128, 192 and 194 (the last one covers c = 256, 257 and
+  //    rewrites 194 .. 255 with the same values); rows past `rows` (the halo
+  //    row) and columns outside [0, wp) read +0.0
+  {
+    const int lrs = (int)L.rs, lps = (int)L.ps;
+    const __amdgpu_buffer_rsrc_t rl =
+        __builtin_amdgcn_make_buffer_rsrc(L.p - lrs, 0, kOffRange, 0x00020000);
+    const int rows_in = min(kFibRows + 2, g.rows - y0 + 2);  // staged rows y0-1 .. rows (halo)
+    for (int i = wv; i < 16 * (kFibRows + 2) * 5; i += kFibCols * kFibRows / 64) {
+      const int row = i / 5, piece = i % 5;
+      const int o = row / (kFibRows + 2), r = row % (kFibRows + 2);
+      const int c = (piece < 4 ? 64 * piece : 194) + lane;
+      const int xx = x0 - 1 + c;
+      const bool ok = r < rows_in && xx >= 0 && xx < g.wp;
+      const int vo = ok ? ((y0 + r) * lrs + xx) * 4 : kOffRange;  // row y0-1+r at (y0+r) * lrs
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rl, (fib_lds_void*)&sL[o * kFibPlane + r * kFibLs + (piece < 4 ? 64 * piece : 194)], 4, vo,
+          o * lps * 4, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 3. per action: T of its support, loaded one action ahead (R at the
+  //    action's start: it is consumed after the observation loop)
+  auto load_t = [&](int a, float (&ts)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int sp = kSup[a][j];
+      ts[j] = j < kSupN[a] ? T.p[(long long)yc * T.rs + (long long)(9 * a + sp) * T.ps + xc] : 0.0f;
+    }
+  };
+  // the window's LDS base: row ty + oy + 1, column tx + ox + 1 of sL[o]
+  const float* wl = &sL[ty * kFibLs + tx];
+  float tsn[4];
+  load_t(0, tsn);
+#pragma unroll
+  for (int a = 0; a < 9; ++a) {
+    float ts[4] = {tsn[0], tsn[1], tsn[2], tsn[3]};
+    const float rv = R.p[(long long)yc * R.rs + (long long)a * R.ps + xc];
+    if (a + 1 < 9) load_t(a + 1, tsn);
+    int lo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int sp = kSup[a][j];
+      lo[j] = (sp / 3) * kFibLs + sp % 3;
+    }
+    float rtg = 0.0f;
+#pragma unroll 2
+    for (int o = 0; o < 16; ++o) {
+      const float* wo = wl + o * kFibPlane;
+      float tm[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tm[j] = j < kSupN[a] ? ts[j] * wo[lo[j]] : 0.0f;
+      f2v sq[4] = {f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}};
+      float sq8 = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j >= kSupN[a]) continue;
+        const f2v tj = {tm[j], tm[j]};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) sq[p] = __builtin_elementwise_fma(tj, lap[kSup[a][j]][p], sq[p]);
+        sq8 = __builtin_fmaf(tm[j], la8[kSup[a][j]], sq8);
+      }
+      float rtgo = fmaxf(fmaxf(-FLT_MAX, sq[0].x), sq[0].y);
+#pragma unroll
+      for (int p = 1; p < 4; ++p) rtgo = fmaxf(fmaxf(rtgo, sq[p].x), sq[p].y);
+      rtgo = fmaxf(rtgo, sq8);
+      rtg = rtg + rtgo;
+    }
+    if (cell) a_out.p[(long long)y * a_out.rs + (long long)a * a_out.ps + x] = __builtin_fmaf(gamma, rtg, rv);
+  }
+}
+
 hipError_t launch_fib_sweep(hipStream_t st, const Geom& g, float gamma,
                             PlaneSet T, PlaneSet L, PlaneSet R,
                             PlaneSet a_in, PlaneSet a_out, bool sparse) {
   const int grid = cells_grid(g, 1);
-  if (sparse)
+  // the staging kernel needs several blocks per CU to hide its per-block
+  // start (alpha loads + L staging); small grids keep the sparse kernel.
+  // PP2_FIB_LDS=1 / 0 forces one or the other (tests, A/B).
+  const long long lds_blocks = (long long)((g.wp + kFibCols - 1) / kFibCols) *
+                               ((g.rows + kFibRows - 1) / kFibRows);
+  const char* force = getenv("PP2_FIB_LDS");
+  const bool use_lds = force && *force ? *force == '1' : lds_blocks >= 1024;
+  if (sparse && use_lds)
+    hipLaunchKernelGGL(k_fib_sweep_lds, dim3((g.wp + kFibCols - 1) / kFibCols,
+                                             (g.rows + kFibRows - 1) / kFibRows),
+                       dim3(kFibCols * kFibRows), 0, st, g, gamma, T, L, R, a_in, a_out);
+  else if (sparse)
     hipLaunchKernelGGL(k_fib_sweep_sparse, dim3(grid), dim3(kBlock), 0, st, g, gamma, T, L, R,
                        a_in, a_out);
   else

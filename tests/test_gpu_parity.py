@@ -297,6 +297,26 @@ def test_loop_blocks_equal_across_paths(pp2):
             assert np.float32(ma) == np.float32(mb)
 
 
+@pytest.mark.parametrize("H,W,force", [(1024, 1024, ""), (1025, 700, ""), (301, 333, "1"),
+                                       (257, 1030, "1"), (1, 700, "1"), (256, 256, "0")])
+def test_fib_lds_equals_dense_geometries(pp2, monkeypatch, H, W, force):
+    """The likelihood-staging FIB kernel (2-row x 256-column blocks, L rows
+    y0-1 .. y0+2 in LDS; chosen from 1024 blocks up, PP2_FIB_LDS forces it)
+    on grids whose rows and widths do not fill its blocks, and the sparse
+    kernel it replaces: alphas equal the dense k_fib_sweep's bit for bit."""
+    from path_planning_2d_amd import synthetic as S
+    monkeypatch.setenv("PP2_FIB_LDS", force)
+    grid = S.synth_grid(H, W, seed=H + 3 * W)
+    goal = S.synth_goal(grid)
+    with make_ctx(pp2, grid, goal) as a, make_ctx(pp2, grid, goal) as b:
+        b.set_tuning(b.TUNE_CODED_MODEL, 0)
+        assert a.model_dict_info()[1], "sparse (LDS) FIB path not selected"
+        for c in (a, b):
+            c.fib_reset()
+            c.fib_sweep(3)
+        np.testing.assert_array_equal(a.fib_get(), b.fib_get())
+
+
 @pytest.mark.parametrize("name", ["map_10x10", "sparse_map_100x40", "tile64_sparse_map_100x40"])
 def test_fib_sparse_equals_dense(pp2, name):
     """k_fib_sweep_sparse (support-only terms, observation-outer loads) gives

@@ -11,6 +11,7 @@ the 8 XCDs, so GRBM_GUI_ACTIVE / 8 is the dispatch's wall clock in cycles.
     lds_busy  = SQ_LDS_IDX_ACTIVE / (CUs * wall)
 Usage: python tools/sq_summary.py <round dir, e.g. r03> <steps per launch>
        [kernel substring, default k_loop_resident] [pmc dir under gpurun_out]
+       [output name, default resident_sq.json]
 """
 import csv
 import json
@@ -53,8 +54,10 @@ def main():
         "wall_cycles_per_step": wall / steps,
         "valu_busy": 4.0 * c["SQ_ACTIVE_INST_VALU"] / (4 * CUS * wall),
         "lds_busy": c["SQ_LDS_IDX_ACTIVE"] / (CUS * wall),
-        "lds_bank_conflict_share": c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_LDS_IDX_ACTIVE"], 1.0),
-        "per_wave_per_step": {k: c[f"SQ_INSTS_{k}"] / waves / steps for k in ("VALU", "LDS", "SALU")},
+        "lds_bank_conflict_share": (c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_LDS_IDX_ACTIVE"], 1.0)
+                                    if "SQ_LDS_BANK_CONFLICT" in c else None),
+        "per_wave_per_step": {k: c[f"SQ_INSTS_{k}"] / waves / steps
+                              for k in ("VALU", "LDS", "SALU", "VMEM_RD") if f"SQ_INSTS_{k}" in c},
         "wave_time_split": {k: c[f"SQ_{k}"] / c["SQ_WAVE_CYCLES"]
                             for k in ("ACTIVE_INST_ANY", "WAIT_INST_ANY", "WAIT_ANY")},
         "formulas": {"valu_busy": "4*SQ_ACTIVE_INST_VALU / (4 SIMDs * 256 CUs * GRBM_GUI_ACTIVE/8)",
@@ -62,7 +65,8 @@ def main():
     }
     d = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(d, exist_ok=True)
-    json.dump(out, open(os.path.join(d, "resident_sq.json"), "w"), indent=1)
+    name = sys.argv[5] if len(sys.argv) > 5 else "resident_sq.json"
+    json.dump(out, open(os.path.join(d, name), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
