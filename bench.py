@@ -916,10 +916,13 @@ def main():
                 "algorithmic_bytes_per_launch": algo_launch,
                 "avg_launch_us": launch_s * 1e6,
                 "note": ("bytes the resident kernel must move per launch: code 2, b 4, J 4 in, "
-                         "b' 4, J' 4, A 1 out per cell; every intermediate step stays in LDS "
-                         "(the tiles' edge rows cross CUs through L2/MALL), so HBM is not the "
-                         "binding resource: LDS (roofline_lds) and VALU issue are, plus the "
-                         "per-step edge-row hand-off chain (DESIGN.md §3.2)"
+                         "b' 4, J' 4, A 1 out per cell; every intermediate step stays in LDS, so "
+                         "HBM is not the binding resource: the per-step edge-row hand-off chain "
+                         "is, with VALU and LDS about half busy (sq_counters, roofline_lds; "
+                         "DESIGN.md §3.2). `traffic` is the memory-side bytes (2*FETCH_SIZE + "
+                         "WRITE_SIZE) per launch: ~8.4 MB per step of them are the edge-row "
+                         "granules (2 x 8 KB per tile per step, sc1 stores and loads, which go "
+                         "past L2 to the memory side), not cell data"
                          if resident and coded else
                          "bytes the coded kernel must move per launch: code 2, b 4, b' 4, J 4, "
                          "J' 4, A 1 per cell (a pair launch keeps its intermediate step in "

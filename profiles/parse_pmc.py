@@ -10,6 +10,7 @@ a wide (16 B/lane) coalesced streaming read, so it is doubled; WRITE_SIZE is
 exact for 16-B-per-lane streaming stores.
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
 Usage: python profiles/parse_pmc.py <tag> [cells] [steps per resident launch]
+       [directory under gpurun_out (tools/collect_pmc.sh's PMC_DIR)]
 """
 import csv
 import json
@@ -20,7 +21,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 # algorithmic HBM bytes per cell (bench.py docstring / DESIGN.md)
-ALGO = {"k_mdp_sweep": 369, "k_belief_update": 48, "k_loop_step": 417,
+ALGO = {"k_mdp_sweep": 369, "k_belief_update": 48, "k_loop_step": 381,
         "k_loop_step_coded": 19, "k_mdp_sweep_coded": 11,
         "k_loop_pair_coded": 19,  # two steps per launch, intermediate in LDS
         "k_loop_resident": 19}  # the whole trajectory per launch, tiles in LDS
@@ -42,11 +43,12 @@ def main():
     tag = sys.argv[1]
     cells = int(sys.argv[2]) if len(sys.argv) > 2 else 1024 * 1024
     spl = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    src = os.path.join(OUT, sys.argv[4]) if len(sys.argv) > 4 else OUT
     stats = {}
-    for r in csv.DictReader(open(os.path.join(OUT, "prof", "run_kernel_stats.csv"))):
+    for r in csv.DictReader(open(os.path.join(src, "prof", "run_kernel_stats.csv"))):
         stats[short(r["Name"])] = r
-    fetch = counter(os.path.join(OUT, "pmc_fetch", "run_counter_collection.csv"))
-    write = counter(os.path.join(OUT, "pmc_write", "run_counter_collection.csv"))
+    fetch = counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
+    write = counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
     kernels = {}
     for k, r in stats.items():
         base = k.split("<")[0]

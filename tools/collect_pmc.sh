@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out
+OUT=gpurun_out/${PMC_DIR:-.}
 ARGS="--profile --steps ${STEPS:-20} --warmup ${WARMUP:-20} ${EXTRA:-}"
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py $ARGS > $OUT/prof.log 2>&1 &&
