@@ -159,20 +159,25 @@ __device__ __forceinline__ float pow2f(int k) { return __uint_as_float((uint32_t
 
 // wave_reduce_partials (pp2_device.h) with sc1 loads: the partials were
 // stored by other CUs inside this launch.  Same association, bit for bit.
+// kRedQ quads per lane in flight per round trip.
+#ifndef PP2_REDQ
+#define PP2_REDQ 8
+#endif
+constexpr int kRedQ = PP2_REDQ;
 __device__ __forceinline__ float wave_reduce_partials_sc1(const float* p, int n) {
   const Rsrc r = make_rsrc(p);
   const int lane = threadIdx.x & 63;
   const int nq = n >> 2;
   float s = 0.0f;
-  for (int base = lane; base < nq; base += 64 * 8) {
-    f4a w[8];
+  for (int base = lane; base < nq; base += 64 * kRedQ) {
+    f4a w[kRedQ];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kRedQ; ++j) {
       const int i = base + 64 * j;
       w[j] = ld4_sc1(r, 16 * (i < nq ? i : base));
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < kRedQ; ++j)
       if (base + 64 * j < nq) s += ((w[j][0] + w[j][1]) + w[j][2]) + w[j][3];
   }
   return wave_sum(s);
@@ -197,8 +202,7 @@ constexpr bool belief_row_used(int U, int oy) {
 }
 template <int U>
 __device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0, uint32_t lx4,
-                                            int z, float inv, const Win6& win, float (&p)[4],
-                                            float& local) {
+                                            int z, const Win6& win, float (&p)[4]) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const char* qr = reinterpret_cast<const char*>(lds + kResQR) + U * kFactK * 16;
   const char* lt = reinterpret_cast<const char*>(lds + kResLT) + z * (kResLK * 4);
@@ -233,20 +237,18 @@ __device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0,
       p[k] = __builtin_fmaf(*reinterpret_cast<const float*>(qr + 4 * sl + cb[oy][k + 1 + ox]),
                             win.v[oy][k + 1 + ox], p[k]);
   }
-  local = 0.0f;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 4; ++k)
     p[k] = p[k] * *reinterpret_cast<const float*>(lt + __builtin_amdgcn_ubfe(lx4, 8 * k, 8));
-    p[k] = p[k] * inv;
-    local += p[k];
-  }
 }
 
 // sP: the tile's class planes [9][rt + 2][ps] (ps = wp + 8 bytes: 4 pad
 // bytes on each side); this lane's rows start at plane row ty.
+// p = the gathered quad times L_z (the block-start scale and the mass
+// partial are applied by the caller)
 __device__ __forceinline__ void belief_any(int u, const uint8_t* sP, int prows, int ps, int ty,
-                                           int x0, uint32_t lx4, int z, float inv, const Win6& w,
-                                           float (&p)[4], float& local) {
+                                           int x0, uint32_t lx4, int z, const Win6& w,
+                                           float (&p)[4]) {
   // The plane rows of action u, from the step's u through an opaque (not
   // volatile) asm: otherwise the compiler specialises the address per case
   // and hoists the 9 actions x 3 rows of plane addresses out of the step loop
@@ -257,10 +259,10 @@ __device__ __forceinline__ void belief_any(int u, const uint8_t* sP, int prows, 
   switch (u) {
 #define PP2_BQ(UU)                                                     \
   case UU:                                                             \
-    belief_fact<UU>(pu, ps, x0, lx4, z, inv, w, p, local); \
+    belief_fact<UU>(pu, ps, x0, lx4, z, w, p); \
     break;
     PP2_BQ(0) PP2_BQ(1) PP2_BQ(2) PP2_BQ(3) PP2_BQ(4) PP2_BQ(5) PP2_BQ(6) PP2_BQ(7)
-    default: belief_fact<8>(pu, ps, x0, lx4, z, inv, w, p, local);
+    default: belief_fact<8>(pu, ps, x0, lx4, z, w, p);
 #undef PP2_BQ
   }
 }
@@ -551,34 +553,19 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
     const int u = a.uz[t] & 15, z = a.uz[t] >> 4;
     const int ci = t & 1, co = ci ^ 1;
     const bool last = t == a.n - 1;
-    // ---- a block start inside the run: the exact mass of step t-1's belief
-    // (a shard: the mass of its whole view -- every cell is <= it, so the
-    // power-of-two scale cannot overflow a halo row that holds more mass than
-    // the owned ones)
-    if (t > 0 && (a.kstep0 + t) % a.depth != 0) {
-      inv = 1.0f;
-    } else if (t > 0) {
-      if (wave == 0) {
-        arrivals += a.ntiles;
-        wave_wait(a.sync + kResidentSyncArrive, 1, arrivals, err, a.err_host);
-        const float S = wave_reduce_partials_sc1(
-            a.ring + (size_t)((t - 1) % kResidentRing) * a.nparts, a.nparts);
-        if (threadIdx.x == 0) sS[0] = S;
-      }
-      __syncthreads();
-      if (a.shard) {
-        const int sh = pow2_shift(sS[0]);
-        shift += sh;
-        inv = pow2f(sh);
-      } else {
-        inv = (1.0f / sS[0]) * a.bscale;
-      }
-    }
+    // ---- a block start inside the run needs the exact mass of step t-1's
+    // belief (a shard: the mass of its whole view -- every cell is <= it, so
+    // the power-of-two scale cannot overflow a halo row that holds more mass
+    // than the owned ones).  The step's gather and backup go first: the mass
+    // only scales the gathered quad, so the grid-wide arrival wait overlaps
+    // this tile's compute instead of preceding it.
+    const bool bs = t > 0 && (a.kstep0 + t) % a.depth == 0;
+    if (t > 0 && !bs) inv = 1.0f;
     PP2_RT(0);
     local = 0.0f;
     const bool bnd = nb_up || nb_dn;
     // one quad of step t: window rows from LDS (step t-1), the neighbour rows
-    // of step t-1, or 0 off the grid
+    // of step t-1, or 0 off the grid; b' before the scale in p
     auto step_quad = [&]() {
       Win6 wb, wj;
       if (ty > 0) {
@@ -602,7 +589,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
         row_zero(wj.v[2]);
       }
       PP2_RT(1);
-      belief_any(u, sP, prows, ps, ty, x0, lx4, z, inv, wb, p, local);
+      belief_any(u, sP, prows, ps, ty, x0, lx4, z, wb, p);
       float jn[9][4];
 #pragma unroll
       for (int i = 0; i < 9; ++i)
@@ -610,21 +597,48 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
         for (int k = 0; k < 4; ++k) jn[i][k] = wj.v[i / 3][k + i % 3];
       if (last) coded_sweep_iw<4, true>(sTC, iwr, jn, best, arg);  // actions: last step only
       else coded_sweep_iw<4, false>(sTC, iwr, jn, best, arg);
-      *reinterpret_cast<f4a*>(sbuf(0, co) + ty * xs + x0) = f4a{p[0], p[1], p[2], p[3]};
       *reinterpret_cast<f4a*>(sbuf(1, co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
     };
-    if (valid) {
-      // the boundary waves take the neighbours' step t-1 rows (published at
-      // the end of their step t-1), compute with issue priority and publish
-      // -- the neighbours' next inputs
-      if (bnd) __builtin_amdgcn_s_setprio(2);  // 6.0 vs 7.4 us/step at 1024^2 without
-      step_quad();
+    // the scale, the mass partial, b' into LDS and the boundary rows out --
+    // the neighbours' next inputs
+    auto finish_quad = [&]() {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        p[k] = p[k] * inv;
+        local += p[k];
+      }
+      *reinterpret_cast<f4a*>(sbuf(0, co) + ty * xs + x0) = f4a{p[0], p[1], p[2], p[3]};
       if (bnd) {
         if (!last) publish(ci, p, best, (use[ci] + 1u) & 1u);
         __builtin_amdgcn_s_setprio(0);
       }
-      PP2_RT(2);
+    };
+    if (valid) {
+      // the boundary waves take the neighbours' step t-1 rows (published at
+      // the end of their step t-1) and compute with issue priority
+      if (bnd) __builtin_amdgcn_s_setprio(2);  // 6.0 vs 7.4 us/step at 1024^2 without
+      step_quad();
+      if (!bs) finish_quad();
     }
+    if (bs) {
+      if (wave == 0) {
+        arrivals += a.ntiles;
+        wave_wait(a.sync + kResidentSyncArrive, 1, arrivals, err, a.err_host);
+        const float S = wave_reduce_partials_sc1(
+            a.ring + (size_t)((t - 1) % kResidentRing) * a.nparts, a.nparts);
+        if (threadIdx.x == 0) sS[0] = S;
+      }
+      __syncthreads();
+      if (a.shard) {
+        const int sh = pow2_shift(sS[0]);
+        shift += sh;
+        inv = pow2f(sh);
+      } else {
+        inv = (1.0f / sS[0]) * a.bscale;
+      }
+      if (valid) finish_quad();
+    }
+    PP2_RT(2);
     if (last) break;  // the last step's outputs are stored after the loop
     ++use[ci];
     // ---- mass partials of step t (dense map), sc1 into the ring
