@@ -214,39 +214,58 @@ __global__ __launch_bounds__(64) void k_lane_chains(const float* __restrict__ A,
     const float* pb = &ring[c % kLaneSlots][rb_][0];
     const int m = min(kLaneCH, n - c * kLaneCH);
     if (m == kLaneCH) {
-      // groups of 8 elements, reads issued two groups ahead of the dependent
-      // adds (12 LDS reads in flight at most: lgkmcnt counts to 15)
+      // groups of 8 elements, their LDS reads (inline asm) issued LA groups
+      // ahead of the dependent adds, each group waited for with a counted
+      // lgkmcnt that leaves the younger groups' reads in flight (the
+      // compiler's own waits drain to lgkmcnt(0) every few groups: a full
+      // LDS round trip per 24 adds); the empty asm pins the adds below it
       constexpr int G = 8, NG = kLaneCH / G;
-      f4 ga[3][2], gb[3][2];
+      constexpr int R = MODE == CH_DOT ? 4 : 2;  // b128 reads per group
+      constexpr int LA = 3, NB = LA + 1;          // lookahead (LA * R <= 15), register groups
+      f4 ga[NB][2], gb[NB][2];
+      const uint32_t la = (uint32_t)(uintptr_t)pa, lb = (uint32_t)(uintptr_t)pb;
       auto rd = [&](int g) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          ga[g % 3][q] = *(const f4*)(pa + G * g + 4 * q);
-          if (MODE == CH_DOT) gb[g % 3][q] = *(const f4*)(pb + G * g + 4 * q);
+          asm volatile("ds_read_b128 %0, %1" : "=v"(ga[g % NB][q]) : "v"(la + 4u * (G * g + 4 * q)));
+          if (MODE == CH_DOT)
+            asm volatile("ds_read_b128 %0, %1" : "=v"(gb[g % NB][q]) : "v"(lb + 4u * (G * g + 4 * q)));
         }
       };
-      rd(0);
-      rd(1);
+#pragma unroll
+      for (int g = 0; g < LA; ++g) rd(g);
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
-        if (g + 2 < NG) rd(g + 2);
-        __builtin_amdgcn_sched_barrier(0);
+        if (g + LA < NG) {
+          rd(g + LA);
+          asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(LA * R) : "memory");
+        } else if (g + 2 < NG) {
+          asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(2 * R) : "memory");
+        } else if (g + 1 < NG) {
+          asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(R) : "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          asm volatile("" : "+v"(ga[g % NB][q]));
+          if (MODE == CH_DOT) asm volatile("" : "+v"(gb[g % NB][q]));
+        }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           if (MODE == CH_DOT) {
-            const f4 pr = ga[g % 3][q] * gb[g % 3][q];  // the products, then the chain
+            const f4 pr = ga[g % NB][q] * gb[g % NB][q];  // the products, then the chain
             acc = acc + pr.x;
             acc = acc + pr.y;
             acc = acc + pr.z;
             acc = acc + pr.w;
           } else {
-            acc = acc + ga[g % 3][q].x;
-            acc = acc + ga[g % 3][q].y;
-            acc = acc + ga[g % 3][q].z;
-            acc = acc + ga[g % 3][q].w;
+            acc = acc + ga[g % NB][q].x;
+            acc = acc + ga[g % NB][q].y;
+            acc = acc + ga[g % NB][q].z;
+            acc = acc + ga[g % NB][q].w;
           }
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
     } else {
       for (int j = 0; j < m; ++j) acc = MODE == CH_DOT ? acc + pa[j] * pb[j] : acc + pa[j];
