@@ -11,10 +11,16 @@ resident in HBM before the timed region.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size 1024] [--grid G]
 
 For N > 1 launch with torch.distributed.run.  Default (weak scaling): rank r
-owns rows [r*S, (r+1)*S) of an (N*S) x S grid.  --grid G (strong scaling):
-one fixed G x G grid, rows split as evenly as possible over the N ranks.
-Every 8 steps a rank exchanges 8 halo rows of belief and values with its
-neighbours and all-reduces the belief mass over RCCL.
+owns rows [r*R, (r+1)*R) of an (N*R) x S grid, S = --size = 1024 and R =
+--shard-rows = 896: a rank's view (its rows plus e = 64 halo rows per side)
+is then 1024 x 1024, one 4-row tile per CU, so every rank runs the
+tile-resident loop; per-GPU work is fixed for N >= 2 (7/8 of
+N = 1's grid).  Each resident launch of up to e steps follows one RCCL
+exchange of e halo rows of belief and values and a {mass, shift} all-reduce
+(768 / 896 / 960 rows measured 0.61-0.67 / 0.63-0.74 / 0.56-0.71 projected
+efficiency, tools/weak_shard_rows.py).  --grid G
+(strong scaling): one fixed G x G grid, rows split as evenly as possible over
+the N ranks.
 
 Every run also reports `config4` (BASELINE.json configs[3]): the 2048 x 2048
 grid row-sharded over all N ranks (strong scaling), its cells/s, the same
@@ -23,11 +29,10 @@ the sharded J / A gathered to rank 0 equal the unsharded run bit for bit and
 the belief agrees to rel 1e-5.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant (and only)
-kernel of a step, timed live with HIP events around the timed steps on the
-stream it runs on: k_loop_pair_coded (default at 1024^2: two steps per
-launch, the first over the tile plus a one-row halo kept in LDS) or
-k_loop_step_coded (one step per launch) on the dictionary-coded model
-(DESIGN.md §2.1).  Its algorithmic bytes are the ones the kernel must move
+kernel, timed live with HIP events on the stream it runs on: at 1024^2 the
+tile-resident k_loop_resident (the whole timed trajectory in one launch,
+DESIGN.md §3.2) on the dictionary-coded model; with
+PP2_TUNE_RESIDENT 0 the launch-per-pair k_loop_pair_coded.  Its algorithmic bytes are the ones the kernel must move
 per cell and launch: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1 = 19 B (the
 intermediate step of a pair stays in LDS); `traffic` is the PMC-measured HBM
 bytes per launch from profiles/pmc_*.json.  `contract_equivalent` states the
@@ -76,6 +81,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, default=1024, help="grid side per GPU (weak scaling)")
+    ap.add_argument("--shard-rows", type=int, default=896,
+                    help="owned rows per GPU at N > 1 (weak scaling; the view adds 2 x e "
+                         "halo rows, e = (1024 - rows) / 2)")
     ap.add_argument("--grid", type=int, default=0,
                     help="strong scaling: one G x G grid row-sharded over the ranks")
     ap.add_argument("--c4-size", type=int, default=2048,
@@ -619,6 +627,57 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
                         "a projection, not a measurement (one GPU)"}}
 
 
+def weak_rank_share(args, local, stream, n1_cells_per_s):
+    """The weak-scaling line's per-rank work at N >= 2, measured on this GPU:
+    rank 1's shard (rows [R, 2R) of a 2R x S grid, R = --shard-rows) as an
+    RCCL shard with a 1-rank communicator, so pp2_loop_run takes the resident
+    shard path exactly as a rank of the N-GPU job does, with every RCCL call
+    a 1-rank no-op.  Projection as in config4: + the call's RCCL rounds at an
+    ASSUMED xGMI round trip; the implied weak-scaling efficiency is the
+    projected per-rank cells/s over N = 1's."""
+    import torch
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    W, R = args.size, args.shard_rows
+    grid = S.synth_grid(2 * R, W, seed=2 * R)
+    goal = S.synth_goal(grid)
+    w, k = args.warmup, args.steps
+    us, zs, _ = S.synth_trajectory(grid, w + k, seed=42)
+    b0 = S.uniform_belief(grid)
+    ctx = P.GridContext(grid, goal, gamma=GAMMA, device=local, rows=(R, 2 * R))
+    ctx.set_stream(stream.cuda_stream)
+    ctx.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
+    ctx.model_generate()
+    ctx.belief_set(b0[R * W:2 * R * W])
+    ctx.mdp_reset()
+    ctx.synchronize()
+    e = ctx.loop_steps_per_launch()
+    ctx.loop_run(us[:w], zs[:w])
+    torch.cuda.synchronize()
+    l0 = ctx.resident_launches()[0]
+    t0 = time.perf_counter()
+    ctx.loop_run(us[w:], zs[w:])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    launches = ctx.resident_launches()[0] - l0
+    ctx.close()
+    t = 1e6 * el / k
+    rounds = 2 * (-(-k // e)) + 1
+    proj = [t + rounds * r / k for r in RCCL_ROUND_US]
+    return {"shard": f"rows [{R}, {2 * R}) x {W} of a {2 * R}x{W} grid (rank 1 of 2), 1-rank "
+                     f"RCCL communicator",
+            "steps_per_launch": e, "resident_launches_in_run": launches,
+            "measured_us_per_step": t,
+            "measured_cells_per_s_per_rank": R * W / (t * 1e-6),
+            "projection": {
+                "assumed_rccl_round_us": list(RCCL_ROUND_US),
+                "rccl_rounds_per_call": rounds,
+                "us_per_step": proj,
+                "weak_efficiency_vs_n1": [R * W / (p * 1e-6) / n1_cells_per_s for p in proj[::-1]],
+                "note": "measured per-rank step + rounds x assumed RCCL round trip / steps; "
+                        "a projection, not a measurement (one GPU)"}}
+
+
 def sq_counters():
     """LDS / VALU busy fractions of k_loop_resident from the newest committed
     SQ-counter summary (profiles/r*/resident_sq.json, tools/collect_lds_pmc.sh
@@ -665,8 +724,9 @@ def main():
         r0, r1 = rank * gh // ws, (rank + 1) * gh // ws
     else:
         N = args.size
-        gh, gw = N * ws, N
-        r0, r1 = rank * N, (rank + 1) * N
+        R = N if ws == 1 else args.shard_rows
+        gh, gw = R * ws, N
+        r0, r1 = rank * R, (rank + 1) * R
     grid = S.synth_grid(gh, gw, seed=gh)
     goal = S.synth_goal(grid)
     total = args.warmup + args.steps
@@ -857,6 +917,9 @@ def main():
     pbvi = None
     if rank == 0 and ws == 1 and not args.no_pbvi:
         pbvi = pbvi_bench(args, local, stream.cuda_stream, with_cpu=not args.no_cpu_baseline)
+    weak = None
+    if rank == 0 and ws == 1 and not strong and args.shard_rows > 0:
+        weak = weak_rank_share(args, local, stream, value)
     rollout = None
     if rank == 0 and ws == 1 and args.rollout_copies > 0:
         rollout = rollout_bench(args, local, stream)
@@ -881,12 +944,15 @@ def main():
             "config": {
                 "workload": (f"{gh}x{gw} grid row-sharded over {ws} GPU(s): 1 belief update + "
                              f"1 MDP Bellman sweep per step" if strong else
-                             f"{args.size}x{args.size} cells per GPU: 1 belief update + 1 MDP "
-                             f"Bellman sweep per step (BASELINE.json configs[2] grid)"),
+                             f"{r1 - r0}x{args.size} cells per GPU: 1 belief update + 1 MDP "
+                             f"Bellman sweep per step (BASELINE.json configs[2] grid"
+                             + (")" if ws == 1 else f"; {r1 - r0}-row shards so that each "
+                                f"rank's view with its halo rows is one tile per CU)")),
                 "grid": [gh, gw],
                 "rows_per_gpu": r1 - r0,
-                "parallelism": (f"row-shard x{ws}: 8-row RCCL halo exchange and one "
-                                f"1-float mass all-reduce every 8 steps"
+                "parallelism": (f"row-shard x{ws}: tile-resident launches of up to e steps, "
+                                f"each after one RCCL exchange of e halo rows and a "
+                                f"{{mass, shift}} all-reduce (e = {(args.size - (r1 - r0)) // 2})"
                                 if ws > 1 else "single GPU"),
                 "cells_per_lane": args.cpt,
                 "model": (f"dictionary-coded ({dict_entries} entries, uint16 code per cell)"
@@ -947,6 +1013,7 @@ def main():
                 "bytes_per_cell": lds_bytes} if coded else None),
             "dense_path": dense,
             "config4": c4,
+            "weak_rank_share": weak,
             "kernels": {
                 "mdp_sweep_kernel": (("k_sweep_resident (all the timed sweeps in one launch; "
                                       "gbs/frac count its 11 B/cell once per launch)")
