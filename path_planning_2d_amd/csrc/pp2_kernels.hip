@@ -720,7 +720,10 @@ __global__ __launch_bounds__(kFibCols * kFibRows, 4) void k_fib_sweep_lds(
         for (int p = 0; p < 4; ++p) sq[p] = __builtin_elementwise_fma(tj, lap[kSup[a][j]][p], sq[p]);
         sq8 = __builtin_fmaf(tm[j], la8[kSup[a][j]], sq8);
       }
-      float rtgo = fmaxf(fmaxf(-FLT_MAX, sq[0].x), sq[0].y);
+      // (no -FLT_MAX seed: the chains are finite -- finite alphas, finite
+      // T * L -- so the max of the nine equals the reference's scan from
+      // -FLT_MAX with strict <)
+      float rtgo = fmaxf(sq[0].x, sq[0].y);
 #pragma unroll
       for (int p = 1; p < 4; ++p) rtgo = fmaxf(fmaxf(rtgo, sq[p].x), sq[p].y);
       rtgo = fmaxf(rtgo, sq8);

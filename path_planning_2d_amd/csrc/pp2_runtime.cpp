@@ -571,9 +571,12 @@ int mdp_sweep_once(pp2_ctx* c) {
 
 int fib_sweep_once(pp2_ctx* c) {
   const int fn = c->fcur ^ 1;
+  // the support-only kernels drop fmaf(0 * L, alpha, s) terms, which equal s
+  // only for finite alphas (uploaded alphas may not be)
   HIPCHK(pp2::launch_fib_sweep(c->stream, c->g, c->gamma, c->T.v, c->L.v, c->R.v,
                                c->fib[c->fcur].v, c->fib[fn].v,
-                               c->use_coded && c->dict_n > 0 && c->dict_sparse));
+                               c->use_coded && c->dict_n > 0 && c->dict_sparse &&
+                                   c->fib_finite));
   c->fcur = fn;
   ++c->fib_version;
   return PP2_OK;
@@ -1890,6 +1893,7 @@ int pp2_fib_reset(pp2_ctx* c) {
   for (Planes* P : {&c->fib[0], &c->fib[1], &c->fibsnap})
     HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
   c->fcur = 0;
+  c->fib_finite = true;
   ++c->fib_version;
   return PP2_OK;
 }
@@ -1934,6 +1938,10 @@ int pp2_fib_set(pp2_ctx* c, const float* alphas) {
   if (!alphas) return set_err(PP2_EINVAL, "alphas is null");
   DeviceGuard dg(c->device);
   ++c->fib_version;
+  const size_t n = owned_cells(c) * 9;
+  c->fib_finite = true;
+  for (size_t i = 0; i < n && c->fib_finite; ++i)
+    if (!std::isfinite(alphas[i])) c->fib_finite = false;
   return upload_planes(c, c->fib[c->fcur], alphas);
 }
 

@@ -317,6 +317,26 @@ def test_fib_lds_equals_dense_geometries(pp2, monkeypatch, H, W, force):
         np.testing.assert_array_equal(a.fib_get(), b.fib_get())
 
 
+def test_fib_nonfinite_alphas_take_full_sums(pp2):
+    """Uploaded alphas with an infinity: the support-only kernels' dropped
+    terms are fmaf(0 * L, alpha, s), which is NaN, not s, for alpha = inf --
+    the context then sweeps with the full 9-term sums, so it still equals
+    the dense kernel bit for bit (NaNs included)."""
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(64, 64, seed=7)
+    goal = S.synth_goal(grid)
+    with make_ctx(pp2, grid, goal) as a, make_ctx(pp2, grid, goal) as b:
+        b.set_tuning(b.TUNE_CODED_MODEL, 0)
+        a.fib_reset()
+        a.fib_sweep(5)
+        al = a.fib_get()
+        al.reshape(-1)[1000] = -np.inf
+        for c in (a, b):
+            c.fib_set(al)
+            c.fib_sweep(2)
+        np.testing.assert_array_equal(a.fib_get().view(np.uint32), b.fib_get().view(np.uint32))
+
+
 @pytest.mark.parametrize("name", ["map_10x10", "sparse_map_100x40", "tile64_sparse_map_100x40"])
 def test_fib_sparse_equals_dense(pp2, name):
     """k_fib_sweep_sparse (support-only terms, observation-outer loads) gives
