@@ -771,6 +771,11 @@ def main():
     # ---------------------------------------------------------------- timed
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    # torch creates an event's HIP event at its first record (~20 us of host
+    # time): create both before the timed region
+    ev0.record(stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
     ctx.loop_run(us[args.warmup:total], zs[args.warmup:total])
