@@ -143,7 +143,12 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           launches before reading anything (same bits; the
  *                           context then stays on them: pp2_resident_status).
  *                           Consequence: a call after a resident launch
- *                           first waits for that launch to finish. */
+ *                           first waits for that launch to finish -- except
+ *                           pp2_loop_run and pp2_mdp_sweep(n >= 2) taking
+ *                           the resident path again, which queue behind up
+ *                           to 16 unverified launches without a host sync
+ *                           (a launch queued behind one that timed out does
+ *                           nothing, and all of them are re-run). */
 #define PP2_TUNE_RESIDENT 8
 /*  PP2_TUNE_RESIDENT_HALO   row shards: the loop runs on the resident kernel
  *                           when a view of the owned rows plus e halo rows
