@@ -64,6 +64,8 @@ MFMA_F32_PEAK_TFLOPS = 157.3     # dense f32-input MFMA peak (MI355X_MICROARCH.m
 BYTES_SWEEP = 369                # per cell: T 324 + C 36 + J 4 + J' 4 + A 1
 BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
 BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF   # SURVEY.md §8(d) contract (T counted twice)
+FIB_FLOP_CELL = 25920           # reference full-sum flops per cell and FIB sweep (~25.9 k)
+F32_VALU_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: f32 vector (v_pk_fma_f32) peak
 BYTES_LOOP_DENSE = 381           # k_loop_step: T 324 read ONCE for gather and sweep + C 36 + L_z 4 + b 4 + b' 4 + J 4 + J' 4 + A 1
 BYTES_LOOP_CODED = 19            # per cell: code 2 + b 4 + b' 4 + J 4 + J' 4 + A 1
 BYTES_SWEEP_CODED = 11           # per cell: code 2 + J 4 + J' 4 + A 1
@@ -846,6 +848,22 @@ def main():
         pairs_ms = timed(loop_reps)
         ctx.set_tuning(ctx.TUNE_RESIDENT, 1)
     belief_ms = timed(lambda: [ctx.belief_update(int(us[k]), int(zs[k])) for k in range(reps)])
+    # row a5: the FIB sweep on the same grid (VALU-bound: SURVEY.md §8(d)
+    # prices it on the reference's full-sum flops against the f32 VALU peak)
+    fib = None
+    if rank == 0 and ws == 1:
+        ctx.fib_reset()
+        ctx.fib_sweep(3)
+        fib_ms = timed(lambda: ctx.fib_sweep(reps))
+        fib = {"kernel": ("k_fib_sweep_lds" if coded and cells_per_gpu >= 512 * 1024
+                          else "k_fib_sweep_sparse" if coded else "k_fib_sweep"),
+               "us_per_sweep": fib_ms * 1e3,
+               "full_sum_tflops": FIB_FLOP_CELL * cells_per_gpu / (fib_ms * 1e-3) / 1e12,
+               "frac_of_f32_valu_peak": FIB_FLOP_CELL * cells_per_gpu / (fib_ms * 1e-3) / 1e12
+               / F32_VALU_PEAK_TFLOPS,
+               "note": "flops of the reference's full 9-term sums (SURVEY.md §8(d), ~25.9 "
+                       "kflop/cell); the kernel executes the support terms only (~11.5 k), "
+                       "bit-identical"}
     dense = None
     if coded:
         ctx.set_tuning(ctx.TUNE_CODED_MODEL, 0)
@@ -1036,6 +1054,7 @@ def main():
                 "loop_gbs": loop_gbs,
                 "loop_frac": loop_gbs / HBM_PEAK_GBS,
             },
+            "fib_sweep": fib,
             "belief_mass_ok": mass_ok,
             "mdp_solve": mdp_solve,
             "plan_step": plan,
