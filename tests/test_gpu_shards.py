@@ -338,6 +338,46 @@ def test_shard_group_resident_blocks(bounds, halo):
     assert e == (halo or 128)
 
 
+def test_shard_group_resident_weak_scaling_shards():
+    """The bench's weak-scaling decomposition at N >= 2: 896-row shards of a
+    1024-wide grid, whose views with e = 64 halo rows per side are 1024 rows
+    (one 4-row tile per CU), resident in the shard group; J/A bit-exact and
+    beliefs rel 1e-5 against the unsharded grid."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(1792, 1024, 1792)
+    goal = S.synth_goal(grid)
+    _resident_shard_run(P, grid, goal, [0, 896, 1792], [(0, 70), (70, 200)])
+
+
+def test_rccl_single_rank_resident_896x1024():
+    """The RCCL path of an 896 x 1024 shard (the weak-scaling bench's rank
+    share) with a 1-rank communicator: e = 64, so 200 steps take 4 launches,
+    and the shard equals the unsharded grid."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(896, 1024, 896)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 200, seed=9)
+    b0 = S.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            P.GridContext(grid, goal, gamma=float(GAMMA), rows=(0, 896)) as sh:
+        sh.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
+        for c in (ref, sh):
+            c.model_generate()
+            c.belief_set(b0)
+            c.mdp_reset()
+        assert sh.loop_steps_per_launch() == 64
+        ref.loop_run(us, zs)
+        sh.loop_run(us, zs)
+        np.testing.assert_array_equal(sh.mdp_get()[0].view(np.uint32),
+                                      ref.mdp_get()[0].view(np.uint32))
+        np.testing.assert_array_equal(sh.mdp_get()[1], ref.mdp_get()[1])
+        assert_rel_close(sh.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
+                         msg="belief after 200 steps")
+        assert sh.resident_launches()[0] == 4
+
+
 def test_rccl_single_rank_resident_256x2048():
     """The RCCL path of a 256 x 2048 shard -- the per-rank share of the
     2048^2 grid at 8 ranks -- with a 1-rank communicator: pp2_loop_run takes
