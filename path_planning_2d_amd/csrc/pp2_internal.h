@@ -74,9 +74,10 @@ hipError_t launch_absdiff_max(hipStream_t st, const Geom& g, int planes,
                               int* nparts);
 hipError_t launch_sum_cells(hipStream_t st, const Geom& g, const float* b,
                             float* partials, int* nparts);
-// dense[y*W + x)*K + k]  <->  planes (reference AoS layout <-> SoA planes)
+// dense[y*W + x)*K + k]  <->  planes (reference AoS layout <-> SoA planes);
+// mass_out (optional) receives *divide_by
 hipError_t launch_pack(hipStream_t st, const Geom& g, int K, PlaneSet src,
-                       float* dense, const float* divide_by);
+                       float* dense, const float* divide_by, float* mass_out = nullptr);
 hipError_t launch_unpack(hipStream_t st, const Geom& g, int K,
                          const float* dense, PlaneSet dst);
 hipError_t launch_pack_u8(hipStream_t st, const Geom& g, const uint8_t* src,
@@ -89,10 +90,12 @@ hipError_t launch_expand(hipStream_t st, const Geom& g, int cpt, PlaneSet T,
                          const float* b, PlaneSet R, PlaneSet L, PlaneSet F,
                          PlaneSet P, float* rpartials, float* spartials,
                          float* rewards_out, float* stats_out);
-// out[0] = sum b, out[1+i] = sum b*alpha_i; partials >= tiles*10 floats
+// out[0] = sum b, out[1+i] = sum b*alpha_i; partials >= tiles*10 floats;
+// mass_out (optional) receives *mass
 hipError_t launch_belief_dots(hipStream_t st, const Geom& g, int cpt,
                               const float* b, PlaneSet F, float* partials,
-                              float* out);
+                              float* out, const float* mass = nullptr,
+                              float* mass_out = nullptr);
 hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* mass);
 
 // Batched fp16 rollouts (pp2_rollout.cpp).  Beliefs: fp16 [copy][rows+2][wp],

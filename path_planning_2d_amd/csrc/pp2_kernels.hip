@@ -978,10 +978,14 @@ __global__ __launch_bounds__(kBlock) void k_belief_dots(Geom g, const float* __r
         ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
-// out[j] = sum_r partials[r][j], fixed order over r (r = 0..rows-1)
+// out[j] = sum_r partials[r][j], fixed order over r (r = 0..rows-1);
+// *scalar_out = *scalar when given (a mass riding along to a host mirror)
 __global__ __launch_bounds__(kBlock) void k_reduce_columns(const float* __restrict__ partials,
-                                                           int rows, int cols, float* __restrict__ out) {
+                                                           int rows, int cols, float* __restrict__ out,
+                                                           const float* __restrict__ scalar,
+                                                           float* __restrict__ scalar_out) {
   const int j = blockIdx.x * kBlock + threadIdx.x;
+  if (scalar_out && j == 0) *scalar_out = *scalar;
   if (j >= cols) return;
   // 16 loads in flight ahead of the in-order adds (one L2 round trip per 16
   // rows instead of per row)
@@ -996,6 +1000,33 @@ __global__ __launch_bounds__(kBlock) void k_reduce_columns(const float* __restri
   }
   for (; r < rows; ++r) s += partials[(long long)r * cols + j];
   out[j] = s;
+}
+
+// Both column reductions of one expansion in one launch: blocks [0, nb) sum
+// the stats columns, the last block the 9 reward columns (k_reduce_columns'
+// order).
+__global__ __launch_bounds__(kBlock) void k_reduce_expand(const float* __restrict__ rpartials,
+                                                          const float* __restrict__ spartials,
+                                                          int rows, int scols,
+                                                          float* __restrict__ rewards_out,
+                                                          float* __restrict__ stats_out) {
+  const int nb = (scols + kBlock - 1) / kBlock;
+  const bool rew = (int)blockIdx.x == nb;
+  const int j = rew ? (int)threadIdx.x : (int)blockIdx.x * kBlock + threadIdx.x;
+  const int cols = rew ? 9 : scols;
+  const float* __restrict__ part = rew ? rpartials : spartials;
+  if (j >= cols) return;
+  float s = 0.0f;
+  int r = 0;
+  for (; r + 16 <= rows; r += 16) {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = part[(long long)(r + i) * cols + j];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += v[i];
+  }
+  for (; r < rows; ++r) s += part[(long long)r * cols + j];
+  (rew ? rewards_out : stats_out)[j] = s;
 }
 
 // b := b / *mass over owned cells (materialise a normalised belief in place)
@@ -1021,21 +1052,22 @@ hipError_t launch_expand(hipStream_t st, const Geom& g, int cpt, PlaneSet T,
       hipLaunchKernelGGL(k_expand_stats<1>, dim3(tiles, 16), dim3(kBlock), 0, st, g, P, L, F, spartials);
       break;
   }
-  hipLaunchKernelGGL(k_reduce_columns, dim3(1), dim3(kBlock), 0, st, rpartials, tiles, 9, rewards_out);
   const int cols = 16 * 9 * kStats;
-  hipLaunchKernelGGL(k_reduce_columns, dim3((cols + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
-                     spartials, tiles, cols, stats_out);
+  hipLaunchKernelGGL(k_reduce_expand, dim3((cols + kBlock - 1) / kBlock + 1), dim3(kBlock), 0, st,
+                     rpartials, spartials, tiles, cols, rewards_out, stats_out);
   return hipGetLastError();
 }
 
 hipError_t launch_belief_dots(hipStream_t st, const Geom& g, int cpt, const float* b,
-                              PlaneSet F, float* partials, float* out) {
+                              PlaneSet F, float* partials, float* out, const float* mass,
+                              float* mass_out) {
   const int tiles = cells_grid(g, cpt);
   if (cpt == 4)
     hipLaunchKernelGGL(k_belief_dots<4>, dim3(tiles), dim3(kBlock), 0, st, g, b, F, partials);
   else
     hipLaunchKernelGGL(k_belief_dots<1>, dim3(tiles), dim3(kBlock), 0, st, g, b, F, partials);
-  hipLaunchKernelGGL(k_reduce_columns, dim3(1), dim3(kBlock), 0, st, partials, tiles, kStats, out);
+  hipLaunchKernelGGL(k_reduce_columns, dim3(1), dim3(kBlock), 0, st, partials, tiles, kStats, out,
+                     mass, mass_out);
   return hipGetLastError();
 }
 
@@ -1221,9 +1253,11 @@ hipError_t launch_rollout_broadcast(hipStream_t st, const void* src, void* dst,
 // ============================================================================
 __global__ __launch_bounds__(kBlock) void k_pack(Geom g, int K, PlaneSet src,
                                                  float* __restrict__ dense,
-                                                 const float* __restrict__ divide_by) {
+                                                 const float* __restrict__ divide_by,
+                                                 float* __restrict__ mass_out) {
   const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
   const long long n = (long long)g.rows * g.width * K;
+  if (mass_out && i == 0) *mass_out = *divide_by;
   if (i >= n) return;
   const long long cell = i / K;
   const int k = (int)(i % K);
@@ -1255,10 +1289,11 @@ __global__ __launch_bounds__(kBlock) void k_pack_u8(Geom g, const uint8_t* __res
 }
 
 hipError_t launch_pack(hipStream_t st, const Geom& g, int K, PlaneSet src,
-                       float* dense, const float* divide_by) {
+                       float* dense, const float* divide_by, float* mass_out) {
+  if (mass_out && !divide_by) return hipErrorInvalidValue;
   const long long n = (long long)g.rows * g.width * K;
   hipLaunchKernelGGL(k_pack, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                     g, K, src, dense, divide_by);
+                     g, K, src, dense, divide_by, mass_out);
   return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@
 #include <float.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <cstring>
@@ -91,6 +92,40 @@ struct Slot {
 constexpr int kStatsPerChild = 10;
 constexpr int kStatsFloats = 16 * 9 * kStatsPerChild;
 
+// The x-ordered fp32 prefix sum of a belief: the cdf the QNode constructor
+// samples states from (search_tree_cuda.cu:176-183), one serial chain.
+// Adding a zero cell leaves the running sum bit-identical, so a 16-cell block
+// without a set bit only copies the sum forward (PP2_CDF_SKIP=0 turns that off).
+struct Cdf {
+  std::vector<float> v;
+  bool skip = true;
+
+  void build(const float* b, size_t n) {
+    v.resize(n);
+    float* c = v.data();
+    float acc = 0.0f;
+    size_t i = 0;
+    if (skip)
+      for (; i + 16 <= n; i += 16) {
+        uint32_t bits[16], any = 0;
+        std::memcpy(bits, b + i, sizeof bits);
+        for (int t = 0; t < 16; ++t) any |= bits[t];
+        if (!any) {
+          for (int t = 0; t < 16; ++t) c[i + t] = acc;
+          continue;
+        }
+        for (int t = 0; t < 16; ++t) {
+          acc = acc + b[i + t];
+          c[i + t] = acc;
+        }
+      }
+    for (; i < n; ++i) {
+      acc = acc + b[i];
+      c[i] = acc;
+    }
+  }
+};
+
 }  // namespace
 
 struct pp2_planner {
@@ -110,11 +145,16 @@ struct pp2_planner {
   float* d_rpart = nullptr;     // tiles * 9
   float* d_spart = nullptr;     // tiles * 16 * 90
   float* d_bpart = nullptr;     // belief-update / dots partials
-  float* d_out = nullptr;       // [9 rewards | 1440 stats | 10 dots | 1 mass]
-  float* d_dense = nullptr;     // normalised belief, dense
-  float* h_out = nullptr;       // pinned mirror of d_out
-  float* h_belief = nullptr;    // pinned normalised belief
+  // Results the host reads back live in coherent pinned host memory, and the
+  // kernels that produce them store there directly (d_* = the device view of
+  // h_*): no copy engine between a kernel and the host's wait on it.
+  float* h_out = nullptr;       // [9 rewards | 1440 stats | 10 dots | 1 mass]
+  float* d_out = nullptr;
+  float* h_belief = nullptr;    // normalised belief, dense (the sampling cdf's input)
+  float* d_dense = nullptr;
   hipEvent_t ev_belief = nullptr;
+  hipEvent_t ev_done = nullptr;  // an expansion's last device work (cheaper to wait on than the stream)
+  Cdf cdf;                      // the expanded belief's cdf (host sampling)
 
   // lower_bound_mode 1: PBVI leaf bounds (evaluatePbviCpu) of all 144
   // (observation, action) children per expansion, as one split-x MFMA GEMM
@@ -126,8 +166,8 @@ struct pp2_planner {
   float* d_lbpart = nullptr;    // [lb_split][256][Sp] split-x partial dots
   float* d_lbdots = nullptr;    // [256][Sp]
   int* d_lbidx = nullptr;
-  float* d_lbv = nullptr;
   float* h_lbv = nullptr;       // pinned: max_k <row, alpha_k>
+  float* d_lbv = nullptr;
   int* d_srow = nullptr;
   uint8_t *d_us = nullptr, *d_zs = nullptr;
 
@@ -142,8 +182,8 @@ struct pp2_planner {
   hipStream_t side = nullptr;   // reward chains beside the child chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   float* d_rsum = nullptr;      // [256] row sums
-  float* d_rout = nullptr;      // [9 rewards | 256 x 9 FIB dots]
-  float* h_rout = nullptr;      // pinned mirror of d_rout
+  float* h_rout = nullptr;      // pinned: [9 rewards | 256 x 9 FIB dots]
+  float* d_rout = nullptr;
 
   VNode* root = nullptr;
   uint32_t n_vnodes = 0, n_qnodes = 0, expansions = 0;
@@ -156,6 +196,15 @@ constexpr int kOutStats = 9;
 constexpr int kOutDots = 9 + kStatsFloats;
 constexpr int kOutMass = kOutDots + kStatsPerChild;
 constexpr int kOutFloats = kOutMass + 1;
+
+// `count` floats of coherent pinned host memory and their device view.
+bool host_mapped(size_t count, float** host, float** dev) {
+  if (hipHostMalloc((void**)host, count * sizeof(float),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return false;
+  std::memset(*host, 0, count * sizeof(float));
+  return hipHostGetDevicePointer((void**)dev, *host, 0) == hipSuccess;
+}
 
 int acquire_slot(pp2_planner* p, int* out) {
   if (!p->free_slots.empty()) {
@@ -237,8 +286,6 @@ int pbvi_row_max(pp2_planner* p, const float* d_rows, int nrows) {
   HIPCHK(pp2::launch_sum_splits(c->stream, p->d_lbpart, p->lb_split, sstride, (int)sstride,
                                 p->d_lbdots));
   HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, nrows, S, Sp, p->d_lbidx, p->d_lbv));
-  HIPCHK(hipMemcpyAsync(p->h_lbv, p->d_lbv, nrows * sizeof(float), hipMemcpyDeviceToHost,
-                        c->stream));
   return PP2_OK;
 }
 
@@ -342,8 +389,6 @@ int ref_leaf_bounds(pp2_planner* p, const float* d_rows, int rows) {
     HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, al, S, ld, n,
                                   p->d_lbdots, S));
     HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, rows, S, S, p->d_lbidx, p->d_lbv));
-    HIPCHK(hipMemcpyAsync(p->h_lbv, p->d_lbv, rows * sizeof(float), hipMemcpyDeviceToHost,
-                          c->stream));
   }
   return PP2_OK;
 }
@@ -389,9 +434,8 @@ int make_root(pp2_planner* p, int s, uint8_t z, VNode** out) {
     // the slot holds the normalised belief (mass 1)
     HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
     CHECK(ref_leaf_bounds(p, p->d_parent, 1));
-    HIPCHK(hipMemcpyAsync(p->h_rout + 9, p->d_rout + 9, 9 * sizeof(float),
-                          hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventRecord(p->ev_done, c->stream));
+    HIPCHK(hipEventSynchronize(p->ev_done));
     VNode* v = new_vnode(p, z, 0.0f, nullptr);
     v->slot = s;
     v->upper_bound = first_max9(p->h_rout + 9);
@@ -401,17 +445,14 @@ int make_root(pp2_planner* p, int s, uint8_t z, VNode** out) {
     return PP2_OK;
   }
   HIPCHK(pp2::launch_belief_dots(c->stream, c->g, c->cpt, sl.b.v.p, c->fib[c->fcur].v,
-                                 p->d_bpart, p->d_out + kOutDots));
-  HIPCHK(hipMemcpyAsync(p->d_out + kOutMass, sl.mass, sizeof(float),
-                        hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(p->h_out + kOutDots, p->d_out + kOutDots,
-                        (kStatsPerChild + 1) * sizeof(float), hipMemcpyDeviceToHost,
-                        c->stream));
+                                 p->d_bpart, p->d_out + kOutDots, sl.mass,
+                                 p->d_out + kOutMass));
   if (p->pbvi) {
     HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_children, nullptr));
     CHECK(pbvi_row_max(p, p->d_children, 1));
   }
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipEventRecord(p->ev_done, c->stream));
+  HIPCHK(hipEventSynchronize(p->ev_done));
   VNode* v = new_vnode(p, z, 0.0f, nullptr);
   v->slot = s;
   v->upper_bound = fib_upper(p->h_out + kOutDots + 1, p->h_out[kOutMass]);
@@ -481,35 +522,25 @@ int expand_vnode(pp2_planner* p, VNode* v) {
   const size_t n = p->n;
   // normalised belief -> host (for the state samples), then the batched
   // scoring pass runs on the device while the host samples
-  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_dense, sl.mass));
-  HIPCHK(hipMemcpyAsync(p->h_belief, p->d_dense, n * sizeof(float), hipMemcpyDeviceToHost,
-                        c->stream));
+  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_dense, sl.mass, p->d_out + kOutMass));
   HIPCHK(hipEventRecord(p->ev_belief, c->stream));
   HIPCHK(pp2::launch_expand(c->stream, c->g, c->cpt, c->T.v, sl.b.v.p, c->R.v, c->L.v,
                             c->fib[c->fcur].v, p->P.v, p->d_rpart, p->d_spart,
                             p->d_out + kOutRewards, p->d_out + kOutStats));
-  HIPCHK(hipMemcpyAsync(p->d_out + kOutMass, sl.mass, sizeof(float), hipMemcpyDeviceToDevice,
-                        c->stream));
-  HIPCHK(hipMemcpyAsync(p->h_out, p->d_out, kOutFloats * sizeof(float), hipMemcpyDeviceToHost,
-                        c->stream));
   if (p->pbvi) {
     HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
     HIPCHK(pp2::launch_pbvi_update(c->stream, c->g, c->T.v, c->L.v, p->d_parent, p->lb_ld,
                                    p->d_srow, p->d_us, p->d_zs, 144, p->d_children));
     CHECK(pbvi_row_max(p, p->d_children, 144));
   }
+  HIPCHK(hipEventRecord(p->ev_done, c->stream));
   HIPCHK(hipEventSynchronize(p->ev_belief));
 
-  std::vector<float> cdf(n);
-  float acc = 0.0f;
-  for (size_t i = 0; i < n; ++i) {
-    acc = acc + p->h_belief[i];
-    cdf[i] = acc;
-  }
+  p->cdf.build(p->h_belief, n);
   std::vector<uint8_t> zs[9];
   std::vector<float> fq[9];
-  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, cdf, a, zs[a], fq[a]);
-  HIPCHK(hipStreamSynchronize(c->stream));
+  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, p->cdf.v, a, zs[a], fq[a]);
+  HIPCHK(hipEventSynchronize(p->ev_done));
 
   for (QNode* q : v->children)
     if (q) delete_subtree(p, q);
@@ -551,10 +582,9 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   const Slot& sl = p->slots[v->slot];
   const size_t n = p->n;
   const int ld = p->ref_ld;
-  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
-  HIPCHK(hipMemcpyAsync(p->h_belief, p->d_parent, n * sizeof(float), hipMemcpyDeviceToHost,
-                        c->stream));
+  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_dense, nullptr));
   HIPCHK(hipEventRecord(p->ev_belief, c->stream));
+  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
   // the 9 reward chains need only the parent: on the side stream, beside
   // the children's update and renormalisation chains
   HIPCHK(hipEventRecord(p->ev_fork, c->stream));
@@ -568,20 +598,14 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   HIPCHK(pp2::launch_rows_div(c->stream, p->d_children, ld, 144, (int)n, p->d_rsum));
   CHECK(ref_leaf_bounds(p, p->d_children, 144));
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
-  HIPCHK(hipMemcpyAsync(p->h_rout, p->d_rout, kRefOutFloats * sizeof(float),
-                        hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipEventRecord(p->ev_done, c->stream));
   HIPCHK(hipEventSynchronize(p->ev_belief));
 
-  std::vector<float> cdf(n);
-  float acc = 0.0f;
-  for (size_t i = 0; i < n; ++i) {
-    acc = acc + p->h_belief[i];
-    cdf[i] = acc;
-  }
+  p->cdf.build(p->h_belief, n);
   std::vector<uint8_t> zs[9];
   std::vector<float> fq[9];
-  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, cdf, a, zs[a], fq[a]);
-  HIPCHK(hipStreamSynchronize(c->stream));
+  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, p->cdf.v, a, zs[a], fq[a]);
+  HIPCHK(hipEventSynchronize(p->ev_done));
 
   for (QNode* q : v->children)
     if (q) delete_subtree(p, q);
@@ -740,6 +764,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   p->u1.resize(prm->sample_num);
   p->u2.resize(prm->sample_num);
   pp2_curand_uniforms(prm->curand_seed, (int)prm->sample_num, p->u1.data(), p->u2.data());
+  {
+    const char* e = getenv("PP2_CDF_SKIP");
+    p->cdf.skip = !(e && e[0] == '0');
+  }
   p->rng.seed(prm->rand_seed);
   for (uint64_t k = 0; k < prm->rand_skip; ++k) (void)p->rng.next();
   const int tiles1 = pp2::cells_grid(c->g, 1);
@@ -747,11 +775,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   if (hipMalloc(&p->d_rpart, (size_t)tiles1 * 9 * sizeof(float)) != hipSuccess ||
       hipMalloc(&p->d_spart, (size_t)tiles1 * kStatsFloats * sizeof(float)) != hipSuccess ||
       hipMalloc(&p->d_bpart, (size_t)(tiles1 + 1) * kStatsPerChild * sizeof(float)) != hipSuccess ||
-      hipMalloc(&p->d_out, kOutFloats * sizeof(float)) != hipSuccess ||
-      hipMalloc(&p->d_dense, p->n * sizeof(float)) != hipSuccess ||
-      hipHostMalloc(&p->h_out, kOutFloats * sizeof(float), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&p->h_belief, p->n * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+      !host_mapped(kOutFloats, &p->h_out, &p->d_out) ||
+      !host_mapped(p->n, &p->h_belief, &p->d_dense) ||
       hipEventCreateWithFlags(&p->ev_belief, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess)
@@ -781,10 +808,9 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         hipMalloc(&p->d_lbpart, (size_t)p->lb_split * dots * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_lbdots, dots * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_lbidx, 256 * sizeof(int)) != hipSuccess ||
-        hipMalloc(&p->d_lbv, 256 * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_srow, 144 * sizeof(int)) != hipSuccess ||
         hipMalloc(&p->d_us, 144) != hipSuccess || hipMalloc(&p->d_zs, 144) != hipSuccess ||
-        hipHostMalloc(&p->h_lbv, 256 * sizeof(float), hipHostMallocDefault) != hipSuccess)
+        !host_mapped(256, &p->h_lbv, &p->d_lbv))
       return fail(set_err(PP2_ENOMEM, "planner PBVI scratch allocation failed"));
     if (hipMemsetAsync(p->d_parent, 0, (size_t)pld * sizeof(float), c->stream) != hipSuccess ||
         hipMemsetAsync(p->d_children, 0, rows * sizeof(float), c->stream) != hipSuccess ||
@@ -805,9 +831,7 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         hipMalloc(&p->d_rrows, (size_t)9 * row_ld * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_frows, (size_t)9 * row_ld * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_rsum, 256 * sizeof(float)) != hipSuccess ||
-        hipMalloc(&p->d_rout, kRefOutFloats * sizeof(float)) != hipSuccess ||
-        hipHostMalloc(&p->h_rout, kRefOutFloats * sizeof(float), hipHostMallocDefault) !=
-            hipSuccess)
+        !host_mapped(kRefOutFloats, &p->h_rout, &p->d_rout))
       return fail(set_err(PP2_ENOMEM, "planner reference-order scratch allocation failed"));
     std::vector<int> srow(144, 0);
     std::vector<uint8_t> us(144), zs(144);
@@ -851,9 +875,8 @@ int pp2_planner_destroy(pp2_planner* p) {
     if (s.mass) (void)hipFree(s.mass);
   }
   free_planes(&p->P);
-  for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_out, p->d_dense, p->d_parent,
-                   p->d_children, p->d_lbpart, p->d_lbdots, p->d_lbv, p->d_rrows, p->d_frows,
-                   p->d_rsum, p->d_rout})
+  for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_parent, p->d_children,
+                   p->d_lbpart, p->d_lbdots, p->d_rrows, p->d_frows, p->d_rsum})
     if (d) (void)hipFree(d);
   if (p->h_rout) (void)hipHostFree(p->h_rout);
   for (void* d : {(void*)p->d_lbidx, (void*)p->d_srow, (void*)p->d_us, (void*)p->d_zs})
@@ -862,6 +885,7 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (p->h_out) (void)hipHostFree(p->h_out);
   if (p->h_belief) (void)hipHostFree(p->h_belief);
   if (p->ev_belief) (void)hipEventDestroy(p->ev_belief);
+  if (p->ev_done) (void)hipEventDestroy(p->ev_done);
   for (hipEvent_t e : {p->ev_fork, p->ev_join})
     if (e) (void)hipEventDestroy(e);
   if (p->side) {
