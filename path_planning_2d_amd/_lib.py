@@ -70,7 +70,9 @@ SIGNATURES = {
     "pp2_mdp_solve": [_vp, C.c_int, _i32p, _f64p],
     "pp2_mdp_get": [_vp, _f32p, _u8p],
     "pp2_loop_step": [_vp, C.c_uint8, C.c_uint8],
-    "pp2_loop_run": [_vp, C.c_int, _u8p, _u8p],
+    # trajectories go in as bytes objects (c_char_p: a pointer to their
+    # buffer, no per-call ctypes array objects -- ~8 us of host time per call)
+    "pp2_loop_run": [_vp, C.c_int, C.c_char_p, C.c_char_p],
     "pp2_fib_reset": [_vp],
     "pp2_fib_sweep": [_vp, C.c_int],
     "pp2_fib_solve": [_vp, C.c_int, _i32p, _f32p],
@@ -105,7 +107,7 @@ SIGNATURES = {
     "pp2_shard_group_create": [C.POINTER(_vp), C.POINTER(_vp), C.c_int],
     "pp2_shard_group_destroy": [_vp],
     "pp2_shard_group_loop_step": [_vp, C.c_uint8, C.c_uint8],
-    "pp2_shard_group_loop_run": [_vp, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)],
+    "pp2_shard_group_loop_run": [_vp, C.c_int, C.c_char_p, C.c_char_p],
     "pp2_shard_group_belief_update": [_vp, C.c_uint8, C.c_uint8],
     "pp2_shard_group_mdp_sweep": [_vp, C.c_int],
     "pp2_shard_group_mdp_solve": [_vp, C.c_int, _i32p, _f64p],

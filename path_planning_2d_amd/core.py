@@ -220,7 +220,7 @@ class GridContext:
         zs = np.ascontiguousarray(zs, np.uint8)
         if us.shape != zs.shape:
             raise ValueError("us and zs must have the same length")
-        call("pp2_loop_run", self._h, int(us.size), _u8(us), _u8(zs))
+        call("pp2_loop_run", self._h, int(us.size), us.tobytes(), zs.tobytes())
 
     # ------------------------------------------------------------ FIB
     def fib_reset(self):
@@ -391,7 +391,9 @@ class ShardGroup:
     def loop_run(self, us, zs):
         us = np.ascontiguousarray(us, np.uint8)
         zs = np.ascontiguousarray(zs, np.uint8)
-        call("pp2_shard_group_loop_run", self._h, int(us.size), _u8(us), _u8(zs))
+        if us.shape != zs.shape:
+            raise ValueError("us and zs must have the same length")
+        call("pp2_shard_group_loop_run", self._h, int(us.size), us.tobytes(), zs.tobytes())
 
     def set_tuning(self, key: int, value: int):
         for s in self.shards:
