@@ -759,59 +759,17 @@ def main():
         ctx.set_tuning(ctx.TUNE_CODED_MODEL, 0)
     dict_entries, coded = ctx.model_dict_info()
     steps_per_launch = ctx.loop_steps_per_launch()
+    cells_per_gpu = (r1 - r0) * gw  # this rank's cells
     ctx.belief_set(b0[r0 * gw:r1 * gw])
     ctx.mdp_reset()
     ctx.synchronize()
 
-    # ---------------------------------------------------------------- warmup
-    ctx.loop_run(us[:args.warmup], zs[:args.warmup])
-    torch.cuda.synchronize()
-    if ws > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-
-    # ---------------------------------------------------------------- timed
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    # torch creates an event's HIP event at its first record (~20 us of host
-    # time): create both before the timed region
-    ev0.record(stream)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    ctx.loop_run(us[args.warmup:total], zs[args.warmup:total])
-    enqueue_s = time.perf_counter() - t0
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if ws > 1:  # (one rank: the synchronize above already closes the region)
-        dist.barrier()
-        torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    loop_ms_events = ev0.elapsed_time(ev1) / args.steps
-    if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    cells_per_gpu = (r1 - r0) * gw  # this rank's cells
-    value = gh * gw * args.steps / elapsed
-    # sanity: the belief is still a distribution (checks the timed work ran)
-    mass_ok = None
-    if rank == 0 and ws == 1:
-        bsum = float(ctx.belief_get().astype(np.float64).sum())
-        mass_ok = abs(bsum - 1.0) < 1e-4
-
-    if args.profile:
-        if rank == 0:
-            print(json.dumps({"profile_run": True, "steps": args.steps,
-                              "ms_per_step": 1e3 * elapsed / args.steps}))
-        ctx.close()
-        if ws > 1:
-            dist.destroy_process_group()
-        return
-
     # ------------------------------------------- per-kernel timing (HIP events)
+    # These secondary legs run BEFORE the headline's warmup and timed steps:
+    # they keep the GPU busy for tens of ms, so the timed steps run at the
+    # working clock (a GPU fresh out of idle runs the same 20-step launch
+    # ~8 % slower, tools/micro/clock_warmup.py).  The state is reset after.
+    legs_t0 = time.perf_counter()
     reps = args.kernel_reps
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
@@ -826,20 +784,6 @@ def main():
     def loop_reps():
         ctx.loop_run(us[:reps], zs[:reps])
 
-    # the resident kernel's duration per launch for the roofline: launches of
-    # the timed region's length back to back, so the host enqueue of one
-    # overlaps the previous (the timed region's events also hold its single
-    # enqueue; rocprof's per-dispatch average is the comparable figure)
-    res_launch_us = None
-    if coded and steps_per_launch >= RESIDENT_STEPS:
-        n_l = -(-args.steps // -(-args.steps // RESIDENT_STEPS))
-        n_rep = 10
-        e0.record(stream)
-        for _ in range(n_rep):
-            ctx.loop_run(us[:n_l], zs[:n_l])
-        e1.record(stream)
-        torch.cuda.synchronize()
-        res_launch_us = e0.elapsed_time(e1) / n_rep * 1e3
     sweep_ms = timed(lambda: ctx.mdp_sweep(reps))  # coded when active
     pairs_ms = None
     if coded and steps_per_launch >= RESIDENT_STEPS:
@@ -903,6 +847,72 @@ def main():
                      "us_per_sweep": solve_ms[1] * 1e3 / max(1, n_sw),
                      "kernel": ("k_sweep_resident" if coded and steps_per_launch >= RESIDENT_STEPS
                                 else "k_mdp_sweep_coded" if coded else "k_mdp_sweep")}
+    ctx.belief_set(b0[r0 * gw:r1 * gw])
+    ctx.mdp_reset()
+    ctx.synchronize()
+    legs_ms = (time.perf_counter() - legs_t0) * 1e3
+
+    # ---------------------------------------------------------------- warmup
+    ctx.loop_run(us[:args.warmup], zs[:args.warmup])
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    # ---------------------------------------------------------------- timed
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    # torch creates an event's HIP event at its first record (~20 us of host
+    # time): create both before the timed region
+    ev0.record(stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    ctx.loop_run(us[args.warmup:total], zs[args.warmup:total])
+    enqueue_s = time.perf_counter() - t0
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if ws > 1:  # (one rank: the synchronize above already closes the region)
+        dist.barrier()
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    loop_ms_events = ev0.elapsed_time(ev1) / args.steps
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    value = gh * gw * args.steps / elapsed
+    # sanity: the belief is still a distribution (checks the timed work ran)
+    mass_ok = None
+    if rank == 0 and ws == 1:
+        bsum = float(ctx.belief_get().astype(np.float64).sum())
+        mass_ok = abs(bsum - 1.0) < 1e-4
+
+    if args.profile:
+        if rank == 0:
+            print(json.dumps({"profile_run": True, "steps": args.steps,
+                              "ms_per_step": 1e3 * elapsed / args.steps}))
+        ctx.close()
+        if ws > 1:
+            dist.destroy_process_group()
+        return
+
+    # the resident kernel's duration per launch for the roofline: launches of
+    # the timed region's length back to back, so the host enqueue of one
+    # overlaps the previous (the timed region's events also hold its single
+    # enqueue; rocprof's per-dispatch average is the comparable figure)
+    res_launch_us = None
+    if coded and steps_per_launch >= RESIDENT_STEPS:
+        n_l = -(-args.steps // -(-args.steps // RESIDENT_STEPS))
+        n_rep = 10
+        e0.record(stream)
+        for _ in range(n_rep):
+            ctx.loop_run(us[:n_l], zs[:n_l])
+        e1.record(stream)
+        torch.cuda.synchronize()
+        res_launch_us = e0.elapsed_time(e1) / n_rep * 1e3
     ctx.close()
 
     bytes_loop = BYTES_LOOP_CODED if coded else BYTES_LOOP
@@ -1055,6 +1065,13 @@ def main():
                 "loop_frac": loop_gbs / HBM_PEAK_GBS,
             },
             "fib_sweep": fib,
+            "headline_after": {
+                "secondary_legs_ms": legs_ms,
+                "note": "the per-kernel timings, FIB sweeps, dense path and MDP solve run before "
+                        "the warmup + timed steps (then belief and values are reset), so the "
+                        "timed steps run at the GPU's working clock; a GPU fresh out of idle "
+                        "runs the same 20-step launch ~8 % slower (tools/micro/clock_warmup.py, "
+                        "profiles/r03/clock_warmup.txt)"},
             "belief_mass_ok": mass_ok,
             "mdp_solve": mdp_solve,
             "plan_step": plan,
