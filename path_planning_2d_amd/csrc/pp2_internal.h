@@ -242,7 +242,7 @@ struct ResidentPlan {
   int rt = 0, ntiles = 0, threads = 0;
   size_t lds = 0;
 };
-struct ResidentRun {
+struct ResidentHead {
   Geom g;                    // the launch's rows: the grid, or a shard's view
   float gamma;
   int E;                     // dictionary entries
@@ -272,6 +272,13 @@ struct ResidentRun {
   unsigned arrive_base;      // arrival counter of earlier launches (epoch-tagged)
   unsigned slot_use[2];      // uses of exchange slots 0 / 1 by earlier launches
   int stall_tile;            // diagnostic (tests): this tile returns at once, -1 none
+};
+// Runs of at most kResidentShortSteps steps launch a kernel instance whose
+// trajectory argument holds just that many steps: 256 B of kernel arguments
+// instead of ~2.3 KB, about 3 us less host time per launch from an idle
+// stream (tools/micro/kernarg_cost.hip).
+constexpr int kResidentShortSteps = 24;
+struct ResidentRun : ResidentHead {
   uint8_t uz[kResidentMaxSteps];  // u | z << 4 per step
 };
 // Resident MDP solve (pp2_mdp_solve): sweeps in blocks of kSolveBlock, a

@@ -62,6 +62,7 @@
 // launch queued behind an unverified one reads the error word first and
 // exits before any global store if it is raised (the host re-runs it too).
 #include <algorithm>
+#include <cstring>
 
 #include "pp2_coded_dev.h"
 
@@ -367,7 +368,14 @@ __device__ __forceinline__ void row_quad(const float (&m)[4], float e, float (&v
                                                     0x130, 0xf, 0xf, false));
 }
 
-__global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) {
+template <int CAP>
+struct Trajectory {
+  uint8_t uz[CAP];  // u | z << 4 per step
+};
+
+template <int CAP>
+__global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
+                                                           const Trajectory<CAP> tr) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wp = a.g.wp, rows = a.g.rows, tpr = wp >> 2, wpr = wp >> 8;
   const int xs = wp + 4;                // padded LDS row stride
@@ -550,7 +558,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentRun a) 
   PP2_RP(2);
 
   for (int t = 0; t < a.n; ++t) {
-    const int u = a.uz[t] & 15, z = a.uz[t] >> 4;
+    const int u = tr.uz[t] & 15, z = tr.uz[t] >> 4;
     const int ci = t & 1, co = ci ^ 1;
     const bool last = t == a.n - 1;
     // ---- a block start inside the run needs the exact mass of step t-1's
@@ -869,12 +877,15 @@ bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p) {
   if (threads > 1024) return false;
   const size_t lds = resident_lds_bytes(g, E, rt);
   if (lds > kDictLdsMaxBytes) return false;
-  static unsigned long long attr = 0;
-  allow_lds(reinterpret_cast<const void*>(&k_loop_resident), attr);
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_loop_resident, (int)threads, lds) !=
-          hipSuccess ||
-      nb < 1) {
+  static unsigned long long attr[2] = {0, 0};
+  allow_lds(reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps>), attr[0]);
+  allow_lds(reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps>), attr[1]);
+  int nb = 0, nb2 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_loop_resident<kResidentMaxSteps>,
+                                                   (int)threads, lds) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, k_loop_resident<kResidentShortSteps>,
+                                                   (int)threads, lds) != hipSuccess ||
+      nb < 1 || nb2 < 1) {
     (void)hipGetLastError();
     return false;
   }
@@ -887,7 +898,7 @@ bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p) {
   // get one slot per CU, so this is ntiles <= ncus; the guide's SGPR caveat
   // (one block fewer than the API answer) applies to 256-lane blocks at
   // several per CU, not here.
-  return (long long)nb * ncus >= p->ntiles;
+  return (long long)std::min(nb, nb2) * ncus >= p->ntiles;
 }
 
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a) {
@@ -896,7 +907,18 @@ hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const Res
       a.own0 >= a.own1 || a.b_out == a.b_in || a.j_out == a.j_in ||
       (a.in_partials && a.in_partials == a.out_partials))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_loop_resident, dim3(p.ntiles), dim3(p.threads), p.lds, st, a);
+  const ResidentHead& h = a;
+  if (a.n <= kResidentShortSteps) {
+    Trajectory<kResidentShortSteps> tr{};
+    std::memcpy(tr.uz, a.uz, (size_t)a.n);
+    hipLaunchKernelGGL(k_loop_resident<kResidentShortSteps>, dim3(p.ntiles), dim3(p.threads),
+                       p.lds, st, h, tr);
+  } else {
+    Trajectory<kResidentMaxSteps> tr;
+    std::memcpy(tr.uz, a.uz, sizeof tr.uz);
+    hipLaunchKernelGGL(k_loop_resident<kResidentMaxSteps>, dim3(p.ntiles), dim3(p.threads),
+                       p.lds, st, h, tr);
+  }
   return hipGetLastError();
 }
 
