@@ -124,6 +124,49 @@ def test_planner_256_plan_step(oracle):
         opl.close()
 
 
+def test_planner_cdf_zero_block_skip_exact(oracle, monkeypatch):
+    """The host cdf skips 16-cell blocks without mass (adding +0 leaves the
+    fp32 running sum bit-identical): on a belief that is zero outside a band
+    of rows, plans with the skip (default) and without it (PP2_CDF_SKIP=0)
+    are identical, and equal the oracle's."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    name = "sparse_map_100x40"
+    grid = golden_map(name)
+    m = golden("model", name)
+    H, W = grid.shape
+    b0 = S.uniform_belief(grid).reshape(H, W).copy()
+    b0[:12] = 0.0
+    b0[20:] = 0.0
+    b0 = (b0 / b0.sum(dtype=np.float64)).astype(np.float32).ravel()
+    _, zs, _ = S.synth_trajectory(grid, 4, seed=11)
+    runs = []
+    with P.GridContext(grid, tuple(m["goal"]), gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_solve()
+        alphas = ctx.fib_get()
+        for skip in ("1", "0"):
+            monkeypatch.setenv("PP2_CDF_SKIP", skip)
+            infos = []
+            with P.QVTreePlanner(ctx, max_search_tree_depth=5, max_online_iteration=15) as gpl:
+                a, v = gpl.step(0, 0, b0)
+                infos.append((a, v, gpl.info()))
+                for k in range(4):
+                    a, v = gpl.step(a, int(zs[k]))
+                    infos.append((a, v, gpl.info()))
+            runs.append(infos)
+        opl = oracle.Planner(grid, m["T"], m["L"], m["R"], alphas, max_depth=5, max_iter=15,
+                             accurate=True)
+        a_o, v_o = opl.step(0, 0, b0)
+        compare(runs[0][0][2], opl.info(), "skip step 0")
+        assert runs[0][0][0] == a_o
+        opl.close()
+    for (a1, v1, i1), (a0, v0, i0) in zip(*runs):
+        assert a1 == a0 and np.float32(v1) == np.float32(v0)
+        for k in i1:
+            assert np.array_equal(np.asarray(i1[k]), np.asarray(i0[k])), k
+
+
 @pytest.mark.parametrize("name,S,max_depth,steps", [
     ("map_10x10", 64, 50, 5),
     ("sparse_map_100x40", 500, 5, 4),   # the reference node: S = 500, PBVI leaves
