@@ -63,6 +63,7 @@ HBM_COPY_GBS = 6290.0            # measured float4 copy rate, the achievable cei
 MFMA_F32_PEAK_TFLOPS = 157.3     # dense f32-input MFMA peak (MI355X_MICROARCH.md, Matrix cores)
 BYTES_SWEEP = 369                # per cell: T 324 + C 36 + J 4 + J' 4 + A 1
 BYTES_BELIEF = 48                # per cell: T_u 36 + L_z 4 + b 4 + b' 4
+BYTES_BELIEF_CODED = 10          # per cell: code 2 + b 4 + b' 4 (pp2_belief_update on the coded model)
 BYTES_LOOP = BYTES_SWEEP + BYTES_BELIEF   # SURVEY.md §8(d) contract (T counted twice)
 FIB_FLOP_CELL = 25920           # reference full-sum flops per cell and FIB sweep (~25.9 k)
 F32_VALU_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: f32 vector (v_pk_fma_f32) peak
@@ -927,7 +928,8 @@ def main():
     # a resident sweep launch moves its 11 B/cell once for all `reps` sweeps
     sweep_res = coded and resident
     sweep_gbs = bytes_sweep * cells_per_gpu / ((sweep_ms * (reps if sweep_res else 1)) * 1e-3) / 1e9
-    belief_gbs = BYTES_BELIEF * cells_per_gpu / (belief_ms * 1e-3) / 1e9
+    bytes_belief = BYTES_BELIEF_CODED if coded else BYTES_BELIEF
+    belief_gbs = bytes_belief * cells_per_gpu / (belief_ms * 1e-3) / 1e9
     # one launch = spl steps; its average duration: back-to-back resident
     # launches (above), else the timed region's events
     launch_s = res_launch_us * 1e-6 if res_launch_us else loop_ms_events * 1e-3 * spl
@@ -1055,6 +1057,9 @@ def main():
                 "mdp_sweep_us": sweep_ms * 1e3,
                 "mdp_sweep_gbs": sweep_gbs,
                 "mdp_sweep_frac": sweep_gbs / HBM_PEAK_GBS,
+                "belief_update_kernel": ("k_loop_step_coded without its sweep + k_sum_finalize "
+                                         "(10 B/cell: code, b, b')" if coded else
+                                         "k_belief_update + k_sum_finalize (48 B/cell)"),
                 "belief_update_us": belief_ms * 1e3,
                 "belief_update_gbs": belief_gbs,
                 "belief_update_frac": belief_gbs / HBM_PEAK_GBS,

@@ -192,9 +192,11 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       const bool own = y >= own0 && y < own1;
       if (!own) local = 0.0f;
       PP2_PHASE(2);
-      Win6 jw;
-      load_win6(J_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, jw);
-      sweep_cells<SPARSE, NT>(g, sTC, gamma, cw.m0[1], cw.m1[1], jw, y, x0, own, J_out, A);
+      if (J_in) {  // (null: a belief update alone, pp2_belief_update)
+        Win6 jw;
+        load_win6(J_in, g.wp, y, x0, x0 == 0, x0 + 4 == g.wp, jw);
+        sweep_cells<SPARSE, NT>(g, sTC, gamma, cw.m0[1], cw.m1[1], jw, y, x0, own, J_out, A);
+      }
       PP2_PHASE(3);
     }
     const int d = QPB * tile0 + q;
@@ -212,8 +214,10 @@ __global__ __launch_bounds__(QPB * kQuarter, MINB * QPB) void k_loop_step_coded(
       belief_cells<SPARSE, U, NT>(g, sTu, sL, slot, inv, c2, w2, yy, xx, b_out, local);
       const bool own = yy >= own0 && yy < own1;
       if (!own) local = 0.0f;
-      load_win6(J_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
-      sweep_cells<SPARSE, NT>(g, sTC, gamma, c2.m0[1], c2.m1[1], w2, yy, xx, own, J_out, A);
+      if (J_in) {
+        load_win6(J_in, g.wp, yy, xx, xx == 0, xx + 4 == g.wp, w2);
+        sweep_cells<SPARSE, NT>(g, sTC, gamma, c2.m0[1], c2.m1[1], w2, yy, xx, own, J_out, A);
+      }
     }
     const int d = QPB * tl + q;
     if (d < dense_blocks) write_wave_partial(local, out_partials, d);

@@ -626,9 +626,21 @@ int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_s
   break_pipeline(c);
   const int bn = c->bcur ^ 1;
   const int nparts = pp2::mass_partials(c->g, c->cpt);
-  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
-                                   c->b[c->bcur].v.p, c->b[bn].v.p, u, z,
-                                   c->bsum + c->bcur, c->pbuf[bn]));
+  if (coded_active(c)) {
+    // the coded fused kernel without its sweep: codes and b in, b' out (10 B
+    // per cell instead of the dense planes' 48), the same arithmetic and
+    // partial layout (cpt 4) as k_belief_update
+    HIPCHK(pp2::launch_loop_step_coded(
+        c->stream, c->g, c->gamma, c->d_code, c->d_rows,
+        c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3),
+        c->d_tu + (size_t)u * (((size_t)c->dict_n * pp2::tu_width(c->dict_sparse) + 3) & ~(size_t)3),
+        c->dict_n, c->dict_sparse, c->b[c->bcur].v.p, c->b[bn].v.p, u, nullptr, 0,
+        c->bsum + c->bcur, nullptr, c->pbuf[bn], nullptr, nullptr, nullptr, 0, c->g.rows, 1.0f));
+  } else {
+    HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
+                                     c->b[c->bcur].v.p, c->b[bn].v.p, u, z,
+                                     c->bsum + c->bcur, c->pbuf[bn]));
+  }
   HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bn], nparts, c->bsum + bn));
   c->pending[bn] = false;
   CHECK(allreduce_mass(c, c->bsum + bn));
