@@ -110,19 +110,19 @@ int rollout_min_chunk();  // smallest chunk of any variant (sizes chunk tables)
 // raw T tables [u][tstride] with tw floats per entry, sparse = support-only
 // rows; dl = L transposed [z][es]) or E = 0 for the T/L planes.  R is always
 // the R plane.  Writes bout, then stats_out[copy][3] (k_rollout_reduce).
+// istride: halfs between consecutive copies' input planes (0: every copy
+// reads the one plane at bin -- the first step, from the root image).
 hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,
                                PlaneSet R, const uint16_t* code, const float* tu_all,
                                long long tstride, int tw, const float* dl, int es, int E,
                                bool sparse, const void* bin, void* bout, long long cstride,
-                               int nchunks, const int* chunk_u, const int* chunk_first,
+                               long long istride, int nchunks, const int* chunk_u, const int* chunk_first,
                                const int* copies, const uint8_t* zs, const float* in_stats,
                                float* partials, float* stats_out, int ncopies);
 hipError_t launch_rollout_reduce(hipStream_t st, const float* partials, int nwaves,
                                  int ncopies, float* stats_out);
 hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const void* b,
                                long long cstride, int ncopies, float* partials, float* out);
-hipError_t launch_rollout_broadcast(hipStream_t st, const void* src, void* dst,
-                                    long long cstride, int ncopies);
 
 // Dictionary-coded model (pp2_coded.hip).  code: uint16 per cell over rows
 // [-1, rows] (same geometry as a plane); dict: kDictRow floats per entry,

@@ -1081,8 +1081,9 @@ hipError_t launch_scale(hipStream_t st, const Geom& g, float* b, const float* ma
 // ============================================================================
 // Batched fp16 QV-tree rollouts (BASELINE configs[4]): the per-copy
 // reduction of the step kernel's partials, the FIB leaf pass
-// (fast_informed_bound_cuda.cu:278-297) and the root broadcast.  The step
-// kernel itself (k_rollout_band) is in pp2_rollout_dev.hip.
+// (fast_informed_bound_cuda.cu:278-297).  The step kernel itself
+// (k_rollout_band) is in pp2_rollout_dev.hip; its first step reads the root
+// image for every copy (no broadcast).
 //  * beliefs live as fp16 planes [copy][row][x] (2 B per cell-copy), each
 //    copy max-normalised, math in fp32;
 //  * per (copy, wave) partial sums of {stored sum, stored max, reward dot} are
@@ -1197,16 +1198,6 @@ __global__ __launch_bounds__(64) void k_rollout_leaf_reduce(const float* __restr
   }
 }
 
-// broadcast one fp16 plane image (rows+2 halo rows, wp) into every copy
-__global__ __launch_bounds__(kBlock) void k_rollout_broadcast(const _Float16* __restrict__ src,
-                                                              _Float16* __restrict__ dst,
-                                                              long long cstride, int copies) {
-  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= cstride) return;
-  const _Float16 v = src[i];
-  for (int c = blockIdx.y; c < copies; c += gridDim.y) dst[(long long)c * cstride + i] = v;
-}
-
 int rollout_tiles(const Geom& g) {
   const long long cells = (long long)g.rows * g.wp;
   const long long per = (long long)kRollIter * kBlock * 4;
@@ -1235,15 +1226,6 @@ hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const 
                      (const _Float16*)b + g.wp, cstride, ncopies, partials, nw);
   hipLaunchKernelGGL(k_rollout_leaf_reduce, dim3(ncopies), dim3(64), 0, st, partials, nw,
                      ncopies, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_rollout_broadcast(hipStream_t st, const void* src, void* dst,
-                                    long long cstride, int ncopies) {
-  const int gx = (int)((cstride + kBlock - 1) / kBlock);
-  const int gy = ncopies < 256 ? ncopies : 256;
-  hipLaunchKernelGGL(k_rollout_broadcast, dim3(gx, gy), dim3(kBlock), 0, st,
-                     (const _Float16*)src, (_Float16*)dst, cstride, ncopies);
   return hipGetLastError();
 }
 

@@ -108,9 +108,10 @@ int pp2_rollout_set_root(pp2_rollout* r, const float* belief) {
       s += (double)(float)h;
       m = std::max(m, (float)h);
     }
+  // no per-copy broadcast: the first step of every run reads this one image
+  // for all copies (an L2-resident input), then the copies diverge
   HIPCHK(hipMemcpyAsync(r->d_root, img.data(), img.size() * sizeof(_Float16),
                         hipMemcpyHostToDevice, c->stream));
-  HIPCHK(pp2::launch_rollout_broadcast(c->stream, r->d_root, r->buf[0], r->cstride, r->copies));
   std::vector<float> st((size_t)r->copies * kRollStats);
   for (int i = 0; i < r->copies; ++i) {
     st[i * kRollStats + 0] = (float)s;
@@ -173,8 +174,10 @@ int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs) {
     const int tw = pp2::tu_width(c->dict_sparse);
     HIPCHK(pp2::launch_rollout_step(c->stream, c->g, c->T.v, c->L.v, c->R.v, c->d_code,
                                     c->d_tu, ((long long)E * tw + 3) & ~3LL, tw, c->d_dl,
-                                    (E + 3) & ~3, E, c->dict_sparse, r->buf[k & 1],
-                                    r->buf[(k + 1) & 1], r->cstride, r->nchunks[k], base,
+                                    (E + 3) & ~3, E, c->dict_sparse,
+                                    k == 0 ? (const void*)r->d_root : r->buf[k & 1],
+                                    r->buf[(k + 1) & 1], r->cstride, k == 0 ? 0LL : r->cstride,
+                                    r->nchunks[k], base,
                                     base + M, base + 3 * M, r->d_zs + (size_t)k * C,
                                     r->d_stats + (size_t)k * C * kRollStats, r->d_partials,
                                     r->d_stats + (size_t)(k + 1) * C * kRollStats, C));
@@ -225,7 +228,9 @@ int pp2_rollout_get_belief(pp2_rollout* r, int copy, float* belief) {
   pp2_ctx* c = r->ctx;
   DeviceGuard dg(c->device);
   std::vector<_Float16> img((size_t)r->cstride);
-  const _Float16* src = (const _Float16*)r->buf[r->ran ? (r->depth & 1) : 0] + (size_t)copy * r->cstride;
+  // before a run every copy is the root image
+  const _Float16* src = r->ran ? (const _Float16*)r->buf[r->depth & 1] + (size_t)copy * r->cstride
+                               : r->d_root;
   HIPCHK(hipMemcpyAsync(img.data(), src, img.size() * sizeof(_Float16), hipMemcpyDeviceToHost,
                         c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));

@@ -115,7 +115,8 @@ struct BandArgs {
   const uint16_t* code;  // code plane at row -1
   const _Float16* bin;   // copy 0's plane at row -1
   _Float16* bout;
-  long long cstride;
+  long long cstride;  // halfs per copy plane (outputs)
+  long long istride;  // between the copies' input planes (0: one shared image)
   float* partials;
   int nwaves;
 };
@@ -177,14 +178,14 @@ __device__ __forceinline__ void band(const BandArgs& a, const float* sTu, const 
   const int ej = lane >> 1, es_ = lane & 1;
   const bool eside_ok = es_ == 0 ? xs > 0 : xs + 256 < g.wp;
   const uint32_t ebyte = 2u * (uint32_t)(es_ == 0 ? xs - 2 : xs + 256);
-  const void* ebase = ej < CH ? (const void*)(a.bin + (long long)ecid * a.cstride)
+  const void* ebase = ej < CH ? (const void*)(a.bin + (long long)ecid * a.istride)
                               : (const void*)a.code;
   const bool eok = eside_ok && ej <= CH;
   const _Float16* bb[CH];
   _Float16* ob[CH];
 #pragma unroll
   for (int j = 0; j < CH; ++j) {
-    bb[j] = a.bin + (long long)cid[j] * a.cstride;
+    bb[j] = a.bin + (long long)cid[j] * a.istride;
     ob[j] = a.bout + (long long)cid[j] * a.cstride;
   }
   const float* rbase = a.R.p + (long long)u * a.R.ps + xs;
@@ -472,7 +473,7 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
                                PlaneSet R, const uint16_t* code, const float* tu_all,
                                long long tstride, int tw, const float* dl, int es, int E,
                                bool sparse, const void* bin, void* bout, long long cstride,
-                               int nchunks, const int* chunk_u, const int* chunk_first,
+                               long long istride, int nchunks, const int* chunk_u, const int* chunk_first,
                                const int* copies, const uint8_t* zs, const float* in_stats,
                                float* partials, float* stats_out, int ncopies) {
   const int gx = band_gx(g), nseg = band_nseg(g), nband = band_nband(g);
@@ -486,6 +487,7 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
   a.bin = (const _Float16*)bin;            // copy planes start at row -1
   a.bout = (_Float16*)bout;
   a.cstride = cstride;
+  a.istride = istride;
   a.partials = partials;
   a.nwaves = nw;
   const long long nblocks = (long long)gx * nchunks;

@@ -131,3 +131,37 @@ def test_rollout_coded_equals_dense(H, W, copies, depth):
         np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
     for x, y in zip(ba, bb):
         np.testing.assert_array_equal(x, y)
+
+
+def test_rollout_runs_restart_from_root():
+    """Every run starts from the root image set by set_root (its first step
+    reads the one image for all copies): a second run after one set_root
+    equals a fresh set_root + run bit for bit, and before any run every copy
+    reads back as the root."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(96, 128, seed=9)
+    goal = S.synth_goal(grid)
+    b0 = S.uniform_belief(grid)
+    copies, depth = 40, 3
+    us1, zs1 = S.rollout_trajectories(grid, b0, copies, depth, seed=1)
+    us2, zs2 = S.rollout_trajectories(grid, b0, copies, depth, seed=2)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_solve(max_sweeps=20)
+        with P.BatchedRollout(ctx, copies, depth) as r:
+            r.set_root(b0)
+            for c in (0, copies - 1):
+                got = r.belief(c).astype(np.float64)
+                assert np.all(np.abs(got - b0) <= 1e-3 * b0.max())
+            r.run(us1, zs1)
+            r.run(us2, zs2)
+            again = r.results()
+            b_again = r.belief(copies // 2)
+            r.set_root(b0)
+            r.run(us2, zs2)
+            fresh = r.results()
+            b_fresh = r.belief(copies // 2)
+    for k in fresh:
+        np.testing.assert_array_equal(again[k], fresh[k], err_msg=k)
+    np.testing.assert_array_equal(b_again, b_fresh)
