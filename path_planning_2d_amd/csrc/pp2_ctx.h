@@ -219,6 +219,8 @@ int check_model(pp2_ctx* c);
 size_t owned_cells(const pp2_ctx* c);
 int download_planes(pp2_ctx* c, const Planes& P, float* host, const float* divide_by);
 int belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep);
+int launch_belief(pp2_ctx* c, const float* b_in, float* b_out, uint8_t u, uint8_t z,
+                  const float* mass, float* partials);
 int loop_step_fused(pp2_ctx* c, uint8_t u, uint8_t z, bool eager_mass);
 int ensure_mass(pp2_ctx* c);
 void break_pipeline(pp2_ctx* c);

@@ -618,6 +618,27 @@ int pp2rt::ensure_mass(pp2_ctx* c) {
 
 void pp2rt::break_pipeline(pp2_ctx* c) { c->kstep = 0; }
 
+// One belief update of planes b_in -> b_out (the context's geometry) divided
+// by *mass, its mass partials (mass_partials(g, cpt) of them) into partials:
+// on a coded model the coded fused kernel without its sweep (code and b in,
+// b' out: 10 B per cell instead of the dense planes' 48), else
+// k_belief_update -- the same arithmetic and partial layout either way.
+int pp2rt::launch_belief(pp2_ctx* c, const float* b_in, float* b_out, uint8_t u, uint8_t z,
+                         const float* mass, float* partials) {
+  if (coded_active(c)) {
+    HIPCHK(pp2::launch_loop_step_coded(
+        c->stream, c->g, c->gamma, c->d_code, c->d_rows,
+        c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3),
+        c->d_tu + (size_t)u * (((size_t)c->dict_n * pp2::tu_width(c->dict_sparse) + 3) & ~(size_t)3),
+        c->dict_n, c->dict_sparse, b_in, b_out, u, nullptr, 0, mass, nullptr, partials, nullptr,
+        nullptr, nullptr, 0, c->g.rows, 1.0f));
+    return PP2_OK;
+  }
+  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v, b_in, b_out, u, z,
+                                   mass, partials));
+  return PP2_OK;
+}
+
 // Belief update alone (k_belief_update), mass finalised eagerly.
 int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_sweep) {
   if (fuse_with_sweep) return loop_step_fused(c, u, z, true);
@@ -626,21 +647,7 @@ int pp2rt::belief_update_impl(pp2_ctx* c, uint8_t u, uint8_t z, bool fuse_with_s
   break_pipeline(c);
   const int bn = c->bcur ^ 1;
   const int nparts = pp2::mass_partials(c->g, c->cpt);
-  if (coded_active(c)) {
-    // the coded fused kernel without its sweep: codes and b in, b' out (10 B
-    // per cell instead of the dense planes' 48), the same arithmetic and
-    // partial layout (cpt 4) as k_belief_update
-    HIPCHK(pp2::launch_loop_step_coded(
-        c->stream, c->g, c->gamma, c->d_code, c->d_rows,
-        c->d_dl + (size_t)z * ((c->dict_n + 3) & ~3),
-        c->d_tu + (size_t)u * (((size_t)c->dict_n * pp2::tu_width(c->dict_sparse) + 3) & ~(size_t)3),
-        c->dict_n, c->dict_sparse, c->b[c->bcur].v.p, c->b[bn].v.p, u, nullptr, 0,
-        c->bsum + c->bcur, nullptr, c->pbuf[bn], nullptr, nullptr, nullptr, 0, c->g.rows, 1.0f));
-  } else {
-    HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v,
-                                     c->b[c->bcur].v.p, c->b[bn].v.p, u, z,
-                                     c->bsum + c->bcur, c->pbuf[bn]));
-  }
+  CHECK(launch_belief(c, c->b[c->bcur].v.p, c->b[bn].v.p, u, z, c->bsum + c->bcur, c->pbuf[bn]));
   HIPCHK(pp2::launch_sum_finalize(c->stream, c->pbuf[bn], nparts, c->bsum + bn));
   c->pending[bn] = false;
   CHECK(allreduce_mass(c, c->bsum + bn));

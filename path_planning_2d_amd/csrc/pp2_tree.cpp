@@ -415,9 +415,8 @@ int materialize(pp2_planner* p, VNode* v) {
   pp2_ctx* c = p->ctx;
   const Slot& ps = p->slots[pv->slot];
   const Slot& ns = p->slots[s];
-  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v, ps.b.v.p,
-                                   ns.b.v.p, v->parent->action, v->observation,
-                                   ps.mass, p->d_bpart));
+  CHECK(launch_belief(c, ps.b.v.p, ns.b.v.p, v->parent->action, v->observation, ps.mass,
+                      p->d_bpart));
   HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
                                   ns.mass));
   v->slot = s;
@@ -682,8 +681,7 @@ int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
   pp2_ctx* c = p->ctx;
   const Slot& os = p->slots[root->slot];
   const Slot& ns = p->slots[s];
-  HIPCHK(pp2::launch_belief_update(c->stream, c->g, c->cpt, c->T.v, c->L.v, os.b.v.p,
-                                   ns.b.v.p, a, z, os.mass, p->d_bpart));
+  CHECK(launch_belief(c, os.b.v.p, ns.b.v.p, a, z, os.mass, p->d_bpart));
   HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
                                   ns.mass));
   if (p->ref) CHECK(ref_normalize_slot(p, s));
