@@ -1,0 +1,193 @@
+"""CPU, world_size 2 and 3 (gloo): the resident row-shard scheme that
+pp2_loop_run runs on RCCL shards (pp2_runtime.cpp shard_loop_resident,
+pp2_resident.hip k_loop_resident shard mode + k_shard_mass_vec /
+k_shard_rebase) reproduces the unsharded loop.
+
+Restated on the oracle kernels: every rank computes a *view* of its owned
+rows extended by e rows per side (rows off the grid are zero, and so are
+their model rows); a call of n steps runs in blocks of m <= e steps, each
+after ONE exchange of e halo rows of b and J with the neighbours (the view's
+edge rows go stale by one row per step, so the owned rows stay exact for e
+steps).  The first step of a block divides by the global mass M and scales
+by 2^96; inside a block every `depth` steps the view is rescaled by a power
+of two chosen from the view's own mass (exact, so shards may pick different
+shifts).  At a block boundary and at the end of the call each rank posts
+{owned mass, total shift}, the vector is all-reduced, and every rank rebases
+its rows -- a halo row by its owner's shift -- to the common (minimum) shift,
+the global mass being the rank-ordered sum at that scale.  Values and
+actions must equal the global oracle bit for bit; the normalised belief
+within rel 1e-5 of the fp64-normalised global chain."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _pow2_shift(S):
+    """pp2_resident.hip pow2_shift: the shift bringing S into [2^96, 2^97)."""
+    S = np.float32(S)
+    if not (S > 0) or not np.isfinite(S):
+        return 0
+    e = int(np.frexp(S)[1]) - 1  # S = f * 2^e, f in [1, 2)
+    return min(max(96 - e, 0), 127)
+
+
+def _worker(rank, world, port, name, steps, e, depth, result_q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import torch
+    import torch.distributed as dist
+    from conftest import GAMMA, golden, golden_map
+    from oracle import oracle as O
+    from path_planning_2d_amd import synthetic as S
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        grid = golden_map(name)
+        H, W = grid.shape
+        m = golden("model", name)
+        T = m["T"].reshape(H, W, 81)
+        L = m["L"].reshape(H, W, 16)
+        Cc = m["C"].reshape(H, W, 9)
+        bounds = np.linspace(0, H, world + 1).astype(int)
+        r0, r1 = bounds[rank], bounds[rank + 1]
+        R = r1 - r0
+        V = R + 2 * e  # view rows r0-e .. r1+e-1
+
+        def view(a):  # model rows of the view, zero off the grid
+            out = np.zeros((V,) + a.shape[1:], a.dtype)
+            lo, hi = max(r0 - e, 0), min(r1 + e, H)
+            out[lo - (r0 - e):hi - (r0 - e)] = a[lo:hi]
+            return out
+        Tv = np.ascontiguousarray(view(T).reshape(-1, 9, 9))
+        Lv = np.ascontiguousarray(view(L).reshape(-1, 16))
+        Cv = np.ascontiguousarray(view(Cc).reshape(-1, 9))
+        us, zs, _ = S.synth_trajectory(grid, steps, seed=42)
+        b = view(S.uniform_belief(grid).reshape(H, W))  # mass 1, a common scale
+        J = np.zeros((V, W), np.float32)
+        own = slice(e, e + R)
+        lib = O.lib()
+
+        def exchange(a):  # e halo rows each side (one RCCL group in the product)
+            t = torch.from_numpy(a)
+            ops = []
+            if rank > 0:
+                ops += [dist.P2POp(dist.isend, t[e:2 * e].clone(), rank - 1),
+                        dist.P2POp(dist.irecv, t[0:e], rank - 1)]
+            if rank < world - 1:
+                ops += [dist.P2POp(dist.isend, t[R:R + e].clone(), rank + 1),
+                        dist.P2POp(dist.irecv, t[R + e:V], rank + 1)]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+
+        def mass_vec(shift):  # k_shard_mass_vec + the all-reduce
+            vec = torch.zeros(2 * world, dtype=torch.float64)
+            vec[2 * rank] = float(np.float32(b[own].astype(np.float64).sum()))
+            vec[2 * rank + 1] = float(shift)
+            dist.all_reduce(vec)
+            return vec.numpy()
+
+        def rebase(vec, rows):  # k_shard_rebase over view rows `rows`
+            C = int(min(vec[2 * q + 1] for q in range(world)))
+            M = np.float32(0.0)
+            for q in range(world):
+                M = np.float32(M + np.float32(np.ldexp(np.float32(vec[2 * q]),
+                                                      C - int(vec[2 * q + 1]))))
+            for y in rows:
+                q = rank - 1 if y < e else rank + 1 if y >= e + R else rank
+                if q < 0 or q >= world:
+                    q = rank
+                k = C - int(vec[2 * q + 1])
+                if k:
+                    b[y] = np.ldexp(b[y], k).astype(np.float32)
+            return M
+
+        M = np.float32(1.0)
+        shift, pending = 0, False
+        for i in range(0, steps, e):
+            mm = min(e, steps - i)
+            if pending:
+                vec = mass_vec(shift)
+                exchange(b)
+                exchange(J)
+                M = rebase(vec, range(V))
+            else:
+                exchange(b)
+                exchange(J)
+            shift = 0
+            for t in range(mm):
+                k = i + t
+                if t == 0:
+                    inv = np.float32(np.float32(1.0) / M) * np.float32(2.0 ** 96)
+                elif t % depth == 0:
+                    sh = _pow2_shift(b.astype(np.float64).sum())
+                    shift += sh
+                    inv = np.float32(2.0 ** sh)
+                else:
+                    inv = np.float32(1.0)
+                bo = np.zeros_like(b)
+                lib.orc_belief_update_rows(V, W, Tv, Lv, b.reshape(-1), int(us[k]), int(zs[k]),
+                                           bo.reshape(-1), 1, 0, V)
+                b = (bo * inv).astype(np.float32)
+                Jo = np.zeros_like(J)
+                A = np.zeros(V * W, np.uint8)
+                lib.orc_mdp_sweep_rows(V, W, GAMMA, Tv, Cv, J.reshape(-1), Jo.reshape(-1), A, 0, V)
+                J = Jo
+            pending = True
+        # the close: the global mass at a common scale
+        M = rebase(mass_vec(shift), range(e, e + R))
+        bn = (b[own].astype(np.float64) / float(M)).astype(np.float32)
+        parts = [bn, J[own], A.reshape(V, W)[own]]
+        gathered = []
+        for p in parts:
+            got = [None] * world
+            dist.all_gather_object(got, np.ascontiguousarray(p))
+            gathered.append(np.concatenate(got))
+        if rank == 0:
+            result_q.put(tuple(g.copy() for g in gathered))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,world,steps,e,depth", [
+    ("sparse_map_100x40", 2, 13, 5, 2),
+    ("tile64_sparse_map_100x40", 3, 10, 4, 3),
+])
+def test_resident_shard_scheme_matches_global(name, world, steps, e, depth):
+    import torch.multiprocessing as mp
+    from conftest import GAMMA, assert_rel_close, golden, golden_map
+    from oracle import oracle as O
+    from path_planning_2d_amd import synthetic as S
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, steps, e, depth, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    bs, Js, As = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    grid = golden_map(name)
+    H, W = grid.shape
+    m = golden("model", name)
+    us, zs, _ = S.synth_trajectory(grid, steps, seed=42)
+    b = S.uniform_belief(grid)
+    J = np.zeros(H * W, np.float32)
+    for k in range(steps):
+        b = O.belief_step(H, W, m["T"], m["L"], b, us[k], zs[k], mode="f64")
+        J, A = O.mdp_sweep(H, W, GAMMA, m["T"], m["C"], J)
+    np.testing.assert_array_equal(Js.reshape(-1), J)
+    np.testing.assert_array_equal(As.reshape(-1), A)
+    assert_rel_close(bs.reshape(-1), b, rel=1e-5, msg="resident shard scheme (gloo)")
