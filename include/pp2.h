@@ -416,15 +416,17 @@ typedef struct pp2_rollout pp2_rollout;
 /* copies 1..131072, depth >= 1 */
 int pp2_rollout_create(pp2_rollout** out, pp2_ctx* ctx, int copies, int depth);
 int pp2_rollout_destroy(pp2_rollout* r);
-/* root belief (hw floats) copied into every copy */
+/* root belief (hw floats): every copy starts from it (one fp16 image that
+ * the first step of every run reads for all copies) */
 int pp2_rollout_set_root(pp2_rollout* r, const float* belief);
-/* us, zs: [depth][copies].  Asynchronous. */
+/* us, zs: [depth][copies]; every run starts from the root.  Asynchronous. */
 int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs);
 /* rewards, obs_prob: [depth][copies]; leaf_upper, value: [copies]; any may be
  * NULL.  Synchronises. */
 int pp2_rollout_results(pp2_rollout* r, float* rewards, float* obs_prob,
                         float* leaf_upper, float* value);
-/* normalised fp32 belief of one copy after the run (hw floats) */
+/* normalised fp32 belief of one copy after the run, or the root before any
+ * run (hw floats) */
 int pp2_rollout_get_belief(pp2_rollout* r, int copy, float* belief);
 
 /* ---------------------------------------------------------------- shards
