@@ -914,12 +914,14 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         res_launch_us = e0.elapsed_time(e1) / n_rep * 1e3
+    # a row shard (N >= 2) runs resident launches of up to e steps on its view
+    shard_res = ws > 1 and coded and ctx.resident_tiling()[0] > 0
     ctx.close()
 
     bytes_loop = BYTES_LOOP_CODED if coded else BYTES_LOOP
     bytes_sweep = BYTES_SWEEP_CODED if coded else BYTES_SWEEP
     resident = steps_per_launch >= RESIDENT_STEPS
-    loop_kernel = ("k_loop_resident" if resident else
+    loop_kernel = ("k_loop_resident" if resident or shard_res else
                    "k_loop_pair_coded" if steps_per_launch == 2 else "k_loop_step_coded") \
         if coded else "k_loop_step"
     # the resident loop runs the whole timed trajectory in ceil(steps / 2048) launches
@@ -938,7 +940,8 @@ def main():
     contract_gbs = BYTES_LOOP * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(loop_kernel, cells_per_gpu,
                                        exclude=None if coded else "coded",
-                                       steps=round(spl) if resident else None)
+                                       steps=round(spl) if resident else None) \
+        if not shard_res else (None, "not collected for row-shard views")
 
     c4 = None
     if args.c4_size > 0:
@@ -997,6 +1000,9 @@ def main():
                 "kernel": (f"{loop_kernel} (the whole timed trajectory, {args.steps} fused loop "
                            f"steps, in one launch: one tile of rows per CU resident in LDS)"
                            if resident else
+                           f"{loop_kernel} (row-shard view of the owned rows + e halo rows: "
+                           f"launches of up to e = {steps_per_launch} steps, each after one RCCL "
+                           f"halo exchange and {{mass, shift}} all-reduce)" if shard_res else
                            f"{loop_kernel} (two fused loop steps per launch: belief update + "
                            f"MDP Bellman sweep, twice)" if spl == 2 else
                            f"{loop_kernel} (fused belief update + MDP Bellman sweep)"),
@@ -1004,7 +1010,7 @@ def main():
                 # period is the per-step hand-off latency chain, with HBM, LDS
                 # and VALU all below saturation (sq_counters); the others are
                 # HBM-priced
-                "bound": "latency" if resident and coded else "hbm",
+                "bound": "latency" if (resident or shard_res) and coded else "hbm",
                 "sq_counters": sq_counters() if resident and coded else None,
                 "achieved": loop_gbs,
                 "peak": HBM_PEAK_GBS,
@@ -1024,7 +1030,7 @@ def main():
                          "WRITE_SIZE) per launch: ~8.4 MB per step of them are the edge-row "
                          "granules (2 x 8 KB per tile per step, sc1 stores and loads, which go "
                          "past L2 to the memory side), not cell data"
-                         if resident and coded else
+                         if (resident or shard_res) and coded else
                          "bytes the coded kernel must move per launch: code 2, b 4, b' 4, J 4, "
                          "J' 4, A 1 per cell (a pair launch keeps its intermediate step in "
                          "LDS); launch-latency and LDS bound, see roofline_lds"

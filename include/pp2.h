@@ -161,6 +161,14 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           and the CUs allow).  Values and actions are
  *                           bit-identical to the unsharded grid either way. */
 #define PP2_TUNE_RESIDENT_HALO 9
+/*  PP2_TUNE_RESIDENT_TILE_COLS  tiles of the resident loop: 0 (default) =
+ *                           whole rows; 1 = whole rows always; 2 = two
+ *                           tile columns -- 2-D tiles whose first and last
+ *                           columns cross CUs as well -- wherever they fit
+ *                           (measured slower on a 256 x 2048 rank share of
+ *                           the 2048^2 grid).  Results are
+ *                           bit-identical either way. */
+#define PP2_TUNE_RESIDENT_TILE_COLS 12
 /*  Diagnostics (tests):
  *  PP2_TUNE_RESIDENT_CUS    plan resident launches for at most this many CUs
  *                           (0: all); a grid whose tiles do not fit falls
@@ -207,6 +215,11 @@ int pp2_model_dict_info(pp2_ctx* ctx, int* entries, int* active);
  * tile per CU; unsharded, RCCL row shard or shard-group member), else 1.
  * A query: allocates nothing. */
 int pp2_loop_steps_per_launch(pp2_ctx* ctx, int* steps);
+/* The tiling of the tile-resident loop this context would launch (its grid,
+ * or a row shard's view): tiles (one per CU), rows per tile and tile columns
+ * (1: whole rows; 2: 2-D tiles, PP2_TUNE_RESIDENT_TILE_COLS); all 0 when the
+ * loop does not run resident.  A query: allocates nothing. */
+int pp2_resident_tiling(pp2_ctx* ctx, int* tiles, int* rows_per_tile, int* tile_cols);
 /* Diagnostics: resident launches so far on this context -- tile-resident loop
  * launches (pp2_loop_run) and resident MDP-solve launches (pp2_mdp_solve);
  * either pointer may be NULL.  No reference counterpart. */

@@ -58,6 +58,7 @@ SIGNATURES = {
     "pp2_model_load": [_vp, C.c_char_p],
     "pp2_model_dict_info": [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pp2_loop_steps_per_launch": [_vp, C.POINTER(C.c_int)],
+    "pp2_resident_tiling": [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pp2_resident_launches": [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pp2_resident_status": [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pp2_belief_set": [_vp, _f32p],

@@ -105,6 +105,7 @@ class GridContext:
     TUNE_RESIDENT_HALO = 9
     TUNE_RESIDENT_CUS = 10
     TUNE_RESIDENT_STALL = 11
+    TUNE_RESIDENT_TILE_COLS = 12
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))
@@ -139,6 +140,13 @@ class GridContext:
         n = C.c_int(0)
         call("pp2_loop_steps_per_launch", self._h, C.byref(n))
         return n.value
+
+    def resident_tiling(self):
+        """(tiles, rows per tile, tile columns) of the resident loop on this
+        context, (0, 0, 0) when it does not run resident."""
+        t, r, c = C.c_int(0), C.c_int(0), C.c_int(0)
+        call("pp2_resident_tiling", self._h, C.byref(t), C.byref(r), C.byref(c))
+        return t.value, r.value, c.value
 
     def model_download(self):
         n = self.cells

@@ -173,6 +173,8 @@ struct pp2_ctx {
   int res_fallbacks = 0;           // launches re-run after a timeout (pp2_resident_status)
   int res_stall_tile = -1;         // PP2_TUNE_RESIDENT_STALL (tests)
   int res_cus = 0;                 // PP2_TUNE_RESIDENT_CUS: CUs the plans may use (0: all)
+  int res_tc_pref = 0;             // PP2_TUNE_RESIDENT_TILE_COLS (0: automatic)
+  int res_loop_tc = 0;             // tile columns of the last loop launch (0: fresh buffers)
   // row shards on the resident loop: halo depth per resident
   // launch, the run's power-of-two shift and the {mass, shift} rank vector
   int res_halo = 0;                // PP2_TUNE_RESIDENT_HALO (0: the most the shards allow)

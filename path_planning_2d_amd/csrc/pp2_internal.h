@@ -238,8 +238,13 @@ constexpr int kResidentSyncWords = 16;
 // carries the slot use's tag bit (every handed-over value is finite and
 // >= +0), so every 4-B word validates itself.  The loop hands over b and J.
 constexpr int kResidentGranules = 2;
+// 2-D tiles (tc tile columns of tw = wp / tc cells): a tile's first and last
+// column cross CUs too, one 8-B {b, j} side granule per row, at most
+// kResidentMaxRt rows per tile (rt * tw / 4 <= 1024 lanes, tw >= 256).
+constexpr int kResidentMaxRt = 16;
 struct ResidentPlan {
   int rt = 0, ntiles = 0, threads = 0;
+  int tc = 1;  // tile columns (1: tiles of whole rows)
   size_t lds = 0;
 };
 struct ResidentHead {
@@ -256,6 +261,7 @@ struct ResidentHead {
   float* xch;                // exchange granules, resident_xch_floats(): [step & 1][tile][top, bottom][wave][kResidentGranules][lane] x 16 B
   uint8_t* A;                // actions (view row 0; owned rows stored)
   int n, kstep0, depth, rt, ntiles, nparts;
+  int tc;                    // tile columns (ResidentPlan::tc)
   int own0, own1;            // owned view rows: only they store b', J', A and add to the mass
   int shard;                 // 1: block starts inside the run scale by 2^k from the owned
                              //   mass (no cross-rank reduction), k summed into *scale_out
@@ -308,7 +314,7 @@ struct SweepRun {
   int nsweeps;         // > 0: exactly this many sweeps, no convergence checks
   int stall_tile;      // diagnostic (tests): this tile returns at once, -1 none
 };
-size_t resident_lds_bytes(const Geom& g, int E, int rt);
+size_t resident_lds_bytes(const Geom& g, int E, int rt, int tc);
 // Plans fail (the caller falls back BEFORE launching) unless every tile can
 // be resident at once: occupancy per CU x ncus >= tiles (one 1024-lane
 // workgroup per CU at these LDS sizes).
@@ -316,9 +322,14 @@ bool solve_plan(const Geom& g, int E, int ncus, ResidentPlan* p);
 hipError_t launch_sweep_resident(hipStream_t st, const ResidentPlan& p, const SweepRun& a);
 inline size_t resident_xch_floats(const Geom& g, int ntiles) {
   // [step & 1][tile][top, bottom][wave of row][granule][lane] 16-B granules
-  return (size_t)2 * ntiles * 2 * (g.wp / 256) * kResidentGranules * 64 * 4;
+  // (sized for whole-row tiles, the most), then the 2-D tiles' side granules
+  // [step & 1][tile][left, right][row < kResidentMaxRt] x 8 B
+  return (size_t)2 * ntiles * 2 * (g.wp / 256) * kResidentGranules * 64 * 4 +
+         (size_t)2 * ntiles * 2 * kResidentMaxRt * 2;
 }
-bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p);
+// tc_pref: 0 (automatic) or 1 = whole rows, 2 = two tile columns whenever
+// they fit (else whole rows).
+bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref = 0);
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a);
 // Row-shard boundary kernels (pp2_resident.hip).
 // vec[2 * nranks] := 0 except vec[2 * rank] = mass of the n partials (k_sum_finalize's

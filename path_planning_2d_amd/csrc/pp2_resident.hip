@@ -358,6 +358,67 @@ __device__ __forceinline__ void take_granules(Rsrc r, int o, bool edge, int eo, 
     asm volatile("" ::: "memory");
   }
 }
+// 2-D tiles (tc > 1): a tile's first and last columns cross CUs as well.  The
+// lane holding the first (last) cell of a row publishes {b, j} of that cell as
+// ONE 8-B sc1 store (both words tagged, like the granules) into side granule
+// [slot][tile][0 (first column) / 1 (last)][row], after the top / bottom
+// region; the side lane of the neighbour tile takes the cells of its rows
+// ty-1 .. ty+1 from it (rows -1 / rt from the diagonal tiles' rows rt-1 / 0,
+// so the corners need no granule of their own).  The slot discipline is the
+// granules': a producer rewrites a side slot only after it took the consumer's
+// side cells of the following step, which that consumer published after its
+// loads of the slot returned (the same wave polls, computes and publishes).
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int side_gran(int sbase, int ntiles, int slot, int tl, int side, int r) {
+  return sbase + (((slot * ntiles + tl) * 2 + side) * kResidentMaxRt + r) * 8;
+}
+__device__ __forceinline__ void st_pair(Rsrc r, int off, float b, float j, unsigned bit) {
+  const unsigned m = bit << 31;
+  const u2v t = {__float_as_uint(b) | m, __float_as_uint(j) | m};
+  __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, kSc1);
+}
+// take_granules<2> (when rows) and, on the wave's side lane (sd), the side
+// cells at so[k] (k: rows ty-1 .. ty+1; < 0: off the grid, read as 0) in the
+// same polls, so the two hand-offs cost one round trip.
+__device__ __forceinline__ void take_rows_sides(Rsrc r, bool rows, int o, bool edge, int eo,
+                                                bool sd, const int (&so)[3], int soff, unsigned bit,
+                                                u4v (&g)[2], unsigned (&e)[2], u2v (&s)[3],
+                                                unsigned* err, unsigned* err_host) {
+  const unsigned m = bit << 31;
+  const unsigned long long t0 = wall_clock64();
+  e[0] = e[1] = m;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = u2v{m, m};
+  for (int spin = 0;; ++spin) {
+    if (rows) {
+      g[0] = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, kSc1);
+      g[1] = __builtin_amdgcn_raw_buffer_load_b128(r, o + 1024, 0, kSc1);
+      if (edge) {
+        e[0] = __builtin_amdgcn_raw_buffer_load_b32(r, eo, 0, kSc1);
+        e[1] = __builtin_amdgcn_raw_buffer_load_b32(r, eo + 1024, 0, kSc1);
+      }
+    }
+    if (sd) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (so[k] >= 0) s[k] = __builtin_amdgcn_raw_buffer_load_b64(r, so[k], soff, kSc1);
+    }
+    bool ok = true;
+    if (rows)
+      ok = tagged(g[0], m) && tagged(g[1], m) && (((e[0] ^ m) | (e[1] ^ m)) >> 31) == 0u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ok = ok && (((s[k][0] ^ m) | (s[k][1] ^ m)) >> 31) == 0u;
+    if (__all(ok)) break;
+    if ((spin & 7) == 7) {
+      if (ld_flag(err) != 0u || wall_clock64() - t0 > kSpinTicks) {
+        if ((threadIdx.x & 63) == 0) raise_err(err, err_host);
+        return;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  }
+}
 // One window row from the lane's aligned quad m and the edge dword e of the
 // lane's wave-edge neighbour (lanes 0 / 63), the others by DPP wave shifts.
 __device__ __forceinline__ void row_quad(const float (&m)[4], float e, float (&v)[6]) {
@@ -373,16 +434,21 @@ struct Trajectory {
   uint8_t uz[CAP];  // u | z << 4 per step
 };
 
-template <int CAP>
+// TC: tile columns (a compile-time constant, so the whole-row instance has no
+// side-lane code at all)
+template <int CAP, int TC>
 __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
                                                            const Trajectory<CAP> tr) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int wp = a.g.wp, rows = a.g.rows, tpr = wp >> 2, wpr = wp >> 8;
-  const int xs = wp + 4;                // padded LDS row stride
+  // a tile: rt rows x tw columns (tc tile columns per row of tiles)
+  constexpr int tc = TC;
+  const int wp = a.g.wp, rows = a.g.rows, tw = wp / tc;
+  const int tpr = tw >> 2, wpr = tw >> 8;  // lanes, waves per tile row
+  const int xs = tw + 4;                // padded LDS row stride
   const int bufn = 4 + a.rt * xs;       // one padded tile buffer
   // LDS: class tables (QR, LT: constant offsets), factored sweep rows (QT, CT:
   // constant offsets; IW), class planes, b buffers 0, 1, J buffers 0, 1
-  const int prows = a.rt + 2, ps = wp + 8;
+  const int prows = a.rt + 2, ps = tw + 8;
   float* sTC = lds + lds_span(kResTab);  // (stage_rows writes up to the span)
   uint8_t* sP = reinterpret_cast<uint8_t*>(sTC + lds_span(rows_floats(a.E, true)));
   float* sB0 = reinterpret_cast<float*>(sP) + lds_span(9 * prows * ps / 4);
@@ -390,6 +456,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   if (tile == a.stall_tile) return;  // diagnostic: a tile that never arrives
+  const int trow = tile / tc, cx = tile - trow * tc, gx = cx * tw;  // tile row, column, x
   PP2_RP(0);
   // a chained launch after one that timed out does nothing: its inputs are
   // that launch's garbage outputs (resident_settle re-runs both)
@@ -398,14 +465,21 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   // wave-uniform: a row holds wpr whole waves (wp % 256 == 0)
   const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x / tpr);
   const int wj = __builtin_amdgcn_readfirstlane((threadIdx.x % tpr) >> 6);
-  const int x0 = (threadIdx.x % tpr) * 4;
-  const int y = tile * a.rt + ty;
+  const int x0 = (threadIdx.x % tpr) * 4;  // (tile-relative)
+  const int y = trow * a.rt + ty;
   const bool valid = y < rows;
   const bool own = y >= a.own0 && y < a.own1;  // (a shard's view: owned rows only)
-  // the tile's first row reads the row above from tile - 1 and publishes
-  // itself for it; its last row likewise with tile + 1
-  const bool nb_up = valid && ty == 0 && tile > 0;
+  // the tile's first row reads the row above from tile - tc and publishes
+  // itself for it; its last row likewise with tile + tc
+  const bool nb_up = valid && ty == 0 && trow > 0;
   const bool nb_dn = valid && ty == a.rt - 1 && y + 1 < rows;
+  // 2-D tiles: the first wave of a row takes / publishes the left neighbour's
+  // side cells on lane 0, the last wave the right one's on lane 63 (wpr >= 2:
+  // never both in one wave)
+  const bool sd_l = valid && wj == 0 && cx > 0;
+  const bool sd_r = valid && wj == wpr - 1 && cx + 1 < tc;
+  const bool sd_lane = (sd_l && lane == 0) || (sd_r && lane == 63);
+  const int sbase = 2 * a.ntiles * 2 * (wp >> 8) * kResidentGranules * 64 * 16;  // side region
   unsigned* const err = a.sync + kResidentSyncErr;
   const Rsrc rx = make_rsrc(a.xch);
   auto sbuf = [&](int k, int slot) { return sB0 + (2 * k + slot) * bufn + 4; };
@@ -419,11 +493,34 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       st_quad(rx, o, b, bit);
       st_quad(rx, o + 1024, j, bit);
     }
+    if (sd_lane) {
+      const int o = side_gran(sbase, a.ntiles, slot, tile, sd_l ? 0 : 1, ty);
+      if (sd_l) st_pair(rx, o, b[0], j[0], bit);
+      else st_pair(rx, o, b[3], j[3], bit);
+    }
   };
   // ... and the neighbour's row (tile tl, side) of the slot use with tag bit
   // `bit`: poll its granules over this wave's columns (lanes 0 / 63 also the
   // neighbour waves' edge cells) until every word carries the bit
-  auto take = [&](int slot, int tl, int side, unsigned bit, float (&vb)[6], float (&vj)[6]) {
+  // The side lane's granules of rows ty-1 .. ty+1 in slot 0 (rows -1 / rt from
+  // the diagonal tiles; < 0 off the grid): fixed for the run, the slot's
+  // offset goes in the loads' scalar offset.
+  int so[3] = {-1, -1, -1};
+  if (tc > 1 && sd_lane) {
+    const int dir = sd_l ? -1 : 1, nside = sd_l ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int rr = ty + k - 1, yy = y + k - 1;
+      if (yy < 0 || yy >= rows) continue;
+      const int tl2 = rr < 0 ? tile - tc + dir : rr >= a.rt ? tile + tc + dir : tile + dir;
+      so[k] = side_gran(sbase, a.ntiles, 0, tl2, nside, rr < 0 ? a.rt - 1 : rr >= a.rt ? 0 : rr);
+    }
+  }
+  const int sslot = a.ntiles * 2 * kResidentMaxRt * 8;  // bytes per side slot
+  // (rows: tile tl's row `side`; sides: this wave's side cells of rows ty-1 ..
+  // ty+1 into sb / sj when sd -- one poll for both)
+  auto take = [&](int slot, bool rows_in, int tl, int side, bool sd, unsigned bit, float (&vb)[6],
+                  float (&vj)[6], float (&sb)[3], float (&sj)[3]) {
     const bool el = lane == 0 && wj > 0, er = lane == 63 && wj + 1 < wpr;
     const int o = xch_gran(a.ntiles, wpr, slot, tl, side, wj, 0, lane);
     // lane 0: b3 / j3 of wave wj-1's lane 63 (word 3 of its granules 0, 1);
@@ -432,11 +529,22 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
                       : xch_gran(a.ntiles, wpr, slot, tl, side, wj + 1, 0, 0);
     u4v g[2];
     unsigned e[2];
-    take_granules(rx, o, el || er, eo, bit, g, e, err, a.err_host);
-    const float mb[4] = {untag(g[0][0]), untag(g[0][1]), untag(g[0][2]), untag(g[0][3])};
-    const float mj[4] = {untag(g[1][0]), untag(g[1][1]), untag(g[1][2]), untag(g[1][3])};
-    row_quad(mb, (el || er) ? untag(e[0]) : 0.0f, vb);
-    row_quad(mj, (el || er) ? untag(e[1]) : 0.0f, vj);
+    u2v s[3];
+    take_rows_sides(rx, rows_in, o, el || er, eo, sd && sd_lane, so, slot * sslot, bit, g, e, s,
+                    err, a.err_host);
+    if (rows_in) {
+      const float mb[4] = {untag(g[0][0]), untag(g[0][1]), untag(g[0][2]), untag(g[0][3])};
+      const float mj[4] = {untag(g[1][0]), untag(g[1][1]), untag(g[1][2]), untag(g[1][3])};
+      row_quad(mb, (el || er) ? untag(e[0]) : 0.0f, vb);
+      row_quad(mj, (el || er) ? untag(e[1]) : 0.0f, vj);
+    }
+    if (sd) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        sb[k] = untag(s[k][0]);
+        sj[k] = untag(s[k][1]);
+      }
+    }
   };
 
   // ---- prologue: dictionary, zero pads, codes, the tile's b / J into LDS
@@ -469,7 +577,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   // and L class bytes
   uint32_t cc[4] = {0u, 0u, 0u, 0u}, iwr[4][3], lx4 = 0u;
   if (valid) {
-    const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)y * wp + x0);
+    const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)y * wp + gx + x0);
     cc[0] = m.x & 0xffffu; cc[1] = m.x >> 16; cc[2] = m.y & 0xffffu; cc[3] = m.y >> 16;
     const uint8_t* lx = reinterpret_cast<const uint8_t*>(a.rfact + kResLX);
 #pragma unroll
@@ -482,13 +590,14 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
     const uint4 w = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * cc[k]);
     iwr[k][0] = w.x; iwr[k][1] = w.y; iwr[k][2] = w.z;
   }
-  // class planes of rows tile*rt-1 .. tile*rt+rt: byte x+4 of plane a, row r
-  // = 16 * class of cell (y, x) for action a (0 off the grid and in the pads)
+  // class planes of rows trow*rt-1 .. trow*rt+rt: byte x+4 of plane a, row r
+  // = 16 * class of cell (y, gx + x) for action a (0 off the grid; the pads
+  // hold the side neighbours' cells x = -1 / tw, 0 at the grid's x edges)
   for (int i = threadIdx.x; i < prows * tpr; i += blockDim.x) {
-    const int r = i / tpr, xq = (i % tpr) * 4, yy = tile * a.rt + r - 1;
+    const int r = i / tpr, xq = (i % tpr) * 4, yy = trow * a.rt + r - 1;
     uint32_t pl[9] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     if (yy >= 0 && yy < rows) {
-      const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)yy * wp + xq);
+      const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)yy * wp + gx + xq);
       const uint32_t c4[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -505,18 +614,30 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       *reinterpret_cast<uint32_t*>(sP + (q * prows + r) * ps + 4 + xq) = pl[q];
   }
   for (int i = threadIdx.x; i < 9 * prows; i += blockDim.x) {
-    *reinterpret_cast<uint32_t*>(sP + i * ps) = 0u;
-    *reinterpret_cast<uint32_t*>(sP + i * ps + 4 + wp) = 0u;
+    const int q = i / prows, yy = trow * a.rt + i % prows - 1;
+    uint32_t lp = 0u, rp = 0u;
+    if (yy >= 0 && yy < rows) {
+      auto cls = [&](int x) {
+        const uint4 w = *reinterpret_cast<const uint4*>(
+            sTC + kFactIW + 4 * a.code[(long long)yy * wp + x]);
+        return __builtin_amdgcn_ubfe(q < 4 ? w.x : q < 8 ? w.y : w.z, 8 * (q % 4), 8);
+      };
+      if (gx > 0) lp = cls(gx - 1) << 24;  // byte 3: x = -1
+      if (gx + tw < wp) rp = cls(gx + tw);  // byte 0: x = tw
+    }
+    *reinterpret_cast<uint32_t*>(sP + i * ps) = lp;
+    *reinterpret_cast<uint32_t*>(sP + i * ps + 4 + tw) = rp;
   }
   PP2_RP(4);
   if (prior_err != 0u) return;  // (uniform: before any global store)
+  const bool bnd = nb_up || nb_dn || sd_l || sd_r;  // waves that cross CUs
   if (valid) {
-    const long long off = (long long)y * wp + x0;
+    const long long off = (long long)y * wp + gx + x0;
     const f4a b = *reinterpret_cast<const f4a*>(a.b_in + off);
     const f4a j = *reinterpret_cast<const f4a*>(a.j_in + off);
     *reinterpret_cast<f4a*>(sbuf(0, 0) + ty * xs + x0) = b;
     *reinterpret_cast<f4a*>(sbuf(1, 0) + ty * xs + x0) = j;
-    if (nb_up || nb_dn) {
+    if (bnd) {
       const float bv[4] = {b[0], b[1], b[2], b[3]}, jv[4] = {j[0], j[1], j[2], j[3]};
       publish(1, bv, jv, (a.slot_use[1] + 1u) & 1u);
     }
@@ -549,8 +670,8 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   if (start0)
     inv = (1.0f / (a.in_partials ? sS[0] : a.in_sum ? *a.in_sum : 1.0f)) * a.bscale;
 
-  const int wave_part0 = (int)(((long long)tile * a.rt * tpr) >> 6);  // dense wave of wave 0
-  const int pi = wave_part0 + wave;
+  // the dense kernels' partial of this wave's 256 cells (row y, x gx + 256 wj)
+  const int pi = y * (wp >> 8) + cx * wpr + wj;
   unsigned arrivals = a.arrive_base;
   int shift = 0;  // shard runs: the power-of-two shifts of the block starts so far
   float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, best[4] = {0.0f, 0.0f, 0.0f, 0.0f}, local = 0.0f;
@@ -571,16 +692,18 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
     if (t > 0 && !bs) inv = 1.0f;
     PP2_RT(0);
     local = 0.0f;
-    const bool bnd = nb_up || nb_dn;
     // one quad of step t: window rows from LDS (step t-1), the neighbour rows
     // of step t-1, or 0 off the grid; b' before the scale in p
     auto step_quad = [&]() {
       Win6 wb, wj;
+      float sb[3] = {0.0f, 0.0f, 0.0f}, sj[3] = {0.0f, 0.0f, 0.0f};
+      const bool sd = sd_l || sd_r;
+      const unsigned bit = use[co] & 1u;
       if (ty > 0) {
         row_lds(sbuf(0, ci) + (ty - 1) * xs, x0, wb.v[0]);
         row_lds(sbuf(1, ci) + (ty - 1) * xs, x0, wj.v[0]);
-      } else if (nb_up) {  // the tile above's last row
-        take(co, tile - 1, 1, use[co] & 1u, wb.v[0], wj.v[0]);
+      } else if (nb_up) {  // the tile above's last row (and the side cells)
+        take(co, true, tile - tc, 1, sd, bit, wb.v[0], wj.v[0], sb, sj);
       } else {
         row_zero(wb.v[0]);
         row_zero(wj.v[0]);
@@ -590,11 +713,24 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       if (ty + 1 < a.rt && y + 1 < rows) {
         row_lds(sbuf(0, ci) + (ty + 1) * xs, x0, wb.v[2]);
         row_lds(sbuf(1, ci) + (ty + 1) * xs, x0, wj.v[2]);
-      } else if (nb_dn) {  // the tile below's first row
-        take(co, tile + 1, 0, use[co] & 1u, wb.v[2], wj.v[2]);
+      } else if (nb_dn) {  // the tile below's first row (and the side cells)
+        take(co, true, tile + tc, 0, sd && !nb_up, bit, wb.v[2], wj.v[2], sb, sj);
       } else {
         row_zero(wb.v[2]);
         row_zero(wj.v[2]);
+      }
+      if (sd && !nb_up && !nb_dn) take(co, false, tile, 0, true, bit, wb.v[1], wj.v[1], sb, sj);
+      if (sd_lane) {  // the side neighbour's cells x = -1 (lane 0) / tw (lane 63)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          if (sd_l) {
+            wb.v[k][0] = sb[k];
+            wj.v[k][0] = sj[k];
+          } else {
+            wb.v[k][5] = sb[k];
+            wj.v[k][5] = sj[k];
+          }
+        }
       }
       PP2_RT(1);
       belief_any(u, sP, prows, ps, ty, x0, lx4, z, wb, p);
@@ -669,7 +805,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   // ---- the last step: b, J, A of the (owned) rows and the owned mass
   // partials (a shard's halo rows are its neighbours' rows)
   if (own) {
-    const long long off = (long long)y * wp + x0;
+    const long long off = (long long)y * wp + gx + x0;
     store4<true>(a.b_out + off, p);
     store_ja<true>(a.j_out, a.A, off, best, arg);
   }
@@ -864,33 +1000,39 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
 
 }  // namespace
 
-size_t resident_lds_bytes(const Geom& g, int E, int rt) {
+size_t resident_lds_bytes(const Geom& g, int E, int rt, int tc) {
+  const int tw = g.wp / tc;
   return ((size_t)lds_span(kResTab) + lds_span(rows_floats(E, true)) +
-          lds_span(9 * (rt + 2) * (g.wp + 8) / 4) + 4 * (4 + (size_t)rt * (g.wp + 4)) + 16) *
+          lds_span(9 * (rt + 2) * (tw + 8) / 4) + 4 * (4 + (size_t)rt * (tw + 4)) + 16) *
          sizeof(float);
 }
 
-bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p) {
-  if (E <= 0 || g.rows <= 0 || g.wp % 256 != 0 || ncus <= 0) return false;
-  const int rt = (g.rows + ncus - 1) / ncus;
-  const long long threads = (long long)rt * (g.wp / 4);
-  if (threads > 1024) return false;
-  const size_t lds = resident_lds_bytes(g, E, rt);
+// The plan with tc tile columns: rt rows per tile so that the tiles fit the
+// CUs, or false.
+static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPlan* p) {
+  if (tc < 1 || tc > 2 || g.wp % (256 * tc) != 0 || (tc > 1 && g.wp / tc < 512) || ncus < tc) return false;
+  const int rt = (g.rows + ncus / tc - 1) / (ncus / tc);
+  const long long threads = (long long)rt * (g.wp / tc / 4);
+  if (threads > 1024 || rt > kResidentMaxRt) return false;
+  const size_t lds = resident_lds_bytes(g, E, rt, tc);
   if (lds > kDictLdsMaxBytes) return false;
-  static unsigned long long attr[2] = {0, 0};
-  allow_lds(reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps>), attr[0]);
-  allow_lds(reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps>), attr[1]);
+  static unsigned long long attr[4] = {0, 0, 0, 0};
+  const void* kshort = tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 1>)
+                               : reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 2>);
+  const void* klong = tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 1>)
+                              : reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 2>);
+  allow_lds(kshort, attr[2 * (tc - 1)]);
+  allow_lds(klong, attr[2 * (tc - 1) + 1]);
   int nb = 0, nb2 = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_loop_resident<kResidentMaxSteps>,
-                                                   (int)threads, lds) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, k_loop_resident<kResidentShortSteps>,
-                                                   (int)threads, lds) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, klong, (int)threads, lds) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, kshort, (int)threads, lds) != hipSuccess ||
       nb < 1 || nb2 < 1) {
     (void)hipGetLastError();
     return false;
   }
   p->rt = rt;
-  p->ntiles = (g.rows + rt - 1) / rt;
+  p->tc = tc;
+  p->ntiles = (g.rows + rt - 1) / rt * tc;
   p->threads = (int)threads;
   p->lds = lds;
   // co-residency, checked before any launch: every tile must hold a CU slot
@@ -901,8 +1043,26 @@ bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p) {
   return (long long)std::min(nb, nb2) * ncus >= p->ntiles;
 }
 
+// Whole-row tiles unless two tile columns are asked for (tc_pref 2) and fit.
+// 2-D tiles give a 256-row share of the 2048^2
+// grid 4 x 1024 tiles instead of 2 x 2048 (interior waves that overlap the
+// hand-off wait), but measured slower on it: 5.4 vs 5.0 us per step
+// (tools/ab_tile_cols.py) -- every tile then waits on up to
+// five neighbours per step instead of two.
+bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref) {
+  ResidentPlan p1, p2;
+  const bool ok1 = resident_plan_tc(g, E, ncus, 1, &p1);
+  const bool ok2 = tc_pref == 2 && resident_plan_tc(g, E, ncus, 2, &p2);
+  if (ok2) {
+    *p = p2;
+    return true;
+  }
+  if (ok1) *p = p1;
+  return ok1;
+}
+
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a) {
-  if (a.n < 1 || a.n > kResidentMaxSteps || a.ntiles != p.ntiles || a.rt != p.rt ||
+  if (a.n < 1 || a.n > kResidentMaxSteps || a.ntiles != p.ntiles || a.rt != p.rt || a.tc != p.tc ||
       a.depth < 1 || a.depth > kResidentRing - 2 || a.own0 < 0 || a.own1 > a.g.rows ||
       a.own0 >= a.own1 || a.b_out == a.b_in || a.j_out == a.j_in ||
       (a.in_partials && a.in_partials == a.out_partials))
@@ -911,13 +1071,21 @@ hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const Res
   if (a.n <= kResidentShortSteps) {
     Trajectory<kResidentShortSteps> tr{};
     std::memcpy(tr.uz, a.uz, (size_t)a.n);
-    hipLaunchKernelGGL(k_loop_resident<kResidentShortSteps>, dim3(p.ntiles), dim3(p.threads),
-                       p.lds, st, h, tr);
+    if (p.tc == 1)
+      hipLaunchKernelGGL((k_loop_resident<kResidentShortSteps, 1>), dim3(p.ntiles),
+                         dim3(p.threads), p.lds, st, h, tr);
+    else
+      hipLaunchKernelGGL((k_loop_resident<kResidentShortSteps, 2>), dim3(p.ntiles),
+                         dim3(p.threads), p.lds, st, h, tr);
   } else {
     Trajectory<kResidentMaxSteps> tr;
     std::memcpy(tr.uz, a.uz, sizeof tr.uz);
-    hipLaunchKernelGGL(k_loop_resident<kResidentMaxSteps>, dim3(p.ntiles), dim3(p.threads),
-                       p.lds, st, h, tr);
+    if (p.tc == 1)
+      hipLaunchKernelGGL((k_loop_resident<kResidentMaxSteps, 1>), dim3(p.ntiles), dim3(p.threads),
+                         p.lds, st, h, tr);
+    else
+      hipLaunchKernelGGL((k_loop_resident<kResidentMaxSteps, 2>), dim3(p.ntiles), dim3(p.threads),
+                         p.lds, st, h, tr);
   }
   return hipGetLastError();
 }

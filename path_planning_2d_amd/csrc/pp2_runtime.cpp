@@ -891,6 +891,7 @@ static bool resident_buffers(pp2_ctx* c, const pp2::ResidentPlan& p) {
     return false;
   }
   c->res_ntiles = p.ntiles;
+  c->res_loop_tc = 0;  // fresh (zero) exchange rows: any tile layout may start
   c->res_slot[0] = c->res_slot[1] = c->res_slot[2] = c->res_slot[3] = 0;
   c->res_arrive = 0;
   return true;
@@ -928,7 +929,8 @@ static bool resident_plan_for(pp2_ctx* c, int e) {
     c->res_view_e = e;
     c->res_ok = false;
     pp2::ResidentPlan p;
-    if (!pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p)) return false;
+    if (!pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p, c->res_tc_pref))
+      return false;
     c->res_plan = p;
     c->res_ok = true;
   }
@@ -1168,14 +1170,25 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
   return PP2_OK;
 }
 
-// The fields of a loop run shared by the unsharded and shard launches.
-static void run_common(pp2_ctx* c, const pp2::ResidentPlan& p, pp2::ResidentRun& a) {
+// The fields of a loop run shared by the unsharded and shard launches.  A
+// plan with another tile layout than the previous loop launch (same tile
+// count: whole-row vs 2-D tiles) finds granules of the old layout in its
+// exchange rows, whose tag bits could match: the loop region is cleared and
+// its slot uses restart, as in freshly allocated buffers.
+static int run_common(pp2_ctx* c, const pp2::ResidentPlan& p, pp2::ResidentRun& a) {
+  if (c->res_loop_tc != 0 && c->res_loop_tc != p.tc) {
+    HIPCHK(hipMemsetAsync(c->res_xch, 0,
+                          pp2::resident_xch_floats(c->g, c->res_ntiles) * sizeof(float), c->stream));
+    c->res_slot[0] = c->res_slot[1] = 0;
+  }
+  c->res_loop_tc = p.tc;
   a.gamma = c->gamma;
   a.E = c->dict_n;
   a.rows = c->d_rows;
   a.rfact = c->d_rfact;
   a.xch = c->res_xch;
   a.rt = p.rt;
+  a.tc = p.tc;
   a.ntiles = p.ntiles;
   a.ring = c->res_ring;
   a.sync = c->res_sync;
@@ -1183,6 +1196,7 @@ static void run_common(pp2_ctx* c, const pp2::ResidentPlan& p, pp2::ResidentRun&
   a.slot_use[1] = c->res_slot[1];
   a.arrive_base = c->res_arrive;
   a.stall_tile = c->res_stall_tile;
+  return PP2_OK;
 }
 
 // n loop steps in ceil(n / kResidentMaxSteps) resident launches, with the
@@ -1207,7 +1221,7 @@ static int loop_resident(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs
     const int bc = c->bcur, jc = c->jcur;
     const bool start0 = c->kstep == 0;
     const bool fold = start0 && c->pending[bc];
-    run_common(c, p, a);
+    CHECK(run_common(c, p, a));
     a.g = c->g;
     a.code = c->d_code;
     a.b_in = c->b[bc].v.p;
@@ -1319,7 +1333,7 @@ int pp2rt::shard_resident_e(pp2_ctx* c) {
   int e = shard_resident_depth(c);
   for (; e >= 1; --e) {
     pp2::ResidentPlan p;
-    if (pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p)) break;
+    if (pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p, c->res_tc_pref)) break;
   }
   c->res_e_dict = c->dict_n;
   c->res_e = e;
@@ -1379,7 +1393,7 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
   const int depth = std::min(c->norm_block, pp2::kResidentRing - 2);
   std::unique_ptr<pp2::ResidentRun> run(new pp2::ResidentRun());
   pp2::ResidentRun& a = *run;
-  run_common(c, p, a);
+  CHECK(run_common(c, p, a));
   a.g = gv;
   a.code = c->d_code - sh;
   a.b_in = c->b[bc].v.p - sh;
@@ -1596,6 +1610,11 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
       if (value < 0) return set_err(PP2_EINVAL, "resident CUs %d < 0", value);
       c->res_cus = value;
       c->res_plan_e = c->sol_plan_e = c->res_e_dict = -1;
+      return PP2_OK;
+    case PP2_TUNE_RESIDENT_TILE_COLS:
+      if (value < 0 || value > 2) return set_err(PP2_EINVAL, "tile columns %d not in [0, 2]", value);
+      c->res_tc_pref = value;
+      c->res_plan_e = c->res_e_dict = -1;
       return PP2_OK;
     case PP2_TUNE_RESIDENT_HALO:
       if (value < 0 || value > c->g.halo)
@@ -1849,6 +1868,23 @@ int pp2_loop_steps_per_launch(pp2_ctx* c, int* steps) {
     *steps = resident_model_ok(c) && resident_plan_for(c, 0) ? pp2::kResidentMaxSteps
              : pairs_apply(c) ? 2 : 1;
   }
+  return PP2_OK;
+}
+
+int pp2_resident_tiling(pp2_ctx* c, int* tiles, int* rows_per_tile, int* tile_cols) {
+  CHECK(check_ctx(c));
+  DeviceGuard dg(c->device);
+  int e = 0;
+  bool ok;
+  if (c->comm || c->group) {
+    e = shard_resident_e(c);
+    ok = e > 0 && resident_plan_for(c, e);
+  } else {
+    ok = resident_model_ok(c) && resident_plan_for(c, 0);
+  }
+  if (tiles) *tiles = ok ? c->res_plan.ntiles : 0;
+  if (rows_per_tile) *rows_per_tile = ok ? c->res_plan.rt : 0;
+  if (tile_cols) *tile_cols = ok ? c->res_plan.tc : 0;
   return PP2_OK;
 }
 

@@ -83,6 +83,53 @@ def test_resident_equals_single_steps(pp2, H, W, block):
             _same(a, b, f"after {hi} steps")
 
 
+# 2-D tiles (two tile columns, PP2_TUNE_RESIDENT_TILE_COLS 2): 512 x 2048 (the
+# view of a 256-row rank share of config 4's 2048^2 grid: 4 x 1024 tiles
+# instead of 2 x 2048), a partial last tile row (301 rows in 3-row tiles), a
+# padded width (200 x 1022) and 256 x 2048
+GEOMS_2D = [(512, 2048, 2), (301, 1024, 2), (200, 1022, 2), (256, 2048, 2)]
+
+
+@pytest.mark.parametrize("block", [8, 1])
+@pytest.mark.parametrize("H,W,tc", GEOMS_2D)
+def test_resident_2d_tiles_equal_single_steps(pp2, H, W, tc, block):
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, H, W, block, H * 5 + W)
+    with a, b:
+        if tc:
+            a.set_tuning(a.TUNE_RESIDENT_TILE_COLS, tc)
+        tiles, rt, cols = a.resident_tiling()
+        assert cols == 2 and tiles <= 256, (tiles, rt, cols)
+        us, zs, _ = S.synth_trajectory(grid, 40, seed=6)
+        launches = 0
+        for lo, hi in ((0, 2), (2, 5), (5, 6), (6, 16), (16, 40)):
+            a.loop_run(us[lo:hi], zs[lo:hi])
+            b.loop_run(us[lo:hi], zs[lo:hi])
+            a.synchronize()
+            launches += hi - lo >= 2
+            assert a.resident_launches()[0] == launches
+            assert a.resident_status()[0] == 0, "a resident launch fell back"
+            _same(a, b, f"after {hi} steps")
+
+
+def test_resident_tiling_switch_same_tile_count(pp2):
+    """256 x 2048 runs 256 tiles either way (1 x 2048 whole rows, 2 x 1024 2-D
+    tiles): switching the tiling between runs on one context clears the
+    exchange rows (their stale granules would carry matching tag bits)."""
+    from path_planning_2d_amd import synthetic as S
+    grid, a, b = _pair(pp2, 256, 2048, 8, 17)
+    with a, b:
+        us, zs, _ = S.synth_trajectory(grid, 60, seed=4)
+        for k, (lo, hi) in enumerate(((0, 7), (7, 20), (20, 33), (33, 60))):
+            a.set_tuning(a.TUNE_RESIDENT_TILE_COLS, 1 + k % 2)
+            assert a.resident_tiling() == (256, 1 + k % 2, 1 + k % 2)
+            a.loop_run(us[lo:hi], zs[lo:hi])
+            b.loop_run(us[lo:hi], zs[lo:hi])
+            a.synchronize()
+            assert a.resident_status()[0] == 0, "a resident launch fell back"
+            _same(a, b, f"after {hi} steps")
+
+
 def test_resident_interleaved_with_other_ops(pp2):
     """Single loop steps, belief-only updates, sweeps and a belief_set between
     resident runs: the context's pipeline state (pending masses, block phase,
