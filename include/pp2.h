@@ -162,12 +162,13 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           bit-identical to the unsharded grid either way. */
 #define PP2_TUNE_RESIDENT_HALO 9
 /*  PP2_TUNE_RESIDENT_TILE_COLS  tiles of the resident loop: 0 (default) =
- *                           whole rows; 1 = whole rows always; 2 = two
- *                           tile columns -- 2-D tiles whose first and last
- *                           columns cross CUs as well -- wherever they fit
- *                           (measured slower on a 256 x 2048 rank share of
- *                           the 2048^2 grid).  Results are
- *                           bit-identical either way. */
+ *                           whole rows, or two tile columns (2-D tiles whose
+ *                           first and last columns cross CUs as well) when
+ *                           whole-row tiles would hold fewer than 4 rows and
+ *                           2-D tiles hold 4 or more (a 256 x 2048 rank share
+ *                           of the 2048^2 grid on its 512-row view); 1 = whole
+ *                           rows always; 2 = two tile columns wherever they
+ *                           fit.  Results are bit-identical either way. */
 #define PP2_TUNE_RESIDENT_TILE_COLS 12
 /*  Diagnostics (tests):
  *  PP2_TUNE_RESIDENT_CUS    plan resident launches for at most this many CUs

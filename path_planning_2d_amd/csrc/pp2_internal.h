@@ -327,8 +327,9 @@ inline size_t resident_xch_floats(const Geom& g, int ntiles) {
   return (size_t)2 * ntiles * 2 * (g.wp / 256) * kResidentGranules * 64 * 4 +
          (size_t)2 * ntiles * 2 * kResidentMaxRt * 2;
 }
-// tc_pref: 0 (automatic) or 1 = whole rows, 2 = two tile columns whenever
-// they fit (else whole rows).
+// tc_pref: 0 = automatic (two tile columns when whole-row tiles would hold
+// fewer than 4 rows and 2-D tiles hold 4 or more), 1 = whole rows, 2 = two
+// tile columns whenever they fit (and whole rows do: else no plan changes).
 bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref = 0);
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a);
 // Row-shard boundary kernels (pp2_resident.hip).

@@ -464,8 +464,12 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // wave-uniform: a row holds wpr whole waves (wp % 256 == 0)
   const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x / tpr);
-  const int wj = __builtin_amdgcn_readfirstlane((threadIdx.x % tpr) >> 6);
-  const int x0 = (threadIdx.x % tpr) * 4;  // (tile-relative)
+  // 2-D tiles: a row's column waves rotate with the row, so that the side
+  // waves (which wait on a neighbour tile) of consecutive rows land on
+  // different SIMDs (wave w runs on SIMD w % 4) instead of all on one
+  const int wraw = __builtin_amdgcn_readfirstlane((threadIdx.x % tpr) >> 6);
+  const int wj = tc > 1 ? __builtin_amdgcn_readfirstlane((wraw + ty) % wpr) : wraw;
+  const int x0 = wj * 256 + lane * 4;  // (tile-relative)
   const int y = trow * a.rt + ty;
   const bool valid = y < rows;
   const bool own = y >= a.own0 && y < a.own1;  // (a shard's view: owned rows only)
@@ -1043,17 +1047,17 @@ static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPla
   return (long long)std::min(nb, nb2) * ncus >= p->ntiles;
 }
 
-// Whole-row tiles unless two tile columns are asked for (tc_pref 2) and fit.
-// 2-D tiles give a 256-row share of the 2048^2
-// grid 4 x 1024 tiles instead of 2 x 2048 (interior waves that overlap the
-// hand-off wait), but measured slower on it: 5.4 vs 5.0 us per step
-// (tools/ab_tile_cols.py) -- every tile then waits on up to
-// five neighbours per step instead of two.
+// Whole-row tiles, or two tile columns when whole rows would give tiles of
+// fewer than 4 rows -- every row an edge row, so every wave of the CU waits
+// on a neighbour -- and 2-D tiles hold 4 or more (tc_pref 0), or whenever they
+// fit (tc_pref 2).  A 256-row share of the 2048^2 grid (its 512-row view)
+// then runs 4 x 1024 tiles instead of 2 x 2048: 4.89 vs 5.03 us per step
+// (tools/ab_tile_cols.py).
 bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref) {
   ResidentPlan p1, p2;
   const bool ok1 = resident_plan_tc(g, E, ncus, 1, &p1);
-  const bool ok2 = tc_pref == 2 && resident_plan_tc(g, E, ncus, 2, &p2);
-  if (ok2) {
+  const bool ok2 = tc_pref != 1 && resident_plan_tc(g, E, ncus, 2, &p2);
+  if (ok2 && ok1 && (tc_pref == 2 || (p1.rt < 4 && p2.rt >= 4))) {
     *p = p2;
     return true;
   }

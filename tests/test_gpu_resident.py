@@ -83,11 +83,11 @@ def test_resident_equals_single_steps(pp2, H, W, block):
             _same(a, b, f"after {hi} steps")
 
 
-# 2-D tiles (two tile columns, PP2_TUNE_RESIDENT_TILE_COLS 2): 512 x 2048 (the
-# view of a 256-row rank share of config 4's 2048^2 grid: 4 x 1024 tiles
-# instead of 2 x 2048), a partial last tile row (301 rows in 3-row tiles), a
-# padded width (200 x 1022) and 256 x 2048
-GEOMS_2D = [(512, 2048, 2), (301, 1024, 2), (200, 1022, 2), (256, 2048, 2)]
+# 2-D tiles (two tile columns, PP2_TUNE_RESIDENT_TILE_COLS): the automatic
+# choice on 512 x 2048 (the view of a 256-row rank share of config 4's 2048^2
+# grid: 4 x 1024 tiles instead of 2 x 2048), and forced on a partial last tile
+# row (301 rows in 3-row tiles), a padded width (200 x 1022) and 256 x 2048
+GEOMS_2D = [(512, 2048, 0), (301, 1024, 2), (200, 1022, 2), (256, 2048, 2)]
 
 
 @pytest.mark.parametrize("block", [8, 1])

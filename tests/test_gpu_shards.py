@@ -397,6 +397,8 @@ def test_rccl_single_rank_resident_256x2048():
             c.belief_set(b0)
             c.mdp_reset()
         assert sh.loop_steps_per_launch() == 128
+        # the 512-row view runs 2-D tiles (4 x 1024, two tile columns)
+        assert sh.resident_tiling() == (256, 4, 2)
         for lo, hi in ((0, 17), (17, 300)):
             ref.loop_run(us[lo:hi], zs[lo:hi])
             sh.loop_run(us[lo:hi], zs[lo:hi])
