@@ -174,6 +174,9 @@ struct pp2_ctx {
   int res_stall_tile = -1;         // PP2_TUNE_RESIDENT_STALL (tests)
   int res_cus = 0;                 // PP2_TUNE_RESIDENT_CUS: CUs the plans may use (0: all)
   int res_tc_pref = 0;             // PP2_TUNE_RESIDENT_TILE_COLS (0: automatic)
+  long long agree_gen = 0;         // model builds + tuning calls (RCCL shards: equal on all ranks)
+  long long agree_done = -1;       // agree_gen at the ranks' last agreement on agreed_e
+  int agreed_e = 0;                // the resident halo depth all ranks agreed on (0: none)
   int res_loop_tc = 0;             // tile columns of the last loop launch (0: fresh buffers)
   // row shards on the resident loop: halo depth per resident
   // launch, the run's power-of-two shift and the {mass, shift} rank vector

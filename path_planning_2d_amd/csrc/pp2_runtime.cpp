@@ -345,6 +345,7 @@ static bool finite_nonneg(float v) {
 int build_model_dict(pp2_ctx* c) {
   c->dict_n = 0;
   c->res_e_dict = -1;  // shard_resident_e: recomputed (collectively) on the next run
+  ++c->agree_gen;      // ... and agreed again (pp2_loop_run)
   const long long n = (long long)(c->g.rows + 2 * c->g.halo) * c->g.wp;
   break_pipeline(c);
   if (!c->code_alloc) {
@@ -1593,6 +1594,7 @@ int pp2_get_geometry(pp2_ctx* c, uint32_t* rows, uint32_t* width,
 
 int pp2_set_tuning(pp2_ctx* c, int key, int value) {
   CHECK(check_ctx_settled(c));
+  ++c->agree_gen;  // a shard's resident eligibility may change: agree again
   switch (key) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
@@ -1725,6 +1727,7 @@ int pp2_model_load(pp2_ctx* c, const char* dir) {
 int pp2_belief_set(pp2_ctx* c, const float* b) {
   CHECK(check_ctx_settled(c));
   c->lost_belief = false;
+  ++c->agree_gen;  // (after a lost shard run: every rank agrees again)
   if (!b) return set_err(PP2_EINVAL, "belief is null");
   DeviceGuard dg(c->device);
   break_pipeline(c);
@@ -1776,6 +1779,7 @@ int pp2_belief_update(pp2_ctx* c, uint8_t u, uint8_t z) {
 int pp2_mdp_reset(pp2_ctx* c) {
   CHECK(check_ctx_settled(c));
   c->lost_values = false;
+  ++c->agree_gen;
   DeviceGuard dg(c->device);
   for (Planes* P : {&c->J[0], &c->J[1], &c->Jsnap})
     HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
@@ -1928,9 +1932,21 @@ int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
   if (c->group)
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
   if (n >= 2 && c->comm) {
-    int e = shard_resident_e(c);
-    if (e > 0 && !shard_resident_ready(c, e)) e = 0;
-    CHECK(agree_min(c, &e));
+    // The ranks agree on e (a blocking all-reduce) only when something that
+    // decides it may have changed since the last agreement: the model or a
+    // tuning, events every rank of an SPMD program goes through together, so
+    // the generation counts stay equal across ranks and all of them agree,
+    // or none (a 20-step call saves one RCCL round trip and a host sync).
+    int e;
+    if (c->agree_done != c->agree_gen) {
+      e = shard_resident_e(c);
+      if (e > 0 && !shard_resident_ready(c, e)) e = 0;
+      CHECK(agree_min(c, &e));
+      c->agreed_e = e;
+      c->agree_done = c->agree_gen;
+    } else {
+      e = c->agreed_e;
+    }
     if (e > 0) {
       if (!shard_resident_ready(c, e))
         return set_err(PP2_ENOMEM, "resident shard buffers for a %d-row halo", e);
