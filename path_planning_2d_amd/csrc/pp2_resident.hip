@@ -676,6 +676,11 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
 
   // the dense kernels' partial of this wave's 256 cells (row y, x gx + 256 wj)
   const int pi = y * (wp >> 8) + cx * wpr + wj;
+  // the wave that takes a block start's arrivals and reduces the partials: an
+  // interior one (row 1, not a side wave; SIMD 1) when the tile has interior
+  // rows, so that the reduction overlaps the edge waves' hand-off and compute
+  // instead of following them on wave 0 (an edge wave)
+  const int redw = a.rt >= 3 && wpr >= 4 ? wpr + 1 : 0;
   unsigned arrivals = a.arrive_base;
   int shift = 0;  // shard runs: the power-of-two shifts of the block starts so far
   float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, best[4] = {0.0f, 0.0f, 0.0f, 0.0f}, local = 0.0f;
@@ -769,12 +774,12 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       if (!bs) finish_quad();
     }
     if (bs) {
-      if (wave == 0) {
+      if (wave == redw) {
         arrivals += a.ntiles;
         wave_wait(a.sync + kResidentSyncArrive, 1, arrivals, err, a.err_host);
         const float S = wave_reduce_partials_sc1(
             a.ring + (size_t)((t - 1) % kResidentRing) * a.nparts, a.nparts);
-        if (threadIdx.x == 0) sS[0] = S;
+        if (lane == 0) sS[0] = S;
       }
       __syncthreads();
       if (a.shard) {
