@@ -593,8 +593,11 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
     a rank of the 8-GPU job does (views of 256 + 2e rows, one launch per e
     steps, the {mass, shift} all-reduce, halo exchanges and rebases) -- with
     every RCCL call a 1-rank no-op.  The 8-GPU time is then projected as this
-    measured step plus the RCCL rounds the real job adds per call (2 per block
-    + the agreement and the closing all-reduce) at an ASSUMED xGMI round trip
+    measured step plus the RCCL rounds the real job adds per call (the first
+    block's halo exchange, the {mass, shift} all-reduce + exchange of every
+    later block, the closing all-reduce: 2 per block; the ranks' agreement on
+    e is made once per model / tuning / reset, not per call) at an ASSUMED
+    xGMI round trip
     (RCCL_ROUND_US; multi-GPU RCCL cannot run on one GPU)."""
     import torch
     import path_planning_2d_amd as P
@@ -616,7 +619,7 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
     ctx.close()
     t = 1e6 * el / k
     nblk = -(-k // e)
-    rounds = 2 * nblk + 1
+    rounds = 2 * nblk
     lo, hi = (t + rounds * r / k for r in RCCL_ROUND_US)
     return {"shard": f"rows [{r0}, {r1}) x {G} of the {G}^2 grid (rank 3 of 8), 1-rank RCCL "
                      f"communicator",
@@ -665,7 +668,7 @@ def weak_rank_share(args, local, stream, n1_cells_per_s):
     launches = ctx.resident_launches()[0] - l0
     ctx.close()
     t = 1e6 * el / k
-    rounds = 2 * (-(-k // e)) + 1
+    rounds = 2 * (-(-k // e))
     proj = [t + rounds * r / k for r in RCCL_ROUND_US]
     return {"shard": f"rows [{R}, {2 * R}) x {W} of a {2 * R}x{W} grid (rank 1 of 2), 1-rank "
                      f"RCCL communicator",
