@@ -1062,7 +1062,9 @@ bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref)
   ResidentPlan p1, p2;
   const bool ok1 = resident_plan_tc(g, E, ncus, 1, &p1);
   const bool ok2 = tc_pref != 1 && resident_plan_tc(g, E, ncus, 2, &p2);
-  if (ok2 && ok1 && (tc_pref == 2 || (p1.rt < 4 && p2.rt >= 4))) {
+  // (automatic only with 1024-column tiles or wider: the measured shape, whose
+  // rows keep interior waves beside the side waves)
+  if (ok2 && ok1 && (tc_pref == 2 || (p1.rt < 4 && p2.rt >= 4 && g.wp / 2 >= 1024))) {
     *p = p2;
     return true;
   }
