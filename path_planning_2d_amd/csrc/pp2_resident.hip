@@ -571,6 +571,14 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       pq[j] = q[i < nq ? i : 0];
     }
   }
+  // the tile's b and J: loads issued first, so that their HBM latency
+  // overlaps the table staging and the class planes (consumed below)
+  f4a b_t = {0.0f, 0.0f, 0.0f, 0.0f}, j_t = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (valid) {
+    const long long off = (long long)y * wp + gx + x0;
+    b_t = *reinterpret_cast<const f4a*>(a.b_in + off);
+    j_t = *reinterpret_cast<const f4a*>(a.j_in + off);
+  }
   stage_rows(a.rfact, kResTab, lds);
   stage_rows(a.rows, rows_floats(a.E, true), sTC);
   for (int i = threadIdx.x; i < 4 * (a.rt + 1); i += blockDim.x) {
@@ -636,9 +644,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   if (prior_err != 0u) return;  // (uniform: before any global store)
   const bool bnd = nb_up || nb_dn || sd_l || sd_r;  // waves that cross CUs
   if (valid) {
-    const long long off = (long long)y * wp + gx + x0;
-    const f4a b = *reinterpret_cast<const f4a*>(a.b_in + off);
-    const f4a j = *reinterpret_cast<const f4a*>(a.j_in + off);
+    const f4a b = b_t, j = j_t;
     *reinterpret_cast<f4a*>(sbuf(0, 0) + ty * xs + x0) = b;
     *reinterpret_cast<f4a*>(sbuf(1, 0) + ty * xs + x0) = j;
     if (bnd) {
