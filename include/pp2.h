@@ -364,9 +364,7 @@ typedef struct {
   uint64_t rand_skip;             /* rand() draws already taken from the stream
                                      (the reference's generateBeliefSet runs
                                      first: pp2_pbvi_solve's *rand_calls) */
-  int32_t reference_order;        /* 0 (default): grid-wide sums as parallel
-                                     trees (fp64 where the reference's fp32
-                                     chains lose digits); 1: every sum the
+  int32_t reference_order;        /* 1 (default, the drop-in): every sum the
                                      reference runs on its host -- the QNode
                                      reward inner_product and the child
                                      renormalisation accumulate
@@ -374,13 +372,18 @@ typedef struct {
                                      evaluateFibCpu / evaluatePbviCpu
                                      (fast_informed_bound_cuda.cu:278-297,
                                      point_based_value_iteration_cuda.cu:
-                                     678-699) -- as one x-ordered fp32 chain
-                                     on the device (multiply, then add; IEEE
-                                     division), so bounds, rewards, weights
-                                     and the tree equal the reference's
-                                     arithmetic bit for bit.  Slower: each
-                                     expansion is a few dependent chains of
-                                     H*W adds. */
+                                     678-699) and the sampling cdf (:176-183)
+                                     -- gives the result of the reference's
+                                     x-ordered fp32 chain (multiply, then add;
+                                     IEEE division), so bounds, rewards,
+                                     weights and the tree equal the
+                                     reference's arithmetic bit for bit.
+                                     0 (opt-in fast variant, NOT bit-exact):
+                                     grid-wide sums as parallel trees (fp64
+                                     where the reference's fp32 chains lose
+                                     digits); within rel 1e-4 of the
+                                     reference, which can flip a near-tied
+                                     expansion choice. */
 } pp2_planner_params;
 
 /* Snapshot of the root and its children, for inspection and parity tests. */

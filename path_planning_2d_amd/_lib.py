@@ -11,6 +11,8 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # PP2_LIBRARY points at a diagnostic build of the same ABI (tools/micro/).
+# include/pp2.h PP2_ABI_VERSION (tests/test_abi.py checks the two agree)
+PP2_ABI_VERSION = 3
 LIB_PATH = os.environ.get("PP2_LIBRARY") or os.path.join(PKG_DIR, "libpp2_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "pp2.h")
 
@@ -134,12 +136,16 @@ def load() -> C.CDLL:
     lib = C.CDLL(LIB_PATH)
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name, None)
-        if fn is None and os.environ.get("PP2_LIBRARY"):
-            continue  # an older diagnostic build (A/B timing) lacks newer entry points
+        if fn is None and os.environ.get("PP2_ALLOW_PARTIAL_ABI") == "1":
+            continue  # diagnostic only: an older build (A/B timing) lacks newer entry points
         if fn is None:
             raise ImportError(f"{LIB_PATH} does not export {name}")
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, C.c_int)
+    ver = lib.pp2_abi_version()
+    if ver != PP2_ABI_VERSION and os.environ.get("PP2_ALLOW_PARTIAL_ABI") != "1":
+        raise ImportError(f"{LIB_PATH} has ABI version {ver}, this package expects "
+                          f"{PP2_ABI_VERSION} (rebuild the library)")
     _lib = lib
     return lib
 

@@ -1163,21 +1163,24 @@ namespace {
 // ldexp(m_q, C - shift_q) -- identical on every shard.
 __global__ void k_shard_mass_vec(const float* __restrict__ partials, int n,
                                  const int* __restrict__ shift, float* __restrict__ vec,
-                                 int nranks, int rank) {
+                                 int nranks, int rank, const unsigned* __restrict__ err_word) {
   const float S = wave_reduce_partials(partials, n);  // k_sum_finalize's tree
   for (int i = threadIdx.x; i < 2 * nranks; i += 64)
     if (i != 2 * rank && i != 2 * rank + 1) vec[i] = 0.0f;
   if (threadIdx.x == 0) {
     vec[2 * rank] = S;
     vec[2 * rank + 1] = shift ? (float)*shift : 0.0f;
+    if (err_word) vec[2 * nranks] = ld_flag(err_word) != 0u ? 1.0f : 0.0f;
   }
 }
 
 __global__ void k_shard_rebase(const float* __restrict__ vec, int nranks, int rank,
                                float* __restrict__ b, int wp, int r0, int r1, int own_rows,
-                               float* __restrict__ mass_out) {
+                               float* __restrict__ mass_out, unsigned* __restrict__ err_host) {
   int C = 0x7fffffff;
   for (int q = 0; q < nranks; ++q) C = min(C, (int)vec[2 * q + 1]);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && err_host && vec[2 * nranks] != 0.0f)
+    __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (blockIdx.x == 0 && threadIdx.x == 0 && mass_out) {
     float M = 0.0f;
     for (int q = 0; q < nranks; ++q) M += __builtin_ldexpf(vec[2 * q], C - (int)vec[2 * q + 1]);
@@ -1202,20 +1205,21 @@ __global__ void k_shard_rebase(const float* __restrict__ vec, int nranks, int ra
 }  // namespace
 
 hipError_t launch_shard_mass_vec(hipStream_t st, const float* partials, int n, const int* shift,
-                                 float* vec, int nranks, int rank) {
+                                 float* vec, int nranks, int rank, const unsigned* err_word) {
   if (n < 0 || n % 4 != 0 || nranks < 1 || rank < 0 || rank >= nranks) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_shard_mass_vec, dim3(1), dim3(64), 0, st, partials, n, shift, vec, nranks,
-                     rank);
+                     rank, err_word);
   return hipGetLastError();
 }
 
 hipError_t launch_shard_rebase(hipStream_t st, const float* vec, int nranks, int rank, float* b,
-                               int wp, int r0, int r1, int own_rows, float* mass_out) {
+                               int wp, int r0, int r1, int own_rows, float* mass_out,
+                               unsigned* err_host) {
   if (wp % 4 != 0 || r1 < r0 || nranks < 1) return hipErrorInvalidValue;
   const long long nq = (long long)(r1 - r0) * (wp / 4);
   const int blocks = (int)std::max<long long>(1, (nq + 255) / 256);
   hipLaunchKernelGGL(k_shard_rebase, dim3(blocks), dim3(256), 0, st, vec, nranks, rank, b, wp, r0,
-                     r1, own_rows, mass_out);
+                     r1, own_rows, mass_out, err_host);
   return hipGetLastError();
 }
 

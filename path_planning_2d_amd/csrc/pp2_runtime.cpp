@@ -608,7 +608,8 @@ int pp2rt::ensure_mass(pp2_ctx* c) {
   if (c->shift_pending && c->comm) {  // a shard-resident run's mass: rebase as well
     CHECK(shard_post_mass(c, c->nranks, c->rank));
     CHECK(comm_enter(c));
-    NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, 2 * c->nranks, ncclFloat, ncclSum, c->comm, cst(c)));
+    NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, 2 * c->nranks + 1, ncclFloat, ncclSum, c->comm,
+                          cst(c)));
     CHECK(comm_leave(c));
     return shard_rebase(c, c->nranks, c->rank, 0, c->g.rows);
   }
@@ -1352,7 +1353,7 @@ bool pp2rt::shard_resident_ready(pp2_ctx* c, int e) {
   }
   if (!c->d_vec) {
     const int nr = c->group ? c->group_size : c->nranks;
-    if (hipMalloc(&c->d_vec, (size_t)2 * nr * sizeof(float)) != hipSuccess) {
+    if (hipMalloc(&c->d_vec, (size_t)(2 * nr + 1) * sizeof(float)) != hipSuccess) {
       c->d_vec = nullptr;
       return false;
     }
@@ -1363,9 +1364,12 @@ bool pp2rt::shard_resident_ready(pp2_ctx* c, int e) {
 // {mass, shift} of this shard's pending belief into its slot of d_vec.
 int pp2rt::shard_post_mass(pp2_ctx* c, int nranks, int rank) {
   const int bc = c->bcur;
+  // an RCCL shard's sticky resident error word rides the all-reduce, so a run
+  // lost on any rank is marked lost on every rank (shard_rebase)
+  const unsigned* err = c->comm && c->res_sync ? c->res_sync + pp2::kResidentSyncErr : nullptr;
   HIPCHK(pp2::launch_shard_mass_vec(c->stream, c->pbuf[bc], c->pcount[bc],
                                     c->shift_pending ? c->d_shift : nullptr, c->d_vec, nranks,
-                                    rank));
+                                    rank, err));
   return PP2_OK;
 }
 
@@ -1373,8 +1377,13 @@ int pp2rt::shard_post_mass(pp2_ctx* c, int nranks, int rank) {
 // take the global mass: the state of a finalised, common-scale belief.
 int pp2rt::shard_rebase(pp2_ctx* c, int nranks, int rank, int r0, int r1) {
   const int bc = c->bcur;
+  // the error slot marks this rank's latest journalled launch as failed
+  // (resident_settle then reports the loss, as on the rank that timed out)
+  unsigned* eh = c->comm && c->res_sync && !c->journal.empty()
+                     ? c->res_host + pp2_ctx::kResHostChain + (c->journal.size() - 1)
+                     : nullptr;
   HIPCHK(pp2::launch_shard_rebase(c->stream, c->d_vec, nranks, rank, c->b[bc].v.p, c->g.wp, r0,
-                                  r1, c->g.rows, c->bsum + bc));
+                                  r1, c->g.rows, c->bsum + bc, eh));
   c->pending[bc] = false;
   c->shift_pending = false;
   return PP2_OK;
@@ -1439,7 +1448,8 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
 // all-reduce and the rebase), then the closing all-reduce and rebase.
 static int shard_allreduce_vec(pp2_ctx* c) {
   CHECK(comm_enter(c));
-  NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, 2 * c->nranks, ncclFloat, ncclSum, c->comm, cst(c)));
+  NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, 2 * c->nranks + 1, ncclFloat, ncclSum, c->comm,
+                        cst(c)));
   return comm_leave(c);
 }
 
@@ -1654,6 +1664,7 @@ int pp2_set_cells_per_lane(pp2_ctx* c, int cpt) {
   if (cpt != 1 && cpt != 2 && cpt != 4)
     return set_err(PP2_EINVAL, "cells per lane must be 1, 2 or 4 (got %d)", cpt);
   c->cpt = cpt;
+  ++c->agree_gen;  // cpt decides coded_active, hence a shard's resident eligibility
   return PP2_OK;
 }
 
@@ -1726,9 +1737,8 @@ int pp2_model_load(pp2_ctx* c, const char* dir) {
 // ---------------------------------------------------------------- belief
 int pp2_belief_set(pp2_ctx* c, const float* b) {
   CHECK(check_ctx_settled(c));
-  c->lost_belief = false;
-  ++c->agree_gen;  // (after a lost shard run: every rank agrees again)
   if (!b) return set_err(PP2_EINVAL, "belief is null");
+  ++c->agree_gen;  // (after a lost shard run: every rank agrees again)
   DeviceGuard dg(c->device);
   break_pipeline(c);
   CHECK(upload_planes(c, c->b[c->bcur], b));
@@ -1739,6 +1749,7 @@ int pp2_belief_set(pp2_ctx* c, const float* b) {
   const float one = 1.0f;
   HIPCHK(hipMemcpyAsync(c->bsum + c->bcur, &one, sizeof one, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  c->lost_belief = false;  // only once the new belief is in place
   return PP2_OK;
 }
 
@@ -1778,7 +1789,6 @@ int pp2_belief_update(pp2_ctx* c, uint8_t u, uint8_t z) {
 // ---------------------------------------------------------------- MDP
 int pp2_mdp_reset(pp2_ctx* c) {
   CHECK(check_ctx_settled(c));
-  c->lost_values = false;
   ++c->agree_gen;
   DeviceGuard dg(c->device);
   for (Planes* P : {&c->J[0], &c->J[1], &c->Jsnap})
@@ -1786,6 +1796,7 @@ int pp2_mdp_reset(pp2_ctx* c) {
   HIPCHK(hipMemsetAsync(c->A, 0, (size_t)c->g.rows * c->g.wp, c->stream));
   c->jcur = 0;
   break_pipeline(c);
+  c->lost_values = false;  // only once the values are reset
   return PP2_OK;
 }
 
@@ -1948,8 +1959,13 @@ int pp2_loop_run(pp2_ctx* c, int n, const uint8_t* us, const uint8_t* zs) {
       e = c->agreed_e;
     }
     if (e > 0) {
+      // every generation bump that can change eligibility makes the ranks
+      // agree again above; a cached e that is no longer ready here would
+      // leave this rank alone off the resident path (a collective mismatch)
       if (!shard_resident_ready(c, e))
-        return set_err(PP2_ENOMEM, "resident shard buffers for a %d-row halo", e);
+        return set_err(PP2_ESTATE, "the ranks agreed on a %d-row resident halo that this "
+                       "shard can no longer run (changed without a model build, tuning or "
+                       "belief/value reset on every rank)", e);
       return shard_loop_resident(c, e, n, us, zs);
     }
   }

@@ -115,6 +115,9 @@ bool PomdpPathPlanning2d::initialize() {
   prm.max_online_iteration = max_online_iteration;
   prm.lower_bound_mode = 1;     // leaf lower bounds from the PBVI alphas
   prm.rand_skip = rand_draws;   // the tree's rand() stream continues PBVI's
+  // (the default, stated): every grid-wide sum gives the reference's x-ordered
+  // fp32 host result, so the published actions equal the reference's bit for bit
+  prm.reference_order = 1;
   if (!pp2_ok(pp2_planner_create(&planner_, ctx_, &prm), "planner")) return false;
 
   if (!createRosIO()) {

@@ -32,7 +32,9 @@ def test_binding_covers_header():
 
 def test_version_and_status_strings():
     lib = _lib.load()
-    assert lib.pp2_abi_version() == 3
+    m = re.search(r"#define PP2_ABI_VERSION (\d+)", open(_lib.HEADER_PATH).read())
+    assert m and int(m.group(1)) == _lib.PP2_ABI_VERSION
+    assert lib.pp2_abi_version() == _lib.PP2_ABI_VERSION
     assert lib.pp2_status_string(0) == b"ok"
     assert lib.pp2_status_string(6) == b"RCCL error"
 

@@ -70,7 +70,7 @@ def test_planner_matches_oracle(oracle, name, max_depth, max_iter, steps):
         rpl = oracle.Planner(grid, m["T"], m["L"], m["R"], alphas,
                              max_depth=max_depth, max_iter=max_iter)
         with P.QVTreePlanner(ctx, max_search_tree_depth=max_depth,
-                             max_online_iteration=max_iter) as gpl:
+                             max_online_iteration=max_iter, reference_order=0) as gpl:
             _, zs, _ = S.synth_trajectory(grid, steps, seed=7)
             b0 = S.uniform_belief(grid)
             a_g, v_g = gpl.step(0, 0, b0)
@@ -109,7 +109,8 @@ def test_planner_256_plan_step(oracle):
         T, L, R = oracle.model_pomdp(grid, goal)
         opl = oracle.Planner(grid, T, L, R, alphas, max_depth=3, max_iter=15,
                              accurate=True)
-        with P.QVTreePlanner(ctx, max_search_tree_depth=3, max_online_iteration=15) as gpl:
+        with P.QVTreePlanner(ctx, max_search_tree_depth=3, max_online_iteration=15,
+                             reference_order=0) as gpl:
             b0 = S.uniform_belief(grid)
             a_g, _ = gpl.step(0, 0, b0)
             a_o, _ = opl.step(0, 0, b0)
@@ -148,7 +149,8 @@ def test_planner_cdf_zero_block_skip_exact(oracle, monkeypatch):
         for skip in ("1", "0"):
             monkeypatch.setenv("PP2_CDF_SKIP", skip)
             infos = []
-            with P.QVTreePlanner(ctx, max_search_tree_depth=5, max_online_iteration=15) as gpl:
+            with P.QVTreePlanner(ctx, max_search_tree_depth=5, max_online_iteration=15,
+                                 reference_order=0) as gpl:
                 a, v = gpl.step(0, 0, b0)
                 infos.append((a, v, gpl.info()))
                 for k in range(4):
@@ -192,7 +194,7 @@ def test_planner_pbvi_lower_bound(oracle, name, S, max_depth, steps):
         opl.set_pbvi(pal, pact)
         opl.skip_rand(calls)
         with P.QVTreePlanner(ctx, max_search_tree_depth=max_depth, max_online_iteration=15,
-                             lower_bound_mode=1, rand_skip=calls) as gpl:
+                             lower_bound_mode=1, rand_skip=calls, reference_order=0) as gpl:
             a_g, v_g = gpl.step(0, 0, b0)
             a_o, v_o = opl.step(0, 0, b0)
             gi = gpl.info()
