@@ -1,0 +1,114 @@
+// pp2_fchain.h -- exact parallel evaluation of a sequential fp32 sum.
+//
+// The reference runs every grid-wide sum of its QV-tree on the x86 host as
+// one left-to-right fp32 chain, acc = fl(acc + t_x) for x = 0 .. n-1, IEEE
+// round-to-nearest-even, no FMA contraction:
+//   * std::accumulate of a child belief (search_tree_cuda.cu:225-229),
+//   * std::inner_product for the QNode reward (:168-173), evaluateFibCpu
+//     (fast_informed_bound_cuda.cu:278-297), evaluatePbviCpu
+//     (point_based_value_iteration_cuda.cu:678-699): t_x = fl(b_x * a_x),
+//   * the sampling cdf of forwardSampling (search_tree_cuda.cu:176-183).
+// A chain of n dependent adds costs n add latencies on any core (~0.25 ms at
+// 256^2 on one gfx950 lane).  The result is nevertheless computable in
+// parallel, bit for bit, when every term has the same sign (beliefs >= 0;
+// rewards and FIB / PBVI values <= 0 -- the sign is checked per chain, mixed
+// chains run sequentially):
+//
+// * Work on |t|; the running sum s is then non-decreasing.  Write s = k * u
+//   with u = 2^(E-23) the ulp of its binade [2^E, 2^(E+1)) (E >= -126; the
+//   subnormals and [2^-126, 2^-125) share u = 2^-149, so s = 0 is E = -126,
+//   k = 0).  While s + t stays below 2^(E+1), fl(s + t) = u * RNE(k + t/u),
+//   and t/u = ldexp(t, 23 - E) is exact.  Unless t/u sits exactly halfway
+//   between integers (a tie, resolved by the parity of k), that is
+//   k + rint(t/u): the increment does not depend on k at all.
+// * So a chunk of terms whose sum stays inside binade E and holds no tie
+//   advances k by d = sum of rint(t/u) over the chunk -- an integer sum whose
+//   order does not matter.  Since k only grows, the chunk stayed inside the
+//   binade iff k + d <= 2^24 (k == 2^24 is 2^(E+1), the next binade's first
+//   value; a later term that rounds to 0 at ulp u rounds to 0 at 2u too).
+// * A driver walks the chunks in x order with the exact state (E, k): a
+//   chunk whose table entry was computed for the state's E and holds no tie
+//   advances k by d; any other chunk (the binade crossings, a table computed
+//   for a neighbouring E, a tie) is added term by term in fp32, exactly as
+//   the reference, and the state re-derived from the float.
+// The table entry's E comes from an approximate running sum (any value:
+// the driver only checks it), so the result equals the sequential chain for
+// every input; only the speed depends on how many chunks fall back.
+//
+// Device code includes this after defining PP2_FC_HD (__host__ __device__);
+// the CPU check (tools/fchain_check.cpp) includes it as plain C++.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#ifndef PP2_FC_HD
+#define PP2_FC_HD
+#endif
+
+namespace pp2 {
+namespace fchain {
+
+constexpr int kK24 = 1 << 24;
+constexpr int kEMin = -126;
+constexpr uint32_t kNoEntry = 0xffffffffu;  // table entry that never applies
+constexpr float kQCap = 67108864.0f;        // 2^26: t/u beyond it cannot be valid
+
+PP2_FC_HD inline uint32_t bits_of(float f) { return __builtin_bit_cast(uint32_t, f); }
+PP2_FC_HD inline float float_of(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// Binade domain E of a finite s >= +0 (sign ignored): max(exponent, -126).
+PP2_FC_HD inline int domain_of(float s) {
+  const int et = (int)((bits_of(s) >> 23) & 0xffu);
+  return et <= 1 ? kEMin : et - 127;
+}
+
+// (E, k) of a finite s >= +0.
+PP2_FC_HD inline void state_of(float s, int* E, int* k) {
+  const uint32_t b = bits_of(s) & 0x7fffffffu;
+  const uint32_t et = b >> 23;
+  if (et <= 1) {
+    *E = kEMin;
+    *k = (int)(b & 0xffffffu);
+  } else {
+    *E = (int)et - 127;
+    *k = (int)((b & 0x7fffffu) | 0x800000u);
+  }
+}
+
+// k == 2^24 is the next binade's first value.
+PP2_FC_HD inline void normalise(int* E, int* k) {
+  if (*k == kK24) {
+    *E += 1;
+    *k = 1 << 23;
+  }
+}
+
+// The float k * 2^(E-23) (k <= 2^24; E = -126: any k, else k >= 2^23).
+PP2_FC_HD inline float value_of(int E, int k) {
+  normalise(&E, &k);
+  if (E > 127) return float_of(0x7f800000u);
+  if (E == kEMin && k < (1 << 23)) return float_of((uint32_t)k);
+  return float_of(((uint32_t)(E + 127) << 23) | ((uint32_t)k & 0x7fffffu));
+}
+
+// The increment of one term a = |t| (finite) in domain E: rint(a / u) as a
+// float (exact integer < 2^26, or 2^26 when larger), and whether it is a tie.
+PP2_FC_HD inline float units_of(float a, int E, bool* tie) {
+  float q = ldexpf(a, 23 - E);
+  q = fminf(q, kQCap);
+  const float r = rintf(q);
+  *tie = fabsf(q - r) == 0.5f;
+  return r;
+}
+
+// Table entry of a chunk: d units in domain E, or kNoEntry.
+PP2_FC_HD inline uint32_t make_entry(int E, float d, bool tie) {
+  if (tie || !(d < (float)kK24)) return kNoEntry;
+  return ((uint32_t)(E + 128) << 24) | (uint32_t)d;
+}
+PP2_FC_HD inline int entry_domain(uint32_t e) { return (int)(e >> 24) - 128; }
+PP2_FC_HD inline int entry_units(uint32_t e) { return (int)(e & 0xffffffu); }
+
+}  // namespace fchain
+}  // namespace pp2

@@ -39,6 +39,37 @@ __global__ __launch_bounds__(kThreads) void k_pbvi_update(
   out[(long long)c * ld + idx] = p * L.p[(long long)y * L.rs + (long long)z * L.ps + x];
 }
 
+// The QV-tree expansion's 9 predictions of one dense belief row (the child
+// of (u, z) is pred[u] * L[z], formed by the IEEE sums of pp2_fchain.hip).
+__global__ __launch_bounds__(kThreads) void k_tree_pred(Geom g, PlaneSet T,
+                                                        const float* __restrict__ b, int ld,
+                                                        float* __restrict__ pred) {
+  const int W = g.width, H = g.rows;
+  const int idx = blockIdx.x * kThreads + threadIdx.x;
+  if (idx >= H * W) return;
+  const int y = idx / W, x = idx - y * W;
+  float bv[9];
+  bool in[9];
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const int sy = y + s / 3 - 1, sx = x + s % 3 - 1;
+    in[s] = !(sy < 0 || sy >= H || sx < 0 || sx >= W);
+    bv[s] = in[s] ? b[sy * W + sx] : 0.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    float p = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      if (!in[s]) continue;
+      const int sy = y + s / 3 - 1, sx = x + s % 3 - 1;
+      const float t = T.p[(long long)sy * T.rs + (long long)(9 * u + 8 - s) * T.ps + sx];
+      p = fmaf(t, bv[s], p);
+    }
+    pred[(long long)u * ld + idx] = p;
+  }
+}
+
 // One thread = one cell x, kGaoRows alpha vectors and 8 of the 16
 // observations: the 8x9 products T[x][a][s] * L[nbr_s(x)][o] stay in
 // registers across the alpha rows (blockIdx.z = 2 * action + half).
@@ -96,6 +127,16 @@ hipError_t launch_pbvi_update(hipStream_t st, const Geom& g, PlaneSet T, PlaneSe
   dim3 grid((hw + kThreads - 1) / kThreads, n);
   hipLaunchKernelGGL(k_pbvi_update, grid, dim3(kThreads), 0, st, g, T, L, src, ld, src_row, us,
                      zs, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_pred(hipStream_t st, const Geom& g, PlaneSet T, const float* b, int ld,
+                            float* pred) {
+  const int hw = g.rows * g.width;
+  if (hw <= 0) return hipSuccess;
+  if (ld < hw) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_tree_pred, dim3((hw + kThreads - 1) / kThreads), dim3(kThreads), 0, st, g,
+                     T, b, ld, pred);
   return hipGetLastError();
 }
 

@@ -89,4 +89,51 @@ hipError_t launch_pbvi_select(hipStream_t st, const float* V, const float* Ga, i
 hipError_t launch_sum_splits(hipStream_t st, const float* C, int splits, long long sstride,
                              int n, float* out);
 
+// ---- pp2_fchain.hip (IEEE): the reference-order planner's grid-wide fp32
+// sums, each equal to the reference's x-ordered chain, computed in parallel
+// (pp2_fchain.h).  Group g (blockIdx) has K chains (K = 0: one chain of the
+// base terms; else term i = base * partners[i][x], multiply then add):
+//   FC_ROW:        base = row[g * row_stride + x]
+//   FC_CHILD:      base = fl_ftz(pred[c % 9][x] * L[c / 9][x]), c = g0 + g
+//                  (the unnormalised child of action c % 9, observation c / 9)
+//   FC_CHILD_NORM: the same divided by sums[c] (IEEE)
+// out[c * ldo + i] = the chain's sum (c = g0 + g); with cdf (FC_ROW, K = 0, one
+// group) also every running sum, cdf[x] (std::partial_sum order).
+enum FcBase { FC_ROW = 0, FC_CHILD = 1, FC_CHILD_NORM = 2 };
+constexpr int kFcMaxChunks = 1024;     // chunks per chain (LDS tables)
+constexpr int kFcMaxCells = 1 << 28;
+// cells per lane per chunk: chunks of 64 * m cells, at most kFcMaxChunks
+inline __host__ __device__ int fc_lane_elems(int n) {
+  const long long m = ((long long)n + 64LL * kFcMaxChunks - 1) / (64LL * kFcMaxChunks);
+  return m < 4 ? 4 : (int)m;
+}
+struct FcArgs {
+  int n = 0, ld = 0;
+  const float* row = nullptr;
+  long long row_stride = 0;
+  const float* pred = nullptr;   // [9][ld]
+  const float* lrows = nullptr;  // [16][ld]
+  const float* sums = nullptr;   // [144]
+  int g0 = 0;
+  const float* partners = nullptr;  // [K][ld]
+  float* out = nullptr;
+  int ldo = 1;
+  float* cdf = nullptr;
+};
+hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a);
+// dst[r][x] = fl_ftz(pred[c % 9][x] * L[c / 9][x]) / sums[c], c = child[r], x < n.
+struct FcStoreList {
+  int n = 0;
+  int child[144];
+  float* dst[144];
+};
+hipError_t launch_store_children(hipStream_t st, const FcStoreList& L, const float* pred,
+                                 const float* lrows, const float* sums, int n, int ld);
+
+// ---- pp2_pbvi_dev.hip (FTZ): the 9 action predictions of cudaBayesBeliefUpdate
+// before the likelihood product: pred[u][idx] = sum_s T[sidx][u][8-s] * b[sidx]
+// (fmaf chain, s ascending, in-grid neighbours), b a dense row.
+hipError_t launch_tree_pred(hipStream_t st, const Geom& g, PlaneSet T, const float* b, int ld,
+                            float* pred);
+
 }  // namespace pp2

@@ -85,8 +85,9 @@ struct QNode {
 };
 
 struct Slot {
-  Planes b;
+  Planes b;               // the belief in plane geometry (reference_order 0)
   float* mass = nullptr;  // device scalar: unnormalised mass of b
+  float* row = nullptr;   // reference_order 1: the normalised belief, a dense row
 };
 
 constexpr int kStatsPerChild = 10;
@@ -171,13 +172,19 @@ struct pp2_planner {
   int* d_srow = nullptr;
   uint8_t *d_us = nullptr, *d_zs = nullptr;
 
-  // reference_order: node beliefs are stored normalised (mass 1) exactly as
-  // the reference's host normalises them, and every grid-wide sum is one
-  // x-ordered fp32 chain (pp2_pbvi_host.hip k_rows_chain / k_pair_chain).
+  // reference_order: node beliefs are dense rows stored normalised exactly
+  // as the reference's host normalises them, and every grid-wide sum equals
+  // the reference's x-ordered fp32 chain (pp2_fchain.hip; the PBVI leaf dots
+  // k_pair_chain).
   bool ref = false;
   int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
   float* d_rrows = nullptr;     // [9][ld] R[.][a]
   float* d_frows = nullptr;     // [9][ld] FIB alphas[.][i]
+  float* d_lrows = nullptr;     // [16][ld] L[.][z]
+  float* d_pred = nullptr;      // [9][ld] the expanded belief's predictions
+  float* d_csum = nullptr;      // [144] the children's masses (accumulate)
+  float* h_cdf = nullptr;       // pinned: the expanded belief's running sums
+  float* d_cdf = nullptr;
   unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
   hipStream_t side = nullptr;   // reward chains beside the child chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -213,7 +220,13 @@ int acquire_slot(pp2_planner* p, int* out) {
     return PP2_OK;
   }
   Slot s;
-  CHECK(alloc_planes(p->ctx, &s.b, 1));
+  if (p->ref) {
+    const size_t bytes = (size_t)p->ref_ld * sizeof(float);
+    HIPCHK(hipMalloc(&s.row, bytes));
+    HIPCHK(hipMemsetAsync(s.row, 0, bytes, p->ctx->stream));  // the zero tail past n
+  } else {
+    CHECK(alloc_planes(p->ctx, &s.b, 1));
+  }
   HIPCHK(hipMalloc(&s.mass, 64));
   p->slots.push_back(s);
   *out = (int)p->slots.size() - 1;
@@ -353,42 +366,62 @@ int pack_rows(pp2_planner* p, pp2::PlaneSet src, int K, float* dst) {
   return PP2_OK;
 }
 
-// Normalise the raw belief in slot s as the reference's host does
-// (search_tree_cuda.cu:225-229): sum = accumulate(b) in x order, then
-// b[x] /= sum (IEEE); the slot's mass becomes 1.
-int ref_normalize_slot(pp2_planner* p, int s) {
+// The FIB alphas as 9 dense rows, repacked when they changed.
+int ref_frows(pp2_planner* p) {
   pp2_ctx* c = p->ctx;
-  const Slot& sl = p->slots[s];
-  const int n = (int)p->n, ld = p->ref_ld;
-  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
-  HIPCHK(pp2::launch_lane_sums(c->stream, p->d_parent, ld, 1, n, p->d_rsum));
-  HIPCHK(pp2::launch_rows_div(c->stream, p->d_parent, ld, 1, n, p->d_rsum));
-  HIPCHK(pp2::launch_unpack(c->stream, c->g, 1, p->d_parent, sl.b.v));
-  const float one = 1.0f;
-  HIPCHK(hipMemcpyAsync(sl.mass, &one, sizeof one, hipMemcpyHostToDevice, c->stream));
-  return PP2_OK;
-}
-
-// evaluateFibCpu (first maximum of the 9 x-ordered dots) and evaluatePbviCpu
-// (first maximum over the alphas) of `rows` dense normalised beliefs: FIB dots
-// into d_rout[9 + 9 r + i], PBVI maxima into h_lbv[r].  Asynchronous.
-int ref_leaf_bounds(pp2_planner* p, const float* d_rows, int rows) {
-  pp2_ctx* c = p->ctx;
-  const int n = (int)p->n, ld = p->ref_ld;
-  if (p->frows_version != c->fib_version) {  // the alphas changed since the last pack
+  if (p->frows_version != c->fib_version) {
     CHECK(pack_rows(p, c->fib[c->fcur].v, 9, p->d_frows));
     p->frows_version = c->fib_version;
   }
-  HIPCHK(pp2::launch_lane_dots(c->stream, d_rows, rows, p->d_frows, 9, ld, n, p->d_rout + 9, 9));
-  if (p->pbvi) {
-    const float* al = nullptr;
-    int S = 0, Sp = 0, ald = 0;
-    CHECK(pbvi_alphas(c, &al, &S, &Sp, &ald));
-    if (S != p->lb_S || ald != ld)
-      return set_err(PP2_ESTATE, "PBVI alpha vectors changed size since the planner was created");
-    HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, al, S, ld, n,
-                                  p->d_lbdots, S));
-    HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, rows, S, S, p->d_lbidx, p->d_lbv));
+  return PP2_OK;
+}
+
+// evaluatePbviCpu (first maximum over the alphas, x-ordered dots) of `rows`
+// dense normalised beliefs into h_lbv[r].  Asynchronous.
+int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows) {
+  pp2_ctx* c = p->ctx;
+  const float* al = nullptr;
+  int S = 0, Sp = 0, ald = 0;
+  CHECK(pbvi_alphas(c, &al, &S, &Sp, &ald));
+  if (S != p->lb_S || ald != p->ref_ld)
+    return set_err(PP2_ESTATE, "PBVI alpha vectors changed size since the planner was created");
+  HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, al, S, p->ref_ld,
+                                (int)p->n, p->d_lbdots, S));
+  HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, rows, S, S, p->d_lbidx, p->d_lbv));
+  return PP2_OK;
+}
+
+// The VNode constructor's bounds of one dense normalised row
+// (search_tree_cuda.cu:368-388): evaluateFibCpu's 9 dots into h_rout[9 ..
+// 17], evaluatePbviCpu into h_lbv[0].  Asynchronous.
+int ref_row_bounds(pp2_planner* p, const float* row) {
+  pp2_ctx* c = p->ctx;
+  CHECK(ref_frows(p));
+  pp2::FcArgs a;
+  a.n = (int)p->n;
+  a.ld = p->ref_ld;
+  a.row = row;
+  a.partners = p->d_frows;
+  a.out = p->d_rout + 9;
+  a.ldo = 9;
+  HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 1, a));
+  if (p->pbvi) CHECK(ref_pbvi_bounds(p, row, 1));
+  return PP2_OK;
+}
+
+// The children `cs` (c = z * 9 + a) of the expanded belief, normalised, into
+// the rows `dst` (the QNode constructor's renormalised child beliefs).
+int ref_store_children(pp2_planner* p, const int* cs, float* const* dst, int count) {
+  pp2_ctx* c = p->ctx;
+  for (int i0 = 0; i0 < count; i0 += 144) {
+    pp2::FcStoreList L;
+    L.n = std::min(144, count - i0);
+    for (int r = 0; r < L.n; ++r) {
+      L.child[r] = cs[i0 + r];
+      L.dst[r] = dst[i0 + r];
+    }
+    HIPCHK(pp2::launch_store_children(c->stream, L, p->d_pred, p->d_lrows, p->d_csum, (int)p->n,
+                                      p->ref_ld));
   }
   return PP2_OK;
 }
@@ -406,6 +439,8 @@ float first_max9(const float* v) {
 // cudaBayesBeliefUpdate + renormalisation (search_tree_cuda.cu:213-231).
 int materialize(pp2_planner* p, VNode* v) {
   if (v->slot >= 0) return PP2_OK;
+  if (p->ref)  // every reference-order VNode gets its row when it is created
+    return set_err(PP2_ESTATE, "reference-order VNode without a belief row");
   if (!v->parent || !v->parent->parent)
     return set_err(PP2_ESTATE, "cannot materialise a detached VNode");
   VNode* pv = v->parent->parent;
@@ -420,7 +455,6 @@ int materialize(pp2_planner* p, VNode* v) {
   HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
                                   ns.mass));
   v->slot = s;
-  if (p->ref) CHECK(ref_normalize_slot(p, s));
   return PP2_OK;
 }
 
@@ -430,9 +464,8 @@ int make_root(pp2_planner* p, int s, uint8_t z, VNode** out) {
   pp2_ctx* c = p->ctx;
   const Slot& sl = p->slots[s];
   if (p->ref) {
-    // the slot holds the normalised belief (mass 1)
-    HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
-    CHECK(ref_leaf_bounds(p, p->d_parent, 1));
+    // the slot's row holds the normalised belief
+    CHECK(ref_row_bounds(p, sl.row));
     HIPCHK(hipEventRecord(p->ev_done, c->stream));
     HIPCHK(hipEventSynchronize(p->ev_done));
     VNode* v = new_vnode(p, z, 0.0f, nullptr);
@@ -465,14 +498,13 @@ int make_root(pp2_planner* p, int s, uint8_t z, VNode** out) {
 // QNode::forwardSampling + the unique-observation count of the QNode
 // constructor (search_tree_cuda.cu:176-196, :311-366) for action a, given
 // the fp32 prefix sum `cdf` of the QNode's belief.
-void sample_observations(pp2_planner* p, const std::vector<float>& cdf, uint8_t a,
+void sample_observations(pp2_planner* p, const float* cdf, size_t n, uint8_t a,
                          std::vector<uint8_t>& zs, std::vector<float>& freq) {
   const uint32_t N = p->prm.sample_num;
-  const size_t n = cdf.size();
   std::vector<uint8_t> obs(N);
   for (uint32_t j = 0; j < N; ++j) {
     const float r = (float)p->rng.next() / ((float)RAND_MAX + 1.0f);
-    size_t s1 = (size_t)(std::lower_bound(cdf.begin(), cdf.end(), r) - cdf.begin());
+    size_t s1 = (size_t)(std::lower_bound(cdf, cdf + n, r) - cdf);
     // find_if(x >= r) runs off the end when rounding leaves cdf.back() < r;
     // the reference then reads past its arrays.  Take the last cell with mass.
     if (s1 >= n) {
@@ -538,7 +570,7 @@ int expand_vnode(pp2_planner* p, VNode* v) {
   p->cdf.build(p->h_belief, n);
   std::vector<uint8_t> zs[9];
   std::vector<float> fq[9];
-  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, p->cdf.v, a, zs[a], fq[a]);
+  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, p->cdf.v.data(), n, a, zs[a], fq[a]);
   HIPCHK(hipEventSynchronize(p->ev_done));
 
   for (QNode* q : v->children)
@@ -569,46 +601,88 @@ int expand_vnode(pp2_planner* p, VNode* v) {
   return PP2_OK;
 }
 
-// VNode::expand in reference order: the 9 QNode rewards are inner_product(b,
-// R[.][a]) chains; the 144 children are cudaBayesBeliefUpdate of b
-// (k_pbvi_update), each renormalised by its own accumulate chain and IEEE
-// division; their FIB / PBVI bounds are evaluateFibCpu / evaluatePbviCpu
-// chains.  Only the children the samples select are kept, as in the
-// reference; they are re-derived (materialize) when expanded.
+// VNode::expand in reference order.  Every grid-wide sum of the reference's
+// 9 QNode constructors (search_tree_cuda.cu:161-242) is formed on the device
+// with the bits of its x-ordered fp32 host chain (pp2_fchain.hip):
+//   the sampling cdf of the expanded belief (:176-183),
+//   the 9 rewards inner_product(b, R[.][a]) (:168-173),
+//   the 144 children's accumulate (:225-227) -- child (a, z) =
+//   cudaBayesBeliefUpdate(b, a, z), the 9 action predictions formed once --
+//   and their evaluateFibCpu dots after the division (:228-229, :378).
+// The host draws the samples from the cdf while the device forms the rest;
+// only the children the samples keep are stored (normalised rows), so a
+// later expansion or re-rooting finds them ready.
 int expand_vnode_ref(pp2_planner* p, VNode* v) {
   pp2_ctx* c = p->ctx;
-  CHECK(materialize(p, v));
-  const Slot& sl = p->slots[v->slot];
+  if (v->slot < 0) return set_err(PP2_ESTATE, "reference-order VNode without a belief row");
+  const float* brow = p->slots[v->slot].row;
   const size_t n = p->n;
   const int ld = p->ref_ld;
-  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_dense, nullptr));
+  CHECK(ref_frows(p));
+  {
+    pp2::FcArgs a;  // the running sums, for the host's samples
+    a.n = (int)n;
+    a.ld = ld;
+    a.row = brow;
+    a.out = p->d_rsum;
+    a.cdf = p->d_cdf;
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, a));
+  }
   HIPCHK(hipEventRecord(p->ev_belief, c->stream));
-  HIPCHK(pp2::launch_pack(c->stream, c->g, 1, sl.b.v, p->d_parent, nullptr));
-  // the 9 reward chains need only the parent: on the side stream, beside
-  // the children's update and renormalisation chains
+  HIPCHK(pp2::launch_tree_pred(c->stream, c->g, c->T.v, brow, ld, p->d_pred));
+  // the 9 reward chains need only the parent: on the side stream
   HIPCHK(hipEventRecord(p->ev_fork, c->stream));
   HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
-  HIPCHK(pp2::launch_lane_dots(p->side, p->d_parent, 1, p->d_rrows, 9, ld, (int)n, p->d_rout,
-                                9));
+  {
+    pp2::FcArgs a;
+    a.n = (int)n;
+    a.ld = ld;
+    a.row = brow;
+    a.partners = p->d_rrows;
+    a.out = p->d_rout;
+    a.ldo = 9;
+    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, a));
+  }
   HIPCHK(hipEventRecord(p->ev_join, p->side));
-  HIPCHK(pp2::launch_pbvi_update(c->stream, c->g, c->T.v, c->L.v, p->d_parent, ld, p->d_srow,
-                                 p->d_us, p->d_zs, 144, p->d_children));
-  HIPCHK(pp2::launch_lane_sums(c->stream, p->d_children, ld, 144, (int)n, p->d_rsum));
-  HIPCHK(pp2::launch_rows_div(c->stream, p->d_children, ld, 144, (int)n, p->d_rsum));
-  CHECK(ref_leaf_bounds(p, p->d_children, 144));
+  {
+    pp2::FcArgs a;  // the children's masses, then their FIB dots
+    a.n = (int)n;
+    a.ld = ld;
+    a.pred = p->d_pred;
+    a.lrows = p->d_lrows;
+    a.out = p->d_csum;
+    a.ldo = 1;
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_CHILD, 0, 144, a));
+    a.sums = p->d_csum;
+    a.partners = p->d_frows;
+    a.out = p->d_rout + 9;
+    a.ldo = 9;
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_CHILD_NORM, 9, 144, a));
+  }
+  if (p->pbvi) {  // all 144 children materialised for the PBVI dots
+    int cs[144];
+    float* dst[144];
+    for (int k = 0; k < 144; ++k) {
+      cs[k] = k;
+      dst[k] = p->d_children + (size_t)k * ld;
+    }
+    CHECK(ref_store_children(p, cs, dst, 144));
+    CHECK(ref_pbvi_bounds(p, p->d_children, 144));
+  }
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
   HIPCHK(hipEventSynchronize(p->ev_belief));
 
-  p->cdf.build(p->h_belief, n);
   std::vector<uint8_t> zs[9];
   std::vector<float> fq[9];
-  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, p->cdf.v, a, zs[a], fq[a]);
+  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, p->h_cdf, n, a, zs[a], fq[a]);
   HIPCHK(hipEventSynchronize(p->ev_done));
 
   for (QNode* q : v->children)
     if (q) delete_subtree(p, q);
   v->children.assign(9, nullptr);
+  std::vector<int> keep;
+  std::vector<float*> rows;
   for (uint8_t a = 0; a < 9; ++a) {
     QNode* q = new QNode();
     ++p->n_qnodes;
@@ -622,11 +696,17 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       cv->upper_bound = first_max9(p->h_rout + 9 + 9 * row);
       cv->lower_bound = p->pbvi ? p->h_lbv[row] : p->lb_const;
       cv->heuristic = cv->upper_bound - cv->lower_bound;
+      CHECK(acquire_slot(p, &cv->slot));
+      keep.push_back(row);
+      rows.push_back(p->slots[cv->slot].row);
       q->children.push_back(cv);
     }
     qnode_update(p, q);
     v->children[a] = q;
   }
+  // the kept children's rows (queued behind this expansion's kernels, ahead
+  // of anything that reads them)
+  CHECK(ref_store_children(p, keep.data(), rows.data(), (int)keep.size()));
   vnode_update(v);
   ++p->expansions;
   return PP2_OK;
@@ -681,10 +761,27 @@ int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
   pp2_ctx* c = p->ctx;
   const Slot& os = p->slots[root->slot];
   const Slot& ns = p->slots[s];
-  CHECK(launch_belief(c, os.b.v.p, ns.b.v.p, a, z, os.mass, p->d_bpart));
-  HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
-                                  ns.mass));
-  if (p->ref) CHECK(ref_normalize_slot(p, s));
+  if (p->ref) {
+    // (search_tree_cuda.cu:586-612) update, accumulate, divide: the child
+    // (a, z) of the old root's row, as an expansion forms it
+    const int cz = z * 9 + a;
+    HIPCHK(pp2::launch_tree_pred(c->stream, c->g, c->T.v, os.row, p->ref_ld, p->d_pred));
+    pp2::FcArgs fa;
+    fa.n = (int)p->n;
+    fa.ld = p->ref_ld;
+    fa.pred = p->d_pred;
+    fa.lrows = p->d_lrows;
+    fa.g0 = cz;
+    fa.out = p->d_csum;
+    fa.ldo = 1;
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_CHILD, 0, 1, fa));
+    float* dst = ns.row;
+    CHECK(ref_store_children(p, &cz, &dst, 1));
+  } else {
+    CHECK(launch_belief(c, os.b.v.p, ns.b.v.p, a, z, os.mass, p->d_bpart));
+    HIPCHK(pp2::launch_sum_finalize(c->stream, p->d_bpart, pp2::mass_partials(c->g, c->cpt),
+                                    ns.mass));
+  }
   VNode* nv = nullptr;
   CHECK(make_root(p, s, 0, &nv));
   if (root_q) delete_qnode_only(p, root_q);
@@ -829,7 +926,11 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         hipMalloc(&p->d_rrows, (size_t)9 * row_ld * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_frows, (size_t)9 * row_ld * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_rsum, 256 * sizeof(float)) != hipSuccess ||
-        !host_mapped(kRefOutFloats, &p->h_rout, &p->d_rout))
+        hipMalloc(&p->d_lrows, (size_t)16 * row_ld * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_pred, (size_t)9 * row_ld * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_csum, 144 * sizeof(float)) != hipSuccess ||
+        !host_mapped(kRefOutFloats, &p->h_rout, &p->d_rout) ||
+        !host_mapped(p->n, &p->h_cdf, &p->d_cdf))
       return fail(set_err(PP2_ENOMEM, "planner reference-order scratch allocation failed"));
     std::vector<int> srow(144, 0);
     std::vector<uint8_t> us(144), zs(144);
@@ -848,7 +949,12 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         hipMemcpyAsync(p->d_us, us.data(), 144, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipMemcpyAsync(p->d_zs, zs.data(), 144, hipMemcpyHostToDevice, c->stream) != hipSuccess)
       return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
+    if (hipMemsetAsync(p->d_lrows, 0, (size_t)16 * row_ld * sizeof(float), c->stream) !=
+            hipSuccess ||
+        hipMemsetAsync(p->d_pred, 0, (size_t)9 * row_ld * sizeof(float), c->stream) != hipSuccess)
+      return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
     if ((s = pack_rows(p, c->R.v, 9, p->d_rrows))) return fail(s);
+    if ((s = pack_rows(p, c->L.v, 16, p->d_lrows))) return fail(s);
     if (hipStreamSynchronize(c->stream) != hipSuccess)
       return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
   }
@@ -871,12 +977,15 @@ int pp2_planner_destroy(pp2_planner* p) {
   for (Slot& s : p->slots) {
     free_planes(&s.b);
     if (s.mass) (void)hipFree(s.mass);
+    if (s.row) (void)hipFree(s.row);
   }
   free_planes(&p->P);
   for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_parent, p->d_children,
-                   p->d_lbpart, p->d_lbdots, p->d_rrows, p->d_frows, p->d_rsum})
+                   p->d_lbpart, p->d_lbdots, p->d_rrows, p->d_frows, p->d_rsum, p->d_lrows,
+                   p->d_pred, p->d_csum})
     if (d) (void)hipFree(d);
   if (p->h_rout) (void)hipHostFree(p->h_rout);
+  if (p->h_cdf) (void)hipHostFree(p->h_cdf);
   for (void* d : {(void*)p->d_lbidx, (void*)p->d_srow, (void*)p->d_us, (void*)p->d_zs})
     if (d) (void)hipFree(d);
   if (p->h_lbv) (void)hipHostFree(p->h_lbv);
@@ -904,7 +1013,11 @@ int pp2_planner_step(pp2_planner* p, uint8_t action, uint8_t observation,
     // new SearchTree(msg->belief) (path_planning_2d.cu:212-213)
     int s = -1;
     CHECK(acquire_slot(p, &s));
-    CHECK(upload_planes(c, p->slots[s].b, belief));
+    if (p->ref)
+      HIPCHK(hipMemcpyAsync(p->slots[s].row, belief, p->n * sizeof(float), hipMemcpyHostToDevice,
+                            c->stream));
+    else
+      CHECK(upload_planes(c, p->slots[s].b, belief));
     const float one = 1.0f;
     HIPCHK(hipMemcpyAsync(p->slots[s].mass, &one, sizeof one, hipMemcpyHostToDevice, c->stream));
     CHECK(make_root(p, s, 0, &p->root));

@@ -1,4 +1,4 @@
-// stub (syntax check only): boost::shared_ptr as the adapters use it
+// stand-in (tests only): boost::shared_ptr as the adapters use it
 #pragma once
 #include <memory>
 namespace boost {

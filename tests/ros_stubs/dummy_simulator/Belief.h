@@ -1,4 +1,4 @@
-// stub (syntax check only): the message of dummy_simulator/msg/Belief.msg
+// stand-in (tests only): the message of dummy_simulator/msg/Belief.msg
 // (header; uint8 action; uint8[4] measurement; int32[2] location;
 // float32[] belief) as roscpp generates it
 #pragma once

@@ -1,4 +1,4 @@
-// stub (syntax check only)
+// stand-in (tests only)
 #pragma once
 namespace geometry_msgs {
 struct Point {

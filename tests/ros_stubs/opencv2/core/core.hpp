@@ -1,13 +1,15 @@
-// stub (syntax check only): the cv::Mat members the map loaders use
+// stand-in OpenCV core (tests only): the cv::Mat members the map loaders use
 #pragma once
 #include <cstdint>
+#include <vector>
 namespace cv {
 class Mat {
  public:
   int rows = 0, cols = 0;
+  std::vector<uint8_t> data_;  // 8-bit, one channel, row-major
   template <class T>
-  const T* ptr(int) const {
-    return nullptr;
+  const T* ptr(int y) const {
+    return reinterpret_cast<const T*>(data_.data() + (size_t)y * cols);
   }
 };
 }  // namespace cv

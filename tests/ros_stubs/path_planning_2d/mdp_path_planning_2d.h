@@ -1,4 +1,4 @@
-// stub (syntax check only): the interface of the catkin package's unchanged
+// stand-in (tests only): the interface of the catkin package's unchanged
 // MDP node class, include/path_planning_2d/mdp_path_planning_2d.h:24-78 of
 // the reference -- the members ros/src/mdp/path_planning_2d_pp2.cpp defines.
 #pragma once
@@ -10,6 +10,7 @@ namespace path_planning_2d {
 
 class MdpPathPlanning2d : public PathPlanning2dBase {
  public:
+  typedef boost::shared_ptr<MdpPathPlanning2d> Ptr;
   explicit MdpPathPlanning2d(ros::NodeHandle& n);
   ~MdpPathPlanning2d();
   virtual bool initialize();

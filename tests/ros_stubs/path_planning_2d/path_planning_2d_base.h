@@ -1,7 +1,8 @@
-// stub (syntax check only): the interface of the catkin package's unchanged
+// stand-in (tests only): the interface of the catkin package's unchanged
 // base class, include/path_planning_2d/path_planning_2d_base.h:31-93 of the
 // reference -- the pure virtuals the node classes override and the protected
-// members they use.
+// members they use.  Like the reference's, the destructor is NOT virtual
+// (:43); the node mains hold the derived classes' own Ptr types.
 #pragma once
 #include <cstdint>
 #include <cstdio>
@@ -16,9 +17,10 @@ namespace path_planning_2d {
 class PathPlanning2dBase {
  public:
   typedef boost::shared_ptr<PathPlanning2dBase> Ptr;
+  typedef boost::shared_ptr<const PathPlanning2dBase> ConstPtr;
   explicit PathPlanning2dBase(ros::NodeHandle& n) : nh(n) {}
   PathPlanning2dBase(const PathPlanning2dBase&) = delete;
-  virtual ~PathPlanning2dBase() {}
+  ~PathPlanning2dBase() {}
   virtual bool initialize() = 0;
 
  protected:

@@ -1,4 +1,4 @@
-// stub (syntax check only): std_msgs/Byte
+// stand-in (tests only): std_msgs/Byte
 #pragma once
 #include <cstdint>
 #include <boost/shared_ptr.hpp>

@@ -1,4 +1,4 @@
-// stub (syntax check only)
+// stand-in (tests only)
 #pragma once
 #include <cstdint>
 #include <string>

@@ -1,4 +1,4 @@
-// stub (syntax check only): std_srvs/Trigger
+// stand-in (tests only): std_srvs/Trigger
 #pragma once
 #include <string>
 namespace std_srvs {

@@ -1,4 +1,4 @@
-// stub (syntax check only): visualization_msgs/Marker fields the MDP node sets
+// stand-in (tests only): visualization_msgs/Marker fields the MDP node sets
 #pragma once
 #include <cstdint>
 #include <string>

@@ -1,0 +1,124 @@
+"""GPU: the reference-order sums of pp2_fchain.hip equal the reference's
+sequential x86 fp32 chains bit for bit (std::accumulate, std::partial_sum,
+std::inner_product: search_tree_cuda.cu:168-183, :225-229; evaluateFibCpu
+fast_informed_bound_cuda.cu:278-297), on adversarial rows: ties at half an
+ulp, binade crossings onto powers of two, subnormals, -0, all-non-positive and
+mixed-sign chains, a single huge term, a uniform belief of 65536 cells, and
+sizes across the chunk geometry (1 .. 2^20 cells).
+
+The checker is numpy's float32 add.accumulate (one left-to-right fp32 chain,
+checked against the oracle's orc_sum_seq below) over IEEE float32 products.
+The planner-level parity of the same kernels (children's masses, FIB dots,
+rewards, the sampling cdf) is tests/test_gpu_planner.py's reference-order
+tests."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+_f32p = C.POINTER(C.c_float)
+
+
+def _fn():
+    from path_planning_2d_amd import _lib
+    lib = _lib.load()
+    f = lib.pp2_debug_fchain_row
+    f.argtypes = [C.c_int, _f32p, _f32p, C.c_int, _f32p, _f32p]
+    f.restype = C.c_int
+    return f
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_f32p) if a is not None else _f32p()
+
+
+def device_row(x, partners=None, cdf=False):
+    x = np.ascontiguousarray(x, np.float32)
+    K = 9 if partners is not None else 0
+    out = np.zeros(16, np.float32)
+    c = np.zeros(x.size, np.float32) if cdf else None
+    p = np.ascontiguousarray(partners, np.float32) if partners is not None else None
+    st = _fn()(x.size, _ptr(x), _ptr(p), K, _ptr(out), _ptr(c))
+    assert st == 0, st
+    return out[:9] if K else out[0], c
+
+
+def seq(t):
+    t = np.asarray(t, np.float32)
+    # the chain starts at +0.0 (+0.0 + -0.0 = +0.0)
+    c = np.add.accumulate(np.concatenate([np.zeros(1, np.float32), t]), dtype=np.float32)[1:]
+    return (c[-1] if t.size else np.float32(0.0)), c
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+def rows(rng):
+    U = lambda n: rng.random(n, dtype=np.float32)  # noqa: E731
+    yield "uniform", U(70001)
+    yield "wide", np.ldexp(U(65536), -rng.integers(0, 60, 65536)).astype(np.float32)
+    yield "constant", np.full(65536, 1.0 / 52429.0, np.float32)
+    yield "sparse", np.where(rng.random(65536) < 0.15, U(65536) * 1e-5, 0).astype(np.float32)
+    yield "nonpositive", (-U(40000) * 37).astype(np.float32)
+    yield "few bits (ties)", np.ldexp(rng.integers(0, 8, 65536), -20).astype(np.float32)
+    yield "subnormal", np.ldexp(U(30000), -140).astype(np.float32)
+    yield "mixed sign", (U(30000) - 0.5).astype(np.float32)
+    t = np.full(3001, np.ldexp(1.0, -25), np.float32)
+    t[:3] = [0.5, 0.25, 0.25]
+    yield "onto 2^0", t
+    t = np.full(5001, np.ldexp(1.0, -24), np.float32)
+    t[0] = 1.0
+    yield "half-ulp ties", t
+    t = U(50000) * 1e-3
+    t[25000] = 1e30
+    yield "one huge term", t.astype(np.float32)
+    t = np.zeros(4096, np.float32)
+    t[::2] = -0.0
+    yield "-0 and +0", t
+    yield "empty", np.zeros(0, np.float32)
+    yield "single", np.array([-3.5], np.float32)
+    for n in (1, 63, 64, 65, 255, 256, 257, 4000, 65535, 262144 + 7, 1 << 20):
+        yield f"n={n}", U(n)
+
+
+def test_numpy_accumulate_is_the_sequential_chain(oracle):
+    rng = np.random.default_rng(3)
+    t = rng.random(100003, dtype=np.float32)
+    lib = oracle.lib()
+    lib.orc_sum_seq.restype = C.c_float
+    lib.orc_sum_seq.argtypes = [C.c_size_t, _f32p]
+    assert bits(seq(t)[0]) == bits(lib.orc_sum_seq(t.size, _ptr(t)))
+
+
+def test_fchain_sums_and_running_sums_bit_exact():
+    rng = np.random.default_rng(11)
+    for name, t in rows(rng):
+        want, wc = seq(t)
+        got, gc = device_row(t, cdf=True)
+        assert bits(got) == bits(want), f"{name}: sum {got!r} != {want!r}"
+        assert np.array_equal(bits(gc), bits(wc)), \
+            f"{name}: running sums differ at {np.flatnonzero(bits(gc) != bits(wc))[:5]}"
+
+
+def test_fchain_dots_bit_exact():
+    """inner_product(x, a_i): the product rounded, then the chain."""
+    rng = np.random.default_rng(12)
+    for name, t in rows(rng):
+        n = t.size
+        A = np.empty((9, n), np.float32)
+        A[0] = -(20 + 20 * rng.random(n, dtype=np.float32))   # FIB-like alphas
+        A[1] = rng.random(n, dtype=np.float32) - 0.5            # mixed sign
+        A[2] = 0.0
+        A[3] = -2.0                                              # rewards
+        A[4] = np.ldexp(1.0, -rng.integers(0, 30, n))
+        A[5] = -np.float32(1.0 / 3.0)
+        A[6] = rng.random(n, dtype=np.float32) * 1e20
+        A[7] = -0.0
+        A[8] = 1.0
+        got, _ = device_row(t, partners=A)
+        for i in range(9):
+            want, _ = seq(t * A[i])
+            assert bits(got[i]) == bits(want), f"{name} partner {i}: {got[i]!r} != {want!r}"

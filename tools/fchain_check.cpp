@@ -1,0 +1,182 @@
+// fchain_check.cpp -- CPU check of the exact parallel fp32 chain
+// (path_planning_2d_amd/csrc/pp2_fchain.h) against the plain sequential
+// chain, on adversarial inputs.  It restates the device algorithm's structure
+// (chunk tables from an approximate running sum, a driver that applies 64
+// chunk entries per step by a prefix scan and adds failing chunks term by
+// term) so that the logic is exercised without a GPU.  Built and run by
+// tests/test_fchain_cpu.py:
+//   g++ -O2 -std=c++17 -ffp-contract=off -I path_planning_2d_amd/csrc tools/fchain_check.cpp
+// Exit status 0 = every case bit-exact.
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <cmath>
+#include <random>
+#include <vector>
+
+#include "pp2_fchain.h"
+
+using namespace pp2::fchain;
+
+static float seq_sum(const std::vector<float>& t) {
+  float s = 0.0f;
+  for (float v : t) s = s + v;
+  return s;
+}
+
+struct Stats {
+  long chunks = 0, fallback = 0;
+};
+
+// The device algorithm, chunk = `chunk` terms.
+static float fchain_sum(const std::vector<float>& t, int chunk, Stats* st) {
+  const int n = (int)t.size();
+  if (n == 0) return 0.0f;
+  bool pos = false, neg = false, bad = false;
+  for (float v : t) {
+    if (!std::isfinite(v)) bad = true;
+    else if (v > 0.0f) pos = true;
+    else if (v < 0.0f) neg = true;
+  }
+  if (bad || (pos && neg)) return seq_sum(t);
+  const int nch = (n + chunk - 1) / chunk;
+  // pass 1: approximate chunk sums of |t|, exclusive prefix
+  std::vector<float> P(nch);
+  float run = 0.0f;
+  for (int j = 0; j < nch; ++j) {
+    P[j] = run;
+    float a = 0.0f;
+    for (int x = j * chunk; x < n && x < (j + 1) * chunk; ++x) a += fabsf(t[x]);
+    run += a;
+  }
+  // pass 2: tables (the increment sum in any order: here reversed)
+  std::vector<uint32_t> tab(nch);
+  for (int j = 0; j < nch; ++j) {
+    const int E = domain_of(P[j]);
+    float d = 0.0f;
+    bool tie = false;
+    const int x1 = std::min(n, (j + 1) * chunk);
+    for (int x = x1 - 1; x >= j * chunk; --x) {
+      bool tx;
+      d += units_of(fabsf(t[x]), E, &tx);
+      tie |= tx;
+    }
+    tab[j] = make_entry(E, d, tie);
+  }
+  // driver: 64 chunks per step
+  int E = kEMin, k = 0;
+  int j = 0;
+  while (j < nch) {
+    int incl[64];
+    bool ok[64];
+    int acc = 0;
+    for (int l = 0; l < 64; ++l) {
+      const int jj = j + l;
+      const uint32_t e = jj < nch ? tab[jj] : kNoEntry;
+      const bool valid = e != kNoEntry && entry_domain(e) == E;
+      acc += valid ? entry_units(e) : 0;
+      incl[l] = acc;
+      ok[l] = valid && k + acc <= kK24;
+    }
+    int f = 0;
+    while (f < 64 && ok[f]) ++f;
+    if (f > 0) {
+      k += incl[f - 1];
+      normalise(&E, &k);
+    }
+    st->chunks += f;
+    j += f;
+    if (j < nch && f < 64) {
+      float s = value_of(E, k);
+      const int x1 = std::min(n, (j + 1) * chunk);
+      for (int x = j * chunk; x < x1; ++x) s = s + fabsf(t[x]);
+      state_of(s, &E, &k);
+      ++st->chunks;
+      ++st->fallback;
+      ++j;
+    }
+  }
+  const float r = value_of(E, k);
+  if (neg) return r == 0.0f ? 0.0f : -r;
+  return r;
+}
+
+static int fails = 0;
+
+static void check(const char* what, const std::vector<float>& t, int chunk, Stats* st) {
+  const float a = seq_sum(t), b = fchain_sum(t, chunk, st);
+  if (bits_of(a) != bits_of(b) && !(std::isnan(a) && std::isnan(b))) {
+    if (fails < 20)
+      printf("MISMATCH %s n=%zu chunk=%d: seq %.9g (0x%08x) fchain %.9g (0x%08x)\n", what,
+             t.size(), chunk, a, bits_of(a), b, bits_of(b));
+    ++fails;
+  }
+}
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 200;
+  std::mt19937_64 rng(12345);
+  std::uniform_real_distribution<float> U(0.0f, 1.0f);
+  Stats st;
+  const int chunks[] = {1, 4, 64, 256, 1000};
+  for (int rep = 0; rep < reps; ++rep) {
+    const int n = (int)(rng() % 70000);
+    const int chunk = chunks[rng() % 5];
+    std::vector<float> t(n);
+    const int kind = rep % 10;
+    for (int x = 0; x < n; ++x) {
+      float v = 0.0f;
+      switch (kind) {
+        case 0: v = U(rng); break;                                       // uniform
+        case 1: v = ldexpf(U(rng), -(int)(rng() % 60)); break;           // wide range
+        case 2: v = 1.0f / 52429.0f; break;                              // constant
+        case 3: v = (rng() % 7 == 0) ? U(rng) * 1e-5f : 0.0f; break;     // sparse
+        case 4: v = -U(rng) * 37.0f; break;                              // non-positive
+        case 5: v = ldexpf((float)(rng() % 8), -20); break;              // few bits: ties
+        case 6: v = ldexpf(U(rng), -140); break;                         // subnormal range
+        case 7: v = (rng() % 2 ? 1.0f : -1.0f) * U(rng); break;          // mixed sign
+        case 8: v = (x % 3 == 0) ? -0.0f : -ldexpf(U(rng), -10); break;  // -0 and negatives
+        case 9: v = x == n / 2 ? 1e30f : U(rng) * 1e-3f; break;          // one huge term
+      }
+      t[x] = v;
+    }
+    check("random", t, chunk, &st);
+  }
+  // ties by construction: s = 1 (k = 2^23 at E = 0), terms of half an ulp
+  {
+    std::vector<float> t(1, 1.0f);
+    for (int i = 0; i < 5000; ++i) t.push_back(ldexpf(1.0f, -24));
+    for (int c : chunks) check("half-ulp ties", t, c, &st);
+    t.assign(1, 1.0f + ldexpf(1.0f, -23));
+    for (int i = 0; i < 5000; ++i) t.push_back(ldexpf(1.0f, -24) * (i % 3 == 0 ? 3.0f : 1.0f));
+    for (int c : chunks) check("tie parity", t, c, &st);
+  }
+  // crossing exactly onto a power of two, then tiny terms
+  {
+    std::vector<float> t = {0.5f, 0.25f, 0.25f};
+    for (int i = 0; i < 3000; ++i) t.push_back(ldexpf(1.0f, -25));
+    for (int c : chunks) check("onto 2^k", t, c, &st);
+  }
+  // all zeros, -0, empty, single
+  {
+    std::vector<float> z(1000, 0.0f), mz(1000, -0.0f), e, one(1, -3.5f);
+    for (int c : chunks) {
+      check("zeros", z, c, &st);
+      check("-zeros", mz, c, &st);
+      check("empty", e, c, &st);
+      check("single", one, c, &st);
+    }
+  }
+  // a belief-like sum: uniform over 65536 cells, and products with alphas
+  {
+    std::vector<float> b(65536), d(65536);
+    for (int i = 0; i < 65536; ++i) b[i] = 1.0f / 52429.0f * (i % 5 ? 1.0f : 0.0f);
+    for (int i = 0; i < 65536; ++i) d[i] = b[i] * -(20.0f + 20.0f * U(rng));
+    check("belief", b, 256, &st);
+    check("belief dot", d, 256, &st);
+  }
+  printf("fchain_check: %d mismatches; %ld chunks, %ld term-by-term (%.2f %%)\n", fails,
+         st.chunks, st.fallback, st.chunks ? 100.0 * st.fallback / st.chunks : 0.0);
+  return fails ? 1 : 0;
+}
