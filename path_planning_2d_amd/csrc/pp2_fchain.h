@@ -102,6 +102,23 @@ PP2_FC_HD inline float units_of(float a, int E, bool* tie) {
   return r;
 }
 
+// One term a = |t| (finite) added to the state exactly: its increment when
+// that applies (no tie, the sum stays within 2^(E+1)), else the fp32 add
+// itself.  (k == 2^24 is left as is: a later increment of 0 keeps it, any
+// other goes through the fp32 add from value_of, which normalises.)  A wave
+// applies this to a chunk's terms in parallel: the increments' prefix sum up
+// to the first term that does not apply, that term's fp32 add, and again.
+PP2_FC_HD inline void add_exact(int* E, int* k, float a) {
+  bool tie;
+  const float r = units_of(a, *E, &tie);
+  if (!tie && *k + (int)r <= kK24) {
+    *k += (int)r;
+  } else {
+    const float s = value_of(*E, *k) + a;
+    state_of(s, E, k);
+  }
+}
+
 // Table entry of a chunk: d units in domain E, or kNoEntry.
 PP2_FC_HD inline uint32_t make_entry(int E, float d, bool tie) {
   if (tie || !(d < (float)kK24)) return kNoEntry;

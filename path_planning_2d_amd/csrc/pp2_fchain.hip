@@ -5,14 +5,25 @@
 // (cudaBayesBeliefUpdate under --use_fast_math): their one product per cell
 // is flushed here explicitly, as the oracle's ftzf does.
 //
-//   k_fchain<BASE, K>  one workgroup per group of K chains (K = 0: one chain
-//                      of the base terms themselves) over x = 0 .. n-1:
-//                      std::accumulate (search_tree_cuda.cu:225-229),
-//                      std::inner_product (:168-173, evaluateFibCpu
-//                      fast_informed_bound_cuda.cu:278-297) and, for a row,
-//                      the running sums (forwardSampling's cdf, :176-183)
-//   k_store_children   child = fl(pred_a * L_z) / sum (the QNode constructor's
-//                      renormalisation :225-229) into the kept nodes' rows
+// A set of chains (G groups x K partners, or K = 0: one chain of the base
+// terms per group) runs as three launches:
+//   k_fc_sums    per 256-cell chunk and chain: the approximate sum of |t|
+//                (any order; it only picks each chunk's binade), sign flags
+//   k_fc_tables  per chunk and chain: the approximate running sum before the
+//                chunk, its binade E, and the chunk's increment in E
+//   k_fc_drive   one wave per chain: the exact state walked over the chunk
+//                entries 64 at a time; the chunks whose entry does not apply
+//                (binade crossings, ties, a neighbouring E) term by term with
+//                add_exact -- a prefix scan up to the first term that does
+//                not apply, its fp32 add, again -- from terms prefetched into
+//                LDS where the tables predicted the fallback
+// and, for a row's running sums (forwardSampling's cdf), k_fc_cdf: every
+// chunk from its exact start state, term by term as above.
+//
+// Reference sums (search_tree_cuda.cu): std::accumulate of a child belief
+// (:225-229), std::inner_product for the QNode reward (:168-173),
+// evaluateFibCpu (fast_informed_bound_cuda.cu:278-297), and the sampling cdf
+// (:176-183); k_tree_sample restates forwardSampling's draws (:311-366).
 #include <hip/hip_runtime.h>
 #include <float.h>
 
@@ -25,7 +36,12 @@ namespace {
 
 using namespace fchain;
 
-constexpr int kFcThreads = 1024, kFcWaves = kFcThreads / 64;
+typedef float f4a __attribute__((ext_vector_type(4)));
+
+constexpr int kFcChunk = 256;     // cells per chunk: 4 per lane
+constexpr int kFcSegChunks = 16;  // chunks per k_fc_sums / k_fc_tables workgroup (4 per wave)
+constexpr int kFcWin = 1024;      // chunk entries per driver window (LDS)
+constexpr int kFcStash = 8;       // predicted fallback chunks prefetched per window
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -42,87 +58,104 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
-__device__ __forceinline__ float wave_incl_scan(float v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float y = __shfl_up(v, o);
-    if (lane >= o) v += y;
-  }
-  return v;
-}
-
-__device__ __forceinline__ float lane_value(float v, int q) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), q));
-}
-
 // The device's flush of a product (FTZ build of the reference kernel).
 __device__ __forceinline__ float ftz(float v) {
   return fabsf(v) < FLT_MIN ? copysignf(0.0f, v) : v;
 }
 
-// Term sources of one group.
-template <int BASE>
-struct Base {
-  const float* __restrict__ pr;  // FC_ROW: the row; else the prediction row of action a
-  const float* __restrict__ lr;  // the likelihood row of observation z
-  float s;                       // FC_CHILD_NORM: the child's mass
+enum : uint32_t { kPos = 1u, kNeg = 2u, kBad = 4u };
+enum : uint32_t { kPredicted = 1u };  // tab[].y: the driver will likely fall back here
 
-  __device__ __forceinline__ float operator()(int x) const {
+// group g's id, and whether it is active
+__device__ __forceinline__ bool group_id(const FcArgs& a, int g, int* id) {
+  if (a.gcount && g >= *a.gcount) return false;
+  *id = a.glist ? a.glist[g] : a.g0 + g;
+  return true;
+}
+
+// The base terms of one group, and the chain terms.
+template <int BASE, int K>
+struct Terms {
+  const float* __restrict__ pr;  // FC_ROW: the row; FC_CHILD: the prediction row of action a
+  const float* __restrict__ lr;  // FC_CHILD: the likelihood row of observation z
+  const float* __restrict__ part;
+  int n, ld;
+
+  __device__ __forceinline__ void init(const FcArgs& a, int id) {
+    n = a.n;
+    ld = a.ld;
+    part = a.partners;
+    if (BASE == FC_ROW) {
+      pr = a.row + (long long)id * a.row_stride;
+      lr = nullptr;
+    } else {
+      pr = a.pred + (long long)(id % 9) * ld;
+      lr = a.lrows + (long long)(id / 9) * ld;
+    }
+  }
+  // p *= L[16 idx + z] (point_based_value_iteration_cuda.cu:130), flushed
+  __device__ __forceinline__ float base(int x) const {
     if (BASE == FC_ROW) return pr[x];
-    const float c = ftz(pr[x] * ftz(lr[x]));  // p *= L[16 idx + z] (point_based_value_iteration_cuda.cu:130)
-    return BASE == FC_CHILD_NORM ? c / s : c;  // b[x] /= sum (search_tree_cuda.cu:228-229)
+    return ftz(pr[x] * ftz(lr[x]));
+  }
+  __device__ __forceinline__ float term(float v, int i, int x) const {
+    return K > 0 ? v * part[(long long)i * ld + x] : v;
+  }
+  // the 4 terms of chain i at x0 .. x0+3 (x0 % 4 == 0; 0 past n)
+  __device__ __forceinline__ void terms4(int i, int x0, float (&t)[4]) const {
+    if (x0 + 4 <= n) {
+      const f4a p = *reinterpret_cast<const f4a*>(pr + x0);
+      f4a v = p;
+      if (BASE != FC_ROW) {
+        const f4a l = *reinterpret_cast<const f4a*>(lr + x0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ftz(p[q] * ftz(l[q]));
+      }
+      if (K > 0) {
+        const f4a w = *reinterpret_cast<const f4a*>(part + (long long)i * ld + x0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = v[q] * w[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = v[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = x0 + q < n ? term(base(x0 + q), i, x0 + q) : 0.0f;
+    }
   }
 };
 
-enum : uint32_t { kPos = 1u, kNeg = 2u, kBad = 4u };
-enum : int { kChunkTable = 0, kChunkSeq = 1 };
-
+// ---------------------------------------------------------------- pass 1
 template <int BASE, int K>
-__global__ __launch_bounds__(kFcThreads) void k_fchain(FcArgs a) {
+__global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
   constexpr int KC = K > 0 ? K : 1;
-  constexpr bool kCdfCapable = BASE == FC_ROW && K == 0;
-  __shared__ float sP[KC][kFcMaxChunks];     // approximate running sum before each chunk
-  __shared__ uint32_t sT[KC][kFcMaxChunks];  // chunk table entries
-  __shared__ int sSE[kCdfCapable ? kFcMaxChunks : 1];  // cdf: chunk start state (E + 128 | mode << 16)
-  __shared__ int sSK[kCdfCapable ? kFcMaxChunks : 1];  //      and k
-  __shared__ float sWt[KC][kFcWaves];
   __shared__ uint32_t sFlags[KC];
+  const int g = blockIdx.y, seg = blockIdx.x;
+  int id;
+  if (!group_id(a, g, &id)) return;
+  Terms<BASE, K> T;
+  T.init(a, id);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n = a.n, ld = a.ld;
-  const int cg = a.g0 + blockIdx.x;  // group (child c = z * 9 + a) index
-  Base<BASE> base;
-  if (BASE == FC_ROW) {
-    base.pr = a.row + (long long)blockIdx.x * a.row_stride;
-    base.lr = nullptr;
-    base.s = 1.0f;
-  } else {
-    base.pr = a.pred + (long long)(cg % 9) * ld;
-    base.lr = a.lrows + (long long)(cg / 9) * ld;
-    base.s = BASE == FC_CHILD_NORM ? a.sums[cg] : 1.0f;
-  }
-  const float* __restrict__ part = a.partners;
-  const bool cdf = kCdfCapable && a.cdf != nullptr;
-  const int m = fc_lane_elems(n);
-  const int chunk = 64 * m;
-  const int nch = (n + chunk - 1) / chunk;
+  const int nch = fc_chunks(a.n), nseg = fc_segments(a.n);
   if (threadIdx.x < KC) sFlags[threadIdx.x] = 0u;
   __syncthreads();
-
-  // ---- pass 1: approximate chunk sums of |t|, and the chains' sign flags
   uint32_t fl[KC];
 #pragma unroll
   for (int i = 0; i < KC; ++i) fl[i] = 0u;
-  for (int j = w; j < nch; j += kFcWaves) {
+  for (int cc = 0; cc < kFcSegChunks / 4; ++cc) {
+    const int j = seg * kFcSegChunks + w * (kFcSegChunks / 4) + cc;
+    if (j >= nch) break;
     float acc[KC];
 #pragma unroll
     for (int i = 0; i < KC; ++i) acc[i] = 0.0f;
-    for (int p = 0; p < m; ++p) {
-      const int x = j * chunk + p * 64 + lane;
-      if (x < n) {
-        const float v = base(x);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int x = j * kFcChunk + p * 64 + lane;
+      if (x < a.n) {
+        const float v = T.base(x);
 #pragma unroll
         for (int i = 0; i < KC; ++i) {
-          const float t = K > 0 ? v * part[(long long)i * ld + x] : v;
+          const float t = T.term(v, i, x);
           acc[i] += fabsf(t);
           fl[i] |= !isfinite(t) ? kBad : t > 0.0f ? kPos : t < 0.0f ? kNeg : 0u;
         }
@@ -131,7 +164,7 @@ __global__ __launch_bounds__(kFcThreads) void k_fchain(FcArgs a) {
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
       const float sum = wave_sum(acc[i]);
-      if (lane == 0) sP[i][j] = sum;
+      if (lane == 0) a.csum[(long long)(g * KC + i) * nch + j] = sum;
     }
   }
 #pragma unroll
@@ -142,47 +175,65 @@ __global__ __launch_bounds__(kFcThreads) void k_fchain(FcArgs a) {
     if (lane == 0 && f) atomicOr(&sFlags[i], f);
   }
   __syncthreads();
+  if (threadIdx.x < KC)
+    a.cflag[(long long)(g * KC + threadIdx.x) * nseg + seg] = sFlags[threadIdx.x];
+}
 
-  // ---- exclusive prefix of the chunk sums (thread t <-> chunk t)
-  {
-    const int t = threadIdx.x;
-    float own[KC], incl[KC];
+// ---------------------------------------------------------------- pass 2
+template <int BASE, int K>
+__global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
+  constexpr int KC = K > 0 ? K : 1;
+  __shared__ float sPart[KC][4];
+  __shared__ float sP[KC][kFcSegChunks];
+  const int g = blockIdx.y, seg = blockIdx.x;
+  int id;
+  if (!group_id(a, g, &id)) return;
+  Terms<BASE, K> T;
+  T.init(a, id);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nch = fc_chunks(a.n);
+  const int j0 = seg * kFcSegChunks;
+  // the approximate running sum before this segment, and inside it
 #pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      own[i] = t < nch ? sP[i][t] : 0.0f;
-      incl[i] = wave_incl_scan(own[i], lane);
-      if (lane == 63) sWt[i][w] = incl[i];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      float b0 = 0.0f;
-      for (int q = 0; q < w; ++q) b0 += sWt[i][q];
-      if (t < nch) sP[i][t] = b0 + (incl[i] - own[i]);
+  for (int i = 0; i < KC; ++i) {
+    const float* cs = a.csum + (long long)(g * KC + i) * nch;
+    float acc = 0.0f;
+    for (int t = threadIdx.x; t < j0; t += 256) acc += cs[t];
+    acc = wave_sum(acc);
+    if (lane == 0) sPart[i][w] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < KC) {
+    const int i = threadIdx.x;
+    const float* cs = a.csum + (long long)(g * KC + i) * nch;
+    float run = (sPart[i][0] + sPart[i][1]) + (sPart[i][2] + sPart[i][3]);
+    for (int c = 0; c < kFcSegChunks; ++c) {
+      sP[i][c] = run;
+      if (j0 + c < nch) run += cs[j0 + c];
     }
   }
   __syncthreads();
-
-  // ---- pass 2: chunk tables in the domain of the approximate running sum
-  for (int j = w; j < nch; j += kFcWaves) {
+  for (int cc = 0; cc < kFcSegChunks / 4; ++cc) {
+    const int jl = w * (kFcSegChunks / 4) + cc, j = j0 + jl;
+    if (j >= nch) break;
     int E[KC];
     float d[KC];
     bool tie[KC];
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
-      E[i] = domain_of(sP[i][j]);
+      E[i] = domain_of(sP[i][jl]);
       d[i] = 0.0f;
       tie[i] = false;
     }
-    for (int p = 0; p < m; ++p) {
-      const int x = j * chunk + p * 64 + lane;
-      if (x < n) {
-        const float v = base(x);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int x = j * kFcChunk + p * 64 + lane;
+      if (x < a.n) {
+        const float v = T.base(x);
 #pragma unroll
         for (int i = 0; i < KC; ++i) {
-          const float t = K > 0 ? v * part[(long long)i * ld + x] : v;
           bool tx;
-          d[i] += units_of(fabsf(t), E[i], &tx);
+          d[i] += units_of(fabsf(T.term(v, i, x)), E[i], &tx);
           tie[i] = tie[i] || tx;
         }
       }
@@ -191,130 +242,292 @@ __global__ __launch_bounds__(kFcThreads) void k_fchain(FcArgs a) {
     for (int i = 0; i < KC; ++i) {
       const float ds = wave_sum(d[i]);  // exact below 2^24; else no entry
       const bool anytie = __ballot(tie[i]) != 0ull;
-      if (lane == 0) sT[i][j] = make_entry(E[i], ds, anytie);
+      if (lane == 0) {
+        const uint32_t e = make_entry(E[i], ds, anytie);
+        // predicted fallback: no entry, or the chunk's sum likely crosses
+        // into the next binade (from the approximate running sum)
+        const bool pred = e == kNoEntry ||
+                          ldexpf(sP[i][jl], 23 - E[i]) + ds >= (float)kK24 * (1.0f - 0x1p-12f);
+        a.tab[(long long)(g * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
+      }
     }
+  }
+}
+
+// ---------------------------------------------------------------- exact chunk
+// Chunk of a non-negative chain (|t|) from the exact state (E, k): lane l
+// holds terms 4l .. 4l+3.  Each round applies the increments of the terms
+// from `done` on up to the first that does not apply (a tie, or past
+// 2^(E+1)), adds that one in fp32, and goes on after it (add_exact, in
+// parallel).  With cv, every running value (cv[q] of term 4l + q).
+__device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* pE, int* pk,
+                                            float (*cv)[4]) {
+  int E = *pE, k = *pk, done = 0;
+  for (;;) {
+    int r[4];
+    bool tie[4];
+    int tot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bool tx;
+      const float rf = units_of(t[q], E, &tx);
+      const bool act = 4 * lane + q >= done;
+      r[q] = act ? (int)rf : 0;
+      tie[q] = act && tx;
+      tot += r[q];
+    }
+    tot = min(tot, kK24 + 1);  // no scan overflow; anything above 2^24 fails anyway
+    const int incl = wave_incl_scan(tot, lane);
+    int kk = k + incl - tot, bad = 4, kb = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (bad == 4 && 4 * lane + q >= done) {
+        if (tie[q] || kk + r[q] > kK24) {
+          bad = q;
+          kb = kk;
+        } else {
+          kk += r[q];
+          if (cv) (*cv)[q] = value_of(E, kk);
+        }
+      }
+    }
+    const uint64_t bm = __ballot(bad < 4);
+    if (bm == 0ull) {
+      k += __shfl(incl, 63);
+      break;
+    }
+    const int lb = __builtin_ctzll(bm);
+    const int qb = __shfl(bad, lb), kbef = __shfl(kb, lb);
+    const float tq = qb == 0 ? t[0] : qb == 1 ? t[1] : qb == 2 ? t[2] : t[3];
+    const float tb = __shfl(tq, lb);
+    const float s = value_of(E, kbef) + tb;  // the reference's own add
+    state_of(s, &E, &k);
+    if (cv && lane == lb) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q == qb) (*cv)[q] = s;
+    }
+    // (values of later terms computed in this round were provisional: the
+    // next round recomputes them)
+    done = 4 * lb + qb + 1;
+    if (done >= kFcChunk) break;
+  }
+  *pE = E;
+  *pk = k;
+}
+
+// ---------------------------------------------------------------- driver
+template <int BASE, int K>
+__global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
+  constexpr int KC = K > 0 ? K : 1;
+  __shared__ uint2 sE[kFcWin];
+  __shared__ __attribute__((aligned(16))) float sStash[kFcStash][kFcChunk];
+  __shared__ int sStashId[kFcStash];
+  const int ch = blockIdx.x, g = ch / KC, i = ch % KC;
+  int id;
+  if (!group_id(a, g, &id)) return;
+  Terms<BASE, K> T;
+  T.init(a, id);
+  const int lane = threadIdx.x;
+  const int n = a.n, nch = fc_chunks(n), nseg = fc_segments(n);
+  const uint2* tab = a.tab + (long long)ch * nch;
+  const bool cdf = BASE == FC_ROW && K == 0 && a.cdf != nullptr;
+  uint32_t f = 0u;
+  for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)ch * nseg + s];
+  f = (__ballot((f & kPos) != 0u) ? kPos : 0u) | (__ballot((f & kNeg) != 0u) ? kNeg : 0u) |
+      (__ballot((f & kBad) != 0u) ? kBad : 0u);
+  const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
+  const bool neg = (f & kNeg) && !(f & kPos);
+  if (cdf && lane == 0) a.cst[nch] = make_int2((int)f, 0);
+  float res;
+  if (seq_all) {
+    // mixed signs or a non-finite term: the reference's chain itself
+    float s = 0.0f;
+    for (int j = 0; j < nch; ++j) {
+      float t[4];
+      T.terms4(i, j * kFcChunk + 4 * lane, t);
+      float cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int l = 0; l < 64; ++l) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          s = s + __shfl(t[q], l);
+          if (lane == l) cv[q] = s;
+        }
+      }
+      if (cdf) {
+        const int x0 = j * kFcChunk + 4 * lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (x0 + q < n) a.cdf[x0 + q] = cv[q];
+      }
+    }
+    res = s;
+  } else {
+    int E = kEMin, k = 0, j = 0, wbase = -kFcWin, nstash = 0;
+    while (j < nch) {
+      if (j >= wbase + kFcWin) {  // the next window of entries, and its predicted fallbacks
+        wbase = j;
+        for (int c = lane; c < kFcWin; c += 64)
+          sE[c] = wbase + c < nch ? tab[wbase + c] : make_uint2(kNoEntry, 0u);
+        __syncthreads();
+        nstash = 0;
+        for (int c0 = 0; c0 < kFcWin && nstash < kFcStash && wbase + c0 < nch; c0 += 64) {
+          const bool pr = wbase + c0 + lane < nch && (sE[c0 + lane].y & kPredicted);
+          uint64_t m = __ballot(pr);
+          while (m && nstash < kFcStash) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            if (lane == 0) sStashId[nstash] = wbase + c0 + l;
+            ++nstash;
+          }
+        }
+        __syncthreads();
+        // all of the window's stash loads in flight together
+        float st[kFcStash][4];
+#pragma unroll
+        for (int s2 = 0; s2 < kFcStash; ++s2)
+          if (s2 < nstash) T.terms4(i, sStashId[s2] * kFcChunk + 4 * lane, st[s2]);
+#pragma unroll
+        for (int s2 = 0; s2 < kFcStash; ++s2)
+          if (s2 < nstash)
+            *reinterpret_cast<f4a*>(&sStash[s2][4 * lane]) =
+                f4a{fabsf(st[s2][0]), fabsf(st[s2][1]), fabsf(st[s2][2]), fabsf(st[s2][3])};
+        __syncthreads();
+      }
+      const int jj = j + lane;
+      const uint2 e = jj < nch && jj < wbase + kFcWin ? sE[jj - wbase] : make_uint2(kNoEntry, 0u);
+      const bool valid = e.x != kNoEntry && entry_domain(e.x) == E;
+      const int dl = valid ? entry_units(e.x) : 0;
+      const int incl = wave_incl_scan(dl, lane);
+      const bool ok = valid && k + incl <= kK24;
+      const uint64_t badm = ~__ballot(ok);
+      const int fc = badm == 0ull ? 64 : __builtin_ctzll(badm);
+      if (cdf && lane < fc) a.cst[jj] = make_int2(E, k + incl - dl);
+      if (fc > 0) {
+        k += __shfl(incl, fc - 1);
+        normalise(&E, &k);
+      }
+      j += fc;
+      if (j < nch && fc < 64 && j < wbase + kFcWin) {
+        // chunk j term by term: from the stash, or loaded now
+        if (cdf && lane == 0) a.cst[j] = make_int2(E, k);
+        int slot = -1;
+        for (int s2 = 0; s2 < nstash; ++s2)
+          if (sStashId[s2] == j) slot = s2;
+        float t[4];
+        if (slot >= 0) {
+          const f4a v = *reinterpret_cast<const f4a*>(&sStash[slot][4 * lane]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t[q] = v[q];
+        } else {
+          T.terms4(i, j * kFcChunk + 4 * lane, t);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t[q] = fabsf(t[q]);
+        }
+        chunk_exact(t, lane, &E, &k, nullptr);
+        normalise(&E, &k);
+        ++j;
+      }
+    }
+    const float r = value_of(E, k);
+    res = neg ? (r == 0.0f ? 0.0f : -r) : r;
+  }
+  if (lane == 0) a.out[(long long)id * a.ldo + i] = res;
+}
+
+// ---------------------------------------------------------------- running sums
+// One wave per chunk: every running sum of the row from the chunk's exact
+// start state (k_fc_drive's a.cst), term by term (chunk_exact).
+__global__ __launch_bounds__(256) void k_fc_cdf(FcArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = a.n, nch = fc_chunks(n);
+  if (j >= nch) return;
+  const uint32_t f = (uint32_t)a.cst[nch].x;
+  if ((f & kBad) || ((f & kPos) && (f & kNeg))) return;  // the driver wrote them itself
+  const bool neg = (f & kNeg) && !(f & kPos);
+  Terms<FC_ROW, 0> T;
+  T.init(a, a.g0);
+  float t[4];
+  const int x0 = j * kFcChunk + 4 * lane;
+  T.terms4(0, x0, t);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t[q] = fabsf(t[q]);
+  int E = a.cst[j].x, k = a.cst[j].y;
+  float cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  chunk_exact(t, lane, &E, &k, &cv);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float v = neg ? (cv[q] == 0.0f ? 0.0f : -cv[q]) : cv[q];
+    if (x0 + q < n) a.cdf[x0 + q] = v;
+  }
+}
+
+// ---------------------------------------------------------------- sampling
+// QNode::forwardSampling for the 9 actions of an expansion
+// (search_tree_cuda.cu:176-196, :311-366): draw j of action a takes the
+// state from the belief's cdf with the host's rand() value r[a N + j]
+// (find_if: the first running sum >= r), the next state from the cumulative
+// T row with curand uniform u1[j], the observation from the cumulative L row
+// with u2[j] (host-order fp32 cumulative sums).  Then the observations'
+// counts per action, counts[a * 16 + z], and the kept children c = z * 9 + a
+// in std::set order (klist, *kcount).
+__global__ __launch_bounds__(1024) void k_tree_sample(SampleArgs s) {
+  __shared__ int cnt[144];
+  for (int i = threadIdx.x; i < 144; i += blockDim.x) cnt[i] = 0;
+  __syncthreads();
+  const int N = s.N, n = s.n, W = s.g.width;
+  for (int jt = threadIdx.x; jt < 9 * N; jt += blockDim.x) {
+    const int act = jt / N, j = jt - act * N;
+    const float r = s.r[jt];
+    int lo = 0, hi = n;  // the first x with cdf[x] >= r
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s.cdf[mid] < r) lo = mid + 1;
+      else hi = mid;
+    }
+    int s1 = lo;
+    if (s1 >= n) {  // the reference runs off its arrays: the last cell with mass
+      s1 = n - 1;
+      while (s1 > 0 && s.cdf[s1] == s.cdf[s1 - 1]) --s1;
+    }
+    const int y1 = s1 / W, x1 = s1 - y1 * W;
+    float td = 0.0f;
+    uint32_t s2i = 0;
+    bool found = false;
+    for (int q = 0; q < 9; ++q) {
+      const float tv = s.T.p[(long long)y1 * s.T.rs + (long long)(9 * act + q) * s.T.ps + x1];
+      td = q == 0 ? tv : td + tv;
+      if (!found && s.u1[j] <= td) {
+        s2i = (uint32_t)q;
+        found = true;
+      }
+    }
+    uint32_t s2 = (uint32_t)s1 + (s2i / 3 - 1) * (uint32_t)W + (s2i % 3 - 1);
+    if (s2 >= (uint32_t)n) s2 = (uint32_t)s1;  // (never with a row-stochastic T)
+    const int y2 = (int)(s2 / (uint32_t)W), x2 = (int)(s2 - (uint32_t)y2 * (uint32_t)W);
+    float ld = 0.0f;
+    int o = 0;
+    found = false;
+    for (int q = 0; q < 16; ++q) {
+      const float lv = s.L.p[(long long)y2 * s.L.rs + (long long)q * s.L.ps + x2];
+      ld = q == 0 ? lv : ld + lv;
+      if (!found && s.u2[j] <= ld) {
+        o = q;
+        found = true;
+      }
+    }
+    atomicAdd(&cnt[act * 16 + o], 1);
   }
   __syncthreads();
-
-  // term x of chain i, as the reference forms it
-  auto term = [&](int i, int x) -> float {
-    if (x >= n) return 0.0f;
-    const float v = base(x);
-    return K > 0 ? v * part[(long long)i * ld + x] : v;
-  };
-  // chunk j added term by term to s (|t| when `absd`), in x order
-  auto seq_chunk = [&](int i, int j, float s, bool absd) -> float {
-    for (int p = 0; p < m; ++p) {
-      float t = term(i, j * chunk + p * 64 + lane);
-      if (absd) t = fabsf(t);
-#pragma unroll
-      for (int q = 0; q < 64; ++q) s = s + lane_value(t, q);
-    }
-    return s;
-  };
-
-  // ---- driver: wave i walks chain i
-  if (w < KC) {
-    const int i = w;
-    const uint32_t f = sFlags[i];
-    const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
-    const bool neg = (f & kNeg) && !(f & kPos);
-    float res;
-    if (seq_all) {
-      float s = 0.0f;
-      for (int j = 0; j < nch; ++j) s = seq_chunk(i, j, s, false);
-      res = s;
-    } else {
-      int E = kEMin, k = 0, j = 0;
-      while (j < nch) {
-        const int jj = j + lane;
-        const uint32_t e = jj < nch ? sT[i][jj] : kNoEntry;
-        const bool valid = e != kNoEntry && entry_domain(e) == E;
-        const int dl = valid ? entry_units(e) : 0;
-        const int incl = wave_incl_scan(dl, lane);
-        const bool ok = valid && k + incl <= kK24;
-        const uint64_t bad = ~__ballot(ok);
-        const int fc = bad == 0ull ? 64 : __builtin_ctzll(bad);
-        if (cdf && lane < fc) {
-          sSE[jj] = (E + 128) | (kChunkTable << 16);
-          sSK[jj] = k + incl - dl;
-        }
-        if (fc > 0) {
-          k += __shfl(incl, fc - 1);
-          normalise(&E, &k);
-        }
-        j += fc;
-        if (j < nch && fc < 64) {  // a crossing, a tie or a table of another domain
-          if (cdf && lane == 0) {
-            sSE[j] = (E + 128) | (kChunkSeq << 16);
-            sSK[j] = k;
-          }
-          const float s = seq_chunk(i, j, value_of(E, k), true);
-          state_of(s, &E, &k);
-          ++j;
-        }
-      }
-      const float r = value_of(E, k);
-      res = neg ? (r == 0.0f ? 0.0f : -r) : r;
-    }
-    if (lane == 0) a.out[(long long)cg * a.ldo + i] = res;
-    if (cdf && seq_all) {  // the running sums term by term (mixed or non-finite belief)
-      float s = 0.0f;
-      for (int x0 = 0; x0 < n; x0 += 64) {
-        const float t = term(0, x0 + lane);
-        float mine = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 64; ++q) {
-          s = s + lane_value(t, q);
-          if (lane == q) mine = s;
-        }
-        if (x0 + lane < n) a.cdf[x0 + lane] = mine;
-      }
-    }
+  if (threadIdx.x == 0) {
+    int m = 0;
+    for (int act = 0; act < 9; ++act)
+      for (int z = 0; z < 16; ++z)
+        if (cnt[act * 16 + z]) s.klist[m++] = z * 9 + act;
+    *s.kcount = m;
   }
-
-  // ---- cdf: every running sum from its chunk's start state
-  if (cdf) {
-    __syncthreads();
-    const uint32_t f = sFlags[0];
-    if ((f & kBad) || ((f & kPos) && (f & kNeg))) return;
-    const bool neg = (f & kNeg) && !(f & kPos);
-    auto out_of = [&](float r) { return neg ? (r == 0.0f ? 0.0f : -r) : r; };
-    for (int j = w; j < nch; j += kFcWaves) {
-      const int E = (sSE[j] & 0xffff) - 128, mode = sSE[j] >> 16, k = sSK[j];
-      if (mode == kChunkSeq) {
-        float s = value_of(E, k);
-        for (int p = 0; p < m; ++p) {
-          const int x = j * chunk + p * 64 + lane;
-          const float t = fabsf(term(0, x));
-          float mine = 0.0f;
-#pragma unroll
-          for (int q = 0; q < 64; ++q) {
-            s = s + lane_value(t, q);
-            if (lane == q) mine = s;
-          }
-          if (x < n) a.cdf[x] = out_of(mine);
-        }
-      } else {
-        // lane owns m consecutive cells; the chunk's table applied, so no
-        // term ties and the state stays in domain E: exact integer prefix
-        const int x0 = j * chunk + lane * m;
-        int own = 0;
-        for (int q = 0; q < m; ++q) {
-          bool tx;
-          own += (int)units_of(fabsf(term(0, x0 + q)), E, &tx);
-        }
-        const int excl = wave_incl_scan(own, lane) - own;
-        int kx = k + excl;
-        for (int q = 0; q < m; ++q) {
-          const int x = x0 + q;
-          bool tx;
-          kx += (int)units_of(fabsf(term(0, x)), E, &tx);
-          if (x < n) a.cdf[x] = out_of(value_of(E, kx));
-        }
-      }
-    }
-  }
+  for (int i = threadIdx.x; i < 144; i += blockDim.x) s.counts[i] = cnt[i];
 }
 
 // dst_r[x] = fl(pred_a[x] * L_z[x]) / sums[c_r], c_r = z * 9 + a.
@@ -327,27 +540,44 @@ __global__ __launch_bounds__(256) void k_store_children(FcStoreList L, const flo
   if (x >= n) return;
   const int c = L.child[r];
   const float v = ftz(pred[(long long)(c % 9) * ld + x] * ftz(lrows[(long long)(c / 9) * ld + x]));
-  L.dst[r][x] = v / sums[c];
+  L.dst[r][x] = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
+}
+
+template <int BASE, int K>
+hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a) {
+  constexpr int KC = K > 0 ? K : 1;
+  const int nseg = fc_segments(a.n);
+  hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, groups), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, groups), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(groups * KC), dim3(64), 0, st, a);
+  if (BASE == FC_ROW && K == 0 && a.cdf)
+    hipLaunchKernelGGL(k_fc_cdf, dim3((fc_chunks(a.n) + 3) / 4), dim3(256), 0, st, a);
+  return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a) {
   if (groups <= 0) return hipSuccess;
-  if (a.n < 0 || a.n > kFcMaxCells || (K != 0 && K != 9) || !a.out)
+  if (a.n <= 0 || a.n > kFcMaxCells || (K != 0 && K != 9) || !a.out || !a.csum || !a.cflag ||
+      !a.tab || groups * (K > 0 ? K : 1) > a.max_chains || fc_chunks(a.n) > a.max_chunks)
     return hipErrorInvalidValue;
-  if (base != FC_ROW && (!a.pred || !a.lrows || a.g0 < 0 || a.g0 + groups > 144))
-    return hipErrorInvalidValue;
-  if (base == FC_CHILD_NORM && !a.sums) return hipErrorInvalidValue;
+  if (a.ld < a.n || a.ld % 4 != 0) return hipErrorInvalidValue;
+  if (base == FC_CHILD && (!a.pred || !a.lrows || K != 0)) return hipErrorInvalidValue;
+  if (base == FC_ROW && !a.row) return hipErrorInvalidValue;
   if (K != 0 && !a.partners) return hipErrorInvalidValue;
-  if (a.cdf && (base != FC_ROW || K != 0)) return hipErrorInvalidValue;
-  const dim3 grid(groups), block(kFcThreads);
-  if (base == FC_ROW && K == 0) hipLaunchKernelGGL((k_fchain<FC_ROW, 0>), grid, block, 0, st, a);
-  else if (base == FC_ROW) hipLaunchKernelGGL((k_fchain<FC_ROW, 9>), grid, block, 0, st, a);
-  else if (base == FC_CHILD && K == 0) hipLaunchKernelGGL((k_fchain<FC_CHILD, 0>), grid, block, 0, st, a);
-  else if (base == FC_CHILD_NORM && K == 9)
-    hipLaunchKernelGGL((k_fchain<FC_CHILD_NORM, 9>), grid, block, 0, st, a);
-  else return hipErrorInvalidValue;
+  if (a.cdf && (base != FC_ROW || K != 0 || groups != 1 || !a.cst)) return hipErrorInvalidValue;
+  if (base == FC_ROW && K == 0) return launch_set<FC_ROW, 0>(st, groups, a);
+  if (base == FC_ROW && K == 9) return launch_set<FC_ROW, 9>(st, groups, a);
+  if (base == FC_CHILD) return launch_set<FC_CHILD, 0>(st, groups, a);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_tree_sample(hipStream_t st, const SampleArgs& s) {
+  if (s.N <= 0 || s.n <= 0 || !s.cdf || !s.r || !s.u1 || !s.u2 || !s.counts || !s.klist ||
+      !s.kcount)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_tree_sample, dim3(1), dim3(1024), 0, st, s);
   return hipGetLastError();
 }
 
@@ -360,6 +590,42 @@ hipError_t launch_store_children(hipStream_t st, const FcStoreList& L, const flo
   return hipGetLastError();
 }
 
+void FcScratch::release() {
+  for (void* p : {(void*)csum, (void*)cflag, (void*)tab, (void*)cst})
+    if (p) (void)hipFree(p);
+  csum = nullptr;
+  cflag = nullptr;
+  tab = nullptr;
+  cst = nullptr;
+  chains = 0;
+  chunks = 0;
+}
+
+bool FcScratch::reserve(int n, int max_chains) {
+  release();
+  const size_t nch = (size_t)fc_chunks(n), nseg = (size_t)fc_segments(n);
+  const size_t mc = (size_t)(max_chains > 0 ? max_chains : 1);
+  if (hipMalloc(&csum, mc * nch * sizeof(float)) != hipSuccess ||
+      hipMalloc(&cflag, mc * nseg * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&tab, mc * nch * sizeof(uint2)) != hipSuccess ||
+      hipMalloc(&cst, (nch + 1) * sizeof(int2)) != hipSuccess) {
+    release();
+    return false;
+  }
+  chains = max_chains;
+  chunks = (int)nch;
+  return true;
+}
+
+void FcScratch::attach(FcArgs* a) const {
+  a->csum = csum;
+  a->cflag = cflag;
+  a->tab = tab;
+  a->cst = cst;
+  a->max_chains = chains;
+  a->max_chunks = chunks;
+}
+
 }  // namespace pp2
 
 // Diagnostic entry point for tests/test_gpu_fchain.py (not part of pp2.h):
@@ -370,13 +636,19 @@ extern "C" int pp2_debug_fchain_row(int n, const float* x, const float* partners
                                     float* out, float* cdf) {
   if (n < 0 || !x || !out || (K != 0 && K != 9) || (K == 9 && !partners) || (cdf && K != 0))
     return 1;
-  const size_t ld = ((size_t)n + 63) / 64 * 64 + 64;
+  if (n == 0) {
+    for (int i = 0; i < (K ? 9 : 1); ++i) out[i] = 0.0f;
+    return 0;
+  }
+  const size_t ld = ((size_t)n + 63) / 64 * 64;
   float *dx = nullptr, *dp = nullptr, *dout = nullptr, *dcdf = nullptr;
+  pp2::FcScratch scr;
   int st = 0;
   auto ok = [&](hipError_t e) {
     if (e != hipSuccess && st == 0) st = 2;
     return st == 0;
   };
+  if (!scr.reserve(n, 9)) return 3;
   if (ok(hipMalloc(&dx, ld * sizeof(float))) && ok(hipMalloc(&dout, 16 * sizeof(float))) &&
       ok(hipMemset(dx, 0, ld * sizeof(float))) &&
       ok(hipMemcpy(dx, x, (size_t)n * sizeof(float), hipMemcpyHostToDevice)) &&
@@ -393,6 +665,7 @@ extern "C" int pp2_debug_fchain_row(int n, const float* x, const float* partners
     a.out = dout;
     a.ldo = K == 9 ? 9 : 1;
     a.cdf = dcdf;
+    scr.attach(&a);
     if (ok(pp2::launch_fchain(nullptr, pp2::FC_ROW, K, 1, a)) && ok(hipDeviceSynchronize()) &&
         ok(hipMemcpy(out, dout, (K == 9 ? 9 : 1) * sizeof(float), hipMemcpyDeviceToHost)) && cdf)
       ok(hipMemcpy(cdf, dcdf, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));

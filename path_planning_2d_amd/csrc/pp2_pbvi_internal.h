@@ -91,36 +91,71 @@ hipError_t launch_sum_splits(hipStream_t st, const float* C, int splits, long lo
 
 // ---- pp2_fchain.hip (IEEE): the reference-order planner's grid-wide fp32
 // sums, each equal to the reference's x-ordered chain, computed in parallel
-// (pp2_fchain.h).  Group g (blockIdx) has K chains (K = 0: one chain of the
-// base terms; else term i = base * partners[i][x], multiply then add):
-//   FC_ROW:        base = row[g * row_stride + x]
-//   FC_CHILD:      base = fl_ftz(pred[c % 9][x] * L[c / 9][x]), c = g0 + g
-//                  (the unnormalised child of action c % 9, observation c / 9)
-//   FC_CHILD_NORM: the same divided by sums[c] (IEEE)
-// out[c * ldo + i] = the chain's sum (c = g0 + g); with cdf (FC_ROW, K = 0, one
-// group) also every running sum, cdf[x] (std::partial_sum order).
-enum FcBase { FC_ROW = 0, FC_CHILD = 1, FC_CHILD_NORM = 2 };
-constexpr int kFcMaxChunks = 1024;     // chunks per chain (LDS tables)
+// (pp2_fchain.h).  Group g < groups (or < *gcount) has id = glist[g] (or g0 +
+// g) and K chains (K = 0: one chain of the base terms; K = 9: term i = base *
+// partners[i][x], multiply then add):
+//   FC_ROW:   base = row[id * row_stride + x]
+//   FC_CHILD: base = fl_ftz(pred[id % 9][x] * L[id / 9][x]) -- the unnormalised
+//             child of action id % 9 and observation id / 9
+// out[id * ldo + i] = the chain's sum; with cdf (FC_ROW, K = 0, one group)
+// also every running sum, cdf[x] (std::partial_sum).  Scratch: FcScratch.
+enum FcBase { FC_ROW = 0, FC_CHILD = 1 };
 constexpr int kFcMaxCells = 1 << 28;
-// cells per lane per chunk: chunks of 64 * m cells, at most kFcMaxChunks
-inline __host__ __device__ int fc_lane_elems(int n) {
-  const long long m = ((long long)n + 64LL * kFcMaxChunks - 1) / (64LL * kFcMaxChunks);
-  return m < 4 ? 4 : (int)m;
-}
+inline __host__ __device__ int fc_chunks(int n) { return (n + 255) / 256; }
+inline __host__ __device__ int fc_segments(int n) { return (fc_chunks(n) + 15) / 16; }
 struct FcArgs {
   int n = 0, ld = 0;
   const float* row = nullptr;
   long long row_stride = 0;
   const float* pred = nullptr;   // [9][ld]
   const float* lrows = nullptr;  // [16][ld]
-  const float* sums = nullptr;   // [144]
-  int g0 = 0;
   const float* partners = nullptr;  // [K][ld]
+  int g0 = 0;
+  const int* glist = nullptr;    // device: group -> id
+  const int* gcount = nullptr;   // device: active groups
   float* out = nullptr;
   int ldo = 1;
   float* cdf = nullptr;
+  // scratch (FcScratch::attach)
+  float* csum = nullptr;         // [chains][chunks] approximate chunk sums
+  uint32_t* cflag = nullptr;     // [chains][segments] sign flags
+  uint2* tab = nullptr;          // [chains][chunks] chunk entries
+  int2* cst = nullptr;           // [chunks + 1] chunk start states (cdf)
+  int max_chains = 0, max_chunks = 0;
+};
+// Device scratch of one stream's chain sets (a set may not overlap another
+// set using the same scratch).
+struct FcScratch {
+  float* csum = nullptr;
+  uint32_t* cflag = nullptr;
+  uint2* tab = nullptr;
+  int2* cst = nullptr;
+  int chains = 0, chunks = 0;
+  FcScratch() = default;
+  FcScratch(const FcScratch&) = delete;
+  FcScratch& operator=(const FcScratch&) = delete;
+  ~FcScratch() { release(); }
+  bool reserve(int n, int max_chains);
+  void release();
+  void attach(FcArgs* a) const;
 };
 hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a);
+// forwardSampling of the 9 actions from the expanded belief's running sums
+// cdf[n]: r[9 * N] the host's rand() values (action-major), u1 / u2 [N] the
+// curand uniforms; counts[a * 16 + z] and the kept children z * 9 + a.
+struct SampleArgs {
+  Geom g;
+  PlaneSet T, L;
+  const float* cdf = nullptr;
+  int n = 0, N = 0;
+  const float* r = nullptr;
+  const float* u1 = nullptr;
+  const float* u2 = nullptr;
+  int* counts = nullptr;  // [144]
+  int* klist = nullptr;   // [144]
+  int* kcount = nullptr;
+};
+hipError_t launch_tree_sample(hipStream_t st, const SampleArgs& s);
 // dst[r][x] = fl_ftz(pred[c % 9][x] * L[c / 9][x]) / sums[c], c = child[r], x < n.
 struct FcStoreList {
   int n = 0;

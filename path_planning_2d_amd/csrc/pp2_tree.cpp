@@ -183,8 +183,15 @@ struct pp2_planner {
   float* d_lrows = nullptr;     // [16][ld] L[.][z]
   float* d_pred = nullptr;      // [9][ld] the expanded belief's predictions
   float* d_csum = nullptr;      // [144] the children's masses (accumulate)
-  float* h_cdf = nullptr;       // pinned: the expanded belief's running sums
-  float* d_cdf = nullptr;
+  float* d_cdf = nullptr;       // the expanded belief's running sums
+  float* h_r = nullptr;         // pinned: the expansion's rand() values [9][N]
+  float* d_r = nullptr;
+  float *d_u1 = nullptr, *d_u2 = nullptr;  // the curand uniforms [N]
+  int* h_counts = nullptr;      // pinned: observation counts [9][16]
+  int* d_counts = nullptr;
+  int* d_klist = nullptr;       // the kept children z * 9 + a, and their number
+  int* d_kcount = nullptr;
+  pp2::FcScratch scr_main, scr_side;  // chain-set scratch of the two streams
   unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
   hipStream_t side = nullptr;   // reward chains beside the child chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -404,6 +411,7 @@ int ref_row_bounds(pp2_planner* p, const float* row) {
   a.partners = p->d_frows;
   a.out = p->d_rout + 9;
   a.ldo = 9;
+  p->scr_main.attach(&a);
   HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 1, a));
   if (p->pbvi) CHECK(ref_pbvi_bounds(p, row, 1));
   return PP2_OK;
@@ -603,79 +611,103 @@ int expand_vnode(pp2_planner* p, VNode* v) {
 
 // VNode::expand in reference order.  Every grid-wide sum of the reference's
 // 9 QNode constructors (search_tree_cuda.cu:161-242) is formed on the device
-// with the bits of its x-ordered fp32 host chain (pp2_fchain.hip):
-//   the sampling cdf of the expanded belief (:176-183),
-//   the 9 rewards inner_product(b, R[.][a]) (:168-173),
-//   the 144 children's accumulate (:225-227) -- child (a, z) =
-//   cudaBayesBeliefUpdate(b, a, z), the 9 action predictions formed once --
-//   and their evaluateFibCpu dots after the division (:228-229, :378).
-// The host draws the samples from the cdf while the device forms the rest;
-// only the children the samples keep are stored (normalised rows), so a
-// later expansion or re-rooting finds them ready.
+// with the bits of its x-ordered fp32 host chain (pp2_fchain.hip), and the
+// samples are drawn there with the host's rand() values:
+//   main stream: the expanded belief's running sums (:176-183), the 9 x N
+//     samples (forwardSampling, :311-366) and the kept children; then, once
+//     the children exist, evaluateFibCpu of the kept ones (:378);
+//   side stream: the 9 action predictions, the 144 children's accumulate
+//     (:225-227; child (a, z) = cudaBayesBeliefUpdate(b, a, z)), all of them
+//     normalised into d_children (:228-229), and the 9 rewards
+//     inner_product(b, R[.][a]) (:168-173).
+// One host wait per expansion.  The kept children's rows are stored into
+// their nodes' slots afterwards, queued ahead of anything that reads them.
 int expand_vnode_ref(pp2_planner* p, VNode* v) {
   pp2_ctx* c = p->ctx;
   if (v->slot < 0) return set_err(PP2_ESTATE, "reference-order VNode without a belief row");
   const float* brow = p->slots[v->slot].row;
   const size_t n = p->n;
   const int ld = p->ref_ld;
+  const uint32_t N = p->prm.sample_num;
   CHECK(ref_frows(p));
-  {
-    pp2::FcArgs a;  // the running sums, for the host's samples
+  // the rand() values of the 9 QNode constructors, in the reference's order
+  for (uint32_t a = 0; a < 9; ++a)
+    for (uint32_t j = 0; j < N; ++j)
+      p->h_r[a * N + j] = (float)p->rng.next() / ((float)RAND_MAX + 1.0f);
+  HIPCHK(hipEventRecord(p->ev_fork, c->stream));  // brow and the previous stores are in place
+  HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
+  {  // main: running sums, samples
+    pp2::FcArgs a;
     a.n = (int)n;
     a.ld = ld;
     a.row = brow;
     a.out = p->d_rsum;
     a.cdf = p->d_cdf;
+    p->scr_main.attach(&a);
     HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, a));
+    pp2::SampleArgs sa;
+    sa.g = c->g;
+    sa.T = c->T.v;
+    sa.L = c->L.v;
+    sa.cdf = p->d_cdf;
+    sa.n = (int)n;
+    sa.N = (int)N;
+    sa.r = p->d_r;
+    sa.u1 = p->d_u1;
+    sa.u2 = p->d_u2;
+    sa.counts = p->d_counts;
+    sa.klist = p->d_klist;
+    sa.kcount = p->d_kcount;
+    HIPCHK(pp2::launch_tree_sample(c->stream, sa));
   }
-  HIPCHK(hipEventRecord(p->ev_belief, c->stream));
-  HIPCHK(pp2::launch_tree_pred(c->stream, c->g, c->T.v, brow, ld, p->d_pred));
-  // the 9 reward chains need only the parent: on the side stream
-  HIPCHK(hipEventRecord(p->ev_fork, c->stream));
-  HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
-  {
+  {  // side: predictions, the children's masses and rows, rewards
+    HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred));
     pp2::FcArgs a;
-    a.n = (int)n;
-    a.ld = ld;
-    a.row = brow;
-    a.partners = p->d_rrows;
-    a.out = p->d_rout;
-    a.ldo = 9;
-    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, a));
-  }
-  HIPCHK(hipEventRecord(p->ev_join, p->side));
-  {
-    pp2::FcArgs a;  // the children's masses, then their FIB dots
     a.n = (int)n;
     a.ld = ld;
     a.pred = p->d_pred;
     a.lrows = p->d_lrows;
     a.out = p->d_csum;
     a.ldo = 1;
-    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_CHILD, 0, 144, a));
-    a.sums = p->d_csum;
+    p->scr_side.attach(&a);
+    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, a));
+    pp2::FcStoreList L;
+    L.n = 144;
+    for (int k = 0; k < 144; ++k) {
+      L.child[k] = k;
+      L.dst[k] = p->d_children + (size_t)k * ld;
+    }
+    HIPCHK(pp2::launch_store_children(p->side, L, p->d_pred, p->d_lrows, p->d_csum, (int)n, ld));
+    HIPCHK(hipEventRecord(p->ev_join, p->side));  // (children ready)
+    pp2::FcArgs r;
+    r.n = (int)n;
+    r.ld = ld;
+    r.row = brow;
+    r.partners = p->d_rrows;
+    r.out = p->d_rout;
+    r.ldo = 9;
+    p->scr_side.attach(&r);
+    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
+  }
+  HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
+  {  // main: the kept children's FIB dots (evaluateFibCpu)
+    pp2::FcArgs a;
+    a.n = (int)n;
+    a.ld = ld;
+    a.row = p->d_children;
+    a.row_stride = ld;
+    a.glist = p->d_klist;
+    a.gcount = p->d_kcount;
     a.partners = p->d_frows;
     a.out = p->d_rout + 9;
     a.ldo = 9;
-    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_CHILD_NORM, 9, 144, a));
+    p->scr_main.attach(&a);
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 144, a));
   }
-  if (p->pbvi) {  // all 144 children materialised for the PBVI dots
-    int cs[144];
-    float* dst[144];
-    for (int k = 0; k < 144; ++k) {
-      cs[k] = k;
-      dst[k] = p->d_children + (size_t)k * ld;
-    }
-    CHECK(ref_store_children(p, cs, dst, 144));
-    CHECK(ref_pbvi_bounds(p, p->d_children, 144));
-  }
+  if (p->pbvi) CHECK(ref_pbvi_bounds(p, p->d_children, 144));
+  HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards)
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
-  HIPCHK(hipEventSynchronize(p->ev_belief));
-
-  std::vector<uint8_t> zs[9];
-  std::vector<float> fq[9];
-  for (uint8_t a = 0; a < 9; ++a) sample_observations(p, p->h_cdf, n, a, zs[a], fq[a]);
   HIPCHK(hipEventSynchronize(p->ev_done));
 
   for (QNode* q : v->children)
@@ -689,10 +721,11 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     q->action = a;
     q->parent = v;
     q->reward = p->h_rout[a];
-    for (size_t k = 0; k < zs[a].size(); ++k) {
-      const uint8_t z = zs[a][k];
+    for (uint8_t z = 0; z < 16; ++z) {  // std::set order
+      const int cnt = p->h_counts[a * 16 + z];
+      if (!cnt) continue;
       const int row = z * 9 + a;
-      VNode* cv = new_vnode(p, z, fq[a][k], q);
+      VNode* cv = new_vnode(p, z, (float)cnt / (float)N, q);
       cv->upper_bound = first_max9(p->h_rout + 9 + 9 * row);
       cv->lower_bound = p->pbvi ? p->h_lbv[row] : p->lb_const;
       cv->heuristic = cv->upper_bound - cv->lower_bound;
@@ -704,8 +737,6 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     qnode_update(p, q);
     v->children[a] = q;
   }
-  // the kept children's rows (queued behind this expansion's kernels, ahead
-  // of anything that reads them)
   CHECK(ref_store_children(p, keep.data(), rows.data(), (int)keep.size()));
   vnode_update(v);
   ++p->expansions;
@@ -774,6 +805,7 @@ int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
     fa.g0 = cz;
     fa.out = p->d_csum;
     fa.ldo = 1;
+    p->scr_main.attach(&fa);
     HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_CHILD, 0, 1, fa));
     float* dst = ns.row;
     CHECK(ref_store_children(p, &cz, &dst, 1));
@@ -930,7 +962,15 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         hipMalloc(&p->d_pred, (size_t)9 * row_ld * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_csum, 144 * sizeof(float)) != hipSuccess ||
         !host_mapped(kRefOutFloats, &p->h_rout, &p->d_rout) ||
-        !host_mapped(p->n, &p->h_cdf, &p->d_cdf))
+        hipMalloc(&p->d_cdf, (size_t)row_ld * sizeof(float)) != hipSuccess ||
+        !host_mapped(9 * (size_t)prm->sample_num, &p->h_r, &p->d_r) ||
+        hipMalloc(&p->d_u1, (size_t)prm->sample_num * sizeof(float)) != hipSuccess ||
+        hipMalloc(&p->d_u2, (size_t)prm->sample_num * sizeof(float)) != hipSuccess ||
+        !host_mapped(144, reinterpret_cast<float**>(&p->h_counts),
+                     reinterpret_cast<float**>(&p->d_counts)) ||
+        hipMalloc(&p->d_klist, 144 * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->d_kcount, sizeof(int)) != hipSuccess ||
+        !p->scr_main.reserve((int)p->n, 144 * 9) || !p->scr_side.reserve((int)p->n, 144))
       return fail(set_err(PP2_ENOMEM, "planner reference-order scratch allocation failed"));
     std::vector<int> srow(144, 0);
     std::vector<uint8_t> us(144), zs(144);
@@ -952,6 +992,11 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
     if (hipMemsetAsync(p->d_lrows, 0, (size_t)16 * row_ld * sizeof(float), c->stream) !=
             hipSuccess ||
         hipMemsetAsync(p->d_pred, 0, (size_t)9 * row_ld * sizeof(float), c->stream) != hipSuccess)
+      return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
+    if (hipMemcpyAsync(p->d_u1, p->u1.data(), p->u1.size() * sizeof(float),
+                       hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(p->d_u2, p->u2.data(), p->u2.size() * sizeof(float),
+                       hipMemcpyHostToDevice, c->stream) != hipSuccess)
       return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
     if ((s = pack_rows(p, c->R.v, 9, p->d_rrows))) return fail(s);
     if ((s = pack_rows(p, c->L.v, 16, p->d_lrows))) return fail(s);
@@ -985,7 +1030,11 @@ int pp2_planner_destroy(pp2_planner* p) {
                    p->d_pred, p->d_csum})
     if (d) (void)hipFree(d);
   if (p->h_rout) (void)hipHostFree(p->h_rout);
-  if (p->h_cdf) (void)hipHostFree(p->h_cdf);
+  if (p->h_r) (void)hipHostFree(p->h_r);
+  if (p->h_counts) (void)hipHostFree(p->h_counts);
+  for (void* d : {(void*)p->d_cdf, (void*)p->d_u1, (void*)p->d_u2, (void*)p->d_klist,
+                  (void*)p->d_kcount})
+    if (d) (void)hipFree(d);
   for (void* d : {(void*)p->d_lbidx, (void*)p->d_srow, (void*)p->d_us, (void*)p->d_zs})
     if (d) (void)hipFree(d);
   if (p->h_lbv) (void)hipHostFree(p->h_lbv);

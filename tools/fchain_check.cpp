@@ -25,6 +25,8 @@ static float seq_sum(const std::vector<float>& t) {
   return s;
 }
 
+static long g_exact_fail = 0;
+
 struct Stats {
   long chunks = 0, fallback = 0;
 };
@@ -88,9 +90,17 @@ static float fchain_sum(const std::vector<float>& t, int chunk, Stats* st) {
     st->chunks += f;
     j += f;
     if (j < nch && f < 64) {
+      // the failing chunk term by term, each increment applied exactly
+      // (add_exact: the device's per-element scan) -- and checked against
+      // the plain fp32 adds
       float s = value_of(E, k);
       const int x1 = std::min(n, (j + 1) * chunk);
-      for (int x = j * chunk; x < x1; ++x) s = s + fabsf(t[x]);
+      int E2 = E, k2 = k;
+      for (int x = j * chunk; x < x1; ++x) {
+        s = s + fabsf(t[x]);
+        add_exact(&E2, &k2, fabsf(t[x]));
+        if (bits_of(value_of(E2, k2)) != bits_of(s)) ++g_exact_fail;
+      }
       state_of(s, &E, &k);
       ++st->chunks;
       ++st->fallback;
@@ -104,8 +114,26 @@ static float fchain_sum(const std::vector<float>& t, int chunk, Stats* st) {
 
 static int fails = 0;
 
+// The running sums (cdf) of a non-negative chain, every one of them from
+// add_exact from the chain start, against the plain fp32 running sums.
+static void check_cdf(const std::vector<float>& t) {
+  for (float v : t)
+    if (!(v >= 0.0f) || !std::isfinite(v)) return;
+  float s = 0.0f;
+  int E = kEMin, k = 0;
+  for (float v : t) {
+    s = s + v;
+    add_exact(&E, &k, v);
+    if (bits_of(value_of(E, k)) != bits_of(s)) {
+      ++g_exact_fail;
+      return;
+    }
+  }
+}
+
 static void check(const char* what, const std::vector<float>& t, int chunk, Stats* st) {
   const float a = seq_sum(t), b = fchain_sum(t, chunk, st);
+  check_cdf(t);
   if (bits_of(a) != bits_of(b) && !(std::isnan(a) && std::isnan(b))) {
     if (fails < 20)
       printf("MISMATCH %s n=%zu chunk=%d: seq %.9g (0x%08x) fchain %.9g (0x%08x)\n", what,
@@ -176,7 +204,8 @@ int main(int argc, char** argv) {
     check("belief", b, 256, &st);
     check("belief dot", d, 256, &st);
   }
-  printf("fchain_check: %d mismatches; %ld chunks, %ld term-by-term (%.2f %%)\n", fails,
-         st.chunks, st.fallback, st.chunks ? 100.0 * st.fallback / st.chunks : 0.0);
-  return fails ? 1 : 0;
+  printf("fchain_check: %d mismatches; %ld chunks, %ld term-by-term (%.2f %%); "
+         "%ld add_exact mismatches\n", fails, st.chunks, st.fallback,
+         st.chunks ? 100.0 * st.fallback / st.chunks : 0.0, g_exact_fail);
+  return fails || g_exact_fail ? 1 : 0;
 }
