@@ -144,6 +144,36 @@ def pmc_traffic(kernel_substr: str, cells: int, exclude: str | None = None,
     return None, None
 
 
+def pmc_kernel(kernel_name: str):
+    """The newest committed PMC summary entry of a kernel (by short name)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        v = d.get("kernels", {}).get(kernel_name)
+        if v and v.get("hbm_bytes_per_launch"):
+            return v, os.path.basename(f)
+    return None, None
+
+
+def sweep_resident_traffic(cells):
+    """k_sweep_resident's PMC memory-side bytes per solve launch against the
+    bytes it must move (code 2 + J 4 + J' 4 + A 1 per cell, + the convergence
+    snapshot 4 + 4), from the newest committed PMC summary."""
+    v, src = pmc_kernel("k_sweep_resident")
+    if not v:
+        return None
+    algo = (11 + 8) * cells
+    return {"traffic_per_launch": v["hbm_bytes_per_launch"], "avg_launch_us": v.get("avg_us"),
+            "algorithmic_bytes_per_launch": algo,
+            "traffic_over_algorithmic": v["hbm_bytes_per_launch"] / algo, "source": src,
+            "cause": "every edge-row hand-off granule is an sc1 store / load (round 3), which "
+                     "bypasses L2 to the memory side: each sweep of the solve moves 2 x 8 KB "
+                     "of granules per tile through the fabric/MALL (DESIGN.md §5)"}
+
+
 def cpu_threads():
     """Host threads for the CPU baseline: every core of this process's
     affinity mask (os.sched_getaffinity), i.e. all host cores the run may
@@ -602,10 +632,11 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
     a rank of the 8-GPU job does (views of 256 + 2e rows, one launch per e
     steps, the {mass, shift} all-reduce, halo exchanges and rebases) -- with
     every RCCL call a 1-rank no-op.  The 8-GPU time is then projected as this
-    measured step plus the RCCL rounds the real job adds per call (the first
-    block's halo exchange, the {mass, shift} all-reduce + exchange of every
-    later block, the closing all-reduce: 2 per block; the ranks' agreement on
-    e is made once per model / tuning / reset, not per call) at an ASSUMED
+    measured step plus the RCCL rounds the real job adds per call (one per
+    block: the first block's halo exchange, every later block's {mass, shift,
+    lost} records and halo rows in ONE RCCL group; plus the closing
+    all-reduce; the ranks' agreement on e is made once per model / tuning /
+    reset, not per call) at an ASSUMED
     xGMI round trip
     (RCCL_ROUND_US; multi-GPU RCCL cannot run on one GPU)."""
     import torch
@@ -628,7 +659,7 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
     ctx.close()
     t = 1e6 * el / k
     nblk = -(-k // e)
-    rounds = 2 * nblk
+    rounds = nblk + 1
     lo, hi = (t + rounds * r / k for r in RCCL_ROUND_US)
     return {"shard": f"rows [{r0}, {r1}) x {G} of the {G}^2 grid (rank 3 of 8), 1-rank RCCL "
                      f"communicator",
@@ -677,7 +708,7 @@ def weak_rank_share(args, local, stream, n1_cells_per_s):
     launches = ctx.resident_launches()[0] - l0
     ctx.close()
     t = 1e6 * el / k
-    rounds = 2 * (-(-k // e))
+    rounds = -(-k // e) + 1
     proj = [t + rounds * r / k for r in RCCL_ROUND_US]
     return {"shard": f"rows [{R}, {2 * R}) x {W} of a {2 * R}x{W} grid (rank 1 of 2), 1-rank "
                      f"RCCL communicator",
@@ -1030,6 +1061,7 @@ def main():
                 "frac": loop_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_over_algorithmic": (traffic / algo_launch if traffic else None),
                 "steps_per_launch": spl,
                 "algorithmic_bytes_per_cell_per_launch": bytes_loop,
                 "algorithmic_bytes_per_launch": algo_launch,
@@ -1064,6 +1096,7 @@ def main():
                 "frac": lds_bytes * cells_per_gpu / (loop_ms_events * 1e-3) / 1e9
                 / LDS_PEAK_GBS,
                 "bytes_per_cell": lds_bytes} if coded else None),
+            "sweep_resident_traffic": sweep_resident_traffic(cells_per_gpu),
             "dense_path": dense,
             "config4": c4,
             "weak_rank_share": weak,

@@ -185,7 +185,7 @@ struct pp2_ctx {
   int res_view_e = -1;             // view extension the plan below was made for
   int res_e = 0, res_e_dict = -1;  // shard_resident_e's answer and the dictionary it is for
   int* d_shift = nullptr;          // int: the last shard-resident run's shift
-  float* d_vec = nullptr;          // 2 x nranks floats
+  float* d_vec = nullptr;          // kVecRec x nranks floats: {mass, shift, lost} per rank
   bool shift_pending = false;      // the pending mass comes with *d_shift (rebase owed)
   // a shard-resident run timed out: belief / values unusable until set again
   bool lost_belief = false, lost_values = false;

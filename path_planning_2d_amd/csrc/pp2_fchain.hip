@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 
+#include <utility>
+
 #define PP2_FC_HD __host__ __device__
 #include "pp2_fchain.h"
 #include "pp2_pbvi_internal.h"
@@ -39,23 +41,45 @@ using namespace fchain;
 typedef float f4a __attribute__((ext_vector_type(4)));
 
 constexpr int kFcChunk = 256;     // cells per chunk: 4 per lane
-constexpr int kFcSegChunks = 16;  // chunks per k_fc_sums / k_fc_tables workgroup (4 per wave)
 constexpr int kFcWin = 1024;      // chunk entries per driver window (LDS)
 constexpr int kFcStash = 8;       // predicted fallback chunks prefetched per window
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+// Wave scans and sums on DPP row shifts (no LDS crossbar round trips): the
+// inclusive scan of each 16-lane row, then the rows' totals by readlane.
+__device__ __forceinline__ int row_shr(int v, int ctrl) {
+  switch (ctrl) {
+    case 1: return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    case 2: return __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    case 4: return __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    default: return __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  }
+}
+__device__ __forceinline__ int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rdl(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+  v += row_shr(v, 1);
+  v += row_shr(v, 2);
+  v += row_shr(v, 4);
+  v += row_shr(v, 8);
+  const int r0 = rdl(v, 15), r1 = rdl(v, 31), r2 = rdl(v, 47);
+  const int row = lane >> 4;
+  return v + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
+}
+
+// the wave's total (uniform): any association will do for these sums
+// (approximate running sums, or integer-valued floats below 2^24)
+__device__ __forceinline__ float wave_sum(float v) {
+  int b = __builtin_bit_cast(int, v);
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(v, o);
-    if (lane >= o) v += y;
+  for (int c = 1; c < 16; c <<= 1) {
+    const int o = row_shr(b, c);
+    b = __builtin_bit_cast(int, __builtin_bit_cast(float, b) + __builtin_bit_cast(float, o));
   }
-  return v;
+  const float f = __builtin_bit_cast(float, b);
+  return (rdl(f, 15) + rdl(f, 31)) + (rdl(f, 47) + rdl(f, 63));
 }
 
 // The device's flush of a product (FTZ build of the reference kernel).
@@ -101,7 +125,24 @@ struct Terms {
   __device__ __forceinline__ float term(float v, int i, int x) const {
     return K > 0 ? v * part[(long long)i * ld + x] : v;
   }
-  // the 4 terms of chain i at x0 .. x0+3 (x0 % 4 == 0; 0 past n)
+  // chain i's terms of the 4 cells x0 .. x0+3 from their base values v (0
+  // past n: v is)
+  __device__ __forceinline__ void terms_of(const float (&v)[4], int i, int x0,
+                                          float (&t)[4]) const {
+    if (K == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = v[q];
+    } else if (x0 + 4 <= n) {
+      const f4a w = *reinterpret_cast<const f4a*>(part + (long long)i * ld + x0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = v[q] * w[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = x0 + q < n ? v[q] * part[(long long)i * ld + x0 + q] : 0.0f;
+    }
+  }
+  // the 4 terms of chain i at x0 .. x0+3 (x0 % 4 == 0; 0 past n); i < 0:
+  // the base values
   __device__ __forceinline__ void terms4(int i, int x0, float (&t)[4]) const {
     if (x0 + 4 <= n) {
       const f4a p = *reinterpret_cast<const f4a*>(pr + x0);
@@ -111,7 +152,7 @@ struct Terms {
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = ftz(p[q] * ftz(l[q]));
       }
-      if (K > 0) {
+      if (K > 0 && i >= 0) {
         const f4a w = *reinterpret_cast<const f4a*>(part + (long long)i * ld + x0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = v[q] * w[q];
@@ -120,7 +161,8 @@ struct Terms {
       for (int q = 0; q < 4; ++q) t[q] = v[q];
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) t[q] = x0 + q < n ? term(base(x0 + q), i, x0 + q) : 0.0f;
+      for (int q = 0; q < 4; ++q)
+        t[q] = x0 + q < n ? (i >= 0 ? term(base(x0 + q), i, x0 + q) : base(x0 + q)) : 0.0f;
     }
   }
 };
@@ -142,28 +184,22 @@ __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
   uint32_t fl[KC];
 #pragma unroll
   for (int i = 0; i < KC; ++i) fl[i] = 0u;
-  for (int cc = 0; cc < kFcSegChunks / 4; ++cc) {
-    const int j = seg * kFcSegChunks + w * (kFcSegChunks / 4) + cc;
-    if (j >= nch) break;
-    float acc[KC];
-#pragma unroll
-    for (int i = 0; i < KC; ++i) acc[i] = 0.0f;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int x = j * kFcChunk + p * 64 + lane;
-      if (x < a.n) {
-        const float v = T.base(x);
-#pragma unroll
-        for (int i = 0; i < KC; ++i) {
-          const float t = T.term(v, i, x);
-          acc[i] += fabsf(t);
-          fl[i] |= !isfinite(t) ? kBad : t > 0.0f ? kPos : t < 0.0f ? kNeg : 0u;
-        }
-      }
-    }
+  const int j = seg * kFcSegChunks + w;
+  if (j < nch) {
+    const int x0 = j * kFcChunk + 4 * lane;
+    float v[4];
+    T.terms4(-1, x0, v);  // the base terms
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
-      const float sum = wave_sum(acc[i]);
+      float acc = 0.0f, tt[4];
+      T.terms_of(v, i, x0, tt);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float t = tt[q];
+        acc += fabsf(t);
+        fl[i] |= !isfinite(t) ? kBad : t > 0.0f ? kPos : t < 0.0f ? kNeg : 0u;
+      }
+      const float sum = wave_sum(acc);
       if (lane == 0) a.csum[(long long)(g * KC + i) * nch + j] = sum;
     }
   }
@@ -213,41 +249,32 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
     }
   }
   __syncthreads();
-  for (int cc = 0; cc < kFcSegChunks / 4; ++cc) {
-    const int jl = w * (kFcSegChunks / 4) + cc, j = j0 + jl;
-    if (j >= nch) break;
-    int E[KC];
-    float d[KC];
-    bool tie[KC];
+  {
+    const int jl = w, j = j0 + jl;
+    if (j >= nch) return;
+    const int x0 = j * kFcChunk + 4 * lane;
+    float v[4];
+    T.terms4(-1, x0, v);
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
-      E[i] = domain_of(sP[i][jl]);
-      d[i] = 0.0f;
-      tie[i] = false;
-    }
+      const int E = domain_of(sP[i][jl]);
+      float d = 0.0f, tt[4];
+      bool tie = false;
+      T.terms_of(v, i, x0, tt);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int x = j * kFcChunk + p * 64 + lane;
-      if (x < a.n) {
-        const float v = T.base(x);
-#pragma unroll
-        for (int i = 0; i < KC; ++i) {
-          bool tx;
-          d[i] += units_of(fabsf(T.term(v, i, x)), E[i], &tx);
-          tie[i] = tie[i] || tx;
-        }
+      for (int q = 0; q < 4; ++q) {
+        bool tx;
+        d += units_of(fabsf(tt[q]), E, &tx);
+        tie = tie || tx;
       }
-    }
-#pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      const float ds = wave_sum(d[i]);  // exact below 2^24; else no entry
-      const bool anytie = __ballot(tie[i]) != 0ull;
+      const float ds = wave_sum(d);  // exact below 2^24; else no entry
+      const bool anytie = __ballot(tie) != 0ull;
       if (lane == 0) {
-        const uint32_t e = make_entry(E[i], ds, anytie);
+        const uint32_t e = make_entry(E, ds, anytie);
         // predicted fallback: no entry, or the chunk's sum likely crosses
         // into the next binade (from the approximate running sum)
         const bool pred = e == kNoEntry ||
-                          ldexpf(sP[i][jl], 23 - E[i]) + ds >= (float)kK24 * (1.0f - 0x1p-12f);
+                          ldexpf(sP[i][jl], 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f);
         a.tab[(long long)(g * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
       }
     }
@@ -261,9 +288,10 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
 // 2^(E+1)), adds that one in fp32, and goes on after it (add_exact, in
 // parallel).  With cv, every running value (cv[q] of term 4l + q).
 __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* pE, int* pk,
-                                            float (*cv)[4]) {
+                                            float (*cv)[4], int* rounds = nullptr) {
   int E = *pE, k = *pk, done = 0;
   for (;;) {
+    if (rounds) ++*rounds;
     int r[4];
     bool tie[4];
     int tot = 0;
@@ -293,13 +321,13 @@ __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* 
     }
     const uint64_t bm = __ballot(bad < 4);
     if (bm == 0ull) {
-      k += __shfl(incl, 63);
+      k += rdl(incl, 63);
       break;
     }
     const int lb = __builtin_ctzll(bm);
-    const int qb = __shfl(bad, lb), kbef = __shfl(kb, lb);
+    const int qb = rdl(bad, lb), kbef = rdl(kb, lb);
     const float tq = qb == 0 ? t[0] : qb == 1 ? t[1] : qb == 2 ? t[2] : t[3];
-    const float tb = __shfl(tq, lb);
+    const float tb = rdl(tq, lb);
     const float s = value_of(E, kbef) + tb;  // the reference's own add
     state_of(s, &E, &k);
     if (cv && lane == lb) {
@@ -350,7 +378,7 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
       for (int l = 0; l < 64; ++l) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          s = s + __shfl(t[q], l);
+          s = s + rdl(t[q], l);
           if (lane == l) cv[q] = s;
         }
       }
@@ -364,7 +392,9 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
     res = s;
   } else {
     int E = kEMin, k = 0, j = 0, wbase = -kFcWin, nstash = 0;
+    int n_it = 0, n_fb = 0, n_rounds = 0, n_hit = 0;
     while (j < nch) {
+      ++n_it;
       if (j >= wbase + kFcWin) {  // the next window of entries, and its predicted fallbacks
         wbase = j;
         for (int c = lane; c < kFcWin; c += 64)
@@ -404,7 +434,7 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
       const int fc = badm == 0ull ? 64 : __builtin_ctzll(badm);
       if (cdf && lane < fc) a.cst[jj] = make_int2(E, k + incl - dl);
       if (fc > 0) {
-        k += __shfl(incl, fc - 1);
+        k += rdl(incl, fc - 1);
         normalise(&E, &k);
       }
       j += fc;
@@ -415,7 +445,9 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
         for (int s2 = 0; s2 < nstash; ++s2)
           if (sStashId[s2] == j) slot = s2;
         float t[4];
+        ++n_fb;
         if (slot >= 0) {
+          ++n_hit;
           const f4a v = *reinterpret_cast<const f4a*>(&sStash[slot][4 * lane]);
 #pragma unroll
           for (int q = 0; q < 4; ++q) t[q] = v[q];
@@ -424,10 +456,16 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) t[q] = fabsf(t[q]);
         }
-        chunk_exact(t, lane, &E, &k, nullptr);
+        chunk_exact(t, lane, &E, &k, nullptr, &n_rounds);
         normalise(&E, &k);
         ++j;
       }
+    }
+    if (a.stats && lane == 0) {
+      atomicAdd(a.stats + 0, n_it);
+      atomicAdd(a.stats + 1, n_fb);
+      atomicAdd(a.stats + 2, n_rounds);
+      atomicAdd(a.stats + 3, n_hit);
     }
     const float r = value_of(E, k);
     res = neg ? (r == 0.0f ? 0.0f : -r) : r;
@@ -632,8 +670,16 @@ void FcScratch::attach(FcArgs* a) const {
 // the FC_ROW chains of one host row x[n] on device 0 -- K = 0: out[0] =
 // accumulate(x) and, with cdf, every running sum; K = 9: out[i] =
 // inner_product(x, partners[i]) (partners: 9 rows of n).  Synchronous.
+extern "C" int pp2_debug_fchain_row2(int n, const float* x, const float* partners, int K,
+                                     float* out, float* cdf, int* stats, float* ms);
 extern "C" int pp2_debug_fchain_row(int n, const float* x, const float* partners, int K,
                                     float* out, float* cdf) {
+  return pp2_debug_fchain_row2(n, x, partners, K, out, cdf, nullptr, nullptr);
+}
+// (stats: the driver's {iterations, fallback chunks, exact rounds, stash
+// hits}; ms: the chain set's event time, median of 5 runs after a warm-up)
+extern "C" int pp2_debug_fchain_row2(int n, const float* x, const float* partners, int K,
+                                     float* out, float* cdf, int* stats, float* ms) {
   if (n < 0 || !x || !out || (K != 0 && K != 9) || (K == 9 && !partners) || (cdf && K != 0))
     return 1;
   if (n == 0) {
@@ -666,11 +712,76 @@ extern "C" int pp2_debug_fchain_row(int n, const float* x, const float* partners
     a.ldo = K == 9 ? 9 : 1;
     a.cdf = dcdf;
     scr.attach(&a);
+    int* dstats = nullptr;
+    if (stats && ok(hipMalloc(&dstats, 4 * sizeof(int))) &&
+        ok(hipMemset(dstats, 0, 4 * sizeof(int))))
+      a.stats = dstats;
+    if (ms && st == 0) {
+      hipEvent_t e0, e1;
+      float t[5];
+      if (ok(hipEventCreate(&e0)) && ok(hipEventCreate(&e1))) {
+        pp2::FcArgs w = a;
+        w.stats = nullptr;
+        ok(pp2::launch_fchain(nullptr, pp2::FC_ROW, K, 1, w));
+        for (int r = 0; r < 5 && st == 0; ++r) {
+          ok(hipEventRecord(e0, nullptr));
+          ok(pp2::launch_fchain(nullptr, pp2::FC_ROW, K, 1, w));
+          ok(hipEventRecord(e1, nullptr));
+          ok(hipEventSynchronize(e1));
+          ok(hipEventElapsedTime(&t[r], e0, e1));
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        for (int i = 1; i < 5; ++i)
+          for (int j = i; j > 0 && t[j] < t[j - 1]; --j) std::swap(t[j], t[j - 1]);
+        *ms = t[2];
+      }
+    }
     if (ok(pp2::launch_fchain(nullptr, pp2::FC_ROW, K, 1, a)) && ok(hipDeviceSynchronize()) &&
         ok(hipMemcpy(out, dout, (K == 9 ? 9 : 1) * sizeof(float), hipMemcpyDeviceToHost)) && cdf)
       ok(hipMemcpy(cdf, dcdf, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+    if (dstats) {
+      if (st == 0) ok(hipMemcpy(stats, dstats, 4 * sizeof(int), hipMemcpyDeviceToHost));
+      (void)hipFree(dstats);
+    }
   }
   for (float* p : {dx, dp, dout, dcdf})
+    if (p) (void)hipFree(p);
+  return st;
+}
+
+// Diagnostic (tests/tools only): one FC_ROW K = 0 chain set on a host row,
+// and its scratch: csum[nch] (k_fc_sums), tab[2 nch] (k_fc_tables: entry,
+// flags), cst[2 (nch + 1)] (k_fc_drive's chunk start states).
+extern "C" int pp2_debug_fchain_tables(int n, const float* x, float* csum, uint32_t* tab,
+                                       int* cst) {
+  if (n <= 0 || !x) return 1;
+  const size_t ld = ((size_t)n + 63) / 64 * 64, nch = (size_t)pp2::fc_chunks(n);
+  float *dx = nullptr, *dout = nullptr, *dcdf = nullptr;
+  pp2::FcScratch scr;
+  int st = 0;
+  auto ok = [&](hipError_t e) {
+    if (e != hipSuccess && st == 0) st = 2;
+    return st == 0;
+  };
+  if (!scr.reserve(n, 1)) return 3;
+  if (ok(hipMalloc(&dx, ld * sizeof(float))) && ok(hipMalloc(&dout, 16 * sizeof(float))) &&
+      ok(hipMalloc(&dcdf, ld * sizeof(float))) && ok(hipMemset(dx, 0, ld * sizeof(float))) &&
+      ok(hipMemcpy(dx, x, (size_t)n * sizeof(float), hipMemcpyHostToDevice))) {
+    pp2::FcArgs a;
+    a.n = n;
+    a.ld = (int)ld;
+    a.row = dx;
+    a.out = dout;
+    a.cdf = dcdf;
+    scr.attach(&a);
+    if (ok(pp2::launch_fchain(nullptr, pp2::FC_ROW, 0, 1, a)) && ok(hipDeviceSynchronize())) {
+      if (csum) ok(hipMemcpy(csum, scr.csum, nch * sizeof(float), hipMemcpyDeviceToHost));
+      if (tab) ok(hipMemcpy(tab, scr.tab, nch * sizeof(uint2), hipMemcpyDeviceToHost));
+      if (cst) ok(hipMemcpy(cst, scr.cst, (nch + 1) * sizeof(int2), hipMemcpyDeviceToHost));
+    }
+  }
+  for (float* p : {dx, dout, dcdf})
     if (p) (void)hipFree(p);
   return st;
 }

@@ -332,19 +332,21 @@ inline size_t resident_xch_floats(const Geom& g, int ntiles) {
 // tile columns whenever they fit (and whole rows do: else no plan changes).
 bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref = 0);
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a);
-// Row-shard boundary kernels (pp2_resident.hip).
-// vec[2 * nranks] := 0 except vec[2 * rank] = mass of the n partials (k_sum_finalize's
-// tree), vec[2 * rank + 1] = (float) *shift (0 if shift is null).  With err_word
-// (an RCCL shard's sticky resident error word), vec has one more slot,
-// vec[2 * nranks] := 1 if the word is set, else 0: summed by the all-reduce, it
-// tells every rank that some rank's resident run was lost.
+// Row-shard boundary kernels (pp2_resident.hip).  vec holds one
+// record of kVecRec floats per rank, {owned mass, shift, lost}: the mass of the
+// n partials (k_sum_finalize's tree), (float) *shift (0 if shift is null) and,
+// with err_word (an RCCL shard's sticky resident error word), 1 if the word is
+// set, else 0.  Every other rank's record := 0, so that an all-reduce (sum)
+// shares the records exactly -- or the records travel point to point
+// (exchange_halos_k with records, grouped with the halo rows).
+constexpr int kVecRec = 3;
 hipError_t launch_shard_mass_vec(hipStream_t st, const float* partials, int n, const int* shift,
                                  float* vec, int nranks, int rank, const unsigned* err_word);
 // After the all-reduce of vec: C = min over ranks of the shifts; rows [r0, r1)
 // of plane b (row stride wp) are scaled by 2^(C - shift_q), q = the rank the
 // row came from (rank - 1 above row 0, rank + 1 at rows >= own_rows), and
 // *mass_out = sum over q in rank order of ldexp(m_q, C - shift_q).
-// With err_host, a nonzero vec[2 * nranks] (some rank lost a run) sets *err_host.
+// With err_host, a nonzero `lost` in any record (some rank lost a run) sets *err_host.
 hipError_t launch_shard_rebase(hipStream_t st, const float* vec, int nranks, int rank,
                                float* b, int wp, int r0, int r1, int own_rows, float* mass_out,
                                unsigned* err_host);

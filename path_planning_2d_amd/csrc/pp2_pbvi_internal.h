@@ -101,8 +101,11 @@ hipError_t launch_sum_splits(hipStream_t st, const float* C, int splits, long lo
 // also every running sum, cdf[x] (std::partial_sum).  Scratch: FcScratch.
 enum FcBase { FC_ROW = 0, FC_CHILD = 1 };
 constexpr int kFcMaxCells = 1 << 28;
+constexpr int kFcSegChunks = 4;  // chunks per k_fc_sums / k_fc_tables workgroup (1 per wave)
 inline __host__ __device__ int fc_chunks(int n) { return (n + 255) / 256; }
-inline __host__ __device__ int fc_segments(int n) { return (fc_chunks(n) + 15) / 16; }
+inline __host__ __device__ int fc_segments(int n) {
+  return (fc_chunks(n) + kFcSegChunks - 1) / kFcSegChunks;
+}
 struct FcArgs {
   int n = 0, ld = 0;
   const float* row = nullptr;
@@ -122,6 +125,7 @@ struct FcArgs {
   uint2* tab = nullptr;          // [chains][chunks] chunk entries
   int2* cst = nullptr;           // [chunks + 1] chunk start states (cdf)
   int max_chains = 0, max_chunks = 0;
+  int* stats = nullptr;          // diagnostics: driver {iterations, fallbacks, exact rounds, stash hits}
 };
 // Device scratch of one stream's chain sets (a set may not overlap another
 // set using the same scratch).

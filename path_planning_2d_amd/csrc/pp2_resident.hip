@@ -1165,12 +1165,13 @@ __global__ void k_shard_mass_vec(const float* __restrict__ partials, int n,
                                  const int* __restrict__ shift, float* __restrict__ vec,
                                  int nranks, int rank, const unsigned* __restrict__ err_word) {
   const float S = wave_reduce_partials(partials, n);  // k_sum_finalize's tree
-  for (int i = threadIdx.x; i < 2 * nranks; i += 64)
-    if (i != 2 * rank && i != 2 * rank + 1) vec[i] = 0.0f;
+  for (int i = threadIdx.x; i < kVecRec * nranks; i += 64)
+    if (i / kVecRec != rank) vec[i] = 0.0f;
   if (threadIdx.x == 0) {
-    vec[2 * rank] = S;
-    vec[2 * rank + 1] = shift ? (float)*shift : 0.0f;
-    if (err_word) vec[2 * nranks] = ld_flag(err_word) != 0u ? 1.0f : 0.0f;
+    float* r = vec + kVecRec * rank;
+    r[0] = S;
+    r[1] = shift ? (float)*shift : 0.0f;
+    r[2] = err_word && ld_flag(err_word) != 0u ? 1.0f : 0.0f;
   }
 }
 
@@ -1178,12 +1179,17 @@ __global__ void k_shard_rebase(const float* __restrict__ vec, int nranks, int ra
                                float* __restrict__ b, int wp, int r0, int r1, int own_rows,
                                float* __restrict__ mass_out, unsigned* __restrict__ err_host) {
   int C = 0x7fffffff;
-  for (int q = 0; q < nranks; ++q) C = min(C, (int)vec[2 * q + 1]);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && err_host && vec[2 * nranks] != 0.0f)
+  bool lost = false;
+  for (int q = 0; q < nranks; ++q) {
+    C = min(C, (int)vec[kVecRec * q + 1]);
+    lost = lost || vec[kVecRec * q + 2] != 0.0f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && err_host && lost)
     __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (blockIdx.x == 0 && threadIdx.x == 0 && mass_out) {
     float M = 0.0f;
-    for (int q = 0; q < nranks; ++q) M += __builtin_ldexpf(vec[2 * q], C - (int)vec[2 * q + 1]);
+    for (int q = 0; q < nranks; ++q)
+      M += __builtin_ldexpf(vec[kVecRec * q], C - (int)vec[kVecRec * q + 1]);
     *mass_out = M;
   }
   const int tpr = wp >> 2;
@@ -1193,7 +1199,7 @@ __global__ void k_shard_rebase(const float* __restrict__ vec, int nranks, int ra
   const int row = r0 + (int)(i / tpr), x = (int)(i % tpr) * 4;
   int q = row < 0 ? rank - 1 : row >= own_rows ? rank + 1 : rank;
   if (q < 0 || q >= nranks) q = rank;  // off the grid: zeros either way
-  const int k = C - (int)vec[2 * q + 1];
+  const int k = C - (int)vec[kVecRec * q + 1];
   if (k == 0) return;
   float* p = b + (long long)row * wp + x;
   f4a v = *reinterpret_cast<const f4a*>(p);

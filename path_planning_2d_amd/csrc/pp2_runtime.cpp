@@ -126,9 +126,17 @@ int comm_leave(pp2_ctx* c) {
 
 // k halo rows up and down for each state kind, in one RCCL group
 // (multi-process shards): owned rows [0, k) and [rows-k, rows) go to the
-// neighbours' halo rows [rows, rows+k) and [-k, 0).  Shards of a
-// single-process group exchange through the pp2_shard_group_* drivers.
-int exchange_halos_k(pp2_ctx* c, std::initializer_list<HaloKind> kinds, int k) {
+// neighbours' halo rows [rows, rows+k) and [-k, 0).  With records, the same
+// group also sends this rank's {mass, shift, lost} record of d_vec to every
+// other rank and receives theirs (the shard all-reduce as point-to-point
+// messages, so that a resident block start costs ONE RCCL round: the halo
+// rows travel unrebased and the rebase after the group scales them by their
+// owner's shift).  Within a group the messages between two ranks match in
+// issue order, which is the same on both sides: the record first, then the
+// kinds' rows.  Shards of a single-process group exchange through the
+// pp2_shard_group_* drivers.
+int exchange_halos_k(pp2_ctx* c, std::initializer_list<HaloKind> kinds, int k,
+                     bool records = false) {
   if (c->group)
     return set_err(PP2_ESTATE, "context belongs to a shard group: drive it with pp2_shard_group_*");
   if (!c->comm) {
@@ -137,6 +145,14 @@ int exchange_halos_k(pp2_ctx* c, std::initializer_list<HaloKind> kinds, int k) {
   }
   CHECK(comm_enter(c));
   NCCLCHK(ncclGroupStart());
+  if (records) {
+    const int R = pp2::kVecRec;
+    for (int q = 0; q < c->nranks; ++q) {
+      if (q == c->rank) continue;
+      NCCLCHK(ncclSend(c->d_vec + R * c->rank, R, ncclFloat, q, c->comm, cst(c)));
+      NCCLCHK(ncclRecv(c->d_vec + R * q, R, ncclFloat, q, c->comm, cst(c)));
+    }
+  }
   for (HaloKind kd : kinds) {
     const Planes* P = &halo_planes(c, kd);
     float* p = P->v.p;
@@ -608,7 +624,7 @@ int pp2rt::ensure_mass(pp2_ctx* c) {
   if (c->shift_pending && c->comm) {  // a shard-resident run's mass: rebase as well
     CHECK(shard_post_mass(c, c->nranks, c->rank));
     CHECK(comm_enter(c));
-    NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, 2 * c->nranks + 1, ncclFloat, ncclSum, c->comm,
+    NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, pp2::kVecRec * c->nranks, ncclFloat, ncclSum, c->comm,
                           cst(c)));
     CHECK(comm_leave(c));
     return shard_rebase(c, c->nranks, c->rank, 0, c->g.rows);
@@ -1353,7 +1369,7 @@ bool pp2rt::shard_resident_ready(pp2_ctx* c, int e) {
   }
   if (!c->d_vec) {
     const int nr = c->group ? c->group_size : c->nranks;
-    if (hipMalloc(&c->d_vec, (size_t)(2 * nr + 1) * sizeof(float)) != hipSuccess) {
+    if (hipMalloc(&c->d_vec, (size_t)pp2::kVecRec * nr * sizeof(float)) != hipSuccess) {
       c->d_vec = nullptr;
       return false;
     }
@@ -1443,12 +1459,13 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
   return PP2_OK;
 }
 
-// The RCCL shard's resident run: blocks of m <= e steps, each after an
-// exchange of e halo rows (and, with a pending mass, the {mass, shift}
-// all-reduce and the rebase), then the closing all-reduce and rebase.
+// The RCCL shard's resident run: blocks of m <= e steps, each after ONE RCCL
+// round -- the exchange of e halo rows, grouped (with a pending mass) with the
+// point-to-point {mass, shift, lost} records, then the rebase -- and the
+// closing all-reduce of the records and rebase: n / e + 1 rounds per call.
 static int shard_allreduce_vec(pp2_ctx* c) {
   CHECK(comm_enter(c));
-  NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, 2 * c->nranks + 1, ncclFloat, ncclSum, c->comm,
+  NCCLCHK(ncclAllReduce(c->d_vec, c->d_vec, pp2::kVecRec * c->nranks, ncclFloat, ncclSum, c->comm,
                         cst(c)));
   return comm_leave(c);
 }
@@ -1463,9 +1480,9 @@ static int shard_loop_resident(pp2_ctx* c, int e, int n, const uint8_t* us, cons
   for (int i = 0; i < n;) {
     const int m = std::min(e, n - i);
     if (c->pending[c->bcur]) {
+      // one RCCL round: the records and the (unrebased) halo rows together
       CHECK(shard_post_mass(c, c->nranks, c->rank));
-      CHECK(shard_allreduce_vec(c));
-      CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, e));
+      CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, e, true));
       CHECK(shard_rebase(c, c->nranks, c->rank, -e, c->g.rows + e));
     } else {
       CHECK(exchange_halos_k(c, {HALO_BELIEF, HALO_VALUE}, e));

@@ -158,7 +158,7 @@ int pp2_shard_group_create(pp2_shard_group** out, pp2_ctx* const* ctxs, int n) {
   {
     DeviceGuard dg(ctxs[0]->device);
     if (hipEventCreateWithFlags(&g->ev_total, hipEventDisableTiming) != hipSuccess ||
-        hipMalloc(&g->d_gather, (2 * n + 1) * sizeof(float)) != hipSuccess)
+        hipMalloc(&g->d_gather, (pp2::kVecRec * n + 1) * sizeof(float)) != hipSuccess)
       return fail(set_err(PP2_ENOMEM, "shard group scratch"));
   }
   int min_rows = ctxs[0]->g.rows;
@@ -293,8 +293,8 @@ static int group_share_vec(pp2_shard_group* g) {
     DeviceGuard dg(c0->device);
     for (int r = 0; r < n; ++r) {
       HIPCHK(hipStreamWaitEvent(c0->stream, g->ev_local[r], 0));
-      HIPCHK(hipMemcpyAsync(g->d_gather + 2 * r, g->ctx[r]->d_vec + 2 * r, 2 * sizeof(float),
-                            hipMemcpyDefault, c0->stream));
+      HIPCHK(hipMemcpyAsync(g->d_gather + pp2::kVecRec * r, g->ctx[r]->d_vec + pp2::kVecRec * r,
+                            pp2::kVecRec * sizeof(float), hipMemcpyDefault, c0->stream));
     }
     HIPCHK(hipEventRecord(g->ev_total, c0->stream));
   }
@@ -302,8 +302,8 @@ static int group_share_vec(pp2_shard_group* g) {
     pp2_ctx* c = g->ctx[r];
     DeviceGuard dg(c->device);
     HIPCHK(hipStreamWaitEvent(c->stream, g->ev_total, 0));
-    HIPCHK(hipMemcpyAsync(c->d_vec, g->d_gather, 2 * n * sizeof(float), hipMemcpyDefault,
-                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_vec, g->d_gather, pp2::kVecRec * n * sizeof(float),
+                          hipMemcpyDefault, c->stream));
   }
   return PP2_OK;
 }

@@ -1,6 +1,9 @@
 // Streaming ceilings for the rollout step's traffic (2 B read + 2 B written
 // per cell-copy): a grid-stride copy of N bytes with 8-B and 16-B lanes, and
-// hipMemcpyDtoD, each timed with HIP events.  Build on the host:
+// hipMemcpyDtoD, each timed with HIP events.  Then the alpha re-streaming a
+// leaf pass fused into the last band step would add: the 9
+// fp32 FIB planes of the 512^2 grid (9.4 MB, beyond one XCD's L2) read once
+// per 2-copy chunk, 2048 times = 19.3 GB from L2 / MALL.  Build on the host:
 //   hipcc --offload-arch=gfx950 -O3 -o tools/micro/copy_bw tools/micro/copy_bw.hip
 // run on the GPU box: tools/micro/copy_bw [MiB]
 #include <hip/hip_runtime.h>
@@ -14,6 +17,21 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_copy(const T* __restrict__ a, T* __restrict__ b, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
     __builtin_nontemporal_store(a[i], b + i);
+}
+
+// block (t, r): tile t's 9 x 512 floats of the planes (plane stride ps),
+// summed (so the loads are kept); the same tile for every r, so the working
+// set is the planes' 9.4 MB and the reads come from L2 / MALL
+__global__ __launch_bounds__(256) void k_restream(const float* __restrict__ F, size_t ps,
+                                                  float* __restrict__ sink) {
+  const size_t x = (size_t)blockIdx.x * 512 + threadIdx.x * 2;
+  float acc = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const float2 v = *reinterpret_cast<const float2*>(F + q * ps + x);
+    acc += v.x + v.y;
+  }
+  if (acc == 12345.0f) sink[blockIdx.y] = acc;  // never: keeps the loads
 }
 
 #define CK(x)                                                        \
@@ -70,5 +88,27 @@ int main(int argc, char** argv) {
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= 5;
   printf("%-24s %8.3f ms  %6.2f TB/s (read+write)\n", "hipMemcpyDtoD", ms, 2.0 * bytes / (ms * 1e-3) / 1e12);
+  // the fused leaf pass's alpha re-streaming: 9 planes of 512^2 floats, read
+  // once per 2-copy chunk of 4096 copies
+  {
+    const size_t cells = 512 * 512, ps = cells;
+    float *F, *sink;
+    CK(hipMalloc(&F, 9 * cells * sizeof(float)));
+    CK(hipMalloc(&sink, 4096 * sizeof(float)));
+    CK(hipMemset(F, 0, 9 * cells * sizeof(float)));
+    const int reps = 2048;
+    const dim3 grid((unsigned)(cells / 512), reps);
+    hipLaunchKernelGGL(k_restream, grid, dim3(256), 0, 0, (const float*)F, ps, sink);
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < 5; ++r)
+      hipLaunchKernelGGL(k_restream, grid, dim3(256), 0, 0, (const float*)F, ps, sink);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= 5;
+    const double gb = 9.0 * cells * 4 * reps / 1e9;
+    printf("%-24s %8.3f ms  %6.2f TB/s (%.1f GB of 9.4 MB re-read %d times)\n",
+           "alpha re-stream", ms, gb / (ms * 1e-3) / 1e3, gb, reps);
+  }
   return 0;
 }
