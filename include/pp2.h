@@ -170,6 +170,15 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           rows always; 2 = two tile columns wherever they
  *                           fit.  Results are bit-identical either way. */
 #define PP2_TUNE_RESIDENT_TILE_COLS 12
+/*  PP2_TUNE_SHARD_LAG       row shards' resident launches: 1 (default) = a
+ *                           normalisation block start inside a launch scales
+ *                           the view by the power of two chosen from its mass
+ *                           one block earlier (already reduced: no grid-wide
+ *                           wait); 0 = from the previous step's mass, after
+ *                           every tile of the view has arrived.  Beliefs equal
+ *                           each other to rounding (power-of-two scales are
+ *                           exact); values and actions are bit-identical. */
+#define PP2_TUNE_SHARD_LAG 13
 /*  Diagnostics (tests):
  *  PP2_TUNE_RESIDENT_CUS    plan resident launches for at most this many CUs
  *                           (0: all); a grid whose tiles do not fit falls

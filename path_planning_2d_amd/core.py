@@ -106,6 +106,7 @@ class GridContext:
     TUNE_RESIDENT_CUS = 10
     TUNE_RESIDENT_STALL = 11
     TUNE_RESIDENT_TILE_COLS = 12
+    TUNE_SHARD_LAG = 13
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))

@@ -230,7 +230,7 @@ hipError_t launch_mdp_sweep_coded(hipStream_t st, const Geom& g, float gamma,
 // shard runs it on a *view*: its owned rows extended by e halo rows per side
 // (DESIGN.md §6).
 constexpr int kResidentMaxSteps = 2048;  // steps per launch (kernel-argument trajectory)
-constexpr int kResidentRing = 16;        // partial-mass slots (>= block depth + 2)
+constexpr int kResidentRing = 32;        // partial-mass slots (> 3 x block depth: lagged shard block starts)
 constexpr int kResidentSyncArrive = 0;   // sync words: block-start arrivals,
 constexpr int kResidentSyncErr = 2;      //   sticky timeout flag
 constexpr int kResidentSyncWords = 16;
@@ -263,8 +263,10 @@ struct ResidentHead {
   int n, kstep0, depth, rt, ntiles, nparts;
   int tc;                    // tile columns (ResidentPlan::tc)
   int own0, own1;            // owned view rows: only they store b', J', A and add to the mass
-  int shard;                 // 1: block starts inside the run scale by 2^k from the owned
-                             //   mass (no cross-rank reduction), k summed into *scale_out
+  int shard;                 // 1: block starts inside the run scale by 2^k from the view's
+                             //   mass (no cross-rank reduction), k summed into *scale_out;
+                             // 2: the same, k chosen from the view's mass one block
+                             //   earlier (lagged: no grid-wide wait at a block start)
   float bscale;              // block-start scale (2^96, or 1 for depth 1)
   const float* in_partials;  // step 0's pending input mass (block start), or null
   int in_n;

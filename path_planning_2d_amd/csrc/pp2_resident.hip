@@ -157,6 +157,20 @@ __device__ __forceinline__ int pow2_shift(float S) {
   return sh < 0 ? 0 : sh > 127 ? 127 : sh;
 }
 __device__ __forceinline__ float pow2f(int k) { return __uint_as_float((uint32_t)(127 + k) << 23); }
+// Lagged shard block starts (shard mode 2): the shift at block start t is
+// chosen from X = S * 2^prev, S the view's mass of step t-1-depth (before the
+// previous block start's shift prev): the mass only decreases (T is
+// column-stochastic over the view, L <= 1, rows outside the view read 0), so
+// X bounds the mass of step t-1 and the scaled mass stays below 2^121 --
+// it lands in [2^120 * (decay over depth steps), 2^121).  The target 2^120
+// (not 2^96) keeps the headroom of the non-lagged scheme over the up to
+// 2 x depth steps of decay between two such shifts.
+__device__ __forceinline__ int pow2_shift_lagged(float S, int prev) {
+  if (!(S > 0.0f) || !(S < FLT_MAX)) return 0;
+  const int e = (int)((__float_as_uint(S) >> 23) & 0xffu) - 127;
+  const int sh = 120 - e - prev;
+  return sh < 0 ? 0 : sh > 127 ? 127 : sh;
+}
 
 // wave_reduce_partials (pp2_device.h) with sc1 loads: the partials were
 // stored by other CUs inside this launch.  Same association, bit for bit.
@@ -689,6 +703,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   const int redw = a.rt >= 3 && wpr >= 4 ? wpr + 1 : 0;
   unsigned arrivals = a.arrive_base;
   int shift = 0;  // shard runs: the power-of-two shifts of the block starts so far
+  int sh_prev = 0;  // lagged shard block starts: the previous block start's shift
   float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, best[4] = {0.0f, 0.0f, 0.0f, 0.0f}, local = 0.0f;
   uint32_t arg[4] = {0u, 0u, 0u, 0u};
   PP2_RP(2);
@@ -779,7 +794,28 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       step_quad();
       if (!bs) finish_quad();
     }
-    if (bs) {
+    if (bs && a.shard == 2) {
+      // lagged: step t-1-depth's view mass, whose arrivals were due at the
+      // previous block start (shards run kstep0 = 0, so block starts fall on
+      // multiples of depth; the launch's first one has the input's bound
+      // 2^96 -- step 0 scaled the normalised belief by it -- and keeps it)
+      const int tl = t - 1 - a.depth;
+      if (wave == redw) {
+        arrivals += a.ntiles;
+        float S = -1.0f;
+        if (tl >= 0) {
+          wave_wait(a.sync + kResidentSyncArrive, 1, arrivals - a.ntiles, err, a.err_host);
+          S = wave_reduce_partials_sc1(a.ring + (size_t)(tl % kResidentRing) * a.nparts, a.nparts);
+        }
+        if (lane == 0) sS[0] = S;
+      }
+      __syncthreads();
+      const int sh = tl >= 0 ? pow2_shift_lagged(sS[0], sh_prev) : 0;
+      sh_prev = sh;
+      shift += sh;
+      inv = pow2f(sh);
+      if (valid) finish_quad();
+    } else if (bs) {
       if (wave == redw) {
         arrivals += a.ntiles;
         wave_wait(a.sync + kResidentSyncArrive, 1, arrivals, err, a.err_host);

@@ -1433,7 +1433,7 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
   a.nparts = nparts;
   a.own0 = e;
   a.own1 = e + c->g.rows;
-  a.shard = 1;
+  a.shard = c->shard_lag ? 2 : 1;
   a.bscale = kBlockScale;
   a.in_partials = nullptr;
   a.in_n = 0;
@@ -1650,6 +1650,10 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
         return set_err(PP2_EINVAL, "resident halo %d not in [0, %d]", value, c->g.halo);
       c->res_halo = value;
       c->res_e_dict = -1;
+      return PP2_OK;
+    case PP2_TUNE_SHARD_LAG:
+      if (value < 0 || value > 1) return set_err(PP2_EINVAL, "shard lag %d not in [0, 1]", value);
+      c->shard_lag = value;
       return PP2_OK;
     case PP2_TUNE_STEP_PAIRS:
       if (value < 0 || value > 2) return set_err(PP2_EINVAL, "step pairs %d not in [0, 2]", value);

@@ -11,10 +11,15 @@ edge rows go stale by one row per step, so the owned rows stay exact for e
 steps).  The first step of a block divides by the global mass M and scales
 by 2^96; inside a block every `depth` steps the view is rescaled by a power
 of two chosen from the view's own mass (exact, so shards may pick different
-shifts).  At a block boundary and at the end of the call each rank posts
-{owned mass, total shift}, the vector is all-reduced, and every rank rebases
-its rows -- a halo row by its owner's shift -- to the common (minimum) shift,
-the global mass being the rank-ordered sum at that scale.  Values and
+shifts) -- the mass of the previous step (PP2_TUNE_SHARD_LAG 0), or, lagged
+(the default), the mass of the step before the previous block start times
+the shift applied there, into [2^120, 2^121) (pp2_resident.hip
+pow2_shift_lagged; the launch's first block start keeps the input's scale).  At a block boundary each rank posts its {owned mass, total shift,
+lost} record and sends it to every other rank in the same point-to-point
+group as the halo rows (one RCCL round per block); at the end of the call the
+records are all-reduced.  Every rank then rebases its rows -- a halo row by
+its owner's shift -- to the common (minimum) shift, the global mass being the
+rank-ordered sum at that scale.  Values and
 actions must equal the global oracle bit for bit; the normalised belief
 within rel 1e-5 of the fp64-normalised global chain."""
 import os
@@ -39,7 +44,16 @@ def _pow2_shift(S):
     return min(max(96 - e, 0), 127)
 
 
-def _worker(rank, world, port, name, steps, e, depth, result_q):
+def _pow2_shift_lagged(S, prev):
+    """pp2_resident.hip pow2_shift_lagged: 2^(120 - ilogb(S) - prev)."""
+    S = np.float32(S)
+    if not (S > 0) or not np.isfinite(S):
+        return 0
+    e = int(np.frexp(S)[1]) - 1
+    return min(max(120 - e - prev, 0), 127)
+
+
+def _worker(rank, world, port, name, steps, e, depth, lag, result_q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -78,36 +92,49 @@ def _worker(rank, world, port, name, steps, e, depth, result_q):
         own = slice(e, e + R)
         lib = O.lib()
 
-        def exchange(a):  # e halo rows each side (one RCCL group in the product)
-            t = torch.from_numpy(a)
+        REC = 3  # pp2::kVecRec: {owned mass, shift, lost} per rank
+
+        def exchange(arrays, vec=None):
+            # e halo rows of each array each side, and with vec this rank's
+            # record to / from every other rank: ONE group (exchange_halos_k
+            # with records); the messages between two ranks match in issue
+            # order, the record first
             ops = []
-            if rank > 0:
-                ops += [dist.P2POp(dist.isend, t[e:2 * e].clone(), rank - 1),
-                        dist.P2POp(dist.irecv, t[0:e], rank - 1)]
-            if rank < world - 1:
-                ops += [dist.P2POp(dist.isend, t[R:R + e].clone(), rank + 1),
-                        dist.P2POp(dist.irecv, t[R + e:V], rank + 1)]
+            if vec is not None:
+                for q in range(world):
+                    if q != rank:
+                        ops += [dist.P2POp(dist.isend, vec[REC * rank:REC * rank + REC].clone(), q),
+                                dist.P2POp(dist.irecv, vec[REC * q:REC * q + REC], q)]
+            for a in arrays:
+                t = torch.from_numpy(a)
+                if rank > 0:
+                    ops += [dist.P2POp(dist.isend, t[e:2 * e].clone(), rank - 1),
+                            dist.P2POp(dist.irecv, t[0:e], rank - 1)]
+                if rank < world - 1:
+                    ops += [dist.P2POp(dist.isend, t[R:R + e].clone(), rank + 1),
+                            dist.P2POp(dist.irecv, t[R + e:V], rank + 1)]
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
 
-        def mass_vec(shift):  # k_shard_mass_vec + the all-reduce
-            vec = torch.zeros(2 * world, dtype=torch.float64)
-            vec[2 * rank] = float(np.float32(b[own].astype(np.float64).sum()))
-            vec[2 * rank + 1] = float(shift)
-            dist.all_reduce(vec)
-            return vec.numpy()
+        def post(shift):  # k_shard_mass_vec: this rank's record, zeros elsewhere
+            vec = torch.zeros(REC * world, dtype=torch.float64)
+            vec[REC * rank] = float(np.float32(b[own].astype(np.float64).sum()))
+            vec[REC * rank + 1] = float(shift)
+            return vec
 
         def rebase(vec, rows):  # k_shard_rebase over view rows `rows`
-            C = int(min(vec[2 * q + 1] for q in range(world)))
+            vec = vec.numpy()
+            C = int(min(vec[REC * q + 1] for q in range(world)))
+            assert not any(vec[REC * q + 2] for q in range(world))
             M = np.float32(0.0)
             for q in range(world):
-                M = np.float32(M + np.float32(np.ldexp(np.float32(vec[2 * q]),
-                                                      C - int(vec[2 * q + 1]))))
+                M = np.float32(M + np.float32(np.ldexp(np.float32(vec[REC * q]),
+                                                      C - int(vec[REC * q + 1]))))
             for y in rows:
                 q = rank - 1 if y < e else rank + 1 if y >= e + R else rank
                 if q < 0 or q >= world:
                     q = rank
-                k = C - int(vec[2 * q + 1])
+                k = C - int(vec[REC * q + 1])
                 if k:
                     b[y] = np.ldexp(b[y], k).astype(np.float32)
             return M
@@ -117,20 +144,26 @@ def _worker(rank, world, port, name, steps, e, depth, result_q):
         for i in range(0, steps, e):
             mm = min(e, steps - i)
             if pending:
-                vec = mass_vec(shift)
-                exchange(b)
-                exchange(J)
+                vec = post(shift)
+                exchange([b, J], vec)  # one round: records + halo rows
                 M = rebase(vec, range(V))
             else:
-                exchange(b)
-                exchange(J)
+                exchange([b, J])
             shift = 0
+            vmass = []  # the view's mass after each step of this launch
+            sh_prev = 0
             for t in range(mm):
                 k = i + t
                 if t == 0:
                     inv = np.float32(np.float32(1.0) / M) * np.float32(2.0 ** 96)
                 elif t % depth == 0:
-                    sh = _pow2_shift(b.astype(np.float64).sum())
+                    if not lag:
+                        sh = _pow2_shift(b.astype(np.float64).sum())
+                    elif t - 1 - depth >= 0:
+                        sh = _pow2_shift_lagged(vmass[t - 1 - depth], sh_prev)
+                    else:
+                        sh = 0
+                    sh_prev = sh
                     shift += sh
                     inv = np.float32(2.0 ** sh)
                 else:
@@ -139,13 +172,17 @@ def _worker(rank, world, port, name, steps, e, depth, result_q):
                 lib.orc_belief_update_rows(V, W, Tv, Lv, b.reshape(-1), int(us[k]), int(zs[k]),
                                            bo.reshape(-1), 1, 0, V)
                 b = (bo * inv).astype(np.float32)
+                assert np.all(np.isfinite(b))
+                vmass.append(b.astype(np.float64).sum())
                 Jo = np.zeros_like(J)
                 A = np.zeros(V * W, np.uint8)
                 lib.orc_mdp_sweep_rows(V, W, GAMMA, Tv, Cv, J.reshape(-1), Jo.reshape(-1), A, 0, V)
                 J = Jo
             pending = True
-        # the close: the global mass at a common scale
-        M = rebase(mass_vec(shift), range(e, e + R))
+        # the close: the records all-reduced, the global mass at a common scale
+        vec = post(shift)
+        dist.all_reduce(vec)
+        M = rebase(vec, range(e, e + R))
         bn = (b[own].astype(np.float64) / float(M)).astype(np.float32)
         parts = [bn, J[own], A.reshape(V, W)[own]]
         gathered = []
@@ -159,11 +196,13 @@ def _worker(rank, world, port, name, steps, e, depth, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world,steps,e,depth", [
-    ("sparse_map_100x40", 2, 13, 5, 2),
-    ("tile64_sparse_map_100x40", 3, 10, 4, 3),
+@pytest.mark.parametrize("name,world,steps,e,depth,lag", [
+    ("sparse_map_100x40", 2, 13, 5, 2, 0),
+    ("tile64_sparse_map_100x40", 3, 10, 4, 3, 0),
+    ("sparse_map_100x40", 2, 40, 17, 2, 1),
+    ("tile64_sparse_map_100x40", 3, 30, 12, 3, 1),
 ])
-def test_resident_shard_scheme_matches_global(name, world, steps, e, depth):
+def test_resident_shard_scheme_matches_global(name, world, steps, e, depth, lag):
     import torch.multiprocessing as mp
     from conftest import GAMMA, assert_rel_close, golden, golden_map
     from oracle import oracle as O
@@ -171,7 +210,7 @@ def test_resident_shard_scheme_matches_global(name, world, steps, e, depth):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, steps, e, depth, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, steps, e, depth, lag, q))
              for r in range(world)]
     for p in procs:
         p.start()

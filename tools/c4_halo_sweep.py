@@ -1,7 +1,8 @@
 """Config 4's per-rank share (rank 3 of 8: rows [768, 1024) x 2048 of the
 2048^2 grid on a 1-rank RCCL communicator, bench.config4_rank_share) for
-several resident halo depths e (PP2_TUNE_RESIDENT_HALO) and tilings
-(PP2_TUNE_RESIDENT_TILE_COLS): a smaller e shrinks the view (256 + 2e rows)
+several resident halo depths e (PP2_TUNE_RESIDENT_HALO), tilings
+(PP2_TUNE_RESIDENT_TILE_COLS), normalisation blocks and lagged / waited
+block starts (PP2_TUNE_SHARD_LAG): a smaller e shrinks the view (256 + 2e rows)
 and the cells per CU, at the price of more launches and RCCL rounds per call.
 Prints, per setting, e, the plan's steps per launch, the measured us per
 step and the projection at the assumed 10 / 30 us RCCL round."""
@@ -30,10 +31,11 @@ def main():
     tcs = [int(x) for x in os.environ.get("PP2_TCS", "0,1,2").split(",")]
     # normalisation block depths (PP2_TUNE_NORM_BLOCK) at the first halo and
     # tiling: what a block start costs inside the shard's resident launch
-    norms = [int(x) for x in os.environ.get("PP2_NORMS", "8,4,2").split(",")]
-    cases = [(e_req, tc, 0) for e_req in halos for tc in tcs]
-    cases += [(halos[0], tcs[0], nb) for nb in norms]
-    for e_req, tc, nb in cases:
+    norms = [int(x) for x in os.environ.get("PP2_NORMS", "8,4").split(",")]
+    # (e, tile columns, norm block, lagged shard block starts)
+    cases = [(e_req, tc, 0, 1) for e_req in halos for tc in tcs]
+    cases += [(e_req, 0, nb, lag) for e_req in (halos[0], 64) for nb in norms for lag in (0, 1)]
+    for e_req, tc, nb, lag in cases:
         if True:
             ctx = P.GridContext(grid, goal, gamma=bench.GAMMA, device=0, rows=(r0, r1))
             ctx.set_stream(stream.cuda_stream)
@@ -43,6 +45,7 @@ def main():
                 ctx.set_tuning(P.GridContext.TUNE_RESIDENT_TILE_COLS, tc)
             if nb:
                 ctx.set_tuning(P.GridContext.TUNE_NORM_BLOCK, nb)
+            ctx.set_tuning(P.GridContext.TUNE_SHARD_LAG, lag)
             ctx.model_generate()
             ctx.belief_set(b0[r0 * G:r1 * G])
             ctx.mdp_reset()
@@ -60,7 +63,7 @@ def main():
             t = float(np.median(ts))
             rounds = -(-k // e) + 1 if e > 0 else 0
             proj = [t + rounds * r / k for r in bench.RCCL_ROUND_US]
-            print(f"e_req {e_req:4d} tc {tc} norm {nb or 8} -> e {e:4d}: {t:6.3f} us/step "
+            print(f"e_req {e_req:4d} tc {tc} norm {nb or 8} lag {lag} -> e {e:4d}: {t:6.3f} us/step "
                   f"(runs {', '.join(f'{x:.3f}' for x in ts)}), rounds {rounds}, "
                   f"projection {proj[0]:.3f}-{proj[1]:.3f} us/step", flush=True)
 

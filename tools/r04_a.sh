@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-timeout -k 10 240 python -u -m pytest tests/test_gpu_fchain.py tests/test_gpu_planner.py -x -q \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fchain.py tests/test_gpu_planner.py tests/test_gpu_shards.py -x -q \
   --timeout 120 --timeout-method thread -p no:cacheprovider > $O/r04_t4.log 2>&1 || { tail -30 $O/r04_t4.log; exit 1; }
 tail -2 $O/r04_t4.log
 timeout -k 10 60 python3 tools/fchain_timing.py > $O/r04_fct2.txt 2>&1 || { cat $O/r04_fct2.txt; exit 1; }
