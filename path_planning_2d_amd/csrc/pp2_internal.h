@@ -242,6 +242,8 @@ constexpr int kResidentGranules = 2;
 // column cross CUs too, one 8-B {b, j} side granule per row, at most
 // kResidentMaxRt rows per tile (rt * tw / 4 <= 1024 lanes, tw >= 256).
 constexpr int kResidentMaxRt = 16;
+// Lagged shard block starts: a view's partials staged in LDS (<= this many).
+constexpr int kResRedFloats = 4096;
 struct ResidentPlan {
   int rt = 0, ntiles = 0, threads = 0;
   int tc = 1;  // tile columns (1: tiles of whole rows)
@@ -263,6 +265,8 @@ struct ResidentHead {
   int n, kstep0, depth, rt, ntiles, nparts;
   int tc;                    // tile columns (ResidentPlan::tc)
   int own0, own1;            // owned view rows: only they store b', J', A and add to the mass
+  int red_lds;               // shard mode 2: the lagged partials are staged in LDS
+                             //   (kResRedFloats more dynamic LDS at launch)
   int shard;                 // 1: block starts inside the run scale by 2^k from the view's
                              //   mass (no cross-rank reduction), k summed into *scale_out;
                              // 2: the same, k chosen from the view's mass one block

@@ -449,8 +449,9 @@ struct Trajectory {
 };
 
 // TC: tile columns (a compile-time constant, so the whole-row instance has no
-// side-lane code at all)
-template <int CAP, int TC>
+// side-lane code at all); LAG: shard mode 2's lagged block starts (their own
+// instances, so that the unsharded loop carries none of their state)
+template <int CAP, int TC, bool LAG>
 __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
                                                            const Trajectory<CAP> tr) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -467,6 +468,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   uint8_t* sP = reinterpret_cast<uint8_t*>(sTC + lds_span(rows_floats(a.E, true)));
   float* sB0 = reinterpret_cast<float*>(sP) + lds_span(9 * prows * ps / 4);
   float* sS = sB0 + 4 * bufn;
+  float* sRed = sS + 16;  // (red_lds) the lagged block start's partials
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   if (tile == a.stall_tile) return;  // diagnostic: a tile that never arrives
@@ -703,7 +705,26 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   const int redw = a.rt >= 3 && wpr >= 4 ? wpr + 1 : 0;
   unsigned arrivals = a.arrive_base;
   int shift = 0;  // shard runs: the power-of-two shifts of the block starts so far
-  int sh_prev = 0;  // lagged shard block starts: the previous block start's shift
+  // Lagged shard block starts (shard mode 2; shards run kstep0 = 0, so block
+  // starts fall on multiples of depth).  The shift of the block start at T
+  // comes from step tl = T-1-depth's view mass, whose arrivals were due a
+  // block earlier: the reduction wave polls the arrival counter for it at
+  // the top of step T-2, pulls step tl's partials into sRed by LDS-DMA (sc1,
+  // no VGPRs) at the top of step T-1 -- the wave has no global loads of its
+  // own in flight, and step T-1's drain (T is an arrival step's successor)
+  // completes the copy -- and sums them at the end of step T-1 into sS[0];
+  // every wave takes the shift at the top of step T, before its gather.  No
+  // barrier and no grid-wide wait of its own.  A tile whose poll came back
+  // short (or without red_lds) waits and reduces at the end of step T-1
+  // instead, in the same association: every tile gets the same bits.
+  constexpr bool lag = LAG;
+  int sh_prev = 0;  // the previous lagged block start's shift
+  unsigned arr_v = 0u;
+  bool red_ok = false;
+  auto lag_start = [&](int T) {  // a lagged block start with a reduction
+    return lag && T > 0 && T < a.n && T % a.depth == 0 && T - 1 - a.depth >= 0;
+  };
+  auto lag_target = [&](int T) { return a.arrive_base + (unsigned)(T / a.depth - 1) * a.ntiles; };
   float p[4] = {0.0f, 0.0f, 0.0f, 0.0f}, best[4] = {0.0f, 0.0f, 0.0f, 0.0f}, local = 0.0f;
   uint32_t arg[4] = {0u, 0u, 0u, 0u};
   PP2_RP(2);
@@ -720,6 +741,29 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
     // this tile's compute instead of preceding it.
     const bool bs = t > 0 && (a.kstep0 + t) % a.depth == 0;
     if (t > 0 && !bs) inv = 1.0f;
+    if (lag) {
+      if (wave == redw) {
+        if (lag_start(t + 1)) {  // step t+1-1-depth's partials into sRed
+          red_ok = a.red_lds && reached(arr_v, lag_target(t + 1));
+          if (red_ok) {
+            const float* src = a.ring + (size_t)((t - a.depth) % kResidentRing) * a.nparts;
+            const int nq = a.nparts >> 2;
+            for (int c = 0; c * 64 < nq; ++c) {
+              const int i = c * 64 + lane < nq ? c * 64 + lane : nq - 1;
+              __builtin_amdgcn_global_load_lds((glb_void*)(src + 4 * i), (lds_void*)(sRed + c * 256), 16,
+                                               0, kSc1);
+            }
+          }
+        }
+        if (lag_start(t + 2)) arr_v = ld_flag(a.sync + kResidentSyncArrive);
+      }
+      if (bs) {  // the shift from sS[0] (the end of step t-1), before the gather
+        const int sh = t - 1 - a.depth >= 0 ? pow2_shift_lagged(sS[0], sh_prev) : 0;
+        sh_prev = sh;
+        shift += sh;
+        inv = pow2f(sh);
+      }
+    }
     PP2_RT(0);
     local = 0.0f;
     // one quad of step t: window rows from LDS (step t-1), the neighbour rows
@@ -792,30 +836,9 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       // the end of their step t-1) and compute with issue priority
       if (bnd) __builtin_amdgcn_s_setprio(2);  // 6.0 vs 7.4 us/step at 1024^2 without
       step_quad();
-      if (!bs) finish_quad();
+      if (!bs || lag) finish_quad();
     }
-    if (bs && a.shard == 2) {
-      // lagged: step t-1-depth's view mass, whose arrivals were due at the
-      // previous block start (shards run kstep0 = 0, so block starts fall on
-      // multiples of depth; the launch's first one has the input's bound
-      // 2^96 -- step 0 scaled the normalised belief by it -- and keeps it)
-      const int tl = t - 1 - a.depth;
-      if (wave == redw) {
-        arrivals += a.ntiles;
-        float S = -1.0f;
-        if (tl >= 0) {
-          wave_wait(a.sync + kResidentSyncArrive, 1, arrivals - a.ntiles, err, a.err_host);
-          S = wave_reduce_partials_sc1(a.ring + (size_t)(tl % kResidentRing) * a.nparts, a.nparts);
-        }
-        if (lane == 0) sS[0] = S;
-      }
-      __syncthreads();
-      const int sh = tl >= 0 ? pow2_shift_lagged(sS[0], sh_prev) : 0;
-      sh_prev = sh;
-      shift += sh;
-      inv = pow2f(sh);
-      if (valid) finish_quad();
-    } else if (bs) {
+    if (bs && !lag) {
       if (wave == redw) {
         arrivals += a.ntiles;
         wave_wait(a.sync + kResidentSyncArrive, 1, arrivals, err, a.err_host);
@@ -846,6 +869,23 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
     // ---- arrive for the next step's block start (every wave drained first)
     const bool arrive = (a.kstep0 + t + 1) % a.depth == 0;
     if (arrive) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wave == redw && lag_start(t + 1)) {  // the lagged mass for the next step's block start
+      float S;
+      if (red_ok) {  // (the drain above completed the copy)
+        const int nq = a.nparts >> 2;
+        float sl = 0.0f;
+        for (int i = lane; i < nq; i += 64) {
+          const f4a w = *reinterpret_cast<const f4a*>(sRed + 4 * i);
+          sl += ((w[0] + w[1]) + w[2]) + w[3];
+        }
+        S = wave_sum(sl);
+      } else {
+        wave_wait(a.sync + kResidentSyncArrive, 1, lag_target(t + 1), err, a.err_host);
+        S = wave_reduce_partials_sc1(a.ring + (size_t)((t - a.depth) % kResidentRing) * a.nparts,
+                                     a.nparts);
+      }
+      if (lane == 0) sS[0] = S;
+    }
     __syncthreads();  // also: this step's LDS writes before the next step's reads
     if (arrive && threadIdx.x == 0)
       __hip_atomic_fetch_add(a.sync + kResidentSyncArrive, 1u, __ATOMIC_RELAXED,
@@ -1067,19 +1107,26 @@ static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPla
   if (threads > 1024 || rt > kResidentMaxRt) return false;
   const size_t lds = resident_lds_bytes(g, E, rt, tc);
   if (lds > kDictLdsMaxBytes) return false;
-  static unsigned long long attr[4] = {0, 0, 0, 0};
-  const void* kshort = tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 1>)
-                               : reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 2>);
-  const void* klong = tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 1>)
-                              : reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 2>);
-  allow_lds(kshort, attr[2 * (tc - 1)]);
-  allow_lds(klong, attr[2 * (tc - 1) + 1]);
-  int nb = 0, nb2 = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, klong, (int)threads, lds) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, kshort, (int)threads, lds) != hipSuccess ||
-      nb < 1 || nb2 < 1) {
-    (void)hipGetLastError();
-    return false;
+  static unsigned long long attr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const void* ks[4] = {
+      tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 1, false>)
+              : reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 2, false>),
+      tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 1, false>)
+              : reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 2, false>),
+      tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 1, true>)
+              : reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 2, true>),
+      tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 1, true>)
+              : reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 2, true>)};
+  int nb = 1 << 30;
+  for (int k = 0; k < 4; ++k) {
+    allow_lds(ks[k], attr[4 * (tc - 1) + k]);
+    int n1 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n1, ks[k], (int)threads, lds) != hipSuccess ||
+        n1 < 1) {
+      (void)hipGetLastError();
+      return false;
+    }
+    nb = std::min(nb, n1);
   }
   p->rt = rt;
   p->tc = tc;
@@ -1091,7 +1138,7 @@ static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPla
   // get one slot per CU, so this is ntiles <= ncus; the guide's SGPR caveat
   // (one block fewer than the API answer) applies to 256-lane blocks at
   // several per CU, not here.
-  return (long long)std::min(nb, nb2) * ncus >= p->ntiles;
+  return (long long)nb * ncus >= p->ntiles;
 }
 
 // Whole-row tiles, or two tile columns when whole rows would give tiles of
@@ -1121,25 +1168,31 @@ hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const Res
       (a.in_partials && a.in_partials == a.out_partials))
     return hipErrorInvalidValue;
   const ResidentHead& h = a;
+  const size_t lds = p.lds + (a.red_lds ? (size_t)kResRedFloats * sizeof(float) : 0);
+  if (a.red_lds && (a.shard != 2 || a.kstep0 != 0 || a.nparts > kResRedFloats || lds > kDictLdsMaxBytes))
+    return hipErrorInvalidValue;
+  const bool lag = a.shard == 2;
+#define PP2_RES_LAUNCH(CAPV, TCV)                                                              \
+  do {                                                                                         \
+    if (lag)                                                                                   \
+      hipLaunchKernelGGL((k_loop_resident<CAPV, TCV, true>), dim3(p.ntiles), dim3(p.threads), \
+                         lds, st, h, tr);                                                      \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_loop_resident<CAPV, TCV, false>), dim3(p.ntiles), dim3(p.threads), \
+                         lds, st, h, tr);                                                      \
+  } while (0)
   if (a.n <= kResidentShortSteps) {
     Trajectory<kResidentShortSteps> tr{};
     std::memcpy(tr.uz, a.uz, (size_t)a.n);
-    if (p.tc == 1)
-      hipLaunchKernelGGL((k_loop_resident<kResidentShortSteps, 1>), dim3(p.ntiles),
-                         dim3(p.threads), p.lds, st, h, tr);
-    else
-      hipLaunchKernelGGL((k_loop_resident<kResidentShortSteps, 2>), dim3(p.ntiles),
-                         dim3(p.threads), p.lds, st, h, tr);
+    if (p.tc == 1) PP2_RES_LAUNCH(kResidentShortSteps, 1);
+    else PP2_RES_LAUNCH(kResidentShortSteps, 2);
   } else {
     Trajectory<kResidentMaxSteps> tr;
     std::memcpy(tr.uz, a.uz, sizeof tr.uz);
-    if (p.tc == 1)
-      hipLaunchKernelGGL((k_loop_resident<kResidentMaxSteps, 1>), dim3(p.ntiles), dim3(p.threads),
-                         p.lds, st, h, tr);
-    else
-      hipLaunchKernelGGL((k_loop_resident<kResidentMaxSteps, 2>), dim3(p.ntiles), dim3(p.threads),
-                         p.lds, st, h, tr);
+    if (p.tc == 1) PP2_RES_LAUNCH(kResidentMaxSteps, 1);
+    else PP2_RES_LAUNCH(kResidentMaxSteps, 2);
   }
+#undef PP2_RES_LAUNCH
   return hipGetLastError();
 }
 

@@ -1434,6 +1434,8 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
   a.own0 = e;
   a.own1 = e + c->g.rows;
   a.shard = c->shard_lag ? 2 : 1;
+  a.red_lds = a.shard == 2 && nparts <= pp2::kResRedFloats &&
+              p.lds + (size_t)pp2::kResRedFloats * sizeof(float) <= pp2::kDictLdsMaxBytes;
   a.bscale = kBlockScale;
   a.in_partials = nullptr;
   a.in_n = 0;

@@ -19,6 +19,18 @@ __global__ __launch_bounds__(256) void k_copy(const T* __restrict__ a, T* __rest
     __builtin_nontemporal_store(a[i], b + i);
 }
 
+// read-only stream (the leaf pass's belief traffic): every word xor-folded
+// into a per-lane register, stored only if it equals a value zeros never give
+template <typename T>
+__global__ __launch_bounds__(256) void k_read(const T* __restrict__ a, size_t n, unsigned* sink) {
+  unsigned acc = 0u;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const T v = __builtin_nontemporal_load(a + i);
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k) acc ^= v[k];
+  }
+  if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
 // block (t, r): tile t's 9 x 512 floats of the planes (plane stride ps),
 // summed (so the loads are kept); the same tile for every r, so the working
 // set is the planes' 9.4 MB and the reads come from L2 / MALL
@@ -79,12 +91,25 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  float ms = 0;
+  for (int blocks : {2048, 8192, 32768}) {
+    const size_t n = bytes / 16;
+    hipLaunchKernelGGL(k_read<u4e>, dim3(blocks), dim3(256), 0, 0, (const u4e*)a, n, (unsigned*)b);
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < 10; ++r)
+      hipLaunchKernelGGL(k_read<u4e>, dim3(blocks), dim3(256), 0, 0, (const u4e*)a, n, (unsigned*)b);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= 10;
+    printf("%-24s blocks %6d  %8.3f ms  %6.2f TB/s (read only)\n", "read 16B/lane", blocks, ms,
+           bytes / (ms * 1e-3) / 1e12);
+  }
   CK(hipMemcpyDtoD(b, a, bytes));
   CK(hipEventRecord(e0));
   for (int r = 0; r < 5; ++r) CK(hipMemcpyDtoD(b, a, bytes));
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
-  float ms = 0;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= 5;
   printf("%-24s %8.3f ms  %6.2f TB/s (read+write)\n", "hipMemcpyDtoD", ms, 2.0 * bytes / (ms * 1e-3) / 1e12);

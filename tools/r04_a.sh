@@ -13,7 +13,9 @@ timeout -k 10 60 python3 tools/fchain_timing.py > $O/r04_fct2.txt 2>&1 || { cat 
 cat $O/r04_fct2.txt
 PP2_REF=1 PP2_STEPS=100 timeout -k 10 120 python3 tools/prof_planner.py > $O/r04_plan3.log 2>&1 || { cat $O/r04_plan3.log; exit 1; }
 cat $O/r04_plan3.log
-timeout -k 10 300 python3 tools/c4_halo_sweep.py > $O/r04_c4halo.txt 2>&1
-rc=$?
+timeout -k 10 300 python3 tools/c4_halo_sweep.py > $O/r04_c4halo.txt 2>&1 || { cat $O/r04_c4halo.txt; exit 1; }
 cat $O/r04_c4halo.txt
+timeout -k 10 60 tools/micro/copy_bw > $O/r04_copy_bw2.txt 2>&1
+rc=$?
+cat $O/r04_copy_bw2.txt
 exit $rc
