@@ -168,7 +168,14 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           2-D tiles hold 4 or more (a 256 x 2048 rank share
  *                           of the 2048^2 grid on its 512-row view); 1 = whole
  *                           rows always; 2 = two tile columns wherever they
- *                           fit.  Results are bit-identical either way. */
+ *                           fit; 3 = transposed tiles on a row shard's view
+ *                           whose row count is a multiple of 256 (e and the
+ *                           owned rows multiples of 4): a tile is a strip of
+ *                           grid columns spanning the whole view, so only its
+ *                           two side columns cross CUs (HBM keeps the row-major
+ *                           layout; the launch reads and writes it
+ *                           transposed).  Values and actions are bit-identical
+ *                           either way, beliefs equal to rounding. */
 #define PP2_TUNE_RESIDENT_TILE_COLS 12
 /*  PP2_TUNE_SHARD_LAG       row shards' resident launches: 1 (default) = a
  *                           normalisation block start inside a launch scales
@@ -227,7 +234,8 @@ int pp2_model_dict_info(pp2_ctx* ctx, int* entries, int* active);
 int pp2_loop_steps_per_launch(pp2_ctx* ctx, int* steps);
 /* The tiling of the tile-resident loop this context would launch (its grid,
  * or a row shard's view): tiles (one per CU), rows per tile and tile columns
- * (1: whole rows; 2: 2-D tiles, PP2_TUNE_RESIDENT_TILE_COLS); all 0 when the
+ * (1: whole rows; 2: 2-D tiles, PP2_TUNE_RESIDENT_TILE_COLS; 3: transposed
+ * tiles of a shard view, rows per tile = grid columns per tile); all 0 when the
  * loop does not run resident.  A query: allocates nothing. */
 int pp2_resident_tiling(pp2_ctx* ctx, int* tiles, int* rows_per_tile, int* tile_cols);
 /* Diagnostics: resident launches so far on this context -- tile-resident loop

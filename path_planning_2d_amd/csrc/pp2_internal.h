@@ -247,6 +247,7 @@ constexpr int kResRedFloats = 4096;
 struct ResidentPlan {
   int rt = 0, ntiles = 0, threads = 0;
   int tc = 1;  // tile columns (1: tiles of whole rows)
+  bool tr = false;  // transposed tiles (shard views): the plan is of transposed_geom(view)
   size_t lds = 0;
 };
 struct ResidentHead {
@@ -265,6 +266,7 @@ struct ResidentHead {
   int n, kstep0, depth, rt, ntiles, nparts;
   int tc;                    // tile columns (ResidentPlan::tc)
   int own0, own1;            // owned view rows: only they store b', J', A and add to the mass
+  int ows;                   // TR plans: the grid's row stride (a.g is the transposed view)
   int red_lds;               // shard mode 2: the lagged partials are staged in LDS
                              //   (kResRedFloats more dynamic LDS at launch)
   int shard;                 // 1: block starts inside the run scale by 2^k from the view's
@@ -335,8 +337,23 @@ inline size_t resident_xch_floats(const Geom& g, int ntiles) {
 }
 // tc_pref: 0 = automatic (two tile columns when whole-row tiles would hold
 // fewer than 4 rows and 2-D tiles hold 4 or more), 1 = whole rows, 2 = two
-// tile columns whenever they fit (and whole rows do: else no plan changes).
-bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref = 0);
+// tile columns whenever they fit (and whole rows do: else no plan changes),
+// 3 = transposed tiles when allow_tr (a shard view) and they fit: the plan is
+// then of transposed_geom(g).
+bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref = 0,
+                   bool allow_tr = false);
+// The kernel geometry of transposed tiles over view g: rows = g's row stride
+// (its columns), row stride = g.rows (its rows; a multiple of 256).
+inline Geom transposed_geom(const Geom& g) {
+  Geom t = g;
+  t.rows = g.wp;
+  t.width = g.rows;
+  t.wp = g.rows;
+  t.row0 = 0;
+  t.grows = g.wp;
+  t.halo = 0;
+  return t;
+}
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a);
 // Row-shard boundary kernels (pp2_resident.hip).  vec holds one
 // record of kVecRec floats per rank, {owned mass, shift, lost}: the mass of the

@@ -210,12 +210,17 @@ __device__ __forceinline__ float wave_reduce_partials_sc1(const float* p, int n)
 // LDS rows carry zero pads and off-grid plane bytes are class 0, whose
 // (finite, the host checks) T multiplies b = +0, and fmaf(T, +0, p) == p for
 // the non-negative partial sums.
-constexpr bool belief_row_used(int U, int oy) {
-  for (int s = 3 * oy; s < 3 * oy + 3; ++s)
-    if (sup_slot(U, 8 - s) >= 0) return true;
+// TR (transposed tiles): the kernel's rows are the grid's columns, so the
+// source cell at grid offset (oy - 1, ox) sits in window row ox + 1, window
+// column k + oy of the lane's quad cell k; the terms keep the grid's
+// ascending-s order (the same fmaf chain).
+template <bool TR>
+constexpr bool belief_row_used(int U, int r) {
+  for (int s = 0; s < 9; ++s)
+    if ((TR ? s % 3 : s / 3) == r && sup_slot(U, 8 - s) >= 0) return true;
   return false;
 }
-template <int U>
+template <int U, bool TR>
 __device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0, uint32_t lx4,
                                             int z, const Win6& win, float (&p)[4]) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -226,7 +231,7 @@ __device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0,
   uint32_t cb[3][6];
 #pragma unroll
   for (int oy = 0; oy < 3; ++oy) {
-    if (!belief_row_used(U, oy)) continue;
+    if (!belief_row_used<TR>(U, oy)) continue;
     const uint8_t* r = prow + oy * ps + 4 + x0;
     const uint32_t m = *reinterpret_cast<const uint32_t*>(r);
     uint32_t e = 0u;
@@ -244,13 +249,14 @@ __device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0,
   for (int k = 0; k < 4; ++k) p[k] = 0.0f;
 #pragma unroll
   for (int s = 0; s < 9; ++s) {
-    const int oy = s / 3, ox = s % 3 - 1;
+    // window row and column offset of grid offset s
+    const int wr = TR ? s % 3 : s / 3, wc = TR ? s / 3 - 1 : s % 3 - 1;
     const int sl = sup_slot(U, 8 - s);
     if (sl < 0) continue;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      p[k] = __builtin_fmaf(*reinterpret_cast<const float*>(qr + 4 * sl + cb[oy][k + 1 + ox]),
-                            win.v[oy][k + 1 + ox], p[k]);
+      p[k] = __builtin_fmaf(*reinterpret_cast<const float*>(qr + 4 * sl + cb[wr][k + 1 + wc]),
+                            win.v[wr][k + 1 + wc], p[k]);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -261,6 +267,7 @@ __device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0,
 // bytes on each side); this lane's rows start at plane row ty.
 // p = the gathered quad times L_z (the block-start scale and the mass
 // partial are applied by the caller)
+template <bool TR>
 __device__ __forceinline__ void belief_any(int u, const uint8_t* sP, int prows, int ps, int ty,
                                            int x0, uint32_t lx4, int z, const Win6& w,
                                            float (&p)[4]) {
@@ -274,10 +281,10 @@ __device__ __forceinline__ void belief_any(int u, const uint8_t* sP, int prows, 
   switch (u) {
 #define PP2_BQ(UU)                                                     \
   case UU:                                                             \
-    belief_fact<UU>(pu, ps, x0, lx4, z, w, p); \
+    belief_fact<UU, TR>(pu, ps, x0, lx4, z, w, p); \
     break;
     PP2_BQ(0) PP2_BQ(1) PP2_BQ(2) PP2_BQ(3) PP2_BQ(4) PP2_BQ(5) PP2_BQ(6) PP2_BQ(7)
-    default: belief_fact<8>(pu, ps, x0, lx4, z, w, p);
+    default: belief_fact<8, TR>(pu, ps, x0, lx4, z, w, p);
 #undef PP2_BQ
   }
 }
@@ -450,10 +457,17 @@ struct Trajectory {
 
 // TC: tile columns (a compile-time constant, so the whole-row instance has no
 // side-lane code at all); LAG: shard mode 2's lagged block starts (their own
-// instances, so that the unsharded loop carries none of their state)
-template <int CAP, int TC, bool LAG>
+// instances, so that the unsharded loop carries none of their state); TR:
+// transposed tiles (shard views, TC = 1): the kernel's grid is the view
+// transposed -- its rows are the grid's columns (a.g.rows = the grid's row
+// stride), its columns the view's rows (a.g.wp = the view's row count) -- so
+// a tile is a strip of rt grid columns spanning the whole view and only its
+// first and last columns cross CUs; HBM stays in the grid's layout (row
+// stride a.ows), read and written transposed once per launch.
+template <int CAP, int TC, bool LAG, bool TR>
 __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
                                                            const Trajectory<CAP> tr) {
+  static_assert(!TR || TC == 1, "transposed tiles are whole kernel rows");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // a tile: rt rows x tw columns (tc tile columns per row of tiles)
   constexpr int tc = TC;
@@ -488,7 +502,13 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   const int x0 = wj * 256 + lane * 4;  // (tile-relative)
   const int y = trow * a.rt + ty;
   const bool valid = y < rows;
-  const bool own = y >= a.own0 && y < a.own1;  // (a shard's view: owned rows only)
+  // (a shard's view: owned rows only -- TR: the quad's grid rows x0 .. x0+3,
+  // own0 / own1 multiples of 4)
+  const bool own = TR ? x0 >= a.own0 && x0 < a.own1 : y >= a.own0 && y < a.own1;
+  // HBM offset of kernel cell (yy, xx) (view row 0 = kernel column 0)
+  auto hoff = [&](int yy, int xx) -> long long {
+    return TR ? (long long)xx * a.ows + yy : (long long)yy * wp + xx;
+  };
   // the tile's first row reads the row above from tile - tc and publishes
   // itself for it; its last row likewise with tile + tc
   const bool nb_up = valid && ty == 0 && trow > 0;
@@ -591,9 +611,17 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   // overlaps the table staging and the class planes (consumed below)
   f4a b_t = {0.0f, 0.0f, 0.0f, 0.0f}, j_t = {0.0f, 0.0f, 0.0f, 0.0f};
   if (valid) {
-    const long long off = (long long)y * wp + gx + x0;
-    b_t = *reinterpret_cast<const f4a*>(a.b_in + off);
-    j_t = *reinterpret_cast<const f4a*>(a.j_in + off);
+    if (TR) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        b_t[k] = a.b_in[hoff(y, x0 + k)];
+        j_t[k] = a.j_in[hoff(y, x0 + k)];
+      }
+    } else {
+      const long long off = (long long)y * wp + gx + x0;
+      b_t = *reinterpret_cast<const f4a*>(a.b_in + off);
+      j_t = *reinterpret_cast<const f4a*>(a.j_in + off);
+    }
   }
   stage_rows(a.rfact, kResTab, lds);
   stage_rows(a.rows, rows_floats(a.E, true), sTC);
@@ -605,8 +633,13 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   // and L class bytes
   uint32_t cc[4] = {0u, 0u, 0u, 0u}, iwr[4][3], lx4 = 0u;
   if (valid) {
-    const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)y * wp + gx + x0);
-    cc[0] = m.x & 0xffffu; cc[1] = m.x >> 16; cc[2] = m.y & 0xffffu; cc[3] = m.y >> 16;
+    if (TR) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cc[k] = a.code[hoff(y, x0 + k)];
+    } else {
+      const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)y * wp + gx + x0);
+      cc[0] = m.x & 0xffffu; cc[1] = m.x >> 16; cc[2] = m.y & 0xffffu; cc[3] = m.y >> 16;
+    }
     const uint8_t* lx = reinterpret_cast<const uint8_t*>(a.rfact + kResLX);
 #pragma unroll
     for (int k = 0; k < 4; ++k) lx4 |= (uint32_t)lx[cc[k]] << (8 * k);
@@ -625,8 +658,14 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
     const int r = i / tpr, xq = (i % tpr) * 4, yy = trow * a.rt + r - 1;
     uint32_t pl[9] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     if (yy >= 0 && yy < rows) {
-      const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)yy * wp + gx + xq);
-      const uint32_t c4[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
+      uint32_t c4[4];
+      if (TR) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c4[k] = a.code[hoff(yy, xq + k)];
+      } else {
+        const uint2 m = *reinterpret_cast<const uint2*>(a.code + (long long)yy * wp + gx + xq);
+        c4[0] = m.x & 0xffffu; c4[1] = m.x >> 16; c4[2] = m.y & 0xffffu; c4[3] = m.y >> 16;
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint4 w = *reinterpret_cast<const uint4*>(sTC + kFactIW + 4 * c4[k]);
@@ -647,7 +686,7 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
     if (yy >= 0 && yy < rows) {
       auto cls = [&](int x) {
         const uint4 w = *reinterpret_cast<const uint4*>(
-            sTC + kFactIW + 4 * a.code[(long long)yy * wp + x]);
+            sTC + kFactIW + 4 * a.code[hoff(yy, x)]);
         return __builtin_amdgcn_ubfe(q < 4 ? w.x : q < 8 ? w.y : w.z, 8 * (q % 4), 8);
       };
       if (gx > 0) lp = cls(gx - 1) << 24;  // byte 3: x = -1
@@ -807,12 +846,12 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
         }
       }
       PP2_RT(1);
-      belief_any(u, sP, prows, ps, ty, x0, lx4, z, wb, p);
-      float jn[9][4];
+      belief_any<TR>(u, sP, prows, ps, ty, x0, lx4, z, wb, p);
+      float jn[9][4];  // grid stencil offset i = 3 (dy + 1) + dx + 1
 #pragma unroll
       for (int i = 0; i < 9; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) jn[i][k] = wj.v[i / 3][k + i % 3];
+        for (int k = 0; k < 4; ++k) jn[i][k] = TR ? wj.v[i % 3][k + i / 3] : wj.v[i / 3][k + i % 3];
       if (last) coded_sweep_iw<4, true>(sTC, iwr, jn, best, arg);  // actions: last step only
       else coded_sweep_iw<4, false>(sTC, iwr, jn, best, arg);
       *reinterpret_cast<f4a*>(sbuf(1, co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
@@ -895,7 +934,15 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
 
   // ---- the last step: b, J, A of the (owned) rows and the owned mass
   // partials (a shard's halo rows are its neighbours' rows)
-  if (own) {
+  if (own && TR) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long long off = hoff(y, x0 + k);
+      __builtin_nontemporal_store(p[k], a.b_out + off);
+      __builtin_nontemporal_store(best[k], a.j_out + off);
+      a.A[off] = (uint8_t)arg[k];
+    }
+  } else if (own) {
     const long long off = (long long)y * wp + gx + x0;
     store4<true>(a.b_out + off, p);
     store_ja<true>(a.j_out, a.A, off, best, arg);
@@ -1100,26 +1147,31 @@ size_t resident_lds_bytes(const Geom& g, int E, int rt, int tc) {
 
 // The plan with tc tile columns: rt rows per tile so that the tiles fit the
 // CUs, or false.
-static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPlan* p) {
+static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPlan* p,
+                             bool trn = false) {
   if (tc < 1 || tc > 2 || g.wp % (256 * tc) != 0 || (tc > 1 && g.wp / tc < 512) || ncus < tc) return false;
   const int rt = (g.rows + ncus / tc - 1) / (ncus / tc);
   const long long threads = (long long)rt * (g.wp / tc / 4);
   if (threads > 1024 || rt > kResidentMaxRt) return false;
   const size_t lds = resident_lds_bytes(g, E, rt, tc);
   if (lds > kDictLdsMaxBytes) return false;
-  static unsigned long long attr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (trn && tc != 1) return false;
+  static unsigned long long attr[12] = {};
+#define PP2_K(CAPV, TCV, LAGV, TRV) reinterpret_cast<const void*>(&k_loop_resident<CAPV, TCV, LAGV, TRV>)
   const void* ks[4] = {
-      tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 1, false>)
-              : reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 2, false>),
-      tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 1, false>)
-              : reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 2, false>),
-      tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 1, true>)
-              : reinterpret_cast<const void*>(&k_loop_resident<kResidentShortSteps, 2, true>),
-      tc == 1 ? reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 1, true>)
-              : reinterpret_cast<const void*>(&k_loop_resident<kResidentMaxSteps, 2, true>)};
+      trn ? PP2_K(kResidentShortSteps, 1, false, true)
+          : tc == 1 ? PP2_K(kResidentShortSteps, 1, false, false) : PP2_K(kResidentShortSteps, 2, false, false),
+      trn ? PP2_K(kResidentMaxSteps, 1, false, true)
+          : tc == 1 ? PP2_K(kResidentMaxSteps, 1, false, false) : PP2_K(kResidentMaxSteps, 2, false, false),
+      trn ? PP2_K(kResidentShortSteps, 1, true, true)
+          : tc == 1 ? PP2_K(kResidentShortSteps, 1, true, false) : PP2_K(kResidentShortSteps, 2, true, false),
+      trn ? PP2_K(kResidentMaxSteps, 1, true, true)
+          : tc == 1 ? PP2_K(kResidentMaxSteps, 1, true, false) : PP2_K(kResidentMaxSteps, 2, true, false)};
+#undef PP2_K
+  const int ai = trn ? 8 : 4 * (tc - 1);
   int nb = 1 << 30;
   for (int k = 0; k < 4; ++k) {
-    allow_lds(ks[k], attr[4 * (tc - 1) + k]);
+    allow_lds(ks[k], attr[ai + k]);
     int n1 = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n1, ks[k], (int)threads, lds) != hipSuccess ||
         n1 < 1) {
@@ -1130,6 +1182,7 @@ static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPla
   }
   p->rt = rt;
   p->tc = tc;
+  p->tr = trn;
   p->ntiles = (g.rows + rt - 1) / rt * tc;
   p->threads = (int)threads;
   p->lds = lds;
@@ -1147,8 +1200,13 @@ static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPla
 // fit (tc_pref 2).  A 256-row share of the 2048^2 grid (its 512-row view)
 // then runs 4 x 1024 tiles instead of 2 x 2048: 4.89 vs 5.03 us per step
 // (tools/ab_tile_cols.py).
-bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref) {
-  ResidentPlan p1, p2;
+bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref, bool allow_tr) {
+  ResidentPlan p1, p2, pt;
+  if (tc_pref == 3 && allow_tr && g.rows % 256 == 0 &&
+      resident_plan_tc(transposed_geom(g), E, ncus, 1, &pt, true)) {
+    *p = pt;
+    return true;
+  }
   const bool ok1 = resident_plan_tc(g, E, ncus, 1, &p1);
   const bool ok2 = tc_pref != 1 && resident_plan_tc(g, E, ncus, 2, &p2);
   // (automatic only with 1024-column tiles or wider: the measured shape, whose
@@ -1163,7 +1221,7 @@ bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref)
 
 hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const ResidentRun& a) {
   if (a.n < 1 || a.n > kResidentMaxSteps || a.ntiles != p.ntiles || a.rt != p.rt || a.tc != p.tc ||
-      a.depth < 1 || a.depth > kResidentRing - 2 || a.own0 < 0 || a.own1 > a.g.rows ||
+      a.depth < 1 || a.depth > kResidentRing - 2 || a.own0 < 0 || a.own1 > (p.tr ? a.g.wp : a.g.rows) ||
       a.own0 >= a.own1 || a.b_out == a.b_in || a.j_out == a.j_in ||
       (a.in_partials && a.in_partials == a.out_partials))
     return hipErrorInvalidValue;
@@ -1172,25 +1230,29 @@ hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const Res
   if (a.red_lds && (a.shard != 2 || a.kstep0 != 0 || a.nparts > kResRedFloats || lds > kDictLdsMaxBytes))
     return hipErrorInvalidValue;
   const bool lag = a.shard == 2;
-#define PP2_RES_LAUNCH(CAPV, TCV)                                                              \
-  do {                                                                                         \
-    if (lag)                                                                                   \
-      hipLaunchKernelGGL((k_loop_resident<CAPV, TCV, true>), dim3(p.ntiles), dim3(p.threads), \
-                         lds, st, h, tr);                                                      \
-    else                                                                                       \
-      hipLaunchKernelGGL((k_loop_resident<CAPV, TCV, false>), dim3(p.ntiles), dim3(p.threads), \
-                         lds, st, h, tr);                                                      \
+  if (p.tr && (p.tc != 1 || !a.shard || a.own0 % 4 != 0 || a.own1 % 4 != 0 || a.ows < a.g.rows))
+    return hipErrorInvalidValue;
+#define PP2_RES_LAUNCH(CAPV, TCV, TRV)                                                           \
+  do {                                                                                           \
+    if (lag)                                                                                     \
+      hipLaunchKernelGGL((k_loop_resident<CAPV, TCV, true, TRV>), dim3(p.ntiles),                \
+                         dim3(p.threads), lds, st, h, tr);                                       \
+    else                                                                                         \
+      hipLaunchKernelGGL((k_loop_resident<CAPV, TCV, false, TRV>), dim3(p.ntiles),               \
+                         dim3(p.threads), lds, st, h, tr);                                       \
   } while (0)
   if (a.n <= kResidentShortSteps) {
     Trajectory<kResidentShortSteps> tr{};
     std::memcpy(tr.uz, a.uz, (size_t)a.n);
-    if (p.tc == 1) PP2_RES_LAUNCH(kResidentShortSteps, 1);
-    else PP2_RES_LAUNCH(kResidentShortSteps, 2);
+    if (p.tr) PP2_RES_LAUNCH(kResidentShortSteps, 1, true);
+    else if (p.tc == 1) PP2_RES_LAUNCH(kResidentShortSteps, 1, false);
+    else PP2_RES_LAUNCH(kResidentShortSteps, 2, false);
   } else {
     Trajectory<kResidentMaxSteps> tr;
     std::memcpy(tr.uz, a.uz, sizeof tr.uz);
-    if (p.tc == 1) PP2_RES_LAUNCH(kResidentMaxSteps, 1);
-    else PP2_RES_LAUNCH(kResidentMaxSteps, 2);
+    if (p.tr) PP2_RES_LAUNCH(kResidentMaxSteps, 1, true);
+    else if (p.tc == 1) PP2_RES_LAUNCH(kResidentMaxSteps, 1, false);
+    else PP2_RES_LAUNCH(kResidentMaxSteps, 2, false);
   }
 #undef PP2_RES_LAUNCH
   return hipGetLastError();

@@ -947,7 +947,8 @@ static bool resident_plan_for(pp2_ctx* c, int e) {
     c->res_view_e = e;
     c->res_ok = false;
     pp2::ResidentPlan p;
-    if (!pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p, c->res_tc_pref))
+    if (!pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p, c->res_tc_pref,
+                            e > 0 && e % 4 == 0 && c->g.rows % 4 == 0))
       return false;
     c->res_plan = p;
     c->res_ok = true;
@@ -1194,12 +1195,13 @@ static int solve_resident(pp2_ctx* c, int max_sweeps, double thresh, int* sweeps
 // exchange rows, whose tag bits could match: the loop region is cleared and
 // its slot uses restart, as in freshly allocated buffers.
 static int run_common(pp2_ctx* c, const pp2::ResidentPlan& p, pp2::ResidentRun& a) {
-  if (c->res_loop_tc != 0 && c->res_loop_tc != p.tc) {
+  const int layout = p.tc + (p.tr ? 16 : 0);  // (transposed tiles: another granule layout)
+  if (c->res_loop_tc != 0 && c->res_loop_tc != layout) {
     HIPCHK(hipMemsetAsync(c->res_xch, 0,
                           pp2::resident_xch_floats(c->g, c->res_ntiles) * sizeof(float), c->stream));
     c->res_slot[0] = c->res_slot[1] = 0;
   }
-  c->res_loop_tc = p.tc;
+  c->res_loop_tc = layout;
   a.gamma = c->gamma;
   a.E = c->dict_n;
   a.rows = c->d_rows;
@@ -1351,7 +1353,9 @@ int pp2rt::shard_resident_e(pp2_ctx* c) {
   int e = shard_resident_depth(c);
   for (; e >= 1; --e) {
     pp2::ResidentPlan p;
-    if (pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p, c->res_tc_pref)) break;
+    if (pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p, c->res_tc_pref,
+                           e % 4 == 0 && c->g.rows % 4 == 0))
+      break;
   }
   c->res_e_dict = c->dict_n;
   c->res_e = e;
@@ -1412,7 +1416,8 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
   if (m < 1 || m > e || !shard_resident_ready(c, e))
     return set_err(PP2_ESTATE, "shard resident plan lost");
   const pp2::ResidentPlan& p = c->res_plan;
-  const Geom gv = view_geom(c, e);
+  // (transposed tiles: the kernel's grid is the view transposed, HBM is not)
+  const Geom gv = p.tr ? pp2::transposed_geom(view_geom(c, e)) : view_geom(c, e);
   const long long sh = (long long)e * c->g.wp;
   const int bc = c->bcur, jc = c->jcur;
   const int nparts = pp2::mass_partials(gv, 4);
@@ -1433,6 +1438,7 @@ int pp2rt::shard_resident_launch(pp2_ctx* c, int e, int m, const uint8_t* us, co
   a.nparts = nparts;
   a.own0 = e;
   a.own1 = e + c->g.rows;
+  a.ows = c->g.wp;
   a.shard = c->shard_lag ? 2 : 1;
   a.red_lds = a.shard == 2 && nparts <= pp2::kResRedFloats &&
               p.lds + (size_t)pp2::kResRedFloats * sizeof(float) <= pp2::kDictLdsMaxBytes;
@@ -1643,7 +1649,7 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
       c->res_plan_e = c->sol_plan_e = c->res_e_dict = -1;
       return PP2_OK;
     case PP2_TUNE_RESIDENT_TILE_COLS:
-      if (value < 0 || value > 2) return set_err(PP2_EINVAL, "tile columns %d not in [0, 2]", value);
+      if (value < 0 || value > 3) return set_err(PP2_EINVAL, "tile columns %d not in [0, 3]", value);
       c->res_tc_pref = value;
       c->res_plan_e = c->res_e_dict = -1;
       return PP2_OK;
@@ -1922,7 +1928,7 @@ int pp2_resident_tiling(pp2_ctx* c, int* tiles, int* rows_per_tile, int* tile_co
   }
   if (tiles) *tiles = ok ? c->res_plan.ntiles : 0;
   if (rows_per_tile) *rows_per_tile = ok ? c->res_plan.rt : 0;
-  if (tile_cols) *tile_cols = ok ? c->res_plan.tc : 0;
+  if (tile_cols) *tile_cols = ok ? (c->res_plan.tr ? 3 : c->res_plan.tc) : 0;
   return PP2_OK;
 }
 

@@ -262,7 +262,7 @@ def test_rccl_single_rank_step_pairs():
 
 
 # ------------------------------------------------- row shards on the resident loop
-def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True):
+def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True, tiling=0):
     """pp2_shard_group_loop_run on the resident kernel (one launch per halo
     block of up to e steps on the view of the owned rows plus e halo rows per
     side, power-of-two rescaling inside, rebased at each exchange) against
@@ -277,6 +277,8 @@ def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True):
         grp.model_generate()
         if halo:
             grp.set_tuning(P.GridContext.TUNE_RESIDENT_HALO, halo)
+        if tiling:
+            grp.set_tuning(P.GridContext.TUNE_RESIDENT_TILE_COLS, tiling)
         e = grp.loop_steps_per_launch()
         assert len(set(e)) == 1 and e[0] >= 2, e
         for c in (ref, grp):
@@ -311,16 +313,18 @@ def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True):
         return e[0]
 
 
-def test_shard_group_resident_config4():
+@pytest.mark.parametrize("tiling", [0, 3])
+def test_shard_group_resident_config4(tiling):
     """BASELINE configs[3]'s per-rank geometry: the 2048^2 grid in 8 row shards
     of 256 rows (one device here), each shard's run on the resident kernel
-    (view 256 + 2e rows, e = 128: 256 tiles of 2 x 2048 cells)."""
+    (view 256 + 2e rows, e = 128: 256 tiles of 4 x 1024 cells, or -- tiling
+    3 -- 256 transposed tiles of 8 grid columns x the 512 view rows)."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S
     N = 2048
     grid = S.synth_grid(N, N, N)
     e = _resident_shard_run(P, grid, S.synth_goal(grid), tuple(range(0, N + 1, N // 8)),
-                            ((0, 30), (30, 41)), mixed=False)
+                            ((0, 30), (30, 41)), mixed=tiling == 3, tiling=tiling)
     assert e == 128
 
 
@@ -378,7 +382,8 @@ def test_rccl_single_rank_resident_896x1024():
         assert sh.resident_launches()[0] == 4
 
 
-def test_rccl_single_rank_resident_256x2048():
+@pytest.mark.parametrize("tiling", [0, 3])
+def test_rccl_single_rank_resident_256x2048(tiling):
     """The RCCL path of a 256 x 2048 shard -- the per-rank share of the
     2048^2 grid at 8 ranks -- with a 1-rank communicator: pp2_loop_run takes
     the resident shard path (e = 128: 512-row view, exchanges, {mass, shift}
@@ -392,13 +397,16 @@ def test_rccl_single_rank_resident_256x2048():
     with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
             P.GridContext(grid, goal, gamma=float(GAMMA), rows=(0, 256)) as sh:
         sh.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
+        if tiling:
+            sh.set_tuning(sh.TUNE_RESIDENT_TILE_COLS, tiling)
         for c in (ref, sh):
             c.model_generate()
             c.belief_set(b0)
             c.mdp_reset()
         assert sh.loop_steps_per_launch() == 128
-        # the 512-row view runs 2-D tiles (4 x 1024, two tile columns)
-        assert sh.resident_tiling() == (256, 4, 2)
+        # the 512-row view runs 2-D tiles (4 x 1024, two tile columns), or
+        # transposed tiles (8 grid columns x 512 view rows)
+        assert sh.resident_tiling() == ((256, 8, 3) if tiling == 3 else (256, 4, 2))
         for lo, hi in ((0, 17), (17, 300)):
             ref.loop_run(us[lo:hi], zs[lo:hi])
             sh.loop_run(us[lo:hi], zs[lo:hi])

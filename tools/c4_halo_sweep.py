@@ -27,14 +27,10 @@ def main():
     b0 = S.uniform_belief(grid)
     r0, r1 = 3 * G // 8, 4 * G // 8
     stream = torch.cuda.Stream()
-    halos = [int(x) for x in os.environ.get("PP2_HALOS", "128,96,64,48,32").split(",")]
-    tcs = [int(x) for x in os.environ.get("PP2_TCS", "0,1,2").split(",")]
-    # normalisation block depths (PP2_TUNE_NORM_BLOCK) at the first halo and
-    # tiling: what a block start costs inside the shard's resident launch
-    norms = [int(x) for x in os.environ.get("PP2_NORMS", "8,4").split(",")]
-    # (e, tile columns, norm block, lagged shard block starts)
-    cases = [(e_req, tc, 0, 1) for e_req in halos for tc in tcs]
-    cases += [(e_req, 0, nb, lag) for e_req in (halos[0], 64) for nb in norms for lag in (0, 1)]
+    # cases "e:tile cols:norm block:lag" (PP2_TUNE_RESIDENT_HALO, _TILE_COLS --
+    # 3 = transposed tiles --, _NORM_BLOCK (0: default 8), _SHARD_LAG)
+    spec = os.environ.get("PP2_CASES", "128:0:0:0,128:3:0:0,128:3:0:1,128:3:4:0,64:2:0:0,128:0:0:0")
+    cases = [tuple(int(v) for v in c.split(":")) for c in spec.split(",")]
     for e_req, tc, nb, lag in cases:
         if True:
             ctx = P.GridContext(grid, goal, gamma=bench.GAMMA, device=0, rows=(r0, r1))
@@ -51,6 +47,7 @@ def main():
             ctx.mdp_reset()
             ctx.synchronize()
             e = ctx.loop_steps_per_launch()
+            tiling = ctx.resident_tiling()
             ts = []
             for rep in range(3):
                 ctx.loop_run(us[:w], zs[:w])
@@ -63,7 +60,7 @@ def main():
             t = float(np.median(ts))
             rounds = -(-k // e) + 1 if e > 0 else 0
             proj = [t + rounds * r / k for r in bench.RCCL_ROUND_US]
-            print(f"e_req {e_req:4d} tc {tc} norm {nb or 8} lag {lag} -> e {e:4d}: {t:6.3f} us/step "
+            print(f"e_req {e_req:4d} tc {tc} norm {nb or 8} lag {lag} -> e {e:4d} tiling {tiling}: {t:6.3f} us/step "
                   f"(runs {', '.join(f'{x:.3f}' for x in ts)}), rounds {rounds}, "
                   f"projection {proj[0]:.3f}-{proj[1]:.3f} us/step", flush=True)
 

@@ -15,7 +15,8 @@ PP2_REF=1 PP2_STEPS=100 timeout -k 10 120 python3 tools/prof_planner.py > $O/r04
 cat $O/r04_plan3.log
 timeout -k 10 300 python3 tools/c4_halo_sweep.py > $O/r04_c4halo.txt 2>&1 || { cat $O/r04_c4halo.txt; exit 1; }
 cat $O/r04_c4halo.txt
-timeout -k 10 60 tools/micro/copy_bw > $O/r04_copy_bw2.txt 2>&1
+timeout -k 10 60 tools/micro/copy_bw > $O/r04_copy_bw2.txt 2>&1 || { cat $O/r04_copy_bw2.txt; exit 1; }
+PP2_REF=1 PP2_STEPS=30 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_plan4 -o run -- python3 tools/prof_planner.py > $O/r04_prof_plan4.log 2>&1
 rc=$?
 cat $O/r04_copy_bw2.txt
 exit $rc
