@@ -177,14 +177,19 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           transposed).  Values and actions are bit-identical
  *                           either way, beliefs equal to rounding. */
 #define PP2_TUNE_RESIDENT_TILE_COLS 12
-/*  PP2_TUNE_SHARD_LAG       row shards' resident launches: 1 (default) = a
+/*  PP2_TUNE_SHARD_LAG       row shards' resident launches: 0 (default) = a
  *                           normalisation block start inside a launch scales
- *                           the view by the power of two chosen from its mass
- *                           one block earlier (already reduced: no grid-wide
- *                           wait); 0 = from the previous step's mass, after
- *                           every tile of the view has arrived.  Beliefs equal
- *                           each other to rounding (power-of-two scales are
- *                           exact); values and actions are bit-identical. */
+ *                           the view by the power of two chosen from the
+ *                           previous step's mass, after every tile of the view
+ *                           has arrived; 1 = from its mass one block earlier
+ *                           (staged in LDS ahead of time: no grid-wide wait,
+ *                           no barrier).  Measured on the 2-D tiles of the
+ *                           config-4 rank share the waited block start costs
+ *                           nothing visible and the lagged one's extra state
+ *                           ~0.2 us per step, so it is off by default; on
+ *                           transposed tiles it is the faster one.  Beliefs
+ *                           equal each other to rounding (power-of-two scales
+ *                           are exact); values and actions are bit-identical. */
 #define PP2_TUNE_SHARD_LAG 13
 /*  Diagnostics (tests):
  *  PP2_TUNE_RESIDENT_CUS    plan resident launches for at most this many CUs

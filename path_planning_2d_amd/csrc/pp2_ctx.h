@@ -181,7 +181,7 @@ struct pp2_ctx {
   // row shards on the resident loop: halo depth per resident
   // launch, the run's power-of-two shift and the {mass, shift} rank vector
   int res_halo = 0;                // PP2_TUNE_RESIDENT_HALO (0: the most the shards allow)
-  int shard_lag = 1;               // PP2_TUNE_SHARD_LAG (resident shard block starts)
+  int shard_lag = 0;               // PP2_TUNE_SHARD_LAG (resident shard block starts)
   int min_shard_rows = 0;          // smallest shard of the grid (comm init / group create)
   int res_view_e = -1;             // view extension the plan below was made for
   int res_e = 0, res_e_dict = -1;  // shard_resident_e's answer and the dictionary it is for

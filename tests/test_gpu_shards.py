@@ -262,7 +262,7 @@ def test_rccl_single_rank_step_pairs():
 
 
 # ------------------------------------------------- row shards on the resident loop
-def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True, tiling=0):
+def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True, tiling=0, lag=0):
     """pp2_shard_group_loop_run on the resident kernel (one launch per halo
     block of up to e steps on the view of the owned rows plus e halo rows per
     side, power-of-two rescaling inside, rebased at each exchange) against
@@ -279,6 +279,8 @@ def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True, tilin
             grp.set_tuning(P.GridContext.TUNE_RESIDENT_HALO, halo)
         if tiling:
             grp.set_tuning(P.GridContext.TUNE_RESIDENT_TILE_COLS, tiling)
+        if lag:
+            grp.set_tuning(P.GridContext.TUNE_SHARD_LAG, lag)
         e = grp.loop_steps_per_launch()
         assert len(set(e)) == 1 and e[0] >= 2, e
         for c in (ref, grp):
@@ -313,24 +315,25 @@ def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True, tilin
         return e[0]
 
 
-@pytest.mark.parametrize("tiling", [0, 3])
-def test_shard_group_resident_config4(tiling):
+@pytest.mark.parametrize("tiling,lag", [(0, 0), (3, 0), (0, 1), (3, 1)])
+def test_shard_group_resident_config4(tiling, lag):
     """BASELINE configs[3]'s per-rank geometry: the 2048^2 grid in 8 row shards
     of 256 rows (one device here), each shard's run on the resident kernel
     (view 256 + 2e rows, e = 128: 256 tiles of 4 x 1024 cells, or -- tiling
-    3 -- 256 transposed tiles of 8 grid columns x the 512 view rows)."""
+    3 -- 256 transposed tiles of 8 grid columns x the 512 view rows), with
+    block starts waited for or lagged (PP2_TUNE_SHARD_LAG)."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S
     N = 2048
     grid = S.synth_grid(N, N, N)
     e = _resident_shard_run(P, grid, S.synth_goal(grid), tuple(range(0, N + 1, N // 8)),
-                            ((0, 30), (30, 41)), mixed=tiling == 3, tiling=tiling)
+                            ((0, 30), (30, 41)), mixed=tiling == 3, tiling=tiling, lag=lag)
     assert e == 128
 
 
-@pytest.mark.parametrize("bounds,halo", [((0, 256, 512), 0), ((0, 200, 512), 6),
-                                         ((0, 128, 300, 512), 9)])
-def test_shard_group_resident_blocks(bounds, halo):
+@pytest.mark.parametrize("bounds,halo,lag", [((0, 256, 512), 0, 0), ((0, 200, 512), 6, 0),
+                                             ((0, 128, 300, 512), 9, 0), ((0, 200, 512), 0, 1)])
+def test_shard_group_resident_blocks(bounds, halo, lag):
     """Uneven shards, several halo blocks per call (e = 6, 9: in-kernel
     power-of-two block starts every 8 steps, rebases at every exchange),
     calls ending mid-block, then per-step drivers on the same state."""
@@ -338,7 +341,7 @@ def test_shard_group_resident_blocks(bounds, halo):
     from path_planning_2d_amd import synthetic as S
     grid = S.synth_grid(512, 1024, 7)
     e = _resident_shard_run(P, grid, S.synth_goal(grid), bounds,
-                            ((0, 2), (2, 19), (19, 40)), halo=halo)
+                            ((0, 2), (2, 19), (19, 40)), halo=halo, lag=lag)
     assert e == (halo or 128)
 
 
