@@ -174,14 +174,40 @@ def sweep_resident_traffic(cells):
                      "of granules per tile through the fabric/MALL (DESIGN.md §5)"}
 
 
-def cpu_threads():
-    """Host threads for the CPU baseline: every core of this process's
-    affinity mask (os.sched_getaffinity), i.e. all host cores the run may
-    use; the count is reported as cpu_baseline.cores."""
+def cgroup_cpu_quota():
+    """The CPU bandwidth this process's cgroup grants, in cores (quota /
+    period; cgroup v2 cpu.max or v1 cpu.cfs_quota_us), or None when unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) // int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return max(1, q // p) if q > 0 and p > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_affinity():
     try:
         return max(1, len(os.sched_getaffinity(0)))
     except (AttributeError, OSError):
         return max(1, os.cpu_count() or 1)
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline: every core this process may use --
+    its affinity mask (os.sched_getaffinity), capped by its cgroup's CPU
+    quota (on the GPU box the mask lists the whole machine while the quota
+    grants a share; threads beyond the quota only time-slice).  Reported as
+    cpu_baseline.cores, with both inputs beside it."""
+    q = cgroup_cpu_quota()
+    a = cpu_affinity()
+    return min(a, q) if q else a
 
 
 def cpu_baseline(grid, goal, us, zs, budget_s):
@@ -259,7 +285,9 @@ def cpu_baseline(grid, goal, us, zs, budget_s):
                       f"({single['sample']})",
             "single_thread": single,
             "cpu": cpu_model(), "host_cpus": os.cpu_count(),
-            "cores_source": "len(os.sched_getaffinity(0)) (every core this process may run on)",
+            "cores_source": "min(len(os.sched_getaffinity(0)), cgroup CPU quota): every core "
+                            "this process may run on, capped by the cores its cgroup grants",
+            "affinity_cores": cpu_affinity(), "cgroup_quota_cores": cgroup_cpu_quota(),
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
