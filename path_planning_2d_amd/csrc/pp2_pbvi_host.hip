@@ -290,9 +290,16 @@ __global__ __launch_bounds__(256) void k_rows_div(float* __restrict__ A, int ld,
 }
 
 // ---------------------------------------------------------------- pair chains
-// 64 A rows x 64 B rows per 256-thread block; thread (la, jg) keeps the 16
-// chains (la, 16 jg + m).  A is staged transposed ([x][row]: lane-contiguous
-// reads), B row-major (wave-uniform broadcast reads).
+// TA A rows x TB = (256 / TA) * NC B rows per 256-thread block; thread (la =
+// tid % TA, jg = tid / TA) keeps the NC chains (la, jg * NC + m), each one
+// x-ordered fp32 chain (multiply then add, or |a - b| then add).  A is staged
+// transposed ([x][row]: the lanes of one la read one word), B row-major.
+// Two shapes: 64 x 64 pairs per block with 16 chains per thread for many
+// pairs (ILP), 16 x 16 with one chain per thread and 128-value chunks when
+// the pair grid is small (the planner's reference-order PBVI bounds: 144
+// children x S = 500 alphas give 24 blocks of the large shape for 256 CUs,
+// 288 of the small one; measured 2 and 4 chains per thread ran 1.3x and 1.9x
+// slower there).
 template <int OP>
 __device__ __forceinline__ float pair_step(float acc, float a, float b) {
   if constexpr (OP == PAIR_L1)
@@ -301,42 +308,66 @@ __device__ __forceinline__ float pair_step(float acc, float a, float b) {
     return acc + a * b;
 }
 
-constexpr int kPairChunk = 32;
-
-template <int OP>
+// CH x-values per chunk; the next chunk's loads are issued into registers
+// before the current chunk's chains run (one global round trip per chunk
+// would otherwise bound the small shape: 2048 chunks x ~1 us at 256^2).
+template <int OP, int TA, int NC, int CH>
 __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A, int na,
                                                     const float* __restrict__ B, int nb, int ld,
                                                     int n, float* __restrict__ out, int ldo) {
-  __shared__ float sAT[kPairChunk][64 + 1];
-  __shared__ __attribute__((aligned(16))) float sB[64][kPairChunk + 4];
-  const int tid = threadIdx.x, la = tid & 63, jg = tid >> 6;
-  const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
-  float acc[16];
+  constexpr int G = 256 / TA, TB = G * NC;
+  constexpr int kRowVec = CH / 4;                      // float4 per row of a chunk
+  constexpr int LA = (TA * kRowVec + 255) / 256;       // float4 loads per thread
+  constexpr int LB = (TB * kRowVec + 255) / 256;
+  __shared__ float sAT[CH][TA + 1];
+  __shared__ __attribute__((aligned(16))) float sB[TB][CH + 4];
+  const int tid = threadIdx.x, la = tid % TA, jg = tid / TA;
+  const int i0 = blockIdx.x * TA, j0 = blockIdx.y * TB;
+  float acc[NC];
 #pragma unroll
-  for (int m = 0; m < 16; ++m) acc[m] = 0.0f;
-  for (int x0 = 0; x0 < n; x0 += kPairChunk) {
-    constexpr int kRowVec = kPairChunk / 4;  // float4 per row of the chunk
+  for (int m = 0; m < NC; ++m) acc[m] = 0.0f;
+  f4 ra[LA], rb[LB];
+  auto fetch = [&](int x0) {  // this thread's share of the chunk at x0 (zeros past n)
 #pragma unroll
-    for (int q = 0; q < 64 * kRowVec / 256; ++q) {
+    for (int q = 0; q < LA; ++q) {
+      const int e = tid + 256 * q, row = e / kRowVec, c4 = (e % kRowVec) * 4, ia = i0 + row;
+      ra[q] = e < TA * kRowVec && ia < na && x0 + c4 < n
+                  ? *(const f4*)(A + (long long)ia * ld + x0 + c4) : f4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int q = 0; q < LB; ++q) {
+      const int e = tid + 256 * q, row = e / kRowVec, c4 = (e % kRowVec) * 4, jb = j0 + row;
+      rb[q] = e < TB * kRowVec && jb < nb && x0 + c4 < n
+                  ? *(const f4*)(B + (long long)jb * ld + x0 + c4) : f4{0, 0, 0, 0};
+    }
+  };
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int q = 0; q < LA; ++q) {
       const int e = tid + 256 * q, row = e / kRowVec, c4 = (e % kRowVec) * 4;
-      const int ia = i0 + row, jb = j0 + row;
-      const f4 va = ia < na ? *(const f4*)(A + (long long)ia * ld + x0 + c4) : f4{0, 0, 0, 0};
-      const f4 vb = jb < nb ? *(const f4*)(B + (long long)jb * ld + x0 + c4) : f4{0, 0, 0, 0};
-      sAT[c4 + 0][row] = va.x;
-      sAT[c4 + 1][row] = va.y;
-      sAT[c4 + 2][row] = va.z;
-      sAT[c4 + 3][row] = va.w;
-      *(f4*)&sB[row][c4] = vb;
+      if (e < TA * kRowVec) {
+        sAT[c4 + 0][row] = ra[q].x;
+        sAT[c4 + 1][row] = ra[q].y;
+        sAT[c4 + 2][row] = ra[q].z;
+        sAT[c4 + 3][row] = ra[q].w;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < LB; ++q) {
+      const int e = tid + 256 * q, row = e / kRowVec, c4 = (e % kRowVec) * 4;
+      if (e < TB * kRowVec) *(f4*)&sB[row][c4] = rb[q];
     }
     __syncthreads();
-    const int m = min(kPairChunk, n - x0);
+    if (x0 + CH < n) fetch(x0 + CH);  // in flight during this chunk's chains
+    const int m = min(CH, n - x0);
     int xx = 0;
     for (; xx + 4 <= m; xx += 4) {
       const float a0 = sAT[xx][la], a1 = sAT[xx + 1][la], a2 = sAT[xx + 2][la],
                   a3 = sAT[xx + 3][la];
 #pragma unroll
-      for (int mm = 0; mm < 16; ++mm) {
-        const f4 b = *(const f4*)&sB[jg * 16 + mm][xx];
+      for (int mm = 0; mm < NC; ++mm) {
+        const f4 b = *(const f4*)&sB[jg * NC + mm][xx];
         float v = acc[mm];
         v = pair_step<OP>(v, a0, b.x);
         v = pair_step<OP>(v, a1, b.y);
@@ -348,14 +379,14 @@ __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A,
     for (; xx < m; ++xx) {
       const float av = sAT[xx][la];
 #pragma unroll
-      for (int mm = 0; mm < 16; ++mm) acc[mm] = pair_step<OP>(acc[mm], av, sB[jg * 16 + mm][xx]);
+      for (int mm = 0; mm < NC; ++mm) acc[mm] = pair_step<OP>(acc[mm], av, sB[jg * NC + mm][xx]);
     }
     __syncthreads();
   }
   if (i0 + la < na) {
 #pragma unroll
-    for (int mm = 0; mm < 16; ++mm) {
-      const int j = j0 + jg * 16 + mm;
+    for (int mm = 0; mm < NC; ++mm) {
+      const int j = j0 + jg * NC + mm;
       if (j < nb) out[(long long)(i0 + la) * ldo + j] = acc[mm];
     }
   }
@@ -698,13 +729,27 @@ hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float
 hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, const float* B,
                              int nb, int ld, int n, float* out, int ldo) {
   if (na <= 0 || nb <= 0) return hipSuccess;
-  dim3 grid(cdiv(na, 64), cdiv(nb, 64));
-  if (op == PAIR_L1)
-    hipLaunchKernelGGL(k_pair_chain<PAIR_L1>, grid, dim3(256), 0, st, A, na, B, nb, ld, n, out,
-                       ldo);
-  else
-    hipLaunchKernelGGL(k_pair_chain<PAIR_DOT>, grid, dim3(256), 0, st, A, na, B, nb, ld, n, out,
-                       ldo);
+  // the large shape while it gives the CUs a block each, else the small one
+#ifndef PP2_PAIR_NC  // (A/B builds: chains per thread of the small shape)
+#define PP2_PAIR_NC 1
+#endif
+#ifndef PP2_PAIR_CH
+#define PP2_PAIR_CH 128
+#endif
+  constexpr int kNc = PP2_PAIR_NC, kCh = PP2_PAIR_CH;
+  const bool big = (long long)cdiv(na, 64) * cdiv(nb, 64) >= 256;
+  const dim3 grid = big ? dim3(cdiv(na, 64), cdiv(nb, 64)) : dim3(cdiv(na, 16), cdiv(nb, 16 * kNc));
+#define PP2_PAIR(OPV, TAV, NCV, CHV)                                                        \
+  hipLaunchKernelGGL((k_pair_chain<OPV, TAV, NCV, CHV>), grid, dim3(256), 0, st, A, na, B, nb, ld, \
+                     n, out, ldo)
+  if (op == PAIR_L1) {
+    if (big) PP2_PAIR(PAIR_L1, 64, 16, 32);
+    else PP2_PAIR(PAIR_L1, 16, kNc, kCh);
+  } else {
+    if (big) PP2_PAIR(PAIR_DOT, 64, 16, 32);
+    else PP2_PAIR(PAIR_DOT, 16, kNc, kCh);
+  }
+#undef PP2_PAIR
   return hipGetLastError();
 }
 

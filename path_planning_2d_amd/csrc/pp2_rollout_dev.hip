@@ -461,7 +461,10 @@ int band_gx(const Geom& g) { return (band_nseg(g) * band_nband(g) + 3) / 4; }
 // Band shape: 4 copies per chunk, 4 LDS ring slots, 2 waves per SIMD.  The
 // other shapes measured (MI355X, 512^2 x 4096 copies x 5 steps): (4,4,2) 6.01
 // ms, (4,3,2) 6.21, (2,4,3) 6.25, (8,3,1) 6.36, (4,4,3) 6.20.
-constexpr int kBandCopies = 4, kBandSlots = 4, kBandWaves = 2;
+#ifndef PP2_BAND_SLOTS  // (A/B builds: EXTRA_FLAGS=-DPP2_BAND_SLOTS=n)
+#define PP2_BAND_SLOTS 4
+#endif
+constexpr int kBandCopies = 4, kBandSlots = PP2_BAND_SLOTS, kBandWaves = 2;
 
 }  // namespace
 
