@@ -360,10 +360,13 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
   const int n = a.n, nch = fc_chunks(n), nseg = fc_segments(n);
   const uint2* tab = a.tab + (long long)ch * nch;
   const bool cdf = BASE == FC_ROW && K == 0 && a.cdf != nullptr;
+  const unsigned long long tk0 = a.stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  unsigned long long tk1 = 0ull, tk2 = 0ull;
   uint32_t f = 0u;
   for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)ch * nseg + s];
   f = (__ballot((f & kPos) != 0u) ? kPos : 0u) | (__ballot((f & kNeg) != 0u) ? kNeg : 0u) |
       (__ballot((f & kBad) != 0u) ? kBad : 0u);
+  if (a.stats) tk1 = __builtin_amdgcn_s_memrealtime();
   const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
   const bool neg = (f & kNeg) && !(f & kPos);
   if (cdf && lane == 0) a.cst[nch] = make_int2((int)f, 0);
@@ -423,6 +426,7 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
             *reinterpret_cast<f4a*>(&sStash[s2][4 * lane]) =
                 f4a{fabsf(st[s2][0]), fabsf(st[s2][1]), fabsf(st[s2][2]), fabsf(st[s2][3])};
         __syncthreads();
+        if (a.stats && tk2 == 0ull) tk2 = __builtin_amdgcn_s_memrealtime();
       }
       const int jj = j + lane;
       const uint2 e = jj < nch && jj < wbase + kFcWin ? sE[jj - wbase] : make_uint2(kNoEntry, 0u);
@@ -462,10 +466,16 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
       }
     }
     if (a.stats && lane == 0) {
+      const unsigned long long tk3 = __builtin_amdgcn_s_memrealtime();
       atomicAdd(a.stats + 0, n_it);
       atomicAdd(a.stats + 1, n_fb);
       atomicAdd(a.stats + 2, n_rounds);
       atomicAdd(a.stats + 3, n_hit);
+      // 100 MHz ticks: flags, first window + stash, the walk; chains
+      atomicAdd(a.stats + 4, (int)(tk1 - tk0));
+      atomicAdd(a.stats + 5, (int)(tk2 - tk1));
+      atomicAdd(a.stats + 6, (int)(tk3 - tk2));
+      atomicAdd(a.stats + 7, 1);
     }
     const float r = value_of(E, k);
     res = neg ? (r == 0.0f ? 0.0f : -r) : r;
@@ -676,8 +686,10 @@ extern "C" int pp2_debug_fchain_row(int n, const float* x, const float* partners
                                     float* out, float* cdf) {
   return pp2_debug_fchain_row2(n, x, partners, K, out, cdf, nullptr, nullptr);
 }
-// (stats: the driver's {iterations, fallback chunks, exact rounds, stash
-// hits}; ms: the chain set's event time, median of 5 runs after a warm-up)
+// (stats[8]: the driver's {iterations, fallback chunks, exact rounds, stash
+// hits}, summed over its chains, then 100 MHz ticks summed over the chains
+// in {flags, first window + stash, the walk} and the chains; ms: the chain
+// set's event time, median of 5 runs after a warm-up)
 extern "C" int pp2_debug_fchain_row2(int n, const float* x, const float* partners, int K,
                                      float* out, float* cdf, int* stats, float* ms) {
   if (n < 0 || !x || !out || (K != 0 && K != 9) || (K == 9 && !partners) || (cdf && K != 0))
@@ -713,8 +725,8 @@ extern "C" int pp2_debug_fchain_row2(int n, const float* x, const float* partner
     a.cdf = dcdf;
     scr.attach(&a);
     int* dstats = nullptr;
-    if (stats && ok(hipMalloc(&dstats, 4 * sizeof(int))) &&
-        ok(hipMemset(dstats, 0, 4 * sizeof(int))))
+    if (stats && ok(hipMalloc(&dstats, 8 * sizeof(int))) &&
+        ok(hipMemset(dstats, 0, 8 * sizeof(int))))
       a.stats = dstats;
     if (ms && st == 0) {
       hipEvent_t e0, e1;
@@ -741,7 +753,7 @@ extern "C" int pp2_debug_fchain_row2(int n, const float* x, const float* partner
         ok(hipMemcpy(out, dout, (K == 9 ? 9 : 1) * sizeof(float), hipMemcpyDeviceToHost)) && cdf)
       ok(hipMemcpy(cdf, dcdf, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
     if (dstats) {
-      if (st == 0) ok(hipMemcpy(stats, dstats, 4 * sizeof(int), hipMemcpyDeviceToHost));
+      if (st == 0) ok(hipMemcpy(stats, dstats, 8 * sizeof(int), hipMemcpyDeviceToHost));
       (void)hipFree(dstats);
     }
   }

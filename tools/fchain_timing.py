@@ -37,15 +37,18 @@ def main():
         x = np.ascontiguousarray(x, np.float32)
         out = np.zeros(16, np.float32)
         cd = np.zeros(x.size, np.float32) if cdf else None
-        st = (C.c_int * 4)()
+        st = (C.c_int * 8)()
         ms = C.c_float()
         Pp = np.ascontiguousarray(P, np.float32) if P is not None else None
         rc = f(x.size, x.ctypes.data_as(fp), Pp.ctypes.data_as(fp) if Pp is not None else fp(),
                9 if P is not None else 0, out.ctypes.data_as(fp),
                cd.ctypes.data_as(fp) if cd is not None else fp(), st, C.byref(ms))
         assert rc == 0, rc
+        nc = max(1, st[7])
         print(f"{name:36s} {ms.value * 1e3:8.1f} us  driver: iterations {st[0]}, fallback "
-              f"chunks {st[1]}, exact rounds {st[2]}, stash hits {st[3]}", flush=True)
+              f"chunks {st[1]}, exact rounds {st[2]}, stash hits {st[3]}; per chain: flags "
+              f"{st[4] / nc / 100:.1f} us, window+stash {st[5] / nc / 100:.1f} us, walk "
+              f"{st[6] / nc / 100:.1f} us", flush=True)
 
 
 if __name__ == "__main__":
