@@ -439,12 +439,23 @@ def pbvi_bench(args, device, stream_handle, with_cpu):
                     closed_loop(grid, b0, pl.step, 3, 1e9)
                     pl.reset()
                     ms = closed_loop(grid, b0, pl.step, args.plan_steps, 1e9)
+                with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
+                                     max_online_iteration=15, lower_bound_mode=1,
+                                     reference_order=0) as pl:
+                    closed_loop(grid, b0, pl.step, 3, 1e9)
+                    pl.reset()
+                    ms_ts = closed_loop(grid, b0, pl.step, args.plan_steps, 1e9)
                 plan = {"mode": "reference_order=1 (default; bit-exact)",
                         "config": f"256x256 synthetic grid, max_search_tree_depth {args.plan_depth}, "
                                   f"max_online_iteration 15, FIB upper bound, PBVI lower bound "
                                   f"(S={args.pbvi_S}, 167 backups)",
                         "steps": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
-                        "p90_ms": float(np.percentile(ms, 90)), "mean_ms": float(ms.mean())}
+                        "p90_ms": float(np.percentile(ms, 90)), "mean_ms": float(ms.mean()),
+                        "tree_sum_variant": {
+                            "steps": int(ms_ts.size), "p50_ms": float(np.percentile(ms_ts, 50)),
+                            "p90_ms": float(np.percentile(ms_ts, 90)),
+                            "note": "opt-in reference_order=0 (PBVI dots by the split-x MFMA "
+                                    "GEMM, not the reference's x-ordered chains): NOT bit-exact"}}
             n_it = iters if iters > 0 else int(np.ceil(np.log(np.float32(1e-3) / np.float32(5))
                                                        / np.log(np.float32(GAMMA))))
             Sp = (args.pbvi_S + 127) // 128 * 128
