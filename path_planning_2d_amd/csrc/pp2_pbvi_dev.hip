@@ -40,34 +40,33 @@ __global__ __launch_bounds__(kThreads) void k_pbvi_update(
 }
 
 // The QV-tree expansion's 9 predictions of one dense belief row (the child
-// of (u, z) is pred[u] * L[z], formed by the IEEE sums of pp2_fchain.hip).
+// of (u, z) is pred[u] * L[z], formed by the IEEE sums of pp2_fchain.hip):
+// thread (cell, action u = blockIdx.y).  SPARSE (a coded model whose T rows
+// the host verified to be +0 off the base-kernel support): only the
+// action's <= 4 support taps -- the others are fmaf(+0, b, p) == p for the
+// finite b >= 0 and p != -0 of the chain -- in the same ascending-s order.
+template <bool SPARSE>
 __global__ __launch_bounds__(kThreads) void k_tree_pred(Geom g, PlaneSet T,
                                                         const float* __restrict__ b, int ld,
                                                         float* __restrict__ pred) {
   const int W = g.width, H = g.rows;
-  const int idx = blockIdx.x * kThreads + threadIdx.x;
+  const int idx = blockIdx.x * kThreads + threadIdx.x, u = blockIdx.y;
   if (idx >= H * W) return;
   const int y = idx / W, x = idx - y * W;
-  float bv[9];
-  bool in[9];
-#pragma unroll
-  for (int s = 0; s < 9; ++s) {
+  float p = 0.0f;
+  auto tap = [&](int s) {
     const int sy = y + s / 3 - 1, sx = x + s % 3 - 1;
-    in[s] = !(sy < 0 || sy >= H || sx < 0 || sx >= W);
-    bv[s] = in[s] ? b[sy * W + sx] : 0.0f;
-  }
+    if (sy < 0 || sy >= H || sx < 0 || sx >= W) return;
+    const float t = T.p[(long long)sy * T.rs + (long long)(9 * u + 8 - s) * T.ps + sx];
+    p = fmaf(t, b[sy * W + sx], p);
+  };
+  if constexpr (SPARSE) {
+    for (int j = kSupN[u] - 1; j >= 0; --j) tap(8 - kSup[u][j]);  // s ascending
+  } else {
 #pragma unroll
-  for (int u = 0; u < 9; ++u) {
-    float p = 0.0f;
-#pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      if (!in[s]) continue;
-      const int sy = y + s / 3 - 1, sx = x + s % 3 - 1;
-      const float t = T.p[(long long)sy * T.rs + (long long)(9 * u + 8 - s) * T.ps + sx];
-      p = fmaf(t, bv[s], p);
-    }
-    pred[(long long)u * ld + idx] = p;
+    for (int s = 0; s < 9; ++s) tap(s);
   }
+  pred[(long long)u * ld + idx] = p;
 }
 
 // One thread = one cell x, kGaoRows alpha vectors and 8 of the 16
@@ -131,12 +130,15 @@ hipError_t launch_pbvi_update(hipStream_t st, const Geom& g, PlaneSet T, PlaneSe
 }
 
 hipError_t launch_tree_pred(hipStream_t st, const Geom& g, PlaneSet T, const float* b, int ld,
-                            float* pred) {
+                            float* pred, bool sparse) {
   const int hw = g.rows * g.width;
   if (hw <= 0) return hipSuccess;
   if (ld < hw) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_tree_pred, dim3((hw + kThreads - 1) / kThreads), dim3(kThreads), 0, st, g,
-                     T, b, ld, pred);
+  const dim3 grid((hw + kThreads - 1) / kThreads, 9);
+  if (sparse)
+    hipLaunchKernelGGL(k_tree_pred<true>, grid, dim3(kThreads), 0, st, g, T, b, ld, pred);
+  else
+    hipLaunchKernelGGL(k_tree_pred<false>, grid, dim3(kThreads), 0, st, g, T, b, ld, pred);
   return hipGetLastError();
 }
 

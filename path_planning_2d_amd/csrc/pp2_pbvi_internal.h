@@ -171,8 +171,10 @@ hipError_t launch_store_children(hipStream_t st, const FcStoreList& L, const flo
 
 // ---- pp2_pbvi_dev.hip (FTZ): the 9 action predictions of cudaBayesBeliefUpdate
 // before the likelihood product: pred[u][idx] = sum_s T[sidx][u][8-s] * b[sidx]
-// (fmaf chain, s ascending, in-grid neighbours), b a dense row.
+// (fmaf chain, s ascending, in-grid neighbours), b a dense row; sparse: T is
+// +0 off each action's base-kernel support (the coded model's check), so
+// only the support taps are read.
 hipError_t launch_tree_pred(hipStream_t st, const Geom& g, PlaneSet T, const float* b, int ld,
-                            float* pred);
+                            float* pred, bool sparse);
 
 }  // namespace pp2

@@ -194,7 +194,7 @@ struct pp2_planner {
   pp2::FcScratch scr_main, scr_side;  // chain-set scratch of the two streams
   unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
   hipStream_t side = nullptr;   // reward chains beside the child chains
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_kids = nullptr;
   float* d_rsum = nullptr;      // [256] row sums
   float* h_rout = nullptr;      // pinned: [9 rewards | 256 x 9 FIB dots]
   float* d_rout = nullptr;
@@ -374,6 +374,11 @@ int pack_rows(pp2_planner* p, pp2::PlaneSet src, int K, float* dst) {
 }
 
 // The FIB alphas as 9 dense rows, repacked when they changed.
+// Whether T is +0 off every action's base-kernel support on every cell (the
+// coded model's bitwise-verified sparse dictionary): the predictions read the
+// support taps only.
+static bool tree_sparse_t(const pp2_ctx* c) { return c->dict_n > 0 && c->dict_sparse; }
+
 int ref_frows(pp2_planner* p) {
   pp2_ctx* c = p->ctx;
   if (p->frows_version != c->fib_version) {
@@ -636,6 +641,38 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       p->h_r[a * N + j] = (float)p->rng.next() / ((float)RAND_MAX + 1.0f);
   HIPCHK(hipEventRecord(p->ev_fork, c->stream));  // brow and the previous stores are in place
   HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
+  // the side stream's work is enqueued first: it is the critical path (the
+  // children's masses, then their FIB dots after the join); the main stream's
+  // cdf chain and samples run beside it
+  {  // side: predictions, the children's masses and rows, rewards
+    HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred, tree_sparse_t(c)));
+    pp2::FcArgs a;
+    a.n = (int)n;
+    a.ld = ld;
+    a.pred = p->d_pred;
+    a.lrows = p->d_lrows;
+    a.out = p->d_csum;
+    a.ldo = 1;
+    p->scr_side.attach(&a);
+    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, a));
+    pp2::FcStoreList L;
+    L.n = 144;
+    for (int k = 0; k < 144; ++k) {
+      L.child[k] = k;
+      L.dst[k] = p->d_children + (size_t)k * ld;
+    }
+    HIPCHK(pp2::launch_store_children(p->side, L, p->d_pred, p->d_lrows, p->d_csum, (int)n, ld));
+    HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (children ready)
+    pp2::FcArgs r;
+    r.n = (int)n;
+    r.ld = ld;
+    r.row = brow;
+    r.partners = p->d_rrows;
+    r.out = p->d_rout;
+    r.ldo = 9;
+    p->scr_side.attach(&r);
+    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
+  }
   {  // main: running sums, samples
     pp2::FcArgs a;
     a.n = (int)n;
@@ -660,36 +697,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     sa.kcount = p->d_kcount;
     HIPCHK(pp2::launch_tree_sample(c->stream, sa));
   }
-  {  // side: predictions, the children's masses and rows, rewards
-    HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred));
-    pp2::FcArgs a;
-    a.n = (int)n;
-    a.ld = ld;
-    a.pred = p->d_pred;
-    a.lrows = p->d_lrows;
-    a.out = p->d_csum;
-    a.ldo = 1;
-    p->scr_side.attach(&a);
-    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, a));
-    pp2::FcStoreList L;
-    L.n = 144;
-    for (int k = 0; k < 144; ++k) {
-      L.child[k] = k;
-      L.dst[k] = p->d_children + (size_t)k * ld;
-    }
-    HIPCHK(pp2::launch_store_children(p->side, L, p->d_pred, p->d_lrows, p->d_csum, (int)n, ld));
-    HIPCHK(hipEventRecord(p->ev_join, p->side));  // (children ready)
-    pp2::FcArgs r;
-    r.n = (int)n;
-    r.ld = ld;
-    r.row = brow;
-    r.partners = p->d_rrows;
-    r.out = p->d_rout;
-    r.ldo = 9;
-    p->scr_side.attach(&r);
-    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
-  }
-  HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
+  HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
   {  // main: the kept children's FIB dots (evaluateFibCpu)
     pp2::FcArgs a;
     a.n = (int)n;
@@ -796,7 +804,8 @@ int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
     // (search_tree_cuda.cu:586-612) update, accumulate, divide: the child
     // (a, z) of the old root's row, as an expansion forms it
     const int cz = z * 9 + a;
-    HIPCHK(pp2::launch_tree_pred(c->stream, c->g, c->T.v, os.row, p->ref_ld, p->d_pred));
+    HIPCHK(pp2::launch_tree_pred(c->stream, c->g, c->T.v, os.row, p->ref_ld, p->d_pred,
+                                 tree_sparse_t(c)));
     pp2::FcArgs fa;
     fa.n = (int)p->n;
     fa.ld = p->ref_ld;
@@ -908,6 +917,7 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       hipEventCreateWithFlags(&p->ev_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_kids, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "planner scratch allocation failed"));
   p->ref = prm->reference_order == 1;
@@ -1042,7 +1052,7 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (p->h_belief) (void)hipHostFree(p->h_belief);
   if (p->ev_belief) (void)hipEventDestroy(p->ev_belief);
   if (p->ev_done) (void)hipEventDestroy(p->ev_done);
-  for (hipEvent_t e : {p->ev_fork, p->ev_join})
+  for (hipEvent_t e : {p->ev_fork, p->ev_join, p->ev_kids})
     if (e) (void)hipEventDestroy(e);
   if (p->side) {
     (void)hipStreamSynchronize(p->side);
