@@ -591,21 +591,43 @@ __global__ __launch_bounds__(256) void k_store_children(FcStoreList L, const flo
   L.dst[r][x] = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
 }
 
+// k_store_children over the kept children of the device list (klist,
+// *kcount): child c into dst + c * ld.
+__global__ __launch_bounds__(256) void k_store_kept(const int* __restrict__ klist,
+                                                    const int* __restrict__ kcount,
+                                                    const float* __restrict__ pred,
+                                                    const float* __restrict__ lrows,
+                                                    const float* __restrict__ sums,
+                                                    float* __restrict__ dst, int n, int ld) {
+  const int r = blockIdx.y;
+  if (r >= *kcount) return;
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= n) return;
+  const int c = klist[r];
+  const float v = ftz(pred[(long long)(c % 9) * ld + x] * ftz(lrows[(long long)(c / 9) * ld + x]));
+  dst[(long long)c * ld + x] = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
+}
+
 template <int BASE, int K>
-hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a) {
+hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a, int phases) {
   constexpr int KC = K > 0 ? K : 1;
   const int nseg = fc_segments(a.n);
-  hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, groups), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, groups), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(groups * KC), dim3(64), 0, st, a);
-  if (BASE == FC_ROW && K == 0 && a.cdf)
-    hipLaunchKernelGGL(k_fc_cdf, dim3((fc_chunks(a.n) + 3) / 4), dim3(256), 0, st, a);
+  if (phases & FC_TABLES) {
+    hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, groups), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, groups), dim3(256), 0, st, a);
+  }
+  if (phases & FC_DRIVE) {
+    hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(groups * KC), dim3(64), 0, st, a);
+    if (BASE == FC_ROW && K == 0 && a.cdf)
+      hipLaunchKernelGGL(k_fc_cdf, dim3((fc_chunks(a.n) + 3) / 4), dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a) {
+hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a,
+                         int phases) {
   if (groups <= 0) return hipSuccess;
   if (a.n <= 0 || a.n > kFcMaxCells || (K != 0 && K != 9) || !a.out || !a.csum || !a.cflag ||
       !a.tab || groups * (K > 0 ? K : 1) > a.max_chains || fc_chunks(a.n) > a.max_chunks)
@@ -615,9 +637,9 @@ hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcAr
   if (base == FC_ROW && !a.row) return hipErrorInvalidValue;
   if (K != 0 && !a.partners) return hipErrorInvalidValue;
   if (a.cdf && (base != FC_ROW || K != 0 || groups != 1 || !a.cst)) return hipErrorInvalidValue;
-  if (base == FC_ROW && K == 0) return launch_set<FC_ROW, 0>(st, groups, a);
-  if (base == FC_ROW && K == 9) return launch_set<FC_ROW, 9>(st, groups, a);
-  if (base == FC_CHILD) return launch_set<FC_CHILD, 0>(st, groups, a);
+  if (base == FC_ROW && K == 0) return launch_set<FC_ROW, 0>(st, groups, a, phases);
+  if (base == FC_ROW && K == 9) return launch_set<FC_ROW, 9>(st, groups, a, phases);
+  if (base == FC_CHILD) return launch_set<FC_CHILD, 0>(st, groups, a, phases);
   return hipErrorInvalidValue;
 }
 
@@ -635,6 +657,15 @@ hipError_t launch_store_children(hipStream_t st, const FcStoreList& L, const flo
   if (L.n > 144) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_store_children, dim3((n + 255) / 256, L.n), dim3(256), 0, st, L, pred, lrows,
                      sums, n, ld);
+  return hipGetLastError();
+}
+
+hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount,
+                             const float* pred, const float* lrows, const float* sums, float* dst,
+                             int n, int ld) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_store_kept, dim3((n + 255) / 256, 144), dim3(256), 0, st, klist, kcount,
+                     pred, lrows, sums, dst, n, ld);
   return hipGetLastError();
 }
 

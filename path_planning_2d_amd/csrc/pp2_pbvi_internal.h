@@ -143,7 +143,12 @@ struct FcScratch {
   void release();
   void attach(FcArgs* a) const;
 };
-hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a);
+// phases (bit mask): 1 = the chunk sums and tables, 2 = the driver (and the
+// running sums): a caller may enqueue other work between the two, with the
+// same FcArgs and scratch.
+enum : int { FC_TABLES = 1, FC_DRIVE = 2, FC_ALL = 3 };
+hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a,
+                         int phases = FC_ALL);
 // forwardSampling of the 9 actions from the expanded belief's running sums
 // cdf[n]: r[9 * N] the host's rand() values (action-major), u1 / u2 [N] the
 // curand uniforms; counts[a * 16 + z] and the kept children z * 9 + a.
@@ -168,6 +173,11 @@ struct FcStoreList {
 };
 hipError_t launch_store_children(hipStream_t st, const FcStoreList& L, const float* pred,
                                  const float* lrows, const float* sums, int n, int ld);
+// The same for the children listed on the device (klist[r], r < *kcount, at
+// most 144): child c into dst + c * ld.
+hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount,
+                             const float* pred, const float* lrows, const float* sums, float* dst,
+                             int n, int ld);
 
 // ---- pp2_pbvi_dev.hip (FTZ): the 9 action predictions of cudaBayesBeliefUpdate
 // before the likelihood product: pred[u][idx] = sum_s T[sidx][u][8-s] * b[sidx]

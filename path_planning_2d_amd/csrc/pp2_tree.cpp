@@ -618,13 +618,13 @@ int expand_vnode(pp2_planner* p, VNode* v) {
 // 9 QNode constructors (search_tree_cuda.cu:161-242) is formed on the device
 // with the bits of its x-ordered fp32 host chain (pp2_fchain.hip), and the
 // samples are drawn there with the host's rand() values:
-//   main stream: the expanded belief's running sums (:176-183), the 9 x N
-//     samples (forwardSampling, :311-366) and the kept children; then, once
-//     the children exist, evaluateFibCpu of the kept ones (:378);
 //   side stream: the 9 action predictions, the 144 children's accumulate
-//     (:225-227; child (a, z) = cudaBayesBeliefUpdate(b, a, z)), all of them
-//     normalised into d_children (:228-229), and the 9 rewards
-//     inner_product(b, R[.][a]) (:168-173).
+//     (:225-227; child (a, z) = cudaBayesBeliefUpdate(b, a, z)), then the 9
+//     rewards inner_product(b, R[.][a]) (:168-173);
+//   main stream: the expanded belief's running sums (:176-183) and the 9 x N
+//     samples (forwardSampling, :311-366) with the kept children; once the
+//     masses are in, the kept children normalised (:228-229) into their rows
+//     of d_children and their evaluateFibCpu dots (:378).
 // One host wait per expansion.  The kept children's rows are stored into
 // their nodes' slots afterwards, queued ahead of anything that reads them.
 int expand_vnode_ref(pp2_planner* p, VNode* v) {
@@ -641,47 +641,33 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       p->h_r[a * N + j] = (float)p->rng.next() / ((float)RAND_MAX + 1.0f);
   HIPCHK(hipEventRecord(p->ev_fork, c->stream));  // brow and the previous stores are in place
   HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
-  // the side stream's work is enqueued first: it is the critical path (the
-  // children's masses, then their FIB dots after the join); the main stream's
-  // cdf chain and samples run beside it
-  {  // side: predictions, the children's masses and rows, rewards
-    HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred, tree_sparse_t(c)));
-    pp2::FcArgs a;
-    a.n = (int)n;
-    a.ld = ld;
-    a.pred = p->d_pred;
-    a.lrows = p->d_lrows;
-    a.out = p->d_csum;
-    a.ldo = 1;
-    p->scr_side.attach(&a);
-    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, a));
-    pp2::FcStoreList L;
-    L.n = 144;
-    for (int k = 0; k < 144; ++k) {
-      L.child[k] = k;
-      L.dst[k] = p->d_children + (size_t)k * ld;
-    }
-    HIPCHK(pp2::launch_store_children(p->side, L, p->d_pred, p->d_lrows, p->d_csum, (int)n, ld));
-    HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (children ready)
-    pp2::FcArgs r;
-    r.n = (int)n;
-    r.ld = ld;
-    r.row = brow;
-    r.partners = p->d_rrows;
-    r.out = p->d_rout;
-    r.ldo = 9;
-    p->scr_side.attach(&r);
-    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
-  }
-  {  // main: running sums, samples
-    pp2::FcArgs a;
-    a.n = (int)n;
-    a.ld = ld;
-    a.row = brow;
-    a.out = p->d_rsum;
-    a.cdf = p->d_cdf;
-    p->scr_main.attach(&a);
-    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, a));
+  // The two streams' launches are interleaved phase by phase, so that
+  // neither waits for the host to enqueue the other's (a launch costs the
+  // host several us): predictions (side), the cdf chain's tables (main), the
+  // children's tables (side), the cdf driver and running sums (main), the
+  // children's driver (side), the samples (main); the rewards last (side).
+  HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred, tree_sparse_t(c)));
+  pp2::FcArgs cd;  // main: the expanded belief's running sums
+  cd.n = (int)n;
+  cd.ld = ld;
+  cd.row = brow;
+  cd.out = p->d_rsum;
+  cd.cdf = p->d_cdf;
+  p->scr_main.attach(&cd);
+  pp2::FcArgs ch;  // side: the 144 children's masses
+  ch.n = (int)n;
+  ch.ld = ld;
+  ch.pred = p->d_pred;
+  ch.lrows = p->d_lrows;
+  ch.out = p->d_csum;
+  ch.ldo = 1;
+  p->scr_side.attach(&ch);
+  HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
+  HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
+  HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
+  HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
+  HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
+  {
     pp2::SampleArgs sa;
     sa.g = c->g;
     sa.T = c->T.v;
@@ -697,7 +683,22 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     sa.kcount = p->d_kcount;
     HIPCHK(pp2::launch_tree_sample(c->stream, sa));
   }
+  {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
+    pp2::FcArgs r;
+    r.n = (int)n;
+    r.ld = ld;
+    r.row = brow;
+    r.partners = p->d_rrows;
+    r.out = p->d_rout;
+    r.ldo = 9;
+    p->scr_side.attach(&r);
+    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
+  }
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
+  // main: the kept children (sampled on this stream), normalised by their
+  // masses (side) into their rows of d_children -- only they become nodes
+  HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
+                                p->d_csum, p->d_children, (int)n, ld));
   {  // main: the kept children's FIB dots (evaluateFibCpu)
     pp2::FcArgs a;
     a.n = (int)n;
