@@ -306,18 +306,19 @@ __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* 
     }
     tot = min(tot, kK24 + 1);  // no scan overflow; anything above 2^24 fails anyway
     const int incl = wave_incl_scan(tot, lane);
+    // the lane's terms in order: each applies (k grows by its increment)
+    // until the first that does not (a tie, or past 2^24) -- selects, no
+    // branches (a divergent if per term tripled the round's instructions)
     int kk = k + incl - tot, bad = 4, kb = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (bad == 4 && 4 * lane + q >= done) {
-        if (tie[q] || kk + r[q] > kK24) {
-          bad = q;
-          kb = kk;
-        } else {
-          kk += r[q];
-          if (cv) (*cv)[q] = value_of(E, kk);
-        }
-      }
+      const bool act = bad == 4 && 4 * lane + q >= done;
+      const bool stop = act && (tie[q] || kk + r[q] > kK24);
+      const bool ok = act && !stop;
+      bad = stop ? q : bad;
+      kb = stop ? kk : kb;
+      kk = ok ? kk + r[q] : kk;
+      if (cv) (*cv)[q] = ok ? value_of(E, kk) : (*cv)[q];
     }
     const uint64_t bm = __ballot(bad < 4);
     if (bm == 0ull) {
@@ -330,10 +331,9 @@ __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* 
     const float tb = rdl(tq, lb);
     const float s = value_of(E, kbef) + tb;  // the reference's own add
     state_of(s, &E, &k);
-    if (cv && lane == lb) {
+    if (cv) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (q == qb) (*cv)[q] = s;
+      for (int q = 0; q < 4; ++q) (*cv)[q] = lane == lb && q == qb ? s : (*cv)[q];
     }
     // (values of later terms computed in this round were provisional: the
     // next round recomputes them)
