@@ -396,6 +396,23 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
   } else {
     int E = kEMin, k = 0, j = 0, wbase = -kFcWin, nstash = 0;
     int n_it = 0, n_fb = 0, n_rounds = 0, n_hit = 0;
+    {
+      // chunk 0 from the exact zero state as the chain itself, one fp32 add
+      // per term: its running sum climbs through many binades (about log2
+      // of its term count), each an exact round of ~1000 cycles, where the
+      // sequential chain costs ~10 cycles a term
+      float t[4];
+      T.terms4(i, 4 * lane, t);
+      float s = 0.0f;
+#pragma unroll
+      for (int l = 0; l < 64; ++l)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s = s + rdl(fabsf(t[q]), l);
+      if (cdf && lane == 0) a.cst[0] = make_int2(kEMin, 0);
+      state_of(s, &E, &k);
+      normalise(&E, &k);
+      j = 1;
+    }
     while (j < nch) {
       ++n_it;
       if (j >= wbase + kFcWin) {  // the next window of entries, and its predicted fallbacks
