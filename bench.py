@@ -692,6 +692,7 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
     ctx.mdp_reset()
     ctx.synchronize()
     e = ctx.loop_steps_per_launch()
+    tiling = ctx.resident_tiling()
     l0 = ctx.resident_launches()[0]
     el = run(ctx, False)
     launches = ctx.resident_launches()[0] - l0
@@ -703,6 +704,8 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
     return {"shard": f"rows [{r0}, {r1}) x {G} of the {G}^2 grid (rank 3 of 8), 1-rank RCCL "
                      f"communicator",
             "steps_per_launch": e, "resident_launches_in_run": launches,
+            "resident_tiling": {"tiles": tiling[0], "rows_per_tile": tiling[1],
+                                "tile_cols": tiling[2]},
             "measured_us_per_step": t,
             "projection_8_ranks": {
                 "assumed_rccl_round_us": list(RCCL_ROUND_US),

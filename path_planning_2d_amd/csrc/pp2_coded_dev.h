@@ -103,16 +103,62 @@ __device__ __forceinline__ void coded_sweep_sparse(const float* sTC, const uint3
 }
 
 // The same with the cells' IW records held in registers (the resident loop).
-template <int N, bool ARG>
+// G > 0: action-outer -- the table reads of one action for a group of G cells
+// are in flight together (one LDS round trip per action and group instead of
+// one per cell and action); per cell the same fmaf chain and ascending action
+// order, so the results are the cell-outer ones bit for bit.  It pays where a
+// SIMD holds few waves to hide the round trips (3-row tiles: 4.72 -> 4.46 us
+// per step) and costs 2-4 % at 4 waves per SIMD (profiles/r04/ab_sweep_ao.txt).
+template <int N, bool ARG, int G = 0>
 __device__ __forceinline__ void coded_sweep_iw(const float* sTC, const uint32_t (&iw)[N][3],
                                                const float (&jn)[9][N], float (&best)[N],
                                                uint32_t (&arg)[N]) {
 #pragma unroll
   for (int k = 0; k < N; ++k) { best[k] = FLT_MAX; arg[k] = 0; }
+  if constexpr (G > 0) {
+    static_assert(N % G == 0, "cell groups");
+    const char* qt = reinterpret_cast<const char*>(sTC + kFactQT);
+    const char* ct = reinterpret_cast<const char*>(sTC + kFactCT);
 #pragma unroll
-  for (int k = 0; k < N; ++k) {
-    sweep_cell_fact<N, ARG>(sTC, iw[k][0], iw[k][1], iw[k][2], jn, k, best[k], arg[k]);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int a = 0; a < 9; ++a) {
+      const int tab = a * kFactK * 16;
+#pragma unroll
+      for (int k0 = 0; k0 < N; k0 += G) {
+        float tv[G][4], cost[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int k = k0 + g;
+          const uint32_t w = a < 4 ? iw[k][0] : a < 8 ? iw[k][1] : iw[k][2];
+          const uint32_t off = __builtin_amdgcn_ubfe(w, 8 * (a % 4), 8);
+          if (kSupN[a] == 1) {
+            tv[g][0] = *reinterpret_cast<const float*>(qt + tab + off);
+          } else {
+            const f4a t = *reinterpret_cast<const f4a*>(qt + tab + off);
+            tv[g][0] = t[0]; tv[g][1] = t[1]; tv[g][2] = t[2]; tv[g][3] = t[3];
+          }
+          cost[g] = *reinterpret_cast<const float*>(ct + tab + off);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int k = k0 + g;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < kSupN[a]) cost[g] = __builtin_fmaf(tv[g][j], jn[kSup[a][j]][k], cost[g]);
+          if constexpr (ARG) {
+            if (cost[g] < best[k]) { best[k] = cost[g]; arg[k] = (uint32_t)a; }
+          } else {
+            best[k] = __builtin_fminf(best[k], cost[g]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one group's reads live at a time
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      sweep_cell_fact<N, ARG>(sTC, iw[k][0], iw[k][1], iw[k][2], jn, k, best[k], arg[k]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 

@@ -429,6 +429,9 @@ __device__ __forceinline__ void take_rows_sides(Rsrc r, bool rows, int o, bool e
       ok = tagged(g[0], m) && tagged(g[1], m) && (((e[0] ^ m) | (e[1] ^ m)) >> 31) == 0u;
 #pragma unroll
     for (int k = 0; k < 3; ++k) ok = ok && (((s[k][0] ^ m) | (s[k][1] ^ m)) >> 31) == 0u;
+#ifdef PP2_RES_NOWAIT
+    ok = true;  // diagnostic build only (tools/micro/resident_nowait.sh): no hand-off waits
+#endif
     if (__all(ok)) break;
     if ((spin & 7) == 7) {
       if (ld_flag(err) != 0u || wall_clock64() - t0 > kSpinTicks) {
@@ -468,6 +471,7 @@ template <int CAP, int TC, bool LAG, bool TR>
 __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
                                                            const Trajectory<CAP> tr) {
   static_assert(!TR || TC == 1, "transposed tiles are whole kernel rows");
+  constexpr int kSweepG = TC > 1 ? 2 : 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // a tile: rt rows x tw columns (tc tile columns per row of tiles)
   constexpr int tc = TC;
@@ -852,8 +856,9 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       for (int i = 0; i < 9; ++i)
 #pragma unroll
         for (int k = 0; k < 4; ++k) jn[i][k] = TR ? wj.v[i % 3][k + i / 3] : wj.v[i / 3][k + i % 3];
-      if (last) coded_sweep_iw<4, true>(sTC, iwr, jn, best, arg);  // actions: last step only
-      else coded_sweep_iw<4, false>(sTC, iwr, jn, best, arg);
+      // (2-D tiles: the cells' table reads in pairs, coded_sweep_iw)
+      if (last) coded_sweep_iw<4, true, kSweepG>(sTC, iwr, jn, best, arg);  // actions: last step only
+      else coded_sweep_iw<4, false, kSweepG>(sTC, iwr, jn, best, arg);
       *reinterpret_cast<f4a*>(sbuf(1, co) + ty * xs + x0) = f4a{best[0], best[1], best[2], best[3]};
     };
     // the scale, the mass partial, b' into LDS and the boundary rows out --
@@ -925,7 +930,9 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
       }
       if (lane == 0) sS[0] = S;
     }
+#ifndef PP2_RES_NOBAR
     __syncthreads();  // also: this step's LDS writes before the next step's reads
+#endif
     if (arrive && threadIdx.x == 0)
       __hip_atomic_fetch_add(a.sync + kResidentSyncArrive, 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
@@ -1196,10 +1203,11 @@ static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPla
 
 // Whole-row tiles, or two tile columns when whole rows would give tiles of
 // fewer than 4 rows -- every row an edge row, so every wave of the CU waits
-// on a neighbour -- and 2-D tiles hold 4 or more (tc_pref 0), or whenever they
+// on a neighbour -- and 2-D tiles hold 3 or more (tc_pref 0), or whenever they
 // fit (tc_pref 2).  A 256-row share of the 2048^2 grid (its 512-row view)
 // then runs 4 x 1024 tiles instead of 2 x 2048: 4.89 vs 5.03 us per step
-// (tools/ab_tile_cols.py).
+// (tools/ab_tile_cols.py); its 384-row view (e = 64) 3 x 1024
+// instead of 2 x 2048: 4.46 vs 4.88 (profiles/r04/ab_sweep_ao.txt).
 bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref, bool allow_tr) {
   ResidentPlan p1, p2, pt;
   if (tc_pref == 3 && allow_tr && g.rows % 256 == 0 &&
@@ -1211,7 +1219,7 @@ bool resident_plan(const Geom& g, int E, int ncus, ResidentPlan* p, int tc_pref,
   const bool ok2 = tc_pref != 1 && resident_plan_tc(g, E, ncus, 2, &p2);
   // (automatic only with 1024-column tiles or wider: the measured shape, whose
   // rows keep interior waves beside the side waves)
-  if (ok2 && ok1 && (tc_pref == 2 || (p1.rt < 4 && p2.rt >= 4 && g.wp / 2 >= 1024))) {
+  if (ok2 && ok1 && (tc_pref == 2 || (p1.rt < 4 && p2.rt >= 3 && g.wp / 2 >= 1024))) {
     *p = p2;
     return true;
   }

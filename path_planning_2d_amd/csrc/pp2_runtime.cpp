@@ -1351,11 +1351,25 @@ int pp2rt::shard_resident_e(pp2_ctx* c) {
   if (!(c->comm || c->group) || !resident_model_ok(c)) return 0;
   if (c->res_e_dict == c->dict_n) return c->res_e;
   int e = shard_resident_depth(c);
-  for (; e >= 1; --e) {
-    pp2::ResidentPlan p;
-    if (pp2::resident_plan(view_geom(c, e), c->dict_n, resident_cus(c), &p, c->res_tc_pref,
-                           e % 4 == 0 && c->g.rows % 4 == 0))
-      break;
+  pp2::ResidentPlan p;
+  auto plan = [&](int ee, pp2::ResidentPlan* q) {
+    return pp2::resident_plan(view_geom(c, ee), c->dict_n, resident_cus(c), q, c->res_tc_pref,
+                              ee % 4 == 0 && c->g.rows % 4 == 0);
+  };
+  for (; e >= 1; --e)
+    if (plan(e, &p)) break;
+  // Without a requested halo: half the depth while that gives tiles of fewer
+  // rows (fewer waves per CU).  A step of the resident kernel is the tile's
+  // compute chain, which shrinks with the waves per CU (2048^2 / 8 ranks: e =
+  // 128's 4 x 1024 tiles 4.90 us per step, e = 64's 3 x 1024 tiles 4.46),
+  // while the halved depth adds one RCCL round per e steps (<= 0.5 us per
+  // step at e >= 64 and 30 us per round; profiles/r04/ab_sweep_ao.txt).
+  if (e > 0 && c->res_halo == 0 && c->res_tc_pref != 3) {
+    pp2::ResidentPlan q;
+    while (e / 2 >= 64 && plan(e / 2, &q) && q.rt < p.rt) {
+      e /= 2;
+      p = q;
+    }
   }
   c->res_e_dict = c->dict_n;
   c->res_e = e;

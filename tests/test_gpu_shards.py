@@ -281,8 +281,11 @@ def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True, tilin
             grp.set_tuning(P.GridContext.TUNE_RESIDENT_TILE_COLS, tiling)
         if lag:
             grp.set_tuning(P.GridContext.TUNE_SHARD_LAG, lag)
-        e = grp.loop_steps_per_launch()
-        assert len(set(e)) == 1 and e[0] >= 2, e
+        # each shard's own depth; the group runs the smallest (every shard's
+        # view must hold it)
+        e_all = grp.loop_steps_per_launch()
+        e = min(e_all)
+        assert e >= 2, e_all
         for c in (ref, grp):
             c.belief_set(b0)
             c.mdp_reset()
@@ -290,7 +293,7 @@ def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True, tilin
         for lo, hi in chunks:
             ref.loop_run(us[lo:hi], zs[lo:hi])
             grp.loop_run(us[lo:hi], zs[lo:hi])
-            launches += -(-(hi - lo) // e[0])
+            launches += -(-(hi - lo) // e)
             assert grp.shards[0].resident_launches()[0] == launches
             Jr, Ar = ref.mdp_get()
             Jg, Ag = grp.mdp_get()
@@ -312,37 +315,42 @@ def _resident_shard_run(P, grid, goal, bounds, chunks, halo=0, mixed=True, tilin
             np.testing.assert_array_equal(grp.mdp_get()[1], ref.mdp_get()[1])
             assert_rel_close(grp.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
                              msg="loop after the per-step drivers")
-        return e[0]
+        return e
 
 
 @pytest.mark.parametrize("tiling,lag", [(0, 0), (3, 0), (0, 1), (3, 1)])
 def test_shard_group_resident_config4(tiling, lag):
     """BASELINE configs[3]'s per-rank geometry: the 2048^2 grid in 8 row shards
     of 256 rows (one device here), each shard's run on the resident kernel
-    (view 256 + 2e rows, e = 128: 256 tiles of 4 x 1024 cells, or -- tiling
-    3 -- 256 transposed tiles of 8 grid columns x the 512 view rows), with
-    block starts waited for or lagged (PP2_TUNE_SHARD_LAG)."""
+    (view 256 + 2e rows, e = 64: 256 tiles of 3 x 1024 cells -- the halved
+    depth's tiles hold fewer rows than e = 128's 4 x 1024 --, or -- tiling 3
+    -- e = 128 and 256 transposed tiles of 8 grid columns x the 512 view
+    rows), with block starts waited for or lagged (PP2_TUNE_SHARD_LAG)."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S
     N = 2048
     grid = S.synth_grid(N, N, N)
     e = _resident_shard_run(P, grid, S.synth_goal(grid), tuple(range(0, N + 1, N // 8)),
                             ((0, 30), (30, 41)), mixed=tiling == 3, tiling=tiling, lag=lag)
-    assert e == 128
+    assert e == (128 if tiling == 3 else 64)
 
 
-@pytest.mark.parametrize("bounds,halo,lag", [((0, 256, 512), 0, 0), ((0, 200, 512), 6, 0),
-                                             ((0, 128, 300, 512), 9, 0), ((0, 200, 512), 0, 1)])
-def test_shard_group_resident_blocks(bounds, halo, lag):
+@pytest.mark.parametrize("bounds,halo,lag,e_want", [((0, 256, 512), 0, 0, 128), ((0, 200, 512), 6, 0, 6),
+                                                    ((0, 128, 300, 512), 9, 0, 9),
+                                                    ((0, 200, 512), 0, 1, 64)])
+def test_shard_group_resident_blocks(bounds, halo, lag, e_want):
     """Uneven shards, several halo blocks per call (e = 6, 9: in-kernel
     power-of-two block starts every 8 steps, rebases at every exchange),
-    calls ending mid-block, then per-step drivers on the same state."""
+    calls ending mid-block, then per-step drivers on the same state.  Without
+    a requested halo the shards agree on the deepest e, halved while that
+    gives tiles of fewer rows: 128 for the 256-row shards (2-row tiles
+    either way), 64 for the 312-row one (3 -> 2 rows per tile)."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S
     grid = S.synth_grid(512, 1024, 7)
     e = _resident_shard_run(P, grid, S.synth_goal(grid), bounds,
                             ((0, 2), (2, 19), (19, 40)), halo=halo, lag=lag)
-    assert e == (halo or 128)
+    assert e == e_want
 
 
 def test_shard_group_resident_weak_scaling_shards():
@@ -389,8 +397,9 @@ def test_rccl_single_rank_resident_896x1024():
 def test_rccl_single_rank_resident_256x2048(tiling):
     """The RCCL path of a 256 x 2048 shard -- the per-rank share of the
     2048^2 grid at 8 ranks -- with a 1-rank communicator: pp2_loop_run takes
-    the resident shard path (e = 128: 512-row view, exchanges, {mass, shift}
-    all-reduce, rebase) and equals the unsharded grid."""
+    the resident shard path (e = 64: 384-row view; transposed tiles: e = 128,
+    512-row view; exchanges with the {mass, shift, lost} records, rebase) and
+    equals the unsharded grid."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S
     grid = S.synth_grid(256, 2048, 256)
@@ -406,10 +415,10 @@ def test_rccl_single_rank_resident_256x2048(tiling):
             c.model_generate()
             c.belief_set(b0)
             c.mdp_reset()
-        assert sh.loop_steps_per_launch() == 128
-        # the 512-row view runs 2-D tiles (4 x 1024, two tile columns), or
-        # transposed tiles (8 grid columns x 512 view rows)
-        assert sh.resident_tiling() == ((256, 8, 3) if tiling == 3 else (256, 4, 2))
+        assert sh.loop_steps_per_launch() == (128 if tiling == 3 else 64)
+        # the 384-row view runs 2-D tiles (3 x 1024, two tile columns), the
+        # 512-row one transposed tiles (8 grid columns x 512 view rows)
+        assert sh.resident_tiling() == ((256, 8, 3) if tiling == 3 else (256, 3, 2))
         for lo, hi in ((0, 17), (17, 300)):
             ref.loop_run(us[lo:hi], zs[lo:hi])
             sh.loop_run(us[lo:hi], zs[lo:hi])
@@ -418,5 +427,6 @@ def test_rccl_single_rank_resident_256x2048(tiling):
             np.testing.assert_array_equal(sh.mdp_get()[1], ref.mdp_get()[1])
             assert_rel_close(sh.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
                              msg=f"belief after {hi} steps")
-        assert sh.resident_launches()[0] == 1 + 3
+        e = sh.loop_steps_per_launch()
+        assert sh.resident_launches()[0] == -(-17 // e) + -(-283 // e)  # 1 + 3, or 1 + 5 at e = 64
         assert abs(float(sh.belief_get().astype(np.float64).sum()) - 1.0) < 1e-4
