@@ -1,7 +1,8 @@
 // pp2_rollout.cpp -- batched fp16 QV-tree rollouts (C ABI pp2_rollout_*).
 //
-// Host driver of k_rollout_band (pp2_rollout_dev.hip) and k_rollout_leaf
-// (pp2_kernels.hip): groups the copies of every step by action (chunks of
+// Host driver of k_rollout_band (pp2_rollout_dev.hip) and the leaf pass
+// (k_rollout_leaf_mfma there, or k_rollout_leaf in pp2_kernels.hip for rows
+// that are not 16-B aligned): groups the copies of every step by action (chunks of
 // rollout_chunk() copies sharing u, so a wave gathers its T_u stencil terms
 // once for all of them), chains the depth steps
 // on the context's stream, and turns the per-copy {stored sum, stored max,
@@ -30,6 +31,7 @@ struct pp2_rollout {
   float* d_stats = nullptr;        // [depth+1][copies][3]
   float* d_leaf = nullptr;         // [copies][10]
   float* d_partials = nullptr;     // [copies][waves][10]
+  void* d_leafmm = nullptr;        // the MFMA leaf pass's scratch (null: the fmaf pass)
   int* d_chunks = nullptr;         // per step: u[], first[], n[] (maxchunks each), copies[]
   uint8_t* d_zs = nullptr;         // [depth][copies]
   int maxchunks = 0;
@@ -45,7 +47,8 @@ int pp2_rollout_destroy(pp2_rollout* r) {
   DeviceGuard dg(r->ctx->device);
   (void)hipStreamSynchronize(r->ctx->stream);
   for (void* p : {r->alloc[0], r->alloc[1], (void*)r->d_stats, (void*)r->d_leaf,
-                  (void*)r->d_partials, (void*)r->d_chunks, (void*)r->d_zs, (void*)r->d_root})
+                  (void*)r->d_partials, (void*)r->d_chunks, (void*)r->d_zs, (void*)r->d_root,
+                  r->d_leafmm})
     if (p) (void)hipFree(p);
   delete r;
   return PP2_OK;
@@ -85,6 +88,9 @@ int pp2_rollout_create(pp2_rollout** out, pp2_ctx* c, int copies, int depth) {
       hipMalloc(&r->d_zs, (size_t)depth * copies) != hipSuccess ||
       hipMalloc(&r->d_root, (size_t)r->cstride * sizeof(_Float16)) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "rollout scratch"));
+  if (pp2::rollout_leaf_mfma_ok(c->g, r->cstride) &&
+      hipMalloc(&r->d_leafmm, pp2::rollout_leaf_scratch_bytes(c->g, copies)) != hipSuccess)
+    return fail(set_err(PP2_ENOMEM, "rollout leaf scratch"));
   *out = r;
   return PP2_OK;
 }
@@ -182,8 +188,12 @@ int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs) {
                                     r->d_stats + (size_t)k * C * kRollStats, r->d_partials,
                                     r->d_stats + (size_t)(k + 1) * C * kRollStats, C));
   }
-  HIPCHK(pp2::launch_rollout_leaf(c->stream, c->g, c->fib[c->fcur].v, r->buf[D & 1], r->cstride,
-                                  C, r->d_partials, r->d_leaf));
+  if (r->d_leafmm)
+    HIPCHK(pp2::launch_rollout_leaf_mfma(c->stream, c->g, c->fib[c->fcur].v, r->buf[D & 1],
+                                         r->cstride, C, r->d_leafmm, r->d_leaf));
+  else
+    HIPCHK(pp2::launch_rollout_leaf(c->stream, c->g, c->fib[c->fcur].v, r->buf[D & 1],
+                                    r->cstride, C, r->d_partials, r->d_leaf));
   r->ran = true;
   return PP2_OK;
 }

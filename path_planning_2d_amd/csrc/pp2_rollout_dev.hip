@@ -524,4 +524,249 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
   return launch_rollout_reduce(st, partials, nw, ncopies, stats_out);
 }
 
+
+// ---------------------------------------------------------------- leaf pass
+// The leaf FIB dots of every copy (fast_informed_bound_cuda.cu:278-297's
+// <b_D, alpha_i>, i < 9, and the copy's mass) as ONE GEMM on the matrix
+// cores: D[copy][col] = sum over cells of b[copy][cell] * B[cell][col], with
+// the copies' fp16 planes as A (exact: the stored beliefs ARE fp16) and B's
+// columns {1, hi_0..hi_8, lo_0..lo_8}: alpha_i * 2^k_i = hi_i + lo_i in two
+// fp16 halves (k_i a per-plane power of two bringing max |alpha_i| into
+// [2^13, 2^14): hi + lo carries ~22 bits of it, the rest is below 2^-22 of
+// the value or of the plane's max).  Every product is exact in fp32 and the
+// MFMA sums in fp32, so the dots match the fp32 fmaf pass (k_rollout_leaf)
+// to fp32 rounding -- the fp16 rollout's tolerance (rel 3e-3) is far above.
+// Each wave takes 64 copies (two 32-row tiles sharing every B fragment) over
+// a slab of kLeafSlab cells; A is streamed once (2 B per cell-copy), B is
+// re-read per wave from L2.  The k index of a 32x32x16 step is a permutation
+// of 16 consecutive cells: lane (r, h) loads cells 8h .. 8h+7 of its copy r
+// (16 B) and of its column r of B, so A and B use the same cells.
+namespace {
+
+constexpr int kLeafCols = 19;      // 1 + 9 hi + 9 lo
+constexpr int kLeafColsPad = 32;   // B's columns in memory (the MFMA's N; zero past kLeafCols)
+#ifndef PP2_LEAF_SLAB
+#define PP2_LEAF_SLAB 8192
+#endif
+constexpr int kLeafSlab = PP2_LEAF_SLAB;  // cells per block (B is padded to a multiple)
+constexpr int kLeafParts = 32;     // |alpha| max partials per plane
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f16acc __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256) void k_leaf_alpha_max(Geom g, PlaneSet F, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int plane = blockIdx.y;
+  const long long n = (long long)g.rows * g.wp;
+  float m = 0.0f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += 256LL * gridDim.x) {
+    const long long y = i / g.wp, x = i - y * g.wp;
+    const float v = fabsf(F.p[y * F.rs + plane * F.ps + x]);
+    m = v > m ? v : m;  // (a NaN is skipped; the dots carry it anyway)
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[plane * kLeafParts + blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// B as columns [kLeafColsPad][ldb] fp16 (ldb a multiple of kLeafSlab, zero
+// past the grid's cells and in columns >= kLeafCols); kexp[i] = k_i.
+__global__ __launch_bounds__(256) void k_leaf_alpha_pack(Geom g, PlaneSet F,
+                                                         const float* __restrict__ part,
+                                                         _Float16* __restrict__ B, long long ldb,
+                                                         int* __restrict__ kexp) {
+  __shared__ float sc[9];
+  if (threadIdx.x < 9) {
+    float m = 0.0f;
+    for (int j = 0; j < kLeafParts; ++j) m = fmaxf(m, part[threadIdx.x * kLeafParts + j]);
+    int k = 0;
+    if (m > 0.0f && m <= FLT_MAX) {
+      const int e = (int)((__float_as_uint(m) >> 23) & 0xffu) - 127;  // (FTZ: m is normal)
+      k = 13 - e;
+      k = k < -120 ? -120 : k > 120 ? 120 : k;
+    }
+    sc[threadIdx.x] = ldexpf(1.0f, k);
+    if (blockIdx.x == 0) kexp[threadIdx.x] = k;
+  }
+  __syncthreads();
+  const long long n = (long long)g.rows * g.wp;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < ldb; i += 256LL * gridDim.x) {
+    const bool in = i < n;
+    const long long y = in ? i / g.wp : 0, x = in ? i - y * g.wp : 0;
+    B[i] = (_Float16)(in ? 1.0f : 0.0f);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const float v = in ? F.p[y * F.rs + q * F.ps + x] * sc[q] : 0.0f;  // (exact: a power of two)
+      const _Float16 hi = (_Float16)v;
+      B[(1 + q) * ldb + i] = hi;
+      B[(10 + q) * ldb + i] = (_Float16)(v - (float)hi);
+    }
+#pragma unroll
+    for (int q = kLeafCols; q < kLeafColsPad; ++q) B[q * ldb + i] = (_Float16)0.0f;
+  }
+}
+
+// part[(copy * kLeafCols + col) * nslab + slab].  One wave per workgroup: 64
+// copies (two 32-row tiles) over one slab.  A is staged through a per-wave
+// LDS ring by LDS-DMA (no VGPRs): a stage is 64 cells of the 64 copies, one
+// whole 128-B line per copy row, 8 lanes per line (coalesced; loading the
+// MFMA fragments straight from HBM touches 32 lines per instruction for 32 B
+// each and ran at 2.8 TB/s).  Lane l of DMA instruction i loads unit
+// (l & 7) ^ (l >> 3) of copy 8i + (l >> 3) into ring unit l, so ring unit u
+// of local copy c holds global unit u ^ (c & 7): the fragment reads (copy r,
+// unit 2s + h) then spread over the banks.  The compiler does not track
+// LDS-DMA: the ring is read by inline asm after an explicit vmcnt wait.
+__global__ __launch_bounds__(64) void k_rollout_leaf_mfma(const _Float16* __restrict__ b,
+                                                          const _Float16* __restrict__ zrow,
+                                                          long long cstride, int copies,
+                                                          long long ncells,
+                                                          const _Float16* __restrict__ B,
+                                                          long long ldb, float* __restrict__ part,
+                                                          int nslab) {
+  constexpr int kSlot = 64 * 128;  // bytes per stage: 64 copies x 64 cells
+  __shared__ __attribute__((aligned(16))) char ring[2 * kSlot];
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int slab = blockIdx.x, c0 = blockIdx.y * 64;
+  const long long cell0 = (long long)slab * kLeafSlab;
+  // DMA roles: copy 8i + dc, 8-cell unit du of the stage
+  const int dc = lane >> 3, du = (lane & 7) ^ dc;
+  // B has kLeafColsPad columns (zero past kLeafCols): every lane loads, no branch
+  const h8v* bp = reinterpret_cast<const h8v*>(B + (long long)r * ldb + cell0 + 8 * h);
+  constexpr int nst = kLeafSlab / 64;
+  static_assert(nst % 2 == 0, "stages in pairs");
+  auto issue = [&](int k, char* slot) {
+    const long long cell = cell0 + 64 * k + 8 * du;
+    const bool ok = cell < ncells;  // (ncells is a multiple of 8)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const _Float16* g = b + (long long)min(c0 + 8 * i + dc, copies - 1) * cstride + cell;
+      uintptr_t ga = (uintptr_t)(ok ? g : zrow);
+      asm("" : "+v"(ga));  // one VGPR-addressed DMA per i (not one per side of the select)
+      __builtin_amdgcn_global_load_lds((glb_void*)ga, (lds_void*)(slot + i * 1024), 16, 0, 0);
+    }
+  };
+  // B's fragments by inline asm as well: the compiler's own wait for them
+  // would be a vmcnt(0) (it does not follow the pipeline across the loop),
+  // which also drains the next stage's DMA; stage() waits for them itself
+  auto ldb4 = [&](int k, h8v (&y)[4]) {
+    const h8v* q = bp + 8 * k;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+      asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(y[st]) : "v"(q), "i"(32 * st) : "memory");
+  };
+  // the fragment reads of a stage: tile t, step st -> copy 32t + r, unit 2st + h
+  uint32_t roff[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+      roff[t][st] = (uint32_t)(((32 * t + r) * 8 + ((2 * st + h) ^ (r & 7))) * 16);
+  f16acc acc0 = {}, acc1 = {};
+  h8v B0[4], B1[4];
+  // stage k from slot k & 1 with B fragments Bk; stage k + 1 (slot and
+  // fragments Bn) issued first
+  auto stage = [&](int k, char* cur, char* nxt, h8v (&Bk)[4], h8v (&Bn)[4]) {
+    if (k + 1 < nst) {
+      asm volatile("" ::: "memory");  // slot nxt's reads (stage k-1) completed (lgkmcnt(0))
+      issue(k + 1, nxt);
+      ldb4(k + 1, Bn);
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // stage k's DMA and B loads landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    h8v A[2][4];
+    const uint32_t base = (uint32_t)(uintptr_t)cur;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+        asm volatile("ds_read_b128 %0, %1" : "=v"(A[t][st]) : "v"(base + roff[t][st]));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int st = 0; st < 4; ++st) asm volatile("" : "+v"(A[t][st]));
+#pragma unroll
+    for (int st = 0; st < 4; ++st) asm volatile("" : "+v"(Bk[st]));  // (landed: the vmcnt above)
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0][st], Bk[st], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[1][st], Bk[st], acc1, 0, 0, 0);
+    }
+  };
+  issue(0, ring);
+  ldb4(0, B0);
+  for (int k = 0; k < nst; k += 2) {
+    stage(k, ring, ring + kSlot, B0, B1);
+    stage(k + 1, ring + kSlot, ring, B1, B0);
+  }
+  // D: column r (= lane & 31), rows (v & 3) + 8 (v >> 2) + 4 h
+  if (r < kLeafCols) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int row = (v & 3) + 8 * (v >> 2) + 4 * h;
+      const int ca = c0 + row, cb = c0 + 32 + row;
+      if (ca < copies) part[((long long)ca * kLeafCols + r) * nslab + slab] = acc0[v];
+      if (cb < copies) part[((long long)cb * kLeafCols + r) * nslab + slab] = acc1[v];
+    }
+  }
+}
+
+// out[copy][10] = {sum, dot_0 .. dot_8}: per slab hi + lo, the slabs in a
+// fixed order, times 2^-k_i.
+__global__ __launch_bounds__(64) void k_rollout_leaf_mfma_reduce(const float* __restrict__ part, int nslab,
+                                                                 int copies, const int* __restrict__ kexp,
+                                                                 float* __restrict__ out) {
+  const int c = blockIdx.x;
+  if (c >= copies) return;
+  const float* pc = part + (long long)c * kLeafCols * nslab;
+  float s = 0.0f;
+  for (int j = threadIdx.x; j < nslab; j += 64) s += pc[j];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) out[c * 10] = s;
+  for (int q = 0; q < 9; ++q) {
+    float d = 0.0f;
+    for (int j = threadIdx.x; j < nslab; j += 64) d += pc[(1 + q) * nslab + j] + pc[(10 + q) * nslab + j];
+    d = wave_sum(d);
+    if (threadIdx.x == 0) out[c * 10 + 1 + q] = ldexpf(d, -kexp[q]);
+  }
+}
+
+}  // namespace
+
+bool rollout_leaf_mfma_ok(const Geom& g, long long cstride) {
+#ifdef PP2_LEAF_FMAF
+  return false;  // diagnostic A/B builds only: the fmaf pass everywhere
+#endif
+  return g.wp % 8 == 0 && cstride % 8 == 0;
+}
+long long rollout_leaf_ldb(const Geom& g) {
+  const long long n = (long long)g.rows * g.wp;
+  return (n + kLeafSlab - 1) / kLeafSlab * kLeafSlab;
+}
+size_t rollout_leaf_scratch_bytes(const Geom& g, int ncopies) {
+  const long long ldb = rollout_leaf_ldb(g), nslab = ldb / kLeafSlab;
+  return (size_t)kLeafColsPad * ldb * sizeof(_Float16) + 9 * kLeafParts * sizeof(float) + 64 +
+         (size_t)ncopies * kLeafCols * nslab * sizeof(float);
+}
+
+hipError_t launch_rollout_leaf_mfma(hipStream_t st, const Geom& g, PlaneSet F, const void* b,
+                                    long long cstride, int ncopies, void* scratch, float* out) {
+  const long long ldb = rollout_leaf_ldb(g), nslab = ldb / kLeafSlab;
+  _Float16* B = reinterpret_cast<_Float16*>(scratch);
+  float* amax = reinterpret_cast<float*>(B + (size_t)kLeafColsPad * ldb);
+  int* kexp = reinterpret_cast<int*>(amax + 9 * kLeafParts);
+  float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(kexp) + 64);
+  hipLaunchKernelGGL(k_leaf_alpha_max, dim3(kLeafParts, 9), dim3(256), 0, st, g, F, amax);
+  const unsigned pb = (unsigned)std::min<long long>((ldb + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_leaf_alpha_pack, dim3(pb), dim3(256), 0, st, g, F, amax, B, ldb, kexp);
+  hipLaunchKernelGGL(k_rollout_leaf_mfma, dim3((unsigned)nslab, (unsigned)((ncopies + 63) / 64)),
+                     dim3(64), 0, st, (const _Float16*)b + g.wp, (const _Float16*)b, cstride,
+                     ncopies, (long long)g.rows * g.wp, B, ldb, part, (int)nslab);
+  hipLaunchKernelGGL(k_rollout_leaf_mfma_reduce, dim3(ncopies), dim3(64), 0, st, part, (int)nslab,
+                     ncopies, kexp, out);
+  return hipGetLastError();
+}
+
 }  // namespace pp2
