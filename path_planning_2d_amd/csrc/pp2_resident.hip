@@ -410,6 +410,12 @@ __device__ __forceinline__ void take_rows_sides(Rsrc r, bool rows, int o, bool e
   e[0] = e[1] = m;
 #pragma unroll
   for (int k = 0; k < 3; ++k) s[k] = u2v{m, m};
+#ifdef PP2_RES_NOXCH
+  // diagnostic build only (tools/micro/resident_nowait.sh): no hand-off
+  // loads at all -- the neighbours' rows read as tagged zeros
+  g[0] = g[1] = u4v{m, m, m, m};
+  return;
+#endif
   for (int spin = 0;; ++spin) {
     if (rows) {
       g[0] = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, kSc1);

@@ -548,7 +548,11 @@ constexpr int kLeafColsPad = 32;   // B's columns in memory (the MFMA's N; zero 
 #ifndef PP2_LEAF_SLAB
 #define PP2_LEAF_SLAB 8192
 #endif
-constexpr int kLeafSlab = PP2_LEAF_SLAB;  // cells per block (B is padded to a multiple)
+#ifndef PP2_LEAF_NS
+#define PP2_LEAF_NS 2
+#endif
+constexpr int kLeafNS = PP2_LEAF_NS;  // LDS ring stages per wave (8 KB each)
+constexpr int kLeafSlab = PP2_LEAF_SLAB;  // cells per block (B is padded to a multiple; 64 x NS x n)
 constexpr int kLeafParts = 32;     // |alpha| max partials per plane
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f16acc __attribute__((ext_vector_type(16)));
@@ -625,7 +629,7 @@ __global__ __launch_bounds__(64) void k_rollout_leaf_mfma(const _Float16* __rest
                                                           long long ldb, float* __restrict__ part,
                                                           int nslab) {
   constexpr int kSlot = 64 * 128;  // bytes per stage: 64 copies x 64 cells
-  __shared__ __attribute__((aligned(16))) char ring[2 * kSlot];
+  __shared__ __attribute__((aligned(16))) char ring[kLeafNS * kSlot];
   const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
   const int slab = blockIdx.x, c0 = blockIdx.y * 64;
   const long long cell0 = (long long)slab * kLeafSlab;
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(64) void k_rollout_leaf_mfma(const _Float16* __rest
   // B has kLeafColsPad columns (zero past kLeafCols): every lane loads, no branch
   const h8v* bp = reinterpret_cast<const h8v*>(B + (long long)r * ldb + cell0 + 8 * h);
   constexpr int nst = kLeafSlab / 64;
-  static_assert(nst % 2 == 0, "stages in pairs");
+  static_assert(nst % kLeafNS == 0 && kLeafNS >= 2 && kLeafNS <= 3, "whole ring rounds");
   auto issue = [&](int k, char* slot) {
     const long long cell = cell0 + 64 * k + 8 * du;
     const bool ok = cell < ncells;  // (ncells is a multiple of 8)
@@ -663,20 +667,23 @@ __global__ __launch_bounds__(64) void k_rollout_leaf_mfma(const _Float16* __rest
     for (int st = 0; st < 4; ++st)
       roff[t][st] = (uint32_t)(((32 * t + r) * 8 + ((2 * st + h) ^ (r & 7))) * 16);
   f16acc acc0 = {}, acc1 = {};
-  h8v B0[4], B1[4];
-  // stage k from slot k & 1 with B fragments Bk; stage k + 1 (slot and
-  // fragments Bn) issued first
-  auto stage = [&](int k, char* cur, char* nxt, h8v (&Bk)[4], h8v (&Bn)[4]) {
-    if (k + 1 < nst) {
-      asm volatile("" ::: "memory");  // slot nxt's reads (stage k-1) completed (lgkmcnt(0))
-      issue(k + 1, nxt);
-      ldb4(k + 1, Bn);
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // stage k's DMA and B loads landed
+  h8v Bf[kLeafNS][4];
+  // stage k from slot k % NS with B fragments Bf[k % NS]; stage k + NS - 1
+  // (its slot, its fragments) issued first, so NS - 1 stages stay in flight
+  auto stage = [&](int k, auto kk) {
+    constexpr int q = decltype(kk)::value;  // k % NS
+    constexpr int qn = (q + kLeafNS - 1) % kLeafNS;
+    if (k + kLeafNS - 1 < nst) {
+      asm volatile("" ::: "memory");  // slot qn's reads (stage k-1) completed (lgkmcnt(0))
+      issue(k + kLeafNS - 1, ring + qn * kSlot);
+      ldb4(k + kLeafNS - 1, Bf[qn]);
+      // stage k's DMA and B loads landed (the NS - 1 younger groups of 12 may not have)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(12 * (kLeafNS - 1)) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     h8v A[2][4];
-    const uint32_t base = (uint32_t)(uintptr_t)cur;
+    const uint32_t base = (uint32_t)(uintptr_t)(ring + q * kSlot);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -688,18 +695,22 @@ __global__ __launch_bounds__(64) void k_rollout_leaf_mfma(const _Float16* __rest
 #pragma unroll
       for (int st = 0; st < 4; ++st) asm volatile("" : "+v"(A[t][st]));
 #pragma unroll
-    for (int st = 0; st < 4; ++st) asm volatile("" : "+v"(Bk[st]));  // (landed: the vmcnt above)
+    for (int st = 0; st < 4; ++st) asm volatile("" : "+v"(Bf[q][st]));  // (landed: the vmcnt above)
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0][st], Bk[st], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[1][st], Bk[st], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0][st], Bf[q][st], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[1][st], Bf[q][st], acc1, 0, 0, 0);
     }
   };
-  issue(0, ring);
-  ldb4(0, B0);
-  for (int k = 0; k < nst; k += 2) {
-    stage(k, ring, ring + kSlot, B0, B1);
-    stage(k + 1, ring + kSlot, ring, B1, B0);
+#pragma unroll
+  for (int j = 0; j < kLeafNS - 1; ++j) {
+    issue(j, ring + j * kSlot);
+    ldb4(j, Bf[j]);
+  }
+  for (int k = 0; k < nst; k += kLeafNS) {
+    stage(k, std::integral_constant<int, 0>{});
+    stage(k + 1, std::integral_constant<int, 1>{});
+    if constexpr (kLeafNS > 2) stage(k + 2, std::integral_constant<int, 2 % kLeafNS>{});
   }
   // D: column r (= lane & 31), rows (v & 3) + 8 (v >> 2) + 4 h
   if (r < kLeafCols) {

@@ -165,3 +165,42 @@ def test_rollout_runs_restart_from_root():
     for k in fresh:
         np.testing.assert_array_equal(again[k], fresh[k], err_msg=k)
     np.testing.assert_array_equal(b_again, b_fresh)
+
+
+@pytest.mark.parametrize("H,W,copies,scale", [(40, 64, 96, 1.0), (40, 64, 96, -3e5),
+                                              (300, 200, 130, 1e25), (300, 200, 130, -1e-20),
+                                              (37, 50, 61, 1.0), (37, 50, 61, -3e5)])
+def test_rollout_leaf_dots(H, W, copies, scale):
+    """The leaf FIB bound max_i <b_D, alpha_i> (fast_informed_bound_cuda.cu:
+    278-297) against float64 dots of the same stored fp16 beliefs, for alpha
+    planes of magnitude |scale| (random per plane and cell, so that the
+    argmax plane varies by copy): within rel 1e-5.  40 x 64 and 300 x 200
+    (8 slabs of cells, 130 copies: a partial 64-copy group) take the MFMA
+    pass (copy rows 16-B aligned, wp % 8 == 0), whose per-plane power-of-two
+    scaling and fp16 hi + lo split these magnitudes exercise; 37 x 50 (wp 52)
+    the fmaf pass."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(H, W, seed=H + W)
+    goal = S.synth_goal(grid)
+    b0 = S.uniform_belief(grid)
+    us, zs = S.rollout_trajectories(grid, b0, copies, 3, seed=3)
+    rng = np.random.default_rng(H * W)
+    alphas = (scale * (0.5 + rng.random((H * W, 9)))).astype(np.float32)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_set(alphas)
+        with P.BatchedRollout(ctx, copies, 3) as r:
+            r.set_root(b0)
+            r.run(us, zs)
+            res = r.results()
+            a64 = alphas.astype(np.float64)
+            winners = set()
+            for c in range(copies):
+                b = r.belief(c).astype(np.float64)
+                dots = (b @ a64) / b.sum()
+                winners.add(int(np.argmax(dots)))
+                ub = float(dots.max())
+                got = float(res["leaf_upper"][c])
+                assert abs(got - ub) <= 1e-5 * abs(ub), (c, got, ub)
+            assert len(winners) >= 3, winners

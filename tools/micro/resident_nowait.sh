@@ -16,3 +16,6 @@ make -C "$CS" -j8 OUT="$HERE/_nowait/libpp2_nobar.so" OBJDIR="$HERE/_nowait/obj_
   EXTRA_FLAGS=-DPP2_RES_NOBAR "$HERE/_nowait/libpp2_nobar.so"
 make -C "$CS" -j8 OUT="$HERE/_nowait/libpp2_nowait_nobar.so" OBJDIR="$HERE/_nowait/obj_both" \
   EXTRA_FLAGS="-DPP2_RES_NOWAIT -DPP2_RES_NOBAR" "$HERE/_nowait/libpp2_nowait_nobar.so"
+# ... and with no hand-off loads at all (-DPP2_RES_NOXCH: the neighbours' rows read as zeros)
+make -C "$CS" -j8 OUT="$HERE/_nowait/libpp2_noxch.so" OBJDIR="$HERE/_nowait/obj_noxch" \
+  EXTRA_FLAGS=-DPP2_RES_NOXCH "$HERE/_nowait/libpp2_noxch.so"
