@@ -125,11 +125,13 @@ hipError_t launch_rollout_leaf(hipStream_t st, const Geom& g, PlaneSet F, const 
                                long long cstride, int ncopies, float* partials, float* out);
 // The leaf pass on the matrix cores (pp2_rollout_dev.hip): usable when
 // rollout_leaf_mfma_ok (16-B aligned copy rows); scratch of
-// rollout_leaf_scratch_bytes (B columns, scales, per-slab partials).
+// rollout_leaf_scratch_bytes (B columns, scales, per-slab partials).  pack:
+// rebuild B and the scales from F (false: the scratch holds them for F).
 bool rollout_leaf_mfma_ok(const Geom& g, long long cstride);
 size_t rollout_leaf_scratch_bytes(const Geom& g, int ncopies);
 hipError_t launch_rollout_leaf_mfma(hipStream_t st, const Geom& g, PlaneSet F, const void* b,
-                                    long long cstride, int ncopies, void* scratch, float* out);
+                                    long long cstride, int ncopies, void* scratch, float* out,
+                                    bool pack);
 
 // Dictionary-coded model (pp2_coded.hip).  code: uint16 per cell over rows
 // [-1, rows] (same geometry as a plane); dict: kDictRow floats per entry,

@@ -32,6 +32,8 @@ struct pp2_rollout {
   float* d_leaf = nullptr;         // [copies][10]
   float* d_partials = nullptr;     // [copies][waves][10]
   void* d_leafmm = nullptr;        // the MFMA leaf pass's scratch (null: the fmaf pass)
+  unsigned leaf_fib_version = 0;   // the context's fib_version packed into it (0: none)
+  int leaf_fcur = -1;              // ... and the FIB buffer it came from
   int* d_chunks = nullptr;         // per step: u[], first[], n[] (maxchunks each), copies[]
   uint8_t* d_zs = nullptr;         // [depth][copies]
   int maxchunks = 0;
@@ -188,12 +190,16 @@ int pp2_rollout_run(pp2_rollout* r, const uint8_t* us, const uint8_t* zs) {
                                     r->d_stats + (size_t)k * C * kRollStats, r->d_partials,
                                     r->d_stats + (size_t)(k + 1) * C * kRollStats, C));
   }
-  if (r->d_leafmm)
+  if (r->d_leafmm) {
+    const bool pack = r->leaf_fib_version != c->fib_version || r->leaf_fcur != c->fcur;
     HIPCHK(pp2::launch_rollout_leaf_mfma(c->stream, c->g, c->fib[c->fcur].v, r->buf[D & 1],
-                                         r->cstride, C, r->d_leafmm, r->d_leaf));
-  else
+                                         r->cstride, C, r->d_leafmm, r->d_leaf, pack));
+    r->leaf_fib_version = c->fib_version;
+    r->leaf_fcur = c->fcur;
+  } else {
     HIPCHK(pp2::launch_rollout_leaf(c->stream, c->g, c->fib[c->fcur].v, r->buf[D & 1],
                                     r->cstride, C, r->d_partials, r->d_leaf));
+  }
   r->ran = true;
   return PP2_OK;
 }

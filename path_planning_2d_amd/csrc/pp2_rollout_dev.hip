@@ -763,15 +763,18 @@ size_t rollout_leaf_scratch_bytes(const Geom& g, int ncopies) {
 }
 
 hipError_t launch_rollout_leaf_mfma(hipStream_t st, const Geom& g, PlaneSet F, const void* b,
-                                    long long cstride, int ncopies, void* scratch, float* out) {
+                                    long long cstride, int ncopies, void* scratch, float* out,
+                                    bool pack) {
   const long long ldb = rollout_leaf_ldb(g), nslab = ldb / kLeafSlab;
   _Float16* B = reinterpret_cast<_Float16*>(scratch);
   float* amax = reinterpret_cast<float*>(B + (size_t)kLeafColsPad * ldb);
   int* kexp = reinterpret_cast<int*>(amax + 9 * kLeafParts);
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(kexp) + 64);
-  hipLaunchKernelGGL(k_leaf_alpha_max, dim3(kLeafParts, 9), dim3(256), 0, st, g, F, amax);
-  const unsigned pb = (unsigned)std::min<long long>((ldb + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_leaf_alpha_pack, dim3(pb), dim3(256), 0, st, g, F, amax, B, ldb, kexp);
+  if (pack) {  // (B and the scales of the same alphas are still in the scratch otherwise)
+    hipLaunchKernelGGL(k_leaf_alpha_max, dim3(kLeafParts, 9), dim3(256), 0, st, g, F, amax);
+    const unsigned pb = (unsigned)std::min<long long>((ldb + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_leaf_alpha_pack, dim3(pb), dim3(256), 0, st, g, F, amax, B, ldb, kexp);
+  }
   hipLaunchKernelGGL(k_rollout_leaf_mfma, dim3((unsigned)nslab, (unsigned)((ncopies + 63) / 64)),
                      dim3(64), 0, st, (const _Float16*)b + g.wp, (const _Float16*)b, cstride,
                      ncopies, (long long)g.rows * g.wp, B, ldb, part, (int)nslab);

@@ -204,3 +204,39 @@ def test_rollout_leaf_dots(H, W, copies, scale):
                 got = float(res["leaf_upper"][c])
                 assert abs(got - ub) <= 1e-5 * abs(ub), (c, got, ub)
             assert len(winners) >= 3, winners
+
+
+def test_rollout_leaf_follows_fib():
+    """The MFMA leaf pass keeps the packed alpha columns between runs while
+    the context's FIB alphas are unchanged, and repacks them after fib_set /
+    fib_sweep: a second run repeats the bound bit for bit, alphas x 2 (exact)
+    give exactly twice the bound, and after a FIB sweep the bound follows the
+    new alphas."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    H, W, copies = 40, 64, 70
+    grid = S.synth_grid(H, W, seed=77)
+    goal = S.synth_goal(grid)
+    b0 = S.uniform_belief(grid)
+    us, zs = S.rollout_trajectories(grid, b0, copies, 2, seed=4)
+    rng = np.random.default_rng(5)
+    alphas = (-20.0 * (0.5 + rng.random((H * W, 9)))).astype(np.float32)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_set(alphas)
+        with P.BatchedRollout(ctx, copies, 2) as r:
+            def leaf():
+                r.set_root(b0)
+                r.run(us, zs)
+                return r.results()["leaf_upper"].copy()
+            l1 = leaf()
+            np.testing.assert_array_equal(leaf(), l1)
+            ctx.fib_set(2.0 * alphas)
+            np.testing.assert_array_equal(leaf(), 2.0 * l1)
+            ctx.fib_sweep(1)
+            l3 = leaf()
+            a = ctx.fib_get().astype(np.float64)
+            for c in (0, copies - 1):
+                b = r.belief(c).astype(np.float64)
+                ub = float(((b @ a) / b.sum()).max())
+                assert abs(l3[c] - ub) <= 1e-5 * abs(ub), (c, l3[c], ub)
