@@ -291,40 +291,47 @@ def cpu_baseline(grid, goal, us, zs, budget_s):
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
-def closed_loop(grid, b0, step_fn, max_steps, budget_s):
-    """Closed-loop plan steps: the planner's action moves a simulated robot
-    (T), whose observation (L) is the next message.  Returns the wall time of
-    each step in ms."""
+def closed_loop(grid, b0, step_fn, max_steps, budget_s=1e9, min_steps=0):
+    """Closed-loop plan steps (synthetic.closed_loop): (ms, actions, values)."""
     from path_planning_2d_amd import synthetic as S
-    rng = S.SplitMix64(99)
-    x, y = S.start_cell(grid)
-    times = []
-    a, z, first = 0, 0, True
-    t_start = time.perf_counter()
-    for _ in range(max_steps):
-        t = time.perf_counter()
-        a, _ = step_fn(a, z, b0 if first else None)
-        times.append(time.perf_counter() - t)
-        first = False
-        tp = S.cell_transition(grid, x, y, a)
-        r, c, j = rng.u01(), 0.0, 4
-        for i in range(9):
-            c += float(tp[i])
-            if tp[i] > 0 and r < c:
-                j = i
-                break
-        x += j % 3 - 1
-        y += j // 3 - 1
-        lk = S.cell_likelihood(grid, x, y)
-        r, c, z = rng.u01(), 0.0, 15
-        for i in range(16):
-            c += float(lk[i])
-            if r < c:
-                z = i
-                break
-        if time.perf_counter() - t_start > budget_s:
-            break
-    return np.array(times) * 1e3
+    return S.closed_loop(grid, b0, step_fn, max_steps, budget_s, min_steps=min_steps)
+
+
+def step_stats(ms):
+    return {"steps": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
+            "p90_ms": float(np.percentile(ms, 90)), "mean_ms": float(ms.mean())}
+
+
+def gpu_plan_run(grid, b0, make_planner, steps):
+    """A warm-up of 3 closed-loop steps (code objects, allocations) on one
+    planner, then `steps` timed steps on a fresh one (the warm-up advanced
+    the first planner's rand() stream, which a reset keeps): (ms, actions,
+    values, tree info after the last step)."""
+    with make_planner() as pl:
+        closed_loop(grid, b0, pl.step, 3)
+    with make_planner() as pl:
+        ms, acts, vals = closed_loop(grid, b0, pl.step, steps)
+        return ms, acts, vals, pl.info()
+
+
+def oracle_plan_run(grid, b0, opl, steps, budget_s, min_steps, gpu_acts, gpu_vals, what):
+    """The oracle's reference-arithmetic QV-tree (oracle/pp2_oracle_tree.c,
+    every node holding its own host belief, sequential fp32 sums) on the same
+    closed loop: its plan-step times beside the GPU's, and the parity gate
+    -- the GPU's actions and values equal the oracle's at every step the
+    CPU leg ran (synthetic.action_parity)."""
+    from path_planning_2d_amd import synthetic as S
+    cms, ca, cv = closed_loop(grid, b0, opl.step, steps, budget_s, min_steps=min_steps)
+    cpu = {"p50_ms": float(np.percentile(cms, 50)), "p90_ms": float(np.percentile(cms, 90)),
+           "steps": int(cms.size), "cores": 1, "kind": "port",
+           "sample": f"{cms.size} closed-loop plan steps of the oracle's reference-semantics "
+                     f"QV-tree (oracle/pp2_oracle_tree.c, every node holds a host belief), "
+                     f"{what}"}
+    parity = S.action_parity(gpu_acts, gpu_vals, ca, cv)
+    parity["reference"] = ("oracle/pp2_oracle_tree.c in reference arithmetic on the same "
+                           "seeded closed loop: actions equal and values equal as fp32 bits "
+                           "at every compared step")
+    return cpu, parity
 
 
 def plan_step_bench(args, device, stream_handle, with_cpu):
@@ -333,7 +340,9 @@ def plan_step_bench(args, device, stream_handle, with_cpu):
     bound -5/(1-gamma)).  Closed loop: the planner's action moves a simulated
     robot (T), whose observation (L) is the next message.  Wall time of each
     plan step (tree update + expansions + argmax), as beliefCallback measures
-    it (src/pomdp/path_planning_2d.cu:210-231)."""
+    it (src/pomdp/path_planning_2d.cu:210-231).  With the CPU leg, the parity
+    gate: the GPU's actions and values equal the reference-arithmetic oracle's
+    at every step the oracle ran (>= 100)."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S
     N = args.plan_size
@@ -348,36 +357,27 @@ def plan_step_bench(args, device, stream_handle, with_cpu):
     alphas = ctx.fib_get()
     b0 = S.uniform_belief(grid)
 
-    def run(step_fn, max_steps, budget_s):
-        return closed_loop(grid, b0, step_fn, max_steps, budget_s)
-
     # the drop-in's mode (pp2_planner_default_params: reference_order = 1):
     # bit-exact with the reference's fp32 host arithmetic -- the headline p50
-    with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
-                         max_online_iteration=15, reference_order=1) as pl:
-        run(pl.step, 3, 1e9)  # warm-up (code objects, allocations)
-        pl.reset()
-        ms = run(pl.step, args.plan_steps, 1e9)
-        info = pl.info()
+    ms, acts, vals, info = gpu_plan_run(
+        grid, b0, lambda: P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
+                                          max_online_iteration=15, reference_order=1),
+        args.plan_steps)
     # opt-in fast variant (reference_order = 0): parallel tree / fp64 sums,
     # within rel 1e-4 of the reference arithmetic, NOT bit-exact
-    with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
-                         max_online_iteration=15, reference_order=0) as pl:
-        run(pl.step, 2, 1e9)
-        pl.reset()
-        ms_ts = run(pl.step, args.plan_steps, 1e9)
+    ms_ts, _, _, _ = gpu_plan_run(
+        grid, b0, lambda: P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
+                                          max_online_iteration=15, reference_order=0),
+        args.plan_steps)
     ctx.close()
     out = {"config": f"{N}x{N} synthetic grid, max_search_tree_depth {args.plan_depth}, "
                      f"max_online_iteration 15, FIB upper bound ({fib_sweeps} sweeps, "
                      f"{fib_s * 1e3:.1f} ms on GPU), lower bound -5/(1-gamma)",
            "mode": "reference_order=1 (default; bit-exact with the reference's host "
                    "fp32 arithmetic)",
-           "steps": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
-           "p90_ms": float(np.percentile(ms, 90)), "mean_ms": float(ms.mean()),
+           **step_stats(ms),
            "first_ms": float(ms[0]), "final_tree_vnodes": int(info["total_vnodes"]),
-           "tree_sum_variant": {"steps": int(ms_ts.size),
-                                "p50_ms": float(np.percentile(ms_ts, 50)),
-                                "p90_ms": float(np.percentile(ms_ts, 90)),
+           "tree_sum_variant": {**step_stats(ms_ts),
                                 "note": "opt-in reference_order=0: grid-wide sums as "
                                         "parallel trees, within rel 1e-4 of the reference "
                                         "arithmetic, NOT bit-exact"}}
@@ -385,14 +385,46 @@ def plan_step_bench(args, device, stream_handle, with_cpu):
         from oracle import oracle as O
         T, L, R = O.model_pomdp(grid, goal)
         opl = O.Planner(grid, T, L, R, alphas, max_depth=args.plan_depth, max_iter=15)
-        cms = run(opl.step, args.plan_steps, args.cpu_plan_seconds)
+        out["cpu_baseline"], out["parity"] = oracle_plan_run(
+            grid, b0, opl, args.plan_steps, args.cpu_plan_seconds, 100, acts, vals,
+            "same grid/alphas")
         opl.close()
-        out["cpu_baseline"] = {
-            "p50_ms": float(np.percentile(cms, 50)), "p90_ms": float(np.percentile(cms, 90)),
-            "steps": int(cms.size), "cores": 1, "kind": "port",
-            "sample": f"{cms.size} closed-loop plan steps of the oracle's reference-semantics "
-                      f"QV-tree (oracle/pp2_oracle_tree.c, every node holds a host belief), "
-                      f"same grid/alphas"}
+    return out
+
+
+def pbvi_plan_leg(args, ctx, grid, b0, calls, depth, with_cpu, cpu_budget, min_cpu_steps, what):
+    """Closed-loop plan steps with PBVI leaf lower bounds (lower_bound_mode 1,
+    evaluatePbviCpu per VNode, search_tree_cuda.cu:379) on a context that
+    holds the PBVI alphas, the tree's rand() stream continuing after
+    generateBeliefSet's `calls` draws (PomdpPathPlanning2d::initialize runs
+    PBVI before the first plan step).  Reference order (the drop-in's mode)
+    timed and parity-gated against the oracle; the tree-sum variant timed."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    def planner(ref):
+        return lambda: P.QVTreePlanner(ctx, max_search_tree_depth=depth,
+                                       max_online_iteration=15, lower_bound_mode=1,
+                                       rand_skip=calls, reference_order=ref)
+    ms, acts, vals, _ = gpu_plan_run(grid, b0, planner(1), args.plan_steps)
+    ms_ts, _, _, _ = gpu_plan_run(grid, b0, planner(0), args.plan_steps)
+    out = {"mode": "reference_order=1 (default; bit-exact)", "config": what, **step_stats(ms),
+           "tree_sum_variant": {
+               **step_stats(ms_ts),
+               "note": "opt-in reference_order=0 (PBVI dots by the split-x MFMA GEMM, not the "
+                       "reference's x-ordered chains): NOT bit-exact"}}
+    if with_cpu:
+        from oracle import oracle as O
+        H, W = grid.shape
+        goal = ctx.goal
+        T, L, R = O.model_pomdp(grid, goal)
+        pal, pact = ctx.pbvi_get()
+        opl = O.Planner(grid, T, L, R, ctx.fib_get(), max_depth=depth, max_iter=15)
+        opl.set_pbvi(pal, pact)
+        opl.skip_rand(calls)
+        out["cpu_baseline"], out["parity"] = oracle_plan_run(
+            grid, b0, opl, args.plan_steps, cpu_budget, min_cpu_steps, acts, vals,
+            "same grid, FIB and PBVI alphas, rand() stream")
+        opl.close()
     return out
 
 
@@ -400,10 +432,14 @@ def pbvi_bench(args, device, stream_handle, with_cpu):
     """PBVI lower bound (point_based_value_iteration_cuda.cu): the reference
     node's configuration -- S = 500 beliefs on the 100x40 map, 167 backups
     (gamma 0.95) -- end to end, and the same at 256x256 (BASELINE configs[1]'s
-    grid, which the reference cannot run), followed there by
-    closed-loop plan steps with PBVI leaf lower bounds.  `gemm_equiv_tflops` = the iteration's Sgemm flops (2 * 144 *
-    Sp^2 * ld) / the whole iteration's time: a lower bound on the MFMA GEMM
-    kernel's own rate (its rocprof time is in profiles/)."""
+    grid, which the reference cannot run).  Each is followed
+    by closed-loop plan steps with PBVI leaf lower bounds: on the 100x40 map
+    the reference node's own launch configuration (`node_plan_step`: goal
+    (95, 34), max_search_tree_depth 50, max_online_iteration 15,
+    launch/pomdp_path_planning_2d.launch:7-14), at 256x256 depth 3.
+    `gemm_equiv_tflops` = the iteration's Sgemm flops (2 * 144 * Sp^2 * ld) /
+    the whole iteration's time: a lower bound on the MFMA GEMM kernel's own
+    rate (its rocprof time is in profiles/)."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S
     gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden")
@@ -422,40 +458,33 @@ def pbvi_bench(args, device, stream_handle, with_cpu):
             ctx.pbvi_backup(1)
             ctx.synchronize()
             t0 = time.perf_counter()
-            ctx.pbvi_belief_set(b0, args.pbvi_S)
+            calls = ctx.pbvi_belief_set(b0, args.pbvi_S)
             ctx.synchronize()
             t_set = time.perf_counter() - t0
             t0 = time.perf_counter()
             ctx.pbvi_backup(iters)
             ctx.synchronize()
             t_bk = time.perf_counter() - t0
-            plan = None
-            if iters == 0 and grid.shape == (256, 256) and args.plan_steps > 0:
-                # BASELINE configs[1] with the reference node's PBVI leaf bounds
-                # (the reference itself falls back to -5/(1-gamma) there)
+            plan = node = None
+            if iters == 0 and args.plan_steps > 0:
                 ctx.fib_solve()
-                with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
-                                     max_online_iteration=15, lower_bound_mode=1) as pl:
-                    closed_loop(grid, b0, pl.step, 3, 1e9)
-                    pl.reset()
-                    ms = closed_loop(grid, b0, pl.step, args.plan_steps, 1e9)
-                with P.QVTreePlanner(ctx, max_search_tree_depth=args.plan_depth,
-                                     max_online_iteration=15, lower_bound_mode=1,
-                                     reference_order=0) as pl:
-                    closed_loop(grid, b0, pl.step, 3, 1e9)
-                    pl.reset()
-                    ms_ts = closed_loop(grid, b0, pl.step, args.plan_steps, 1e9)
-                plan = {"mode": "reference_order=1 (default; bit-exact)",
-                        "config": f"256x256 synthetic grid, max_search_tree_depth {args.plan_depth}, "
-                                  f"max_online_iteration 15, FIB upper bound, PBVI lower bound "
-                                  f"(S={args.pbvi_S}, 167 backups)",
-                        "steps": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
-                        "p90_ms": float(np.percentile(ms, 90)), "mean_ms": float(ms.mean()),
-                        "tree_sum_variant": {
-                            "steps": int(ms_ts.size), "p50_ms": float(np.percentile(ms_ts, 50)),
-                            "p90_ms": float(np.percentile(ms_ts, 90)),
-                            "note": "opt-in reference_order=0 (PBVI dots by the split-x MFMA "
-                                    "GEMM, not the reference's x-ordered chains): NOT bit-exact"}}
+                if grid.shape == (256, 256):
+                    # BASELINE configs[1] with the reference node's PBVI leaf
+                    # bounds (the reference itself falls back to -5/(1-gamma))
+                    plan = pbvi_plan_leg(
+                        args, ctx, grid, b0, calls, args.plan_depth, with_cpu,
+                        args.cpu_plan_seconds, 3,
+                        f"256x256 synthetic grid, max_search_tree_depth {args.plan_depth}, "
+                        f"max_online_iteration 15, FIB upper bound, PBVI lower bound "
+                        f"(S={args.pbvi_S}, 167 backups)")
+                elif grid.shape == (40, 100):
+                    node = pbvi_plan_leg(
+                        args, ctx, grid, b0, calls, 50, with_cpu, args.cpu_plan_seconds, 10,
+                        f"the reference node's launch configuration: sparse_map_100x40, goal "
+                        f"(95, 34), max_search_tree_depth 50, max_online_iteration 15, FIB "
+                        f"upper bound, PBVI lower bound (S={args.pbvi_S}, 167 backups), "
+                        f"rand() continuing after generateBeliefSet "
+                        f"(launch/pomdp_path_planning_2d.launch:7-14)")
             n_it = iters if iters > 0 else int(np.ceil(np.log(np.float32(1e-3) / np.float32(5))
                                                        / np.log(np.float32(GAMMA))))
             Sp = (args.pbvi_S + 127) // 128 * 128
@@ -471,6 +500,8 @@ def pbvi_bench(args, device, stream_handle, with_cpu):
                     "root_lower_bound": float(v[0])}
         if plan is not None:
             out[key]["plan_step_pbvi_lb"] = plan
+        if node is not None:
+            out[key]["node_plan_step"] = node
     if with_cpu:
         from oracle import oracle as O
         grid = cases[0][1]
@@ -712,7 +743,13 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
                 "rccl_rounds_per_call": rounds,
                 "us_per_step": [lo, hi],
                 "note": "measured per-rank step + rounds x assumed RCCL round trip / steps; "
-                        "a projection, not a measurement (one GPU)"}}
+                        "a projection, not a measurement (one GPU)",
+                "assumption": "every round costs the assumed neighbour round trip, including "
+                              "the later blocks' rounds in which the {mass, shift, lost} "
+                              "records go point to point to all nranks - 1 peers of the halo "
+                              "group (exchange_halos_k, records=true): an 8-peer grouped "
+                              "send/recv is priced like a 2-neighbour exchange; not measured "
+                              "(the 1-rank communicator skips the records loop)"}}
 
 
 def weak_rank_share(args, local, stream, n1_cells_per_s):

@@ -397,11 +397,12 @@ int orc_fib_solve(int H, int W, float gamma, const float* T, const float* L,
 /* ---- leaves ---------------------------------------------------------------- */
 void orc_fib_eval(size_t n, const float* b, const float* alphas, float* value,
                   uint8_t* action) {
-  float v[9];
-  for (int i = 0; i < 9; ++i) {
-    float s = 0.0f;
-    for (size_t k = 0; k < n; ++k) s = s + b[k] * alphas[9 * k + i];
-    v[i] = s;
+  /* evaluateFibCpu (fast_informed_bound_cuda.cu:278-297): nine x-ordered
+   * fp32 inner_products, walked side by side (independent chains) */
+  float v[9] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  for (size_t k = 0; k < n; ++k) {
+    const float bk = b[k];
+    for (int i = 0; i < 9; ++i) v[i] = v[i] + bk * alphas[9 * k + i];
   }
   int best = 0; /* std::max_element: first maximum */
   for (int i = 1; i < 9; ++i)
@@ -410,11 +411,26 @@ void orc_fib_eval(size_t n, const float* b, const float* alphas, float* value,
   *action = (uint8_t)best; /* host_fib_actions = {0..8} */
 }
 
+/* evaluatePbviCpu (point_based_value_iteration_cuda.cu:678-699): per alpha
+ * one x-ordered fp32 inner_product, then the first maximum.  Eight alphas'
+ * chains are walked side by side (independent chains, each still added in
+ * x order: the same bits, without the add latency of a single chain). */
 void orc_pbvi_eval(size_t n, const float* b, int S, const float* alphas,
                    const uint8_t* actions, float* value, uint8_t* action) {
   int best = 0;
   float bv = 0.0f;
-  for (int i = 0; i < S; ++i) {
+  int i = 0;
+  for (; i + 8 <= S; i += 8) {
+    const float* al = alphas + (size_t)i * n;
+    float s[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (size_t k = 0; k < n; ++k) {
+      const float bk = b[k];
+      for (int m = 0; m < 8; ++m) s[m] = s[m] + bk * al[(size_t)m * n + k];
+    }
+    for (int m = 0; m < 8; ++m)
+      if (i + m == 0 || bv < s[m]) { bv = s[m]; best = i + m; }
+  }
+  for (; i < S; ++i) {
     float s = 0.0f;
     const float* al = alphas + (size_t)i * n;
     for (size_t k = 0; k < n; ++k) s = s + b[k] * al[k];

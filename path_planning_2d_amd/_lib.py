@@ -142,10 +142,20 @@ def load() -> C.CDLL:
             raise ImportError(f"{LIB_PATH} does not export {name}")
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, C.c_int)
-    ver = lib.pp2_abi_version()
-    if ver != PP2_ABI_VERSION and os.environ.get("PP2_ALLOW_PARTIAL_ABI") != "1":
-        raise ImportError(f"{LIB_PATH} has ABI version {ver}, this package expects "
-                          f"{PP2_ABI_VERSION} (rebuild the library)")
+    partial = os.environ.get("PP2_ALLOW_PARTIAL_ABI") == "1"
+    if getattr(lib, "pp2_abi_version", None) is not None:
+        ver = lib.pp2_abi_version()
+    elif partial:
+        ver = 0  # a diagnostic build older than the version symbol
+    else:
+        raise ImportError(f"{LIB_PATH} does not export pp2_abi_version")
+    if ver != PP2_ABI_VERSION:
+        if not partial:
+            raise ImportError(f"{LIB_PATH} has ABI version {ver}, this package expects "
+                              f"{PP2_ABI_VERSION} (rebuild the library)")
+        import warnings
+        warnings.warn(f"PP2_ALLOW_PARTIAL_ABI: {LIB_PATH} has ABI version {ver}, "
+                      f"expected {PP2_ABI_VERSION}")
     _lib = lib
     return lib
 

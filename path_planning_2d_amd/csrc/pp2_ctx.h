@@ -55,6 +55,9 @@ constexpr int kShardHalo = 128;
 // far below FLT_MAX.  Reads divide by the true mass.
 constexpr float kBlockScale = 79228162514264337593543950336.0f;  // 2^96
 constexpr int kMaxNormBlock = 8;
+// a lagged resident shard block (depth <= kMaxNormBlock) reuses mass ring
+// slots race-free only while 3 depth + 1 < kResidentRing (launch_loop_resident)
+static_assert(3 * kMaxNormBlock + 1 < pp2::kResidentRing, "normalisation block vs mass ring");
 
 // A set of K planes over rows [-1, rows] (one halo row each side).
 struct Planes {

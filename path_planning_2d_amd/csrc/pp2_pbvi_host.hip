@@ -311,10 +311,14 @@ __device__ __forceinline__ float pair_step(float acc, float a, float b) {
 // CH x-values per chunk; the next chunk's loads are issued into registers
 // before the current chunk's chains run (one global round trip per chunk
 // would otherwise bound the small shape: 2048 chunks x ~1 us at 256^2).
+// With alist, A row i is row alist[i] of A (i < *acount, the block's rows
+// past it idle) and its results go to out row alist[i].
 template <int OP, int TA, int NC, int CH>
 __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A, int na,
                                                     const float* __restrict__ B, int nb, int ld,
-                                                    int n, float* __restrict__ out, int ldo) {
+                                                    int n, float* __restrict__ out, int ldo,
+                                                    const int* __restrict__ alist,
+                                                    const int* __restrict__ acount) {
   constexpr int G = 256 / TA, TB = G * NC;
   constexpr int kRowVec = CH / 4;                      // float4 per row of a chunk
   constexpr int LA = (TA * kRowVec + 255) / 256;       // float4 loads per thread
@@ -323,6 +327,11 @@ __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A,
   __shared__ __attribute__((aligned(16))) float sB[TB][CH + 4];
   const int tid = threadIdx.x, la = tid % TA, jg = tid / TA;
   const int i0 = blockIdx.x * TA, j0 = blockIdx.y * TB;
+  if (alist) {
+    na = min(na, *acount);
+    if (i0 >= na) return;  // (uniform over the block)
+  }
+  auto arow = [&](int i) { return alist ? alist[i] : i; };
   float acc[NC];
 #pragma unroll
   for (int m = 0; m < NC; ++m) acc[m] = 0.0f;
@@ -332,7 +341,7 @@ __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A,
     for (int q = 0; q < LA; ++q) {
       const int e = tid + 256 * q, row = e / kRowVec, c4 = (e % kRowVec) * 4, ia = i0 + row;
       ra[q] = e < TA * kRowVec && ia < na && x0 + c4 < n
-                  ? *(const f4*)(A + (long long)ia * ld + x0 + c4) : f4{0, 0, 0, 0};
+                  ? *(const f4*)(A + (long long)arow(ia) * ld + x0 + c4) : f4{0, 0, 0, 0};
     }
 #pragma unroll
     for (int q = 0; q < LB; ++q) {
@@ -384,10 +393,11 @@ __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A,
     __syncthreads();
   }
   if (i0 + la < na) {
+    const long long orow = arow(i0 + la);
 #pragma unroll
     for (int mm = 0; mm < NC; ++mm) {
       const int j = j0 + jg * NC + mm;
-      if (j < nb) out[(long long)(i0 + la) * ldo + j] = acc[mm];
+      if (j < nb) out[orow * ldo + j] = acc[mm];
     }
   }
 }
@@ -727,8 +737,10 @@ hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float
 }
 
 hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, const float* B,
-                             int nb, int ld, int n, float* out, int ldo) {
+                             int nb, int ld, int n, float* out, int ldo, const int* alist,
+                             const int* acount) {
   if (na <= 0 || nb <= 0) return hipSuccess;
+  if ((alist == nullptr) != (acount == nullptr)) return hipErrorInvalidValue;
   // the large shape while it gives the CUs a block each, else the small one
 #ifndef PP2_PAIR_NC  // (A/B builds: chains per thread of the small shape)
 #define PP2_PAIR_NC 1
@@ -741,7 +753,7 @@ hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, con
   const dim3 grid = big ? dim3(cdiv(na, 64), cdiv(nb, 64)) : dim3(cdiv(na, 16), cdiv(nb, 16 * kNc));
 #define PP2_PAIR(OPV, TAV, NCV, CHV)                                                        \
   hipLaunchKernelGGL((k_pair_chain<OPV, TAV, NCV, CHV>), grid, dim3(256), 0, st, A, na, B, nb, ld, \
-                     n, out, ldo)
+                     n, out, ldo, alist, acount)
   if (op == PAIR_L1) {
     if (big) PP2_PAIR(PAIR_L1, 64, 16, 32);
     else PP2_PAIR(PAIR_L1, 16, kNc, kCh);

@@ -55,9 +55,12 @@ hipError_t launch_rows_div(hipStream_t st, float* A, int ld, int rows, int n,
 hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float* B, int ld,
                            int rows, int n, float* out);
 // out[i*ldo + j] = x-ordered sum over x < n of |A[i][x] - B[j][x]| (PAIR_L1)
-// or A[i][x] * B[j][x] (PAIR_DOT, multiply then add), i < na, j < nb.
+// or A[i][x] * B[j][x] (PAIR_DOT, multiply then add), i < na, j < nb.  With
+// a device row list (alist, acount): the rows alist[i], i < min(na, *acount),
+// of A, results in out rows alist[i] (the other rows of out untouched).
 hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, const float* B,
-                             int nb, int ld, int n, float* out, int ldo);
+                             int nb, int ld, int n, float* out, int ldo,
+                             const int* alist = nullptr, const int* acount = nullptr);
 // The three draws of generateBeliefSet per (belief i, action a): state from
 // cdf row i, next state from T[s][a][:], observation from L[ns][:].
 hipError_t launch_pbvi_sample(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,

@@ -1244,6 +1244,9 @@ hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const Res
   if (a.red_lds && (a.shard != 2 || a.kstep0 != 0 || a.nparts > kResRedFloats || lds > kDictLdsMaxBytes))
     return hipErrorInvalidValue;
   const bool lag = a.shard == 2;
+  // lagged block starts read ring slot t - depth while the fastest tiles can
+  // be 2 depth + 1 steps ahead: slot reuse is race-free only below the ring
+  if (lag && 3 * a.depth + 1 >= kResidentRing) return hipErrorInvalidValue;
   if (p.tr && (p.tc != 1 || !a.shard || a.own0 % 4 != 0 || a.own1 % 4 != 0 || a.ows < a.g.rows))
     return hipErrorInvalidValue;
 #define PP2_RES_LAUNCH(CAPV, TCV, TRV)                                                           \

@@ -142,6 +142,7 @@ struct pp2_planner {
 
   std::vector<Slot> slots;
   std::vector<int> free_slots;
+  std::vector<void*> arenas;    // reference order: slot rows and masses, a chunk of slots each
   Planes P;                     // 9 prediction planes (scratch)
   float* d_rpart = nullptr;     // tiles * 9
   float* d_spart = nullptr;     // tiles * 16 * 90
@@ -220,23 +221,43 @@ bool host_mapped(size_t count, float** host, float** dev) {
   return hipHostGetDevicePointer((void**)dev, *host, 0) == hipSuccess;
 }
 
+// Reference order: slots come in chunks of rows from one allocation (one
+// hipMalloc and one memset per chunk, not per kept child: every kept child
+// of an expansion takes a row), about 64 MB per chunk, 4 to 64 rows.
+int grow_ref_slots(pp2_planner* p) {
+  const size_t row = (size_t)p->ref_ld * sizeof(float);
+  const size_t nrows = std::min<size_t>(64, std::max<size_t>(4, ((size_t)64 << 20) / row));
+  const size_t bytes = nrows * (row + 64);
+  char* base = nullptr;
+  HIPCHK(hipMalloc(&base, bytes));
+  p->arenas.push_back(base);
+  HIPCHK(hipMemsetAsync(base, 0, bytes, p->ctx->stream));  // the rows' zero tails past n
+  for (size_t r = 0; r < nrows; ++r) {
+    Slot s;
+    s.row = reinterpret_cast<float*>(base + r * row);
+    s.mass = reinterpret_cast<float*>(base + nrows * row + r * 64);
+    p->slots.push_back(s);
+    p->free_slots.push_back((int)p->slots.size() - 1);
+  }
+  // hand out the chunk's first rows first
+  std::reverse(p->free_slots.end() - (long)nrows, p->free_slots.end());
+  return PP2_OK;
+}
+
 int acquire_slot(pp2_planner* p, int* out) {
-  if (!p->free_slots.empty()) {
-    *out = p->free_slots.back();
-    p->free_slots.pop_back();
-    return PP2_OK;
+  if (p->free_slots.empty()) {
+    if (p->ref) {
+      CHECK(grow_ref_slots(p));
+    } else {
+      Slot s;
+      CHECK(alloc_planes(p->ctx, &s.b, 1));
+      HIPCHK(hipMalloc(&s.mass, 64));
+      p->slots.push_back(s);
+      p->free_slots.push_back((int)p->slots.size() - 1);
+    }
   }
-  Slot s;
-  if (p->ref) {
-    const size_t bytes = (size_t)p->ref_ld * sizeof(float);
-    HIPCHK(hipMalloc(&s.row, bytes));
-    HIPCHK(hipMemsetAsync(s.row, 0, bytes, p->ctx->stream));  // the zero tail past n
-  } else {
-    CHECK(alloc_planes(p->ctx, &s.b, 1));
-  }
-  HIPCHK(hipMalloc(&s.mass, 64));
-  p->slots.push_back(s);
-  *out = (int)p->slots.size() - 1;
+  *out = p->free_slots.back();
+  p->free_slots.pop_back();
   return PP2_OK;
 }
 
@@ -389,8 +410,11 @@ int ref_frows(pp2_planner* p) {
 }
 
 // evaluatePbviCpu (first maximum over the alphas, x-ordered dots) of `rows`
-// dense normalised beliefs into h_lbv[r].  Asynchronous.
-int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows) {
+// dense normalised beliefs into h_lbv[r]; with a device list (klist,
+// kcount), of the listed rows only (the kept children of an expansion; the
+// other rows' h_lbv are stale).  Asynchronous.
+int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows, const int* klist = nullptr,
+                    const int* kcount = nullptr) {
   pp2_ctx* c = p->ctx;
   const float* al = nullptr;
   int S = 0, Sp = 0, ald = 0;
@@ -398,7 +422,7 @@ int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows) {
   if (S != p->lb_S || ald != p->ref_ld)
     return set_err(PP2_ESTATE, "PBVI alpha vectors changed size since the planner was created");
   HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, al, S, p->ref_ld,
-                                (int)p->n, p->d_lbdots, S));
+                                (int)p->n, p->d_lbdots, S, klist, kcount));
   HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, rows, S, S, p->d_lbidx, p->d_lbv));
   return PP2_OK;
 }
@@ -713,7 +737,8 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     p->scr_main.attach(&a);
     HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 144, a));
   }
-  if (p->pbvi) CHECK(ref_pbvi_bounds(p, p->d_children, 144));
+  // the kept children's PBVI dots (evaluatePbviCpu), from the device list
+  if (p->pbvi) CHECK(ref_pbvi_bounds(p, p->d_children, 144, p->d_klist, p->d_kcount));
   HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards)
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
@@ -1011,6 +1036,7 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
     if ((s = pack_rows(p, c->R.v, 9, p->d_rrows))) return fail(s);
     if ((s = pack_rows(p, c->L.v, 16, p->d_lrows))) return fail(s);
+    if ((s = grow_ref_slots(p))) return fail(s);  // the first chunk of node rows
     if (hipStreamSynchronize(c->stream) != hipSuccess)
       return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
   }
@@ -1032,9 +1058,9 @@ int pp2_planner_destroy(pp2_planner* p) {
   pp2_planner_reset(p);
   for (Slot& s : p->slots) {
     free_planes(&s.b);
-    if (s.mass) (void)hipFree(s.mass);
-    if (s.row) (void)hipFree(s.row);
+    if (s.mass && !p->ref) (void)hipFree(s.mass);
   }
+  for (void* a : p->arenas) (void)hipFree(a);
   free_planes(&p->P);
   for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_parent, p->d_children,
                    p->d_lbpart, p->d_lbdots, p->d_rrows, p->d_frows, p->d_rsum, p->d_lrows,

@@ -160,6 +160,71 @@ def synth_trajectory(grid: np.ndarray, n: int, seed: int = 42):
     return us, zs, st
 
 
+def closed_loop(grid: np.ndarray, b0: np.ndarray, step_fn, max_steps: int,
+                budget_s: float = 1e9, seed: int = 99, min_steps: int = 0):
+    """Closed-loop plan steps, as the reference node runs against the dummy
+    simulator: step_fn(a, z, belief) is one beliefCallback
+    (src/pomdp/path_planning_2d.cu:199-241) returning (action, value); its
+    action moves a simulated robot (s' ~ T[s][a]) whose observation
+    (z ~ L[s']) is the next message.  The first call gets b0, later calls
+    None.  splitmix64(seed) draws the motion and the observation, so two
+    planners that choose the same actions see the same messages.  The loop
+    stops after max_steps, or once budget_s has passed and at least
+    min_steps ran.
+
+    Returns (ms, actions, values): the wall time of each step, the chosen
+    actions (uint8) and values (float32)."""
+    import time
+    rng = SplitMix64(seed)
+    x, y = start_cell(grid)
+    times, acts, vals = [], [], []
+    a, z, first = 0, 0, True
+    t_start = time.perf_counter()
+    for _ in range(max_steps):
+        t = time.perf_counter()
+        a, v = step_fn(a, z, b0 if first else None)
+        times.append(time.perf_counter() - t)
+        acts.append(a)
+        vals.append(v)
+        first = False
+        tp = cell_transition(grid, x, y, a)
+        r, c, j = rng.u01(), 0.0, 4
+        for i in range(9):
+            c += float(tp[i])
+            if tp[i] > 0 and r < c:
+                j = i
+                break
+        x += j % 3 - 1
+        y += j // 3 - 1
+        lk = cell_likelihood(grid, x, y)
+        r, c, z = rng.u01(), 0.0, 15
+        for i in range(16):
+            c += float(lk[i])
+            if r < c:
+                z = i
+                break
+        if len(times) >= min_steps and time.perf_counter() - t_start > budget_s:
+            break
+    return (np.array(times) * 1e3, np.array(acts, np.uint8),
+            np.array(vals, np.float32))
+
+
+def action_parity(acts_a, vals_a, acts_b, vals_b) -> dict:
+    """Plan-step parity of two closed loops over their common steps: the
+    actions equal and the values equal as fp32 bit patterns, step by step
+    (the loops share their messages while the actions agree, so the first
+    mismatch ends the comparison's meaning)."""
+    n = int(min(len(acts_a), len(acts_b)))
+    a_ok = np.asarray(acts_a[:n]) == np.asarray(acts_b[:n])
+    v_ok = (np.asarray(vals_a[:n], np.float32).view(np.uint32)
+            == np.asarray(vals_b[:n], np.float32).view(np.uint32))
+    bad = np.nonzero(~(a_ok & v_ok))[0]
+    return {"steps_compared": n,
+            "actions_equal": bool(a_ok.all()),
+            "values_bit_exact": bool(v_ok.all()),
+            "first_mismatch": int(bad[0]) if bad.size else None}
+
+
 def rollout_trajectories(grid: np.ndarray, belief: np.ndarray, copies: int, depth: int,
                          seed: int = 5):
     """(us, zs) of shape [depth, copies] for batched rollouts: each copy draws a

@@ -272,33 +272,73 @@ def test_planner_reference_order_bit_exact(oracle, name, max_depth, lb, S, steps
     rpl.close()
 
 
+def lockstep(gpl, rpl, where):
+    """A closed-loop step function that steps the GPU planner and the
+    reference-arithmetic oracle with the same message and holds them equal:
+    the whole tree snapshot bit for bit, the action and its value."""
+    k = [0]
+
+    def step(a, z, b):
+        a_g, v_g = gpl.step(a, z, b)
+        a_r, v_r = rpl.step(a, z, b)
+        compare_exact(gpl.info(), rpl.info(), f"{where} step {k[0]}")
+        assert a_g == a_r, f"{where} step {k[0]}: action {a_g} != {a_r}"
+        assert np.float32(v_g).view(np.uint32) == np.float32(v_r).view(np.uint32)
+        k[0] += 1
+        return a_g, v_g
+    return step
+
+
 def test_planner_reference_order_256(oracle):
-    """BASELINE configs[1] (256x256, max_search_tree_depth 3) in reference
-    order: bit-exact with the reference-arithmetic oracle at every step."""
+    """BASELINE configs[1] exactly as bench.py times it: 256x256 synthetic
+    grid, max_search_tree_depth 3, the converged FIB (fib_solve without a
+    sweep cap), 24 steps of the bench's seeded closed loop
+    (synthetic.closed_loop) -- bit-exact with the reference-arithmetic oracle
+    at every step."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S_
     grid = S_.synth_grid(256, 256, 256)
     goal = S_.synth_goal(grid)
     with P.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
         ctx.model_generate()
-        ctx.fib_solve(max_sweeps=40)
+        ctx.fib_solve()
         alphas = ctx.fib_get()
         T, L, R = oracle.model_pomdp(grid, goal)
         rpl = oracle.Planner(grid, T, L, R, alphas, max_depth=3, max_iter=15)
         with P.QVTreePlanner(ctx, max_search_tree_depth=3, max_online_iteration=15,
                              reference_order=1) as gpl:
-            b0 = S_.uniform_belief(grid)
-            a_g, _ = gpl.step(0, 0, b0)
-            a_r, _ = rpl.step(0, 0, b0)
-            compare_exact(gpl.info(), rpl.info(), "256 ref step 0")
-            assert a_g == a_r
-            _, zs, _ = S_.synth_trajectory(grid, 3, seed=3)
-            for k in range(3):
-                a_g, _ = gpl.step(a_r, int(zs[k]))
-                a_r, _ = rpl.step(a_r, int(zs[k]))
-                compare_exact(gpl.info(), rpl.info(), f"256 ref step {k + 1}")
-                assert a_g == a_r
+            _, acts, _ = S_.closed_loop(grid, S_.uniform_belief(grid),
+                                        lockstep(gpl, rpl, "256 ref"), 24)
         rpl.close()
+    assert acts.size == 24
+
+
+def test_planner_reference_order_pbvi_256(oracle):
+    """The 256x256 PBVI-leaf plan step of bench.py (plan_step_pbvi_lb):
+    lower_bound_mode 1 over the GPU's S = 500 PBVI alphas (generateBeliefSet
+    + 167 backups), reference order, the tree's rand() stream continuing
+    after the belief set's draws; the oracle gets the same alphas
+    (set_pbvi) and is held bit-exact over 4 closed-loop steps."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S_
+    grid = S_.synth_grid(256, 256, 256)
+    goal = S_.synth_goal(grid)
+    b0 = S_.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ctx:
+        ctx.model_generate()
+        ctx.fib_solve()
+        calls = ctx.pbvi_solve(b0, 500)
+        pal, pact = ctx.pbvi_get()
+        T, L, R = oracle.model_pomdp(grid, goal)
+        rpl = oracle.Planner(grid, T, L, R, ctx.fib_get(), max_depth=3, max_iter=15)
+        rpl.set_pbvi(pal, pact)
+        rpl.skip_rand(calls)
+        with P.QVTreePlanner(ctx, max_search_tree_depth=3, max_online_iteration=15,
+                             lower_bound_mode=1, rand_skip=calls, reference_order=1) as gpl:
+            S_.closed_loop(grid, b0, lockstep(gpl, rpl, "256 pbvi ref"), 4)
+            gi = gpl.info()
+        rpl.close()
+    assert gi["root_lower_bound"] > -5.0 / (1.0 - 0.95)
 
 
 def test_planner_pbvi_needs_alphas():

@@ -316,3 +316,25 @@ def test_pbvi_oracle_matches_golden(oracle, name):
     al, act, n = oracle.pbvi_backup(H, W, GAMMA, T, L, R, B, iterations=int(p["iterations"]))
     np.testing.assert_array_equal(al, p["alphas"])
     np.testing.assert_array_equal(act, p["actions"])
+
+
+def test_pbvi_eval_is_the_sequential_chain(oracle):
+    """evaluatePbviCpu (point_based_value_iteration_cuda.cu:678-699): the
+    oracle walks eight alphas' chains side by side; every dot must still be
+    the x-ordered fp32 chain (numpy's float32 cumsum is one sequential
+    chain), with the first maximum."""
+    rng = np.random.default_rng(3)
+    n, S = 1000, 21  # two groups of 8 and a tail of 5
+    b = rng.random(n).astype(np.float32)
+    b /= b.sum(dtype=np.float32)
+    al = -rng.random((S, n)).astype(np.float32) * 40
+    al[13] = al[5]  # a tie: the first maximum wins
+    act = (np.arange(S) % 9).astype(np.uint8)
+    dots = np.array([np.cumsum(b * al[i], dtype=np.float32)[-1] for i in range(S)], np.float32)
+    best = 0
+    for i in range(1, S):
+        if dots[best] < dots[i]:
+            best = i
+    v, a = oracle.pbvi_eval(b, al, act)
+    assert np.float32(v).view(np.uint32) == dots[best].view(np.uint32)
+    assert a == act[best]
