@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-5 GPU driver: one script, one mode per call (tools/README.md).
+#   tests    full `pytest -m gpu` suite
+#   planner  tests/test_gpu_planner.py only
+#   bench    driver-style bench (N=1, 20 steps)
+#   prof     rocprofv3 kernel trace of the bench's timed loop + the plan-step legs
+#   pmc      HBM counters of the resident loop / solve (tools/collect_pmc.sh)
+# Every GPU step has its own time limit, steps are chained with &&.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+T="--timeout 150 --timeout-method thread -p no:cacheprovider"
+run_tests()   { timeout -k 10 900 python -u -m pytest tests -m gpu -x -v $T > $OUT/pytest_gpu.log 2>&1; }
+run_planner() { timeout -k 10 600 python -u -m pytest tests/test_gpu_planner.py -x -v $T > $OUT/pytest_planner.log 2>&1; }
+run_smoke()   { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; }
+run_bench()   { timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; }
+run_prof()    { timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --profile --steps 20 --warmup 20 > $OUT/prof.log 2>&1; }
+run_pmc()     { timeout -k 10 600 bash tools/collect_pmc.sh > $OUT/pmc.log 2>&1; }
+rc=0
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    tests) run_tests ;; planner) run_planner ;; smoke) run_smoke ;; bench) run_bench ;;
+    prof) run_prof ;; pmc) run_pmc ;;
+    *) echo "unknown step $step"; false ;;
+  esac
+  rc=$?
+  [ $rc -ne 0 ] && break
+done
+for f in pytest_gpu.log pytest_planner.log; do [ -f $OUT/$f ] && tail -3 $OUT/$f; done
+echo "exit=$rc"
+exit $rc
