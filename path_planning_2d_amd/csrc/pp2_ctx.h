@@ -96,6 +96,7 @@ struct pp2_ctx {
   Planes fib[2], fibsnap;    // FIB alphas (9 planes)
   int fcur = 0;
   unsigned fib_version = 1;  // bumped whenever the current alphas change (planner caches)
+  unsigned pbvi_version = 1;  // bumped whenever the PBVI alpha vectors change (planner caches)
   bool fib_finite = true;          // every FIB alpha finite: the sparse / LDS sweeps apply
   float* pbuf[2] = {nullptr, nullptr};  // per-block partial masses of b[0], b[1]
   bool pending[2] = {false, false};     // mass of b[i] still in pbuf[i]

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 
+#include <algorithm>
 #include <utility>
 
 #define PP2_FC_HD __host__ __device__
@@ -90,8 +91,11 @@ __device__ __forceinline__ float ftz(float v) {
 enum : uint32_t { kPos = 1u, kNeg = 2u, kBad = 4u };
 enum : uint32_t { kPredicted = 1u };  // tab[].y: the driver will likely fall back here
 
-// group g's id, and whether it is active
+// group g's id, and whether it is active (false: neither is any later g --
+// the kernels walk their groups in grid strides and stop there).  FC_LIST:
+// id = g, the index of the chain's (row, partner) entry in plist.
 __device__ __forceinline__ bool group_id(const FcArgs& a, int g, int* id) {
+  if (g >= a.ngroups) return false;
   if (a.gcount && g >= *a.gcount) return false;
   *id = a.glist ? a.glist[g] : a.g0 + g;
   return true;
@@ -112,14 +116,20 @@ struct Terms {
     if (BASE == FC_ROW) {
       pr = a.row + (long long)id * a.row_stride;
       lr = nullptr;
+    } else if (BASE == FC_LIST) {  // row plist[id].x times partner plist[id].y
+      const int2 e = a.plist[id];
+      pr = a.row + (long long)e.x * a.row_stride;
+      lr = a.partners + (long long)e.y * ld;
     } else {
       pr = a.pred + (long long)(id % 9) * ld;
       lr = a.lrows + (long long)(id / 9) * ld;
     }
   }
-  // p *= L[16 idx + z] (point_based_value_iteration_cuda.cu:130), flushed
+  // p *= L[16 idx + z] (point_based_value_iteration_cuda.cu:130), flushed;
+  // FC_LIST: inner_product's host product b[x] * alpha[x] (IEEE)
   __device__ __forceinline__ float base(int x) const {
     if (BASE == FC_ROW) return pr[x];
+    if (BASE == FC_LIST) return pr[x] * lr[x];
     return ftz(pr[x] * ftz(lr[x]));
   }
   __device__ __forceinline__ float term(float v, int i, int x) const {
@@ -147,10 +157,14 @@ struct Terms {
     if (x0 + 4 <= n) {
       const f4a p = *reinterpret_cast<const f4a*>(pr + x0);
       f4a v = p;
-      if (BASE != FC_ROW) {
+      if (BASE == FC_CHILD) {
         const f4a l = *reinterpret_cast<const f4a*>(lr + x0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = ftz(p[q] * ftz(l[q]));
+      } else if (BASE == FC_LIST) {
+        const f4a l = *reinterpret_cast<const f4a*>(lr + x0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = p[q] * l[q];
       }
       if (K > 0 && i >= 0) {
         const f4a w = *reinterpret_cast<const f4a*>(part + (long long)i * ld + x0);
@@ -172,7 +186,8 @@ template <int BASE, int K>
 __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
   constexpr int KC = K > 0 ? K : 1;
   __shared__ uint32_t sFlags[KC];
-  const int g = blockIdx.y, seg = blockIdx.x;
+  const int seg = blockIdx.x;
+  for (int g = blockIdx.y;; g += gridDim.y) {  // (block-uniform)
   int id;
   if (!group_id(a, g, &id)) return;
   Terms<BASE, K> T;
@@ -213,6 +228,8 @@ __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
   __syncthreads();
   if (threadIdx.x < KC)
     a.cflag[(long long)(g * KC + threadIdx.x) * nseg + seg] = sFlags[threadIdx.x];
+  __syncthreads();  // (sFlags of the next group)
+  }
 }
 
 // ---------------------------------------------------------------- pass 2
@@ -221,7 +238,8 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
   constexpr int KC = K > 0 ? K : 1;
   __shared__ float sPart[KC][4];
   __shared__ float sP[KC][kFcSegChunks];
-  const int g = blockIdx.y, seg = blockIdx.x;
+  const int seg = blockIdx.x;
+  for (int g = blockIdx.y;; g += gridDim.y) {  // (block-uniform)
   int id;
   if (!group_id(a, g, &id)) return;
   Terms<BASE, K> T;
@@ -249,9 +267,8 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
     }
   }
   __syncthreads();
-  {
+  if (j0 + w < nch) {
     const int jl = w, j = j0 + jl;
-    if (j >= nch) return;
     const int x0 = j * kFcChunk + 4 * lane;
     float v[4];
     T.terms4(-1, x0, v);
@@ -278,6 +295,8 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
         a.tab[(long long)(g * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
       }
     }
+  }
+  __syncthreads();  // (sPart / sP of the next group)
   }
 }
 
@@ -351,7 +370,8 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
   __shared__ uint2 sE[kFcWin];
   __shared__ __attribute__((aligned(16))) float sStash[kFcStash][kFcChunk];
   __shared__ int sStashId[kFcStash];
-  const int ch = blockIdx.x, g = ch / KC, i = ch % KC;
+  for (int ch = blockIdx.x;; ch += gridDim.x) {  // (one wave: uniform)
+  const int g = ch / KC, i = ch % KC;
   int id;
   if (!group_id(a, g, &id)) return;
   Terms<BASE, K> T;
@@ -497,7 +517,16 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
     const float r = value_of(E, k);
     res = neg ? (r == 0.0f ? 0.0f : -r) : r;
   }
-  if (lane == 0) a.out[(long long)id * a.ldo + i] = res;
+  if (lane == 0) {
+    if (BASE == FC_LIST) {  // out[row * ldo + partner]
+      const int2 e = a.plist[id];
+      a.out[(long long)e.x * a.ldo + e.y] = res;
+    } else {
+      a.out[(long long)id * a.ldo + i] = res;
+    }
+  }
+  __syncthreads();  // (the window / stash of the next chain)
+  }
 }
 
 // ---------------------------------------------------------------- running sums
@@ -625,16 +654,142 @@ __global__ __launch_bounds__(256) void k_store_kept(const int* __restrict__ klis
   dst[(long long)c * ld + x] = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
 }
 
+// ---------------------------------------------------------------- PBVI candidates
+// evaluatePbviCpu (point_based_value_iteration_cuda.cu:678-699) wants the
+// first maximum over S x-ordered fp32 chains per row.  Most alphas cannot be
+// it: with D_i an approximate dot (the split-x f32 MFMA GEMM: fmaf chains of
+// kchunk terms, then the split partials in order) and E_i the reference's
+// chain, |E_i - D_i| <= c * P_i + n * 2^-148, c = (n + kchunk + splits + 8) u
+// (u = 2^-24, recursive-summation bounds of both sums in any order, plus the
+// products' rounding), P_i = sum_x |b_x alpha_i[x]| -- |D_i| (1 + 2c) when
+// every term has one sign (b >= 0, alpha_i single-signed), else
+// ||b||_1 max_x |alpha_i[x]|.  Alpha i is a candidate when its upper bound
+// D_i + d_i reaches the largest lower bound max_j (D_j - d_j): every other
+// alpha's chain lies strictly below the maximum's, so it can be neither the
+// maximum nor tie it.  The candidates' chains run exactly (FC_LIST); the
+// others' entries are -inf.  A row with a non-finite entry or dot takes
+// every alpha as a candidate.
+
+// per alpha i < S: max_x |alpha_i[x]| (x < n) and its sign / finiteness flags
+__global__ __launch_bounds__(256) void k_alpha_stats(const float* __restrict__ al, int S, int n,
+                                                     int ld, float* __restrict__ amax,
+                                                     uint32_t* __restrict__ aflag) {
+  __shared__ float sM[4];
+  __shared__ uint32_t sF[4];
+  const int i = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float* __restrict__ p = al + (long long)i * ld;
+  float m = 0.0f;
+  uint32_t f = 0u;
+  for (int x = threadIdx.x; x < n; x += 256) {
+    const float v = p[x];
+    f |= !isfinite(v) ? kBad : v > 0.0f ? kPos : v < 0.0f ? kNeg : 0u;
+    m = fmaxf(m, fabsf(v));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    m = fmaxf(m, __shfl_xor(m, o));
+    f |= (uint32_t)__shfl_xor((int)f, o);
+  }
+  if (lane == 0) {
+    sM[w] = m;
+    sF[w] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    amax[i] = fmaxf(fmaxf(sM[0], sM[1]), fmaxf(sM[2], sM[3]));
+    aflag[i] = sF[0] | sF[1] | sF[2] | sF[3];
+  }
+}
+
+__device__ __forceinline__ double block_max_d(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const double r = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const double r = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return r;
+}
+
+// one block per row q < *kcount (klist[q], or q): candidates of the row
+__global__ __launch_bounds__(256) void k_pbvi_cands(PbviCandArgs c) {
+  __shared__ double red[4];
+  const int q = blockIdx.x;
+  if (c.kcount ? q >= *c.kcount : q >= c.nrows) return;
+  const int r = c.klist ? c.klist[q] : q;
+  const float* __restrict__ b = c.rows + (long long)r * c.row_stride;
+  double l1 = 0.0;
+  int neg = 0, bad = 0;
+  for (int x = threadIdx.x; x < c.n; x += 256) {
+    const float v = b[x];
+    bad |= !isfinite(v);
+    neg |= v < 0.0f;
+    l1 += fabs((double)v);
+  }
+  l1 = block_sum_d(l1, red);
+  const int rneg = __syncthreads_or(neg), rbad = __syncthreads_or(bad);
+  const double cr = (double)c.c_rel, tiny = (double)c.n * 0x1p-148;
+  const float* __restrict__ D = c.approx + (long long)r * c.lda;
+  double lo = -INFINITY;
+  int dbad = 0;
+  for (int i = threadIdx.x; i < c.S; i += 256) {
+    const double d = (double)D[i];
+    if (!isfinite(d)) {
+      dbad = 1;
+      continue;
+    }
+    const uint32_t f = c.aflag[i];
+    const bool single = !rneg && !(f & kBad) && !((f & kPos) && (f & kNeg));
+    const double P = single ? fabs(d) * (1.0 + 2.0 * cr) : l1 * (double)c.amax[i] * (1.0 + 1e-6);
+    lo = fmax(lo, d - (cr * P + tiny));
+  }
+  lo = block_max_d(lo, red);
+  const bool all = rbad || __syncthreads_or(dbad);
+  for (int i = threadIdx.x; i < c.S; i += 256) {
+    bool cand = all;
+    if (!cand) {
+      const double d = (double)D[i];
+      const uint32_t f = c.aflag[i];
+      const bool single = !rneg && !(f & kBad) && !((f & kPos) && (f & kNeg));
+      const double P = single ? fabs(d) * (1.0 + 2.0 * cr) : l1 * (double)c.amax[i] * (1.0 + 1e-6);
+      cand = d + (cr * P + tiny) >= lo;
+    }
+    if (cand) {
+      const int k = atomicAdd(c.pcount, 1);
+      c.plist[k] = make_int2(r, i);
+    } else {
+      c.exact[(long long)r * c.lde + i] = -INFINITY;
+    }
+  }
+}
+
+// The kernels walk their groups (drive: chains) in grid strides: the grids
+// are capped, so that a large device-counted set (FC_LIST: up to 144 x S
+// chains, most of them beyond the count) neither overflows a grid dimension
+// nor dispatches a workgroup per inactive group.
+constexpr int kFcGroupBlocks = 16384;  // sums / tables: segments x groups per launch
+constexpr int kFcDriveBlocks = 8192;   // drive: one wave per chain
+
 template <int BASE, int K>
-hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a, int phases) {
+hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) {
   constexpr int KC = K > 0 ? K : 1;
+  FcArgs a = a0;
+  a.ngroups = groups;
   const int nseg = fc_segments(a.n);
   if (phases & FC_TABLES) {
-    hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, groups), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, groups), dim3(256), 0, st, a);
+    const int gy = std::min(groups, std::max(1, kFcGroupBlocks / nseg));
+    hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
   }
   if (phases & FC_DRIVE) {
-    hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(groups * KC), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(std::min(groups * KC, kFcDriveBlocks)), dim3(64),
+                       0, st, a);
     if (BASE == FC_ROW && K == 0 && a.cdf)
       hipLaunchKernelGGL(k_fc_cdf, dim3((fc_chunks(a.n) + 3) / 4), dim3(256), 0, st, a);
   }
@@ -652,12 +807,34 @@ hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcAr
   if (a.ld < a.n || a.ld % 4 != 0) return hipErrorInvalidValue;
   if (base == FC_CHILD && (!a.pred || !a.lrows || K != 0)) return hipErrorInvalidValue;
   if (base == FC_ROW && !a.row) return hipErrorInvalidValue;
+  if (base == FC_LIST && (K != 0 || !a.row || !a.partners || !a.plist || !a.gcount || a.glist ||
+                          a.cdf))
+    return hipErrorInvalidValue;
+  if (base != FC_LIST && a.plist) return hipErrorInvalidValue;
   if (K != 0 && !a.partners) return hipErrorInvalidValue;
   if (a.cdf && (base != FC_ROW || K != 0 || groups != 1 || !a.cst)) return hipErrorInvalidValue;
   if (base == FC_ROW && K == 0) return launch_set<FC_ROW, 0>(st, groups, a, phases);
   if (base == FC_ROW && K == 9) return launch_set<FC_ROW, 9>(st, groups, a, phases);
+  if (base == FC_ROW) return hipErrorInvalidValue;
   if (base == FC_CHILD) return launch_set<FC_CHILD, 0>(st, groups, a, phases);
+  if (base == FC_LIST) return launch_set<FC_LIST, 0>(st, groups, a, phases);
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_alpha_stats(hipStream_t st, const float* al, int S, int n, int ld, float* amax,
+                              uint32_t* aflag) {
+  if (S <= 0 || n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_alpha_stats, dim3(S), dim3(256), 0, st, al, S, n, ld, amax, aflag);
+  return hipGetLastError();
+}
+
+hipError_t launch_pbvi_cands(hipStream_t st, const PbviCandArgs& c) {
+  if (c.nrows <= 0) return hipSuccess;
+  if (!c.rows || !c.approx || !c.amax || !c.aflag || !c.exact || !c.plist || !c.pcount ||
+      c.S <= 0 || c.n <= 0 || (c.klist == nullptr) != (c.kcount == nullptr))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_pbvi_cands, dim3(c.nrows), dim3(256), 0, st, c);
+  return hipGetLastError();
 }
 
 hipError_t launch_tree_sample(hipStream_t st, const SampleArgs& s) {
@@ -842,6 +1019,61 @@ extern "C" int pp2_debug_fchain_tables(int n, const float* x, float* csum, uint3
     }
   }
   for (float* p : {dx, dout, dcdf})
+    if (p) (void)hipFree(p);
+  return st;
+}
+
+// Diagnostic (tests/test_gpu_fchain.py): the FC_LIST chain set of the
+// (row, alpha) pairs on device 0 -- out[r * S + i] = inner_product(x[r],
+// alphas[i]) for every listed pair (r, i) (other entries of out untouched).
+// x: R rows of n, alphas: S rows of n.  Synchronous.
+extern "C" int pp2_debug_fchain_pairs(int n, int R, const float* x, int S, const float* alphas,
+                                      const int* pairs, int npairs, float* out) {
+  if (n <= 0 || R <= 0 || S <= 0 || npairs < 0 || !x || !alphas || !out || (npairs > 0 && !pairs))
+    return 1;
+  for (int k = 0; k < npairs; ++k)
+    if (pairs[2 * k] < 0 || pairs[2 * k] >= R || pairs[2 * k + 1] < 0 || pairs[2 * k + 1] >= S)
+      return 1;
+  const size_t ld = ((size_t)n + 63) / 64 * 64;
+  const int cap = std::max(1, npairs);
+  float *dx = nullptr, *da = nullptr, *dout = nullptr;
+  int2* dlist = nullptr;
+  int* dcnt = nullptr;
+  pp2::FcScratch scr;
+  int st = 0;
+  auto ok = [&](hipError_t e) {
+    if (e != hipSuccess && st == 0) st = 2;
+    return st == 0;
+  };
+  if (!scr.reserve(n, cap)) return 3;
+  if (ok(hipMalloc(&dx, (size_t)R * ld * sizeof(float))) &&
+      ok(hipMalloc(&da, (size_t)S * ld * sizeof(float))) &&
+      ok(hipMalloc(&dout, (size_t)R * S * sizeof(float))) &&
+      ok(hipMalloc(&dlist, (size_t)cap * sizeof(int2))) && ok(hipMalloc(&dcnt, sizeof(int))) &&
+      ok(hipMemset(dx, 0, (size_t)R * ld * sizeof(float))) &&
+      ok(hipMemset(da, 0, (size_t)S * ld * sizeof(float))) &&
+      ok(hipMemcpy(dout, out, (size_t)R * S * sizeof(float), hipMemcpyHostToDevice)) &&
+      ok(hipMemcpy2D(dx, ld * sizeof(float), x, (size_t)n * sizeof(float), (size_t)n * sizeof(float),
+                     R, hipMemcpyHostToDevice)) &&
+      ok(hipMemcpy2D(da, ld * sizeof(float), alphas, (size_t)n * sizeof(float),
+                     (size_t)n * sizeof(float), S, hipMemcpyHostToDevice)) &&
+      (npairs == 0 || ok(hipMemcpy(dlist, pairs, (size_t)npairs * sizeof(int2), hipMemcpyHostToDevice))) &&
+      ok(hipMemcpy(dcnt, &npairs, sizeof(int), hipMemcpyHostToDevice))) {
+    pp2::FcArgs a;
+    a.n = n;
+    a.ld = (int)ld;
+    a.row = dx;
+    a.row_stride = (long long)ld;
+    a.partners = da;
+    a.plist = dlist;
+    a.gcount = dcnt;
+    a.out = dout;
+    a.ldo = S;
+    scr.attach(&a);
+    if (ok(pp2::launch_fchain(nullptr, pp2::FC_LIST, 0, cap, a)) && ok(hipDeviceSynchronize()))
+      ok(hipMemcpy(out, dout, (size_t)R * S * sizeof(float), hipMemcpyDeviceToHost));
+  }
+  for (void* p : {(void*)dx, (void*)da, (void*)dout, (void*)dlist, (void*)dcnt})
     if (p) (void)hipFree(p);
   return st;
 }

@@ -115,6 +115,7 @@ int ensure_state(pp2_ctx* c, int S) {
   HIPCHK(hipMemsetAsync(p->alpha[1], 0, rows * sizeof(float), c->stream));
   HIPCHK(hipMemsetAsync(p->actions, 0, (size_t)Sp, c->stream));
   p->acur = 0;
+  ++c->pbvi_version;
   return PP2_OK;
 }
 
@@ -275,6 +276,7 @@ int backup_impl(pp2_ctx* c, int iterations) {
     HIPCHK(pp2::launch_pbvi_select(c->stream, p->V, p->Ga, Sp, S, ld, p->alpha[p->acur ^ 1],
                                    p->actions));
     p->acur ^= 1;
+    ++c->pbvi_version;
   }
   return PP2_OK;
 }
@@ -389,6 +391,7 @@ int pp2_pbvi_set(pp2_ctx* c, uint32_t set_size, const float* alphas, const uint8
   PbviState* p = c->pbvi;
   p->has_set = keep_set;
   CHECK(upload_rows(c, p->alpha[p->acur], p->ld, alphas, p->hw, p->S));
+  ++c->pbvi_version;
   HIPCHK(hipMemcpyAsync(p->actions, actions, set_size, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return PP2_OK;

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <limits.h>
+#include <stdlib.h>
 
 #include "pp2_pbvi_internal.h"
 
@@ -402,6 +403,106 @@ __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A,
   }
 }
 
+// The pair chains of few long rows -- the planner's PBVI leaf dots: <= 144
+// rows x S = 500 alphas of 65536 cells, about one chain per lane of the chip
+// -- are bound by each chain's own latency per element.  k_pair_chain's
+// small shape waits for every 4-element group's LDS reads before its adds (a
+// full LDS round trip per 4 adds).  Here 16 A rows x 16 B rows per 256-thread
+// block, one chain per thread (thread (la, jb) = A row la, B row jb, so a
+// wave holds 16 A rows x 4 B rows: its A reads hit 16 rows 4 banks apart, its
+// B reads are 4 broadcasts), both operands row-major in LDS (one ds_read_b128
+// per operand and 4 elements), 512-element chunks staged from registers
+// loaded one chunk ahead, and the reads of each 8-element group issued three
+// groups ahead of the dependent adds (inline asm, counted lgkmcnt waits, as
+// k_lane_chains).  Rows past na / nb and cells past n read as 0: their
+// products +-0 leave the chain unchanged (a chain from +0 is never -0).
+constexpr int kSeqCH = 512, kSeqRow = kSeqCH + 4;
+constexpr size_t kSeqLds = 2 * 16 * kSeqRow * sizeof(float);
+
+template <int OP>
+__global__ __launch_bounds__(256) void k_pair_seq(const float* __restrict__ A, int na,
+                                                  const float* __restrict__ B, int nb, int ld,
+                                                  int n, float* __restrict__ out, int ldo,
+                                                  const int* __restrict__ alist,
+                                                  const int* __restrict__ acount) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sA = smem;
+  float* sB = smem + 16 * kSeqRow;
+  const int tid = threadIdx.x, la = tid & 15, jb = tid >> 4;
+  const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
+  if (alist) {
+    na = min(na, *acount);
+    if (i0 >= na) return;  // (uniform over the block)
+  }
+  auto arow = [&](int i) { return alist ? alist[i] : i; };
+  // staging: per operand 16 rows x 128 float4, thread t takes float4 t + 256 q
+  f4 ra[8], rb[8];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 256 * q, row = e >> 7, c4 = (e & 127) * 4;
+      const int ia = i0 + row, jj = j0 + row;
+      ra[q] = ia < na && x0 + c4 < n ? *(const f4*)(A + (long long)arow(ia) * ld + x0 + c4)
+                                     : f4{0, 0, 0, 0};
+      rb[q] = jj < nb && x0 + c4 < n ? *(const f4*)(B + (long long)jj * ld + x0 + c4)
+                                     : f4{0, 0, 0, 0};
+    }
+  };
+  const uint32_t la_addr = (uint32_t)(uintptr_t)(sA + la * kSeqRow);
+  const uint32_t lb_addr = (uint32_t)(uintptr_t)(sB + jb * kSeqRow);
+  float acc = 0.0f;
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += kSeqCH) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 256 * q, row = e >> 7, c4 = (e & 127) * 4;
+      *(f4*)(sA + row * kSeqRow + c4) = ra[q];
+      *(f4*)(sB + row * kSeqRow + c4) = rb[q];
+    }
+    __syncthreads();
+    if (x0 + kSeqCH < n) fetch(x0 + kSeqCH);  // in flight during this chunk's chains
+    constexpr int G = 8, NG = kSeqCH / G, R = 4, LA = 3, NB = LA + 1;
+    f4 ga[NB][2], gb[NB][2];
+    auto rd = [&](int g) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(ga[g % NB][q]) : "v"(la_addr + 4u * (G * g + 4 * q)));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(gb[g % NB][q]) : "v"(lb_addr + 4u * (G * g + 4 * q)));
+      }
+    };
+#pragma unroll
+    for (int g = 0; g < LA; ++g) rd(g);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g + LA < NG) {
+        rd(g + LA);
+        asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(LA * R) : "memory");
+      } else if (g + 2 < NG) {
+        asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(2 * R) : "memory");
+      } else if (g + 1 < NG) {
+        asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(R) : "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        asm volatile("" : "+v"(ga[g % NB][q]));
+        asm volatile("" : "+v"(gb[g % NB][q]));
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f4 a = ga[g % NB][q], b = gb[g % NB][q];
+        acc = pair_step<OP>(acc, a.x, b.x);
+        acc = pair_step<OP>(acc, a.y, b.y);
+        acc = pair_step<OP>(acc, a.z, b.z);
+        acc = pair_step<OP>(acc, a.w, b.w);
+      }
+    }
+    __syncthreads();
+  }
+  if (i0 + la < na && j0 + jb < nb) out[(long long)arow(i0 + la) * ldo + j0 + jb] = acc;
+}
+
 // ---------------------------------------------------------------- sampling
 // find_if(partial_sum >= r) over `cnt` values at stride `stride`; when the
 // sum never reaches r, the last index at which it grew (the reference would
@@ -750,6 +851,22 @@ hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, con
 #endif
   constexpr int kNc = PP2_PAIR_NC, kCh = PP2_PAIR_CH;
   const bool big = (long long)cdiv(na, 64) * cdiv(nb, 64) >= 256;
+  // few long chains (the planner's PBVI leaf dots): the lookahead kernel
+  const char* seq = getenv("PP2_PAIR_SEQ");
+  if (!big && n >= 1024 && !(seq && seq[0] == '0')) {
+    static unsigned long long attr[2] = {0ull, 0ull};
+    const void* fn = op == PAIR_L1 ? reinterpret_cast<const void*>(&k_pair_seq<PAIR_L1>)
+                                   : reinterpret_cast<const void*>(&k_pair_seq<PAIR_DOT>);
+    allow_lds(fn, attr[op == PAIR_L1 ? 0 : 1]);
+    const dim3 g2(cdiv(na, 16), cdiv(nb, 16));
+    if (op == PAIR_L1)
+      hipLaunchKernelGGL(k_pair_seq<PAIR_L1>, g2, dim3(256), kSeqLds, st, A, na, B, nb, ld, n, out,
+                         ldo, alist, acount);
+    else
+      hipLaunchKernelGGL(k_pair_seq<PAIR_DOT>, g2, dim3(256), kSeqLds, st, A, na, B, nb, ld, n, out,
+                         ldo, alist, acount);
+    return hipGetLastError();
+  }
   const dim3 grid = big ? dim3(cdiv(na, 64), cdiv(nb, 64)) : dim3(cdiv(na, 16), cdiv(nb, 16 * kNc));
 #define PP2_PAIR(OPV, TAV, NCV, CHV)                                                        \
   hipLaunchKernelGGL((k_pair_chain<OPV, TAV, NCV, CHV>), grid, dim3(256), 0, st, A, na, B, nb, ld, \

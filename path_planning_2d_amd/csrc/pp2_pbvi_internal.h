@@ -100,9 +100,12 @@ hipError_t launch_sum_splits(hipStream_t st, const float* C, int splits, long lo
 //   FC_ROW:   base = row[id * row_stride + x]
 //   FC_CHILD: base = fl_ftz(pred[id % 9][x] * L[id / 9][x]) -- the unnormalised
 //             child of action id % 9 and observation id / 9
+//   FC_LIST:  (K = 0) group g < *gcount is the chain of the pair plist[g] =
+//             (row r, partner i): inner_product(row[r], partners[i]), terms
+//             fl(row[r][x] * partners[i][x]) (evaluatePbviCpu) -- out[r * ldo + i]
 // out[id * ldo + i] = the chain's sum; with cdf (FC_ROW, K = 0, one group)
 // also every running sum, cdf[x] (std::partial_sum).  Scratch: FcScratch.
-enum FcBase { FC_ROW = 0, FC_CHILD = 1 };
+enum FcBase { FC_ROW = 0, FC_CHILD = 1, FC_LIST = 2 };
 constexpr int kFcMaxCells = 1 << 28;
 constexpr int kFcSegChunks = 4;  // chunks per k_fc_sums / k_fc_tables workgroup (1 per wave)
 inline __host__ __device__ int fc_chunks(int n) { return (n + 255) / 256; }
@@ -129,6 +132,8 @@ struct FcArgs {
   int2* cst = nullptr;           // [chunks + 1] chunk start states (cdf)
   int max_chains = 0, max_chunks = 0;
   int* stats = nullptr;          // diagnostics: driver {iterations, fallbacks, exact rounds, stash hits}
+  const int2* plist = nullptr;   // FC_LIST: device (row, partner) pairs, *gcount of them
+  int ngroups = 0;               // (set by launch_fchain: the launch's group count)
 };
 // Device scratch of one stream's chain sets (a set may not overlap another
 // set using the same scratch).
@@ -168,6 +173,32 @@ struct SampleArgs {
   int* kcount = nullptr;
 };
 hipError_t launch_tree_sample(hipStream_t st, const SampleArgs& s);
+// The planner's PBVI leaf bounds in reference order (pp2_fchain.hip): per
+// alpha, max |alpha[x]| and its sign flags; then per row the alphas whose
+// exact chain can reach the maximum, from approximate dots and a rigorous
+// error bound -- the candidates into plist (+= *pcount), every other entry
+// of exact[r * lde + i] set to -inf.
+hipError_t launch_alpha_stats(hipStream_t st, const float* al, int S, int n, int ld, float* amax,
+                              uint32_t* aflag);
+struct PbviCandArgs {
+  const float* rows = nullptr;   // the rows (beliefs): row r at rows + r * row_stride
+  long long row_stride = 0;
+  int n = 0;                     // chain length (cells)
+  const int* klist = nullptr;    // rows klist[q], q < *kcount (or q < nrows)
+  const int* kcount = nullptr;
+  int nrows = 0;                 // grid rows (max rows)
+  const float* approx = nullptr; // approximate dots [r * lda + i]
+  int lda = 0;
+  const float* amax = nullptr;   // launch_alpha_stats
+  const uint32_t* aflag = nullptr;
+  int S = 0;
+  float c_rel = 0.0f;            // (n + kchunk + splits + 8) * 2^-24, with slack
+  float* exact = nullptr;        // [r * lde + i]
+  int lde = 0;
+  int2* plist = nullptr;
+  int* pcount = nullptr;
+};
+hipError_t launch_pbvi_cands(hipStream_t st, const PbviCandArgs& c);
 // dst[r][x] = fl_ftz(pred[c % 9][x] * L[c / 9][x]) / sums[c], c = child[r], x < n.
 struct FcStoreList {
   int n = 0;

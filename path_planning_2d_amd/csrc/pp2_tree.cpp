@@ -13,6 +13,7 @@
 #include <float.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -193,6 +194,18 @@ struct pp2_planner {
   int* d_klist = nullptr;       // the kept children z * 9 + a, and their number
   int* d_kcount = nullptr;
   pp2::FcScratch scr_main, scr_side;  // chain-set scratch of the two streams
+  // reference order, PBVI leaves: every row's candidate alphas (those whose
+  // exact chain can reach the row's maximum, from the split-x GEMM's
+  // approximate dots and a rigorous bound) as one exact chain set (FC_LIST)
+  pp2::FcScratch scr_pbvi;      // its scratch (reserved when it fits; else k_pair_chain)
+  float* d_lbapprox = nullptr;  // [256][Sp] approximate dots
+  float* d_amax = nullptr;      // [Sp] max |alpha_i|
+  uint32_t* d_aflag = nullptr;  // [Sp] alpha_i's sign flags
+  unsigned astats_version = 0;  // the context's pbvi_version d_amax / d_aflag are from
+  int2* d_plist = nullptr;      // [144 S] candidate (row, alpha) pairs
+  int* d_pcount = nullptr;
+  int* h_pstat = nullptr;       // pinned: candidates of the last set (PP2_PBVI_STATS)
+  long long stat_cands = 0, stat_rows = 0, stat_sets = 0;
   unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
   hipStream_t side = nullptr;   // reward chains beside the child chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_kids = nullptr;
@@ -421,8 +434,65 @@ int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows, const int* kl
   CHECK(pbvi_alphas(c, &al, &S, &Sp, &ald));
   if (S != p->lb_S || ald != p->ref_ld)
     return set_err(PP2_ESTATE, "PBVI alpha vectors changed size since the planner was created");
-  HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, al, S, p->ref_ld,
-                                (int)p->n, p->d_lbdots, S, klist, kcount));
+  if (p->scr_pbvi.chains > 0) {
+    // candidates: approximate dots by the split-x f32 MFMA GEMM (d_rows
+    // holds Mp rows), then the alphas whose chain can reach each row's
+    // maximum (pp2_fchain.hip k_pbvi_cands), then their exact chains
+    if (p->astats_version != c->pbvi_version) {
+      HIPCHK(pp2::launch_alpha_stats(c->stream, al, S, (int)p->n, p->ref_ld, p->d_amax,
+                                     p->d_aflag));
+      p->astats_version = c->pbvi_version;
+    }
+    const int Mp = (rows + pp2::kGemmTile - 1) / pp2::kGemmTile * pp2::kGemmTile;
+    const long long sstride = (long long)Mp * Sp;
+    HIPCHK(pp2::launch_gemm_nt(c->stream, d_rows, al, p->d_lbpart, Mp, Sp, p->ref_ld, 1, 0, 0,
+                               p->lb_split, sstride));
+    HIPCHK(pp2::launch_sum_splits(c->stream, p->d_lbpart, p->lb_split, sstride, (int)sstride,
+                                  p->d_lbapprox));
+    HIPCHK(hipMemsetAsync(p->d_pcount, 0, sizeof(int), c->stream));
+    pp2::PbviCandArgs ca;
+    ca.rows = d_rows;
+    ca.row_stride = p->ref_ld;
+    ca.n = (int)p->n;
+    ca.klist = klist;
+    ca.kcount = kcount;
+    ca.nrows = rows;
+    ca.approx = p->d_lbapprox;
+    ca.lda = Sp;
+    ca.amax = p->d_amax;
+    ca.aflag = p->d_aflag;
+    ca.S = S;
+    // the GEMM's fmaf chains of kchunk terms and its ordered split sum
+    // (launch_gemm_nt's kchunk), the reference's chain of n adds, 1 % slack
+    const long long kchunk = ((p->ref_ld + p->lb_split - 1) / p->lb_split + 31) / 32 * 32;
+    ca.c_rel = (float)((double)((long long)p->n + kchunk + p->lb_split + 8) * 0x1p-24 * 1.01);
+    ca.exact = p->d_lbdots;
+    ca.lde = S;
+    ca.plist = p->d_plist;
+    ca.pcount = p->d_pcount;
+    HIPCHK(pp2::launch_pbvi_cands(c->stream, ca));
+    pp2::FcArgs a;
+    a.n = (int)p->n;
+    a.ld = p->ref_ld;
+    a.row = d_rows;
+    a.row_stride = p->ref_ld;
+    a.partners = al;
+    a.plist = p->d_plist;
+    a.gcount = p->d_pcount;
+    a.out = p->d_lbdots;
+    a.ldo = S;
+    p->scr_pbvi.attach(&a);
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_LIST, 0, rows * S, a));
+    if (p->h_pstat) {
+      HIPCHK(hipMemcpyAsync(p->h_pstat, p->d_pcount, sizeof(int), hipMemcpyDeviceToHost,
+                            c->stream));
+      ++p->stat_sets;
+    }
+  } else {
+    // one sequential chain per lane (grids whose chain-set scratch is too big)
+    HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, al, S, p->ref_ld,
+                                  (int)p->n, p->d_lbdots, S, klist, kcount));
+  }
   HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, rows, S, S, p->d_lbidx, p->d_lbv));
   return PP2_OK;
 }
@@ -442,7 +512,16 @@ int ref_row_bounds(pp2_planner* p, const float* row) {
   a.ldo = 9;
   p->scr_main.attach(&a);
   HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 1, a));
-  if (p->pbvi) CHECK(ref_pbvi_bounds(p, row, 1));
+  if (p->pbvi) {
+    if (p->scr_pbvi.chains > 0) {
+      // the candidate GEMM reads a whole tile of rows: the row into row 0 of
+      // d_children (scratch between expansions)
+      HIPCHK(hipMemcpyAsync(p->d_children, row, (size_t)p->ref_ld * sizeof(float),
+                            hipMemcpyDeviceToDevice, c->stream));
+      row = p->d_children;
+    }
+    CHECK(ref_pbvi_bounds(p, row, 1));
+  }
   return PP2_OK;
 }
 
@@ -505,6 +584,10 @@ int make_root(pp2_planner* p, int s, uint8_t z, VNode** out) {
     CHECK(ref_row_bounds(p, sl.row));
     HIPCHK(hipEventRecord(p->ev_done, c->stream));
     HIPCHK(hipEventSynchronize(p->ev_done));
+    if (p->h_pstat) {
+      p->stat_cands += *p->h_pstat;
+      ++p->stat_rows;
+    }
     VNode* v = new_vnode(p, z, 0.0f, nullptr);
     v->slot = s;
     v->upper_bound = first_max9(p->h_rout + 9);
@@ -743,6 +826,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
   HIPCHK(hipEventSynchronize(p->ev_done));
+  if (p->h_pstat) p->stat_cands += *p->h_pstat;
 
   for (QNode* q : v->children)
     if (q) delete_subtree(p, q);
@@ -772,6 +856,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     v->children[a] = q;
   }
   CHECK(ref_store_children(p, keep.data(), rows.data(), (int)keep.size()));
+  p->stat_rows += (long long)keep.size();
   vnode_update(v);
   ++p->expansions;
   return PP2_OK;
@@ -1037,8 +1122,28 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
     if ((s = pack_rows(p, c->R.v, 9, p->d_rrows))) return fail(s);
     if ((s = pack_rows(p, c->L.v, 16, p->d_lrows))) return fail(s);
     if ((s = grow_ref_slots(p))) return fail(s);  // the first chunk of node rows
-    if (hipStreamSynchronize(c->stream) != hipSuccess)
-      return fail(set_err(PP2_EHIP, "planner reference-order scratch initialisation failed"));
+    if (p->pbvi) {
+      // opt-in (PP2_PBVI_FCHAIN=1): the PBVI leaf bounds' candidate chain
+      // set, scratch for every (row, alpha) pair when that stays <= 1 GiB
+      // (12 B per chain and chunk).  Default: the lane-per-chain pair chains
+      // (measured faster: PBVI alphas lie so close together that 50-300 of
+      // 500 stay candidates per row)
+      const long long chains = 144LL * p->lb_S;
+      const long long bytes = chains * pp2::fc_chunks((int)p->n) * 12LL;
+      const char* e = getenv("PP2_PBVI_FCHAIN");
+      if (e && e[0] == '1' && bytes <= (1LL << 30)) {
+        if (!p->scr_pbvi.reserve((int)p->n, (int)chains) ||
+            hipMalloc(&p->d_lbapprox, (size_t)256 * p->lb_Sp * sizeof(float)) != hipSuccess ||
+            hipMalloc(&p->d_amax, (size_t)p->lb_Sp * sizeof(float)) != hipSuccess ||
+            hipMalloc(&p->d_aflag, (size_t)p->lb_Sp * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&p->d_plist, (size_t)chains * sizeof(int2)) != hipSuccess ||
+            hipMalloc(&p->d_pcount, sizeof(int)) != hipSuccess)
+          return fail(set_err(PP2_ENOMEM, "planner PBVI chain scratch allocation failed"));
+        const char* st = getenv("PP2_PBVI_STATS");
+        if (st && st[0] == '1' && hipHostMalloc((void**)&p->h_pstat, sizeof(int)) != hipSuccess)
+          return fail(set_err(PP2_ENOMEM, "planner stats allocation failed"));
+      }
+    }
   }
   *out = p;
   return PP2_OK;
@@ -1064,8 +1169,17 @@ int pp2_planner_destroy(pp2_planner* p) {
   free_planes(&p->P);
   for (float* d : {p->d_rpart, p->d_spart, p->d_bpart, p->d_parent, p->d_children,
                    p->d_lbpart, p->d_lbdots, p->d_rrows, p->d_frows, p->d_rsum, p->d_lrows,
-                   p->d_pred, p->d_csum})
+                   p->d_pred, p->d_csum, p->d_lbapprox, p->d_amax})
     if (d) (void)hipFree(d);
+  for (void* d : {(void*)p->d_aflag, (void*)p->d_plist, (void*)p->d_pcount})
+    if (d) (void)hipFree(d);
+  if (p->h_pstat) {
+    if (p->stat_sets > 0)
+      fprintf(stderr, "pp2 planner: PBVI candidate chains %lld over %lld rows in %lld sets "
+              "(%.2f per row of %d alphas)\n", p->stat_cands, p->stat_rows, p->stat_sets,
+              p->stat_rows ? (double)p->stat_cands / (double)p->stat_rows : 0.0, p->lb_S);
+    (void)hipHostFree(p->h_pstat);
+  }
   if (p->h_rout) (void)hipHostFree(p->h_rout);
   if (p->h_r) (void)hipHostFree(p->h_r);
   if (p->h_counts) (void)hipHostFree(p->h_counts);

@@ -5,6 +5,9 @@
 #   bench    driver-style bench (N=1, 20 steps)
 #   prof     rocprofv3 kernel trace of the bench's timed loop + the plan-step legs
 #   pmc      HBM counters of the resident loop / solve (tools/collect_pmc.sh)
+#   fchain   tests/test_gpu_fchain.py (the exact chain sets, FC_PAIR included)
+#   pbvi     tools/pbvi_plan_timing.py (PBVI-leaf plan steps, FC_PAIR vs k_pair_chain)
+#   profplan rocprofv3 kernel traces of the node and 256^2 PBVI-leaf plan steps
 # Every GPU step has its own time limit, steps are chained with &&.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -18,17 +21,21 @@ run_smoke()   { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smok
 run_bench()   { timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; }
 run_prof()    { timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --profile --steps 20 --warmup 20 > $OUT/prof.log 2>&1; }
 run_pmc()     { timeout -k 10 600 bash tools/collect_pmc.sh > $OUT/pmc.log 2>&1; }
+run_fchain()  { timeout -k 10 300 python -u -m pytest tests/test_gpu_fchain.py -x -v $T > $OUT/pytest_fchain.log 2>&1; }
+run_pbvi()    { PP2_PBVI_STATS=1 timeout -k 10 300 python3 tools/pbvi_plan_timing.py > $OUT/pbvi_plan_timing.txt 2>&1; }
+run_profplan() { PP2_CASE=node PP2_STEPS=30 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_node -o run -- python3 tools/prof_planner.py > $OUT/prof_node.log 2>&1 &&
+                 PP2_CASE=256 PP2_LB=1 PP2_STEPS=20 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_pbvi256 -o run -- python3 tools/prof_planner.py > $OUT/prof_pbvi256.log 2>&1; }
 rc=0
 for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     tests) run_tests ;; planner) run_planner ;; smoke) run_smoke ;; bench) run_bench ;;
-    prof) run_prof ;; pmc) run_pmc ;;
+    prof) run_prof ;; pmc) run_pmc ;; fchain) run_fchain ;; pbvi) run_pbvi ;; profplan) run_profplan ;;
     *) echo "unknown step $step"; false ;;
   esac
   rc=$?
   [ $rc -ne 0 ] && break
 done
-for f in pytest_gpu.log pytest_planner.log; do [ -f $OUT/$f ] && tail -3 $OUT/$f; done
+for f in pytest_gpu.log pytest_planner.log pytest_fchain.log; do [ -f $OUT/$f ] && tail -3 $OUT/$f; done
 echo "exit=$rc"
 exit $rc
