@@ -416,36 +416,45 @@ __global__ __launch_bounds__(256) void k_pair_chain(const float* __restrict__ A,
 // groups ahead of the dependent adds (inline asm, counted lgkmcnt waits, as
 // k_lane_chains).  Rows past na / nb and cells past n read as 0: their
 // products +-0 leave the chain unchanged (a chain from +0 is never -0).
+// TB: B rows per block.  16 (measured: 20, which fits the planner's 144 x
+// 500 grid in one block per CU, ran 5 % slower, profiles/r05/pbvi_plan_modes_ab.txt).
+inline int cdiv(long long a, int b) { return (int)((a + b - 1) / b); }
 constexpr int kSeqCH = 512, kSeqRow = kSeqCH + 4;
-constexpr size_t kSeqLds = 2 * 16 * kSeqRow * sizeof(float);
+constexpr size_t seq_lds(int tb) { return (size_t)(16 + tb) * kSeqRow * sizeof(float); }
 
-template <int OP>
-__global__ __launch_bounds__(256) void k_pair_seq(const float* __restrict__ A, int na,
-                                                  const float* __restrict__ B, int nb, int ld,
-                                                  int n, float* __restrict__ out, int ldo,
-                                                  const int* __restrict__ alist,
-                                                  const int* __restrict__ acount) {
+template <int OP, int TB>
+__global__ __launch_bounds__(16 * TB) void k_pair_seq(const float* __restrict__ A, int na,
+                                                      const float* __restrict__ B, int nb, int ld,
+                                                      int n, float* __restrict__ out, int ldo,
+                                                      const int* __restrict__ alist,
+                                                      const int* __restrict__ acount) {
+  constexpr int NT = 16 * TB;
+  constexpr int LA4 = (16 * 128 + NT - 1) / NT, LB4 = (TB * 128 + NT - 1) / NT;  // float4 per thread
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sA = smem;
   float* sB = smem + 16 * kSeqRow;
   const int tid = threadIdx.x, la = tid & 15, jb = tid >> 4;
-  const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
+  const int i0 = blockIdx.x * 16, j0 = blockIdx.y * TB;
   if (alist) {
     na = min(na, *acount);
     if (i0 >= na) return;  // (uniform over the block)
   }
   auto arow = [&](int i) { return alist ? alist[i] : i; };
-  // staging: per operand 16 rows x 128 float4, thread t takes float4 t + 256 q
-  f4 ra[8], rb[8];
+  // staging: float4 e of a tile = row e / 128, column 4 (e % 128); thread t
+  // takes e = t + NT q
+  f4 ra[LA4], rb[LB4];
   auto fetch = [&](int x0) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + 256 * q, row = e >> 7, c4 = (e & 127) * 4;
-      const int ia = i0 + row, jj = j0 + row;
-      ra[q] = ia < na && x0 + c4 < n ? *(const f4*)(A + (long long)arow(ia) * ld + x0 + c4)
-                                     : f4{0, 0, 0, 0};
-      rb[q] = jj < nb && x0 + c4 < n ? *(const f4*)(B + (long long)jj * ld + x0 + c4)
-                                     : f4{0, 0, 0, 0};
+    for (int q = 0; q < LA4; ++q) {
+      const int e = tid + NT * q, row = e >> 7, c4 = (e & 127) * 4, ia = i0 + row;
+      ra[q] = e < 16 * 128 && ia < na && x0 + c4 < n
+                  ? *(const f4*)(A + (long long)arow(ia) * ld + x0 + c4) : f4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int q = 0; q < LB4; ++q) {
+      const int e = tid + NT * q, row = e >> 7, c4 = (e & 127) * 4, jj = j0 + row;
+      rb[q] = e < TB * 128 && jj < nb && x0 + c4 < n
+                  ? *(const f4*)(B + (long long)jj * ld + x0 + c4) : f4{0, 0, 0, 0};
     }
   };
   const uint32_t la_addr = (uint32_t)(uintptr_t)(sA + la * kSeqRow);
@@ -454,10 +463,14 @@ __global__ __launch_bounds__(256) void k_pair_seq(const float* __restrict__ A, i
   fetch(0);
   for (int x0 = 0; x0 < n; x0 += kSeqCH) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + 256 * q, row = e >> 7, c4 = (e & 127) * 4;
-      *(f4*)(sA + row * kSeqRow + c4) = ra[q];
-      *(f4*)(sB + row * kSeqRow + c4) = rb[q];
+    for (int q = 0; q < LA4; ++q) {
+      const int e = tid + NT * q;
+      if (e < 16 * 128) *(f4*)(sA + (e >> 7) * kSeqRow + (e & 127) * 4) = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < LB4; ++q) {
+      const int e = tid + NT * q;
+      if (e < TB * 128) *(f4*)(sB + (e >> 7) * kSeqRow + (e & 127) * 4) = rb[q];
     }
     __syncthreads();
     if (x0 + kSeqCH < n) fetch(x0 + kSeqCH);  // in flight during this chunk's chains
@@ -501,6 +514,16 @@ __global__ __launch_bounds__(256) void k_pair_seq(const float* __restrict__ A, i
     __syncthreads();
   }
   if (i0 + la < na && j0 + jb < nb) out[(long long)arow(i0 + la) * ldo + j0 + jb] = acc;
+}
+
+template <int OP, int TB>
+hipError_t launch_pair_seq(hipStream_t st, const float* A, int na, const float* B, int nb, int ld,
+                           int n, float* out, int ldo, const int* alist, const int* acount) {
+  static unsigned long long attr = 0ull;
+  allow_lds(reinterpret_cast<const void*>(&k_pair_seq<OP, TB>), attr);
+  hipLaunchKernelGGL((k_pair_seq<OP, TB>), dim3(cdiv(na, 16), cdiv(nb, TB)), dim3(16 * TB),
+                     seq_lds(TB), st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- sampling
@@ -782,7 +805,6 @@ __global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ C,
   out[e] = v;
 }
 
-inline int cdiv(long long a, int b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
 
@@ -854,18 +876,9 @@ hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, con
   // few long chains (the planner's PBVI leaf dots): the lookahead kernel
   const char* seq = getenv("PP2_PAIR_SEQ");
   if (!big && n >= 1024 && !(seq && seq[0] == '0')) {
-    static unsigned long long attr[2] = {0ull, 0ull};
-    const void* fn = op == PAIR_L1 ? reinterpret_cast<const void*>(&k_pair_seq<PAIR_L1>)
-                                   : reinterpret_cast<const void*>(&k_pair_seq<PAIR_DOT>);
-    allow_lds(fn, attr[op == PAIR_L1 ? 0 : 1]);
-    const dim3 g2(cdiv(na, 16), cdiv(nb, 16));
     if (op == PAIR_L1)
-      hipLaunchKernelGGL(k_pair_seq<PAIR_L1>, g2, dim3(256), kSeqLds, st, A, na, B, nb, ld, n, out,
-                         ldo, alist, acount);
-    else
-      hipLaunchKernelGGL(k_pair_seq<PAIR_DOT>, g2, dim3(256), kSeqLds, st, A, na, B, nb, ld, n, out,
-                         ldo, alist, acount);
-    return hipGetLastError();
+      return launch_pair_seq<PAIR_L1, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+    return launch_pair_seq<PAIR_DOT, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
   }
   const dim3 grid = big ? dim3(cdiv(na, 64), cdiv(nb, 64)) : dim3(cdiv(na, 16), cdiv(nb, 16 * kNc));
 #define PP2_PAIR(OPV, TAV, NCV, CHV)                                                        \

@@ -263,6 +263,98 @@ __device__ __forceinline__ void belief_fact(const uint8_t* prow, int ps, int x0,
     p[k] = p[k] * *reinterpret_cast<const float*>(lt + __builtin_amdgcn_ubfe(lx4, 8 * k, 8));
 }
 
+// The register-rich 2-D instance (TC = 3) holds the lane's class bytes of
+// every used window row of every action in registers for the whole run (the
+// class planes are static): per (action, row) the lane's own dword m and
+// the two neighbour bytes lh (x0 - 1 in bits 0-7, x0 + 4 in bits 8-15), so
+// the gather's table reads issue at the step's top, without the class-byte
+// LDS round trip before them.  Slots in (action, row) order.
+#ifndef PP2_RES_HOIST
+#define PP2_RES_HOIST 1  // (A/B builds: 0 keeps the LDS class reads in the TC = 3 instance)
+#endif
+struct ClsSlots {
+  int s[9][3];
+  int n;
+  constexpr ClsSlots() : s{}, n(0) {
+    for (int u = 0; u < 9; ++u)
+      for (int r = 0; r < 3; ++r) s[u][r] = belief_row_used<false>(u, r) ? n++ : -1;
+  }
+};
+constexpr ClsSlots kCls{};
+constexpr int kClsSlots = kCls.n;
+struct ClassRegs {
+  uint32_t m[kClsSlots], lh[(kClsSlots + 1) / 2];  // lh: two slots per dword
+};
+template <int U>
+__device__ __forceinline__ void belief_fact_regs(const ClassRegs& cr, uint32_t lx4, int z,
+                                                 const Win6& win, float (&p)[4]) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const char* qr = reinterpret_cast<const char*>(lds + kResQR) + U * kFactK * 16;
+  const char* lt = reinterpret_cast<const char*>(lds + kResLT) + z * (kResLK * 4);
+  uint32_t cb[3][6];
+#pragma unroll
+  for (int oy = 0; oy < 3; ++oy) {
+    const int sl = kCls.s[U][oy];
+    if (sl < 0) continue;
+    const uint32_t m = cr.m[sl], lh = cr.lh[sl / 2] >> (16 * (sl & 1));
+    cb[oy][0] = lh & 0xffu;
+    cb[oy][1] = m & 0xffu;
+    cb[oy][2] = __builtin_amdgcn_ubfe(m, 8, 8);
+    cb[oy][3] = __builtin_amdgcn_ubfe(m, 16, 8);
+    cb[oy][4] = m >> 24;
+    cb[oy][5] = __builtin_amdgcn_ubfe(lh, 8, 8);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) p[k] = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const int wr = s / 3, wc = s % 3 - 1;
+    const int sl = sup_slot(U, 8 - s);
+    if (sl < 0) continue;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      p[k] = __builtin_fmaf(*reinterpret_cast<const float*>(qr + 4 * sl + cb[wr][k + 1 + wc]),
+                            win.v[wr][k + 1 + wc], p[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    p[k] = p[k] * *reinterpret_cast<const float*>(lt + __builtin_amdgcn_ubfe(lx4, 8 * k, 8));
+}
+__device__ __forceinline__ void belief_any_regs(int u, const ClassRegs& cr, uint32_t lx4, int z,
+                                                const Win6& w, float (&p)[4]) {
+  switch (u) {
+#define PP2_BQ(UU)                               \
+  case UU:                                       \
+    belief_fact_regs<UU>(cr, lx4, z, w, p);      \
+    break;
+    PP2_BQ(0) PP2_BQ(1) PP2_BQ(2) PP2_BQ(3) PP2_BQ(4) PP2_BQ(5) PP2_BQ(6) PP2_BQ(7)
+    default: belief_fact_regs<8>(cr, lx4, z, w, p);
+#undef PP2_BQ
+  }
+}
+// the lane's class dwords of plane rows ty .. ty + 2 (window rows 0 .. 2)
+// (an odd slot count leaves the last lh dword's high half 0)
+__device__ __forceinline__ void load_class_regs(const uint8_t* sP, int prows, int ps, int ty,
+                                                int x0, ClassRegs& cr) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int U = 0; U < 9; ++U)
+#pragma unroll
+    for (int oy = 0; oy < 3; ++oy) {
+      const int sl = kCls.s[U][oy];
+      if (sl < 0) continue;
+      const uint8_t* r = sP + (U * prows + ty + oy) * ps + 4 + x0;
+      const uint32_t m = *reinterpret_cast<const uint32_t*>(r);
+      uint32_t e = 0u;
+      if (lane == 0 || lane == 63) e = *reinterpret_cast<const uint32_t*>(r + (lane == 0 ? -4 : 4));
+      const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp((int)e, (int)m, 0x138, 0xf, 0xf, false);
+      const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp((int)e, (int)m, 0x130, 0xf, 0xf, false);
+      cr.m[sl] = m;
+      const uint32_t lh = (l >> 24) | ((h & 0xffu) << 8);
+      cr.lh[sl / 2] = (sl & 1) ? cr.lh[sl / 2] | (lh << 16) : lh;
+    }
+}
+
 // sP: the tile's class planes [9][rt + 2][ps] (ps = wp + 8 bytes: 4 pad
 // bytes on each side); this lane's rows start at plane row ty.
 // p = the gathered quad times L_z (the block-start scale and the mass
@@ -337,11 +429,26 @@ __device__ __forceinline__ int xch_gran(int ntiles, int wpr, int slot, int tl, i
                                         int k, int ln) {
   return (((((slot * ntiles + tl) * 2 + side) * wpr + w) * kResidentGranules + k) * 64 + ln) * 16;
 }
-__device__ __forceinline__ void st_quad(Rsrc r, int off, const float (&v)[4], unsigned bit) {
+// Same-XCD hand-offs (PP2_RES_XCD_PLAIN): a plain store keeps the line in
+// the XCD's L2, so the neighbour's sc1 (L1-bypassing, L2-served) loads take
+// it there, where an sc1 store drops it and the reader fetches it over the
+// fabric (MI355X_MICROARCH.md, visibility table).  Only where every reader
+// of the granule runs on the producer's XCD: the tile -> XCD map of
+// xcd_remap (block b on XCD b % 8 owns a contiguous range of tiles).
+#ifndef PP2_RES_XCD_PLAIN
+#define PP2_RES_XCD_PLAIN 0
+#endif
+__device__ __forceinline__ int tile_xcd(int t, int n) {
+  const int q = n / 8, r = n % 8;
+  return t < r * (q + 1) ? t / (q + 1) : r + (q > 0 ? (t - r * (q + 1)) / q : 0);
+}
+__device__ __forceinline__ void st_quad_x(Rsrc r, int off, const float (&v)[4], unsigned bit,
+                                          bool plain) {
   const unsigned m = bit << 31;
   const u4v t = {__float_as_uint(v[0]) | m, __float_as_uint(v[1]) | m, __float_as_uint(v[2]) | m,
                  __float_as_uint(v[3]) | m};
-  __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, kSc1);
+  if (plain) __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, kSc1);
 }
 __device__ __forceinline__ bool tagged(const u4v& g, unsigned m) {
   return (((g[0] ^ m) | (g[1] ^ m) | (g[2] ^ m) | (g[3] ^ m)) >> 31) == 0u;
@@ -473,14 +580,17 @@ struct Trajectory {
 // a tile is a strip of rt grid columns spanning the whole view and only its
 // first and last columns cross CUs; HBM stays in the grid's layout (row
 // stride a.ows), read and written transposed once per launch.
+// TC = 3: the 2-D tiling (2 tile columns) with at most 768 threads -- 3 waves
+// per SIMD, so a 168-VGPR budget instead of 128: the sweep's table reads of
+// all 4 cells of an action in flight together (coded_sweep_iw G = 4).
 template <int CAP, int TC, bool LAG, bool TR>
-__global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
-                                                           const Trajectory<CAP> tr) {
+__global__ __launch_bounds__(TC == 3 ? 768 : 1024, TC == 3 ? 3 : 4) void k_loop_resident(
+    const ResidentHead a, const Trajectory<CAP> tr) {
   static_assert(!TR || TC == 1, "transposed tiles are whole kernel rows");
-  constexpr int kSweepG = TC > 1 ? 2 : 0;
+  constexpr int kSweepG = TC == 3 ? 4 : TC > 1 ? 2 : 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // a tile: rt rows x tw columns (tc tile columns per row of tiles)
-  constexpr int tc = TC;
+  constexpr int tc = TC == 3 ? 2 : TC;
   const int wp = a.g.wp, rows = a.g.rows, tw = wp / tc;
   const int tpr = tw >> 2, wpr = tw >> 8;  // lanes, waves per tile row
   const int xs = tw + 4;                // padded LDS row stride
@@ -535,13 +645,18 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
   auto sbuf = [&](int k, int slot) { return sB0 + (2 * k + slot) * bufn + 4; };
   // the boundary waves' hand-off: b and J of the lane's quad as two
   // self-tagged granules {b0..b3}, {j0..j3} in exchange slot `slot`
+  // (whether the row granules' reader, tile -+ tc, shares this tile's XCD)
+  const int myx = tile_xcd(tile, (int)gridDim.x);
+  const bool plain_up = PP2_RES_XCD_PLAIN && nb_up && tile_xcd(tile - tc, (int)gridDim.x) == myx;
+  const bool plain_dn = PP2_RES_XCD_PLAIN && nb_dn && tile_xcd(tile + tc, (int)gridDim.x) == myx;
   auto publish = [&](int slot, const float (&b)[4], const float (&j)[4], unsigned bit) {
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       if (side == 0 ? !nb_up : !nb_dn) continue;
       const int o = xch_gran(a.ntiles, wpr, slot, tile, side, wj, 0, lane);
-      st_quad(rx, o, b, bit);
-      st_quad(rx, o + 1024, j, bit);
+      const bool plain = side == 0 ? plain_up : plain_dn;
+      st_quad_x(rx, o, b, bit, plain);
+      st_quad_x(rx, o + 1024, j, bit, plain);
     }
     if (sd_lane) {
       const int o = side_gran(sbase, a.ntiles, slot, tile, sd_l ? 0 : 1, ty);
@@ -706,6 +821,11 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
     *reinterpret_cast<uint32_t*>(sP + i * ps + 4 + tw) = rp;
   }
   PP2_RP(4);
+  ClassRegs creg;
+  if constexpr (TC == 3 && PP2_RES_HOIST) {
+    __syncthreads();  // the class planes
+    if (valid) load_class_regs(sP, prows, ps, ty, x0, creg);
+  }
   if (prior_err != 0u) return;  // (uniform: before any global store)
   const bool bnd = nb_up || nb_dn || sd_l || sd_r;  // waves that cross CUs
   if (valid) {
@@ -856,7 +976,16 @@ __global__ __launch_bounds__(1024, 4) void k_loop_resident(const ResidentHead a,
         }
       }
       PP2_RT(1);
-      belief_any<TR>(u, sP, prows, ps, ty, x0, lx4, z, wb, p);
+      if constexpr (TC == 3 && PP2_RES_HOIST) {
+        // opaque per step (empty asm): otherwise the compiler hoists the 9
+        // actions' table addresses, loop-invariant now, out of the step loop
+#pragma unroll
+        for (int i = 0; i < kClsSlots; ++i) asm volatile("" : "+v"(creg.m[i]));
+#pragma unroll
+        for (int i = 0; i < (kClsSlots + 1) / 2; ++i) asm volatile("" : "+v"(creg.lh[i]));
+        belief_any_regs(u, creg, lx4, z, wb, p);
+      }
+      else belief_any<TR>(u, sP, prows, ps, ty, x0, lx4, z, wb, p);
       float jn[9][4];  // grid stencil offset i = 3 (dy + 1) + dx + 1
 #pragma unroll
       for (int i = 0; i < 9; ++i)
@@ -1003,11 +1132,15 @@ __global__ __launch_bounds__(1024, 4) void k_sweep_resident(const SweepRun a) {
   const Rsrc rx = make_rsrc(a.xch);
   auto sbuf = [&](int i) { return sJ0 + i * bufn + 4; };
   // k_loop_resident's hand-off with J alone: granule 0, {j0..j3}
+  const int myx = tile_xcd(tile, (int)gridDim.x);
+  const bool plain_up = PP2_RES_XCD_PLAIN && nb_up && tile_xcd(tile - 1, (int)gridDim.x) == myx;
+  const bool plain_dn = PP2_RES_XCD_PLAIN && nb_dn && tile_xcd(tile + 1, (int)gridDim.x) == myx;
   auto publish = [&](int slot, const float (&j)[4], unsigned bit) {
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       if (side == 0 ? !nb_up : !nb_dn) continue;
-      st_quad(rx, xch_gran(a.ntiles, wpr, slot, tile, side, wj, 0, lane), j, bit);
+      st_quad_x(rx, xch_gran(a.ntiles, wpr, slot, tile, side, wj, 0, lane), j, bit,
+                side == 0 ? plain_up : plain_dn);
     }
   };
   auto take = [&](int slot, int tl, int side, unsigned bit, float (&v)[6]) {
@@ -1160,6 +1293,15 @@ size_t resident_lds_bytes(const Geom& g, int E, int rt, int tc) {
 
 // The plan with tc tile columns: rt rows per tile so that the tiles fit the
 // CUs, or false.
+// The kernel instance of a tiling: 2-D tiles of <= 768 threads run the
+// register-rich TC = 3 instance (PP2_RES_RICH=0 at build time: never).
+static int resident_tc(int tc, int threads) {
+#ifndef PP2_RES_RICH
+#define PP2_RES_RICH 1
+#endif
+  return tc == 2 && threads <= 768 && PP2_RES_RICH ? 3 : tc;
+}
+
 static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPlan* p,
                              bool trn = false) {
   if (tc < 1 || tc > 2 || g.wp % (256 * tc) != 0 || (tc > 1 && g.wp / tc < 512) || ncus < tc) return false;
@@ -1169,19 +1311,19 @@ static bool resident_plan_tc(const Geom& g, int E, int ncus, int tc, ResidentPla
   const size_t lds = resident_lds_bytes(g, E, rt, tc);
   if (lds > kDictLdsMaxBytes) return false;
   if (trn && tc != 1) return false;
-  static unsigned long long attr[12] = {};
+  static unsigned long long attr[16] = {};
+  // the instance: TC = 3 for 2-D tiles of <= 768 threads (resident_tc)
+  const int ktc = resident_tc(tc, (int)threads);
 #define PP2_K(CAPV, TCV, LAGV, TRV) reinterpret_cast<const void*>(&k_loop_resident<CAPV, TCV, LAGV, TRV>)
-  const void* ks[4] = {
-      trn ? PP2_K(kResidentShortSteps, 1, false, true)
-          : tc == 1 ? PP2_K(kResidentShortSteps, 1, false, false) : PP2_K(kResidentShortSteps, 2, false, false),
-      trn ? PP2_K(kResidentMaxSteps, 1, false, true)
-          : tc == 1 ? PP2_K(kResidentMaxSteps, 1, false, false) : PP2_K(kResidentMaxSteps, 2, false, false),
-      trn ? PP2_K(kResidentShortSteps, 1, true, true)
-          : tc == 1 ? PP2_K(kResidentShortSteps, 1, true, false) : PP2_K(kResidentShortSteps, 2, true, false),
-      trn ? PP2_K(kResidentMaxSteps, 1, true, true)
-          : tc == 1 ? PP2_K(kResidentMaxSteps, 1, true, false) : PP2_K(kResidentMaxSteps, 2, true, false)};
+#define PP2_KT(CAPV, LAGV)                                                                    \
+  (trn ? PP2_K(CAPV, 1, LAGV, true)                                                           \
+       : ktc == 1 ? PP2_K(CAPV, 1, LAGV, false)                                               \
+                  : ktc == 2 ? PP2_K(CAPV, 2, LAGV, false) : PP2_K(CAPV, 3, LAGV, false))
+  const void* ks[4] = {PP2_KT(kResidentShortSteps, false), PP2_KT(kResidentMaxSteps, false),
+                       PP2_KT(kResidentShortSteps, true), PP2_KT(kResidentMaxSteps, true)};
+#undef PP2_KT
 #undef PP2_K
-  const int ai = trn ? 8 : 4 * (tc - 1);
+  const int ai = trn ? 8 : 4 * (ktc - 1) + (ktc == 3 ? 4 : 0);
   int nb = 1 << 30;
   for (int k = 0; k < 4; ++k) {
     allow_lds(ks[k], attr[ai + k]);
@@ -1258,18 +1400,21 @@ hipError_t launch_loop_resident(hipStream_t st, const ResidentPlan& p, const Res
       hipLaunchKernelGGL((k_loop_resident<CAPV, TCV, false, TRV>), dim3(p.ntiles),               \
                          dim3(p.threads), lds, st, h, tr);                                       \
   } while (0)
+  const int ktc = resident_tc(p.tc, p.threads);
   if (a.n <= kResidentShortSteps) {
     Trajectory<kResidentShortSteps> tr{};
     std::memcpy(tr.uz, a.uz, (size_t)a.n);
     if (p.tr) PP2_RES_LAUNCH(kResidentShortSteps, 1, true);
-    else if (p.tc == 1) PP2_RES_LAUNCH(kResidentShortSteps, 1, false);
-    else PP2_RES_LAUNCH(kResidentShortSteps, 2, false);
+    else if (ktc == 1) PP2_RES_LAUNCH(kResidentShortSteps, 1, false);
+    else if (ktc == 2) PP2_RES_LAUNCH(kResidentShortSteps, 2, false);
+    else PP2_RES_LAUNCH(kResidentShortSteps, 3, false);
   } else {
     Trajectory<kResidentMaxSteps> tr;
     std::memcpy(tr.uz, a.uz, sizeof tr.uz);
     if (p.tr) PP2_RES_LAUNCH(kResidentMaxSteps, 1, true);
-    else if (p.tc == 1) PP2_RES_LAUNCH(kResidentMaxSteps, 1, false);
-    else PP2_RES_LAUNCH(kResidentMaxSteps, 2, false);
+    else if (ktc == 1) PP2_RES_LAUNCH(kResidentMaxSteps, 1, false);
+    else if (ktc == 2) PP2_RES_LAUNCH(kResidentMaxSteps, 2, false);
+    else PP2_RES_LAUNCH(kResidentMaxSteps, 3, false);
   }
 #undef PP2_RES_LAUNCH
   return hipGetLastError();

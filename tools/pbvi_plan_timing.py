@@ -33,7 +33,7 @@ def main():
         calls = ctx.pbvi_belief_set(b0, 500)
         ctx.pbvi_backup(int(os.environ.get("PP2_ITERS", "0")))
         res = {}
-        modes = (("fc", "1", "1"), ("seq", "0", "1"), ("pair", "0", "0"))
+        modes = (("seq", "0", "1"), ("fc", "1", "1"), ("pair", "0", "0"))
         for rep in range(2):
             for mode, fc, sq in modes:
                 os.environ["PP2_PBVI_FCHAIN"] = fc
@@ -46,13 +46,14 @@ def main():
                     ms, acts, vals = S.closed_loop(grid, b0, pl.step, steps)
                 res.setdefault(mode, []).append((float(np.percentile(ms, 50)), acts, vals))
         ctx.close()
-        for mode, name in (("fc", "FC_LIST candidate chains"), ("seq", "k_pair_seq lookahead"),
-                           ("pair", "k_pair_chain")):
+        for mode, name in (("seq", "k_pair_seq (default)"),
+                           ("fc", "FC_LIST candidate chain sets (PP2_PBVI_FCHAIN=1)"),
+                           ("pair", "k_pair_chain (PP2_PAIR_SEQ=0)")):
             p50 = [r[0] for r in res[mode]]
             print(f"{label}: {name}: p50 {p50[0]:.3f} / {p50[1]:.3f} ms", flush=True)
         same = all(np.array_equal(res[m][k][1], res["pair"][k][1]) and
                    np.array_equal(res[m][k][2].view(np.uint32), res["pair"][k][2].view(np.uint32))
-                   for k in range(2) for m in ("fc", "seq"))
+                   for k in range(2) for m in ("seq", "fc"))
         print(f"{label}: actions and values identical across the modes: {same}", flush=True)
 
 

@@ -8,6 +8,8 @@
 #   fchain   tests/test_gpu_fchain.py (the exact chain sets, FC_PAIR included)
 #   pbvi     tools/pbvi_plan_timing.py (PBVI-leaf plan steps, FC_PAIR vs k_pair_chain)
 #   profplan rocprofv3 kernel traces of the node and 256^2 PBVI-leaf plan steps
+#   shards   tests/test_gpu_shards.py + test_gpu_resident.py (the resident / shard kernels)
+#   ab       tools/r05_ab.sh: config-4 rank share + 1024^2 loop, in-tree vs tools/_var/*.so
 # Every GPU step has its own time limit, steps are chained with &&.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -20,7 +22,10 @@ run_planner() { timeout -k 10 600 python -u -m pytest tests/test_gpu_planner.py 
 run_smoke()   { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; }
 run_bench()   { timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; }
 run_prof()    { timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --profile --steps 20 --warmup 20 > $OUT/prof.log 2>&1; }
-run_pmc()     { timeout -k 10 600 bash tools/collect_pmc.sh > $OUT/pmc.log 2>&1; }
+run_pmc()     { PMC_DIR=pmc_r05 timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmc.log 2>&1; }
+run_pmcx()    { PP2_LIBRARY=$PWD/tools/_var/c_xcd.so PMC_DIR=pmc_r05x timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmcx.log 2>&1; }
+run_shards()  { timeout -k 10 600 python -u -m pytest tests/test_gpu_shards.py tests/test_gpu_resident.py -x -v $T > $OUT/pytest_shards.log 2>&1; }
+run_ab()      { timeout -k 10 900 bash tools/r05_ab.sh > $OUT/ab.log 2>&1; }
 run_fchain()  { timeout -k 10 300 python -u -m pytest tests/test_gpu_fchain.py -x -v $T > $OUT/pytest_fchain.log 2>&1; }
 run_pbvi()    { PP2_PBVI_STATS=1 timeout -k 10 300 python3 tools/pbvi_plan_timing.py > $OUT/pbvi_plan_timing.txt 2>&1; }
 run_profplan() { PP2_CASE=node PP2_STEPS=30 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_node -o run -- python3 tools/prof_planner.py > $OUT/prof_node.log 2>&1 &&
@@ -30,12 +35,12 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     tests) run_tests ;; planner) run_planner ;; smoke) run_smoke ;; bench) run_bench ;;
-    prof) run_prof ;; pmc) run_pmc ;; fchain) run_fchain ;; pbvi) run_pbvi ;; profplan) run_profplan ;;
+    prof) run_prof ;; pmc) run_pmc ;; pmcx) run_pmcx ;; fchain) run_fchain ;; shards) run_shards ;; ab) run_ab ;; pbvi) run_pbvi ;; profplan) run_profplan ;;
     *) echo "unknown step $step"; false ;;
   esac
   rc=$?
   [ $rc -ne 0 ] && break
 done
-for f in pytest_gpu.log pytest_planner.log pytest_fchain.log; do [ -f $OUT/$f ] && tail -3 $OUT/$f; done
+for f in pytest_gpu.log pytest_planner.log pytest_fchain.log pytest_shards.log; do [ -f $OUT/$f ] && tail -3 $OUT/$f; done
 echo "exit=$rc"
 exit $rc
