@@ -301,10 +301,16 @@ __global__ __launch_bounds__(256) void k_rows_div(float* __restrict__ A, int ld,
 // children x S = 500 alphas give 24 blocks of the large shape for 256 CUs,
 // 288 of the small one; measured 2 and 4 chains per thread ran 1.3x and 1.9x
 // slower there).
+// the device's flush of a product (the FTZ reference kernel's product, as
+// pp2_fchain.hip's ftz)
+__device__ __forceinline__ float ftz_f(float v) { return fabsf(v) < FLT_MIN ? copysignf(0.0f, v) : v; }
+
 template <int OP>
 __device__ __forceinline__ float pair_step(float acc, float a, float b) {
   if constexpr (OP == PAIR_L1)
     return acc + fabsf(a - b);
+  else if constexpr (OP == PAIR_CHILD)  // cudaBayesBeliefUpdate's p *= L, flushed (a: L, b: p)
+    return acc + ftz_f(b * ftz_f(a));
   else
     return acc + a * b;
 }
@@ -422,19 +428,20 @@ inline int cdiv(long long a, int b) { return (int)((a + b - 1) / b); }
 constexpr int kSeqCH = 512, kSeqRow = kSeqCH + 4;
 constexpr size_t seq_lds(int tb) { return (size_t)(16 + tb) * kSeqRow * sizeof(float); }
 
-template <int OP, int TB>
-__global__ __launch_bounds__(16 * TB) void k_pair_seq(const float* __restrict__ A, int na,
+template <int OP, int TA, int TB>
+__global__ __launch_bounds__(TA * TB) void k_pair_seq(const float* __restrict__ A, int na,
                                                       const float* __restrict__ B, int nb, int ld,
                                                       int n, float* __restrict__ out, int ldo,
                                                       const int* __restrict__ alist,
                                                       const int* __restrict__ acount) {
-  constexpr int NT = 16 * TB;
-  constexpr int LA4 = (16 * 128 + NT - 1) / NT, LB4 = (TB * 128 + NT - 1) / NT;  // float4 per thread
+  constexpr int NT = TA * TB;
+  static_assert(NT % 64 == 0, "whole waves");
+  constexpr int LA4 = (TA * 128 + NT - 1) / NT, LB4 = (TB * 128 + NT - 1) / NT;  // float4 per thread
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sA = smem;
-  float* sB = smem + 16 * kSeqRow;
-  const int tid = threadIdx.x, la = tid & 15, jb = tid >> 4;
-  const int i0 = blockIdx.x * 16, j0 = blockIdx.y * TB;
+  float* sB = smem + TA * kSeqRow;
+  const int tid = threadIdx.x, la = tid % TA, jb = tid / TA;
+  const int i0 = blockIdx.x * TA, j0 = blockIdx.y * TB;
   if (alist) {
     na = min(na, *acount);
     if (i0 >= na) return;  // (uniform over the block)
@@ -447,7 +454,7 @@ __global__ __launch_bounds__(16 * TB) void k_pair_seq(const float* __restrict__ 
 #pragma unroll
     for (int q = 0; q < LA4; ++q) {
       const int e = tid + NT * q, row = e >> 7, c4 = (e & 127) * 4, ia = i0 + row;
-      ra[q] = e < 16 * 128 && ia < na && x0 + c4 < n
+      ra[q] = e < TA * 128 && ia < na && x0 + c4 < n
                   ? *(const f4*)(A + (long long)arow(ia) * ld + x0 + c4) : f4{0, 0, 0, 0};
     }
 #pragma unroll
@@ -465,7 +472,7 @@ __global__ __launch_bounds__(16 * TB) void k_pair_seq(const float* __restrict__ 
 #pragma unroll
     for (int q = 0; q < LA4; ++q) {
       const int e = tid + NT * q;
-      if (e < 16 * 128) *(f4*)(sA + (e >> 7) * kSeqRow + (e & 127) * 4) = ra[q];
+      if (e < TA * 128) *(f4*)(sA + (e >> 7) * kSeqRow + (e & 127) * 4) = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < LB4; ++q) {
@@ -516,14 +523,64 @@ __global__ __launch_bounds__(16 * TB) void k_pair_seq(const float* __restrict__ 
   if (i0 + la < na && j0 + jb < nb) out[(long long)arow(i0 + la) * ldo + j0 + jb] = acc;
 }
 
-template <int OP, int TB>
+template <int OP, int TA, int TB>
 hipError_t launch_pair_seq(hipStream_t st, const float* A, int na, const float* B, int nb, int ld,
                            int n, float* out, int ldo, const int* alist, const int* acount) {
   static unsigned long long attr = 0ull;
-  allow_lds(reinterpret_cast<const void*>(&k_pair_seq<OP, TB>), attr);
-  hipLaunchKernelGGL((k_pair_seq<OP, TB>), dim3(cdiv(na, 16), cdiv(nb, TB)), dim3(16 * TB),
-                     seq_lds(TB), st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+  allow_lds(reinterpret_cast<const void*>(&k_pair_seq<OP, TA, TB>), attr);
+  hipLaunchKernelGGL((k_pair_seq<OP, TA, TB>), dim3(cdiv(na, TA), cdiv(nb, TB)), dim3(TA * TB),
+                     seq_lds(TA + TB), st, A, na, B, nb, ld, n, out, ldo, alist, acount);
   return hipGetLastError();
+}
+
+// The running sums of one row, sequentially: one wave stages 1024-value
+// chunks in LDS, lane 0 walks them (4 values per LDS read, the next reads
+// issued ahead), the wave stores the running sums; sum[0] = the total.
+// (std::partial_sum / accumulate from +0, x-ordered, search_tree_cuda.cu:
+// 176-183, 225-229.)
+constexpr int kCdfCH = 1024;
+__global__ __launch_bounds__(64) void k_row_cdf_seq(const float* __restrict__ row, int n,
+                                                    float* __restrict__ cdf,
+                                                    float* __restrict__ sum) {
+  __shared__ __attribute__((aligned(16))) float sIn[kCdfCH], sOut[kCdfCH];
+  const int lane = threadIdx.x;
+  float acc = 0.0f;
+  for (int x0 = 0; x0 < n; x0 += kCdfCH) {
+    const int m = min(kCdfCH, n - x0);
+#pragma unroll
+    for (int q = 0; q < kCdfCH / 256; ++q) {
+      const int c4 = 4 * (lane + 64 * q);
+      f4 v = f4{0, 0, 0, 0};
+      if (c4 + 4 <= m) {
+        v = *(const f4*)(row + x0 + c4);
+      } else {
+        for (int k = 0; k < 4; ++k)
+          if (c4 + k < m) v[k] = row[x0 + c4 + k];
+      }
+      *(f4*)(sIn + c4) = v;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      for (int j = 0; j + 4 <= kCdfCH; j += 4) {
+        const f4 v = *(const f4*)(sIn + j);
+        f4 o;
+        acc = acc + v.x;
+        o.x = acc;
+        acc = acc + v.y;
+        o.y = acc;
+        acc = acc + v.z;
+        o.z = acc;
+        acc = acc + v.w;
+        o.w = acc;
+        *(f4*)(sOut + j) = o;
+        if (j + 4 >= m) break;
+      }
+    }
+    __syncthreads();
+    for (int j = lane; j < m; j += 64) cdf[x0 + j] = sOut[j];
+    __syncthreads();
+  }
+  if (lane == 0) *sum = acc;
 }
 
 // ---------------------------------------------------------------- sampling
@@ -877,8 +934,10 @@ hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, con
   const char* seq = getenv("PP2_PAIR_SEQ");
   if (!big && n >= 1024 && !(seq && seq[0] == '0')) {
     if (op == PAIR_L1)
-      return launch_pair_seq<PAIR_L1, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
-    return launch_pair_seq<PAIR_DOT, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+      return launch_pair_seq<PAIR_L1, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+    if (op == PAIR_CHILD)
+      return launch_pair_seq<PAIR_CHILD, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+    return launch_pair_seq<PAIR_DOT, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
   }
   const dim3 grid = big ? dim3(cdiv(na, 64), cdiv(nb, 64)) : dim3(cdiv(na, 16), cdiv(nb, 16 * kNc));
 #define PP2_PAIR(OPV, TAV, NCV, CHV)                                                        \
@@ -892,6 +951,25 @@ hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, con
     else PP2_PAIR(PAIR_DOT, 16, kNc, kCh);
   }
 #undef PP2_PAIR
+  return hipGetLastError();
+}
+
+hipError_t launch_pair_seq_small(hipStream_t st, int op, const float* A, int na, const float* B,
+                                 int nb, int ld, int n, float* out, int ldo, const int* alist,
+                                 const int* acount) {
+  if (na <= 0 || nb <= 0) return hipSuccess;
+  if ((alist == nullptr) != (acount == nullptr) || n <= 0 || ld < n) return hipErrorInvalidValue;
+  // one wave per block (4 A rows x 16 B rows): few chains, each block on a CU of its own
+  if (op == PAIR_DOT)
+    return launch_pair_seq<PAIR_DOT, 4, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+  if (op == PAIR_CHILD)
+    return launch_pair_seq<PAIR_CHILD, 4, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_row_cdf_seq(hipStream_t st, const float* row, int n, float* cdf, float* sum) {
+  if (n <= 0 || !row || !cdf || !sum) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_row_cdf_seq, dim3(1), dim3(64), 0, st, row, n, cdf, sum);
   return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ namespace pp2 {
 constexpr int kPbviChunk = 64;  // x-chunk of the pair kernel and the GEMM (ld multiple)
 constexpr int kGemmTile = 128;  // GEMM tile rows / cols (Sp multiple)
 
-enum PairOp { PAIR_L1 = 0, PAIR_DOT = 1 };
+enum PairOp { PAIR_L1 = 0, PAIR_DOT = 1, PAIR_CHILD = 2 };
 enum RowMode { ROW_SUM = 0, ROW_CDF = 1 };
 
 // ---- pp2_pbvi_dev.hip
@@ -61,6 +61,16 @@ hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float
 hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, const float* B,
                              int nb, int ld, int n, float* out, int ldo,
                              const int* alist = nullptr, const int* acount = nullptr);
+// The reference-order planner's sums on small grids, sequentially, one chain
+// per lane, one wave per block (latency-bound chains: each block on a CU of
+// its own): PAIR_DOT as launch_pair_chain; PAIR_CHILD: the term
+// fl_ftz(B[j][x] * fl_ftz(A[i][x])) (a child's unnormalised belief, A = L
+// rows, B = prediction rows).
+hipError_t launch_pair_seq_small(hipStream_t st, int op, const float* A, int na, const float* B,
+                                 int nb, int ld, int n, float* out, int ldo,
+                                 const int* alist = nullptr, const int* acount = nullptr);
+// cdf[x] = the running sums of row[0 .. n), *sum = the last (std::partial_sum)
+hipError_t launch_row_cdf_seq(hipStream_t st, const float* row, int n, float* cdf, float* sum);
 // The three draws of generateBeliefSet per (belief i, action a): state from
 // cdf row i, next state from T[s][a][:], observation from L[ns][:].
 hipError_t launch_pbvi_sample(hipStream_t st, const Geom& g, PlaneSet T, PlaneSet L,

@@ -438,6 +438,9 @@ __device__ __forceinline__ int xch_gran(int ntiles, int wpr, int slot, int tl, i
 #ifndef PP2_RES_XCD_PLAIN
 #define PP2_RES_XCD_PLAIN 0
 #endif
+#ifndef PP2_RES_XCD_AUX
+#define PP2_RES_XCD_AUX 0  // the same-XCD stores' cache policy (0 plain, 1 sc0, 2 nt)
+#endif
 __device__ __forceinline__ int tile_xcd(int t, int n) {
   const int q = n / 8, r = n % 8;
   return t < r * (q + 1) ? t / (q + 1) : r + (q > 0 ? (t - r * (q + 1)) / q : 0);
@@ -447,7 +450,7 @@ __device__ __forceinline__ void st_quad_x(Rsrc r, int off, const float (&v)[4], 
   const unsigned m = bit << 31;
   const u4v t = {__float_as_uint(v[0]) | m, __float_as_uint(v[1]) | m, __float_as_uint(v[2]) | m,
                  __float_as_uint(v[3]) | m};
-  if (plain) __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, 0);
+  if (plain) __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, PP2_RES_XCD_AUX);
   else __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, kSc1);
 }
 __device__ __forceinline__ bool tagged(const u4v& g, unsigned m) {

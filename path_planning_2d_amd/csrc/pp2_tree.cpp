@@ -179,6 +179,11 @@ struct pp2_planner {
   // the reference's x-ordered fp32 chain (pp2_fchain.hip; the PBVI leaf dots
   // k_pair_chain).
   bool ref = false;
+  // small grids (n <= PP2_SEQ_CHAIN_MAX, default 8192 cells): the sums as
+  // sequential chains, one per lane (launch_pair_seq_small, k_row_cdf_seq),
+  // whose n dependent adds take less than the exact parallel scheme's fixed
+  // latency of three dependent launches (~40 us per chain set)
+  bool seq = false;
   int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
   float* d_rrows = nullptr;     // [9][ld] R[.][a]
   float* d_frows = nullptr;     // [9][ld] FIB alphas[.][i]
@@ -497,12 +502,31 @@ int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows, const int* kl
   return PP2_OK;
 }
 
+// evaluatePbviCpu of one dense normalised row into h_lbv[0] (no-op without
+// PBVI leaves).  Asynchronous.
+int ref_row_pbvi(pp2_planner* p, const float* row) {
+  if (!p->pbvi) return PP2_OK;
+  if (p->scr_pbvi.chains > 0) {
+    // the candidate GEMM reads a whole tile of rows: the row into row 0 of
+    // d_children (scratch between expansions)
+    HIPCHK(hipMemcpyAsync(p->d_children, row, (size_t)p->ref_ld * sizeof(float),
+                          hipMemcpyDeviceToDevice, p->ctx->stream));
+    row = p->d_children;
+  }
+  return ref_pbvi_bounds(p, row, 1);
+}
+
 // The VNode constructor's bounds of one dense normalised row
 // (search_tree_cuda.cu:368-388): evaluateFibCpu's 9 dots into h_rout[9 ..
 // 17], evaluatePbviCpu into h_lbv[0].  Asynchronous.
 int ref_row_bounds(pp2_planner* p, const float* row) {
   pp2_ctx* c = p->ctx;
   CHECK(ref_frows(p));
+  if (p->seq) {
+    HIPCHK(pp2::launch_pair_seq_small(c->stream, pp2::PAIR_DOT, row, 1, p->d_frows, 9, p->ref_ld,
+                                      (int)p->n, p->d_rout + 9, 9));
+    return ref_row_pbvi(p, row);
+  }
   pp2::FcArgs a;
   a.n = (int)p->n;
   a.ld = p->ref_ld;
@@ -512,17 +536,7 @@ int ref_row_bounds(pp2_planner* p, const float* row) {
   a.ldo = 9;
   p->scr_main.attach(&a);
   HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 1, a));
-  if (p->pbvi) {
-    if (p->scr_pbvi.chains > 0) {
-      // the candidate GEMM reads a whole tile of rows: the row into row 0 of
-      // d_children (scratch between expansions)
-      HIPCHK(hipMemcpyAsync(p->d_children, row, (size_t)p->ref_ld * sizeof(float),
-                            hipMemcpyDeviceToDevice, c->stream));
-      row = p->d_children;
-    }
-    CHECK(ref_pbvi_bounds(p, row, 1));
-  }
-  return PP2_OK;
+  return ref_row_pbvi(p, row);
 }
 
 // The children `cs` (c = z * 9 + a) of the expanded belief, normalised, into
@@ -754,6 +768,16 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   // children's tables (side), the cdf driver and running sums (main), the
   // children's driver (side), the samples (main); the rewards last (side).
   HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred, tree_sparse_t(c)));
+  if (p->seq) {
+    // main: the expanded belief's running sums; side: the 144 children's
+    // masses, then the 9 rewards -- sequential chains (small grid)
+    HIPCHK(pp2::launch_row_cdf_seq(c->stream, brow, (int)n, p->d_cdf, p->d_rsum));
+    HIPCHK(pp2::launch_pair_seq_small(p->side, pp2::PAIR_CHILD, p->d_lrows, 16, p->d_pred, 9, ld,
+                                      (int)n, p->d_csum, 9));
+    HIPCHK(hipEventRecord(p->ev_kids, p->side));
+    HIPCHK(pp2::launch_pair_seq_small(p->side, pp2::PAIR_DOT, brow, 1, p->d_rrows, 9, ld, (int)n,
+                                      p->d_rout, 9));
+  }
   pp2::FcArgs cd;  // main: the expanded belief's running sums
   cd.n = (int)n;
   cd.ld = ld;
@@ -769,11 +793,13 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   ch.out = p->d_csum;
   ch.ldo = 1;
   p->scr_side.attach(&ch);
-  HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
-  HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
-  HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
-  HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
-  HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
+  if (!p->seq) {
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
+    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
+    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
+    HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
+  }
   {
     pp2::SampleArgs sa;
     sa.g = c->g;
@@ -790,7 +816,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     sa.kcount = p->d_kcount;
     HIPCHK(pp2::launch_tree_sample(c->stream, sa));
   }
-  {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
+  if (!p->seq) {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
     pp2::FcArgs r;
     r.n = (int)n;
     r.ld = ld;
@@ -806,7 +832,10 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   // masses (side) into their rows of d_children -- only they become nodes
   HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
                                 p->d_csum, p->d_children, (int)n, ld));
-  {  // main: the kept children's FIB dots (evaluateFibCpu)
+  if (p->seq) {  // main: the kept children's FIB dots (evaluateFibCpu), sequential chains
+    HIPCHK(pp2::launch_pair_seq_small(c->stream, pp2::PAIR_DOT, p->d_children, 144, p->d_frows, 9,
+                                      ld, (int)n, p->d_rout + 9, 9, p->d_klist, p->d_kcount));
+  } else {  // main: the kept children's FIB dots (evaluateFibCpu)
     pp2::FcArgs a;
     a.n = (int)n;
     a.ld = ld;
@@ -917,16 +946,23 @@ int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
     const int cz = z * 9 + a;
     HIPCHK(pp2::launch_tree_pred(c->stream, c->g, c->T.v, os.row, p->ref_ld, p->d_pred,
                                  tree_sparse_t(c)));
-    pp2::FcArgs fa;
-    fa.n = (int)p->n;
-    fa.ld = p->ref_ld;
-    fa.pred = p->d_pred;
-    fa.lrows = p->d_lrows;
-    fa.g0 = cz;
-    fa.out = p->d_csum;
-    fa.ldo = 1;
-    p->scr_main.attach(&fa);
-    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_CHILD, 0, 1, fa));
+    if (p->seq) {
+      HIPCHK(pp2::launch_pair_seq_small(c->stream, pp2::PAIR_CHILD,
+                                        p->d_lrows + (size_t)z * p->ref_ld, 1,
+                                        p->d_pred + (size_t)a * p->ref_ld, 1, p->ref_ld, (int)p->n,
+                                        p->d_csum + cz, 1));
+    } else {
+      pp2::FcArgs fa;
+      fa.n = (int)p->n;
+      fa.ld = p->ref_ld;
+      fa.pred = p->d_pred;
+      fa.lrows = p->d_lrows;
+      fa.g0 = cz;
+      fa.out = p->d_csum;
+      fa.ldo = 1;
+      p->scr_main.attach(&fa);
+      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_CHILD, 0, 1, fa));
+    }
     float* dst = ns.row;
     CHECK(ref_store_children(p, &cz, &dst, 1));
   } else {
@@ -1032,6 +1068,11 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "planner scratch allocation failed"));
   p->ref = prm->reference_order == 1;
+  {
+    const char* e = getenv("PP2_SEQ_CHAIN_MAX");
+    const long long lim = e ? atoll(e) : 8192;
+    p->seq = p->ref && (long long)p->n <= lim;
+  }
   // dense rows of the children / PBVI / reference-order passes: the PBVI
   // alphas' row length, else the cells rounded up to 64
   const int row_ld = prm->lower_bound_mode == 1 ? pld : (int)((p->n + 63) / 64 * 64);

@@ -225,22 +225,32 @@ def compare_exact(gi, oi, where):
             assert np.array_equal(a, b), f"{where}: {k} {a} != {b}"
 
 
-@pytest.mark.parametrize("name,max_depth,lb,S,steps", [
-    ("map_10x10", 50, 0, 0, 8),
-    ("sparse_map_100x40", 50, 0, 0, 6),
-    ("sparse_map_100x40", 5, 1, 500, 5),    # the reference node: PBVI leaves, S = 500
-    ("tile64_sparse_map_100x40", 8, 1, 64, 6),
+@pytest.mark.parametrize("name,max_depth,lb,S,steps,seq_max", [
+    ("map_10x10", 50, 0, 0, 8, None),
+    ("sparse_map_100x40", 50, 0, 0, 6, None),
+    ("sparse_map_100x40", 5, 1, 500, 5, None),    # the reference node: PBVI leaves, S = 500
+    ("tile64_sparse_map_100x40", 8, 1, 64, 6, None),
+    # the same small grids on the exact parallel chain sets (pp2_fchain.hip)
+    # instead of the small-grid sequential chains
+    ("sparse_map_100x40", 50, 0, 0, 6, "0"),
+    ("sparse_map_100x40", 5, 1, 500, 3, "0"),
 ])
-def test_planner_reference_order_bit_exact(oracle, name, max_depth, lb, S, steps):
+def test_planner_reference_order_bit_exact(oracle, monkeypatch, name, max_depth, lb, S, steps,
+                                           seq_max):
     """reference_order = 1: rewards, renormalisations and leaf bounds run as
     the reference's own x-ordered fp32 chains (inner_product / accumulate,
     search_tree_cuda.cu:168-173, :225-229; evaluateFibCpu, evaluatePbviCpu),
     so the tree equals the reference-arithmetic oracle at EVERY plan step:
     shape, observations, weights, bounds, rewards, heuristics bit for bit, and
     the chosen action and its value exactly -- deep trees included, where the
-    fp64-accumulating mode may legitimately pick another near-tied node."""
+    fp64-accumulating mode may legitimately pick another near-tied node.
+    Grids up to PP2_SEQ_CHAIN_MAX cells (default 8192) run the sums as
+    sequential lane chains, larger ones as exact parallel chain sets; seq_max
+    "0" forces the latter here."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S_
+    if seq_max is not None:
+        monkeypatch.setenv("PP2_SEQ_CHAIN_MAX", seq_max)
     grid = golden_map(name)
     m = golden("model", name)
     b0 = S_.uniform_belief(grid)

@@ -10,6 +10,15 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#define CK(x)                                                        \
+  do {                                                               \
+    hipError_t e_ = (x);                                             \
+    if (e_ != hipSuccess) {                                          \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));        \
+      return 1;                                                      \
+    }                                                                \
+  } while (0)
+
 typedef unsigned int u2e __attribute__((ext_vector_type(2)));
 typedef unsigned int u4e __attribute__((ext_vector_type(4)));
 
@@ -17,6 +26,52 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_copy(const T* __restrict__ a, T* __restrict__ b, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
     __builtin_nontemporal_store(a[i], b + i);
+}
+
+// Unrolled one-shot copy: each thread moves U 16-B words, all U loads issued
+// before the stores (U loads in flight per lane), the grid sized to the
+// buffer (no grid-stride loop); NT: nontemporal stores, else plain.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_copy_u(const u4e* __restrict__ a, u4e* __restrict__ b,
+                                                size_t n) {
+  const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+  u4e v[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const size_t i = base + (size_t)k * 256;
+    v[k] = i < n ? __builtin_nontemporal_load(a + i) : u4e{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const size_t i = base + (size_t)k * 256;
+    if (i < n) {
+      if (NT) __builtin_nontemporal_store(v[k], b + i);
+      else b[i] = v[k];
+    }
+  }
+}
+
+template <int U, bool NT>
+static int run_u(const char* name, void* a, void* b, size_t bytes) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const size_t n = bytes / 16;
+  const int blocks = (int)((n + 256 * U - 1) / (256 * U));
+  for (int w = 0; w < 2; ++w)
+    hipLaunchKernelGGL((k_copy_u<U, NT>), dim3(blocks), dim3(256), 0, 0, (const u4e*)a, (u4e*)b, n);
+  CK(hipEventRecord(e0));
+  const int reps = 10;
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((k_copy_u<U, NT>), dim3(blocks), dim3(256), 0, 0, (const u4e*)a, (u4e*)b, n);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  printf("%-24s blocks %6d  %8.3f ms  %6.2f TB/s (read+write)\n", name, blocks, ms,
+         2.0 * bytes / (ms * 1e-3) / 1e12);
+  return 0;
 }
 
 // read-only stream (the leaf pass's belief traffic): every word xor-folded
@@ -46,14 +101,6 @@ __global__ __launch_bounds__(256) void k_restream(const float* __restrict__ F, s
   if (acc == 12345.0f) sink[blockIdx.y] = acc;  // never: keeps the loads
 }
 
-#define CK(x)                                                        \
-  do {                                                               \
-    hipError_t e_ = (x);                                             \
-    if (e_ != hipSuccess) {                                          \
-      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));        \
-      return 1;                                                      \
-    }                                                                \
-  } while (0)
 
 template <typename T>
 static int run(const char* name, void* a, void* b, size_t bytes, int blocks) {
@@ -88,6 +135,13 @@ int main(int argc, char** argv) {
     if (run<u2e>("copy 8B/lane", a, b, bytes, blocks)) return 1;
     if (run<u4e>("copy 16B/lane", a, b, bytes, blocks)) return 1;
   }
+  // one-shot unrolled copies (the guide's float4 copy: 6.29 TB/s)
+  if (run_u<1, false>("copy16 U1 plain", a, b, bytes)) return 1;
+  if (run_u<4, false>("copy16 U4 plain", a, b, bytes)) return 1;
+  if (run_u<8, false>("copy16 U8 plain", a, b, bytes)) return 1;
+  if (run_u<1, true>("copy16 U1 nt", a, b, bytes)) return 1;
+  if (run_u<4, true>("copy16 U4 nt", a, b, bytes)) return 1;
+  if (run_u<8, true>("copy16 U8 nt", a, b, bytes)) return 1;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

@@ -26,6 +26,7 @@ run_pmc()     { PMC_DIR=pmc_r05 timeout -k 10 900 bash tools/collect_pmc.sh > $O
 run_pmcx()    { PP2_LIBRARY=$PWD/tools/_var/c_xcd.so PMC_DIR=pmc_r05x timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmcx.log 2>&1; }
 run_shards()  { timeout -k 10 600 python -u -m pytest tests/test_gpu_shards.py tests/test_gpu_resident.py -x -v $T > $OUT/pytest_shards.log 2>&1; }
 run_ab()      { timeout -k 10 900 bash tools/r05_ab.sh > $OUT/ab.log 2>&1; }
+run_copy()    { timeout -k 10 120 tools/micro/copy_bw 2048 > $OUT/copy_bw.txt 2>&1; }
 run_fchain()  { timeout -k 10 300 python -u -m pytest tests/test_gpu_fchain.py -x -v $T > $OUT/pytest_fchain.log 2>&1; }
 run_pbvi()    { PP2_PBVI_STATS=1 timeout -k 10 300 python3 tools/pbvi_plan_timing.py > $OUT/pbvi_plan_timing.txt 2>&1; }
 run_profplan() { PP2_CASE=node PP2_STEPS=30 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_node -o run -- python3 tools/prof_planner.py > $OUT/prof_node.log 2>&1 &&
@@ -35,7 +36,7 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     tests) run_tests ;; planner) run_planner ;; smoke) run_smoke ;; bench) run_bench ;;
-    prof) run_prof ;; pmc) run_pmc ;; pmcx) run_pmcx ;; fchain) run_fchain ;; shards) run_shards ;; ab) run_ab ;; pbvi) run_pbvi ;; profplan) run_profplan ;;
+    prof) run_prof ;; pmc) run_pmc ;; pmcx) run_pmcx ;; fchain) run_fchain ;; copy) run_copy ;; shards) run_shards ;; ab) run_ab ;; pbvi) run_pbvi ;; profplan) run_profplan ;;
     *) echo "unknown step $step"; false ;;
   esac
   rc=$?
