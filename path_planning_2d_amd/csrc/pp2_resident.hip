@@ -436,7 +436,7 @@ __device__ __forceinline__ int xch_gran(int ntiles, int wpr, int slot, int tl, i
 // of the granule runs on the producer's XCD: the tile -> XCD map of
 // xcd_remap (block b on XCD b % 8 owns a contiguous range of tiles).
 #ifndef PP2_RES_XCD_PLAIN
-#define PP2_RES_XCD_PLAIN 0
+#define PP2_RES_XCD_PLAIN 1
 #endif
 #ifndef PP2_RES_XCD_AUX
 #define PP2_RES_XCD_AUX 0  // the same-XCD stores' cache policy (0 plain, 1 sc0, 2 nt)

@@ -179,10 +179,11 @@ struct pp2_planner {
   // the reference's x-ordered fp32 chain (pp2_fchain.hip; the PBVI leaf dots
   // k_pair_chain).
   bool ref = false;
-  // small grids (n <= PP2_SEQ_CHAIN_MAX, default 8192 cells): the sums as
-  // sequential chains, one per lane (launch_pair_seq_small, k_row_cdf_seq),
-  // whose n dependent adds take less than the exact parallel scheme's fixed
-  // latency of three dependent launches (~40 us per chain set)
+  // opt-in (grids of n <= PP2_SEQ_CHAIN_MAX cells; default 0 = off): the
+  // sums as sequential chains, one per lane (launch_pair_seq_small,
+  // k_row_cdf_seq).  Measured slower than the exact parallel chain sets
+  // even at 100 x 40 (node plan step 4.22 vs 3.89 ms): a lane's dependent
+  // add costs ~12 ns per element there (profiles/r05/pbvi_plan_modes_ab.txt)
   bool seq = false;
   int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
   float* d_rrows = nullptr;     // [9][ld] R[.][a]
@@ -1070,7 +1071,7 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   p->ref = prm->reference_order == 1;
   {
     const char* e = getenv("PP2_SEQ_CHAIN_MAX");
-    const long long lim = e ? atoll(e) : 8192;
+    const long long lim = e ? atoll(e) : 0;
     p->seq = p->ref && (long long)p->n <= lim;
   }
   // dense rows of the children / PBVI / reference-order passes: the PBVI
