@@ -46,6 +46,14 @@ constexpr int kGuard = pp2::kPlaneGuard;  // floats of guard before/after each p
 // exchange up to kMaxNormBlock of them per block, the resident shard runs up
 // to all (one exchange per up to kShardHalo steps).
 constexpr int kShardHalo = 128;
+// ... but only the per-cell b / J planes and the code plane carry them: the
+// dense model and FIB planes (568 of the 590 bytes per cell) keep
+// kDenseHalo rows per side, all the per-step paths read (kdepth_max <=
+// kMaxNormBlock); the model generation of a deeper shard writes the deep
+// rows into a transient full-halo copy that only the code plane keeps
+// (pp2_model_generate), so a 2048^2 8-shard group allocates < 10 % above
+// the unsharded planes.
+constexpr int kDenseHalo = 8;
 // Loop normalisation blocks (row shards, and PP2_TUNE_NORM_BLOCK > 1) start
 // by dividing the belief by its exact (global) mass and multiplying by 2^96
 // (exact), then divide by 1: the stored belief decays by < 8 observation
@@ -85,7 +93,9 @@ struct pp2_ctx {
   bool nt_streams = true;   // non-temporal loads of the once-read T/C streams
   bool model_ready = false;
 
-  uint8_t* d_map = nullptr;  // global map (grows x width)
+  uint8_t* d_map = nullptr;  // the map, indexed by global row (only rows [row0 - halo - 1,
+                             // row0 + rows + halo + 1) exist: d_map_alloc)
+  uint8_t* d_map_alloc = nullptr;
   Planes T, L, R, C;         // 81, 16, 9, 9 planes
   Planes b[2];               // belief ping-pong (1 plane)
   int bcur = 0;
@@ -97,6 +107,7 @@ struct pp2_ctx {
   int fcur = 0;
   unsigned fib_version = 1;  // bumped whenever the current alphas change (planner caches)
   unsigned pbvi_version = 1;  // bumped whenever the PBVI alpha vectors change (planner caches)
+  int dense_halo = 1;         // halo rows of the dense model / FIB planes (min(g.halo, kDenseHalo))
   bool fib_finite = true;          // every FIB alpha finite: the sparse / LDS sweeps apply
   float* pbuf[2] = {nullptr, nullptr};  // per-block partial masses of b[0], b[1]
   bool pending[2] = {false, false};     // mass of b[i] still in pbuf[i]
@@ -220,7 +231,8 @@ struct DeviceGuard {
   }
 };
 
-int alloc_planes(pp2_ctx* c, Planes* P, int K);
+// halo < 0: the context's own (g.halo); the dense sets take c->dense_halo
+int alloc_planes(pp2_ctx* c, Planes* P, int K, int halo = -1);
 void free_planes(Planes* P);
 int ensure_staging(pp2_ctx* c, size_t bytes);
 int check_ctx(pp2_ctx* c);          // null check, resident_settle, lost shard state

@@ -42,13 +42,14 @@ int set_err(int code, const char* fmt, ...) {
 }
 
 
-int alloc_planes(pp2_ctx* c, Planes* P, int K) {
+int alloc_planes(pp2_ctx* c, Planes* P, int K, int halo) {
+  if (halo < 0) halo = c->g.halo;
   const long long rs = (long long)K * c->g.wp;
   P->K = K;
-  P->floats = (size_t)(2 * kGuard) + (size_t)(c->g.rows + 2 * c->g.halo) * rs;
+  P->floats = (size_t)(2 * kGuard) + (size_t)(c->g.rows + 2 * halo) * rs;
   HIPCHK(hipMalloc(&P->alloc, P->floats * sizeof(float)));
   HIPCHK(hipMemsetAsync(P->alloc, 0, P->floats * sizeof(float), c->stream));
-  P->v.p = P->alloc + kGuard + (long long)c->g.halo * rs;  // skip the top halo rows
+  P->v.p = P->alloc + kGuard + (long long)halo * rs;  // skip the top halo rows
   P->v.rs = rs;
   P->v.ps = c->g.wp;
   return PP2_OK;
@@ -228,6 +229,7 @@ int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
   c->g.row0 = (int)row_begin;
   c->g.grows = (int)grows;
   c->g.halo = shard ? kShardHalo : 1;  // shards: room for deep halo exchanges
+  c->dense_halo = std::min(c->g.halo, kDenseHalo);
   c->gx = gx;
   c->gy = gy;
   c->gamma = gamma;
@@ -241,19 +243,26 @@ int create_impl(pp2_ctx** out, int device, uint32_t grows, uint32_t width,
   if (hipDeviceGetAttribute(&c->ncus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->ncus = 0;
 
-  const size_t map_bytes = (size_t)grows * width;
-  if (hipMalloc(&c->d_map, map_bytes) != hipSuccess)
+  // the map rows the model generation reads: the shard's rows and halo rows
+  // plus one more per side (a shard keeps its window, not the whole map)
+  const long long mlo = std::max(0LL, (long long)row_begin - c->g.halo - 1);
+  const long long mhi = std::min((long long)grows, (long long)row_end + c->g.halo + 1);
+  const size_t map_bytes = (size_t)(mhi - mlo) * width;
+  if (hipMalloc(&c->d_map_alloc, map_bytes) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "hipMalloc map (%zu B)", map_bytes));
-  if (hipMemcpyAsync(c->d_map, map, map_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+  c->d_map = c->d_map_alloc - mlo * (long long)width;  // indexed by global row
+  if (hipMemcpyAsync(c->d_map_alloc, map + mlo * (long long)width, map_bytes,
+                     hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return fail(set_err(PP2_EHIP, "map upload"));
 
   int s = PP2_OK;
-  if ((s = alloc_planes(c, &c->T, 81)) || (s = alloc_planes(c, &c->L, 16)) ||
-      (s = alloc_planes(c, &c->R, 9)) || (s = alloc_planes(c, &c->C, 9)) ||
+  const int dh = c->dense_halo;
+  if ((s = alloc_planes(c, &c->T, 81, dh)) || (s = alloc_planes(c, &c->L, 16, dh)) ||
+      (s = alloc_planes(c, &c->R, 9, dh)) || (s = alloc_planes(c, &c->C, 9, dh)) ||
       (s = alloc_planes(c, &c->b[0], 1)) || (s = alloc_planes(c, &c->b[1], 1)) ||
       (s = alloc_planes(c, &c->J[0], 1)) || (s = alloc_planes(c, &c->J[1], 1)) ||
-      (s = alloc_planes(c, &c->Jsnap, 1)) || (s = alloc_planes(c, &c->fib[0], 9)) ||
-      (s = alloc_planes(c, &c->fib[1], 9)) || (s = alloc_planes(c, &c->fibsnap, 9)))
+      (s = alloc_planes(c, &c->Jsnap, 1)) || (s = alloc_planes(c, &c->fib[0], 9, dh)) ||
+      (s = alloc_planes(c, &c->fib[1], 9, dh)) || (s = alloc_planes(c, &c->fibsnap, 9, dh)))
     return fail(s);
   const size_t abytes = (size_t)c->g.rows * c->g.wp + 16;
   if (hipMalloc(&c->A, abytes) != hipSuccess ||
@@ -358,7 +367,14 @@ static bool finite_nonneg(float v) {
 // gather of one representative per entry, then a bitwise check of every cell
 // against its entry.  More than kDictMax entries or any mismatch (a hash
 // collision) leaves dict_n = 0, i.e. the dense kernels.
-int build_model_dict(pp2_ctx* c) {
+int build_model_dict(pp2_ctx* c, const Planes* mT, const Planes* mL, const Planes* mR,
+                     const Planes* mC);
+int build_model_dict(pp2_ctx* c) { return build_model_dict(c, &c->T, &c->L, &c->R, &c->C); }
+
+// (mT .. mC: the dense model over rows [-g.halo, rows + g.halo) -- the
+// context's planes, or pp2_model_generate's transient full-halo copy)
+int build_model_dict(pp2_ctx* c, const Planes* mT, const Planes* mL, const Planes* mR,
+                     const Planes* mC) {
   c->dict_n = 0;
   c->res_e_dict = -1;  // shard_resident_e: recomputed (collectively) on the next run
   ++c->agree_gen;      // ... and agreed again (pp2_loop_run)
@@ -389,7 +405,7 @@ int build_model_dict(pp2_ctx* c) {
     ~Free() { (void)hipFree(a); (void)hipFree(b); }
   } fr{d_hash, d_aux};
   std::vector<uint64_t> h((size_t)n);
-  HIPCHK(pp2::launch_dict_hash(c->stream, c->g, c->T.v, c->C.v, c->R.v, c->L.v, d_hash));
+  HIPCHK(pp2::launch_dict_hash(c->stream, c->g, mT->v, mC->v, mR->v, mL->v, d_hash));
   HIPCHK(hipMemcpyAsync(h.data(), d_hash, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost,
                         c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -421,9 +437,9 @@ int build_model_dict(pp2_ctx* c) {
                         hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d_aux, reps.data(), E * sizeof(int), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d_aux + pp2::kDictMax, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(pp2::launch_dict_gather(c->stream, c->g, c->T.v, c->C.v, c->R.v, c->L.v, d_aux, E,
+  HIPCHK(pp2::launch_dict_gather(c->stream, c->g, mT->v, mC->v, mR->v, mL->v, d_aux, E,
                                  c->d_dict));
-  HIPCHK(pp2::launch_dict_verify(c->stream, c->g, c->T.v, c->C.v, c->R.v, c->L.v,
+  HIPCHK(pp2::launch_dict_verify(c->stream, c->g, mT->v, mC->v, mR->v, mL->v,
                                  c->code_alloc + kGuard, c->d_dict, d_aux + pp2::kDictMax));
   int bad = 1;
   std::vector<float> dh((size_t)E * pp2::kDictRow);
@@ -1560,6 +1576,26 @@ const char* pp2_status_string(int s) {
 
 const char* pp2_last_error(void) { return g_last_error.c_str(); }
 
+// Diagnostic (tests/test_gpu_shards.py, not part of pp2.h): the device bytes
+// a context's grid-sized buffers hold -- every plane set, the code plane,
+// the actions and the map window (the fixed-size buffers aside).
+int pp2_debug_context_bytes(pp2_ctx* c, unsigned long long* bytes) {
+  if (!c || !bytes) return set_err(PP2_EINVAL, "null argument");
+  unsigned long long b = 0;
+  for (const Planes* P : {&c->T, &c->L, &c->R, &c->C, &c->b[0], &c->b[1], &c->J[0], &c->J[1],
+                          &c->Jsnap, &c->fib[0], &c->fib[1], &c->fibsnap})
+    b += (unsigned long long)P->floats * sizeof(float);
+  if (c->code_alloc)
+    b += ((unsigned long long)(c->g.rows + 2 * c->g.halo) * c->g.wp + 2 * kGuard) * sizeof(uint16_t);
+  b += (unsigned long long)c->g.rows * c->g.wp + 16;  // actions
+  const long long mlo = std::max(0LL, (long long)c->g.row0 - c->g.halo - 1);
+  const long long mhi =
+      std::min((long long)c->g.grows, (long long)c->g.row0 + c->g.rows + c->g.halo + 1);
+  b += (unsigned long long)(mhi - mlo) * c->g.width;
+  *bytes = b;
+  return PP2_OK;
+}
+
 int pp2_device_count(int* count) {
   if (!count) return set_err(PP2_EINVAL, "count is null");
   *count = 0;
@@ -1596,7 +1632,7 @@ int pp2_destroy(pp2_ctx* c) {
   for (Planes* P : {&c->T, &c->L, &c->R, &c->C, &c->b[0], &c->b[1], &c->J[0],
                     &c->J[1], &c->Jsnap, &c->fib[0], &c->fib[1], &c->fibsnap})
     free_planes(P);
-  if (c->d_map) (void)hipFree(c->d_map);
+  if (c->d_map_alloc) (void)hipFree(c->d_map_alloc);
   if (c->A) (void)hipFree(c->A);
   if (c->bsum) (void)hipFree(c->bsum);
   for (float* pb : c->pbuf)
@@ -1715,10 +1751,36 @@ int pp2_set_cells_per_lane(pp2_ctx* c, int cpt) {
 int pp2_model_generate(pp2_ctx* c) {
   CHECK(check_ctx(c));
   DeviceGuard dg(c->device);
-  HIPCHK(pp2::launch_model_gen(c->stream, c->g, c->d_map, c->gx, c->gy, c->T.v,
-                               c->L.v, c->R.v, c->C.v));
+  if (c->dense_halo >= c->g.halo) {
+    HIPCHK(pp2::launch_model_gen(c->stream, c->g, c->d_map, c->gx, c->gy, c->T.v,
+                                 c->L.v, c->R.v, c->C.v));
+    c->model_ready = true;
+    return build_model_dict(c);
+  }
+  // A shard with deep halo rows: the model over rows [-g.halo, rows +
+  // g.halo) into a transient full-halo copy, the code plane built from it,
+  // then rows [-dense_halo, rows + dense_halo) kept in the context's planes
+  // (contiguous: [row][plane][x])
+  Planes t[4];
+  struct Free {
+    Planes* t;
+    ~Free() { for (int i = 0; i < 4; ++i) free_planes(&t[i]); }
+  } fr{t};
+  const int K[4] = {81, 16, 9, 9};
+  for (int i = 0; i < 4; ++i) CHECK(alloc_planes(c, &t[i], K[i], c->g.halo));
+  HIPCHK(pp2::launch_model_gen(c->stream, c->g, c->d_map, c->gx, c->gy, t[0].v, t[1].v, t[2].v,
+                               t[3].v));
+  Planes* dst[4] = {&c->T, &c->L, &c->R, &c->C};
+  const int dh = c->dense_halo;
+  for (int i = 0; i < 4; ++i)
+    HIPCHK(hipMemcpyAsync(dst[i]->v.p - (long long)dh * dst[i]->v.rs,
+                          t[i].v.p - (long long)dh * t[i].v.rs,
+                          (size_t)(c->g.rows + 2 * dh) * t[i].v.rs * sizeof(float),
+                          hipMemcpyDeviceToDevice, c->stream));
   c->model_ready = true;
-  return build_model_dict(c);
+  const int s = build_model_dict(c, &t[0], &t[1], &t[2], &t[3]);
+  HIPCHK(hipStreamSynchronize(c->stream));  // (before the transient planes go)
+  return s;
 }
 
 int pp2_model_dict_info(pp2_ctx* c, int* entries, int* active) {

@@ -73,6 +73,50 @@ def test_config4_2048_eight_row_shards():
     run_pair(P, grid, goal, tuple(range(0, N + 1, N // 8)), steps=4)
 
 
+def test_config4_shard_group_memory():
+    """The 2048^2 grid in 8 row shards allocates <= 10 % above the unsharded
+    context (round-4 ADVICE): a shard's deep halo (kShardHalo rows per side,
+    for the resident shard runs) lives only in the per-cell b / J planes and
+    the code plane; the dense model and FIB planes keep kDenseHalo rows, and
+    a shard holds only its window of the map.  Counted by the
+    library (every grid-sized buffer), and the group still equals the
+    unsharded grid after a few loop steps."""
+    import ctypes
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    f = P._lib.load().pp2_debug_context_bytes
+    f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]
+
+    def held(ctx):
+        v = ctypes.c_ulonglong()
+        assert f(ctx.handle, ctypes.byref(v)) == 0
+        return v.value
+
+    N = 2048
+    grid = S.synth_grid(N, N, N)
+    goal = S.synth_goal(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            P.ShardGroup(grid, goal, tuple(range(0, N + 1, N // 8)), gamma=float(GAMMA)) as grp:
+        ref.model_generate()
+        grp.model_generate()
+        used_ref = held(ref)
+        used_grp = sum(held(s) for s in grp.shards)
+        assert used_ref > 2_000_000_000  # the dense planes are there
+        print(f"unsharded {used_ref / 1e6:.1f} MB, 8 shards {used_grp / 1e6:.1f} MB")
+        assert used_grp <= 1.10 * used_ref, (used_grp, used_ref)
+        us, zs, _ = S.synth_trajectory(grid, 3, seed=9)
+        b0 = S.uniform_belief(grid)
+        for c in (ref, grp):
+            c.belief_set(b0)
+            c.mdp_reset()
+            for k in range(3):
+                c.loop_step(us[k], zs[k])
+        Jr, Ar = ref.mdp_get()
+        Jg, Ag = grp.mdp_get()
+        np.testing.assert_array_equal(Jg, Jr)
+        np.testing.assert_array_equal(Ag, Ar)
+
+
 def test_shards_mdp_solve_and_fib():
     import path_planning_2d_amd as P
     name = "sparse_map_100x40"
