@@ -2,7 +2,7 @@
 rows [768, 1024) x 2048 of the 2048^2 grid on a 1-rank RCCL communicator,
 16 warm-up + 200 timed loop steps), and the unsharded 1024^2 loop (20-step
 resident launches), on the library PP2_LIBRARY points at -- for same-box A/B
-of builds (tools/r05_ab.sh).  Prints us per step (median of PP2_REPS runs)."""
+of builds (tools/ab_builds.sh).  Prints us per step (median of PP2_REPS runs)."""
 import os
 import sys
 import time

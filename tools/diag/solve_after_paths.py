@@ -1,5 +1,9 @@
+"""Diagnostic: sweeps and wall time of the 1024^2 MDP solve (ctx.mdp_solve)
+fresh and after each other path has touched the context (resident loop,
+sweeps, single belief updates, the pair loop, the dense model) -- a solve
+must not depend on what ran before it."""
 import os, sys, time
-sys.path.insert(0, "/root/repo" if os.path.exists("/root/repo") else os.environ["GRAFT_REPO_ROOT"])
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np, torch
 import path_planning_2d_amd as P
 from path_planning_2d_amd import synthetic as S

@@ -1,15 +1,17 @@
 #!/bin/bash
-# Round-5 GPU driver: one script, one mode per call (tools/README.md).
+# The GPU driver: one script, one mode per step argument (tools/README.md);
+# ROUND (default r05) names the PMC summary directories.
 #   tests    full `pytest -m gpu` suite
 #   planner  tests/test_gpu_planner.py only
 #   bench    driver-style bench (N=1, 20 steps)
 #   prof     rocprofv3 kernel trace of the bench's timed loop + the plan-step legs
 #   pmc      HBM counters of the resident loop / solve (tools/collect_pmc.sh)
-#   fchain   tests/test_gpu_fchain.py (the exact chain sets, FC_PAIR included)
-#   pbvi     tools/pbvi_plan_timing.py (PBVI-leaf plan steps, FC_PAIR vs k_pair_chain)
+#   fchain   tests/test_gpu_fchain.py (the exact chain sets, FC_LIST included)
+#   pbvi     tools/pbvi_plan_timing.py (PBVI-leaf plan steps: k_pair_seq / FC_LIST / k_pair_chain)
 #   profplan rocprofv3 kernel traces of the node and 256^2 PBVI-leaf plan steps
 #   shards   tests/test_gpu_shards.py + test_gpu_resident.py (the resident / shard kernels)
-#   ab       tools/r05_ab.sh: config-4 rank share + 1024^2 loop, in-tree vs tools/_var/*.so
+#   ab       tools/ab_builds.sh: config-4 rank share + 1024^2 loop, in-tree vs tools/_var/*.so
+#   copy     tools/micro/copy_bw (the one-shot copy ceiling, built here with hipcc)
 # Every GPU step has its own time limit, steps are chained with &&.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -22,10 +24,10 @@ run_planner() { timeout -k 10 600 python -u -m pytest tests/test_gpu_planner.py 
 run_smoke()   { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; }
 run_bench()   { timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; }
 run_prof()    { timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --profile --steps 20 --warmup 20 > $OUT/prof.log 2>&1; }
-run_pmc()     { PMC_DIR=pmc_r05 timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmc.log 2>&1; }
-run_pmcx()    { PP2_LIBRARY=$PWD/tools/_var/c_xcd.so PMC_DIR=pmc_r05x timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmcx.log 2>&1; }
+run_pmc()     { PMC_DIR=pmc_${ROUND:-r05} timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmc.log 2>&1; }
+run_pmcx()    { PP2_LIBRARY=$PWD/tools/_var/c_xcd.so PMC_DIR=pmc_${ROUND:-r05}x timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmcx.log 2>&1; }
 run_shards()  { timeout -k 10 600 python -u -m pytest tests/test_gpu_shards.py tests/test_gpu_resident.py -x -v $T > $OUT/pytest_shards.log 2>&1; }
-run_ab()      { timeout -k 10 900 bash tools/r05_ab.sh > $OUT/ab.log 2>&1; }
+run_ab()      { timeout -k 10 900 bash tools/ab_builds.sh > $OUT/ab.log 2>&1; }
 run_copy()    { timeout -k 10 120 tools/micro/copy_bw 2048 > $OUT/copy_bw.txt 2>&1; }
 run_fchain()  { timeout -k 10 300 python -u -m pytest tests/test_gpu_fchain.py -x -v $T > $OUT/pytest_fchain.log 2>&1; }
 run_pbvi()    { PP2_PBVI_STATS=1 timeout -k 10 300 python3 tools/pbvi_plan_timing.py > $OUT/pbvi_plan_timing.txt 2>&1; }
