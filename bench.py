@@ -169,9 +169,9 @@ def sweep_resident_traffic(cells):
     return {"traffic_per_launch": v["hbm_bytes_per_launch"], "avg_launch_us": v.get("avg_us"),
             "algorithmic_bytes_per_launch": algo,
             "traffic_over_algorithmic": v["hbm_bytes_per_launch"] / algo, "source": src,
-            "cause": "every edge-row hand-off granule is an sc1 store / load (round 3), which "
-                     "bypasses L2 to the memory side: each sweep of the solve moves 2 x 8 KB "
-                     "of granules per tile through the fabric/MALL (DESIGN.md §5)"}
+            "cause": "edge-row hand-off granules: plain stores where the neighbouring tile "
+                     "sits on the same XCD (they stay in its L2), sc1 stores / loads only at "
+                     "the XCD boundaries, which go past L2 to the memory side (DESIGN.md §5)"}
 
 
 def cgroup_cpu_quota():
@@ -1150,9 +1150,10 @@ def main():
                          "HBM is not the binding resource: the per-step edge-row hand-off chain "
                          "is, with VALU and LDS about half busy (sq_counters, roofline_lds; "
                          "DESIGN.md §3.2). `traffic` is the memory-side bytes (2*FETCH_SIZE + "
-                         "WRITE_SIZE) per launch: ~8.4 MB per step of them are the edge-row "
-                         "granules (2 x 8 KB per tile per step, sc1 stores and loads, which go "
-                         "past L2 to the memory side), not cell data"
+                         "WRITE_SIZE) per launch; above the algorithmic bytes are the edge-row "
+                         "hand-off granules that cross an XCD boundary (sc1 stores and loads, "
+                         "past L2 to the memory side; same-XCD hand-offs are plain stores that "
+                         "stay in L2), not cell data"
                          if (resident or shard_res) and coded else
                          "bytes the coded kernel must move per launch: code 2, b 4, b' 4, J 4, "
                          "J' 4, A 1 per cell (a pair launch keeps its intermediate step in "
