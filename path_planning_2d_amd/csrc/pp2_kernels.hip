@@ -622,6 +622,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_fib_sweep_sparse(
 // Same values, same arithmetic: the alphas are k_fib_sweep_sparse's bit for
 // bit.  2 blocks (16 waves) per CU.
 constexpr int kFibCols = 256, kFibRows = 2, kFibLs = kFibCols + 4;
+// observations per unrolled step of the (action, observation) loop (A/B builds)
+#ifndef PP2_FIB_UNROLL
+#define PP2_FIB_UNROLL 2
+#endif
+#define PP2_STR_(x) #x
+#define PP2_UNROLL_(n) _Pragma(PP2_STR_(unroll n))
 constexpr int kFibPlane = (kFibRows + 2) * kFibLs;  // observation plane stride in LDS
 typedef __attribute__((address_space(3))) void fib_lds_void;
 
@@ -704,7 +710,7 @@ __global__ __launch_bounds__(kFibCols * kFibRows, 4) void k_fib_sweep_lds(
       lo[j] = (sp / 3) * kFibLs + sp % 3;
     }
     float rtg = 0.0f;
-#pragma unroll 2
+PP2_UNROLL_(PP2_FIB_UNROLL)
     for (int o = 0; o < 16; ++o) {
       const float* wo = wl + o * kFibPlane;
       float tm[4];

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #define CK(x)                                                        \
@@ -33,9 +34,21 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 static int cdiv(long long a, int b) { return (int)((a + b - 1) / b); }
 
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 // ---------------------------------------------------------------- v0: the library shape
 constexpr int kCH = 512, kRow = kCH + 4;
 
+// XCD: the grid is 1-D; block L runs on XCD L % 8 (dispatch order), and
+// the tiles are numbered so that each XCD's blocks cover whole alpha tiles
+// against every row tile (the alphas' chunks then come from that XCD's L2)
+template <bool XCD>
 __global__ __launch_bounds__(256) void k_v0(const float* __restrict__ A, int na,
                                             const float* __restrict__ B, int nb, int ld, int n,
                                             float* __restrict__ out, int ldo) {
@@ -45,7 +58,15 @@ __global__ __launch_bounds__(256) void k_v0(const float* __restrict__ A, int na,
   float* sA = smem;
   float* sB = smem + TA * kRow;
   const int tid = threadIdx.x, la = tid % TA, jb = tid / TA;
-  const int i0 = blockIdx.x * TA, j0 = blockIdx.y * TB;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (XCD) {
+    const int nrt = (na + TA - 1) / TA, ntiles = nrt * ((nb + TB - 1) / TB);
+    const int per = (gridDim.x + 7) / 8, t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (t >= ntiles) return;
+    bx = t % nrt;
+    by = t / nrt;
+  }
+  const int i0 = bx * TA, j0 = by * TB;
   f4 ra[LA4], rb[LB4];
   auto fetch = [&](int x0) {
 #pragma unroll
@@ -243,6 +264,539 @@ __global__ __launch_bounds__(64 * W) void k_tile(const float* __restrict__ A, in
     }
 }
 
+
+// ---------------------------------------------------------------- lanes of two chains, one block per CU
+// Block = 2*RP rows x A alphas; lane q < RP*A: alpha q % A, rows 2(q / A),
+// 2(q / A) + 1 (a packed pair of chains, v_pk_mul_f32 / v_pk_add_f32);
+// ceil(RP*A / 64) waves (at most one per SIMD).  Grid 1-D, tiles numbered
+// per XCD as k_v0<true> (each XCD: whole alpha tiles x every row tile).
+// Per 4 cells a lane reads 3 float4 (its alpha, its two rows); the products
+// of the next group are formed between the dependent adds of this one.
+// MODE 0: the product; 1: chunk 0 only fetched (no global loads after it);
+// 2: no chains (fetch + LDS stores only)
+template <int RP, int A, int CH, int MODE = 0>
+__global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_t2(const float* __restrict__ Ag, int na,
+                                                                const float* __restrict__ Bg, int nb,
+                                                                int ld, int n, float* __restrict__ out,
+                                                                int ldo) {
+  constexpr int NT = (RP * A + 63) / 64 * 64, ROW = CH + 4, NR = 2 * RP + A, C4 = CH / 4;
+  constexpr int L4 = (NR * C4 + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int nrt = (na + 2 * RP - 1) / (2 * RP), ntiles = nrt * ((nb + A - 1) / A);
+  const int per = (gridDim.x + 7) / 8, t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= ntiles) return;
+  const int i0 = (t % nrt) * 2 * RP, j0 = (t / nrt) * A;
+  // LDS rows: 0 .. 2RP-1 the A rows, 2RP .. the alphas
+  f4 rg[L4];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k, r = e / C4, c4 = (e % C4) * 4;
+      f4 v = f4{0, 0, 0, 0};
+      if (e < NR * C4 && x0 + c4 < n) {
+        if (r < 2 * RP) {
+          if (i0 + r < na) v = *(const f4*)(Ag + (long long)(i0 + r) * ld + x0 + c4);
+        } else if (j0 + r - 2 * RP < nb) {
+          v = *(const f4*)(Bg + (long long)(j0 + r - 2 * RP) * ld + x0 + c4);
+        }
+      }
+      rg[k] = v;
+    }
+  };
+  const int q = tid < RP * A ? tid : 0, qa = q % A, qr = q / A;
+  const uint32_t r0_addr = (uint32_t)(uintptr_t)(smem + (2 * qr) * ROW);
+  const uint32_t r1_addr = (uint32_t)(uintptr_t)(smem + (2 * qr + 1) * ROW);
+  const uint32_t b_addr = (uint32_t)(uintptr_t)(smem + (2 * RP + qa) * ROW);
+  f2 acc = f2{0.0f, 0.0f};
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k;
+      if (e < NR * C4) *(f4*)(smem + (e / C4) * ROW + (e % C4) * 4) = rg[k];
+    }
+    __syncthreads();
+    if (x0 + CH < n && MODE != 1) fetch(x0 + CH);
+    if (MODE == 2) {
+      acc[0] += smem[tid];
+      __syncthreads();
+      continue;
+    }
+    constexpr int NG = CH / 4, R = 3, LA = 4, NB = LA + 1;
+    f4 g0[NB], g1[NB], gb[NB];
+    auto rd = [&](int g) {
+      asm volatile("ds_read_b128 %0, %1" : "=v"(g0[g % NB]) : "v"(r0_addr + 16u * g));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(g1[g % NB]) : "v"(r1_addr + 16u * g));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(gb[g % NB]) : "v"(b_addr + 16u * g));
+    };
+    auto wait_for = [&](int g) {
+      // groups issued so far: up to min(h - 1 + LA, NG - 1) for h = g
+      const int left = NG - 1 - g < LA - 1 ? NG - 1 - g : LA - 1;
+      switch (left) {
+        case 3: asm volatile("s_waitcnt lgkmcnt(9)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); break;
+      }
+      asm volatile("" : "+v"(g0[g % NB]), "+v"(g1[g % NB]), "+v"(gb[g % NB]));
+    };
+    auto products = [&](int g, f2 p[4]) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        p[k] = f2{g0[g % NB][k], g1[g % NB][k]} * f2{gb[g % NB][k], gb[g % NB][k]};
+    };
+#pragma unroll
+    for (int g = 0; g < LA; ++g) rd(g);
+    f2 p[4], pn[4];
+    wait_for(0);
+    products(0, p);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g + LA < NG) rd(g + LA);
+      if (g + 1 < NG) {
+        wait_for(g + 1);
+        products(g + 1, pn);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = acc + p[k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p[k] = pn[k];
+    }
+    __syncthreads();
+  }
+  if (tid < RP * A) {
+    const int j = j0 + qa;
+    if (j < nb) {
+      if (i0 + 2 * qr < na) out[(long long)(i0 + 2 * qr) * ldo + j] = acc[0];
+      if (i0 + 2 * qr + 1 < na) out[(long long)(i0 + 2 * qr + 1) * ldo + j] = acc[1];
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------- packed pairs, interleaved rows
+// As k_t2, but each row pair is staged interleaved ([x][2]: r0[x], r1[x]),
+// so one ds_read_b128 returns two cells of both rows already paired for
+// v_pk_mul_f32 (no register shuffles), the alpha broadcast by op_sel; LDS
+// reads take immediate offsets (no address arithmetic per group).
+// MODE 0: the product; 1: no global loads after chunk 0; 3: also no LDS
+// reads after each chunk's first LA groups (the ring's registers reused,
+// opaque to the compiler) -- diagnostics, wrong results.  clk (when given):
+// block 0 thread 0 writes its s_memtime / s_memrealtime span.
+template <int RP, int A, int CH, int MODE = 0>
+__global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_t3(const float* __restrict__ Ag, int na,
+                                                                const float* __restrict__ Bg, int nb,
+                                                                int ld, int n, float* __restrict__ out,
+                                                                int ldo, unsigned long long* clk) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  constexpr int NT = (RP * A + 63) / 64 * 64, C4 = CH / 4;
+  constexpr int PROW = 2 * CH + 4, ROW = CH + 4;  // floats; both = 4 mod 64 banks
+  constexpr int NPI = RP * C4, NAI = A * C4;      // staging items: pair f4-columns, alpha f4s
+  constexpr int LP = (NPI + NT - 1) / NT, LB = (NAI + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sP = smem;
+  float* sB = smem + RP * PROW;
+  const int tid = threadIdx.x;
+  const int nrt = (na + 2 * RP - 1) / (2 * RP), ntiles = nrt * ((nb + A - 1) / A);
+  const int per = (gridDim.x + 7) / 8, t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= ntiles) return;
+  const int i0 = (t % nrt) * 2 * RP, j0 = (t / nrt) * A;
+  f4 rp0[LP], rp1[LP], rb[LB];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const int e = tid + NT * k, p = e / C4, c4 = (e % C4) * 4, r = i0 + 2 * p;
+      const bool ok = e < NPI && x0 + c4 < n;
+      rp0[k] = ok && r < na ? *(const f4*)(Ag + (long long)r * ld + x0 + c4) : f4{0, 0, 0, 0};
+      rp1[k] = ok && r + 1 < na ? *(const f4*)(Ag + (long long)(r + 1) * ld + x0 + c4) : f4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int e = tid + NT * k, a = e / C4, c4 = (e % C4) * 4;
+      rb[k] = e < NAI && j0 + a < nb && x0 + c4 < n ? *(const f4*)(Bg + (long long)(j0 + a) * ld + x0 + c4)
+                                                  : f4{0, 0, 0, 0};
+    }
+  };
+  const int q = tid < RP * A ? tid : 0, qa = q % A, qr = q / A;
+  f2 acc = f2{0.0f, 0.0f};
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const int e = tid + NT * k;
+      if (e < NPI) {
+        float* d = sP + (e / C4) * PROW + (e % C4) * 8;
+        *(f4*)d = f4{rp0[k].x, rp1[k].x, rp0[k].y, rp1[k].y};
+        *(f4*)(d + 4) = f4{rp0[k].z, rp1[k].z, rp0[k].w, rp1[k].w};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int e = tid + NT * k;
+      if (e < NAI) *(f4*)(sB + (e / C4) * ROW + (e % C4) * 4) = rb[k];
+    }
+    __syncthreads();
+    if (x0 + CH < n && MODE == 0) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
+    // plain LDS loads into a ring, LA groups ahead: the compiler numbers
+    // the in-order LDS returns and waits for exactly the group it uses
+    const f4* pp = (const f4*)(sP + qr * PROW);
+    const f4* pb = (const f4*)(sB + qa * ROW);
+    f4 gp0[NB], gp1[NB], gb[NB];
+#pragma unroll
+    for (int g = 0; g < LA; ++g) {
+      gp0[g] = pp[2 * g];
+      gp1[g] = pp[2 * g + 1];
+      gb[g] = pb[g];
+    }
+    f2 pr[4];
+    {
+      const f4 a0 = gp0[0], a1 = gp1[0], b = gb[0];
+      pr[0] = f2{a0.x, a0.y} * f2{b.x, b.x};
+      pr[1] = f2{a0.z, a0.w} * f2{b.y, b.y};
+      pr[2] = f2{a1.x, a1.y} * f2{b.z, b.z};
+      pr[3] = f2{a1.z, a1.w} * f2{b.w, b.w};
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (MODE == 3) {
+        asm volatile("" : "+v"(gp0[(g + 1) % NB]), "+v"(gp1[(g + 1) % NB]), "+v"(gb[(g + 1) % NB]));
+      } else if (g + LA < NG) {
+        gp0[(g + LA) % NB] = pp[2 * (g + LA)];
+        gp1[(g + LA) % NB] = pp[2 * (g + LA) + 1];
+        gb[(g + LA) % NB] = pb[g + LA];
+      }
+      f2 pn[4];
+      if (g + 1 < NG) {
+        const f4 a0 = gp0[(g + 1) % NB], a1 = gp1[(g + 1) % NB], b = gb[(g + 1) % NB];
+        pn[0] = f2{a0.x, a0.y} * f2{b.x, b.x};
+        pn[1] = f2{a0.z, a0.w} * f2{b.y, b.y};
+        pn[2] = f2{a1.x, a1.y} * f2{b.z, b.z};
+        pn[3] = f2{a1.z, a1.w} * f2{b.w, b.w};
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = acc + pr[k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pr[k] = pn[k];
+    }
+    __syncthreads();
+  }
+  if (tid < RP * A) {
+    const int j = j0 + qa;
+    if (j < nb) {
+      if (i0 + 2 * qr < na) out[(long long)(i0 + 2 * qr) * ldo + j] = acc[0];
+      if (i0 + 2 * qr + 1 < na) out[(long long)(i0 + 2 * qr + 1) * ldo + j] = acc[1];
+    }
+  }
+  if (clk && blockIdx.x == 0 && tid == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - c0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
+
+// ---------------------------------------------------------------- t4: t3 with the inner loop in asm
+// Reads by ds_read_b128 with immediate offsets LA groups ahead and counted
+// lgkmcnt waits; products by v_pk_mul_f32 with the alpha broadcast by
+// op_sel straight from its float4's register pair; the pair's dependent
+// v_pk_add_f32 of group g interleaved with the products of group g + 1.
+__device__ __forceinline__ f2 lo2(f4 v) { return __builtin_shufflevector(v, v, 0, 1); }
+__device__ __forceinline__ f2 hi2(f4 v) { return __builtin_shufflevector(v, v, 2, 3); }
+#ifdef PD_ASM_ARITH
+__device__ __forceinline__ f2 pk_mul_blo(f2 a, f2 b) {  // (a.x * b.x, a.y * b.x)
+  f2 r;
+  asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 pk_mul_bhi(f2 a, f2 b) {  // (a.x * b.y, a.y * b.y)
+  f2 r;
+  asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ void pk_acc(f2& acc, f2 p) {
+  asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(acc) : "v"(p));
+}
+__device__ __forceinline__ float mul_f(float a, float b) {
+  float r;
+  asm volatile("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ void add_f(float& acc, float p) {
+  asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc) : "v"(p));
+}
+#else
+// plain arithmetic (the compiler's hazard recognizer pads inline-asm VALU
+// ops with s_nop; these compile to the same v_pk_mul_f32 / v_pk_add_f32 /
+// v_mul_f32 / v_add_f32, in an order the scheduler may change)
+__device__ __forceinline__ f2 pk_mul_blo(f2 a, f2 b) { return a * f2{b.x, b.x}; }
+__device__ __forceinline__ f2 pk_mul_bhi(f2 a, f2 b) { return a * f2{b.y, b.y}; }
+__device__ __forceinline__ void pk_acc(f2& acc, f2 p) { acc = acc + p; }
+__device__ __forceinline__ float mul_f(float a, float b) { return a * b; }
+__device__ __forceinline__ void add_f(float& acc, float p) { acc = acc + p; }
+#endif
+
+template <int NB>
+struct T4Ring {
+  f4 p0[NB], p1[NB], b[NB];
+};
+
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void t4_read(T4Ring<NB>& r, uint32_t pa, uint32_t ba) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.p0[G % NB]) : "v"(pa), "n"(32 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.p1[G % NB]) : "v"(pa), "n"(32 * G + 16));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.b[G % NB]) : "v"(ba), "n"(16 * G));
+}
+
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void t4_products(T4Ring<NB>& r, f2 (&pr)[4]) {
+  // groups issued: up to min(G - 1 + LA, NG - 1); wait for group G
+  constexpr int left = (NG - 1 - G) < (LA - 1) ? (NG - 1 - G) : (LA - 1);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(3 * left) : "memory");
+  asm volatile("" : "+v"(r.p0[G % NB]), "+v"(r.p1[G % NB]), "+v"(r.b[G % NB]));
+  const f4 a0 = r.p0[G % NB], a1 = r.p1[G % NB], b = r.b[G % NB];
+  pr[0] = pk_mul_blo(lo2(a0), lo2(b));
+  pr[1] = pk_mul_bhi(hi2(a0), lo2(b));
+  pr[2] = pk_mul_blo(lo2(a1), hi2(b));
+  pr[3] = pk_mul_bhi(hi2(a1), hi2(b));
+}
+
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void t4_group(T4Ring<NB>& r, uint32_t pa, uint32_t ba, f2& acc, f2 (&pr)[4]) {
+  if constexpr (G < NG) {
+    if constexpr (G + LA < NG) t4_read<G + LA, NG, LA, NB>(r, pa, ba);
+    f2 pn[4];
+    if constexpr (G + 1 < NG) {
+      // wait for group G + 1, then its products between this group's adds
+      constexpr int left = (NG - 2 - G) < (LA - 1) ? (NG - 2 - G) : (LA - 1);
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(3 * left) : "memory");
+      constexpr int H = (G + 1) % NB;
+      asm volatile("" : "+v"(r.p0[H]), "+v"(r.p1[H]), "+v"(r.b[H]));
+      pn[0] = pk_mul_blo(lo2(r.p0[H]), lo2(r.b[H]));
+      pk_acc(acc, pr[0]);
+      pn[1] = pk_mul_bhi(hi2(r.p0[H]), lo2(r.b[H]));
+      pk_acc(acc, pr[1]);
+      pn[2] = pk_mul_blo(lo2(r.p1[H]), hi2(r.b[H]));
+      pk_acc(acc, pr[2]);
+      pn[3] = pk_mul_bhi(hi2(r.p1[H]), hi2(r.b[H]));
+      pk_acc(acc, pr[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pk_acc(acc, pr[k]);
+    }
+    if constexpr (G + 1 < NG) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pr[k] = pn[k];
+      t4_group<G + 1, NG, LA, NB>(r, pa, ba, acc, pr);
+    }
+  }
+}
+
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void t4_prologue(T4Ring<NB>& r, uint32_t pa, uint32_t ba) {
+  if constexpr (G < LA) {
+    t4_read<G, NG, LA, NB>(r, pa, ba);
+    t4_prologue<G + 1, NG, LA, NB>(r, pa, ba);
+  }
+}
+
+template <int RP, int A, int CH>
+__global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_t4(const float* __restrict__ Ag, int na,
+                                                                const float* __restrict__ Bg, int nb,
+                                                                int ld, int n, float* __restrict__ out,
+                                                                int ldo, unsigned long long* clk) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  constexpr int NT = (RP * A + 63) / 64 * 64, C4 = CH / 4;
+  constexpr int PROW = 2 * CH + 4, ROW = CH + 4;
+  constexpr int NPI = RP * C4, NAI = A * C4;
+  constexpr int LP = (NPI + NT - 1) / NT, LB = (NAI + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sP = smem;
+  float* sB = smem + RP * PROW;
+  const int tid = threadIdx.x;
+  const int nrt = (na + 2 * RP - 1) / (2 * RP), ntiles = nrt * ((nb + A - 1) / A);
+  const int per = (gridDim.x + 7) / 8, t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= ntiles) return;
+  const int i0 = (t % nrt) * 2 * RP, j0 = (t / nrt) * A;
+  f4 rp0[LP], rp1[LP], rb[LB];
+  // buffer resources from the block's first row / alpha: loads past the
+  // matrix (rows >= na / nb, cells >= n) are given an offset past the range
+  // and read +0.0, with no branch
+  constexpr int kOff = 0x7ffffff0;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Ag + (long long)i0 * ld), 0, kOff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Bg + (long long)j0 * ld), 0, kOff, 0x00020000);
+  auto ldq = [](__amdgpu_buffer_rsrc_t rs, int off) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  };
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const int e = tid + NT * k, p = e / C4, c4 = (e % C4) * 4, r = 2 * p;
+      const bool ok = e < NPI && x0 + c4 < n;
+      rp0[k] = ldq(rsa, ok && i0 + r < na ? (r * ld + x0 + c4) * 4 : kOff);
+      rp1[k] = ldq(rsa, ok && i0 + r + 1 < na ? ((r + 1) * ld + x0 + c4) * 4 : kOff);
+    }
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int e = tid + NT * k, a = e / C4, c4 = (e % C4) * 4;
+      rb[k] = ldq(rsb, e < NAI && j0 + a < nb && x0 + c4 < n ? (a * ld + x0 + c4) * 4 : kOff);
+    }
+  };
+  const int q = tid < RP * A ? tid : 0, qa = q % A, qr = q / A;
+  const uint32_t pa = (uint32_t)(uintptr_t)(sP + qr * PROW);
+  const uint32_t ba = (uint32_t)(uintptr_t)(sB + qa * ROW);
+  f2 acc = f2{0.0f, 0.0f};
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const int e = tid + NT * k;
+      if (e < NPI) {
+        float* d = sP + (e / C4) * PROW + (e % C4) * 8;
+        *(f4*)d = f4{rp0[k].x, rp1[k].x, rp0[k].y, rp1[k].y};
+        *(f4*)(d + 4) = f4{rp0[k].z, rp1[k].z, rp0[k].w, rp1[k].w};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int e = tid + NT * k;
+      if (e < NAI) *(f4*)(sB + (e / C4) * ROW + (e % C4) * 4) = rb[k];
+    }
+    __syncthreads();
+    if (x0 + CH < n) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
+    T4Ring<NB> ring;
+    f2 pr[4];
+    t4_prologue<0, NG, LA, NB>(ring, pa, ba);
+    t4_products<0, NG, LA, NB>(ring, pr);
+    t4_group<0, NG, LA, NB>(ring, pa, ba, acc, pr);
+    __syncthreads();
+  }
+  if (tid < RP * A) {
+    const int j = j0 + qa;
+    if (j < nb) {
+      if (i0 + 2 * qr < na) out[(long long)(i0 + 2 * qr) * ldo + j] = acc[0];
+      if (i0 + 2 * qr + 1 < na) out[(long long)(i0 + 2 * qr + 1) * ldo + j] = acc[1];
+    }
+  }
+  if (clk && blockIdx.x == 0 && tid == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - c0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
+
+template <int NB>
+struct T1Ring {
+  f4 a[NB], b[NB];
+};
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void t1_read(T1Ring<NB>& r, uint32_t aa, uint32_t ba) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.a[G % NB]) : "v"(aa), "n"(16 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.b[G % NB]) : "v"(ba), "n"(16 * G));
+}
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void t1_prologue(T1Ring<NB>& r, uint32_t aa, uint32_t ba) {
+  if constexpr (G < LA) {
+    t1_read<G, NG, LA, NB>(r, aa, ba);
+    t1_prologue<G + 1, NG, LA, NB>(r, aa, ba);
+  }
+}
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void t1_group(T1Ring<NB>& r, uint32_t aa, uint32_t ba, float& acc, float (&pr)[4]) {
+  if constexpr (G < NG) {
+    if constexpr (G + LA < NG) t1_read<G + LA, NG, LA, NB>(r, aa, ba);
+    constexpr int left = (NG - 1 - G) < LA ? (NG - 1 - G) : LA;
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * left) : "memory");
+    constexpr int H = G % NB;
+    asm volatile("" : "+v"(r.a[H]), "+v"(r.b[H]));
+    const f4 a = r.a[H], b = r.b[H];
+    // products of this group between the adds of the previous one
+    float pn[4];
+    pn[0] = mul_f(a.x, b.x);
+    if (G > 0) add_f(acc, pr[0]);
+    pn[1] = mul_f(a.y, b.y);
+    if (G > 0) add_f(acc, pr[1]);
+    pn[2] = mul_f(a.z, b.z);
+    if (G > 0) add_f(acc, pr[2]);
+    pn[3] = mul_f(a.w, b.w);
+    if (G > 0) add_f(acc, pr[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pr[k] = pn[k];
+    if constexpr (G + 1 == NG) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) add_f(acc, pr[k]);
+    }
+    t1_group<G + 1, NG, LA, NB>(r, aa, ba, acc, pr);
+  }
+}
+
+// ---------------------------------------------------------------- v1: one chain per lane, tuned
+// k_pair_seq's shape (TA A rows x TB alphas per block, thread (la, jb), one
+// scalar chain) with t4's machinery: branch-free buffer-load staging, LDS
+// reads with immediate offsets LA groups ahead, XCD-grouped tiles.
+template <int TA, int TB, int CH>
+__global__ __launch_bounds__(TA * TB) void k_v1(const float* __restrict__ Ag, int na,
+                                               const float* __restrict__ Bg, int nb, int ld, int n,
+                                               float* __restrict__ out, int ldo, unsigned long long* clk) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  constexpr int NT = TA * TB, C4 = CH / 4, ROW = CH + 4;
+  constexpr int NI = (TA + TB) * C4, L4 = (NI + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, la = tid % TA, jb = tid / TA;
+  const int nrt = (na + TA - 1) / TA, ntiles = nrt * ((nb + TB - 1) / TB);
+  const int per = (gridDim.x + 7) / 8, t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= ntiles) return;
+  const int i0 = (t % nrt) * TA, j0 = (t / nrt) * TB;
+  constexpr int kOff = 0x7ffffff0;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Ag + (long long)i0 * ld), 0, kOff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Bg + (long long)j0 * ld), 0, kOff, 0x00020000);
+  f4 rg[L4];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k, r = e / C4, c4 = (e % C4) * 4;
+      int off = kOff;
+      __amdgpu_buffer_rsrc_t rs = rsa;
+      if (r < TA) {
+        if (i0 + r < na && x0 + c4 < n) off = (r * ld + x0 + c4) * 4;
+      } else {
+        rs = rsb;
+        if (e < NI && j0 + r - TA < nb && x0 + c4 < n) off = ((r - TA) * ld + x0 + c4) * 4;
+      }
+      rg[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  };
+  const uint32_t aa = (uint32_t)(uintptr_t)(smem + la * ROW);
+  const uint32_t ba = (uint32_t)(uintptr_t)(smem + (TA + jb) * ROW);
+  float acc = 0.0f;
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k;
+      if (e < NI) *(f4*)(smem + (e / C4) * ROW + (e % C4) * 4) = rg[k];
+    }
+    __syncthreads();
+    if (x0 + CH < n) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
+    T1Ring<NB> ring;
+    t1_prologue<0, NG, LA, NB>(ring, aa, ba);
+    float pr[4];
+    t1_group<0, NG, LA, NB>(ring, aa, ba, acc, pr);
+    __syncthreads();
+  }
+  if (i0 + la < na && j0 + jb < nb) out[(long long)(i0 + la) * ldo + j0 + jb] = acc;
+  if (clk && blockIdx.x == 0 && tid == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - c0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
 // ---------------------------------------------------------------- harness
 static uint64_t sm_state = 0x243F6A8885A308D3ull;
 static uint64_t splitmix() {
@@ -269,16 +823,84 @@ static void launch_tile(hipStream_t st, const float* A, int na, const float* B, 
                      lds, st, A, na, B, nb, ld, n, out, ldo);
 }
 
+template <bool XCD>
 static void launch_v0(hipStream_t st, const float* A, int na, const float* B, int nb, int ld, int n,
                       float* out, int ldo) {
   const size_t lds = (size_t)32 * kRow * sizeof(float);
   static bool once = false;
   if (!once) {
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_v0),
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_v0<XCD>),
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     once = true;
   }
-  hipLaunchKernelGGL(k_v0, dim3(cdiv(na, 16), cdiv(nb, 16)), dim3(256), lds, st, A, na, B, nb, ld, n, out, ldo);
+  if (XCD) {
+    const int tiles = cdiv(na, 16) * cdiv(nb, 16);
+    hipLaunchKernelGGL(k_v0<XCD>, dim3(cdiv(tiles, 8) * 8), dim3(256), lds, st, A, na, B, nb, ld, n, out, ldo);
+  } else {
+    hipLaunchKernelGGL(k_v0<XCD>, dim3(cdiv(na, 16), cdiv(nb, 16)), dim3(256), lds, st, A, na, B, nb, ld, n,
+                       out, ldo);
+  }
+}
+
+static unsigned long long* g_clk = nullptr;
+template <int RP, int A, int CH, int MODE = 0>
+static void launch_t3(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n,
+                      float* out, int ldo) {
+  const size_t lds = (size_t)(RP * (2 * CH + 4) + A * (CH + 4)) * sizeof(float);
+  static bool once = false;
+  if (!once) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_t3<RP, A, CH, MODE>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    once = true;
+  }
+  const int tiles = cdiv(na, 2 * RP) * cdiv(nb, A);
+  hipLaunchKernelGGL((k_t3<RP, A, CH, MODE>), dim3(cdiv(tiles, 8) * 8), dim3((RP * A + 63) / 64 * 64), lds,
+                     st, Ag, na, Bg, nb, ld, n, out, ldo, g_clk);
+}
+
+template <int RP, int A, int CH>
+static void launch_t4(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n,
+                      float* out, int ldo) {
+  const size_t lds = (size_t)(RP * (2 * CH + 4) + A * (CH + 4)) * sizeof(float);
+  static bool once = false;
+  if (!once) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_t4<RP, A, CH>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    once = true;
+  }
+  const int tiles = cdiv(na, 2 * RP) * cdiv(nb, A);
+  hipLaunchKernelGGL((k_t4<RP, A, CH>), dim3(cdiv(tiles, 8) * 8), dim3((RP * A + 63) / 64 * 64), lds, st,
+                     Ag, na, Bg, nb, ld, n, out, ldo, g_clk);
+}
+
+template <int TA, int TB, int CH>
+static void launch_v1(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n,
+                      float* out, int ldo) {
+  const size_t lds = (size_t)(TA + TB) * (CH + 4) * sizeof(float);
+  static bool once = false;
+  if (!once) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_v1<TA, TB, CH>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    once = true;
+  }
+  const int tiles = cdiv(na, TA) * cdiv(nb, TB);
+  hipLaunchKernelGGL((k_v1<TA, TB, CH>), dim3(cdiv(tiles, 8) * 8), dim3(TA * TB), lds, st, Ag, na, Bg, nb, ld,
+                     n, out, ldo, g_clk);
+}
+
+template <int RP, int A, int CH, int MODE = 0>
+static void launch_t2(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n,
+                      float* out, int ldo) {
+  const size_t lds = (size_t)(2 * RP + A) * (CH + 4) * sizeof(float);
+  static bool once = false;
+  if (!once) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_t2<RP, A, CH, MODE>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    once = true;
+  }
+  const int tiles = cdiv(na, 2 * RP) * cdiv(nb, A);
+  hipLaunchKernelGGL((k_t2<RP, A, CH, MODE>), dim3(cdiv(tiles, 8) * 8), dim3((RP * A + 63) / 64 * 64), lds, st,
+                     Ag, na, Bg, nb, ld, n, out, ldo);
 }
 
 struct Variant {
@@ -314,15 +936,15 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dB, hB.data(), hB.size() * 4, hipMemcpyHostToDevice));
   hipStream_t st;
   CK(hipStreamCreate(&st));
+  CK(hipMalloc(&g_clk, 16));
   const Variant vs[] = {
-      {"v0 k_pair_seq 16x16, 1 chain/lane", launch_v0},
-      {"tile RR2 CA1 W4 CH256 (144 blk)", launch_tile<2, 1, 4, 256>},
-      {"tile RR2 CA1 W3 CH256 (192 blk)", launch_tile<2, 1, 3, 256>},
-      {"tile RR2 CA1 W2 CH256 (288 blk)", launch_tile<2, 1, 2, 256>},
-      {"tile RR1 CA2 W4 CH256", launch_tile<1, 2, 4, 256>},
-      {"tile RR2 CA2 W4 CH128", launch_tile<2, 2, 4, 128>},
-      {"tile RR4 CA1 W4 CH256", launch_tile<4, 1, 4, 256>},
-      {"tile RR2 CA1 W4 CH512", launch_tile<2, 1, 4, 512>},
+      {"v0 k_pair_seq 16x16, 1 chain/lane", launch_v0<false>},
+      {"t4 16 rows x 32 alphas (pk pairs)", launch_t4<8, 32, 512>},
+      {"t4 16 rows x 18 alphas (pk pairs)", launch_t4<8, 18, 512>},
+      {"t4 16x32 CH256", launch_t4<8, 32, 256>},
+      {"v1 16x16 (1 chain/lane, tuned)", launch_v1<16, 16, 512>},
+      {"v1 16x8 (1 chain/lane, tuned)", launch_v1<16, 8, 512>},
+      {"v1 8x16 (1 chain/lane, tuned)", launch_v1<8, 16, 512>},
   };
   const int NV = sizeof(vs) / sizeof(vs[0]);
   std::vector<float> ref((size_t)na * nb), got((size_t)na * nb);
@@ -368,8 +990,13 @@ int main(int argc, char** argv) {
       best = ms < best ? ms : best;
       tot += ms;
     }
-    printf("%-40s min %8.1f us  mean %8.1f us  bit-exact vs v0: %s\n", vs[v].name, best * 1e3,
+    unsigned long long hc[2] = {0, 0};
+    CK(hipMemcpy(hc, g_clk, 16, hipMemcpyDeviceToHost));
+    CK(hipMemset(g_clk, 0, 16));
+    printf("%-40s min %8.1f us  mean %8.1f us  bit-exact vs v0: %s", vs[v].name, best * 1e3,
            tot / reps * 1e3, same ? "yes" : "NO");
+    if (hc[1]) printf("  block 0: %.2f cycles/cell, clock %.2f GHz", (double)hc[0] / n, hc[0] / (hc[1] * 10.0));
+    printf("\n");
     fflush(stdout);
   }
   return bad ? 2 : 0;
