@@ -523,6 +523,241 @@ __global__ __launch_bounds__(TA * TB) void k_pair_seq(const float* __restrict__ 
   if (i0 + la < na && j0 + jb < nb) out[(long long)arow(i0 + la) * ldo + j0 + jb] = acc;
 }
 
+// ---------------------------------------------------------------- PBVI leaf dots
+// The planner's reference-order PBVI leaf dots (evaluatePbviCpu,
+// point_based_value_iteration_cuda.cu:678-699: acc = acc + a[x] * b[x] from
+// +0, x in order): <= 144 kept children x S alphas of up to a grid's cells,
+// each pair one chain whose length alone sets the time once every chain has
+// a lane (tools/micro/pair_dots.hip measures the shapes).  Two shapes, both
+// with branch-free staging (buffer loads; past the matrix they read +0.0,
+// whose products leave a chain unchanged), the chunk's LDS reads issued LA
+// groups ahead of their use (the compiler counts the in-order LDS returns)
+// and the blocks' tiles numbered per XCD (each XCD takes whole alpha tiles
+// against every row tile):
+//   k_pair_dot_pk  a lane keeps two chains (rows 2p, 2p + 1 against one
+//                  alpha) as one packed pair: v_pk_mul_f32 / v_pk_add_f32,
+//                  the IEEE products and sums of the scalar ops; the row
+//                  pair is staged interleaved, so one ds_read_b128 returns
+//                  two cells of both rows already paired;
+//   k_pair_dot_1   one chain per lane (k_pair_seq's thread layout).
+// PP2_PAIR_DOT selects: 1 packed, 2 one chain per lane, 0 k_pair_seq.
+constexpr int kDotOff = 0x7ffffff0;  // buffer offset past any range: the load reads +0.0
+__device__ __forceinline__ f4 ldq_rs(__amdgpu_buffer_rsrc_t rs, int off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+__device__ __forceinline__ int xcd_tile(int ntiles_grid) {
+  const int per = (ntiles_grid + 7) / 8;
+  return (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+}
+
+typedef float f2p __attribute__((ext_vector_type(2)));
+
+template <int RP, int A, int CH>
+__global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_pair_dot_pk(
+    const float* __restrict__ Ag, int na, const float* __restrict__ Bg, int nb, int ld, int n,
+    float* __restrict__ out, int ldo, const int* __restrict__ alist, const int* __restrict__ acount) {
+  constexpr int NT = (RP * A + 63) / 64 * 64, C4 = CH / 4;
+  constexpr int PROW = 2 * CH + 4, ROW = CH + 4;  // floats; both = 4 (mod 64) banks
+  constexpr int NPI = RP * C4, NAI = A * C4;      // staging items: pair float4 columns, alpha float4s
+  constexpr int LP = (NPI + NT - 1) / NT, LB = (NAI + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sP = smem;
+  float* sB = smem + RP * PROW;
+  if (alist) na = min(na, *acount);
+  const int tid = threadIdx.x;
+  const int nrt = (na + 2 * RP - 1) / (2 * RP), ntiles = nrt * ((nb + A - 1) / A);
+  const int t = xcd_tile(gridDim.x);
+  if (t >= ntiles) return;  // (uniform over the block)
+  const int i0 = (t % nrt) * 2 * RP, j0 = (t / nrt) * A;
+  // rows through the full A (alist: any row of it), alphas from the tile's first
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)Ag, 0, kDotOff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Bg + (long long)j0 * ld), 0, kDotOff, 0x00020000);
+  auto arow = [&](int i) { return alist ? alist[i] : i; };
+  int ro0[LP], ro1[LP];  // the staged rows' word offsets (kDotOff / 4: past the matrix)
+#pragma unroll
+  for (int k = 0; k < LP; ++k) {
+    const int e = tid + NT * k, r = i0 + 2 * (e / C4);
+    ro0[k] = e < NPI && r < na ? arow(r) * ld : kDotOff / 4;
+    ro1[k] = e < NPI && r + 1 < na ? arow(r + 1) * ld : kDotOff / 4;
+  }
+  f4 rp0[LP], rp1[LP], rb[LB];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const int c4 = ((tid + NT * k) % C4) * 4;
+      const bool in = x0 + c4 < n;
+      rp0[k] = ldq_rs(rsa, in && ro0[k] != kDotOff / 4 ? (ro0[k] + x0 + c4) * 4 : kDotOff);
+      rp1[k] = ldq_rs(rsa, in && ro1[k] != kDotOff / 4 ? (ro1[k] + x0 + c4) * 4 : kDotOff);
+    }
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int e = tid + NT * k, a = e / C4, c4 = (e % C4) * 4;
+      rb[k] = ldq_rs(rsb, e < NAI && j0 + a < nb && x0 + c4 < n ? (a * ld + x0 + c4) * 4 : kDotOff);
+    }
+  };
+  const int q = tid < RP * A ? tid : 0, qa = q % A, qr = q / A;
+  const f4* pp = (const f4*)(sP + qr * PROW);
+  const f4* pb = (const f4*)(sB + qa * ROW);
+  f2p acc = f2p{0.0f, 0.0f};
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const int e = tid + NT * k;
+      if (e < NPI) {
+        float* d = sP + (e / C4) * PROW + (e % C4) * 8;
+        *(f4*)d = f4{rp0[k].x, rp1[k].x, rp0[k].y, rp1[k].y};
+        *(f4*)(d + 4) = f4{rp0[k].z, rp1[k].z, rp0[k].w, rp1[k].w};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int e = tid + NT * k;
+      if (e < NAI) *(f4*)(sB + (e / C4) * ROW + (e % C4) * 4) = rb[k];
+    }
+    __syncthreads();
+    if (x0 + CH < n) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
+    f4 g0[NB], g1[NB], gb[NB];
+#pragma unroll
+    for (int g = 0; g < LA; ++g) {
+      g0[g] = pp[2 * g];
+      g1[g] = pp[2 * g + 1];
+      gb[g] = pb[g];
+    }
+    // the products of group g + 1 are formed between the dependent adds of group g
+    f2p pr[4];
+    pr[0] = f2p{g0[0].x, g0[0].y} * f2p{gb[0].x, gb[0].x};
+    pr[1] = f2p{g0[0].z, g0[0].w} * f2p{gb[0].y, gb[0].y};
+    pr[2] = f2p{g1[0].x, g1[0].y} * f2p{gb[0].z, gb[0].z};
+    pr[3] = f2p{g1[0].z, g1[0].w} * f2p{gb[0].w, gb[0].w};
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g + LA < NG) {
+        g0[(g + LA) % NB] = pp[2 * (g + LA)];
+        g1[(g + LA) % NB] = pp[2 * (g + LA) + 1];
+        gb[(g + LA) % NB] = pb[g + LA];
+      }
+      if (g + 1 < NG) {
+        const int h = (g + 1) % NB;
+        const f4 a0 = g0[h], a1 = g1[h], b = gb[h];
+        const f2p n0 = f2p{a0.x, a0.y} * f2p{b.x, b.x};
+        acc = acc + pr[0];
+        const f2p n1 = f2p{a0.z, a0.w} * f2p{b.y, b.y};
+        acc = acc + pr[1];
+        const f2p n2 = f2p{a1.x, a1.y} * f2p{b.z, b.z};
+        acc = acc + pr[2];
+        const f2p n3 = f2p{a1.z, a1.w} * f2p{b.w, b.w};
+        acc = acc + pr[3];
+        pr[0] = n0;
+        pr[1] = n1;
+        pr[2] = n2;
+        pr[3] = n3;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = acc + pr[k];
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < RP * A) {
+    const int j = j0 + qa, i = i0 + 2 * qr;
+    if (j < nb) {
+      if (i < na) out[(long long)arow(i) * ldo + j] = acc[0];
+      if (i + 1 < na) out[(long long)arow(i + 1) * ldo + j] = acc[1];
+    }
+  }
+}
+
+template <int TA, int TB, int CH>
+__global__ __launch_bounds__(TA * TB) void k_pair_dot_1(
+    const float* __restrict__ Ag, int na, const float* __restrict__ Bg, int nb, int ld, int n,
+    float* __restrict__ out, int ldo, const int* __restrict__ alist, const int* __restrict__ acount) {
+  constexpr int NT = TA * TB, C4 = CH / 4, ROW = CH + 4;
+  constexpr int NI = (TA + TB) * C4, L4 = (NI + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  if (alist) na = min(na, *acount);
+  const int tid = threadIdx.x, la = tid % TA, jb = tid / TA;
+  const int nrt = (na + TA - 1) / TA, ntiles = nrt * ((nb + TB - 1) / TB);
+  const int t = xcd_tile(gridDim.x);
+  if (t >= ntiles) return;  // (uniform over the block)
+  const int i0 = (t % nrt) * TA, j0 = (t / nrt) * TB;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)Ag, 0, kDotOff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Bg + (long long)j0 * ld), 0, kDotOff, 0x00020000);
+  auto arow = [&](int i) { return alist ? alist[i] : i; };
+  int ro[L4];  // staged row e / C4: A rows first (word offsets in A), then the alphas (in B)
+#pragma unroll
+  for (int k = 0; k < L4; ++k) {
+    const int e = tid + NT * k, r = e / C4;
+    ro[k] = e >= NI ? kDotOff / 4
+            : r < TA ? (i0 + r < na ? arow(i0 + r) * ld : kDotOff / 4)
+                     : (j0 + r - TA < nb ? (r - TA) * ld : kDotOff / 4);
+  }
+  f4 rg[L4];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k, c4 = (e % C4) * 4;
+      const int off = ro[k] != kDotOff / 4 && x0 + c4 < n ? (ro[k] + x0 + c4) * 4 : kDotOff;
+      rg[k] = ldq_rs(e / C4 < TA ? rsa : rsb, off);
+    }
+  };
+  const f4* pa = (const f4*)(smem + la * ROW);
+  const f4* pb = (const f4*)(smem + (TA + jb) * ROW);
+  float acc = 0.0f;
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k;
+      if (e < NI) *(f4*)(smem + (e / C4) * ROW + (e % C4) * 4) = rg[k];
+    }
+    __syncthreads();
+    if (x0 + CH < n) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
+    f4 ga[NB], gb[NB];
+#pragma unroll
+    for (int g = 0; g < LA; ++g) {
+      ga[g] = pa[g];
+      gb[g] = pb[g];
+    }
+    float pr[4];
+    pr[0] = ga[0].x * gb[0].x;
+    pr[1] = ga[0].y * gb[0].y;
+    pr[2] = ga[0].z * gb[0].z;
+    pr[3] = ga[0].w * gb[0].w;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g + LA < NG) {
+        ga[(g + LA) % NB] = pa[g + LA];
+        gb[(g + LA) % NB] = pb[g + LA];
+      }
+      if (g + 1 < NG) {
+        const f4 a = ga[(g + 1) % NB], b = gb[(g + 1) % NB];
+        const float n0 = a.x * b.x;
+        acc = acc + pr[0];
+        const float n1 = a.y * b.y;
+        acc = acc + pr[1];
+        const float n2 = a.z * b.z;
+        acc = acc + pr[2];
+        const float n3 = a.w * b.w;
+        acc = acc + pr[3];
+        pr[0] = n0;
+        pr[1] = n1;
+        pr[2] = n2;
+        pr[3] = n3;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = acc + pr[k];
+      }
+    }
+    __syncthreads();
+  }
+  if (i0 + la < na && j0 + jb < nb) out[(long long)arow(i0 + la) * ldo + j0 + jb] = acc;
+}
+
 template <int OP, int TA, int TB>
 hipError_t launch_pair_seq(hipStream_t st, const float* A, int na, const float* B, int nb, int ld,
                            int n, float* out, int ldo, const int* alist, const int* acount) {
@@ -916,6 +1151,38 @@ hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float
   return hipGetLastError();
 }
 
+// The planner's PBVI leaf dots: the packed two-chain shape by default
+// (PP2_PAIR_DOT: 1 packed, 2 one chain per lane, 0 k_pair_seq).
+static hipError_t launch_pair_dot(hipStream_t st, const float* A, int na, const float* B, int nb,
+                                  int ld, int n, float* out, int ldo, const int* alist,
+                                  const int* acount) {
+  const char* env = getenv("PP2_PAIR_DOT");
+  const int mode = env && *env ? atoi(env) : 0;
+  // 32-bit buffer offsets: the rows (alist entries index the na rows of A)
+  // and a tile's alphas
+  const bool fits = (long long)na * ld < (long long)kDotOff / 4 && 32LL * ld < (long long)kDotOff / 4;
+  if (mode == 0 || !fits)
+    return launch_pair_seq<PAIR_DOT, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+  if (mode == 2) {
+    constexpr int TA = 16, TB = 16, CH = 512;
+    static unsigned long long attr = 0ull;
+    allow_lds(reinterpret_cast<const void*>(&k_pair_dot_1<TA, TB, CH>), attr);
+    const int tiles = cdiv(na, TA) * cdiv(nb, TB);
+    hipLaunchKernelGGL((k_pair_dot_1<TA, TB, CH>), dim3(cdiv(tiles, 8) * 8), dim3(TA * TB),
+                       (size_t)(TA + TB) * (CH + 4) * sizeof(float), st, A, na, B, nb, ld, n, out, ldo,
+                       alist, acount);
+    return hipGetLastError();
+  }
+  constexpr int RP = 8, AL = 32, CH = 512;
+  static unsigned long long attr = 0ull;
+  allow_lds(reinterpret_cast<const void*>(&k_pair_dot_pk<RP, AL, CH>), attr);
+  const int tiles = cdiv(na, 2 * RP) * cdiv(nb, AL);
+  hipLaunchKernelGGL((k_pair_dot_pk<RP, AL, CH>), dim3(cdiv(tiles, 8) * 8), dim3(RP * AL),
+                     (size_t)(RP * (2 * CH + 4) + AL * (CH + 4)) * sizeof(float), st, A, na, B, nb, ld,
+                     n, out, ldo, alist, acount);
+  return hipGetLastError();
+}
+
 hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, const float* B,
                              int nb, int ld, int n, float* out, int ldo, const int* alist,
                              const int* acount) {
@@ -937,7 +1204,7 @@ hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, con
       return launch_pair_seq<PAIR_L1, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
     if (op == PAIR_CHILD)
       return launch_pair_seq<PAIR_CHILD, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
-    return launch_pair_seq<PAIR_DOT, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+    return launch_pair_dot(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
   }
   const dim3 grid = big ? dim3(cdiv(na, 64), cdiv(nb, 64)) : dim3(cdiv(na, 16), cdiv(nb, 16 * kNc));
 #define PP2_PAIR(OPV, TAV, NCV, CHV)                                                        \

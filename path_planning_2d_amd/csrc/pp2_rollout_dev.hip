@@ -140,10 +140,16 @@ __device__ __forceinline__ void dma16(const void* g, void* l) {
 // the code row (512), the R_u row (1 KB) and 64 edge dwords (lane l of the
 // edge copy writes dword l: 2j / 2j+1 = copy j's x-1 / x+256 dwords, 2CH /
 // 2CH+1 the code row's).
+// PP2_BAND_DMA16 (A/B builds; needs wp % 8 == 0): the belief rows by 16-B
+// LDS-DMA, two copies' rows per instruction (lanes 0-31 / 32-63), the code
+// row by half a wave -- 5 DMA instructions per row instead of 12.
+#ifndef PP2_BAND_DMA16
+#define PP2_BAND_DMA16 0
+#endif
 template <int CH>
 struct Slot {
   static constexpr int code = CH * 512, r = code + 512, edge = r + 1024, bytes = edge + 256;
-  static constexpr int groups = 2 * CH + 4;  // DMA instructions per row
+  static constexpr int groups = PP2_BAND_DMA16 ? CH / 2 + 3 : 2 * CH + 4;  // DMA instructions per row
 };
 
 // One wave's band: rows [ya, yb) of the segment starting at xs.
@@ -191,19 +197,34 @@ __device__ __forceinline__ void band(const BandArgs& a, const float* sTu, const 
   const float* rbase = a.R.p + (long long)u * a.R.ps + xs;
   const bool rok = xs + 4 * lane < g.wp;  // R lane (4 floats)
   // issue the DMA group of row r (beliefs, codes, edges, R_u) into a slot
+  // 16-B DMA lanes: 8 cells of copy 2k + (lane >> 5) per instruction k
+  const int qx = xs + 8 * (lane & 31);
+  const bool qok = qx < g.wp;
+  const uint32_t qb = 2u * (uint32_t)qx;
   auto issue = [&](int r, char* slot) {
     const uint32_t ro = (uint32_t)(r + 1) * rowb;
+    if constexpr (PP2_BAND_DMA16) {
 #pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      dma4(cptr(bb[j], d0ok ? ro + db0 : 0u), slot + j * 512);
-      dma4(cptr(bb[j], d1ok ? ro + db1 : 0u), slot + j * 512 + 256);
-    }
-    if constexpr (SRC != kDense) {
-      dma4(cptr(a.code, d0ok ? ro + db0 : 0u), slot + SL_::code);
-      dma4(cptr(a.code, d1ok ? ro + db1 : 0u), slot + SL_::code + 256);
+      for (int k = 0; k < CH / 2; ++k) {
+        const _Float16* src = lane < 32 ? bb[2 * k] : bb[2 * k + 1];
+        dma16(cptr(src, qok ? ro + qb : 0u), slot + 2 * k * 512);
+      }
+      if (lane < 32) dma16(cptr(SRC != kDense ? (const void*)a.code : (const void*)bb[0],
+                                SRC != kDense && qok ? ro + qb : 0u),
+                           slot + SL_::code);
     } else {
-      dma4(cptr(bb[0], 0u), slot + SL_::code);  // keep G fixed (zeros)
-      dma4(cptr(bb[0], 0u), slot + SL_::code + 256);
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        dma4(cptr(bb[j], d0ok ? ro + db0 : 0u), slot + j * 512);
+        dma4(cptr(bb[j], d1ok ? ro + db1 : 0u), slot + j * 512 + 256);
+      }
+      if constexpr (SRC != kDense) {
+        dma4(cptr(a.code, d0ok ? ro + db0 : 0u), slot + SL_::code);
+        dma4(cptr(a.code, d1ok ? ro + db1 : 0u), slot + SL_::code + 256);
+      } else {
+        dma4(cptr(bb[0], 0u), slot + SL_::code);  // keep G fixed (zeros)
+        dma4(cptr(bb[0], 0u), slot + SL_::code + 256);
+      }
     }
     const int rr = r < yb ? (r >= 0 ? r : 0) : yb - 1;  // R rows stay inside the grid
     dma16(rbase + (rok ? (long long)rr * a.R.rs + 4 * lane : 0), slot + SL_::r);

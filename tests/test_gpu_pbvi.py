@@ -125,6 +125,34 @@ def test_evaluate_batch_matches_oracle(pp2, oracle):
         assert np.float32(vo) == v[i] and ao == a[i], i
 
 
+@pytest.mark.parametrize("mode", ["1", "2", "0"])
+def test_evaluate_dot_shapes_bit_exact(pp2, oracle, monkeypatch, mode):
+    """The leaf-dot kernels (PP2_PAIR_DOT 1: packed two-chain lanes, 2: one
+    chain per lane, 0: k_pair_seq) against evaluatePbviCpu's x-ordered chain
+    on adversarial rows: an odd number of beliefs (a packed pair with no
+    partner row), zeros, subnormal and huge terms, mixed-sign alphas, a
+    ragged S."""
+    monkeypatch.setenv("PP2_PAIR_DOT", mode)
+    ctx, (H, W, T, L, R), b0 = setup(pp2, oracle, "sparse_map_100x40")
+    rng = np.random.default_rng(11)
+    S, hw = 53, H * W
+    al = rng.uniform(-40, 5, (S, hw)).astype(np.float32)
+    al[3, ::7] = 3e38
+    al[4, ::5] = -1e-30
+    act = rng.integers(0, 9, S).astype(np.uint8)
+    beliefs = (rng.random((19, hw)) * (rng.random((19, hw)) < 0.6)).astype(np.float32)
+    beliefs[2, 1::3] = np.float32(1e-42)  # subnormal terms
+    beliefs[5] = 0.0
+    beliefs[5, hw - 1] = 1.0
+    beliefs[7, ::11] = 7e-39
+    with ctx:
+        ctx.pbvi_set(al, act)
+        v, a = ctx.pbvi_evaluate(beliefs)
+    for i in range(len(beliefs)):
+        vo, ao = oracle.pbvi_eval(beliefs[i], al, act)
+        assert np.float32(vo).view(np.uint32) == np.float32(v[i]).view(np.uint32) and ao == a[i], i
+
+
 def test_reference_configuration_properties(pp2):
     """S = 500, 100x40, the reference's iteration count: every belief's
     action is valid, values are finite and below the FIB upper bound (within

@@ -7,11 +7,16 @@
 #   prof     rocprofv3 kernel trace of the bench's timed loop + the plan-step legs
 #   pmc      HBM counters of the resident loop / solve (tools/collect_pmc.sh)
 #   fchain   tests/test_gpu_fchain.py (the exact chain sets, FC_LIST included)
-#   pbvi     tools/pbvi_plan_timing.py (PBVI-leaf plan steps: k_pair_seq / FC_LIST / k_pair_chain)
+#   pbvi     tools/pbvi_plan_timing.py (PBVI-leaf plan steps: packed / one-chain / k_pair_seq dots)
 #   profplan rocprofv3 kernel traces of the node and 256^2 PBVI-leaf plan steps
 #   shards   tests/test_gpu_shards.py + test_gpu_resident.py (the resident / shard kernels)
 #   ab       tools/ab_builds.sh: config-4 rank share + 1024^2 loop, in-tree vs tools/_var/*.so
 #   copy     tools/micro/copy_bw (the one-shot copy ceiling, built here with hipcc)
+#   pbvitests tests/test_gpu_pbvi.py (the PBVI kernels, the leaf-dot shapes)
+#   dots     tools/micro/pair_dots (the leaf-dot shapes in isolation, built here with hipcc)
+#   rollsq   SQ counters of the rollout's band kernel (tools/collect_lds_pmc.sh)
+#   abroll   tests/test_gpu_rollout.py on each tools/_var/roll_*.so, then tools/ab_rollout.sh
+#   abfib    tools/fib_ab_timing.py on the in-tree library and tools/_var/fib_*.so
 # Every GPU step has its own time limit, steps are chained with &&.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -29,6 +34,12 @@ run_pmcx()    { PP2_LIBRARY=$PWD/tools/_var/c_xcd.so PMC_DIR=pmc_${ROUND:-r05}x 
 run_shards()  { timeout -k 10 600 python -u -m pytest tests/test_gpu_shards.py tests/test_gpu_resident.py -x -v $T > $OUT/pytest_shards.log 2>&1; }
 run_ab()      { timeout -k 10 900 bash tools/ab_builds.sh > $OUT/ab.log 2>&1; }
 run_copy()    { timeout -k 10 120 tools/micro/copy_bw 2048 > $OUT/copy_bw.txt 2>&1; }
+run_pbvitests() { timeout -k 10 300 python -u -m pytest tests/test_gpu_pbvi.py -x -v $T > $OUT/pytest_pbvi.log 2>&1; }
+run_dots()    { timeout -k 10 120 tools/micro/pair_dots > $OUT/pair_dots.txt 2>&1; }
+run_rollsq()  { PMC_OUT=rollout_sq DRIVER="tools/prof_rollout.py --reps 2" timeout -k 10 300 bash tools/collect_lds_pmc.sh > $OUT/rollout_sq.log 2>&1; }
+run_abroll()  { for lib in tools/_var/roll_*.so; do PP2_LIBRARY=$PWD/$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_rollout.py -x -q $T > $OUT/pytest_rollout_$(basename $lib .so).log 2>&1 || return 1; done &&
+                AB_GLOB="tools/_var/roll_*.so" timeout -k 10 600 bash tools/ab_rollout.sh > $OUT/ab_rollout.log 2>&1; }
+run_abfib()   { AB_SCRIPT=tools/fib_ab_timing.py AB_GLOB="tools/_var/fib_*.so" timeout -k 10 600 bash tools/ab_builds.sh > $OUT/ab_fib.log 2>&1; }
 run_fchain()  { timeout -k 10 300 python -u -m pytest tests/test_gpu_fchain.py -x -v $T > $OUT/pytest_fchain.log 2>&1; }
 run_pbvi()    { PP2_PBVI_STATS=1 timeout -k 10 300 python3 tools/pbvi_plan_timing.py > $OUT/pbvi_plan_timing.txt 2>&1; }
 run_profplan() { PP2_CASE=node PP2_STEPS=30 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_node -o run -- python3 tools/prof_planner.py > $OUT/prof_node.log 2>&1 &&
@@ -38,12 +49,12 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     tests) run_tests ;; planner) run_planner ;; smoke) run_smoke ;; bench) run_bench ;;
-    prof) run_prof ;; pmc) run_pmc ;; pmcx) run_pmcx ;; fchain) run_fchain ;; copy) run_copy ;; shards) run_shards ;; ab) run_ab ;; pbvi) run_pbvi ;; profplan) run_profplan ;;
+    prof) run_prof ;; pmc) run_pmc ;; pbvitests) run_pbvitests ;; dots) run_dots ;; rollsq) run_rollsq ;; abroll) run_abroll ;; abfib) run_abfib ;; pmcx) run_pmcx ;; fchain) run_fchain ;; copy) run_copy ;; shards) run_shards ;; ab) run_ab ;; pbvi) run_pbvi ;; profplan) run_profplan ;;
     *) echo "unknown step $step"; false ;;
   esac
   rc=$?
   [ $rc -ne 0 ] && break
 done
-for f in pytest_gpu.log pytest_planner.log pytest_fchain.log pytest_shards.log; do [ -f $OUT/$f ] && tail -3 $OUT/$f; done
+for f in pytest_gpu.log pytest_planner.log pytest_fchain.log pytest_shards.log pytest_pbvi.log; do [ -f $OUT/$f ] && tail -3 $OUT/$f; done
 echo "exit=$rc"
 exit $rc

@@ -1,7 +1,8 @@
 """The bench's PBVI-leaf plan steps alone, reference order, with the PBVI
-leaf dots as FC_LIST candidate chain sets (PP2_PBVI_FCHAIN=1), as the
-lookahead lane-per-chain k_pair_seq (default) and as k_pair_chain
-(PP2_PAIR_SEQ=0), alternated on one box:
+leaf dots as packed two-chain lanes (k_pair_dot_pk, PP2_PAIR_DOT=1, the
+default), one chain per lane (k_pair_dot_1, =2), the round-5 lookahead
+k_pair_seq (=0) and, with PP2_AB_FC=1, FC_LIST candidate chain sets
+(PP2_PBVI_FCHAIN=1), alternated on one box:
   * 256^2 synthetic, S = 500 alphas, depth 3 (bench plan_step_pbvi_lb);
   * sparse_map_100x40, goal (95, 34), depth 50 (bench node_plan_step).
 The alphas come from the full PBVI solve (PP2_ITERS backups, 0 = the
@@ -33,11 +34,13 @@ def main():
         calls = ctx.pbvi_belief_set(b0, 500)
         ctx.pbvi_backup(int(os.environ.get("PP2_ITERS", "0")))
         res = {}
-        modes = (("seq", "0", "1"), ("fc", "1", "1"), ("pair", "0", "0"))
+        modes = [("pk", "0", "1"), ("one", "0", "2"), ("seq", "0", "0")]
+        if os.environ.get("PP2_AB_FC") == "1":
+            modes.append(("fc", "1", "1"))
         for rep in range(2):
             for mode, fc, sq in modes:
                 os.environ["PP2_PBVI_FCHAIN"] = fc
-                os.environ["PP2_PAIR_SEQ"] = sq
+                os.environ["PP2_PAIR_DOT"] = sq
                 with P.QVTreePlanner(ctx, max_search_tree_depth=depth, max_online_iteration=15,
                                      lower_bound_mode=1, rand_skip=calls) as pl:
                     S.closed_loop(grid, b0, pl.step, 3)
@@ -46,14 +49,16 @@ def main():
                     ms, acts, vals = S.closed_loop(grid, b0, pl.step, steps)
                 res.setdefault(mode, []).append((float(np.percentile(ms, 50)), acts, vals))
         ctx.close()
-        for mode, name in (("seq", "k_pair_seq (default)"),
-                           ("fc", "FC_LIST candidate chain sets (PP2_PBVI_FCHAIN=1)"),
-                           ("pair", "k_pair_chain (PP2_PAIR_SEQ=0)")):
+        names = {"pk": "k_pair_dot_pk (default)", "one": "k_pair_dot_1 (PP2_PAIR_DOT=2)",
+                 "seq": "k_pair_seq (PP2_PAIR_DOT=0)",
+                 "fc": "FC_LIST candidate chain sets (PP2_PBVI_FCHAIN=1)"}
+        for mode, _, _ in modes:
+            name = names[mode]
             p50 = [r[0] for r in res[mode]]
             print(f"{label}: {name}: p50 {p50[0]:.3f} / {p50[1]:.3f} ms", flush=True)
-        same = all(np.array_equal(res[m][k][1], res["pair"][k][1]) and
-                   np.array_equal(res[m][k][2].view(np.uint32), res["pair"][k][2].view(np.uint32))
-                   for k in range(2) for m in ("seq", "fc"))
+        same = all(np.array_equal(res[m][k][1], res["seq"][k][1]) and
+                   np.array_equal(res[m][k][2].view(np.uint32), res["seq"][k][2].view(np.uint32))
+                   for k in range(2) for m, _, _ in modes)
         print(f"{label}: actions and values identical across the modes: {same}", flush=True)
 
 
