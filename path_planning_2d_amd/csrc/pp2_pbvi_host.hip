@@ -552,6 +552,101 @@ __device__ __forceinline__ int xcd_tile(int ntiles_grid) {
 
 typedef float f2p __attribute__((ext_vector_type(2)));
 
+// The chains' LDS reads: ds_read_b128 at immediate offsets into a ring of NB
+// register groups, LA groups ahead of their use, with counted lgkmcnt waits
+// (the compiler, left to itself, waits for each group as it issues it).
+// One group = 4 cells: R reads (the packed kernel: the row pair's two
+// float4 and the alpha's; the one-chain kernel: the row's and the alpha's).
+template <int NB, int R>
+struct DotRing {
+  f4 v[NB][R];
+};
+template <int G, int NB>
+__device__ __forceinline__ void dot_read_pk(DotRing<NB, 3>& r, uint32_t pa, uint32_t ba) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.v[G % NB][0]) : "v"(pa), "n"(32 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.v[G % NB][1]) : "v"(pa), "n"(32 * G + 16));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.v[G % NB][2]) : "v"(ba), "n"(16 * G));
+}
+template <int G, int NB>
+__device__ __forceinline__ void dot_read_1(DotRing<NB, 2>& r, uint32_t aa, uint32_t ba) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.v[G % NB][0]) : "v"(aa), "n"(16 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.v[G % NB][1]) : "v"(ba), "n"(16 * G));
+}
+// wait until group G has landed (groups issued so far: up to min(G - 1 + LA, NG - 1))
+template <int G, int NG, int LA, int NB, int R>
+__device__ __forceinline__ void dot_wait(DotRing<NB, R>& r) {
+  constexpr int left = (NG - 1 - G) < (LA - 1) ? (NG - 1 - G) : (LA - 1);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(R * left) : "memory");
+#pragma unroll
+  for (int k = 0; k < R; ++k) asm volatile("" : "+v"(r.v[G % NB][k]));
+}
+// packed: the products of group G (row pair x the alpha's cell, broadcast)
+template <int G, int NB>
+__device__ __forceinline__ void dot_products_pk(const DotRing<NB, 3>& r, f2p (&pr)[4]) {
+  const f4 a0 = r.v[G % NB][0], a1 = r.v[G % NB][1], b = r.v[G % NB][2];
+  pr[0] = f2p{a0.x, a0.y} * f2p{b.x, b.x};
+  pr[1] = f2p{a0.z, a0.w} * f2p{b.y, b.y};
+  pr[2] = f2p{a1.x, a1.y} * f2p{b.z, b.z};
+  pr[3] = f2p{a1.z, a1.w} * f2p{b.w, b.w};
+}
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void dot_chunk_pk(DotRing<NB, 3>& r, uint32_t pa, uint32_t ba, f2p& acc,
+                                             f2p (&pr)[4]) {
+  if constexpr (G < NG) {
+    if constexpr (G + LA < NG) dot_read_pk<G + LA, NB>(r, pa, ba);
+    if constexpr (G + 1 < NG) {
+      // group G + 1's products between group G's dependent adds
+      dot_wait<G + 1, NG, LA, NB, 3>(r);
+      f2p pn[4];
+      dot_products_pk<G + 1, NB>(r, pn);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc = acc + pr[k];
+        pr[k] = pn[k];
+      }
+      dot_chunk_pk<G + 1, NG, LA, NB>(r, pa, ba, acc, pr);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = acc + pr[k];
+    }
+  }
+}
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void dot_chunk_1(DotRing<NB, 2>& r, uint32_t aa, uint32_t ba, float& acc,
+                                            float (&pr)[4]) {
+  if constexpr (G < NG) {
+    if constexpr (G + LA < NG) dot_read_1<G + LA, NB>(r, aa, ba);
+    if constexpr (G + 1 < NG) {
+      dot_wait<G + 1, NG, LA, NB, 2>(r);
+      const f4 a = r.v[(G + 1) % NB][0], b = r.v[(G + 1) % NB][1];
+      const float pn[4] = {a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc = acc + pr[k];
+        pr[k] = pn[k];
+      }
+      dot_chunk_1<G + 1, NG, LA, NB>(r, aa, ba, acc, pr);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = acc + pr[k];
+    }
+  }
+}
+template <int G, int LA, int NB>
+__device__ __forceinline__ void dot_prologue_pk(DotRing<NB, 3>& r, uint32_t pa, uint32_t ba) {
+  if constexpr (G < LA) {
+    dot_read_pk<G, NB>(r, pa, ba);
+    dot_prologue_pk<G + 1, LA, NB>(r, pa, ba);
+  }
+}
+template <int G, int LA, int NB>
+__device__ __forceinline__ void dot_prologue_1(DotRing<NB, 2>& r, uint32_t aa, uint32_t ba) {
+  if constexpr (G < LA) {
+    dot_read_1<G, NB>(r, aa, ba);
+    dot_prologue_1<G + 1, LA, NB>(r, aa, ba);
+  }
+}
+
 template <int RP, int A, int CH>
 __global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_pair_dot_pk(
     const float* __restrict__ Ag, int na, const float* __restrict__ Bg, int nb, int ld, int n,
@@ -597,8 +692,8 @@ __global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_pair_dot_pk(
     }
   };
   const int q = tid < RP * A ? tid : 0, qa = q % A, qr = q / A;
-  const f4* pp = (const f4*)(sP + qr * PROW);
-  const f4* pb = (const f4*)(sB + qa * ROW);
+  const uint32_t pa = (uint32_t)(uintptr_t)(sP + qr * PROW);
+  const uint32_t ba = (uint32_t)(uintptr_t)(sB + qa * ROW);
   f2p acc = f2p{0.0f, 0.0f};
   fetch(0);
   for (int x0 = 0; x0 < n; x0 += CH) {
@@ -618,47 +713,13 @@ __global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_pair_dot_pk(
     }
     __syncthreads();
     if (x0 + CH < n) fetch(x0 + CH);
-    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
-    f4 g0[NB], g1[NB], gb[NB];
-#pragma unroll
-    for (int g = 0; g < LA; ++g) {
-      g0[g] = pp[2 * g];
-      g1[g] = pp[2 * g + 1];
-      gb[g] = pb[g];
-    }
-    // the products of group g + 1 are formed between the dependent adds of group g
+    constexpr int NG = CH / 4, LA = 5, NB = LA + 1;  // 3 reads per group: lgkmcnt <= 15
+    DotRing<NB, 3> ring;
+    dot_prologue_pk<0, LA, NB>(ring, pa, ba);
+    dot_wait<0, NG, LA, NB, 3>(ring);
     f2p pr[4];
-    pr[0] = f2p{g0[0].x, g0[0].y} * f2p{gb[0].x, gb[0].x};
-    pr[1] = f2p{g0[0].z, g0[0].w} * f2p{gb[0].y, gb[0].y};
-    pr[2] = f2p{g1[0].x, g1[0].y} * f2p{gb[0].z, gb[0].z};
-    pr[3] = f2p{g1[0].z, g1[0].w} * f2p{gb[0].w, gb[0].w};
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (g + LA < NG) {
-        g0[(g + LA) % NB] = pp[2 * (g + LA)];
-        g1[(g + LA) % NB] = pp[2 * (g + LA) + 1];
-        gb[(g + LA) % NB] = pb[g + LA];
-      }
-      if (g + 1 < NG) {
-        const int h = (g + 1) % NB;
-        const f4 a0 = g0[h], a1 = g1[h], b = gb[h];
-        const f2p n0 = f2p{a0.x, a0.y} * f2p{b.x, b.x};
-        acc = acc + pr[0];
-        const f2p n1 = f2p{a0.z, a0.w} * f2p{b.y, b.y};
-        acc = acc + pr[1];
-        const f2p n2 = f2p{a1.x, a1.y} * f2p{b.z, b.z};
-        acc = acc + pr[2];
-        const f2p n3 = f2p{a1.z, a1.w} * f2p{b.w, b.w};
-        acc = acc + pr[3];
-        pr[0] = n0;
-        pr[1] = n1;
-        pr[2] = n2;
-        pr[3] = n3;
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc = acc + pr[k];
-      }
-    }
+    dot_products_pk<0, NB>(ring, pr);
+    dot_chunk_pk<0, NG, LA, NB>(ring, pa, ba, acc, pr);
     __syncthreads();
   }
   if (tid < RP * A) {
@@ -704,8 +765,8 @@ __global__ __launch_bounds__(TA * TB) void k_pair_dot_1(
       rg[k] = ldq_rs(e / C4 < TA ? rsa : rsb, off);
     }
   };
-  const f4* pa = (const f4*)(smem + la * ROW);
-  const f4* pb = (const f4*)(smem + (TA + jb) * ROW);
+  const uint32_t aa = (uint32_t)(uintptr_t)(smem + la * ROW);
+  const uint32_t ba = (uint32_t)(uintptr_t)(smem + (TA + jb) * ROW);
   float acc = 0.0f;
   fetch(0);
   for (int x0 = 0; x0 < n; x0 += CH) {
@@ -716,43 +777,19 @@ __global__ __launch_bounds__(TA * TB) void k_pair_dot_1(
     }
     __syncthreads();
     if (x0 + CH < n) fetch(x0 + CH);
-    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
-    f4 ga[NB], gb[NB];
-#pragma unroll
-    for (int g = 0; g < LA; ++g) {
-      ga[g] = pa[g];
-      gb[g] = pb[g];
-    }
+    constexpr int NG = CH / 4, LA = 7, NB = LA + 1;  // 2 reads per group: lgkmcnt <= 15
+    DotRing<NB, 2> ring;
+    dot_prologue_1<0, LA, NB>(ring, aa, ba);
+    dot_wait<0, NG, LA, NB, 2>(ring);
     float pr[4];
-    pr[0] = ga[0].x * gb[0].x;
-    pr[1] = ga[0].y * gb[0].y;
-    pr[2] = ga[0].z * gb[0].z;
-    pr[3] = ga[0].w * gb[0].w;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (g + LA < NG) {
-        ga[(g + LA) % NB] = pa[g + LA];
-        gb[(g + LA) % NB] = pb[g + LA];
-      }
-      if (g + 1 < NG) {
-        const f4 a = ga[(g + 1) % NB], b = gb[(g + 1) % NB];
-        const float n0 = a.x * b.x;
-        acc = acc + pr[0];
-        const float n1 = a.y * b.y;
-        acc = acc + pr[1];
-        const float n2 = a.z * b.z;
-        acc = acc + pr[2];
-        const float n3 = a.w * b.w;
-        acc = acc + pr[3];
-        pr[0] = n0;
-        pr[1] = n1;
-        pr[2] = n2;
-        pr[3] = n3;
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc = acc + pr[k];
-      }
+    {
+      const f4 a = ring.v[0][0], b = ring.v[0][1];
+      pr[0] = a.x * b.x;
+      pr[1] = a.y * b.y;
+      pr[2] = a.z * b.z;
+      pr[3] = a.w * b.w;
     }
+    dot_chunk_1<0, NG, LA, NB>(ring, aa, ba, acc, pr);
     __syncthreads();
   }
   if (i0 + la < na && j0 + jb < nb) out[(long long)arow(i0 + la) * ldo + j0 + jb] = acc;
@@ -1157,10 +1194,10 @@ static hipError_t launch_pair_dot(hipStream_t st, const float* A, int na, const 
                                   int ld, int n, float* out, int ldo, const int* alist,
                                   const int* acount) {
   const char* env = getenv("PP2_PAIR_DOT");
-  const int mode = env && *env ? atoi(env) : 0;
+  const int mode = env && *env ? atoi(env) : 1;
   // 32-bit buffer offsets: the rows (alist entries index the na rows of A)
   // and a tile's alphas
-  const bool fits = (long long)na * ld < (long long)kDotOff / 4 && 32LL * ld < (long long)kDotOff / 4;
+  const bool fits = (long long)na * ld < (long long)kDotOff / 4 && 18LL * ld < (long long)kDotOff / 4;
   if (mode == 0 || !fits)
     return launch_pair_seq<PAIR_DOT, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
   if (mode == 2) {
@@ -1173,11 +1210,11 @@ static hipError_t launch_pair_dot(hipStream_t st, const float* A, int na, const 
                        alist, acount);
     return hipGetLastError();
   }
-  constexpr int RP = 8, AL = 32, CH = 512;
+  constexpr int RP = 8, AL = 18, CH = 512;  // 144 x 500: 9 x 28 = 252 blocks, one per CU
   static unsigned long long attr = 0ull;
   allow_lds(reinterpret_cast<const void*>(&k_pair_dot_pk<RP, AL, CH>), attr);
   const int tiles = cdiv(na, 2 * RP) * cdiv(nb, AL);
-  hipLaunchKernelGGL((k_pair_dot_pk<RP, AL, CH>), dim3(cdiv(tiles, 8) * 8), dim3(RP * AL),
+  hipLaunchKernelGGL((k_pair_dot_pk<RP, AL, CH>), dim3(cdiv(tiles, 8) * 8), dim3((RP * AL + 63) / 64 * 64),
                      (size_t)(RP * (2 * CH + 4) + AL * (CH + 4)) * sizeof(float), st, A, na, B, nb, ld,
                      n, out, ldo, alist, acount);
   return hipGetLastError();

@@ -140,16 +140,14 @@ __device__ __forceinline__ void dma16(const void* g, void* l) {
 // the code row (512), the R_u row (1 KB) and 64 edge dwords (lane l of the
 // edge copy writes dword l: 2j / 2j+1 = copy j's x-1 / x+256 dwords, 2CH /
 // 2CH+1 the code row's).
-// PP2_BAND_DMA16 (A/B builds; needs wp % 8 == 0): the belief rows by 16-B
-// LDS-DMA, two copies' rows per instruction (lanes 0-31 / 32-63), the code
-// row by half a wave -- 5 DMA instructions per row instead of 12.
-#ifndef PP2_BAND_DMA16
-#define PP2_BAND_DMA16 0
-#endif
-template <int CH>
+// W16 (row stride wp % 8 == 0, and 16-B aligned copy planes): the belief
+// rows by 16-B LDS-DMA, two copies' rows per instruction (lanes 0-31 /
+// 32-63), the code row by half a wave -- 5 DMA instructions per row instead
+// of 12 (512^2 x 4096 x 5: 5.34 vs 5.46-5.69 ms, profiles/r05/ab_rollout_dma16.txt).
+template <int CH, bool W16>
 struct Slot {
   static constexpr int code = CH * 512, r = code + 512, edge = r + 1024, bytes = edge + 256;
-  static constexpr int groups = PP2_BAND_DMA16 ? CH / 2 + 3 : 2 * CH + 4;  // DMA instructions per row
+  static constexpr int groups = W16 ? CH / 2 + 3 : 2 * CH + 4;  // DMA instructions per row
 };
 
 // One wave's band: rows [ya, yb) of the segment starting at xs.
@@ -161,12 +159,12 @@ struct Slot {
 // store them into row -1 and add 0 to every statistic, so no lane is masked
 // (the dense source zeroes their L_z explicitly: its L plane is read at the
 // clamped cell).
-template <int CH, int NS, int SRC, int U>
+template <int CH, int NS, int SRC, int U, bool W16>
 __device__ __forceinline__ void band(const BandArgs& a, const float* sTu, const float* sLz,
                                      char* ring, int E, int ecid, const int (&cid)[CH],
                                      const int (&zc)[CH], const float (&inv)[CH], int u, int ya,
                                      int yb, int xs, int lane, float (&acc)[CH][kRollStats]) {
-  using SL_ = Slot<CH>;
+  using SL_ = Slot<CH, W16>;
   constexpr int NT = n_terms<SRC, U>();
   constexpr int TW = tu_width(SRC == kSparse);
   constexpr int G = SL_::groups;
@@ -203,7 +201,7 @@ __device__ __forceinline__ void band(const BandArgs& a, const float* sTu, const 
   const uint32_t qb = 2u * (uint32_t)qx;
   auto issue = [&](int r, char* slot) {
     const uint32_t ro = (uint32_t)(r + 1) * rowb;
-    if constexpr (PP2_BAND_DMA16) {
+    if constexpr (W16) {
 #pragma unroll
       for (int k = 0; k < CH / 2; ++k) {
         const _Float16* src = lane < 32 ? bb[2 * k] : bb[2 * k + 1];
@@ -395,7 +393,7 @@ __device__ __forceinline__ void band(const BandArgs& a, const float* sTu, const 
 // grid: nchunks x gx workgroups of 4 waves (1-D, XCD-remapped so that the
 // waves of one chunk run on one XCD and share its L2 for the band halos).
 // Wave v of a chunk walks band v / nseg of segment v % nseg.
-template <int CH, int NS, int WPS, int SRC>
+template <int CH, int NS, int WPS, int SRC, bool W16>
 __global__ __launch_bounds__(kBlock, WPS) void k_rollout_band(
     BandArgs a, const float* __restrict__ tu_all, long long tstride,
     const float* __restrict__ dl, int es, int E, int gx, int nseg, int nband,
@@ -409,9 +407,9 @@ __global__ __launch_bounds__(kBlock, WPS) void k_rollout_band(
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // the rings are their own LDS object, so the compiler's LDS-DMA tracking
   // can tell them from the dictionary tables (sTu [E][TW], sLz [CH][E])
-  __shared__ __attribute__((aligned(16))) char rings[4 * NS * Slot<CH>::bytes];
+  __shared__ __attribute__((aligned(16))) char rings[4 * NS * Slot<CH, W16>::bytes];
   extern __shared__ float rlds[];
-  char* ring = rings + w * NS * Slot<CH>::bytes;
+  char* ring = rings + w * NS * Slot<CH, W16>::bytes;
   float* sTu = rlds;
   float* sLz = sTu + ((E * TW + 3) & ~3);
   int cid[CH], zc[CH];
@@ -446,16 +444,16 @@ __global__ __launch_bounds__(kBlock, WPS) void k_rollout_band(
       switch (u) {
 #define PP2_BAND_U(UU)                                                                         \
   case UU:                                                                                     \
-    band<CH, NS, kSparse, UU>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc); \
+    band<CH, NS, kSparse, UU, W16>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc); \
     break;
         PP2_BAND_U(0) PP2_BAND_U(1) PP2_BAND_U(2) PP2_BAND_U(3) PP2_BAND_U(4)
         PP2_BAND_U(5) PP2_BAND_U(6) PP2_BAND_U(7)
         default:
-          band<CH, NS, kSparse, 8>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc);
+          band<CH, NS, kSparse, 8, W16>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc);
 #undef PP2_BAND_U
       }
     } else {
-      band<CH, NS, SRC, 0>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc);
+      band<CH, NS, SRC, 0, W16>(a, sTu, sLz, ring, E, ecid, cid, zc, inv, u, ya, yb, xs, lane, acc);
     }
   }
   // one partial per (copy, wave); repeated copies of a partial chunk write
@@ -518,27 +516,33 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
   if (nblocks <= 0) return hipSuccess;
   const int CH = rollout_chunk();
   const size_t lds = E > 0 ? (size_t)(((E * tw + 3) & ~3) + CH * E) * sizeof(float) : 0;
-#define PP2_BAND(CC, PP, WW)                                                                 \
-  do {                                                                                       \
-    static unsigned long long attr[3] = {0, 0, 0};                                           \
-    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kSparse>), attr[0]); \
-    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kFull>), attr[1]);   \
-    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kDense>), attr[2]);  \
-    if (src == kSparse)                                                                      \
-      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kSparse>), dim3((unsigned)nblocks),     \
-                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,     \
-                         nband, chunk_u, chunk_first, copies, zs, in_stats);                 \
-    else if (src == kFull)                                                                   \
-      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kFull>), dim3((unsigned)nblocks),       \
-                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,     \
-                         nband, chunk_u, chunk_first, copies, zs, in_stats);                 \
-    else                                                                                     \
-      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kDense>), dim3((unsigned)nblocks),      \
-                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,     \
-                         nband, chunk_u, chunk_first, copies, zs, in_stats);                 \
+#define PP2_BAND(CC, PP, WW, W16)                                                                 \
+  do {                                                                                            \
+    static unsigned long long attr[3] = {0, 0, 0};                                                \
+    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kSparse, W16>), attr[0]); \
+    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kFull, W16>), attr[1]);   \
+    allow_lds(reinterpret_cast<const void*>(&k_rollout_band<CC, PP, WW, kDense, W16>), attr[2]);  \
+    if (src == kSparse)                                                                           \
+      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kSparse, W16>), dim3((unsigned)nblocks),     \
+                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,          \
+                         nband, chunk_u, chunk_first, copies, zs, in_stats);                      \
+    else if (src == kFull)                                                                        \
+      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kFull, W16>), dim3((unsigned)nblocks),       \
+                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,          \
+                         nband, chunk_u, chunk_first, copies, zs, in_stats);                      \
+    else                                                                                          \
+      hipLaunchKernelGGL((k_rollout_band<CC, PP, WW, kDense, W16>), dim3((unsigned)nblocks),      \
+                         dim3(kBlock), lds, st, a, tu_all, tstride, dl, es, E, gx, nseg,          \
+                         nband, chunk_u, chunk_first, copies, zs, in_stats);                      \
   } while (0)
   const int src = E <= 0 ? kDense : sparse ? kSparse : kFull;
-  PP2_BAND(kBandCopies, kBandSlots, kBandWaves);
+  // 16-B DMA staging: 8-cell lanes must not straddle the row end, and the
+  // copy planes must be 16-B aligned (PP2_BAND_DMA16=0 forces 4-B staging)
+  const char* w16env = getenv("PP2_BAND_DMA16");
+  const bool w16 = g.wp % 8 == 0 && istride % 8 == 0 && cstride % 8 == 0 &&
+                   (reinterpret_cast<uintptr_t>(bin) & 15) == 0 && !(w16env && w16env[0] == '0');
+  if (w16) PP2_BAND(kBandCopies, kBandSlots, kBandWaves, true);
+  else PP2_BAND(kBandCopies, kBandSlots, kBandWaves, false);
 #undef PP2_BAND
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

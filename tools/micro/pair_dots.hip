@@ -600,7 +600,7 @@ __device__ __forceinline__ void t4_prologue(T4Ring<NB>& r, uint32_t pa, uint32_t
   }
 }
 
-template <int RP, int A, int CH>
+template <int RP, int A, int CH, int LAV = 4>
 __global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_t4(const float* __restrict__ Ag, int na,
                                                                 const float* __restrict__ Bg, int nb,
                                                                 int ld, int n, float* __restrict__ out,
@@ -666,7 +666,7 @@ __global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_t4(const float* __r
     }
     __syncthreads();
     if (x0 + CH < n) fetch(x0 + CH);
-    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
+    constexpr int NG = CH / 4, LA = LAV, NB = LA + 1;
     T4Ring<NB> ring;
     f2 pr[4];
     t4_prologue<0, NG, LA, NB>(ring, pa, ba);
@@ -704,11 +704,11 @@ __device__ __forceinline__ void t1_prologue(T1Ring<NB>& r, uint32_t aa, uint32_t
     t1_prologue<G + 1, NG, LA, NB>(r, aa, ba);
   }
 }
-template <int G, int NG, int LA, int NB>
+template <int G, int NG, int LA, int NB, int MODE = 0>
 __device__ __forceinline__ void t1_group(T1Ring<NB>& r, uint32_t aa, uint32_t ba, float& acc, float (&pr)[4]) {
   if constexpr (G < NG) {
-    if constexpr (G + LA < NG) t1_read<G + LA, NG, LA, NB>(r, aa, ba);
-    constexpr int left = (NG - 1 - G) < LA ? (NG - 1 - G) : LA;
+    if constexpr (G + LA < NG && MODE != 3) t1_read<G + LA, NG, LA, NB>(r, aa, ba);
+    constexpr int left = MODE == 3 ? 0 : (NG - 1 - G) < LA ? (NG - 1 - G) : LA;
     asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * left) : "memory");
     constexpr int H = G % NB;
     asm volatile("" : "+v"(r.a[H]), "+v"(r.b[H]));
@@ -729,7 +729,7 @@ __device__ __forceinline__ void t1_group(T1Ring<NB>& r, uint32_t aa, uint32_t ba
 #pragma unroll
       for (int k = 0; k < 4; ++k) add_f(acc, pr[k]);
     }
-    t1_group<G + 1, NG, LA, NB>(r, aa, ba, acc, pr);
+    t1_group<G + 1, NG, LA, NB, MODE>(r, aa, ba, acc, pr);
   }
 }
 
@@ -737,7 +737,9 @@ __device__ __forceinline__ void t1_group(T1Ring<NB>& r, uint32_t aa, uint32_t ba
 // k_pair_seq's shape (TA A rows x TB alphas per block, thread (la, jb), one
 // scalar chain) with t4's machinery: branch-free buffer-load staging, LDS
 // reads with immediate offsets LA groups ahead, XCD-grouped tiles.
-template <int TA, int TB, int CH>
+// MODE 1: no global loads after chunk 0; 3: also the LDS ring refilled only
+// once per chunk (diagnostics, wrong results)
+template <int TA, int TB, int CH, int MODE = 0, int LAV = 4>
 __global__ __launch_bounds__(TA * TB) void k_v1(const float* __restrict__ Ag, int na,
                                                const float* __restrict__ Bg, int nb, int ld, int n,
                                                float* __restrict__ out, int ldo, unsigned long long* clk) {
@@ -782,12 +784,12 @@ __global__ __launch_bounds__(TA * TB) void k_v1(const float* __restrict__ Ag, in
       if (e < NI) *(f4*)(smem + (e / C4) * ROW + (e % C4) * 4) = rg[k];
     }
     __syncthreads();
-    if (x0 + CH < n) fetch(x0 + CH);
-    constexpr int NG = CH / 4, LA = 4, NB = LA + 1;
+    if (x0 + CH < n && MODE == 0) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = LAV, NB = LA + 1;
     T1Ring<NB> ring;
     t1_prologue<0, NG, LA, NB>(ring, aa, ba);
     float pr[4];
-    t1_group<0, NG, LA, NB>(ring, aa, ba, acc, pr);
+    t1_group<0, NG, LA, NB, MODE>(ring, aa, ba, acc, pr);
     __syncthreads();
   }
   if (i0 + la < na && j0 + jb < nb) out[(long long)(i0 + la) * ldo + j0 + jb] = acc;
@@ -858,33 +860,33 @@ static void launch_t3(hipStream_t st, const float* Ag, int na, const float* Bg, 
                      st, Ag, na, Bg, nb, ld, n, out, ldo, g_clk);
 }
 
-template <int RP, int A, int CH>
+template <int RP, int A, int CH, int LAV = 4>
 static void launch_t4(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n,
                       float* out, int ldo) {
   const size_t lds = (size_t)(RP * (2 * CH + 4) + A * (CH + 4)) * sizeof(float);
   static bool once = false;
   if (!once) {
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_t4<RP, A, CH>),
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_t4<RP, A, CH, LAV>),
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     once = true;
   }
   const int tiles = cdiv(na, 2 * RP) * cdiv(nb, A);
-  hipLaunchKernelGGL((k_t4<RP, A, CH>), dim3(cdiv(tiles, 8) * 8), dim3((RP * A + 63) / 64 * 64), lds, st,
+  hipLaunchKernelGGL((k_t4<RP, A, CH, LAV>), dim3(cdiv(tiles, 8) * 8), dim3((RP * A + 63) / 64 * 64), lds, st,
                      Ag, na, Bg, nb, ld, n, out, ldo, g_clk);
 }
 
-template <int TA, int TB, int CH>
+template <int TA, int TB, int CH, int MODE = 0, int LAV = 4>
 static void launch_v1(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n,
                       float* out, int ldo) {
   const size_t lds = (size_t)(TA + TB) * (CH + 4) * sizeof(float);
   static bool once = false;
   if (!once) {
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_v1<TA, TB, CH>),
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_v1<TA, TB, CH, MODE, LAV>),
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     once = true;
   }
   const int tiles = cdiv(na, TA) * cdiv(nb, TB);
-  hipLaunchKernelGGL((k_v1<TA, TB, CH>), dim3(cdiv(tiles, 8) * 8), dim3(TA * TB), lds, st, Ag, na, Bg, nb, ld,
+  hipLaunchKernelGGL((k_v1<TA, TB, CH, MODE, LAV>), dim3(cdiv(tiles, 8) * 8), dim3(TA * TB), lds, st, Ag, na, Bg, nb, ld,
                      n, out, ldo, g_clk);
 }
 
@@ -939,12 +941,14 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&g_clk, 16));
   const Variant vs[] = {
       {"v0 k_pair_seq 16x16, 1 chain/lane", launch_v0<false>},
-      {"t4 16 rows x 32 alphas (pk pairs)", launch_t4<8, 32, 512>},
+      {"v1 16x16 LA4", launch_v1<16, 16, 512>},
+      {"v1 16x16 LA6", launch_v1<16, 16, 512, 0, 6>},
+      {"v1 16x16 LA7", launch_v1<16, 16, 512, 0, 7>},
+      {"v1 16x16 LA7 no refetch (diag)", launch_v1<16, 16, 512, 1, 7>},
+      {"v1 8x16 LA7", launch_v1<8, 16, 512, 0, 7>},
       {"t4 16 rows x 18 alphas (pk pairs)", launch_t4<8, 18, 512>},
-      {"t4 16x32 CH256", launch_t4<8, 32, 256>},
-      {"v1 16x16 (1 chain/lane, tuned)", launch_v1<16, 16, 512>},
-      {"v1 16x8 (1 chain/lane, tuned)", launch_v1<16, 8, 512>},
-      {"v1 8x16 (1 chain/lane, tuned)", launch_v1<8, 16, 512>},
+      {"t4 16x18 LA5", launch_t4<8, 18, 512, 5>},
+      {"t4 16x32 LA5", launch_t4<8, 32, 512, 5>},
   };
   const int NV = sizeof(vs) / sizeof(vs[0]);
   std::vector<float> ref((size_t)na * nb), got((size_t)na * nb);
