@@ -622,12 +622,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_fib_sweep_sparse(
 // Same values, same arithmetic: the alphas are k_fib_sweep_sparse's bit for
 // bit.  2 blocks (16 waves) per CU.
 constexpr int kFibCols = 256, kFibRows = 2, kFibLs = kFibCols + 4;
-// observations per unrolled step of the (action, observation) loop (A/B builds)
+// observations per unrolled step of the (action, observation) loop (A/B
+// builds: 1, 2, 4 and 8 within 2 %; the next observation's likelihoods read
+// ahead in registers: 3 % slower, profiles/r05/ab_fib_prefetch.txt)
 #ifndef PP2_FIB_UNROLL
 #define PP2_FIB_UNROLL 2
-#endif
-#ifndef PP2_FIB_PREFETCH
-#define PP2_FIB_PREFETCH 0
 #endif
 #define PP2_STR_(x) #x
 #define PP2_UNROLL_(n) _Pragma(PP2_STR_(unroll n))
@@ -713,29 +712,12 @@ __global__ __launch_bounds__(kFibCols * kFibRows, 4) void k_fib_sweep_lds(
       lo[j] = (sp / 3) * kFibLs + sp % 3;
     }
     float rtg = 0.0f;
-#if PP2_FIB_PREFETCH
-    // the next observation's likelihoods are read while this one's chains run
-    float lv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) lv[j] = j < kSupN[a] ? wl[lo[j]] : 0.0f;
-#endif
 PP2_UNROLL_(PP2_FIB_UNROLL)
     for (int o = 0; o < 16; ++o) {
-      float tm[4];
-#if PP2_FIB_PREFETCH
-      float lvn[4];
-      const float* wn = wl + (o + 1 < 16 ? o + 1 : o) * kFibPlane;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) lvn[j] = j < kSupN[a] ? wn[lo[j]] : 0.0f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) tm[j] = j < kSupN[a] ? ts[j] * lv[j] : 0.0f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) lv[j] = lvn[j];
-#else
       const float* wo = wl + o * kFibPlane;
+      float tm[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) tm[j] = j < kSupN[a] ? ts[j] * wo[lo[j]] : 0.0f;
-#endif
       f2v sq[4] = {f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}, f2v{0.0f, 0.0f}};
       float sq8 = 0.0f;
 #pragma unroll
