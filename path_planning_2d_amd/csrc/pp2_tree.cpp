@@ -215,6 +215,7 @@ struct pp2_planner {
   unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
   hipStream_t side = nullptr;   // reward chains beside the child chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_kids = nullptr;
+  hipEvent_t ev_kept = nullptr;  // the kept children's rows are stored (main -> side)
   float* d_rsum = nullptr;      // [256] row sums
   float* h_rout = nullptr;      // pinned: [9 rewards | 256 x 9 FIB dots]
   float* d_rout = nullptr;
@@ -433,8 +434,9 @@ int ref_frows(pp2_planner* p) {
 // kcount), of the listed rows only (the kept children of an expansion; the
 // other rows' h_lbv are stale).  Asynchronous.
 int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows, const int* klist = nullptr,
-                    const int* kcount = nullptr) {
+                    const int* kcount = nullptr, hipStream_t st = nullptr) {
   pp2_ctx* c = p->ctx;
+  if (!st) st = c->stream;
   const float* al = nullptr;
   int S = 0, Sp = 0, ald = 0;
   CHECK(pbvi_alphas(c, &al, &S, &Sp, &ald));
@@ -445,17 +447,17 @@ int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows, const int* kl
     // holds Mp rows), then the alphas whose chain can reach each row's
     // maximum (pp2_fchain.hip k_pbvi_cands), then their exact chains
     if (p->astats_version != c->pbvi_version) {
-      HIPCHK(pp2::launch_alpha_stats(c->stream, al, S, (int)p->n, p->ref_ld, p->d_amax,
+      HIPCHK(pp2::launch_alpha_stats(st, al, S, (int)p->n, p->ref_ld, p->d_amax,
                                      p->d_aflag));
       p->astats_version = c->pbvi_version;
     }
     const int Mp = (rows + pp2::kGemmTile - 1) / pp2::kGemmTile * pp2::kGemmTile;
     const long long sstride = (long long)Mp * Sp;
-    HIPCHK(pp2::launch_gemm_nt(c->stream, d_rows, al, p->d_lbpart, Mp, Sp, p->ref_ld, 1, 0, 0,
+    HIPCHK(pp2::launch_gemm_nt(st, d_rows, al, p->d_lbpart, Mp, Sp, p->ref_ld, 1, 0, 0,
                                p->lb_split, sstride));
-    HIPCHK(pp2::launch_sum_splits(c->stream, p->d_lbpart, p->lb_split, sstride, (int)sstride,
+    HIPCHK(pp2::launch_sum_splits(st, p->d_lbpart, p->lb_split, sstride, (int)sstride,
                                   p->d_lbapprox));
-    HIPCHK(hipMemsetAsync(p->d_pcount, 0, sizeof(int), c->stream));
+    HIPCHK(hipMemsetAsync(p->d_pcount, 0, sizeof(int), st));
     pp2::PbviCandArgs ca;
     ca.rows = d_rows;
     ca.row_stride = p->ref_ld;
@@ -476,7 +478,7 @@ int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows, const int* kl
     ca.lde = S;
     ca.plist = p->d_plist;
     ca.pcount = p->d_pcount;
-    HIPCHK(pp2::launch_pbvi_cands(c->stream, ca));
+    HIPCHK(pp2::launch_pbvi_cands(st, ca));
     pp2::FcArgs a;
     a.n = (int)p->n;
     a.ld = p->ref_ld;
@@ -488,18 +490,18 @@ int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows, const int* kl
     a.out = p->d_lbdots;
     a.ldo = S;
     p->scr_pbvi.attach(&a);
-    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_LIST, 0, rows * S, a));
+    HIPCHK(pp2::launch_fchain(st, pp2::FC_LIST, 0, rows * S, a));
     if (p->h_pstat) {
       HIPCHK(hipMemcpyAsync(p->h_pstat, p->d_pcount, sizeof(int), hipMemcpyDeviceToHost,
-                            c->stream));
+                            st));
       ++p->stat_sets;
     }
   } else {
     // one sequential chain per lane (grids whose chain-set scratch is too big)
-    HIPCHK(pp2::launch_pair_chain(c->stream, pp2::PAIR_DOT, d_rows, rows, al, S, p->ref_ld,
+    HIPCHK(pp2::launch_pair_chain(st, pp2::PAIR_DOT, d_rows, rows, al, S, p->ref_ld,
                                   (int)p->n, p->d_lbdots, S, klist, kcount));
   }
-  HIPCHK(pp2::launch_argmax_rows(c->stream, p->d_lbdots, rows, S, S, p->d_lbidx, p->d_lbv));
+  HIPCHK(pp2::launch_argmax_rows(st, p->d_lbdots, rows, S, S, p->d_lbidx, p->d_lbv));
   return PP2_OK;
 }
 
@@ -833,6 +835,13 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   // masses (side) into their rows of d_children -- only they become nodes
   HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
                                 p->d_csum, p->d_children, (int)n, ld));
+  // side: the kept children's PBVI dots (evaluatePbviCpu, the long chains),
+  // beside main's FIB dots, after the rewards already queued there
+  if (p->pbvi) {
+    HIPCHK(hipEventRecord(p->ev_kept, c->stream));
+    HIPCHK(hipStreamWaitEvent(p->side, p->ev_kept, 0));
+    CHECK(ref_pbvi_bounds(p, p->d_children, 144, p->d_klist, p->d_kcount, p->side));
+  }
   if (p->seq) {  // main: the kept children's FIB dots (evaluateFibCpu), sequential chains
     HIPCHK(pp2::launch_pair_seq_small(c->stream, pp2::PAIR_DOT, p->d_children, 144, p->d_frows, 9,
                                       ld, (int)n, p->d_rout + 9, 9, p->d_klist, p->d_kcount));
@@ -850,9 +859,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     p->scr_main.attach(&a);
     HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 144, a));
   }
-  // the kept children's PBVI dots (evaluatePbviCpu), from the device list
-  if (p->pbvi) CHECK(ref_pbvi_bounds(p, p->d_children, 144, p->d_klist, p->d_kcount));
-  HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards)
+  HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards, the PBVI dots)
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
   HIPCHK(hipEventSynchronize(p->ev_done));
@@ -1066,6 +1073,7 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_kids, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_kept, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "planner scratch allocation failed"));
   p->ref = prm->reference_order == 1;
@@ -1235,7 +1243,7 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (p->h_belief) (void)hipHostFree(p->h_belief);
   if (p->ev_belief) (void)hipEventDestroy(p->ev_belief);
   if (p->ev_done) (void)hipEventDestroy(p->ev_done);
-  for (hipEvent_t e : {p->ev_fork, p->ev_join, p->ev_kids})
+  for (hipEvent_t e : {p->ev_fork, p->ev_join, p->ev_kids, p->ev_kept})
     if (e) (void)hipEventDestroy(e);
   if (p->side) {
     (void)hipStreamSynchronize(p->side);
