@@ -18,6 +18,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <limits.h>
 #include <stdlib.h>
 
@@ -540,7 +541,7 @@ __global__ __launch_bounds__(TA * TB) void k_pair_seq(const float* __restrict__ 
 //                  pair is staged interleaved, so one ds_read_b128 returns
 //                  two cells of both rows already paired;
 //   k_pair_dot_1   one chain per lane (k_pair_seq's thread layout).
-// PP2_PAIR_DOT selects: 1 packed, 2 one chain per lane, 0 k_pair_seq.
+// PP2_PAIR_DOT selects: 1 packed, 2 one chain per lane (default), 0 k_pair_seq.
 constexpr int kDotOff = 0x7ffffff0;  // buffer offset past any range: the load reads +0.0
 __device__ __forceinline__ f4 ldq_rs(__amdgpu_buffer_rsrc_t rs, int off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -855,6 +856,142 @@ __global__ __launch_bounds__(64) void k_row_cdf_seq(const float* __restrict__ ro
   if (lane == 0) *sum = acc;
 }
 
+// ---------------------------------------------------------------- small-grid chains
+// A chain of a small grid (n <= kWalkMax cells) is bound by its own
+// dependent adds, not by the chip: one wave per chain forms all n terms
+// in parallel (each lane its cells' IEEE products, the reference's) into
+// LDS, then lane 0 alone walks them -- 32-term blocks read 8 float4 ahead of
+// their adds -- so a term costs about one dependent v_add_f32.  (A lane per
+// chain instead pays the LDS delivery of both operands per term, ~20 cycles,
+// tools/micro/pair_dots.hip; the exact parallel chain sets need three
+// launches.)  Chains (i, j), i < na (or the first *acount entries of alist),
+// j < nb: grid na x nb one-wave blocks.  CDF: one chain of A's row 0, every
+// running sum to cdf, the total to out[0].
+constexpr int kWalkMax = 8192;
+constexpr int kWalkLA = 6, kWalkNB = 8;
+// floats of LDS the terms take: n rounded up to whole walk iterations, plus
+// the kWalkLA groups read ahead of the last one
+__host__ __device__ constexpr int walk_cap(int n) {
+  return ((n + 4 * kWalkNB - 1) / (4 * kWalkNB)) * 4 * kWalkNB + 4 * kWalkLA;
+}
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for_h(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for_h<B + 1, E>(f);
+  }
+}
+enum { WALK_DOT = 0, WALK_CHILD = 1, WALK_CDF = 2 };
+
+template <int K, int LA, int NB>
+__device__ __forceinline__ void walk_prologue(f4 (&ring)[NB], uint32_t base) {
+  if constexpr (K < LA) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ring[K]) : "v"(base), "n"(16 * K));
+    walk_prologue<K + 1, LA, NB>(ring, base);
+  }
+}
+// group K of an iteration: read group K + LA ahead, wait for group K, its
+// four dependent adds (and, for a cdf, its four running sums to LDS)
+template <int K, int LA, int NB, int W, bool CDF>
+__device__ __forceinline__ void walk_groups(f4 (&ring)[NB], uint32_t ad, uint32_t od, float& acc) {
+  if constexpr (K < NB) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2"
+                 : "=v"(ring[(K + LA) % NB]) : "v"(ad), "n"(16 * (K + LA)));
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(W) : "memory");
+    asm volatile("" : "+v"(ring[K]));
+    const f4 v = ring[K];
+    f4 r;
+    acc = acc + v.x;
+    r.x = acc;
+    acc = acc + v.y;
+    r.y = acc;
+    acc = acc + v.z;
+    r.z = acc;
+    acc = acc + v.w;
+    r.w = acc;
+    if constexpr (CDF)
+      asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(od), "v"(r), "n"(16 * K) : "memory");
+    walk_groups<K + 1, LA, NB, W, CDF>(ring, ad, od, acc);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_chain_walk(const float* __restrict__ A, int na,
+                                                  const float* __restrict__ B, int nb, int ld,
+                                                  int n, float* __restrict__ out, int ldo,
+                                                  const int* __restrict__ alist,
+                                                  const int* __restrict__ acount,
+                                                  float* __restrict__ cdf) {
+  extern __shared__ __attribute__((aligned(16))) float sT[];  // n terms (+ n running sums)
+  const int lane = threadIdx.x;
+  const int i = blockIdx.x / nb, j = blockIdx.x % nb;
+  if (alist && i >= *acount) return;  // (uniform)
+  const int row = alist ? alist[i] : i;
+  const float* __restrict__ a = A + (long long)row * ld;
+  const float* __restrict__ b = MODE == WALK_CDF ? nullptr : B + (long long)j * ld;
+  const int n4 = (n + 3) & ~3;
+  const int tcap = walk_cap(n);  // terms + zero padding the walk reads past the end
+  // the terms, 4 cells per lane per step, the loads of 8 steps in flight
+  // together (cells past n are +0: they leave the chain unchanged -- it
+  // starts at +0 and so is never -0)
+  constexpr int KB = 8;
+  for (int x0 = 4 * lane; x0 < tcap; x0 += 256 * KB) {
+    f4 va[KB], vb[KB];
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+      const int x = x0 + 256 * q;
+      va[q] = vb[q] = f4{0, 0, 0, 0};
+      if (x + 3 < n) {
+        va[q] = *(const f4*)(a + x);
+        if (MODE != WALK_CDF) vb[q] = *(const f4*)(b + x);
+      } else if (x < n) {
+        for (int k = 0; k < 4; ++k)
+          if (x + k < n) {
+            va[q][k] = a[x + k];
+            if (MODE != WALK_CDF) vb[q][k] = b[x + k];
+          }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+      const int x = x0 + 256 * q;
+      if (x >= tcap) break;
+      f4 t;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (MODE == WALK_DOT) t[k] = va[q][k] * vb[q][k];
+        else if (MODE == WALK_CHILD) t[k] = ftz_f(vb[q][k] * ftz_f(va[q][k]));  // (a: L row, b: prediction)
+        else t[k] = va[q][k];
+      }
+      *(f4*)(sT + x) = t;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    // lane 0 walks: group = 4 terms, read kWalkLA groups ahead at immediate
+    // offsets with counted waits, kWalkNB groups per iteration (the padding
+    // keeps every read in bounds and adds +0 past the end); in order, the
+    // CDF's LDS writes count in lgkmcnt too
+    constexpr int LA = kWalkLA, NB = kWalkNB, W = (MODE == WALK_CDF ? 2 : 1) * LA;
+    const int ng = n4 / 4;
+    const uint32_t base = (uint32_t)(uintptr_t)sT;
+    const uint32_t obase = base + 4u * (uint32_t)tcap;
+    f4 ring[NB];
+    walk_prologue<0, LA, NB>(ring, base);
+    float acc = 0.0f;
+    for (int g0 = 0; g0 < ng; g0 += NB) {
+      const uint32_t ad = base + 16u * (uint32_t)g0, od = obase + 16u * (uint32_t)g0;
+      walk_groups<0, LA, NB, W, MODE == WALK_CDF>(ring, ad, od, acc);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    out[(long long)row * ldo + j] = acc;
+  }
+  if (MODE == WALK_CDF) {
+    __syncthreads();
+    for (int x = lane; x < n; x += 64) cdf[x] = sT[walk_cap(n) + x];
+  }
+}
+
 // ---------------------------------------------------------------- sampling
 // find_if(partial_sum >= r) over `cnt` values at stride `stride`; when the
 // sum never reaches r, the last index at which it grew (the reference would
@@ -1064,11 +1201,18 @@ __global__ __launch_bounds__(256) void k_argmax_rows(const float* __restrict__ C
   const float* __restrict__ p = C + (long long)row * ldc;
   float bv = -INFINITY;
   int bi = INT_MAX;
-  for (int k = lane; k < n; k += 64) {
-    const float v = p[k];
-    if (bi == INT_MAX || v > bv) {
-      bv = v;
-      bi = k;
+  // 8 loads per lane in flight together (a row of S <= 512 alphas in one go)
+  for (int k0 = lane; k0 < n; k0 += 512) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = k0 + 64 * q < n ? p[k0 + 64 * q] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = k0 + 64 * q;
+      if (k < n && (bi == INT_MAX || v[q] > bv)) {
+        bv = v[q];
+        bi = k;
+      }
     }
   }
 #pragma unroll
@@ -1188,13 +1332,15 @@ hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float
   return hipGetLastError();
 }
 
-// The planner's PBVI leaf dots: the packed two-chain shape by default
-// (PP2_PAIR_DOT: 1 packed, 2 one chain per lane, 0 k_pair_seq).
+// The planner's PBVI leaf dots: one chain per lane (k_pair_dot_1) by
+// default -- beside the FIB dots on the other stream it is 0-10 % faster than
+// the packed shape in the plan step (profiles/r05/pbvi_plan_dots_*.txt);
+// PP2_PAIR_DOT: 1 packed, 2 one chain per lane, 0 k_pair_seq.
 static hipError_t launch_pair_dot(hipStream_t st, const float* A, int na, const float* B, int nb,
                                   int ld, int n, float* out, int ldo, const int* alist,
                                   const int* acount) {
   const char* env = getenv("PP2_PAIR_DOT");
-  const int mode = env && *env ? atoi(env) : 1;
+  const int mode = env && *env ? atoi(env) : 2;
   // 32-bit buffer offsets: the rows (alist entries index the na rows of A)
   // and a tile's alphas
   const bool fits = (long long)na * ld < (long long)kDotOff / 4 && 18LL * ld < (long long)kDotOff / 4;
@@ -1263,16 +1409,39 @@ hipError_t launch_pair_seq_small(hipStream_t st, int op, const float* A, int na,
                                  const int* acount) {
   if (na <= 0 || nb <= 0) return hipSuccess;
   if ((alist == nullptr) != (acount == nullptr) || n <= 0 || ld < n) return hipErrorInvalidValue;
+  if (op != PAIR_DOT && op != PAIR_CHILD) return hipErrorInvalidValue;
+  const char* env = getenv("PP2_CHAIN_WALK");
+  if (n <= kWalkMax && !(env && env[0] == '0')) {
+    // one wave per chain, lane 0 walking the chain's terms from LDS
+    const size_t lds = (size_t)walk_cap(n) * sizeof(float);
+    static unsigned long long attr[2] = {0ull, 0ull};
+    allow_lds(reinterpret_cast<const void*>(&k_chain_walk<WALK_DOT>), attr[0]);
+    allow_lds(reinterpret_cast<const void*>(&k_chain_walk<WALK_CHILD>), attr[1]);
+    if (op == PAIR_DOT)
+      hipLaunchKernelGGL(k_chain_walk<WALK_DOT>, dim3(na * nb), dim3(64), lds, st, A, na, B, nb, ld,
+                         n, out, ldo, alist, acount, nullptr);
+    else
+      hipLaunchKernelGGL(k_chain_walk<WALK_CHILD>, dim3(na * nb), dim3(64), lds, st, A, na, B, nb,
+                         ld, n, out, ldo, alist, acount, nullptr);
+    return hipGetLastError();
+  }
   // one wave per block (4 A rows x 16 B rows): few chains, each block on a CU of its own
   if (op == PAIR_DOT)
     return launch_pair_seq<PAIR_DOT, 4, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
-  if (op == PAIR_CHILD)
-    return launch_pair_seq<PAIR_CHILD, 4, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
-  return hipErrorInvalidValue;
+  return launch_pair_seq<PAIR_CHILD, 4, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
 }
 
 hipError_t launch_row_cdf_seq(hipStream_t st, const float* row, int n, float* cdf, float* sum) {
   if (n <= 0 || !row || !cdf || !sum) return hipErrorInvalidValue;
+  const char* env = getenv("PP2_CHAIN_WALK");
+  if (n <= kWalkMax && !(env && env[0] == '0')) {
+    const size_t lds = 2 * (size_t)walk_cap(n) * sizeof(float);
+    static unsigned long long attr = 0ull;
+    allow_lds(reinterpret_cast<const void*>(&k_chain_walk<WALK_CDF>), attr);
+    hipLaunchKernelGGL(k_chain_walk<WALK_CDF>, dim3(1), dim3(64), lds, st, row, 1, nullptr, 1, n,
+                       n, sum, 0, nullptr, nullptr, cdf);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_row_cdf_seq, dim3(1), dim3(64), 0, st, row, n, cdf, sum);
   return hipGetLastError();
 }

@@ -92,6 +92,9 @@ struct Slot {
 };
 
 constexpr int kStatsPerChild = 10;
+// grids up to this many cells run the reference-order sums as walked chains
+// (k_chain_walk; its LDS holds n terms, pp2_pbvi_host.hip kWalkMax)
+constexpr long long kSeqChainMax = 8192;
 constexpr int kStatsFloats = 16 * 9 * kStatsPerChild;
 
 // The x-ordered fp32 prefix sum of a belief: the cdf the QNode constructor
@@ -179,11 +182,12 @@ struct pp2_planner {
   // the reference's x-ordered fp32 chain (pp2_fchain.hip; the PBVI leaf dots
   // k_pair_chain).
   bool ref = false;
-  // opt-in (grids of n <= PP2_SEQ_CHAIN_MAX cells; default 0 = off): the
-  // sums as sequential chains, one per lane (launch_pair_seq_small,
-  // k_row_cdf_seq).  Measured slower than the exact parallel chain sets
-  // even at 100 x 40 (node plan step 4.22 vs 3.89 ms): a lane's dependent
-  // add costs ~12 ns per element there (profiles/r05/pbvi_plan_modes_ab.txt)
+  // grids of n <= PP2_SEQ_CHAIN_MAX cells (default kSeqChainMax; 0 = off):
+  // the sums as sequential chains, one wave per chain whose lanes form the
+  // terms into LDS and whose lane 0 walks them (launch_pair_seq_small,
+  // launch_row_cdf_seq: k_chain_walk), one launch per chain set instead of
+  // the exact parallel chain sets' three.  The reference node's 100 x 40
+  // plan step: p50 2.54 vs 3.34-3.51 ms (profiles/r05/chain_walk_ab.txt).
   bool seq = false;
   int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
   float* d_rrows = nullptr;     // [9][ld] R[.][a]
@@ -1079,7 +1083,7 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   p->ref = prm->reference_order == 1;
   {
     const char* e = getenv("PP2_SEQ_CHAIN_MAX");
-    const long long lim = e ? atoll(e) : 0;
+    const long long lim = e && *e ? atoll(e) : kSeqChainMax;
     p->seq = p->ref && (long long)p->n <= lim;
   }
   // dense rows of the children / PBVI / reference-order passes: the PBVI

@@ -230,10 +230,11 @@ def compare_exact(gi, oi, where):
     ("sparse_map_100x40", 50, 0, 0, 6, None),
     ("sparse_map_100x40", 5, 1, 500, 5, None),    # the reference node: PBVI leaves, S = 500
     ("tile64_sparse_map_100x40", 8, 1, 64, 6, None),
-    # the same small grids on the opt-in sequential lane chains instead of
-    # the exact parallel chain sets (pp2_fchain.hip)
-    ("sparse_map_100x40", 50, 0, 0, 6, "8192"),
-    ("sparse_map_100x40", 5, 1, 500, 3, "8192"),
+    # the same small grids on the exact parallel chain sets (pp2_fchain.hip)
+    # instead of the walked chains (k_chain_walk, the default up to 8192 cells)
+    ("sparse_map_100x40", 50, 0, 0, 6, "0"),
+    ("sparse_map_100x40", 5, 1, 500, 3, "0"),
+    ("tile64_sparse_map_100x40", 8, 1, 64, 4, "0"),
 ])
 def test_planner_reference_order_bit_exact(oracle, monkeypatch, name, max_depth, lb, S, steps,
                                            seq_max):
@@ -244,8 +245,9 @@ def test_planner_reference_order_bit_exact(oracle, monkeypatch, name, max_depth,
     shape, observations, weights, bounds, rewards, heuristics bit for bit, and
     the chosen action and its value exactly -- deep trees included, where the
     fp64-accumulating mode may legitimately pick another near-tied node.
-    The sums run as exact parallel chain sets; with PP2_SEQ_CHAIN_MAX (seq_max)
-    grids up to that many cells run them as sequential lane chains."""
+    Grids up to PP2_SEQ_CHAIN_MAX cells (seq_max; default 8192) run the sums
+    as walked chains, larger ones as exact parallel chain sets; seq_max "0"
+    forces the latter on the small grids."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S_
     if seq_max is not None:

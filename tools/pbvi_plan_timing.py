@@ -1,6 +1,6 @@
 """The bench's PBVI-leaf plan steps alone, reference order, with the PBVI
-leaf dots as packed two-chain lanes (k_pair_dot_pk, PP2_PAIR_DOT=1, the
-default), one chain per lane (k_pair_dot_1, =2), the round-5 lookahead
+leaf dots as packed two-chain lanes (k_pair_dot_pk, PP2_PAIR_DOT=1), one
+chain per lane (k_pair_dot_1, =2, the default), the round-5 lookahead
 k_pair_seq (=0) and, with PP2_AB_FC=1, FC_LIST candidate chain sets
 (PP2_PBVI_FCHAIN=1), alternated on one box:
   * 256^2 synthetic, S = 500 alphas, depth 3 (bench plan_step_pbvi_lb);
@@ -49,7 +49,7 @@ def main():
                     ms, acts, vals = S.closed_loop(grid, b0, pl.step, steps)
                 res.setdefault(mode, []).append((float(np.percentile(ms, 50)), acts, vals))
         ctx.close()
-        names = {"pk": "k_pair_dot_pk (default)", "one": "k_pair_dot_1 (PP2_PAIR_DOT=2)",
+        names = {"pk": "k_pair_dot_pk (PP2_PAIR_DOT=1)", "one": "k_pair_dot_1 (default)",
                  "seq": "k_pair_seq (PP2_PAIR_DOT=0)",
                  "fc": "FC_LIST candidate chain sets (PP2_PBVI_FCHAIN=1)"}
         for mode, _, _ in modes:
