@@ -231,6 +231,24 @@ class GridContext:
             raise ValueError("us and zs must have the same length")
         call("pp2_loop_run", self._h, int(us.size), us.tobytes(), zs.tobytes())
 
+    def loop_launcher(self, us, zs):
+        """A zero-argument callable that runs pp2_loop_run on this trajectory:
+        the arguments are converted once, here, so a timed call pays only the
+        C-ABI call itself (what a compiled client pays)."""
+        us = np.ascontiguousarray(us, np.uint8)
+        zs = np.ascontiguousarray(zs, np.uint8)
+        if us.shape != zs.shape:
+            raise ValueError("us and zs must have the same length")
+        lib = _lib.load()
+        fn, h, n, ub, zb = lib.pp2_loop_run, self._h, int(us.size), us.tobytes(), zs.tobytes()
+
+        def run():
+            st = fn(h, n, ub, zb)
+            if st != _lib.PP2_OK:
+                msg = lib.pp2_last_error()
+                raise _lib.Pp2Error(st, "pp2_loop_run", msg.decode() if msg else "")
+        return run
+
     # ------------------------------------------------------------ FIB
     def fib_reset(self):
         call("pp2_fib_reset", self._h)
