@@ -17,6 +17,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <set>
 #include <vector>
@@ -95,6 +96,7 @@ constexpr int kStatsPerChild = 10;
 // grids up to this many cells run the reference-order sums as walked chains
 // (k_chain_walk; its LDS holds n terms, pp2_pbvi_host.hip kWalkMax)
 constexpr long long kSeqChainMax = 8192;
+
 constexpr int kStatsFloats = 16 * 9 * kStatsPerChild;
 
 // The x-ordered fp32 prefix sum of a belief: the cdf the QNode constructor
@@ -216,6 +218,13 @@ struct pp2_planner {
   int* d_pcount = nullptr;
   int* h_pstat = nullptr;       // pinned: candidates of the last set (PP2_PBVI_STATS)
   long long stat_cands = 0, stat_rows = 0, stat_sets = 0;
+  // PP2_PLAN_TIMING=1: host time per expansion (us): enqueue (first launch ..
+  // the wait), the tree work after the wait .. store_children enqueued, and
+  // the time from there to the next expansion's first launch
+  bool timing = false;
+  double t_enq = 0, t_post = 0, t_between = 0;
+  long long t_n = 0;
+  std::chrono::steady_clock::time_point t_last_store{};
   unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
   hipStream_t side = nullptr;   // reward chains beside the child chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_kids = nullptr;
@@ -758,6 +767,10 @@ int expand_vnode(pp2_planner* p, VNode* v) {
 int expand_vnode_ref(pp2_planner* p, VNode* v) {
   pp2_ctx* c = p->ctx;
   if (v->slot < 0) return set_err(PP2_ESTATE, "reference-order VNode without a belief row");
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t_begin = p->timing ? clk::now() : clk::time_point{};
+  if (p->timing && p->t_n > 0)
+    p->t_between += std::chrono::duration<double, std::micro>(t_begin - p->t_last_store).count();
   const float* brow = p->slots[v->slot].row;
   const size_t n = p->n;
   const int ld = p->ref_ld;
@@ -866,7 +879,9 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards, the PBVI dots)
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
+  const clk::time_point t_enq = p->timing ? clk::now() : clk::time_point{};
   HIPCHK(hipEventSynchronize(p->ev_done));
+  const clk::time_point t_ret = p->timing ? clk::now() : clk::time_point{};
   if (p->h_pstat) p->stat_cands += *p->h_pstat;
 
   for (QNode* q : v->children)
@@ -900,6 +915,12 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   p->stat_rows += (long long)keep.size();
   vnode_update(v);
   ++p->expansions;
+  if (p->timing) {
+    p->t_last_store = clk::now();
+    p->t_enq += std::chrono::duration<double, std::micro>(t_enq - t_begin).count();
+    p->t_post += std::chrono::duration<double, std::micro>(p->t_last_store - t_ret).count();
+    ++p->t_n;
+  }
   return PP2_OK;
 }
 
@@ -1199,6 +1220,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       }
     }
   }
+  {
+    const char* tm = getenv("PP2_PLAN_TIMING");
+    p->timing = tm && tm[0] == '1';
+  }
   *out = p;
   return PP2_OK;
 }
@@ -1227,6 +1252,10 @@ int pp2_planner_destroy(pp2_planner* p) {
     if (d) (void)hipFree(d);
   for (void* d : {(void*)p->d_aflag, (void*)p->d_plist, (void*)p->d_pcount})
     if (d) (void)hipFree(d);
+  if (p->timing && p->t_n > 0)
+    fprintf(stderr, "pp2 planner: %lld expansions, host us per expansion: enqueue %.1f, "
+            "after the wait .. children stored %.1f, .. next expansion %.1f\n", p->t_n,
+            p->t_enq / p->t_n, p->t_post / p->t_n, p->t_between / (p->t_n > 1 ? p->t_n - 1 : 1));
   if (p->h_pstat) {
     if (p->stat_sets > 0)
       fprintf(stderr, "pp2 planner: PBVI candidate chains %lld over %lld rows in %lld sets "
