@@ -541,7 +541,8 @@ __global__ __launch_bounds__(TA * TB) void k_pair_seq(const float* __restrict__ 
 //                  pair is staged interleaved, so one ds_read_b128 returns
 //                  two cells of both rows already paired;
 //   k_pair_dot_1   one chain per lane (k_pair_seq's thread layout).
-// PP2_PAIR_DOT selects: 1 packed, 2 one chain per lane (default), 0 k_pair_seq.
+// PP2_PAIR_DOT selects: 1 packed, 2 one chain per lane, 0 k_pair_seq (3, the
+// default: k_pair_dot_bq in pp2_pbvi_dots.hip).
 constexpr int kDotOff = 0x7ffffff0;  // buffer offset past any range: the load reads +0.0
 __device__ __forceinline__ f4 ldq_rs(__amdgpu_buffer_rsrc_t rs, int off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -1332,20 +1333,22 @@ hipError_t launch_rows_dot(hipStream_t st, const float* A, int amod, const float
   return hipGetLastError();
 }
 
-// The planner's PBVI leaf dots: one chain per lane (k_pair_dot_1) by
-// default -- beside the FIB dots on the other stream it is 0-10 % faster than
-// the packed shape in the plan step (profiles/r05/pbvi_plan_dots_*.txt);
-// PP2_PAIR_DOT: 1 packed, 2 one chain per lane, 0 k_pair_seq.
+// The planner's PBVI leaf dots: one chain per lane with the child rows
+// through DPP broadcasts (k_pair_dot_bq, pp2_pbvi_dots.hip) by default;
+// PP2_PAIR_DOT: 3 that, 2 one chain per lane from LDS (k_pair_dot_1; beside
+// the FIB dots 0-10 % faster than the packed shape,
+// profiles/r05/pbvi_plan_dots_*.txt), 1 packed, 0 k_pair_seq.
 static hipError_t launch_pair_dot(hipStream_t st, const float* A, int na, const float* B, int nb,
                                   int ld, int n, float* out, int ldo, const int* alist,
                                   const int* acount) {
   const char* env = getenv("PP2_PAIR_DOT");
-  const int mode = env && *env ? atoi(env) : 2;
+  const int mode = env && *env ? atoi(env) : 3;
   // 32-bit buffer offsets: the rows (alist entries index the na rows of A)
   // and a tile's alphas
   const bool fits = (long long)na * ld < (long long)kDotOff / 4 && 18LL * ld < (long long)kDotOff / 4;
   if (mode == 0 || !fits)
     return launch_pair_seq<PAIR_DOT, 16, 16>(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
+  if (mode == 3) return launch_pair_dot_bq(st, A, na, B, nb, ld, n, out, ldo, alist, acount);
   if (mode == 2) {
     constexpr int TA = 16, TB = 16, CH = 512;
     static unsigned long long attr = 0ull;

@@ -69,6 +69,11 @@ hipError_t launch_pair_chain(hipStream_t st, int op, const float* A, int na, con
 hipError_t launch_pair_seq_small(hipStream_t st, int op, const float* A, int na, const float* B,
                                  int nb, int ld, int n, float* out, int ldo,
                                  const int* alist = nullptr, const int* acount = nullptr);
+// The planner's PBVI leaf dots (PAIR_DOT, n >= 1024) with the child rows
+// handed to the products by DPP broadcasts (pp2_pbvi_dots.hip); the same
+// arguments and results as launch_pair_chain.  Needs na * ld < 2^29.
+hipError_t launch_pair_dot_bq(hipStream_t st, const float* A, int na, const float* B, int nb, int ld, int n,
+                              float* out, int ldo, const int* alist, const int* acount);
 // cdf[x] = the running sums of row[0 .. n), *sum = the last (std::partial_sum)
 hipError_t launch_row_cdf_seq(hipStream_t st, const float* row, int n, float* cdf, float* sum);
 // The three draws of generateBeliefSet per (belief i, action a): state from

@@ -125,10 +125,11 @@ def test_evaluate_batch_matches_oracle(pp2, oracle):
         assert np.float32(vo) == v[i] and ao == a[i], i
 
 
-@pytest.mark.parametrize("mode", ["1", "2", "0"])
+@pytest.mark.parametrize("mode", ["3", "1", "2", "0"])
 def test_evaluate_dot_shapes_bit_exact(pp2, oracle, monkeypatch, mode):
-    """The leaf-dot kernels (PP2_PAIR_DOT 1: packed two-chain lanes, 2: one
-    chain per lane, 0: k_pair_seq) against evaluatePbviCpu's x-ordered chain
+    """The leaf-dot kernels (PP2_PAIR_DOT 3: one chain per lane, rows by DPP
+    broadcast; 1: packed two-chain lanes; 2: one chain per lane from LDS; 0:
+    k_pair_seq) against evaluatePbviCpu's x-ordered chain
     on adversarial rows: an odd number of beliefs (a packed pair with no
     partner row), zeros, subnormal and huge terms, mixed-sign alphas, a
     ragged S."""

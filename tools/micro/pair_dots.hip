@@ -9,7 +9,7 @@
 // the same IEEE products and sums as the scalar ops).  Every variant's
 // results are compared bit for bit with the first one, and a sample of
 // chains with the host's sequential fp32 loop.
-//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/micro/pair_dots tools/micro/pair_dots.hip
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form=1 -o tools/micro/pair_dots tools/micro/pair_dots.hip
 //   tools/micro/pair_dots [na nb n]     (default 144 500 65536: 256^2, S = 500)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -799,6 +799,395 @@ __global__ __launch_bounds__(TA * TB) void k_v1(const float* __restrict__ Ag, in
   }
 }
 
+// ---------------------------------------------------------------- bc: the row through DPP broadcasts
+// Block = W waves x 64 alphas; wave w owns rows i0 + RR w + r, the same for
+// every lane.  Lane l holds A[i][x0 + 16 q + (l & 15)] (one VGPR per 16 cells
+// and row, loaded a chunk ahead), and v_mul_f32_dpp row_newbcast:k hands cell
+// 16 q + k to every lane of each 16-lane row inside the product: the row
+// costs neither an LDS read nor an extra VALU op.  Lane l's alpha j0 + l comes
+// from the block's LDS tile, one ds_read_b128 per 4 cells, LA groups ahead.
+// (Needs -fno-slp-vectorize: paired into v_pk_mul_f32, the products keep
+// the broadcasts as separate v_mov_b32_dpp.)
+template <int K>
+__device__ __forceinline__ float bcast16(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + K, 0xf,
+                                                               0xf, true));
+}
+template <int NB>
+struct BcRing {
+  f4 b[NB];
+};
+template <int G, int NB>
+__device__ __forceinline__ void bc_read(BcRing<NB>& r, uint32_t ba) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.b[G % NB]) : "v"(ba), "n"(16 * G));
+}
+template <int G, int LA, int NB>
+__device__ __forceinline__ void bc_prologue(BcRing<NB>& r, uint32_t ba) {
+  if constexpr (G < LA) {
+    bc_read<G, NB>(r, ba);
+    bc_prologue<G + 1, LA, NB>(r, ba);
+  }
+}
+// wait for group G (issued so far: up to min(G - 1 + LA, NG - 1)), its products
+template <int G, int NG, int LA, int NB, int RR, int NQ>
+__device__ __forceinline__ void bc_products(BcRing<NB>& r, const float (&av)[RR][NQ], float (&p)[RR][4]) {
+  constexpr int left = (NG - 1 - G) < (LA - 1) ? (NG - 1 - G) : (LA - 1);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(left) : "memory");
+  asm volatile("" : "+v"(r.b[G % NB]));
+  const f4 b = r.b[G % NB];
+  constexpr int q = G / 4, k0 = (G % 4) * 4;
+#pragma unroll
+  for (int i = 0; i < RR; ++i) {
+    p[i][0] = bcast16<k0>(av[i][q]) * b.x;
+    p[i][1] = bcast16<k0 + 1>(av[i][q]) * b.y;
+    p[i][2] = bcast16<k0 + 2>(av[i][q]) * b.z;
+    p[i][3] = bcast16<k0 + 3>(av[i][q]) * b.w;
+  }
+}
+template <int G, int NG, int LA, int NB, int RR, int NQ>
+__device__ __forceinline__ void bc_group(BcRing<NB>& r, uint32_t ba, const float (&av)[RR][NQ], float (&acc)[RR],
+                                         float (&pr)[RR][4]) {
+  if constexpr (G < NG) {
+    if constexpr (G + LA < NG) bc_read<G + LA, NB>(r, ba);
+    if constexpr (G + 1 < NG) {
+      float pn[RR][4];
+      bc_products<G + 1, NG, LA, NB, RR, NQ>(r, av, pn);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < RR; ++i) {
+          acc[i] = acc[i] + pr[i][k];
+          pr[i][k] = pn[i][k];
+        }
+      bc_group<G + 1, NG, LA, NB, RR, NQ>(r, ba, av, acc, pr);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < RR; ++i) acc[i] = acc[i] + pr[i][k];
+    }
+  }
+}
+
+template <int RR, int W, int CH, int LAV>
+__global__ __launch_bounds__(64 * W) void k_bc(const float* __restrict__ Ag, int na, const float* __restrict__ Bg,
+                                              int nb, int ld, int n, float* __restrict__ out, int ldo,
+                                              unsigned long long* clk) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  constexpr int NT = 64 * W, C4 = CH / 4, ROW = CH + 4, NI = 64 * C4, L4 = (NI + NT - 1) / NT;
+  constexpr int NQ = CH / 16, RB = W * RR;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int nrt = (na + RB - 1) / RB, ntiles = nrt * ((nb + 63) / 64);
+  const int per = (gridDim.x + 7) / 8, t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= ntiles) return;
+  const int i0 = (t % nrt) * RB, j0 = (t / nrt) * 64;
+  constexpr int kOff = 0x7ffffff0, kNo = kOff / 4;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)Ag, 0, kOff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Bg + (long long)j0 * ld), 0, kOff, 0x00020000);
+  int ao[RR], bo[L4];
+#pragma unroll
+  for (int i = 0; i < RR; ++i) {
+    const int row = i0 + w * RR + i;
+    ao[i] = row < na ? row * ld + (l & 15) : kNo;
+  }
+#pragma unroll
+  for (int k = 0; k < L4; ++k) {
+    const int e = tid + NT * k, row = e / C4;
+    bo[k] = e < NI && j0 + row < nb ? row * ld + (e % C4) * 4 : kNo;
+  }
+  f4 rg[L4];
+  float an[RR][NQ], av[RR][NQ];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int c4 = ((tid + NT * k) % C4) * 4;
+      rg[k] = __builtin_bit_cast(
+          f4, __builtin_amdgcn_raw_buffer_load_b128(rsb, bo[k] != kNo && x0 + c4 < n ? (bo[k] + x0) * 4 : kOff, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < RR; ++i)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int x = x0 + 16 * q + (l & 15);
+        an[i][q] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rsa, ao[i] != kNo && x < n ? (ao[i] + x0 + 16 * q) * 4 : kOff,
+                                                        0, 0));
+      }
+  };
+  const uint32_t ba = (uint32_t)(uintptr_t)(smem + l * ROW);
+  float acc[RR];
+#pragma unroll
+  for (int i = 0; i < RR; ++i) acc[i] = 0.0f;
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k;
+      if (e < NI) *(f4*)(smem + (e / C4) * ROW + (e % C4) * 4) = rg[k];
+    }
+#pragma unroll
+    for (int i = 0; i < RR; ++i)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) av[i][q] = an[i][q];
+    __syncthreads();
+    if (x0 + CH < n) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = LAV, NB = LA + 1;
+    BcRing<NB> ring;
+    bc_prologue<0, LA, NB>(ring, ba);
+    float pr[RR][4];
+    bc_products<0, NG, LA, NB, RR, NQ>(ring, av, pr);
+    bc_group<0, NG, LA, NB, RR, NQ>(ring, ba, av, acc, pr);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < RR; ++i) {
+    const int row = i0 + w * RR + i, j = j0 + l;
+    if (row < na && j < nb) out[(long long)row * ldo + j] = acc[i];
+  }
+  if (clk && blockIdx.x == 0 && tid == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - c0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
+// ---------------------------------------------------------------- bq: v1's 16 x 16 tiles, rows through DPP
+// Block = 4 waves = 16 rows x 16 alphas.  Wave w, 16-lane row r: A row
+// i0 + 4 w + r; lane k of that row: alpha j0 + k.  A row's cells come as one
+// float4 per lane (lane k: cells 64 q + 4 k .. + 3, one buffer_load_dwordx4 per
+// 64 cells, a chunk ahead) and reach the products through v_mul_f32_dpp
+// row_newbcast:(g % 16): the rows cost no LDS traffic, and the block stages
+// only its 16 alphas (one ds_read_b128 per 4 cells, broadcast to 4 lanes).
+template <int G, int NG, int LA, int NB, int NQ>
+__device__ __forceinline__ void bq_products(BcRing<NB>& r, const f4 (&av)[NQ], float (&p)[4]) {
+  constexpr int left = (NG - 1 - G) < (LA - 1) ? (NG - 1 - G) : (LA - 1);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(left) : "memory");
+  asm volatile("" : "+v"(r.b[G % NB]));
+  const f4 b = r.b[G % NB];
+  constexpr int q = G / 16, s = G % 16;
+  p[0] = bcast16<s>(av[q].x) * b.x;
+  p[1] = bcast16<s>(av[q].y) * b.y;
+  p[2] = bcast16<s>(av[q].z) * b.z;
+  p[3] = bcast16<s>(av[q].w) * b.w;
+}
+template <int G, int NG, int LA, int NB, int NQ>
+__device__ __forceinline__ void bq_group(BcRing<NB>& r, uint32_t ba, const f4 (&av)[NQ], float& acc, float (&pr)[4]) {
+  if constexpr (G < NG) {
+    if constexpr (G + LA < NG) bc_read<G + LA, NB>(r, ba);
+    if constexpr (G + 1 < NG) {
+      float pn[4];
+      bq_products<G + 1, NG, LA, NB, NQ>(r, av, pn);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc = acc + pr[k];
+        pr[k] = pn[k];
+      }
+      bq_group<G + 1, NG, LA, NB, NQ>(r, ba, av, acc, pr);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = acc + pr[k];
+    }
+  }
+}
+
+template <int CH, int LAV>
+__global__ __launch_bounds__(256) void k_bq(const float* __restrict__ Ag, int na, const float* __restrict__ Bg,
+                                           int nb, int ld, int n, float* __restrict__ out, int ldo,
+                                           unsigned long long* clk) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  constexpr int NT = 256, C4 = CH / 4, ROW = CH + 4, NI = 16 * C4, L4 = NI / NT, NQ = CH / 64;
+  static_assert(NI % NT == 0 && CH % 64 == 0, "whole float4 columns per thread, whole 64-cell blocks");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, rr = l >> 4, kk = l & 15;
+  const int nrt = (na + 15) / 16, ntiles = nrt * ((nb + 15) / 16);
+  const int per = (gridDim.x + 7) / 8, t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= ntiles) return;
+  const int i0 = (t % nrt) * 16, j0 = (t / nrt) * 16;
+  constexpr int kOff = 0x7ffffff0, kNo = kOff / 4;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)Ag, 0, kOff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Bg + (long long)j0 * ld), 0, kOff, 0x00020000);
+  const int row = i0 + 4 * w + rr;
+  const int ao = row < na ? row * ld + 4 * kk : kNo;
+  int bo[L4], bc4[L4];
+#pragma unroll
+  for (int k = 0; k < L4; ++k) {
+    const int e = tid + NT * k, br = e / C4;
+    bc4[k] = (e % C4) * 4;
+    bo[k] = j0 + br < nb ? br * ld + bc4[k] : kNo;
+  }
+  f4 rg[L4], an[NQ], av[NQ];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const bool in = (bo[k] != kNo) & (x0 + bc4[k] < n);
+      rg[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsb, in ? (bo[k] + x0) * 4 : kOff, 0, 0));
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const bool in = (ao != kNo) & (x0 + 64 * q + 4 * kk < n);
+      an[q] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsa, in ? (ao + x0 + 64 * q) * 4 : kOff,
+                                                                           0, 0));
+    }
+  };
+  const uint32_t ba = (uint32_t)(uintptr_t)(smem + kk * ROW);
+  float acc = 0.0f;
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k;
+      *(f4*)(smem + (e / C4) * ROW + (e % C4) * 4) = rg[k];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) av[q] = an[q];
+    __syncthreads();
+    if (x0 + CH < n) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = LAV, NB = LA + 1;
+    BcRing<NB> ring;
+    bc_prologue<0, LA, NB>(ring, ba);
+    float pr[4];
+    bq_products<0, NG, LA, NB, NQ>(ring, av, pr);
+    bq_group<0, NG, LA, NB, NQ>(ring, ba, av, acc, pr);
+    __syncthreads();
+  }
+  if (row < na && j0 + kk < nb) out[(long long)row * ldo + j0 + kk] = acc;
+  if (clk && blockIdx.x == 0 && tid == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - c0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
+// ---------------------------------------------------------------- mf: products on the matrix cores
+// v_mfma_f32_4x4x1_16b_f32 with C = 0 returns 16 blocks of 4 x 4 outer
+// products, each the IEEE product fl(a * b) (one rounding of the exact
+// product; a -0 product comes back +0, which leaves a chain from +0
+// unchanged).  Lane l = 4 b + t supplies A_b[t] and B_b[t] and receives
+// D_b[0..3][t]: block b = (row group b >> 2, alpha group b & 3), A_b = rows
+// K (b >> 2) + (t % K) (K = 2: rows r0, r1, r0, r1), B_b[t] = alpha 4 (b & 3) + t,
+// so lane l's chains are rows K (b >> 2) + v (v < K) against alpha 4 (b & 3) + t,
+// D[0..K) added in cell order by v_pk_add_f32.  One wave per block (4K rows x
+// 16 alphas), its rows staged by 16-B LDS-DMA into a ring of NS chunks of 256
+// cells (no VGPRs, no barriers: the wave reads only what it loaded).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+typedef float f4m __attribute__((ext_vector_type(4)));
+template <int NB>
+struct MfRing {
+  f4 a[NB], b[NB];
+};
+template <int G, int NB>
+__device__ __forceinline__ void mf_read(MfRing<NB>& r, uint32_t aa, uint32_t ba) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.a[G % NB]) : "v"(aa), "n"(16 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.b[G % NB]) : "v"(ba), "n"(16 * G));
+}
+template <int G, int LA, int NB>
+__device__ __forceinline__ void mf_prologue(MfRing<NB>& r, uint32_t aa, uint32_t ba) {
+  if constexpr (G < LA) {
+    mf_read<G, NB>(r, aa, ba);
+    mf_prologue<G + 1, LA, NB>(r, aa, ba);
+  }
+}
+template <int G, int NG, int LA, int NB>
+__device__ __forceinline__ void mf_products(MfRing<NB>& r, f4m (&d)[4]) {
+  constexpr int left = (NG - 1 - G) < (LA - 1) ? (NG - 1 - G) : (LA - 1);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * left) : "memory");
+  asm volatile("" : "+v"(r.a[G % NB]), "+v"(r.b[G % NB]));
+  const f4 a = r.a[G % NB], b = r.b[G % NB];
+  const f4m z = {0.0f, 0.0f, 0.0f, 0.0f};
+  d[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(a.x, b.x, z, 0, 0, 0);
+  d[1] = __builtin_amdgcn_mfma_f32_4x4x1f32(a.y, b.y, z, 0, 0, 0);
+  d[2] = __builtin_amdgcn_mfma_f32_4x4x1f32(a.z, b.z, z, 0, 0, 0);
+  d[3] = __builtin_amdgcn_mfma_f32_4x4x1f32(a.w, b.w, z, 0, 0, 0);
+}
+template <int K>
+__device__ __forceinline__ void mf_add(f2 (&acc)[K / 2], const f4m (&d)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    acc[0] = acc[0] + f2{d[c][0], d[c][1]};
+    if constexpr (K == 4) acc[1] = acc[1] + f2{d[c][2], d[c][3]};
+  }
+}
+template <int G, int NG, int LA, int NB, int K>
+__device__ __forceinline__ void mf_group(MfRing<NB>& r, uint32_t aa, uint32_t ba, f2 (&acc)[K / 2], f4m (&pr)[4]) {
+  if constexpr (G < NG) {
+    if constexpr (G + LA < NG) mf_read<G + LA, NB>(r, aa, ba);
+    if constexpr (G + 1 < NG) {
+      f4m pn[4];
+      mf_products<G + 1, NG, LA, NB>(r, pn);
+      mf_add<K>(acc, pr);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pr[c] = pn[c];
+      mf_group<G + 1, NG, LA, NB, K>(r, aa, ba, acc, pr);
+    } else {
+      mf_add<K>(acc, pr);
+    }
+  }
+}
+
+static float* g_zero = nullptr;
+template <int K, int LAV, int NS>
+__global__ __launch_bounds__(64) void k_mf(const float* __restrict__ Ag, int na, const float* __restrict__ Bg,
+                                          int nb, int ld, int n, float* __restrict__ out, int ldo,
+                                          unsigned long long* clk, const float* __restrict__ zero) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  constexpr int CH = 256, RW = 4 * K, NR = RW + 16, ROWB = CH * 4 + 16, SLOT = NR * ROWB;
+  extern __shared__ __attribute__((aligned(16))) char ring[];
+  const int lane = threadIdx.x, b = lane >> 2, t = lane & 3;
+  const int nrt = (na + RW - 1) / RW, ntiles = nrt * ((nb + 15) / 16);
+  const int per = (gridDim.x + 7) / 8, tile = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (tile >= ntiles) return;
+  const int i0 = (tile % nrt) * RW, j0 = (tile / nrt) * 16;
+  const int nch = (n + CH - 1) / CH;
+  auto issue = [&](int k, int s) {
+    const int x = k * CH + 4 * lane;
+    char* slot = ring + s * SLOT;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const bool ok = r < RW ? i0 + r < na : j0 + r - RW < nb;
+      const float* row = r < RW ? Ag + (long long)(i0 + r) * ld : Bg + (long long)(j0 + r - RW) * ld;
+      uintptr_t g = (uintptr_t)(ok && x < n ? row + x : zero + 4 * lane);
+      asm("" : "+v"(g));
+      __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)(slot + r * ROWB), 16, 0, 0);
+    }
+  };
+  const uint32_t base = (uint32_t)(uintptr_t)ring;
+  const uint32_t aoff = (uint32_t)((K * (b >> 2) + (t % K)) * ROWB), boff = (uint32_t)((RW + 4 * (b & 3) + t) * ROWB);
+  f2 acc[K / 2];
+#pragma unroll
+  for (int v = 0; v < K / 2; ++v) acc[v] = f2{0.0f, 0.0f};
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nch) issue(s, s);
+  for (int k = 0; k < nch; ++k) {
+    const int s = k % NS;
+    if (k + NS - 1 < nch) {
+      issue(k + NS - 1, (k + NS - 1) % NS);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR * (NS - 1)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint32_t aa = base + s * SLOT + aoff, ba = base + s * SLOT + boff;
+    constexpr int NG = CH / 4, LA = LAV, NB = LA + 1;
+    MfRing<NB> rr;
+    mf_prologue<0, LA, NB>(rr, aa, ba);
+    f4m pr[4];
+    mf_products<0, NG, LA, NB>(rr, pr);
+    mf_group<0, NG, LA, NB, K>(rr, aa, ba, acc, pr);
+  }
+  const int j = j0 + 4 * (b & 3) + t;
+#pragma unroll
+  for (int v = 0; v < K; ++v) {
+    const int i = i0 + K * (b >> 2) + v;
+    if (i < na && j < nb) out[(long long)i * ldo + j] = acc[v / 2][v & 1];
+  }
+  if (clk && blockIdx.x == 0 && lane == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - c0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
 // ---------------------------------------------------------------- harness
 static uint64_t sm_state = 0x243F6A8885A308D3ull;
 static uint64_t splitmix() {
@@ -905,6 +1294,51 @@ static void launch_t2(hipStream_t st, const float* Ag, int na, const float* Bg, 
                      Ag, na, Bg, nb, ld, n, out, ldo);
 }
 
+template <int RR, int W, int CH, int LAV>
+static void launch_bc(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n, float* out,
+                      int ldo) {
+  const size_t lds = (size_t)64 * (CH + 4) * sizeof(float);
+  static bool once = false;
+  if (!once) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bc<RR, W, CH, LAV>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    once = true;
+  }
+  const int tiles = cdiv(na, W * RR) * cdiv(nb, 64);
+  hipLaunchKernelGGL((k_bc<RR, W, CH, LAV>), dim3(cdiv(tiles, 8) * 8), dim3(64 * W), lds, st, Ag, na, Bg, nb, ld,
+                     n, out, ldo, g_clk);
+}
+
+template <int CH, int LAV>
+static void launch_bq(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n, float* out,
+                      int ldo) {
+  const size_t lds = (size_t)16 * (CH + 4) * sizeof(float);
+  static bool once = false;
+  if (!once) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bq<CH, LAV>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    once = true;
+  }
+  const int tiles = cdiv(na, 16) * cdiv(nb, 16);
+  hipLaunchKernelGGL((k_bq<CH, LAV>), dim3(cdiv(tiles, 8) * 8), dim3(256), lds, st, Ag, na, Bg, nb, ld, n, out, ldo,
+                     g_clk);
+}
+
+template <int K, int LAV, int NS>
+static void launch_mf(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n, float* out,
+                      int ldo) {
+  const size_t lds = (size_t)NS * (4 * K + 16) * (256 * 4 + 16);
+  static bool once = false;
+  if (!once) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mf<K, LAV, NS>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    once = true;
+  }
+  const int tiles = cdiv(na, 4 * K) * cdiv(nb, 16);
+  hipLaunchKernelGGL((k_mf<K, LAV, NS>), dim3(cdiv(tiles, 8) * 8), dim3(64), lds, st, Ag, na, Bg, nb, ld, n, out,
+                     ldo, g_clk, g_zero);
+}
+
 struct Variant {
   const char* name;
   Launch fn;
@@ -939,6 +1373,8 @@ int main(int argc, char** argv) {
   hipStream_t st;
   CK(hipStreamCreate(&st));
   CK(hipMalloc(&g_clk, 16));
+  CK(hipMalloc(&g_zero, 4096));
+  CK(hipMemset(g_zero, 0, 4096));
   const Variant vs[] = {
       {"v0 k_pair_seq 16x16, 1 chain/lane", launch_v0<false>},
       {"v1 16x16 LA4", launch_v1<16, 16, 512>},
@@ -949,6 +1385,12 @@ int main(int argc, char** argv) {
       {"t4 16 rows x 18 alphas (pk pairs)", launch_t4<8, 18, 512>},
       {"t4 16x18 LA5", launch_t4<8, 18, 512, 5>},
       {"t4 16x32 LA5", launch_t4<8, 32, 512, 5>},
+      {"bc 4 rows x 64 alphas CH256 LA8", launch_bc<1, 4, 256, 8>},
+      {"bc 8x64 (W8) CH256 LA8", launch_bc<1, 8, 256, 8>},
+      {"bq 16x16 rows by DPP CH512 LA8", launch_bq<512, 8>},
+      {"mf K2 8x16 per wave LA7 NS2", launch_mf<2, 7, 2>},
+      {"mf K2 LA4 NS2", launch_mf<2, 4, 2>},
+      {"mf K4 16x16 per wave LA7 NS2", launch_mf<4, 7, 2>},
   };
   const int NV = sizeof(vs) / sizeof(vs[0]);
   std::vector<float> ref((size_t)na * nb), got((size_t)na * nb);

@@ -1,6 +1,7 @@
 """The bench's PBVI-leaf plan steps alone, reference order, with the PBVI
-leaf dots as packed two-chain lanes (k_pair_dot_pk, PP2_PAIR_DOT=1), one
-chain per lane (k_pair_dot_1, =2, the default), the round-5 lookahead
+leaf dots as one chain per lane with the rows by DPP broadcast
+(k_pair_dot_bq, PP2_PAIR_DOT=3, the default), packed two-chain lanes
+(k_pair_dot_pk, =1), one chain per lane from LDS (k_pair_dot_1, =2), the lookahead
 k_pair_seq (=0) and, with PP2_AB_FC=1, FC_LIST candidate chain sets
 (PP2_PBVI_FCHAIN=1), alternated on one box:
   * 256^2 synthetic, S = 500 alphas, depth 3 (bench plan_step_pbvi_lb);
@@ -34,7 +35,7 @@ def main():
         calls = ctx.pbvi_belief_set(b0, 500)
         ctx.pbvi_backup(int(os.environ.get("PP2_ITERS", "0")))
         res = {}
-        modes = [("pk", "0", "1"), ("one", "0", "2"), ("seq", "0", "0")]
+        modes = [("bq", "0", "3"), ("pk", "0", "1"), ("one", "0", "2"), ("seq", "0", "0")]
         if os.environ.get("PP2_AB_FC") == "1":
             modes.append(("fc", "1", "1"))
         for rep in range(2):
@@ -49,7 +50,8 @@ def main():
                     ms, acts, vals = S.closed_loop(grid, b0, pl.step, steps)
                 res.setdefault(mode, []).append((float(np.percentile(ms, 50)), acts, vals))
         ctx.close()
-        names = {"pk": "k_pair_dot_pk (PP2_PAIR_DOT=1)", "one": "k_pair_dot_1 (default)",
+        names = {"bq": "k_pair_dot_bq (default)", "pk": "k_pair_dot_pk (PP2_PAIR_DOT=1)",
+                 "one": "k_pair_dot_1 (PP2_PAIR_DOT=2)",
                  "seq": "k_pair_seq (PP2_PAIR_DOT=0)",
                  "fc": "FC_LIST candidate chain sets (PP2_PBVI_FCHAIN=1)"}
         for mode, _, _ in modes:
