@@ -1059,6 +1059,121 @@ __global__ __launch_bounds__(256) void k_bq(const float* __restrict__ Ag, int na
   }
 }
 
+// ---------------------------------------------------------------- bq2: two child rows per 16-lane row
+// As bq, but each 16-lane row holds two child rows (two float4 sets) against
+// its lanes' alphas: per cell two v_mul_f32_dpp and one v_pk_add_f32 for two
+// chains, one alpha read per 4 cells for both.  Block = 4 waves = 32 rows x
+// 16 alphas: 144 x 500 is 640 waves, every SIMD at most one.
+template <int G, int NG, int LA, int NB, int NQ>
+__device__ __forceinline__ void bq2_products(BcRing<NB>& r, const f4 (&av)[2][NQ], f2 (&p)[4]) {
+  constexpr int left = (NG - 1 - G) < (LA - 1) ? (NG - 1 - G) : (LA - 1);
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(left) : "memory");
+  asm volatile("" : "+v"(r.b[G % NB]));
+  const f4 b = r.b[G % NB];
+  constexpr int q = G / 16, s = G % 16;
+  p[0] = f2{bcast16<s>(av[0][q].x) * b.x, bcast16<s>(av[1][q].x) * b.x};
+  p[1] = f2{bcast16<s>(av[0][q].y) * b.y, bcast16<s>(av[1][q].y) * b.y};
+  p[2] = f2{bcast16<s>(av[0][q].z) * b.z, bcast16<s>(av[1][q].z) * b.z};
+  p[3] = f2{bcast16<s>(av[0][q].w) * b.w, bcast16<s>(av[1][q].w) * b.w};
+}
+template <int G, int NG, int LA, int NB, int NQ>
+__device__ __forceinline__ void bq2_group(BcRing<NB>& r, uint32_t ba, const f4 (&av)[2][NQ], f2& acc, f2 (&pr)[4]) {
+  if constexpr (G < NG) {
+    if constexpr (G + LA < NG) bc_read<G + LA, NB>(r, ba);
+    if constexpr (G + 1 < NG) {
+      f2 pn[4];
+      bq2_products<G + 1, NG, LA, NB, NQ>(r, av, pn);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc = acc + pr[k];
+        pr[k] = pn[k];
+      }
+      bq2_group<G + 1, NG, LA, NB, NQ>(r, ba, av, acc, pr);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = acc + pr[k];
+    }
+  }
+}
+
+template <int CH, int LAV>
+__global__ __launch_bounds__(256) void k_bq2(const float* __restrict__ Ag, int na, const float* __restrict__ Bg,
+                                            int nb, int ld, int n, float* __restrict__ out, int ldo,
+                                            unsigned long long* clk) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  constexpr int NT = 256, C4 = CH / 4, ROW = CH + 4, NI = 16 * C4, L4 = NI / NT, NQ = CH / 64;
+  static_assert(NI % NT == 0 && CH % 64 == 0, "whole float4 columns per thread, whole 64-cell blocks");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, rr = l >> 4, kk = l & 15;
+  const int nrt = (na + 31) / 32, ntiles = nrt * ((nb + 15) / 16);
+  const int per = (gridDim.x + 7) / 8, t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= ntiles) return;
+  const int i0 = (t % nrt) * 32, j0 = (t / nrt) * 16;
+  constexpr int kOff = 0x7ffffff0, kNo = kOff / 4;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)Ag, 0, kOff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Bg + (long long)j0 * ld), 0, kOff, 0x00020000);
+  int rows[2], ao[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    rows[h] = i0 + 8 * w + 4 * h + rr;
+    ao[h] = rows[h] < na ? rows[h] * ld + 4 * kk : kNo;
+  }
+  int bo[L4], bc4[L4];
+#pragma unroll
+  for (int k = 0; k < L4; ++k) {
+    const int e = tid + NT * k, br = e / C4;
+    bc4[k] = (e % C4) * 4;
+    bo[k] = j0 + br < nb ? br * ld + bc4[k] : kNo;
+  }
+  f4 rg[L4], an[2][NQ], av[2][NQ];
+  auto fetch = [&](int x0) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const bool in = (bo[k] != kNo) & (x0 + bc4[k] < n);
+      rg[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsb, in ? (bo[k] + x0) * 4 : kOff, 0, 0));
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const bool in = (ao[h] != kNo) & (x0 + 64 * q + 4 * kk < n);
+        an[h][q] = __builtin_bit_cast(
+            f4, __builtin_amdgcn_raw_buffer_load_b128(rsa, in ? (ao[h] + x0 + 64 * q) * 4 : kOff, 0, 0));
+      }
+  };
+  const uint32_t ba = (uint32_t)(uintptr_t)(smem + kk * ROW);
+  f2 acc = f2{0.0f, 0.0f};
+  fetch(0);
+  for (int x0 = 0; x0 < n; x0 += CH) {
+#pragma unroll
+    for (int k = 0; k < L4; ++k) {
+      const int e = tid + NT * k;
+      *(f4*)(smem + (e / C4) * ROW + (e % C4) * 4) = rg[k];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) av[h][q] = an[h][q];
+    __syncthreads();
+    if (x0 + CH < n) fetch(x0 + CH);
+    constexpr int NG = CH / 4, LA = LAV, NB = LA + 1;
+    BcRing<NB> ring;
+    bc_prologue<0, LA, NB>(ring, ba);
+    f2 pr[4];
+    bq2_products<0, NG, LA, NB, NQ>(ring, av, pr);
+    bq2_group<0, NG, LA, NB, NQ>(ring, ba, av, acc, pr);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (rows[h] < na && j0 + kk < nb) out[(long long)rows[h] * ldo + j0 + kk] = acc[h];
+  if (clk && blockIdx.x == 0 && tid == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - c0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
 // ---------------------------------------------------------------- mf: products on the matrix cores
 // v_mfma_f32_4x4x1_16b_f32 with C = 0 returns 16 blocks of 4 x 4 outer
 // products, each the IEEE product fl(a * b) (one rounding of the exact
@@ -1324,6 +1439,21 @@ static void launch_bq(hipStream_t st, const float* Ag, int na, const float* Bg, 
                      g_clk);
 }
 
+template <int CH, int LAV>
+static void launch_bq2(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n, float* out,
+                       int ldo) {
+  const size_t lds = (size_t)16 * (CH + 4) * sizeof(float);
+  static bool once = false;
+  if (!once) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bq2<CH, LAV>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    once = true;
+  }
+  const int tiles = cdiv(na, 32) * cdiv(nb, 16);
+  hipLaunchKernelGGL((k_bq2<CH, LAV>), dim3(cdiv(tiles, 8) * 8), dim3(256), lds, st, Ag, na, Bg, nb, ld, n, out,
+                     ldo, g_clk);
+}
+
 template <int K, int LAV, int NS>
 static void launch_mf(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n, float* out,
                       int ldo) {
@@ -1388,9 +1518,9 @@ int main(int argc, char** argv) {
       {"bc 4 rows x 64 alphas CH256 LA8", launch_bc<1, 4, 256, 8>},
       {"bc 8x64 (W8) CH256 LA8", launch_bc<1, 8, 256, 8>},
       {"bq 16x16 rows by DPP CH512 LA8", launch_bq<512, 8>},
-      {"mf K2 8x16 per wave LA7 NS2", launch_mf<2, 7, 2>},
-      {"mf K2 LA4 NS2", launch_mf<2, 4, 2>},
-      {"mf K4 16x16 per wave LA7 NS2", launch_mf<4, 7, 2>},
+      {"bq2 32x16, 2 rows per 16-lane row CH512 LA8", launch_bq2<512, 8>},
+      {"bq2 CH256 LA8", launch_bq2<256, 8>},
+      {"bq2 CH512 LA4", launch_bq2<512, 4>},
   };
   const int NV = sizeof(vs) / sizeof(vs[0]);
   std::vector<float> ref((size_t)na * nb), got((size_t)na * nb);
