@@ -6,6 +6,7 @@
 // Built with -fno-slp-vectorize (Makefile): paired into v_pk_mul_f32, the
 // products would keep each broadcast as a separate v_mov_b32_dpp.
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <stdint.h>
 
 #include "pp2_pbvi_internal.h"
@@ -75,9 +76,14 @@ __device__ __forceinline__ void group(Ring<NB>& r, uint32_t ba, const f4 (&av)[N
   }
 }
 
-__device__ __forceinline__ int xcd_tile(int ntiles_grid) {
-  const int per = (ntiles_grid + 7) / 8;
-  return (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+// The live tiles (ntiles: known on the device only, from acount) numbered
+// per XCD: block b runs on XCD b % 8 and takes tile (b % 8) * per + b / 8, so
+// each XCD's blocks cover whole alpha tiles and the live tiles spread over
+// all 8 XCDs whatever the launch's grid (sized for every row); past them
+// INT_MAX (the block exits).
+__device__ __forceinline__ int xcd_tile(int ntiles) {
+  const int per = (ntiles + 7) / 8, k = (int)(blockIdx.x / 8);
+  return k < per ? (int)(blockIdx.x % 8) * per + k : INT_MAX;
 }
 
 // Block = 4 waves = 16 children x 16 alphas (k_pair_dot_1's tile, its tiles
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(256) void k_pair_dot_bq(const float* __restrict__ A
   if (alist) na = min(na, *acount);
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, rr = l >> 4, kk = l & 15;
   const int nrt = (na + 15) / 16, ntiles = nrt * ((nb + 15) / 16);
-  const int t = xcd_tile(gridDim.x);
+  const int t = xcd_tile(ntiles);
   if (t >= ntiles) return;  // (uniform over the block)
   const int i0 = (t % nrt) * 16, j0 = (t / nrt) * 16;
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)Ag, 0, kOff, 0x00020000);

@@ -547,9 +547,14 @@ constexpr int kDotOff = 0x7ffffff0;  // buffer offset past any range: the load r
 __device__ __forceinline__ f4 ldq_rs(__amdgpu_buffer_rsrc_t rs, int off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
 }
-__device__ __forceinline__ int xcd_tile(int ntiles_grid) {
-  const int per = (ntiles_grid + 7) / 8;
-  return (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+// The live tiles (ntiles: known on the device only, from acount) numbered
+// per XCD: block b runs on XCD b % 8 and takes tile (b % 8) * per + b / 8, so
+// each XCD's blocks cover whole alpha tiles and the live tiles spread over
+// all 8 XCDs whatever the launch's grid (sized for every row); past them
+// INT_MAX (the block exits).
+__device__ __forceinline__ int xcd_tile(int ntiles) {
+  const int per = (ntiles + 7) / 8, k = (int)(blockIdx.x / 8);
+  return k < per ? (int)(blockIdx.x % 8) * per + k : INT_MAX;
 }
 
 typedef float f2p __attribute__((ext_vector_type(2)));
@@ -663,7 +668,7 @@ __global__ __launch_bounds__((RP * A + 63) / 64 * 64) void k_pair_dot_pk(
   if (alist) na = min(na, *acount);
   const int tid = threadIdx.x;
   const int nrt = (na + 2 * RP - 1) / (2 * RP), ntiles = nrt * ((nb + A - 1) / A);
-  const int t = xcd_tile(gridDim.x);
+  const int t = xcd_tile(ntiles);
   if (t >= ntiles) return;  // (uniform over the block)
   const int i0 = (t % nrt) * 2 * RP, j0 = (t / nrt) * A;
   // rows through the full A (alist: any row of it), alphas from the tile's first
@@ -743,7 +748,7 @@ __global__ __launch_bounds__(TA * TB) void k_pair_dot_1(
   if (alist) na = min(na, *acount);
   const int tid = threadIdx.x, la = tid % TA, jb = tid / TA;
   const int nrt = (na + TA - 1) / TA, ntiles = nrt * ((nb + TB - 1) / TB);
-  const int t = xcd_tile(gridDim.x);
+  const int t = xcd_tile(ntiles);
   if (t >= ntiles) return;  // (uniform over the block)
   const int i0 = (t % nrt) * TA, j0 = (t / nrt) * TB;
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)Ag, 0, kDotOff, 0x00020000);

@@ -1254,8 +1254,9 @@ int pp2_planner_destroy(pp2_planner* p) {
     if (d) (void)hipFree(d);
   if (p->timing && p->t_n > 0)
     fprintf(stderr, "pp2 planner: %lld expansions, host us per expansion: enqueue %.1f, "
-            "after the wait .. children stored %.1f, .. next expansion %.1f\n", p->t_n,
-            p->t_enq / p->t_n, p->t_post / p->t_n, p->t_between / (p->t_n > 1 ? p->t_n - 1 : 1));
+            "after the wait .. children stored %.1f, .. next expansion %.1f; kept children "
+            "per expansion %.1f\n", p->t_n, p->t_enq / p->t_n, p->t_post / p->t_n,
+            p->t_between / (p->t_n > 1 ? p->t_n - 1 : 1), (double)p->stat_rows / (double)p->t_n);
   if (p->h_pstat) {
     if (p->stat_sets > 0)
       fprintf(stderr, "pp2 planner: PBVI candidate chains %lld over %lld rows in %lld sets "
