@@ -991,7 +991,7 @@ __device__ __forceinline__ void bq_group(BcRing<NB>& r, uint32_t ba, const f4 (&
   }
 }
 
-template <int CH, int LAV>
+template <int CH, int LAV, int MODE = 0>
 __global__ __launch_bounds__(256) void k_bq(const float* __restrict__ Ag, int na, const float* __restrict__ Bg,
                                            int nb, int ld, int n, float* __restrict__ out, int ldo,
                                            unsigned long long* clk) {
@@ -1043,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_bq(const float* __restrict__ Ag, int na
 #pragma unroll
     for (int q = 0; q < NQ; ++q) av[q] = an[q];
     __syncthreads();
-    if (x0 + CH < n) fetch(x0 + CH);
+    if (x0 + CH < n && MODE == 0) fetch(x0 + CH);
     constexpr int NG = CH / 4, LA = LAV, NB = LA + 1;
     BcRing<NB> ring;
     bc_prologue<0, LA, NB>(ring, ba);
@@ -1424,18 +1424,18 @@ static void launch_bc(hipStream_t st, const float* Ag, int na, const float* Bg, 
                      n, out, ldo, g_clk);
 }
 
-template <int CH, int LAV>
+template <int CH, int LAV, int MODE = 0>
 static void launch_bq(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n, float* out,
                       int ldo) {
   const size_t lds = (size_t)16 * (CH + 4) * sizeof(float);
   static bool once = false;
   if (!once) {
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bq<CH, LAV>),
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bq<CH, LAV, MODE>),
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     once = true;
   }
   const int tiles = cdiv(na, 16) * cdiv(nb, 16);
-  hipLaunchKernelGGL((k_bq<CH, LAV>), dim3(cdiv(tiles, 8) * 8), dim3(256), lds, st, Ag, na, Bg, nb, ld, n, out, ldo,
+  hipLaunchKernelGGL((k_bq<CH, LAV, MODE>), dim3(cdiv(tiles, 8) * 8), dim3(256), lds, st, Ag, na, Bg, nb, ld, n, out, ldo,
                      g_clk);
 }
 
@@ -1518,9 +1518,8 @@ int main(int argc, char** argv) {
       {"bc 4 rows x 64 alphas CH256 LA8", launch_bc<1, 4, 256, 8>},
       {"bc 8x64 (W8) CH256 LA8", launch_bc<1, 8, 256, 8>},
       {"bq 16x16 rows by DPP CH512 LA8", launch_bq<512, 8>},
+      {"bq CH512 LA8 no refetch (diag)", launch_bq<512, 8, 1>},
       {"bq2 32x16, 2 rows per 16-lane row CH512 LA8", launch_bq2<512, 8>},
-      {"bq2 CH256 LA8", launch_bq2<256, 8>},
-      {"bq2 CH512 LA4", launch_bq2<512, 4>},
   };
   const int NV = sizeof(vs) / sizeof(vs[0]);
   std::vector<float> ref((size_t)na * nb), got((size_t)na * nb);
