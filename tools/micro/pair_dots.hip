@@ -1059,6 +1059,71 @@ __global__ __launch_bounds__(256) void k_bq(const float* __restrict__ Ag, int na
   }
 }
 
+// ---------------------------------------------------------------- bv: bq without LDS
+// bq's tiles and DPP rows, but each lane loads its own alpha's cells straight
+// into registers (one buffer_load_dwordx4 per 4 cells, a 64-cell block ahead;
+// the block's 4 waves read the same 16 alphas, L1 hits): no staging, no LDS,
+// no barriers; the compiler counts the in-order vmcnt returns.
+template <int NQB>
+__device__ __forceinline__ void bv_block(const f4& a, const f4 (&al)[16], float& acc) {
+  static_for<0, 16>([&](auto gc) {
+    constexpr int g = decltype(gc)::value;
+    const f4 b = al[g];
+    const float p0 = bcast16<g>(a.x) * b.x, p1 = bcast16<g>(a.y) * b.y;
+    const float p2 = bcast16<g>(a.z) * b.z, p3 = bcast16<g>(a.w) * b.w;
+    acc = acc + p0;
+    acc = acc + p1;
+    acc = acc + p2;
+    acc = acc + p3;
+  });
+}
+
+__global__ __launch_bounds__(256) void k_bv(const float* __restrict__ Ag, int na, const float* __restrict__ Bg,
+                                           int nb, int ld, int n, float* __restrict__ out, int ldo,
+                                           unsigned long long* clk) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, rr = l >> 4, kk = l & 15;
+  const int nrt = (na + 15) / 16, ntiles = nrt * ((nb + 15) / 16);
+  const int per = (ntiles + 7) / 8, kb = blockIdx.x / 8;
+  if (kb >= per) return;
+  const int t = (blockIdx.x % 8) * per + kb;
+  if (t >= ntiles) return;
+  const int i0 = (t % nrt) * 16, j0 = (t / nrt) * 16;
+  constexpr int kOff = 0x7ffffff0, kNo = kOff / 4;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)Ag, 0, kOff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)Bg, 0, kOff, 0x00020000);
+  const int row = i0 + 4 * w + rr, alpha = j0 + kk;
+  const int ao = row < na ? row * ld + 4 * kk : kNo;
+  const int bo = alpha < nb ? alpha * ld : kNo;
+  auto load = [&](int x0, f4& a, f4 (&al)[16]) {
+    const bool ina = (ao != kNo) & (x0 + 4 * kk < n);
+    a = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsa, ina ? (ao + x0) * 4 : kOff, 0, 0));
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const bool inb = (bo != kNo) & (x0 + 4 * g < n);
+      al[g] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsb, inb ? (bo + x0 + 4 * g) * 4 : kOff,
+                                                                           0, 0));
+    }
+  };
+  float acc = 0.0f;
+  f4 a0, a1, al0[16], al1[16];
+  load(0, a0, al0);
+  for (int x0 = 0; x0 < n; x0 += 128) {
+    load(x0 + 64, a1, al1);  // (past n: reads +0.0)
+    __builtin_amdgcn_sched_barrier(0);  // the next block's loads stay ahead of this block
+    bv_block<0>(a0, al0, acc);
+    if (x0 + 64 >= n) break;
+    load(x0 + 128, a0, al0);
+    __builtin_amdgcn_sched_barrier(0);
+    bv_block<0>(a1, al1, acc);
+  }
+  if (row < na && alpha < nb) out[(long long)row * ldo + alpha] = acc;
+  if (clk && blockIdx.x == 0 && tid == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - c0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
 // ---------------------------------------------------------------- bq2: two child rows per 16-lane row
 // As bq, but each 16-lane row holds two child rows (two float4 sets) against
 // its lanes' alphas: per cell two v_mul_f32_dpp and one v_pk_add_f32 for two
@@ -1439,6 +1504,12 @@ static void launch_bq(hipStream_t st, const float* Ag, int na, const float* Bg, 
                      g_clk);
 }
 
+static void launch_bv(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n, float* out,
+                      int ldo) {
+  const int tiles = cdiv(na, 16) * cdiv(nb, 16);
+  hipLaunchKernelGGL(k_bv, dim3(cdiv(tiles, 8) * 8), dim3(256), 0, st, Ag, na, Bg, nb, ld, n, out, ldo, g_clk);
+}
+
 template <int CH, int LAV>
 static void launch_bq2(hipStream_t st, const float* Ag, int na, const float* Bg, int nb, int ld, int n, float* out,
                        int ldo) {
@@ -1519,6 +1590,7 @@ int main(int argc, char** argv) {
       {"bc 8x64 (W8) CH256 LA8", launch_bc<1, 8, 256, 8>},
       {"bq 16x16 rows by DPP CH512 LA8", launch_bq<512, 8>},
       {"bq CH512 LA8 no refetch (diag)", launch_bq<512, 8, 1>},
+      {"bv bq without LDS (alphas by buffer loads)", launch_bv},
       {"bq2 32x16, 2 rows per 16-lane row CH512 LA8", launch_bq2<512, 8>},
   };
   const int NV = sizeof(vs) / sizeof(vs[0]);
