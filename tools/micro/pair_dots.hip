@@ -1590,6 +1590,8 @@ int main(int argc, char** argv) {
       {"bc 8x64 (W8) CH256 LA8", launch_bc<1, 8, 256, 8>},
       {"bq 16x16 rows by DPP CH512 LA8", launch_bq<512, 8>},
       {"bq CH512 LA8 no refetch (diag)", launch_bq<512, 8, 1>},
+      {"bq CH256 LA8", launch_bq<256, 8>},
+      {"bq CH128 LA8", launch_bq<128, 8>},
       {"bv bq without LDS (alphas by buffer loads)", launch_bv},
       {"bq2 32x16, 2 rows per 16-lane row CH512 LA8", launch_bq2<512, 8>},
   };
