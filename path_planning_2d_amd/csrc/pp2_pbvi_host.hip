@@ -987,7 +987,10 @@ __global__ __launch_bounds__(64) void k_chain_walk(const float* __restrict__ A, 
     float acc = 0.0f;
     for (int g0 = 0; g0 < ng; g0 += NB) {
       const uint32_t ad = base + 16u * (uint32_t)g0, od = obase + 16u * (uint32_t)g0;
-      walk_groups<0, LA, NB, W, MODE == WALK_CDF>(ring, ad, od, acc);
+      // a cdf's first groups have fewer than LA sums writes behind their
+      // read: wait as the dot does (the writes complete too)
+      if (g0 == 0) walk_groups<0, LA, NB, LA, MODE == WALK_CDF>(ring, ad, od, acc);
+      else walk_groups<0, LA, NB, W, MODE == WALK_CDF>(ring, ad, od, acc);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     out[(long long)row * ldo + j] = acc;
@@ -996,6 +999,97 @@ __global__ __launch_bounds__(64) void k_chain_walk(const float* __restrict__ A, 
     __syncthreads();
     for (int x = lane; x < n; x += 64) cdf[x] = sT[walk_cap(n) + x];
   }
+}
+
+// The same walk with its terms formed beside it (PP2_CHAIN_WALK=2; no faster
+// on the node's plan step, profiles/r05/chain_walk2_ab.txt): wave 1 forms
+// chunk k's terms (and loads chunk k + 1's cells) while lane 0 of wave 0
+// walks chunk k - 1, one barrier per chunk, terms (and a cdf's running sums)
+// double-buffered in LDS -- k_chain_walk forms all n terms before its walk
+// starts.  Same terms, same order of adds: bit-identical results.
+constexpr int kWalk2C = 512;  // terms per chunk: whole walk iterations (4 * kWalkNB)
+static_assert(kWalk2C % (4 * kWalkNB) == 0 && kWalk2C % 256 == 0, "whole iterations, whole lane steps");
+template <int MODE>
+__global__ __launch_bounds__(128) void k_chain_walk2(const float* __restrict__ A, int na,
+                                                    const float* __restrict__ B, int nb, int ld,
+                                                    int n, float* __restrict__ out, int ldo,
+                                                    const int* __restrict__ alist,
+                                                    const int* __restrict__ acount,
+                                                    float* __restrict__ cdf) {
+  constexpr int C = kWalk2C, CP = C + 4 * kWalkLA, Q = C / 256;
+  constexpr bool CDF = MODE == WALK_CDF;
+  __shared__ __attribute__((aligned(16))) float sT[2][CP];  // terms (+ the walk's read-ahead slack)
+  __shared__ __attribute__((aligned(16))) float sS[2][CDF ? C : 4];  // a cdf's running sums
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = blockIdx.x / nb, j = blockIdx.x % nb;
+  if (alist && i >= *acount) return;  // (uniform over the block)
+  const int row = alist ? alist[i] : i;
+  const float* __restrict__ a = A + (long long)row * ld;
+  const float* __restrict__ b = CDF ? nullptr : B + (long long)j * ld;
+  const int nch = (n + C - 1) / C;
+  // wave 1: the cells of chunk k, 4 per lane per 256-cell step (past n: +0,
+  // which leaves the chain unchanged -- it starts at +0, so is never -0)
+  f4 va[Q], vb[Q];
+  auto load = [&](int k) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int x = k * C + 4 * lane + 256 * q;
+      va[q] = vb[q] = f4{0, 0, 0, 0};
+      if (x + 3 < n) {
+        va[q] = *(const f4*)(a + x);
+        if (!CDF) vb[q] = *(const f4*)(b + x);
+      } else if (x < n) {
+        for (int c = 0; c < 4; ++c)
+          if (x + c < n) {
+            va[q][c] = a[x + c];
+            if (!CDF) vb[q][c] = b[x + c];
+          }
+      }
+    }
+  };
+  float acc = 0.0f;
+  if (w == 1) load(0);
+  for (int k = 0; k <= nch; ++k) {
+    if (w == 1) {
+      if (k < nch) {
+        float* t = sT[k & 1];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          f4 tv;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (MODE == WALK_DOT) tv[c] = va[q][c] * vb[q][c];
+            else if (MODE == WALK_CHILD) tv[c] = ftz_f(vb[q][c] * ftz_f(va[q][c]));  // (a: L row, b: prediction)
+            else tv[c] = va[q][c];
+          }
+          *(f4*)(t + 4 * lane + 256 * q) = tv;
+        }
+        if (k + 1 < nch) load(k + 1);  // in flight during the next walk
+      }
+      if (CDF && k >= 2)  // chunk k - 2's running sums (written in iteration k - 1)
+        for (int x = lane; x < C && (k - 2) * C + x < n; x += 64) cdf[(k - 2) * C + x] = sS[k & 1][x];
+    } else if (k >= 1 && lane == 0) {
+      // lane 0 walks chunk k - 1: group = 4 terms, read kWalkLA groups ahead
+      // (the last ones into the buffer's slack, unused) with counted waits
+      constexpr int LA = kWalkLA, NB = kWalkNB, W = (CDF ? 2 : 1) * LA;
+      const uint32_t base = (uint32_t)(uintptr_t)sT[(k - 1) & 1];
+      const uint32_t obase = (uint32_t)(uintptr_t)sS[(k - 1) & 1];
+      f4 ring[NB];
+      walk_prologue<0, LA, NB>(ring, base);
+      // (the first NB groups: fewer than LA sums writes behind each read, so
+      // the dot's count; the writes complete too)
+      walk_groups<0, LA, NB, LA, CDF>(ring, base, obase, acc);
+      for (int g0 = NB; g0 < C / 4; g0 += NB)
+        walk_groups<0, LA, NB, W, CDF>(ring, base + 16u * (uint32_t)g0, obase + 16u * (uint32_t)g0, acc);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the sums and reads done before the barrier)
+    }
+    __syncthreads();
+  }
+  if (CDF) {  // the last chunk's running sums
+    const int k = nch - 1;
+    for (int x = tid; x < C && k * C + x < n; x += 128) cdf[k * C + x] = sS[k & 1][x];
+  }
+  if (w == 0 && lane == 0) out[(long long)row * ldo + j] = acc;
 }
 
 // ---------------------------------------------------------------- sampling
@@ -1419,8 +1513,18 @@ hipError_t launch_pair_seq_small(hipStream_t st, int op, const float* A, int na,
   if ((alist == nullptr) != (acount == nullptr) || n <= 0 || ld < n) return hipErrorInvalidValue;
   if (op != PAIR_DOT && op != PAIR_CHILD) return hipErrorInvalidValue;
   const char* env = getenv("PP2_CHAIN_WALK");
+  if (n <= kWalkMax && env && env[0] == '2') {
+    // PP2_CHAIN_WALK=2: the walk with its terms formed beside it (two waves per chain)
+    if (op == PAIR_DOT)
+      hipLaunchKernelGGL(k_chain_walk2<WALK_DOT>, dim3(na * nb), dim3(128), 0, st, A, na, B, nb, ld, n,
+                         out, ldo, alist, acount, nullptr);
+    else
+      hipLaunchKernelGGL(k_chain_walk2<WALK_CHILD>, dim3(na * nb), dim3(128), 0, st, A, na, B, nb, ld,
+                         n, out, ldo, alist, acount, nullptr);
+    return hipGetLastError();
+  }
   if (n <= kWalkMax && !(env && env[0] == '0')) {
-    // one wave per chain, lane 0 walking the chain's terms from LDS
+    // one wave per chain, all terms formed, then lane 0 walks them
     const size_t lds = (size_t)walk_cap(n) * sizeof(float);
     static unsigned long long attr[2] = {0ull, 0ull};
     allow_lds(reinterpret_cast<const void*>(&k_chain_walk<WALK_DOT>), attr[0]);
@@ -1442,6 +1546,11 @@ hipError_t launch_pair_seq_small(hipStream_t st, int op, const float* A, int na,
 hipError_t launch_row_cdf_seq(hipStream_t st, const float* row, int n, float* cdf, float* sum) {
   if (n <= 0 || !row || !cdf || !sum) return hipErrorInvalidValue;
   const char* env = getenv("PP2_CHAIN_WALK");
+  if (n <= kWalkMax && env && env[0] == '2') {
+    hipLaunchKernelGGL(k_chain_walk2<WALK_CDF>, dim3(1), dim3(128), 0, st, row, 1, nullptr, 1, n, n, sum,
+                       0, nullptr, nullptr, cdf);
+    return hipGetLastError();
+  }
   if (n <= kWalkMax && !(env && env[0] == '0')) {
     const size_t lds = 2 * (size_t)walk_cap(n) * sizeof(float);
     static unsigned long long attr = 0ull;

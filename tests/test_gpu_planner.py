@@ -225,19 +225,22 @@ def compare_exact(gi, oi, where):
             assert np.array_equal(a, b), f"{where}: {k} {a} != {b}"
 
 
-@pytest.mark.parametrize("name,max_depth,lb,S,steps,seq_max", [
-    ("map_10x10", 50, 0, 0, 8, None),
-    ("sparse_map_100x40", 50, 0, 0, 6, None),
-    ("sparse_map_100x40", 5, 1, 500, 5, None),    # the reference node: PBVI leaves, S = 500
-    ("tile64_sparse_map_100x40", 8, 1, 64, 6, None),
+@pytest.mark.parametrize("name,max_depth,lb,S,steps,seq_max,walk", [
+    ("map_10x10", 50, 0, 0, 8, None, None),
+    ("sparse_map_100x40", 50, 0, 0, 6, None, None),
+    ("sparse_map_100x40", 5, 1, 500, 5, None, None),    # the reference node: PBVI leaves, S = 500
+    ("tile64_sparse_map_100x40", 8, 1, 64, 6, None, None),
     # the same small grids on the exact parallel chain sets (pp2_fchain.hip)
     # instead of the walked chains (k_chain_walk, the default up to 8192 cells)
-    ("sparse_map_100x40", 50, 0, 0, 6, "0"),
-    ("sparse_map_100x40", 5, 1, 500, 3, "0"),
-    ("tile64_sparse_map_100x40", 8, 1, 64, 4, "0"),
+    ("sparse_map_100x40", 50, 0, 0, 6, "0", None),
+    ("sparse_map_100x40", 5, 1, 500, 3, "0", None),
+    ("tile64_sparse_map_100x40", 8, 1, 64, 4, "0", None),
+    # and on the walk with its terms formed beside it (k_chain_walk2)
+    ("map_10x10", 50, 0, 0, 4, None, "2"),
+    ("sparse_map_100x40", 5, 1, 500, 3, None, "2"),
 ])
 def test_planner_reference_order_bit_exact(oracle, monkeypatch, name, max_depth, lb, S, steps,
-                                           seq_max):
+                                           seq_max, walk):
     """reference_order = 1: rewards, renormalisations and leaf bounds run as
     the reference's own x-ordered fp32 chains (inner_product / accumulate,
     search_tree_cuda.cu:168-173, :225-229; evaluateFibCpu, evaluatePbviCpu),
@@ -247,11 +250,14 @@ def test_planner_reference_order_bit_exact(oracle, monkeypatch, name, max_depth,
     fp64-accumulating mode may legitimately pick another near-tied node.
     Grids up to PP2_SEQ_CHAIN_MAX cells (seq_max; default 8192) run the sums
     as walked chains, larger ones as exact parallel chain sets; seq_max "0"
-    forces the latter on the small grids."""
+    forces the latter on the small grids, walk "2" the walk whose terms are
+    formed beside it (PP2_CHAIN_WALK)."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S_
     if seq_max is not None:
         monkeypatch.setenv("PP2_SEQ_CHAIN_MAX", seq_max)
+    if walk is not None:
+        monkeypatch.setenv("PP2_CHAIN_WALK", walk)
     grid = golden_map(name)
     m = golden("model", name)
     b0 = S_.uniform_belief(grid)
