@@ -10,7 +10,10 @@ resident in HBM before the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size 1024] [--grid G]
 
-For N > 1 launch with torch.distributed.run.  Default (weak scaling): rank r
+For N > 1 launch with torch.distributed.run, or run it directly: without a
+launcher environment `bench.py --gpus N` starts `torch.distributed.run
+--nproc-per-node N bench.py ...` as a child process (the parent imports no
+torch and touches no GPU) and exits with its code.  Default (weak scaling): rank r
 owns rows [r*R, (r+1)*R) of an (N*R) x S grid, S = --size = 1024 and R =
 --shard-rows = 896: a rank's view (its rows plus e = 64 halo rows per side)
 is then 1024 x 1024, one 4-row tile per CU, so every rank runs the
@@ -78,7 +81,7 @@ GAMMA = 0.95
 RCCL_ROUND_US = (10.0, 30.0)     # assumed RCCL small-message round trip over xGMI (not measurable on 1 GPU)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -114,7 +117,10 @@ def parse():
                     help="time the dense-plane kernels as the main loop")
     ap.add_argument("--profile", action="store_true",
                     help="only run warmup+timed steps (for rocprofv3)")
-    return ap.parse_args()
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="ranks join a gloo group, all-reduce one value and rank 0 prints "
+                         "one JSON line; nothing touches a GPU (tests the N > 1 launch)")
+    return ap.parse_args(argv)
 
 
 def dist_env():
@@ -122,6 +128,56 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     return ws, rank, local
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """The torch.distributed.run command that starts this script's n ranks
+    (one process per GPU, rendezvous on 127.0.0.1) with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(argv, n):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start the
+    N-rank job as a CHILD process and return its exit code.  This process
+    never imports torch and never touches a GPU, and it does not exec: the
+    child's stdout is this process's stdout, so rank 0's JSON line is relayed
+    as is."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = launcher_cmd(argv, n, free_port())
+    print(f"bench.py: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launcher_selftest(ws, rank):
+    """--launcher-selftest: the ranks of this job join a gloo process group
+    and all-reduce their rank + 1; rank 0 prints one JSON line."""
+    if os.environ.get("PP2_BENCH_FORCE_FAIL"):  # (tests: the exit code is relayed)
+        raise SystemExit(3)
+    import torch
+    import torch.distributed as dist
+    if ws > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank + 1)])
+    if ws > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launcher_selftest": True, "world_size": ws,
+                          "rank_sum": float(t.item()),
+                          "launched_by": "torch.distributed.run"
+                          if "TORCHELASTIC_RUN_ID" in os.environ else "direct"}), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
 
 
 def pmc_traffic(kernel_substr: str, cells: int, exclude: str | None = None,
@@ -646,6 +702,9 @@ def config4_leg(args, ws, rank, local, stream):
         el = run(ctx, True)
         b = ctx.belief_get()  # collective: global mass all-reduce
         J, A = ctx.mdp_get()
+        # the RCCL rounds of the same call, event-timed on the stream they run
+        # on, in a second (untimed) run continuing from the gathered state
+        rounds = comm_round_stats(ctx, lambda: ctx.loop_run(us[w:], zs[w:]), torch, dist)
         ctx.close()
         bg = _gather_rows(b, r0, r1, G, G, ws, torch, dist)
         Jg = _gather_rows(J, r0, r1, G, G, ws, torch, dist)
@@ -676,6 +735,7 @@ def config4_leg(args, ws, rank, local, stream):
             b_ok = b_rel <= 1e-5 and bool(np.all(np.abs(bg[~bmask]) <= 1e-30))
             out.update({"cells_per_s": v, "ms_per_step": 1e3 * el / k,
                         "speedup_vs_unsharded_1gpu": v / v1,
+                        "rccl_round_us": rounds,
                         "parity": {"J_bit_exact": j_ok, "A_bit_exact": a_ok,
                                    "belief_max_rel_err": b_rel, "belief_ok": b_ok,
                                    "pass": j_ok and a_ok and b_ok}})
@@ -692,6 +752,36 @@ def config4_leg(args, ws, rank, local, stream):
                 out["rank_share_8"] = rank_share
     if ws > 1:
         dist.barrier()
+    return out
+
+
+def comm_round_stats(ctx, call, torch, dist=None):
+    """Run `call` once with PP2_TUNE_COMM_TIMING on: every RCCL round of the
+    context (halo exchange + {mass, shift, lost} records, closing all-reduce)
+    between HIP events on the stream it is issued on.  Per rank: rounds,
+    mean / median / max us; with `dist`, the max over ranks of each figure
+    beside rank 0's own."""
+    ctx.synchronize()
+    ctx.set_tuning(ctx.TUNE_COMM_TIMING, 1)
+    call()
+    us_r, untimed = ctx.comm_rounds()
+    ctx.set_tuning(ctx.TUNE_COMM_TIMING, 0)
+    n = int(us_r.size)
+    mine = [float(n), float(us_r.mean()) if n else 0.0,
+            float(np.median(us_r)) if n else 0.0, float(us_r.max()) if n else 0.0,
+            float(us_r.sum())]
+    out = {"rounds": n, "untimed_rounds": int(untimed), "mean_us": mine[1],
+           "median_us": mine[2], "max_us": mine[3], "total_us": mine[4],
+           "first_us": float(us_r[0]) if n else None,
+           "method": "hipEventRecord before / after each RCCL group on the issuing stream "
+                     "(PP2_TUNE_COMM_TIMING): the group's own time plus any wait for the "
+                     "peers; a second run of the timed call, not inside the timed region"}
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor(mine, dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        m = t.cpu().tolist()
+        out["max_over_ranks"] = {"mean_us": m[1], "median_us": m[2], "max_us": m[3],
+                                 "total_us": m[4]}
     return out
 
 
@@ -727,6 +817,9 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
     l0 = ctx.resident_launches()[0]
     el = run(ctx, False)
     launches = ctx.resident_launches()[0] - l0
+    rounds1 = comm_round_stats(ctx, lambda: ctx.loop_run(us[w:], zs[w:]), torch)
+    rounds1["note"] = ("1-rank communicator: every round is an RCCL no-op group / all-reduce, so "
+                       "this is the issue floor of a round on this GPU, not an xGMI transfer")
     ctx.close()
     t = 1e6 * el / k
     nblk = -(-k // e)
@@ -738,6 +831,7 @@ def config4_rank_share(args, grid, goal, us, zs, b0, local, stream, run):
             "resident_tiling": {"tiles": tiling[0], "rows_per_tile": tiling[1],
                                 "tile_cols": tiling[2]},
             "measured_us_per_step": t,
+            "rccl_round_us_1rank": rounds1,
             "projection_8_ranks": {
                 "assumed_rccl_round_us": list(RCCL_ROUND_US),
                 "rccl_rounds_per_call": rounds,
@@ -831,9 +925,14 @@ def cpu_model():
 def main():
     args = parse()
     ws, rank, local = dist_env()
-    if ws != args.gpus and not (ws == 1 and args.gpus == 1):
-        if ws == 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher environment: start the N-rank job as a child process
+        return launch_ranks(sys.argv[1:], args.gpus)
+    if ws != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {ws}")
+    if args.launcher_selftest:
+        launcher_selftest(ws, rank)
+        return 0
     import torch
     import torch.distributed as dist
     import path_planning_2d_amd as P
@@ -996,18 +1095,6 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # the same launch between HIP events (untimed; b and J continue from the
-    # timed steps, which changes neither the work nor its bytes)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    ev0.record(stream)
-    run_timed()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    loop_ms_events = ev0.elapsed_time(ev1) / args.steps
     if ws > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1028,6 +1115,22 @@ def main():
         if ws > 1:
             dist.destroy_process_group()
         return
+
+    # the same launch between HIP events (untimed; b and J continue from the
+    # timed steps, which changes neither the work nor its bytes; skipped with
+    # --profile, so a profile holds the timed region's launches only)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    ev0.record(stream)
+    run_timed()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    loop_ms_events = ev0.elapsed_time(ev1) / args.steps
+    # N > 1: the timed call's RCCL rounds, event-timed in one more run
+    head_rounds = comm_round_stats(ctx, run_timed, torch, dist) if ws > 1 else None
 
     # the resident kernel's duration per launch for the roofline: launches of
     # the timed region's length back to back, so the host enqueue of one
@@ -1185,6 +1288,7 @@ def main():
                 "bytes_per_cell": lds_bytes} if coded else None),
             "sweep_resident_traffic": sweep_resident_traffic(cells_per_gpu),
             "dense_path": dense,
+            "rccl_round_us": head_rounds,
             "config4": c4,
             "weak_rank_share": weak,
             "kernels": {
@@ -1229,4 +1333,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -200,7 +200,20 @@ int pp2_set_cells_per_lane(pp2_ctx* ctx, int cpt);
  *                           re-run of a failed resident launch */
 #define PP2_TUNE_RESIDENT_CUS 10
 #define PP2_TUNE_RESIDENT_STALL 11
+/*  PP2_TUNE_COMM_TIMING     1 = bracket every RCCL round of the context (halo
+ *                           exchanges, record groups, all-reduces) with timing
+ *                           events on the stream it runs on; read with
+ *                           pp2_comm_rounds.  0 (default) = no events. */
+#define PP2_TUNE_COMM_TIMING 14
 int pp2_set_tuning(pp2_ctx* ctx, int key, int value);
+/* Measurement, no reference counterpart (the reference is single-GPU): the
+ * RCCL rounds timed since PP2_TUNE_COMM_TIMING was set or the last call --
+ * `rounds` timed rounds (at most 256 between calls; later ones are counted in
+ * `untimed`, which may be NULL), the first max_rounds of their durations in
+ * microseconds (begin event to end event on the issuing stream: the group's
+ * own time plus any wait for the peers).  Synchronises; clears the record. */
+int pp2_comm_rounds(pp2_ctx* ctx, int* rounds, long long* untimed, float* round_us,
+                    int max_rounds);
 
 /* ---------------------------------------------------------------- model
  * generateModelData (src/pomdp/model_generation_cuda.cu:349-368) and the MDP

@@ -53,6 +53,7 @@ SIGNATURES = {
     "pp2_get_geometry": [_vp, _u32p, _u32p, _u32p, _u32p],
     "pp2_set_cells_per_lane": [_vp, C.c_int],
     "pp2_set_tuning": [_vp, C.c_int, C.c_int],
+    "pp2_comm_rounds": [_vp, C.POINTER(C.c_int), C.POINTER(C.c_longlong), _f32p, C.c_int],
     "pp2_model_generate": [_vp],
     "pp2_model_download": [_vp, _f32p, _f32p, _f32p, _f32p],
     "pp2_model_upload": [_vp, _f32p, _f32p, _f32p, _f32p],

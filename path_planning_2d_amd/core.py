@@ -107,9 +107,21 @@ class GridContext:
     TUNE_RESIDENT_STALL = 11
     TUNE_RESIDENT_TILE_COLS = 12
     TUNE_SHARD_LAG = 13
+    TUNE_COMM_TIMING = 14
 
     def set_tuning(self, key: int, value: int):
         call("pp2_set_tuning", self._h, int(key), int(value))
+
+    def comm_rounds(self, max_rounds: int = 256):
+        """The RCCL rounds timed since TUNE_COMM_TIMING was set or the last
+        call (pp2_comm_rounds): (durations in us as a float32 array, rounds
+        beyond the 256 timed ones).  Synchronises; clears the record."""
+        n = C.c_int(0)
+        dropped = C.c_longlong(0)
+        buf = np.zeros(max(1, max_rounds), np.float32)
+        call("pp2_comm_rounds", self._h, C.byref(n), C.byref(dropped), _f32(buf),
+             int(max_rounds))
+        return buf[:min(n.value, max_rounds)].copy(), dropped.value
 
     # ------------------------------------------------------------ model
     def model_generate(self):

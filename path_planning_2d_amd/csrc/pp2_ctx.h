@@ -211,6 +211,13 @@ struct pp2_ctx {
   hipStream_t comm_stream = nullptr;  // RCCL operations when use_comm_stream (PP2_TUNE_COMM_STREAM)
   bool use_comm_stream = false;
   hipEvent_t ev_enter = nullptr, ev_leave = nullptr;
+  // PP2_TUNE_COMM_TIMING: every RCCL round bracketed by timing events on the
+  // stream it runs on (pp2_comm_rounds reads and clears them)
+  static constexpr int kCommTimed = 256;
+  bool comm_timing = false, comm_open = false;
+  std::vector<hipEvent_t> comm_ev;  // 2 * kCommTimed (begin, end) pairs, made on demand
+  int comm_nev = 0;                 // rounds recorded since the last pp2_comm_rounds
+  long long comm_dropped = 0;       // rounds beyond kCommTimed (not timed)
   pp2_shard_group* group = nullptr;  // single-process shard group, if any
   int grank = 0;                     // rank (row-block order) inside the group
   int group_size = 0;                // shards in the group

@@ -146,8 +146,25 @@ __device__ __forceinline__ void dma16(const void* g, void* l) {
 // of 12 (512^2 x 4096 x 5: 5.34 vs 5.46-5.69 ms, profiles/r05/ab_rollout_dma16.txt).
 template <int CH, bool W16>
 struct Slot {
+  // (W16 stages two copies' rows per 16-B instruction: an odd CH would leave
+  // the last copy's rows unstaged)
+  static_assert(!W16 || CH % 2 == 0, "16-B belief staging needs an even copy count");
   static constexpr int code = CH * 512, r = code + 512, edge = r + 1024, bytes = edge + 256;
   static constexpr int groups = W16 ? CH / 2 + 3 : 2 * CH + 4;  // DMA instructions per row
+};
+
+// Ring budget of a band build (kBandSlots = NS): every row of a wave's ring
+// travels as one DMA group of G instructions into its own slot, and band()
+// waits on hand-counted vmcnt values of up to (NS - 2) (G + CH) (the younger
+// groups plus the stores of the phases between), which must fit the 6-bit
+// counter; the 4 waves' rings of WPS workgroups must fit one CU's 160 KB of
+// LDS beside the dictionary tables (the launch checks the dynamic part).
+template <int CH, int NS, int WPS, bool W16>
+struct RingBudget {
+  static_assert(NS >= 3, "the window needs rows y-1, y, y+1 resident plus one in flight");
+  static_assert((NS - 2) * (Slot<CH, W16>::groups + CH) < 64, "vmcnt wait exceeds 6 bits");
+  static constexpr int ring_bytes = 4 * NS * Slot<CH, W16>::bytes;
+  static_assert(WPS * ring_bytes <= 160 * 1024, "rings of WPS workgroups exceed the CU's LDS");
 };
 
 // One wave's band: rows [ya, yb) of the segment starting at xs.
@@ -165,6 +182,7 @@ __device__ __forceinline__ void band(const BandArgs& a, const float* sTu, const 
                                      const int (&zc)[CH], const float (&inv)[CH], int u, int ya,
                                      int yb, int xs, int lane, float (&acc)[CH][kRollStats]) {
   using SL_ = Slot<CH, W16>;
+  static_assert(sizeof(RingBudget<CH, NS, 1, W16>) > 0, "");
   constexpr int NT = n_terms<SRC, U>();
   constexpr int TW = tu_width(SRC == kSparse);
   constexpr int G = SL_::groups;
@@ -401,6 +419,7 @@ __global__ __launch_bounds__(kBlock, WPS) void k_rollout_band(
     const int* __restrict__ copies, const uint8_t* __restrict__ zs,
     const float* __restrict__ in_stats) {
   constexpr int TW = tu_width(SRC == kSparse);
+  static_assert(sizeof(RingBudget<CH, NS, WPS, W16>) > 0, "");
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int ch = lin / gx, bx = lin % gx;
   const int u = chunk_u[ch], first = chunk_first[ch];
@@ -516,6 +535,10 @@ hipError_t launch_rollout_step(hipStream_t st, const Geom& g, PlaneSet T, PlaneS
   if (nblocks <= 0) return hipSuccess;
   const int CH = rollout_chunk();
   const size_t lds = E > 0 ? (size_t)(((E * tw + 3) & ~3) + CH * E) * sizeof(float) : 0;
+  // the rings (static) and the tables (dynamic) of one workgroup must fit
+  // the CU's LDS; the tables of kDictMax entries always do with 4 slots
+  if (lds + (size_t)RingBudget<kBandCopies, kBandSlots, 1, true>::ring_bytes > 160 * 1024)
+    return hipErrorInvalidValue;
 #define PP2_BAND(CC, PP, WW, W16)                                                                 \
   do {                                                                                            \
     static unsigned long long attr[3] = {0, 0, 0};                                                \

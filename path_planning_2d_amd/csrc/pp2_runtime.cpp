@@ -111,14 +111,41 @@ const Planes& halo_planes(pp2_ctx* c, HaloKind k) {
 // dedicated comm stream, entered and left through events.
 hipStream_t cst(const pp2_ctx* c) { return c->use_comm_stream ? c->comm_stream : c->stream; }
 
-int comm_enter(pp2_ctx* c) {
-  if (!c->use_comm_stream) return PP2_OK;
-  HIPCHK(hipEventRecord(c->ev_enter, c->stream));
-  HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_enter, 0));
+// With PP2_TUNE_COMM_TIMING, a round's begin event is recorded on cst(c)
+// after the enter hand-off and its end event before the leave hand-off, so
+// the pair brackets the RCCL group alone (including the wait for the peers).
+static int comm_time_mark(pp2_ctx* c, bool begin) {
+  if (!c->comm_timing || !c->comm) return PP2_OK;
+  if (begin) {
+    c->comm_open = c->comm_nev < pp2_ctx::kCommTimed;
+    if (!c->comm_open) {
+      ++c->comm_dropped;
+      return PP2_OK;
+    }
+    if (c->comm_ev.empty()) {
+      c->comm_ev.assign(2 * pp2_ctx::kCommTimed, nullptr);
+      for (hipEvent_t& e : c->comm_ev) HIPCHK(hipEventCreate(&e));
+    }
+    HIPCHK(hipEventRecord(c->comm_ev[2 * c->comm_nev], cst(c)));
+    return PP2_OK;
+  }
+  if (!c->comm_open) return PP2_OK;
+  HIPCHK(hipEventRecord(c->comm_ev[2 * c->comm_nev + 1], cst(c)));
+  ++c->comm_nev;
+  c->comm_open = false;
   return PP2_OK;
 }
 
+int comm_enter(pp2_ctx* c) {
+  if (c->use_comm_stream) {
+    HIPCHK(hipEventRecord(c->ev_enter, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_enter, 0));
+  }
+  return comm_time_mark(c, true);
+}
+
 int comm_leave(pp2_ctx* c) {
+  CHECK(comm_time_mark(c, false));
   if (!c->use_comm_stream) return PP2_OK;
   HIPCHK(hipEventRecord(c->ev_leave, c->comm_stream));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_leave, 0));
@@ -1596,6 +1623,24 @@ int pp2_debug_context_bytes(pp2_ctx* c, unsigned long long* bytes) {
   return PP2_OK;
 }
 
+int pp2_comm_rounds(pp2_ctx* c, int* rounds, long long* untimed, float* round_us,
+                    int max_rounds) {
+  CHECK(check_ctx_settled(c));
+  if (!rounds) return set_err(PP2_EINVAL, "rounds is null");
+  if (max_rounds > 0 && !round_us) return set_err(PP2_EINVAL, "round_us is null");
+  DeviceGuard dg(c->device);
+  if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *rounds = c->comm_nev;
+  if (untimed) *untimed = c->comm_dropped;
+  for (int i = 0; i < c->comm_nev && i < max_rounds; ++i)
+    HIPCHK(hipEventElapsedTime(&round_us[i], c->comm_ev[2 * i], c->comm_ev[2 * i + 1]));
+  for (int i = 0; i < c->comm_nev && i < max_rounds; ++i) round_us[i] *= 1e3f;
+  c->comm_nev = 0;
+  c->comm_dropped = 0;
+  return PP2_OK;
+}
+
 int pp2_device_count(int* count) {
   if (!count) return set_err(PP2_EINVAL, "count is null");
   *count = 0;
@@ -1627,6 +1672,8 @@ int pp2_destroy(pp2_ctx* c) {
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (hipEvent_t e : {c->ev_enter, c->ev_leave})
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->comm_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
   for (Planes* P : {&c->T, &c->L, &c->R, &c->C, &c->b[0], &c->b[1], &c->J[0],
@@ -1679,7 +1726,9 @@ int pp2_get_geometry(pp2_ctx* c, uint32_t* rows, uint32_t* width,
 
 int pp2_set_tuning(pp2_ctx* c, int key, int value) {
   CHECK(check_ctx_settled(c));
-  ++c->agree_gen;  // a shard's resident eligibility may change: agree again
+  // a shard's resident eligibility may change: agree again (not for the
+  // measurement knob, which changes nothing the ranks agree on)
+  if (key != PP2_TUNE_COMM_TIMING) ++c->agree_gen;
   switch (key) {
     case PP2_TUNE_CELLS_PER_LANE: return pp2_set_cells_per_lane(c, value);
     case PP2_TUNE_NT_STREAMS: c->nt_streams = value != 0; return PP2_OK;
@@ -1727,6 +1776,13 @@ int pp2_set_tuning(pp2_ctx* c, int key, int value) {
       if (c->comm_stream) HIPCHK(hipStreamSynchronize(c->comm_stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       c->use_comm_stream = value != 0;
+      return PP2_OK;
+    case PP2_TUNE_COMM_TIMING:
+      if (value < 0 || value > 1) return set_err(PP2_EINVAL, "comm timing %d not in [0, 1]", value);
+      c->comm_timing = value != 0;
+      c->comm_nev = 0;
+      c->comm_dropped = 0;
+      c->comm_open = false;
       return PP2_OK;
     case PP2_TUNE_HALO_DEPTH:
       if (value < 1 || value > c->kdepth_max)
@@ -1813,7 +1869,29 @@ int pp2_model_upload(pp2_ctx* c, const float* T, const float* L, const float* R,
   if (R) CHECK(upload_planes(c, c->R, R));
   if (C) CHECK(upload_planes(c, c->C, C));
   c->model_ready = true;
-  return build_model_dict(c);
+  if (c->dense_halo >= c->g.halo) return build_model_dict(c);
+  // A whole-grid shard context (rows == grows, its own RCCL rank or none):
+  // its dense planes hold dense_halo < g.halo halo rows, but the dictionary
+  // build walks rows [-g.halo, rows + g.halo).  Build it from transient
+  // full-halo copies: rows [-dense_halo, rows + dense_halo) from the context,
+  // the rest zero -- the off-grid rows, which is what they are here.
+  Planes t[4];
+  struct Free {
+    Planes* t;
+    ~Free() { for (int i = 0; i < 4; ++i) free_planes(&t[i]); }
+  } fr{t};
+  Planes* src[4] = {&c->T, &c->L, &c->R, &c->C};
+  const int dh = c->dense_halo;
+  for (int i = 0; i < 4; ++i) {
+    CHECK(alloc_planes(c, &t[i], src[i]->K, c->g.halo));
+    HIPCHK(hipMemcpyAsync(t[i].v.p - (long long)dh * t[i].v.rs,
+                          src[i]->v.p - (long long)dh * src[i]->v.rs,
+                          (size_t)(c->g.rows + 2 * dh) * t[i].v.rs * sizeof(float),
+                          hipMemcpyDeviceToDevice, c->stream));
+  }
+  const int s = build_model_dict(c, &t[0], &t[1], &t[2], &t[3]);
+  HIPCHK(hipStreamSynchronize(c->stream));  // (before the transient planes go)
+  return s;
 }
 
 int pp2_model_save(pp2_ctx* c, const char* dir) {

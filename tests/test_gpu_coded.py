@@ -11,7 +11,7 @@ path's parity (test_gpu_parity.py), and is re-checked here against the oracle.
 import numpy as np
 import pytest
 
-from conftest import GAMMA, golden, golden_map
+from conftest import GAMMA, assert_rel_close, golden, golden_map
 
 pytestmark = pytest.mark.gpu
 
@@ -197,6 +197,41 @@ def test_irregular_model_falls_back_to_dense(pp2):
         ctx.model_upload(T1, L, R, Cc)
         e1, act = ctx.model_dict_info()
         assert act and e1 == e0 + 1
+
+
+def test_model_upload_on_whole_grid_shard(pp2):
+    """pp2_model_upload on a rows=(0, H) shard context (round-5 ADVICE): its
+    dense planes keep only kDenseHalo halo rows while the dictionary build
+    walks the deep shard halo, so the upload builds the dictionary from a
+    transient full-halo copy.  The shard's coded dictionary equals the
+    unsharded context's, and an uploaded (perturbed) model runs the same
+    loop steps bit for bit on both."""
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(96, 128, 5)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 6, seed=3)
+    b0 = S.uniform_belief(grid)
+    with pp2.GridContext(grid, goal, gamma=float(GAMMA)) as ref, \
+            pp2.GridContext(grid, goal, gamma=float(GAMMA), rows=(0, grid.shape[0])) as sh:
+        sh.shard_comm_init(pp2.GridContext.rccl_unique_id(), 1, 0)
+        ref.model_generate()
+        T, L, R, Cc = ref.model_download()
+        T1 = T.copy()
+        T1[5 * 128 + 7, 4, 4] = np.float32(0.5)  # one more dictionary entry
+        for c in (ref, sh):
+            c.model_upload(T1, L, R, Cc)
+        assert sh.model_dict_info() == ref.model_dict_info()
+        assert ref.model_dict_info()[1]
+        for c in (ref, sh):
+            c.belief_set(b0)
+            c.mdp_reset()
+        for k in range(6):
+            ref.loop_step(int(us[k]), int(zs[k]))
+            sh.loop_step(int(us[k]), int(zs[k]))
+        np.testing.assert_array_equal(sh.mdp_get()[0], ref.mdp_get()[0])
+        np.testing.assert_array_equal(sh.mdp_get()[1], ref.mdp_get()[1])
+        assert_rel_close(sh.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=1e-30,
+                         msg="belief on the uploaded model")
 
 
 def test_off_support_model_uses_full_rows(pp2):

@@ -73,6 +73,54 @@ def test_config4_2048_eight_row_shards():
     run_pair(P, grid, goal, tuple(range(0, N + 1, N // 8)), steps=4)
 
 
+@pytest.mark.parametrize("resident", [0, 1])
+def test_config4_2048_eight_row_shards_vs_oracle(oracle, resident):
+    """The same 8-shard group against the CPU oracle itself (not the
+    unsharded HIP context): the reference loop -- cudaBayesBeliefUpdate +
+    host renormalisation (point_based_value_iteration_cuda.cu:88-133,
+    search_tree_cuda.cu:225-229), then cudaOneStepValueIteration
+    (mdp/path_planning_2d_cuda.cu:215-264) -- as orc_loop_run_mt, rows over
+    the host threads, 8 steps on the 2048^2 grid.  Values and actions bit
+    for bit, the belief rel 1e-5 above the FTZ floor.  resident 1: the
+    shards run the resident kernel on their 384-row views (the 8-GPU job's
+    default path); 0: step pairs / single steps."""
+    import os
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    O = oracle
+    N = 2048
+    steps = 8
+    grid = S.synth_grid(N, N, N)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, steps, seed=42)
+    T, L, _ = O.model_pomdp(grid, goal)
+    _, Cc = O.model_mdp(grid, goal)
+    b = S.uniform_belief(grid).astype(np.float32).reshape(-1)
+    bo = np.empty_like(b)
+    J = np.zeros(N * N, np.float32)
+    Jo = np.empty_like(J)
+    A = np.zeros(N * N, np.uint8)
+    nt = max(1, min(16, len(os.sched_getaffinity(0))))
+    assert O.lib().orc_loop_run_mt(N, N, np.float32(GAMMA), T, L, Cc, b, bo, J, Jo, A, steps,
+                                   np.ascontiguousarray(us, np.uint8),
+                                   np.ascontiguousarray(zs, np.uint8), nt) == steps
+    # (an even step count leaves the results in b and J)
+    with P.ShardGroup(grid, goal, tuple(range(0, N + 1, N // 8)), gamma=float(GAMMA)) as grp:
+        grp.model_generate()
+        grp.set_tuning(P.GridContext.TUNE_RESIDENT, resident)
+        grp.belief_set(S.uniform_belief(grid))
+        grp.mdp_reset()
+        grp.loop_run(us, zs)
+        if resident:
+            assert grp.shards[0].resident_launches()[0] >= 1
+        Jg, Ag = grp.mdp_get()
+        bg = grp.belief_get()
+    np.testing.assert_array_equal(Jg.reshape(-1).view(np.uint32), J.view(np.uint32))
+    np.testing.assert_array_equal(Ag.reshape(-1), A)
+    assert_rel_close(bg.reshape(-1), b, rel=1e-5, abs_floor=FTZ_FLOOR,
+                     msg="8-shard belief vs the oracle")
+
+
 def test_config4_shard_group_memory():
     """The 2048^2 grid in 8 row shards allocates <= 10 % above the unsharded
     context (round-4 ADVICE): a shard's deep halo (kShardHalo rows per side,
@@ -435,6 +483,46 @@ def test_rccl_single_rank_resident_896x1024():
         assert_rel_close(sh.belief_get(), ref.belief_get(), rel=1e-5, abs_floor=FTZ_FLOOR,
                          msg="belief after 200 steps")
         assert sh.resident_launches()[0] == 4
+
+
+def test_comm_round_timing_single_rank():
+    """PP2_TUNE_COMM_TIMING / pp2_comm_rounds on the config-4 rank share with
+    a 1-rank communicator: one timed round per resident block (its halo
+    exchange, with the {mass, shift, lost} records after the first) plus the
+    closing all-reduce; durations positive; the record clears on read; no
+    events without the knob; results unchanged."""
+    import path_planning_2d_amd as P
+    from path_planning_2d_amd import synthetic as S
+    grid = S.synth_grid(256, 2048, 256)
+    goal = S.synth_goal(grid)
+    us, zs, _ = S.synth_trajectory(grid, 150, seed=8)
+    b0 = S.uniform_belief(grid)
+    with P.GridContext(grid, goal, gamma=float(GAMMA), rows=(0, 256)) as sh, \
+            P.GridContext(grid, goal, gamma=float(GAMMA), rows=(0, 256)) as sh2:
+        for c in (sh, sh2):
+            c.shard_comm_init(P.GridContext.rccl_unique_id(), 1, 0)
+            c.model_generate()
+            c.belief_set(b0)
+            c.mdp_reset()
+        e = sh.loop_steps_per_launch()
+        sh.loop_run(us[:10], zs[:10])  # (agreement on e happens here)
+        sh2.loop_run(us[:10], zs[:10])
+        sh.set_tuning(sh.TUNE_COMM_TIMING, 1)
+        sh.loop_run(us[10:], zs[10:])
+        sh2.loop_run(us[10:], zs[10:])
+        t, untimed = sh.comm_rounds()
+        assert untimed == 0
+        nblk = -(-140 // e)
+        assert nblk + 1 <= t.size <= nblk + 2, (t, e)
+        assert (t > 0).all() and (t < 1e5).all(), t
+        assert sh.comm_rounds()[0].size == 0  # cleared
+        sh.set_tuning(sh.TUNE_COMM_TIMING, 0)
+        sh.loop_run(us[:5], zs[:5])
+        sh2.loop_run(us[:5], zs[:5])
+        assert sh.comm_rounds()[0].size == 0
+        np.testing.assert_array_equal(sh.mdp_get()[0].view(np.uint32),
+                                      sh2.mdp_get()[0].view(np.uint32))
+        np.testing.assert_array_equal(sh.belief_get(), sh2.belief_get())
 
 
 @pytest.mark.parametrize("tiling", [0, 3])
