@@ -654,6 +654,398 @@ __global__ __launch_bounds__(256) void k_store_kept(const int* __restrict__ klis
   dst[(long long)c * ld + x] = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
 }
 
+// ================================================================ fused chain sets
+// (round 6) A chain set as ONE launch: one workgroup of 1024 threads per
+// chain of n <= 1024 C cells (C = 16, 32 or 64 terms per thread; 256^2 takes
+// C = 64), the chain's |terms| held in registers from the first pass to the
+// last --
+//   A  thread t forms the C consecutive terms of chunk t (cells [C t, C t +
+//      C)), keeps |t|, its approximate chunk sum and the sign flags;
+//   B  a workgroup scan of the approximate sums: the approximate running sum
+//      before each chunk;
+//   C  each chunk's table entry (binade E of that running sum, the chunk's
+//      integer increment d in E) and whether the walk will likely fall back
+//      there -- those chunks' |terms| go to an LDS stash;
+//   D  wave 0 walks the entries 64 at a time with the exact state (E, k) and
+//      adds each fallback chunk term by term, one fp32 add per term (the
+//      reference's own chain), from the stash or from the terms formed again;
+// and, for the expanded belief (k_fx_cdf_sample), every running sum from its
+// chunk's exact start state, then forwardSampling's 9 x N draws on them.  The
+// three launches of a k_fc_* set (sums, tables, drive: ~70-80 us on the 256^2
+// plan step's critical path, profiles/r05 kernel_stats_plan_*) become one.
+constexpr int kFxThreads = 1024;
+constexpr int kFxStash = 32;  // predicted fallback chunks whose |terms| wave 0 reads from LDS
+
+// inclusive float scan of a wave (any association: approximate running sums)
+__device__ __forceinline__ float wave_incl_scan_f(float v, int lane) {
+  int b = __builtin_bit_cast(int, v);
+#pragma unroll
+  for (int c = 1; c < 16; c <<= 1)
+    b = __builtin_bit_cast(int, __builtin_bit_cast(float, b) +
+                                    __builtin_bit_cast(float, row_shr(b, c)));
+  const float f = __builtin_bit_cast(float, b);
+  const float r0 = rdl(f, 15), r1 = rdl(f, 31), r2 = rdl(f, 47);
+  const int row = lane >> 4;
+  return f + (row >= 1 ? r0 : 0.0f) + (row >= 2 ? r1 : 0.0f) + (row >= 3 ? r2 : 0.0f);
+}
+
+__device__ __forceinline__ bool fx_group(const FxArgs& a, int g, int* id) {
+  if (g >= a.ngroups) return false;
+  if (a.gcount && g >= *a.gcount) return false;
+  *id = a.glist ? a.glist[g] : a.g0 + g;
+  return true;
+}
+
+// The terms of one chain (group id, partner i):
+//   FX_ROW    row[id][x] (K = 9: * partners[i][x], the host's product)
+//   FX_CHILD  fl_ftz(pred[id % 9][x] * fl_ftz(L[id / 9][x])) -- the
+//             unnormalised child (cudaBayesBeliefUpdate's last product)
+//   FX_KEPT   the normalised child b[x] = that / sums[id] (search_tree_cuda.cu:
+//             228-229), times partners[i][x] (evaluateFibCpu's product)
+// the same per-cell operations as k_fc_* (Terms) and k_store_kept.
+template <int SRC, int K>
+struct FxTerms {
+  const float* __restrict__ pr;
+  const float* __restrict__ lr;
+  const float* __restrict__ al;
+  float mass;
+  int n;
+
+  __device__ __forceinline__ void init(const FxArgs& a, int id, int i) {
+    n = a.n;
+    al = K > 0 ? a.partners + (long long)i * a.ld : nullptr;
+    if (SRC == FX_ROW) {
+      pr = a.row + (long long)id * a.row_stride;
+      lr = nullptr;
+      mass = 1.0f;
+    } else {
+      pr = a.pred + (long long)(id % 9) * a.ld;
+      lr = a.lrows + (long long)(id / 9) * a.ld;
+      mass = SRC == FX_KEPT ? a.sums[id] : 1.0f;
+    }
+  }
+  // the base value (FX_KEPT: the normalised child) of one cell
+  __device__ __forceinline__ float base1(float p, float l) const {
+    if (SRC == FX_ROW) return p;
+    const float v = ftz(p * ftz(l));
+    return SRC == FX_KEPT ? v / mass : v;
+  }
+  __device__ __forceinline__ float term1(float b, float w) const { return K > 0 ? b * w : b; }
+  // the term of cell x (0 at or past n): the walker's reload
+  __device__ __forceinline__ float at(int x) const {
+    if (x >= n) return 0.0f;
+    return term1(base1(pr[x], SRC == FX_ROW ? 0.0f : lr[x]), K > 0 ? al[x] : 0.0f);
+  }
+  // 4 cells from x0 (x0 + 4 <= the row stride): the bases (FX_KEPT's stored
+  // rows) and the terms, 0 past n
+  __device__ __forceinline__ void at4(int x0, float (&b)[4], float (&t)[4]) const {
+    const f4a p = *reinterpret_cast<const f4a*>(pr + x0);
+    f4a l = {0.0f, 0.0f, 0.0f, 0.0f}, w = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (SRC != FX_ROW) l = *reinterpret_cast<const f4a*>(lr + x0);
+    if (K > 0) w = *reinterpret_cast<const f4a*>(al + x0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      b[q] = x0 + q < n ? base1(p[q], l[q]) : 0.0f;
+      t[q] = x0 + q < n ? term1(b[q], w[q]) : 0.0f;
+    }
+  }
+};
+
+// Shared state of one chain's workgroup.
+template <int C>
+struct FxShared {
+  uint32_t e[kFxThreads];      // chunk entries (kNoEntry: none)
+  int slot[kFxThreads];        // the chunk's stash slot, or -1
+  float start[kFxThreads];     // the chunk's exact start value (running sums)
+  float end[kFxThreads];       // the chunk's last running sum (sampling)
+  __attribute__((aligned(16))) float st[kFxStash][C];
+  float wsum[16];
+  uint32_t flag;
+  int nst;
+  float res;
+};
+
+// Phases A-D of one chain (every thread of the workgroup calls it; returns
+// with the workgroup synchronised, the result in S.res (wave 0 wrote it) and,
+// with RUN, every chunk's exact start value in S.start).  a[] keeps the
+// thread's |terms|; *pf the chain's sign flags.
+template <int SRC, int K, int C, bool RUN>
+__device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& T, float (&av)[C],
+                                        FxShared<C>& S, uint32_t* pf, int id, int i) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = a.n, nch = (n + C - 1) / C;
+  const int x0 = C * tid;
+  if (tid == 0) {
+    S.flag = 0u;
+    S.nst = 0;
+  }
+  // A: the terms, |terms|, flags, the approximate chunk sum
+  uint32_t fl = 0u;
+  float csum = 0.0f;
+  {
+    float* __restrict__ store = nullptr;  // FX_KEPT, partner 0: the child's row(s)
+    float* __restrict__ store2 = nullptr;
+    if (SRC == FX_KEPT && i == 0) {
+      store = a.rows_out ? a.rows_out + (long long)id * a.ld : nullptr;
+      store2 = a.use_dst ? a.dst[id] : nullptr;
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < C / 4; ++q4) {
+      float b[4] = {0.0f, 0.0f, 0.0f, 0.0f}, t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (x0 < n) T.at4(x0 + 4 * q4, b, t);
+      if (SRC == FX_KEPT && x0 < n) {
+        if (store) *reinterpret_cast<f4a*>(store + x0 + 4 * q4) = f4a{b[0], b[1], b[2], b[3]};
+        if (store2) *reinterpret_cast<f4a*>(store2 + x0 + 4 * q4) = f4a{b[0], b[1], b[2], b[3]};
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v = t[q];
+        fl |= !isfinite(v) ? kBad : v > 0.0f ? kPos : v < 0.0f ? kNeg : 0u;
+        av[4 * q4 + q] = fabsf(v);
+        csum += fabsf(v);
+      }
+    }
+  }
+  {
+    const uint32_t f = (__ballot((fl & kPos) != 0u) ? kPos : 0u) |
+                       (__ballot((fl & kNeg) != 0u) ? kNeg : 0u) |
+                       (__ballot((fl & kBad) != 0u) ? kBad : 0u);
+    __syncthreads();  // (S.flag, S.nst initialised)
+    if (lane == 0 && f) atomicOr(&S.flag, f);
+  }
+  // B: the approximate running sum before the chunk
+  const float incl = wave_incl_scan_f(csum, lane);
+  if (lane == 63) S.wsum[w] = incl;
+  __syncthreads();
+  const uint32_t f = S.flag;
+  *pf = f;
+  const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
+  float before = incl - csum;
+  for (int v = 0; v < w; ++v) before += S.wsum[v];
+  // C: the chunk's entry, and the predicted fallbacks' stash
+  if (tid < nch) {
+    uint32_t e = kNoEntry;
+    bool pred = true;
+    if (!seq_all) {
+      const int E = domain_of(before);
+      int d = 0;
+      bool tie = false;
+#pragma unroll
+      for (int q = 0; q < C; ++q) {
+        bool tx;
+        const float r = units_of(av[q], E, &tx);
+        d += (int)fminf(r, (float)(kK24 + 1));
+        tie = tie || tx;
+      }
+      if (!tie && d < kK24 && E <= 127) e = ((uint32_t)(E + 128) << 24) | (uint32_t)d;
+      const float pu = ldexpf(before, 23 - E);  // the running sum in units of E
+      pred = e == kNoEntry || tid == 0 || pu + (float)d >= (float)kK24 * (1.0f - 0x1p-12f) ||
+             pu < (float)(1 << 23) * (1.0f + 0x1p-10f);
+    }
+    S.e[tid] = e;
+    int s = -1;
+    if (pred && !seq_all) {
+      s = atomicAdd(&S.nst, 1);
+      if (s < kFxStash) {
+#pragma unroll
+        for (int q4 = 0; q4 < C / 4; ++q4)
+          *reinterpret_cast<f4a*>(&S.st[s][4 * q4]) =
+              f4a{av[4 * q4], av[4 * q4 + 1], av[4 * q4 + 2], av[4 * q4 + 3]};
+      } else {
+        s = -1;
+      }
+    }
+    S.slot[tid] = s;
+  }
+  __syncthreads();
+  // D: wave 0 walks
+  if (w == 0) {
+    float res;
+    if (seq_all) {
+      // mixed signs or a non-finite term: the reference's chain itself, the
+      // next chunk's terms loaded while this one's are added
+      float s = 0.0f;
+      float tn = lane < C ? T.at(lane) : 0.0f;
+      for (int j = 0; j < nch; ++j) {
+        const float tl = tn;
+        if (j + 1 < nch) tn = lane < C ? T.at(C * (j + 1) + lane) : 0.0f;
+        if (RUN && lane == 0) S.start[j] = s;
+#pragma unroll
+        for (int q = 0; q < C; ++q) s = s + rdl(tl, q);
+      }
+      res = s;
+    } else {
+      const bool neg = (f & kNeg) && !(f & kPos);
+      int E = kEMin, k = 0, j = 0;
+      while (j < nch) {
+        const int jj = j + lane;
+        const uint32_t e = jj < nch ? S.e[jj] : kNoEntry;
+        const bool valid = e != kNoEntry && entry_domain(e) == E;
+        const int dl = valid ? entry_units(e) : 0;
+        const int inc = wave_incl_scan(dl, lane);
+        const bool ok = valid && k + inc <= kK24;
+        const uint64_t badm = ~__ballot(ok);
+        const int fc = badm == 0ull ? 64 : __builtin_ctzll(badm);
+        if (RUN && lane < fc && jj < nch) S.start[jj] = value_of(E, k + inc - dl);
+        if (fc > 0) {
+          k += rdl(inc, fc - 1);
+          normalise(&E, &k);
+        }
+        j += fc;
+        if (j < nch && fc < 64) {
+          // chunk j term by term, one fp32 add per term
+          const int sl = S.slot[j];
+          const float tl = lane < C ? (sl >= 0 ? S.st[sl][lane] : fabsf(T.at(C * j + lane))) : 0.0f;
+          float s = value_of(E, k);
+          if (RUN && lane == 0) S.start[j] = s;
+#pragma unroll
+          for (int q = 0; q < C; ++q) s = s + rdl(tl, q);
+          state_of(s, &E, &k);
+          normalise(&E, &k);
+          ++j;
+        }
+      }
+      const float r = value_of(E, k);
+      res = neg ? (r == 0.0f ? 0.0f : -r) : r;
+    }
+    if (lane == 0) S.res = res;
+  }
+  __syncthreads();
+}
+
+// One chain per workgroup: out[id * ldo + i].
+template <int SRC, int K, int C>
+__global__ __launch_bounds__(kFxThreads) void k_fx_chain(FxArgs a) {
+  constexpr int KC = K > 0 ? K : 1;
+  __shared__ FxShared<C> S;
+  const int g = blockIdx.x / KC, i = blockIdx.x % KC;
+  int id;
+  if (!fx_group(a, g, &id)) return;  // (workgroup-uniform)
+  FxTerms<SRC, K> T;
+  T.init(a, id, i);
+  float av[C];
+  uint32_t f;
+  fx_walk<SRC, K, C, false>(a, T, av, S, &f, id, i);
+  if (threadIdx.x == 0) a.out[(long long)id * a.ldo + i] = S.res;
+}
+
+// The expanded belief's cdf (std::partial_sum, search_tree_cuda.cu:176-183)
+// and forwardSampling's 9 x N draws from it (:311-366), as k_fc_* + k_fc_cdf +
+// k_tree_sample do in four launches: out[0] = the row's sum, cdf[x] every
+// running sum, then counts[a * 16 + z] and the kept children z * 9 + a in
+// std::set order (klist, *kcount).  The state of a draw is the first x with
+// cdf[x] >= r: on a non-decreasing cdf (no negative or non-finite cell) the
+// first chunk whose last running sum reaches r (a search of S.end in LDS),
+// then the first such cell inside it; else the plain binary search.
+template <int C>
+__global__ __launch_bounds__(kFxThreads) void k_fx_cdf_sample(FxArgs a, SampleArgs s) {
+  __shared__ FxShared<C> S;
+  __shared__ int cnt[144];
+  const int tid = threadIdx.x;
+  for (int q = tid; q < 144; q += kFxThreads) cnt[q] = 0;
+  FxTerms<FX_ROW, 0> T;
+  T.init(a, a.g0, 0);
+  float av[C];
+  uint32_t f;
+  fx_walk<FX_ROW, 0, C, true>(a, T, av, S, &f, a.g0, 0);
+  const int n = a.n, nch = (n + C - 1) / C, x0 = C * tid;
+  const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
+  const bool neg = (f & kNeg) && !(f & kPos);
+  if (tid < nch) {
+    float v = S.start[tid];
+    if (seq_all) {  // signed terms, the chain from the walker's start values
+#pragma unroll
+      for (int q = 0; q < C; ++q) {
+        v = v + T.at(x0 + q);
+        if (x0 + q < n) a.cdf[x0 + q] = v;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < C; ++q) {
+        v = v + av[q];
+        if (x0 + q < n) a.cdf[x0 + q] = neg ? (v == 0.0f ? 0.0f : -v) : v;
+      }
+    }
+    S.end[tid] = v;
+  }
+  if (tid == 0) a.out[0] = S.res;
+  const int N = s.N, W = s.g.width;
+  if (N <= 0) return;  // (the running sums only)
+  __syncthreads();  // (the cdf: stores of this workgroup, visible to it after the barrier)
+  const bool mono = !(f & kNeg) && !(f & kBad);
+  const float* __restrict__ cdf = a.cdf;
+  for (int jt = tid; jt < 9 * N; jt += kFxThreads) {
+    const int act = jt / N, j = jt - act * N;
+    const float r = s.r[jt];
+    int s1 = n;  // the first x with cdf[x] >= r (n: none)
+    if (mono) {
+      int lo = 0, hi = nch;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (S.end[mid] < r) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < nch) {
+        for (int q = 0; q < C; ++q) {
+          const int x = C * lo + q;
+          if (x < n && cdf[x] >= r) {
+            s1 = x;
+            break;
+          }
+        }
+      }
+    } else {
+      int lo = 0, hi = n;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf[mid] < r) lo = mid + 1;
+        else hi = mid;
+      }
+      s1 = lo;
+    }
+    if (s1 >= n) {  // the reference runs off its arrays: the last cell with mass
+      s1 = n - 1;
+      while (s1 > 0 && cdf[s1] == cdf[s1 - 1]) --s1;
+    }
+    const int y1 = s1 / W, x1 = s1 - y1 * W;
+    float td = 0.0f;
+    uint32_t s2i = 0;
+    bool found = false;
+    for (int q = 0; q < 9; ++q) {
+      const float tv = s.T.p[(long long)y1 * s.T.rs + (long long)(9 * act + q) * s.T.ps + x1];
+      td = q == 0 ? tv : td + tv;
+      if (!found && s.u1[j] <= td) {
+        s2i = (uint32_t)q;
+        found = true;
+      }
+    }
+    uint32_t s2 = (uint32_t)s1 + (s2i / 3 - 1) * (uint32_t)W + (s2i % 3 - 1);
+    if (s2 >= (uint32_t)n) s2 = (uint32_t)s1;  // (never with a row-stochastic T)
+    const int y2 = (int)(s2 / (uint32_t)W), x2 = (int)(s2 - (uint32_t)y2 * (uint32_t)W);
+    float ld = 0.0f;
+    int o = 0;
+    found = false;
+    for (int q = 0; q < 16; ++q) {
+      const float lv = s.L.p[(long long)y2 * s.L.rs + (long long)q * s.L.ps + x2];
+      ld = q == 0 ? lv : ld + lv;
+      if (!found && s.u2[j] <= ld) {
+        o = q;
+        found = true;
+      }
+    }
+    atomicAdd(&cnt[act * 16 + o], 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int m = 0;
+    for (int act = 0; act < 9; ++act)
+      for (int z = 0; z < 16; ++z)
+        if (cnt[act * 16 + z]) s.klist[m++] = z * 9 + act;
+    *s.kcount = m;
+  }
+  for (int q = tid; q < 144; q += kFxThreads) s.counts[q] = cnt[q];
+}
+
 // ---------------------------------------------------------------- PBVI candidates
 // evaluatePbviCpu (point_based_value_iteration_cuda.cu:678-699) wants the
 // first maximum over S x-ordered fp32 chains per row.  Most alphas cannot be
@@ -819,6 +1211,69 @@ hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcAr
   if (base == FC_CHILD) return launch_set<FC_CHILD, 0>(st, groups, a, phases);
   if (base == FC_LIST) return launch_set<FC_LIST, 0>(st, groups, a, phases);
   return hipErrorInvalidValue;
+}
+
+namespace {
+// terms per thread of a fused chain set over n cells (0: too long for one workgroup)
+int fx_terms_per_thread(int n) {
+  return n <= 0 ? 0 : n <= 16 * kFxThreads ? 16 : n <= 32 * kFxThreads ? 32
+                                                  : n <= 64 * kFxThreads ? 64 : 0;
+}
+
+template <int SRC, int K>
+hipError_t launch_fx_set(hipStream_t st, int groups, const FxArgs& a0) {
+  constexpr int KC = K > 0 ? K : 1;
+  FxArgs a = a0;
+  a.ngroups = groups;
+  const dim3 grid((unsigned)(groups * KC)), block(kFxThreads);
+  switch (fx_terms_per_thread(a.n)) {
+    case 16: hipLaunchKernelGGL((k_fx_chain<SRC, K, 16>), grid, block, 0, st, a); break;
+    case 32: hipLaunchKernelGGL((k_fx_chain<SRC, K, 32>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((k_fx_chain<SRC, K, 64>), grid, block, 0, st, a); break;
+  }
+  return hipGetLastError();
+}
+}  // namespace
+
+bool fx_fits(int n, int ld) {
+  const int C = fx_terms_per_thread(n);
+  return C > 0 && ld >= n && ld % 64 == 0;
+}
+
+hipError_t launch_fx(hipStream_t st, int base, int K, int groups, const FxArgs& a) {
+  if (groups <= 0) return hipSuccess;
+  if (!fx_fits(a.n, a.ld) || (K != 0 && K != 9) || !a.out || groups * (K > 0 ? K : 1) > 65535)
+    return hipErrorInvalidValue;
+  if (K != 0 && !a.partners) return hipErrorInvalidValue;
+  if (base == FX_ROW && !a.row) return hipErrorInvalidValue;
+  if (base != FX_ROW && (!a.pred || !a.lrows)) return hipErrorInvalidValue;
+  if (base == FX_KEPT && (!a.sums || K != 9)) return hipErrorInvalidValue;
+  if (base == FX_CHILD && K != 0) return hipErrorInvalidValue;
+  if ((base == FX_CHILD || base == FX_KEPT) && !a.glist && a.g0 + groups > 144)
+    return hipErrorInvalidValue;
+  if (base == FX_ROW && K == 0) return launch_fx_set<FX_ROW, 0>(st, groups, a);
+  if (base == FX_ROW && K == 9) return launch_fx_set<FX_ROW, 9>(st, groups, a);
+  if (base == FX_CHILD) return launch_fx_set<FX_CHILD, 0>(st, groups, a);
+  if (base == FX_KEPT) return launch_fx_set<FX_KEPT, 9>(st, groups, a);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_fx_cdf_sample(hipStream_t st, const FxArgs& a0, const SampleArgs& s) {
+  if (!fx_fits(a0.n, a0.ld) || !a0.row || !a0.cdf || !a0.out || s.N < 0 || 9 * s.N > (1 << 20))
+    return hipErrorInvalidValue;
+  if (s.N > 0 && (s.n != a0.n || !s.r || !s.u1 || !s.u2 || !s.counts || !s.klist || !s.kcount ||
+                  !s.T.p || !s.L.p || (long long)s.g.rows * s.g.width != a0.n))
+    return hipErrorInvalidValue;
+  FxArgs a = a0;
+  a.ngroups = 1;
+  a.glist = nullptr;
+  a.gcount = nullptr;
+  switch (fx_terms_per_thread(a.n)) {
+    case 16: hipLaunchKernelGGL(k_fx_cdf_sample<16>, dim3(1), dim3(kFxThreads), 0, st, a, s); break;
+    case 32: hipLaunchKernelGGL(k_fx_cdf_sample<32>, dim3(1), dim3(kFxThreads), 0, st, a, s); break;
+    default: hipLaunchKernelGGL(k_fx_cdf_sample<64>, dim3(1), dim3(kFxThreads), 0, st, a, s); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_alpha_stats(hipStream_t st, const float* al, int S, int n, int ld, float* amax,
@@ -1074,6 +1529,112 @@ extern "C" int pp2_debug_fchain_pairs(int n, int R, const float* x, int S, const
       ok(hipMemcpy(out, dout, (size_t)R * S * sizeof(float), hipMemcpyDeviceToHost));
   }
   for (void* p : {(void*)dx, (void*)da, (void*)dout, (void*)dlist, (void*)dcnt})
+    if (p) (void)hipFree(p);
+  return st;
+}
+
+// Diagnostic (tests/test_gpu_fchain.py): the fused chain sets on device 0.
+// mode 0: FX_ROW chains of one host row x[n] (K = 0: out[0] and, with cdf,
+//   every running sum through k_fx_cdf_sample without draws; K = 9: out[i] =
+//   inner_product(x, partners[i])).
+// mode 1: the children of 9 prediction rows pred[9][n] and 16 likelihood rows
+//   L[16][n]: out[c] = accumulate of child c = z * 9 + a (FX_CHILD, all 144),
+//   then for the kcount children klist[] the normalised rows (rows[c][n]) and
+//   their 9 dots with partners (out[144 + 9 c + i], FX_KEPT).
+// ms (if set): the set's event time, median of 5 runs after a warm-up.  Synchronous.
+extern "C" int pp2_debug_fx(int mode, int n, const float* x, const float* partners, int K,
+                            const float* pred, const float* lrows, const int* klist, int kcount,
+                            float* out, float* cdf, float* rows, float* ms) {
+  if (n <= 0 || n > 65536 || (K != 0 && K != 9) || !out || (mode == 0 && !x) ||
+      (mode == 1 && (!pred || !lrows || !partners || kcount < 0 || kcount > 144 ||
+                     (kcount > 0 && !klist))) ||
+      (mode != 0 && mode != 1) || (K == 9 && !partners && mode == 0))
+    return 1;
+  const size_t ld = ((size_t)n + 63) / 64 * 64;
+  float *dx = nullptr, *dp = nullptr, *dout = nullptr, *dcdf = nullptr, *dpred = nullptr,
+        *dl = nullptr, *drows = nullptr;
+  int* dk = nullptr;
+  int st = 0;
+  auto ok = [&](hipError_t e) {
+    if (e != hipSuccess && st == 0) st = 2;
+    return st == 0;
+  };
+  auto up = [&](float** d, const float* h, int nrow) {
+    return ok(hipMalloc(d, (size_t)nrow * ld * sizeof(float))) &&
+           ok(hipMemset(*d, 0, (size_t)nrow * ld * sizeof(float))) &&
+           (!h || ok(hipMemcpy2D(*d, ld * sizeof(float), h, (size_t)n * sizeof(float),
+                                 (size_t)n * sizeof(float), nrow, hipMemcpyHostToDevice)));
+  };
+  const int nout = mode == 0 ? 16 : 144 + 144 * 9;
+  if (ok(hipMalloc(&dout, nout * sizeof(float))) && ok(hipMemset(dout, 0, nout * sizeof(float))) &&
+      (mode != 0 || up(&dx, x, 1)) && (!partners || up(&dp, partners, 9)) &&
+      (mode != 0 || !cdf || up(&dcdf, nullptr, 1)) &&
+      (mode != 1 || (up(&dpred, pred, 9) && up(&dl, lrows, 16) && up(&drows, nullptr, 144) &&
+                     ok(hipMalloc(&dk, 145 * sizeof(int))) &&
+                     (kcount == 0 || ok(hipMemcpy(dk, klist, kcount * sizeof(int),
+                                                  hipMemcpyHostToDevice))) &&
+                     ok(hipMemcpy(dk + 144, &kcount, sizeof(int), hipMemcpyHostToDevice))))) {
+    auto run = [&]() -> hipError_t {
+      pp2::FxArgs a;
+      a.n = n;
+      a.ld = (int)ld;
+      a.partners = dp;
+      a.out = dout;
+      if (mode == 0) {
+        a.row = dx;
+        a.ldo = K == 9 ? 9 : 1;
+        if (K == 0 && cdf) {
+          a.cdf = dcdf;
+          pp2::SampleArgs sa{};
+          sa.N = 0;
+          return pp2::launch_fx_cdf_sample(nullptr, a, sa);
+        }
+        return pp2::launch_fx(nullptr, pp2::FX_ROW, K, 1, a);
+      }
+      a.pred = dpred;
+      a.lrows = dl;
+      a.ldo = 1;
+      hipError_t e = pp2::launch_fx(nullptr, pp2::FX_CHILD, 0, 144, a);
+      if (e != hipSuccess) return e;
+      pp2::FxArgs b = a;
+      b.sums = dout;
+      b.out = dout + 144;
+      b.ldo = 9;
+      b.glist = dk;
+      b.gcount = dk + 144;
+      b.rows_out = drows;
+      return pp2::launch_fx(nullptr, pp2::FX_KEPT, 9, 144, b);
+    };
+    if (ms && st == 0) {
+      hipEvent_t e0, e1;
+      float t[5];
+      if (ok(hipEventCreate(&e0)) && ok(hipEventCreate(&e1))) {
+        ok(run());
+        for (int r = 0; r < 5 && st == 0; ++r) {
+          ok(hipEventRecord(e0, nullptr));
+          ok(run());
+          ok(hipEventRecord(e1, nullptr));
+          ok(hipEventSynchronize(e1));
+          ok(hipEventElapsedTime(&t[r], e0, e1));
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        for (int i = 1; i < 5; ++i)
+          for (int j = i; j > 0 && t[j] < t[j - 1]; --j) std::swap(t[j], t[j - 1]);
+        *ms = t[2];
+      }
+    }
+    if (st == 0) ok(hipMemset(dout, 0, nout * sizeof(float)));
+    if (ok(run()) && ok(hipDeviceSynchronize()) &&
+        ok(hipMemcpy(out, dout, nout * sizeof(float), hipMemcpyDeviceToHost))) {
+      if (cdf && dcdf) ok(hipMemcpy(cdf, dcdf, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+      if (rows && drows)
+        ok(hipMemcpy2D(rows, (size_t)n * sizeof(float), drows, ld * sizeof(float),
+                       (size_t)n * sizeof(float), 144, hipMemcpyDeviceToHost));
+    }
+  }
+  for (void* p : {(void*)dx, (void*)dp, (void*)dout, (void*)dcdf, (void*)dpred, (void*)dl,
+                  (void*)drows, (void*)dk})
     if (p) (void)hipFree(p);
   return st;
 }

@@ -188,6 +188,43 @@ struct SampleArgs {
   int* kcount = nullptr;
 };
 hipError_t launch_tree_sample(hipStream_t st, const SampleArgs& s);
+// Fused chain sets (pp2_fchain.hip, round 6): the same sums as launch_fchain,
+// equal bit for bit, in ONE launch per set -- a workgroup of 1024 threads per
+// chain holds the chain's terms in registers through the chunk sums, the
+// tables and the walk -- for n <= 65536 cells and a row stride ld % 64 == 0
+// (fx_fits).  Group g < groups (or < *gcount) has id = glist[g] (or g0 + g)
+// and K chains (0, or 9 partners), out[id * ldo + i]:
+//   FX_ROW    K 0 / 9: row[id * row_stride + x] (* partners[i][x])
+//   FX_CHILD  K 0: fl_ftz(pred[id % 9][x] * L[id / 9][x]) (the children's masses)
+//   FX_KEPT   K 9: b[x] = that / sums[id] (the normalised child) * partners[i][x]
+//             (evaluateFibCpu of the kept children); the workgroups of partner
+//             0 also store b into rows_out + id * ld (if set) and dst[id] (use_dst)
+enum FxBase { FX_ROW = 0, FX_CHILD = 1, FX_KEPT = 2 };
+struct FxArgs {
+  int n = 0, ld = 0;
+  const float* row = nullptr;
+  long long row_stride = 0;
+  const float* pred = nullptr;      // [9][ld]
+  const float* lrows = nullptr;     // [16][ld]
+  const float* partners = nullptr;  // [K][ld]
+  const float* sums = nullptr;      // FX_KEPT: the children's masses [144]
+  int g0 = 0;
+  const int* glist = nullptr;
+  const int* gcount = nullptr;
+  float* out = nullptr;
+  int ldo = 1;
+  float* cdf = nullptr;             // launch_fx_cdf_sample: every running sum
+  float* rows_out = nullptr;        // FX_KEPT: the normalised children [144][ld]
+  int use_dst = 0;
+  float* dst[144] = {};             // FX_KEPT: and child c's row at dst[c]
+  int ngroups = 0;                  // (set by the launcher)
+};
+bool fx_fits(int n, int ld);
+hipError_t launch_fx(hipStream_t st, int base, int K, int groups, const FxArgs& a);
+// The expanded belief's cdf and forwardSampling in one launch (FX_ROW, K 0,
+// row a.row): out[0] = its sum, cdf[x], and s.counts / s.klist / s.kcount as
+// launch_tree_sample from that cdf.
+hipError_t launch_fx_cdf_sample(hipStream_t st, const FxArgs& a, const SampleArgs& s);
 // The planner's PBVI leaf bounds in reference order (pp2_fchain.hip): per
 // alpha, max |alpha[x]| and its sign flags; then per row the alphas whose
 // exact chain can reach the maximum, from approximate dots and a rigorous

@@ -191,6 +191,12 @@ struct pp2_planner {
   // the exact parallel chain sets' three.  The reference node's 100 x 40
   // plan step: p50 2.54 vs 3.34-3.51 ms (profiles/r05/chain_walk_ab.txt).
   bool seq = false;
+  // larger grids up to 65536 cells (PP2_FX=0: off): each chain set as ONE
+  // launch, a workgroup per chain holding its terms in registers (pp2::launch_fx,
+  // launch_fx_cdf_sample), and the kept children's rows stored straight into
+  // rows acquired for all 144 children before the expansion (pre[c])
+  bool fx = false;
+  std::vector<int> pre;
   int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
   float* d_rrows = nullptr;     // [9][ld] R[.][a]
   float* d_frows = nullptr;     // [9][ld] FIB alphas[.][i]
@@ -543,6 +549,17 @@ int ref_row_bounds(pp2_planner* p, const float* row) {
                                       (int)p->n, p->d_rout + 9, 9));
     return ref_row_pbvi(p, row);
   }
+  if (p->fx) {
+    pp2::FxArgs a;
+    a.n = (int)p->n;
+    a.ld = p->ref_ld;
+    a.row = row;
+    a.partners = p->d_frows;
+    a.out = p->d_rout + 9;
+    a.ldo = 9;
+    HIPCHK(pp2::launch_fx(c->stream, pp2::FX_ROW, 9, 1, a));
+    return ref_row_pbvi(p, row);
+  }
   pp2::FcArgs a;
   a.n = (int)p->n;
   a.ld = p->ref_ld;
@@ -780,6 +797,13 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   for (uint32_t a = 0; a < 9; ++a)
     for (uint32_t j = 0; j < N; ++j)
       p->h_r[a * N + j] = (float)p->rng.next() / ((float)RAND_MAX + 1.0f);
+  if (p->fx) {
+    // a row for each of the 144 children, before anything is enqueued (a new
+    // chunk of rows is zeroed on the main stream); the kept ones are stored
+    // straight into theirs, the others go back after the wait
+    p->pre.assign(144, -1);
+    for (int cc = 0; cc < 144; ++cc) CHECK(acquire_slot(p, &p->pre[cc]));
+  }
   HIPCHK(hipEventRecord(p->ev_fork, c->stream));  // brow and the previous stores are in place
   HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
   // The two streams' launches are interleaved phase by phase, so that
@@ -788,6 +812,69 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   // children's tables (side), the cdf driver and running sums (main), the
   // children's driver (side), the samples (main); the rewards last (side).
   HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred, tree_sparse_t(c)));
+  if (p->fx) {
+    // main: the expanded belief's running sums and the 9 x N samples (one
+    // launch); side: the 144 children's masses, then the 9 rewards (a launch
+    // each); main: the kept children normalised into their rows and their
+    // FIB dots (one launch)
+    pp2::FxArgs cd;
+    cd.n = (int)n;
+    cd.ld = ld;
+    cd.row = brow;
+    cd.out = p->d_rsum;
+    cd.cdf = p->d_cdf;
+    pp2::SampleArgs sa;
+    sa.g = c->g;
+    sa.T = c->T.v;
+    sa.L = c->L.v;
+    sa.n = (int)n;
+    sa.N = (int)N;
+    sa.r = p->d_r;
+    sa.u1 = p->d_u1;
+    sa.u2 = p->d_u2;
+    sa.counts = p->d_counts;
+    sa.klist = p->d_klist;
+    sa.kcount = p->d_kcount;
+    HIPCHK(pp2::launch_fx_cdf_sample(c->stream, cd, sa));
+    pp2::FxArgs ch;
+    ch.n = (int)n;
+    ch.ld = ld;
+    ch.pred = p->d_pred;
+    ch.lrows = p->d_lrows;
+    ch.out = p->d_csum;
+    ch.ldo = 1;
+    HIPCHK(pp2::launch_fx(p->side, pp2::FX_CHILD, 0, 144, ch));
+    HIPCHK(hipEventRecord(p->ev_kids, p->side));
+    pp2::FxArgs r;
+    r.n = (int)n;
+    r.ld = ld;
+    r.row = brow;
+    r.partners = p->d_rrows;
+    r.out = p->d_rout;
+    r.ldo = 9;
+    HIPCHK(pp2::launch_fx(p->side, pp2::FX_ROW, 9, 1, r));
+    HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
+    pp2::FxArgs kd;
+    kd.n = (int)n;
+    kd.ld = ld;
+    kd.pred = p->d_pred;
+    kd.lrows = p->d_lrows;
+    kd.sums = p->d_csum;
+    kd.partners = p->d_frows;
+    kd.glist = p->d_klist;
+    kd.gcount = p->d_kcount;
+    kd.out = p->d_rout + 9;
+    kd.ldo = 9;
+    kd.rows_out = p->pbvi ? p->d_children : nullptr;  // (the PBVI dots read them there)
+    kd.use_dst = 1;
+    for (int cc = 0; cc < 144; ++cc) kd.dst[cc] = p->slots[p->pre[cc]].row;
+    HIPCHK(pp2::launch_fx(c->stream, pp2::FX_KEPT, 9, 144, kd));
+    if (p->pbvi) {
+      HIPCHK(hipEventRecord(p->ev_kept, c->stream));
+      HIPCHK(hipStreamWaitEvent(p->side, p->ev_kept, 0));
+      CHECK(ref_pbvi_bounds(p, p->d_children, 144, p->d_klist, p->d_kcount, p->side));
+    }
+  }
   if (p->seq) {
     // main: the expanded belief's running sums; side: the 144 children's
     // masses, then the 9 rewards -- sequential chains (small grid)
@@ -798,84 +885,86 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     HIPCHK(pp2::launch_pair_seq_small(p->side, pp2::PAIR_DOT, brow, 1, p->d_rrows, 9, ld, (int)n,
                                       p->d_rout, 9));
   }
-  pp2::FcArgs cd;  // main: the expanded belief's running sums
-  cd.n = (int)n;
-  cd.ld = ld;
-  cd.row = brow;
-  cd.out = p->d_rsum;
-  cd.cdf = p->d_cdf;
-  p->scr_main.attach(&cd);
-  pp2::FcArgs ch;  // side: the 144 children's masses
-  ch.n = (int)n;
-  ch.ld = ld;
-  ch.pred = p->d_pred;
-  ch.lrows = p->d_lrows;
-  ch.out = p->d_csum;
-  ch.ldo = 1;
-  p->scr_side.attach(&ch);
-  if (!p->seq) {
-    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
-    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
-    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
-    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
-    HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
-  }
-  {
-    pp2::SampleArgs sa;
-    sa.g = c->g;
-    sa.T = c->T.v;
-    sa.L = c->L.v;
-    sa.cdf = p->d_cdf;
-    sa.n = (int)n;
-    sa.N = (int)N;
-    sa.r = p->d_r;
-    sa.u1 = p->d_u1;
-    sa.u2 = p->d_u2;
-    sa.counts = p->d_counts;
-    sa.klist = p->d_klist;
-    sa.kcount = p->d_kcount;
-    HIPCHK(pp2::launch_tree_sample(c->stream, sa));
-  }
-  if (!p->seq) {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
-    pp2::FcArgs r;
-    r.n = (int)n;
-    r.ld = ld;
-    r.row = brow;
-    r.partners = p->d_rrows;
-    r.out = p->d_rout;
-    r.ldo = 9;
-    p->scr_side.attach(&r);
-    HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
-  }
-  HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
-  // main: the kept children (sampled on this stream), normalised by their
-  // masses (side) into their rows of d_children -- only they become nodes
-  HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
-                                p->d_csum, p->d_children, (int)n, ld));
-  // side: the kept children's PBVI dots (evaluatePbviCpu, the long chains),
-  // beside main's FIB dots, after the rewards already queued there
-  if (p->pbvi) {
-    HIPCHK(hipEventRecord(p->ev_kept, c->stream));
-    HIPCHK(hipStreamWaitEvent(p->side, p->ev_kept, 0));
-    CHECK(ref_pbvi_bounds(p, p->d_children, 144, p->d_klist, p->d_kcount, p->side));
-  }
-  if (p->seq) {  // main: the kept children's FIB dots (evaluateFibCpu), sequential chains
-    HIPCHK(pp2::launch_pair_seq_small(c->stream, pp2::PAIR_DOT, p->d_children, 144, p->d_frows, 9,
-                                      ld, (int)n, p->d_rout + 9, 9, p->d_klist, p->d_kcount));
-  } else {  // main: the kept children's FIB dots (evaluateFibCpu)
-    pp2::FcArgs a;
-    a.n = (int)n;
-    a.ld = ld;
-    a.row = p->d_children;
-    a.row_stride = ld;
-    a.glist = p->d_klist;
-    a.gcount = p->d_kcount;
-    a.partners = p->d_frows;
-    a.out = p->d_rout + 9;
-    a.ldo = 9;
-    p->scr_main.attach(&a);
-    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 144, a));
-  }
+  if (!p->fx) {
+    pp2::FcArgs cd;  // main: the expanded belief's running sums
+    cd.n = (int)n;
+    cd.ld = ld;
+    cd.row = brow;
+    cd.out = p->d_rsum;
+    cd.cdf = p->d_cdf;
+    p->scr_main.attach(&cd);
+    pp2::FcArgs ch;  // side: the 144 children's masses
+    ch.n = (int)n;
+    ch.ld = ld;
+    ch.pred = p->d_pred;
+    ch.lrows = p->d_lrows;
+    ch.out = p->d_csum;
+    ch.ldo = 1;
+    p->scr_side.attach(&ch);
+    if (!p->seq) {
+      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
+      HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
+      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
+      HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
+      HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
+    }
+    {
+      pp2::SampleArgs sa;
+      sa.g = c->g;
+      sa.T = c->T.v;
+      sa.L = c->L.v;
+      sa.cdf = p->d_cdf;
+      sa.n = (int)n;
+      sa.N = (int)N;
+      sa.r = p->d_r;
+      sa.u1 = p->d_u1;
+      sa.u2 = p->d_u2;
+      sa.counts = p->d_counts;
+      sa.klist = p->d_klist;
+      sa.kcount = p->d_kcount;
+      HIPCHK(pp2::launch_tree_sample(c->stream, sa));
+    }
+    if (!p->seq) {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
+      pp2::FcArgs r;
+      r.n = (int)n;
+      r.ld = ld;
+      r.row = brow;
+      r.partners = p->d_rrows;
+      r.out = p->d_rout;
+      r.ldo = 9;
+      p->scr_side.attach(&r);
+      HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
+    }
+    HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
+    // main: the kept children (sampled on this stream), normalised by their
+    // masses (side) into their rows of d_children -- only they become nodes
+    HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
+                                  p->d_csum, p->d_children, (int)n, ld));
+    // side: the kept children's PBVI dots (evaluatePbviCpu, the long chains),
+    // beside main's FIB dots, after the rewards already queued there
+    if (p->pbvi) {
+      HIPCHK(hipEventRecord(p->ev_kept, c->stream));
+      HIPCHK(hipStreamWaitEvent(p->side, p->ev_kept, 0));
+      CHECK(ref_pbvi_bounds(p, p->d_children, 144, p->d_klist, p->d_kcount, p->side));
+    }
+    if (p->seq) {  // main: the kept children's FIB dots (evaluateFibCpu), sequential chains
+      HIPCHK(pp2::launch_pair_seq_small(c->stream, pp2::PAIR_DOT, p->d_children, 144, p->d_frows, 9,
+                                        ld, (int)n, p->d_rout + 9, 9, p->d_klist, p->d_kcount));
+    } else {  // main: the kept children's FIB dots (evaluateFibCpu)
+      pp2::FcArgs a;
+      a.n = (int)n;
+      a.ld = ld;
+      a.row = p->d_children;
+      a.row_stride = ld;
+      a.glist = p->d_klist;
+      a.gcount = p->d_kcount;
+      a.partners = p->d_frows;
+      a.out = p->d_rout + 9;
+      a.ldo = 9;
+      p->scr_main.attach(&a);
+      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 144, a));
+    }
+  }  // (!p->fx)
   HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards, the PBVI dots)
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
@@ -889,6 +978,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   v->children.assign(9, nullptr);
   std::vector<int> keep;
   std::vector<float*> rows;
+  long long kept = 0;
   for (uint8_t a = 0; a < 9; ++a) {
     QNode* q = new QNode();
     ++p->n_qnodes;
@@ -900,19 +990,32 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       if (!cnt) continue;
       const int row = z * 9 + a;
       VNode* cv = new_vnode(p, z, (float)cnt / (float)N, q);
+      ++kept;
       cv->upper_bound = first_max9(p->h_rout + 9 + 9 * row);
       cv->lower_bound = p->pbvi ? p->h_lbv[row] : p->lb_const;
       cv->heuristic = cv->upper_bound - cv->lower_bound;
-      CHECK(acquire_slot(p, &cv->slot));
-      keep.push_back(row);
-      rows.push_back(p->slots[cv->slot].row);
+      if (p->fx) {  // (already stored there)
+        cv->slot = p->pre[row];
+        p->pre[row] = -1;
+      } else {
+        CHECK(acquire_slot(p, &cv->slot));
+        keep.push_back(row);
+        rows.push_back(p->slots[cv->slot].row);
+      }
       q->children.push_back(cv);
     }
     qnode_update(p, q);
     v->children[a] = q;
   }
-  CHECK(ref_store_children(p, keep.data(), rows.data(), (int)keep.size()));
-  p->stat_rows += (long long)keep.size();
+  if (p->fx) {
+    for (int& sl : p->pre) {
+      if (sl >= 0) release_slot(p, sl);
+      sl = -1;
+    }
+  } else {
+    CHECK(ref_store_children(p, keep.data(), rows.data(), (int)keep.size()));
+  }
+  p->stat_rows += kept;
   vnode_update(v);
   ++p->expansions;
   if (p->timing) {
@@ -984,6 +1087,16 @@ int tree_update(pp2_planner* p, uint8_t a, uint8_t z) {
                                         p->d_lrows + (size_t)z * p->ref_ld, 1,
                                         p->d_pred + (size_t)a * p->ref_ld, 1, p->ref_ld, (int)p->n,
                                         p->d_csum + cz, 1));
+    } else if (p->fx) {
+      pp2::FxArgs fa;
+      fa.n = (int)p->n;
+      fa.ld = p->ref_ld;
+      fa.pred = p->d_pred;
+      fa.lrows = p->d_lrows;
+      fa.g0 = cz;
+      fa.out = p->d_csum;
+      fa.ldo = 1;
+      HIPCHK(pp2::launch_fx(c->stream, pp2::FX_CHILD, 0, 1, fa));
     } else {
       pp2::FcArgs fa;
       fa.n = (int)p->n;
@@ -1111,6 +1224,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   // alphas' row length, else the cells rounded up to 64
   const int row_ld = prm->lower_bound_mode == 1 ? pld : (int)((p->n + 63) / 64 * 64);
   p->ref_ld = row_ld;
+  {
+    const char* e = getenv("PP2_FX");
+    p->fx = p->ref && !p->seq && pp2::fx_fits((int)p->n, row_ld) && !(e && e[0] == '0');
+  }
   if (prm->lower_bound_mode == 1) {
     p->pbvi = true;
     p->lb_S = pS;

@@ -162,3 +162,113 @@ def test_fchain_pair_dots_bit_exact():
             want, _ = seq(X[r] * A[i])
             assert bits(out[r, i]) == bits(want), f"n={n} row {r} alpha {i}: {out[r, i]!r} != {want!r}"
         assert np.isnan(out[~listed]).all(), "an unlisted entry was written"
+
+
+# ------------------------------------------------------- fused chain sets (round 6)
+def _fx():
+    from path_planning_2d_amd import _lib
+    f = _lib.load().pp2_debug_fx
+    f.argtypes = [C.c_int, C.c_int, _f32p, _f32p, C.c_int, _f32p, _f32p, C.POINTER(C.c_int),
+                  C.c_int, _f32p, _f32p, _f32p, _f32p]
+    f.restype = C.c_int
+    return f
+
+
+def fx_row(x, partners=None, cdf=False):
+    x = np.ascontiguousarray(x, np.float32)
+    K = 9 if partners is not None else 0
+    out = np.zeros(16, np.float32)
+    c = np.zeros(x.size, np.float32) if cdf else None
+    p = np.ascontiguousarray(partners, np.float32) if partners is not None else None
+    st = _fx()(0, x.size, _ptr(x), _ptr(p), K, None, None, None, 0, _ptr(out), _ptr(c), None, None)
+    assert st == 0, st
+    return out[:9] if K else out[0], c
+
+
+def fx_rows(rng):
+    for name, t in rows(rng):
+        if 0 < t.size <= 65536:
+            yield name, t
+    U = lambda n: rng.random(n, dtype=np.float32)  # noqa: E731
+    for n in (8193, 16384, 16385, 32768, 32769, 65536):
+        yield f"n={n}", U(n)
+    b = U(65536)
+    yield "a 256^2 belief", (b / b.sum(dtype=np.float64)).astype(np.float32)
+
+
+def test_fx_sums_and_running_sums_bit_exact():
+    """k_fx_chain / k_fx_cdf_sample (one launch per chain set, the terms in
+    registers) against the sequential chain on the adversarial rows that fit
+    one workgroup (n <= 65536)."""
+    rng = np.random.default_rng(11)
+    for name, t in fx_rows(rng):
+        want, wc = seq(t)
+        got, _ = fx_row(t)
+        assert bits(got) == bits(want), f"{name}: sum {got!r} != {want!r}"
+        got, gc = fx_row(t, cdf=True)
+        assert bits(got) == bits(want), f"{name}: cdf kernel's sum {got!r} != {want!r}"
+        assert np.array_equal(bits(gc), bits(wc)), \
+            f"{name}: running sums differ at {np.flatnonzero(bits(gc) != bits(wc))[:5]}"
+
+
+def test_fx_dots_bit_exact():
+    rng = np.random.default_rng(12)
+    for name, t in fx_rows(rng):
+        n = t.size
+        A = np.empty((9, n), np.float32)
+        A[0] = -(20 + 20 * rng.random(n, dtype=np.float32))
+        A[1] = rng.random(n, dtype=np.float32) - 0.5
+        A[2] = 0.0
+        A[3] = -2.0
+        A[4] = np.ldexp(1.0, -rng.integers(0, 30, n))
+        A[5] = -np.float32(1.0 / 3.0)
+        A[6] = rng.random(n, dtype=np.float32) * 1e20
+        A[7] = -0.0
+        A[8] = 1.0
+        got, _ = fx_row(t, partners=A)
+        for i in range(9):
+            want, _ = seq(t * A[i])
+            assert bits(got[i]) == bits(want), f"{name} partner {i}: {got[i]!r} != {want!r}"
+
+
+def ftz(v):
+    v = np.asarray(v, np.float32)
+    return np.where(np.abs(v) < np.finfo(np.float32).tiny, np.copysign(np.float32(0), v), v)
+
+
+@pytest.mark.parametrize("n", [9000, 40000, 65536])
+def test_fx_children_and_kept_dots_bit_exact(n):
+    """FX_CHILD (the 144 children's masses: accumulate of fl_ftz(pred_a *
+    fl_ftz(L_z)), search_tree_cuda.cu:225-227) and FX_KEPT (the kept
+    children normalised, :228-229, and their 9 FIB dots, evaluateFibCpu)
+    against numpy: masses, stored rows and dots bit for bit."""
+    rng = np.random.default_rng(n)
+    pred = (rng.random((9, n), dtype=np.float32) / np.float32(n)).astype(np.float32)
+    pred[:, rng.random(n) < 0.3] = 0.0
+    pred[3] = np.ldexp(pred[3], -100)                 # products into the FTZ range
+    L = rng.random((16, n), dtype=np.float32)
+    L[5, ::7] = np.float32(1e-39)                     # subnormal likelihoods flushed
+    L[9] = 0.0
+    A = -(20 + 20 * rng.random((9, n), dtype=np.float32))
+    A[4] = rng.random(n, dtype=np.float32) - 0.5
+    # kept children have mass (the planner keeps sampled observations only)
+    live = [c for c in range(144) if seq(ftz(pred[c % 9] * ftz(L[c // 9])))[0] > 0]
+    klist = np.array(sorted(rng.choice(live, 46, replace=False)), np.int32)
+    out = np.zeros(144 + 144 * 9, np.float32)
+    rows_ = np.zeros((144, n), np.float32)
+    st = _fx()(1, n, None, _ptr(A), 9, _ptr(pred), _ptr(L),
+               klist.ctypes.data_as(C.POINTER(C.c_int)), len(klist), _ptr(out), None,
+               _ptr(rows_), None)
+    assert st == 0, st
+    for c in range(144):
+        a, z = c % 9, c // 9
+        v = ftz(pred[a] * ftz(L[z]))
+        m, _ = seq(v)
+        assert bits(out[c]) == bits(m), f"child {c}: mass {out[c]!r} != {m!r}"
+        if c in klist:
+            b = (v / m).astype(np.float32)
+            assert np.array_equal(bits(rows_[c]), bits(b)), f"child {c}: row"
+            for i in range(9):
+                want, _ = seq(b * A[i])
+                got = out[144 + 9 * c + i]
+                assert bits(got) == bits(want), f"child {c} dot {i}: {got!r} != {want!r}"
