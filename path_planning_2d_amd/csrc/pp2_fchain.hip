@@ -689,6 +689,12 @@ __device__ __forceinline__ float wave_incl_scan_f(float v, int lane) {
   return f + (row >= 1 ? r0 : 0.0f) + (row >= 2 ? r1 : 0.0f) + (row >= 3 ? r2 : 0.0f);
 }
 
+// diagnostics: workgroup thread 0 stamps the 100 MHz clock at phase k
+__device__ __forceinline__ void fx_stamp(const FxArgs& a, int k) {
+  if (a.stamps && threadIdx.x == 0)
+    a.stamps[8 * (long long)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ __forceinline__ bool fx_group(const FxArgs& a, int g, int* id) {
   if (g >= a.ngroups) return false;
   if (a.gcount && g >= *a.gcount) return false;
@@ -757,7 +763,6 @@ struct FxShared {
   uint32_t e[kFxThreads];      // chunk entries (kNoEntry: none)
   int slot[kFxThreads];        // the chunk's stash slot, or -1
   float start[kFxThreads];     // the chunk's exact start value (running sums)
-  float end[kFxThreads];       // the chunk's last running sum (sampling)
   __attribute__((aligned(16))) float st[kFxStash][C];
   float wsum[16];
   uint32_t flag;
@@ -767,33 +772,39 @@ struct FxShared {
 
 // Phases A-D of one chain (every thread of the workgroup calls it; returns
 // with the workgroup synchronised, the result in S.res (wave 0 wrote it) and,
-// with RUN, every chunk's exact start value in S.start).  a[] keeps the
-// thread's |terms|; *pf the chain's sign flags.
+// with RUN, every chunk's exact start value in S.start); *pf the chain's sign
+// flags.  The passes form the thread's terms again from the (L2-resident)
+// rows instead of holding C of them in registers: the loops stay loops (a
+// fully unrolled kernel runs once through ~20 KB of code, which the
+// instruction cache fetches at ~70 us per launch, measured round 6), and the
+// registers stay few (two workgroups per CU).
 template <int SRC, int K, int C, bool RUN>
-__device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& T, float (&av)[C],
+__device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& T,
                                         FxShared<C>& S, uint32_t* pf, int id, int i) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = a.n, nch = (n + C - 1) / C;
   const int x0 = C * tid;
+  fx_stamp(a, 0);
   if (tid == 0) {
     S.flag = 0u;
     S.nst = 0;
   }
-  // A: the terms, |terms|, flags, the approximate chunk sum
+  // A: the terms' flags and the approximate chunk sum (FX_KEPT, partner 0:
+  // the normalised child stored on the way)
   uint32_t fl = 0u;
   float csum = 0.0f;
-  {
-    float* __restrict__ store = nullptr;  // FX_KEPT, partner 0: the child's row(s)
+  if (x0 < n) {
+    float* __restrict__ store = nullptr;
     float* __restrict__ store2 = nullptr;
     if (SRC == FX_KEPT && i == 0) {
       store = a.rows_out ? a.rows_out + (long long)id * a.ld : nullptr;
       store2 = a.use_dst ? a.dst[id] : nullptr;
     }
-#pragma unroll
+#pragma unroll 4
     for (int q4 = 0; q4 < C / 4; ++q4) {
-      float b[4] = {0.0f, 0.0f, 0.0f, 0.0f}, t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (x0 < n) T.at4(x0 + 4 * q4, b, t);
-      if (SRC == FX_KEPT && x0 < n) {
+      float b[4], t[4];
+      T.at4(x0 + 4 * q4, b, t);
+      if (SRC == FX_KEPT) {
         if (store) *reinterpret_cast<f4a*>(store + x0 + 4 * q4) = f4a{b[0], b[1], b[2], b[3]};
         if (store2) *reinterpret_cast<f4a*>(store2 + x0 + 4 * q4) = f4a{b[0], b[1], b[2], b[3]};
       }
@@ -801,7 +812,6 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
       for (int q = 0; q < 4; ++q) {
         const float v = t[q];
         fl |= !isfinite(v) ? kBad : v > 0.0f ? kPos : v < 0.0f ? kNeg : 0u;
-        av[4 * q4 + q] = fabsf(v);
         csum += fabsf(v);
       }
     }
@@ -811,18 +821,20 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
                        (__ballot((fl & kNeg) != 0u) ? kNeg : 0u) |
                        (__ballot((fl & kBad) != 0u) ? kBad : 0u);
     __syncthreads();  // (S.flag, S.nst initialised)
+    fx_stamp(a, 1);
     if (lane == 0 && f) atomicOr(&S.flag, f);
   }
   // B: the approximate running sum before the chunk
   const float incl = wave_incl_scan_f(csum, lane);
   if (lane == 63) S.wsum[w] = incl;
   __syncthreads();
+  fx_stamp(a, 2);
   const uint32_t f = S.flag;
   *pf = f;
   const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
   float before = incl - csum;
   for (int v = 0; v < w; ++v) before += S.wsum[v];
-  // C: the chunk's entry, and the predicted fallbacks' stash
+  // C: the chunk's entry; the predicted fallbacks' |terms| into the stash
   if (tid < nch) {
     uint32_t e = kNoEntry;
     bool pred = true;
@@ -830,12 +842,17 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
       const int E = domain_of(before);
       int d = 0;
       bool tie = false;
+#pragma unroll 4
+      for (int q4 = 0; q4 < C / 4; ++q4) {
+        float b[4], t[4];
+        T.at4(x0 + 4 * q4, b, t);
 #pragma unroll
-      for (int q = 0; q < C; ++q) {
-        bool tx;
-        const float r = units_of(av[q], E, &tx);
-        d += (int)fminf(r, (float)(kK24 + 1));
-        tie = tie || tx;
+        for (int q = 0; q < 4; ++q) {
+          bool tx;
+          const float r = units_of(fabsf(t[q]), E, &tx);
+          d += (int)fminf(r, (float)(kK24 + 1));
+          tie = tie || tx;
+        }
       }
       if (!tie && d < kK24 && E <= 127) e = ((uint32_t)(E + 128) << 24) | (uint32_t)d;
       const float pu = ldexpf(before, 23 - E);  // the running sum in units of E
@@ -843,21 +860,25 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
              pu < (float)(1 << 23) * (1.0f + 0x1p-10f);
     }
     S.e[tid] = e;
-    int s = -1;
+    int sl = -1;
     if (pred && !seq_all) {
-      s = atomicAdd(&S.nst, 1);
-      if (s < kFxStash) {
-#pragma unroll
-        for (int q4 = 0; q4 < C / 4; ++q4)
-          *reinterpret_cast<f4a*>(&S.st[s][4 * q4]) =
-              f4a{av[4 * q4], av[4 * q4 + 1], av[4 * q4 + 2], av[4 * q4 + 3]};
+      sl = atomicAdd(&S.nst, 1);
+      if (sl < kFxStash) {
+#pragma unroll 4
+        for (int q4 = 0; q4 < C / 4; ++q4) {
+          float b[4], t[4];
+          T.at4(x0 + 4 * q4, b, t);
+          *reinterpret_cast<f4a*>(&S.st[sl][4 * q4]) =
+              f4a{fabsf(t[0]), fabsf(t[1]), fabsf(t[2]), fabsf(t[3])};
+        }
       } else {
-        s = -1;
+        sl = -1;
       }
     }
-    S.slot[tid] = s;
+    S.slot[tid] = sl;
   }
   __syncthreads();
+  fx_stamp(a, 3);
   // D: wave 0 walks
   if (w == 0) {
     float res;
@@ -870,7 +891,7 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
         const float tl = tn;
         if (j + 1 < nch) tn = lane < C ? T.at(C * (j + 1) + lane) : 0.0f;
         if (RUN && lane == 0) S.start[j] = s;
-#pragma unroll
+#pragma unroll 8
         for (int q = 0; q < C; ++q) s = s + rdl(tl, q);
       }
       res = s;
@@ -898,7 +919,7 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
           const float tl = lane < C ? (sl >= 0 ? S.st[sl][lane] : fabsf(T.at(C * j + lane))) : 0.0f;
           float s = value_of(E, k);
           if (RUN && lane == 0) S.start[j] = s;
-#pragma unroll
+#pragma unroll 8
           for (int q = 0; q < C; ++q) s = s + rdl(tl, q);
           state_of(s, &E, &k);
           normalise(&E, &k);
@@ -911,6 +932,7 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
     if (lane == 0) S.res = res;
   }
   __syncthreads();
+  fx_stamp(a, 4);
 }
 
 // One chain per workgroup: out[id * ldo + i].
@@ -923,9 +945,8 @@ __global__ __launch_bounds__(kFxThreads) void k_fx_chain(FxArgs a) {
   if (!fx_group(a, g, &id)) return;  // (workgroup-uniform)
   FxTerms<SRC, K> T;
   T.init(a, id, i);
-  float av[C];
   uint32_t f;
-  fx_walk<SRC, K, C, false>(a, T, av, S, &f, id, i);
+  fx_walk<SRC, K, C, false>(a, T, S, &f, id, i);
   if (threadIdx.x == 0) a.out[(long long)id * a.ldo + i] = S.res;
 }
 
@@ -941,37 +962,41 @@ template <int C>
 __global__ __launch_bounds__(kFxThreads) void k_fx_cdf_sample(FxArgs a, SampleArgs s) {
   __shared__ FxShared<C> S;
   __shared__ int cnt[144];
+  __shared__ float sub[kFxThreads * C / 16];  // the last running sum of every 16 cells
   const int tid = threadIdx.x;
   for (int q = tid; q < 144; q += kFxThreads) cnt[q] = 0;
   FxTerms<FX_ROW, 0> T;
   T.init(a, a.g0, 0);
-  float av[C];
   uint32_t f;
-  fx_walk<FX_ROW, 0, C, true>(a, T, av, S, &f, a.g0, 0);
+  fx_walk<FX_ROW, 0, C, true>(a, T, S, &f, a.g0, 0);
   const int n = a.n, nch = (n + C - 1) / C, x0 = C * tid;
   const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
   const bool neg = (f & kNeg) && !(f & kPos);
   if (tid < nch) {
+    // every running sum of the chunk from its exact start value: signed terms
+    // after a mixed chain, else |terms| (one sign) negated back; 16-B stores
+    // (x0 + C <= the row stride: cells past n get a running sum too, inside
+    // the row's zero tail)
     float v = S.start[tid];
-    if (seq_all) {  // signed terms, the chain from the walker's start values
+#pragma unroll 4
+    for (int q4 = 0; q4 < C / 4; ++q4) {
+      float b[4], t[4];
+      T.at4(x0 + 4 * q4, b, t);
+      f4a o;
 #pragma unroll
-      for (int q = 0; q < C; ++q) {
-        v = v + T.at(x0 + q);
-        if (x0 + q < n) a.cdf[x0 + q] = v;
+      for (int q = 0; q < 4; ++q) {
+        v = v + (seq_all ? t[q] : fabsf(t[q]));
+        o[q] = seq_all || !neg ? v : (v == 0.0f ? 0.0f : -v);
       }
-    } else {
-#pragma unroll
-      for (int q = 0; q < C; ++q) {
-        v = v + av[q];
-        if (x0 + q < n) a.cdf[x0 + q] = neg ? (v == 0.0f ? 0.0f : -v) : v;
-      }
+      *reinterpret_cast<f4a*>(a.cdf + x0 + 4 * q4) = o;
+      if (q4 % 4 == 3) sub[(x0 + 4 * q4) / 16] = v;
     }
-    S.end[tid] = v;
   }
   if (tid == 0) a.out[0] = S.res;
   const int N = s.N, W = s.g.width;
   if (N <= 0) return;  // (the running sums only)
   __syncthreads();  // (the cdf: stores of this workgroup, visible to it after the barrier)
+  fx_stamp(a, 5);
   const bool mono = !(f & kNeg) && !(f & kBad);
   const float* __restrict__ cdf = a.cdf;
   for (int jt = tid; jt < 9 * N; jt += kFxThreads) {
@@ -979,20 +1004,26 @@ __global__ __launch_bounds__(kFxThreads) void k_fx_cdf_sample(FxArgs a, SampleAr
     const float r = s.r[jt];
     int s1 = n;  // the first x with cdf[x] >= r (n: none)
     if (mono) {
-      int lo = 0, hi = nch;
+      // the first 16 cells whose last running sum reaches r (LDS), then the
+      // first such cell among them
+      const int nsub = (n + 15) / 16;
+      int lo = 0, hi = nsub;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (S.end[mid] < r) lo = mid + 1;
+        if (sub[mid] < r) lo = mid + 1;
         else hi = mid;
       }
-      if (lo < nch) {
-        for (int q = 0; q < C; ++q) {
-          const int x = C * lo + q;
-          if (x < n && cdf[x] >= r) {
-            s1 = x;
-            break;
-          }
+      if (lo < nsub) {
+        float cv[16];
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const f4a v = *reinterpret_cast<const f4a*>(cdf + 16 * lo + 4 * q4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cv[4 * q4 + q] = v[q];
         }
+#pragma unroll
+        for (int q = 15; q >= 0; --q)
+          if (16 * lo + q < n && cv[q] >= r) s1 = 16 * lo + q;
       }
     } else {
       int lo = 0, hi = n;
@@ -1036,6 +1067,7 @@ __global__ __launch_bounds__(kFxThreads) void k_fx_cdf_sample(FxArgs a, SampleAr
     atomicAdd(&cnt[act * 16 + o], 1);
   }
   __syncthreads();
+  fx_stamp(a, 6);
   if (tid == 0) {
     int m = 0;
     for (int act = 0; act < 9; ++act)
@@ -1635,6 +1667,93 @@ extern "C" int pp2_debug_fx(int mode, int n, const float* x, const float* partne
   }
   for (void* p : {(void*)dx, (void*)dp, (void*)dout, (void*)dcdf, (void*)dpred, (void*)dl,
                   (void*)drows, (void*)dk})
+    if (p) (void)hipFree(p);
+  return st;
+}
+
+// Diagnostic (tests/test_gpu_fchain.py, round-5 ADVICE): the planner's PBVI
+// candidate filter as ref_pbvi_bounds runs it (pp2_tree.cpp, PP2_PBVI_FCHAIN=1)
+// on host rows x[R][n] and alphas[S][n]: the split-x MFMA GEMM's approximate
+// dots, k_pbvi_cands with the bound priced from gemm_kchunk, the candidates'
+// exact chains (FC_LIST), the first argmax per row -> idx[r], val[r];
+// *ncand = the candidates kept.  Synchronous, device 0.
+extern "C" int pp2_debug_pbvi_cands(int n, int R, const float* x, int S, const float* alphas,
+                                    int ksplit, int* idx, float* val, int* ncand) {
+  if (n <= 0 || R <= 0 || R > 256 || S <= 0 || !x || !alphas || !idx || !val || ksplit < 1)
+    return 1;
+  const int ld = (n + pp2::kPbviChunk - 1) / pp2::kPbviChunk * pp2::kPbviChunk;
+  const int Mp = (R + pp2::kGemmTile - 1) / pp2::kGemmTile * pp2::kGemmTile;
+  const int Sp = (S + pp2::kGemmTile - 1) / pp2::kGemmTile * pp2::kGemmTile;
+  const long long sstride = (long long)Mp * Sp;
+  float *dx = nullptr, *da = nullptr, *dpart = nullptr, *dapprox = nullptr, *damax = nullptr,
+        *dexact = nullptr, *dv = nullptr;
+  uint32_t* dflag = nullptr;
+  int2* dlist = nullptr;
+  int *dcnt = nullptr, *didx = nullptr;
+  pp2::FcScratch scr;
+  int st = 0;
+  auto ok = [&](hipError_t e) {
+    if (e != hipSuccess && st == 0) st = 2;
+    return st == 0;
+  };
+  if (!scr.reserve(n, R * S)) return 3;
+  if (ok(hipMalloc(&dx, (size_t)Mp * ld * sizeof(float))) &&
+      ok(hipMalloc(&da, (size_t)Sp * ld * sizeof(float))) &&
+      ok(hipMalloc(&dpart, (size_t)ksplit * sstride * sizeof(float))) &&
+      ok(hipMalloc(&dapprox, (size_t)sstride * sizeof(float))) &&
+      ok(hipMalloc(&damax, (size_t)Sp * sizeof(float))) &&
+      ok(hipMalloc(&dflag, (size_t)Sp * sizeof(uint32_t))) &&
+      ok(hipMalloc(&dexact, (size_t)R * S * sizeof(float))) &&
+      ok(hipMalloc(&dv, (size_t)R * sizeof(float))) &&
+      ok(hipMalloc(&didx, (size_t)R * sizeof(int))) &&
+      ok(hipMalloc(&dlist, (size_t)R * S * sizeof(int2))) && ok(hipMalloc(&dcnt, sizeof(int))) &&
+      ok(hipMemset(dx, 0, (size_t)Mp * ld * sizeof(float))) &&
+      ok(hipMemset(da, 0, (size_t)Sp * ld * sizeof(float))) &&
+      ok(hipMemset(dcnt, 0, sizeof(int))) &&
+      ok(hipMemcpy2D(dx, ld * sizeof(float), x, (size_t)n * sizeof(float), (size_t)n * sizeof(float),
+                     R, hipMemcpyHostToDevice)) &&
+      ok(hipMemcpy2D(da, ld * sizeof(float), alphas, (size_t)n * sizeof(float),
+                     (size_t)n * sizeof(float), S, hipMemcpyHostToDevice)) &&
+      ok(pp2::launch_alpha_stats(nullptr, da, S, n, ld, damax, dflag)) &&
+      ok(pp2::launch_gemm_nt(nullptr, dx, da, dpart, Mp, Sp, ld, 1, 0, 0, ksplit, sstride)) &&
+      ok(pp2::launch_sum_splits(nullptr, dpart, ksplit, sstride, (int)sstride, dapprox))) {
+    pp2::PbviCandArgs ca;
+    ca.rows = dx;
+    ca.row_stride = ld;
+    ca.n = n;
+    ca.nrows = R;
+    ca.approx = dapprox;
+    ca.lda = Sp;
+    ca.amax = damax;
+    ca.aflag = dflag;
+    ca.S = S;
+    const long long kchunk = pp2::gemm_kchunk(ld, ksplit);
+    ca.c_rel = (float)((double)((long long)n + kchunk + ksplit + 8) * 0x1p-24 * 1.01);
+    ca.exact = dexact;
+    ca.lde = S;
+    ca.plist = dlist;
+    ca.pcount = dcnt;
+    pp2::FcArgs a;
+    a.n = n;
+    a.ld = ld;
+    a.row = dx;
+    a.row_stride = ld;
+    a.partners = da;
+    a.plist = dlist;
+    a.gcount = dcnt;
+    a.out = dexact;
+    a.ldo = S;
+    scr.attach(&a);
+    if (ok(pp2::launch_pbvi_cands(nullptr, ca)) &&
+        ok(pp2::launch_fchain(nullptr, pp2::FC_LIST, 0, R * S, a)) &&
+        ok(pp2::launch_argmax_rows(nullptr, dexact, R, S, S, didx, dv)) &&
+        ok(hipDeviceSynchronize()) &&
+        ok(hipMemcpy(idx, didx, (size_t)R * sizeof(int), hipMemcpyDeviceToHost)) &&
+        ok(hipMemcpy(val, dv, (size_t)R * sizeof(float), hipMemcpyDeviceToHost)) && ncand)
+      ok(hipMemcpy(ncand, dcnt, sizeof(int), hipMemcpyDeviceToHost));
+  }
+  for (void* p : {(void*)dx, (void*)da, (void*)dpart, (void*)dapprox, (void*)damax, (void*)dflag,
+                  (void*)dexact, (void*)dv, (void*)didx, (void*)dlist, (void*)dcnt})
     if (p) (void)hipFree(p);
   return st;
 }

@@ -1580,12 +1580,16 @@ hipError_t launch_pbvi_pick(hipStream_t st, const float* l1, int ldo, int n, int
   return hipGetLastError();
 }
 
+int gemm_kchunk(int ld, int ksplit) {
+  const int kchunk = (ld + ksplit - 1) / ksplit;
+  return (kchunk + GK - 1) / GK * GK;
+}
+
 hipError_t launch_gemm_nt(hipStream_t st, const float* A, const float* B, float* C, int Mp,
                           int Np, int ld, int batch, long long bstride, long long cstride,
                           int ksplit, long long sstride) {
   if (Mp % GT || Np % GT || ld % GK || ksplit < 1) return hipErrorInvalidValue;
-  int kchunk = (ld + ksplit - 1) / ksplit;
-  kchunk = (kchunk + GK - 1) / GK * GK;
+  const int kchunk = gemm_kchunk(ld, ksplit);
   const long long blocks = (long long)(Mp / GT) * (Np / GT) * ksplit * batch;
   if (blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_gemm_nt, dim3((unsigned)blocks), dim3(256), 0, st, A, B, C, Mp, Np, ld,

@@ -91,6 +91,9 @@ hipError_t launch_pbvi_pick(hipStream_t st, const float* l1, int ldo, int n, int
 hipError_t launch_gemm_nt(hipStream_t st, const float* A, const float* B, float* C, int Mp,
                           int Np, int ld, int batch, long long bstride, long long cstride,
                           int ksplit, long long sstride);
+// x-cells per split of launch_gemm_nt (each split's chain length): the
+// planner's PBVI candidate bound (k_pbvi_cands) prices its rounding from it
+int gemm_kchunk(int ld, int ksplit);
 // out[r] = first argmax over k < n of C[r*ldc + k]
 hipError_t launch_argmax_rows(hipStream_t st, const float* C, int rows, int n, int ldc,
                               int* out, float* vmax);
@@ -217,6 +220,7 @@ struct FxArgs {
   float* rows_out = nullptr;        // FX_KEPT: the normalised children [144][ld]
   int use_dst = 0;
   float* dst[144] = {};             // FX_KEPT: and child c's row at dst[c]
+  unsigned long long* stamps = nullptr;  // diagnostics: s_memrealtime at the phase ends, 8 per workgroup
   int ngroups = 0;                  // (set by the launcher)
 };
 bool fx_fits(int n, int ld);

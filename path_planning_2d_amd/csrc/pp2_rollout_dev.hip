@@ -718,10 +718,13 @@ __global__ __launch_bounds__(64) void k_rollout_leaf_mfma(const _Float16* __rest
   h8v Bf[kLeafNS][4];
   // stage k from slot k % NS with B fragments Bf[k % NS]; stage k + NS - 1
   // (its slot, its fragments) issued first, so NS - 1 stages stay in flight
-  auto stage = [&](int k, auto kk) {
+  // (MORE: stage k + NS - 1 exists -- a compile-time flag, so that the
+  // issue and its wait stay one branch-free block: tools/asm_hazard_check.py
+  // follows each wait to the loads it covers)
+  auto stage = [&](int k, auto kk, auto more) {
     constexpr int q = decltype(kk)::value;  // k % NS
     constexpr int qn = (q + kLeafNS - 1) % kLeafNS;
-    if (k + kLeafNS - 1 < nst) {
+    if constexpr (decltype(more)::value) {
       asm volatile("" ::: "memory");  // slot qn's reads (stage k-1) completed (lgkmcnt(0))
       issue(k + kLeafNS - 1, ring + qn * kSlot);
       ldb4(k + kLeafNS - 1, Bf[qn]);
@@ -755,11 +758,18 @@ __global__ __launch_bounds__(64) void k_rollout_leaf_mfma(const _Float16* __rest
     issue(j, ring + j * kSlot);
     ldb4(j, Bf[j]);
   }
-  for (int k = 0; k < nst; k += kLeafNS) {
-    stage(k, std::integral_constant<int, 0>{});
-    stage(k + 1, std::integral_constant<int, 1>{});
-    if constexpr (kLeafNS > 2) stage(k + 2, std::integral_constant<int, 2 % kLeafNS>{});
+  using Yes = std::true_type;
+  using No = std::false_type;
+  int k = 0;
+  for (; k + kLeafNS < nst; k += kLeafNS) {
+    stage(k, std::integral_constant<int, 0>{}, Yes{});
+    stage(k + 1, std::integral_constant<int, 1>{}, Yes{});
+    if constexpr (kLeafNS > 2) stage(k + 2, std::integral_constant<int, 2 % kLeafNS>{}, Yes{});
   }
+  // the last round (k = nst - NS): only its first stage has a stage NS - 1 ahead
+  stage(k, std::integral_constant<int, 0>{}, Yes{});
+  stage(k + 1, std::integral_constant<int, 1>{}, No{});
+  if constexpr (kLeafNS > 2) stage(k + 2, std::integral_constant<int, 2 % kLeafNS>{}, No{});
   // D: column r (= lane & 31), rows (v & 3) + 8 (v >> 2) + 4 h
   if (r < kLeafCols) {
 #pragma unroll

@@ -197,6 +197,11 @@ struct pp2_planner {
   // rows acquired for all 144 children before the expansion (pre[c])
   bool fx = false;
   std::vector<int> pre;
+  // PP2_FX_STAMPS=1 (diagnostics): the fused kernels' phase clocks, 8 per
+  // workgroup, summed per kernel and phase, printed when the planner goes
+  unsigned long long* d_stamps = nullptr;
+  double fx_phase[4][8] = {};
+  long long fx_groups[4] = {}, fx_sets = 0;
   int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
   float* d_rrows = nullptr;     // [9][ld] R[.][a]
   float* d_frows = nullptr;     // [9][ld] FIB alphas[.][i]
@@ -491,7 +496,7 @@ int ref_pbvi_bounds(pp2_planner* p, const float* d_rows, int rows, const int* kl
     ca.S = S;
     // the GEMM's fmaf chains of kchunk terms and its ordered split sum
     // (launch_gemm_nt's kchunk), the reference's chain of n adds, 1 % slack
-    const long long kchunk = ((p->ref_ld + p->lb_split - 1) / p->lb_split + 31) / 32 * 32;
+    const long long kchunk = pp2::gemm_kchunk(p->ref_ld, p->lb_split);
     ca.c_rel = (float)((double)((long long)p->n + kchunk + p->lb_split + 8) * 0x1p-24 * 1.01);
     ca.exact = p->d_lbdots;
     ca.lde = S;
@@ -768,6 +773,47 @@ int expand_vnode(pp2_planner* p, VNode* v) {
   return PP2_OK;
 }
 
+// PP2_FX_STAMPS: the stamp rows of the four fused kernels of an expansion
+// (cdf + samples 1, children 144, rewards 9, kept dots 1296)
+constexpr int kFxStampOff[5] = {0, 1, 145, 154, 1450};
+constexpr int kFxStampWGs = 1450;
+
+void fx_stamps_collect(pp2_planner* p) {
+  std::vector<unsigned long long> h((size_t)kFxStampWGs * 8);
+  if (hipMemcpy(h.data(), p->d_stamps, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return;
+  for (int k = 0; k < 4; ++k) {
+    unsigned long long first = ~0ull, last = 0;
+    for (int b = kFxStampOff[k]; b < kFxStampOff[k + 1]; ++b) {
+      const unsigned long long* t = &h[(size_t)b * 8];
+      if (!t[0]) continue;  // (an inactive workgroup)
+      ++p->fx_groups[k];
+      const int np = k == 0 ? 6 : 4;
+      for (int ph = 0; ph < np; ++ph)
+        if (t[ph + 1] >= t[ph]) p->fx_phase[k][ph] += (double)(t[ph + 1] - t[ph]) * 0.01;
+      first = std::min(first, t[0]);
+      last = std::max(last, t[np]);
+    }
+    if (last > first) p->fx_phase[k][7] += (double)(last - first) * 0.01;
+  }
+  ++p->fx_sets;
+}
+
+void fx_stamps_print(pp2_planner* p) {
+  if (!p->d_stamps || !p->fx_sets) return;
+  const char* names[4] = {"cdf+samples", "children", "rewards", "kept dots"};
+  for (int k = 0; k < 4; ++k) {
+    const double g = p->fx_groups[k] ? (double)p->fx_groups[k] : 1.0;
+    std::fprintf(stderr,
+                 "fx %-11s: %6.1f workgroups/set; per workgroup us: A %.2f B %.2f C %.2f walk %.2f"
+                 " cdf %.2f samples %.2f; set span %.2f us\n",
+                 names[k], g / (double)p->fx_sets, p->fx_phase[k][0] / g, p->fx_phase[k][1] / g,
+                 p->fx_phase[k][2] / g, p->fx_phase[k][3] / g, p->fx_phase[k][4] / g,
+                 p->fx_phase[k][5] / g, p->fx_phase[k][7] / (double)p->fx_sets);
+  }
+}
+
 // VNode::expand in reference order.  Every grid-wide sum of the reference's
 // 9 QNode constructors (search_tree_cuda.cu:161-242) is formed on the device
 // with the bits of its x-ordered fp32 host chain (pp2_fchain.hip), and the
@@ -823,6 +869,11 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     cd.row = brow;
     cd.out = p->d_rsum;
     cd.cdf = p->d_cdf;
+    if (p->d_stamps) {
+      HIPCHK(hipMemsetAsync(p->d_stamps, 0, kFxStampWGs * 8 * sizeof(unsigned long long),
+                            c->stream));
+      cd.stamps = p->d_stamps + 8 * kFxStampOff[0];
+    }
     pp2::SampleArgs sa;
     sa.g = c->g;
     sa.T = c->T.v;
@@ -843,6 +894,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     ch.lrows = p->d_lrows;
     ch.out = p->d_csum;
     ch.ldo = 1;
+    if (p->d_stamps) ch.stamps = p->d_stamps + 8 * kFxStampOff[1];
     HIPCHK(pp2::launch_fx(p->side, pp2::FX_CHILD, 0, 144, ch));
     HIPCHK(hipEventRecord(p->ev_kids, p->side));
     pp2::FxArgs r;
@@ -852,6 +904,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     r.partners = p->d_rrows;
     r.out = p->d_rout;
     r.ldo = 9;
+    if (p->d_stamps) r.stamps = p->d_stamps + 8 * kFxStampOff[2];
     HIPCHK(pp2::launch_fx(p->side, pp2::FX_ROW, 9, 1, r));
     HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
     pp2::FxArgs kd;
@@ -868,6 +921,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     kd.rows_out = p->pbvi ? p->d_children : nullptr;  // (the PBVI dots read them there)
     kd.use_dst = 1;
     for (int cc = 0; cc < 144; ++cc) kd.dst[cc] = p->slots[p->pre[cc]].row;
+    if (p->d_stamps) kd.stamps = p->d_stamps + 8 * kFxStampOff[3];
     HIPCHK(pp2::launch_fx(c->stream, pp2::FX_KEPT, 9, 144, kd));
     if (p->pbvi) {
       HIPCHK(hipEventRecord(p->ev_kept, c->stream));
@@ -972,6 +1026,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   HIPCHK(hipEventSynchronize(p->ev_done));
   const clk::time_point t_ret = p->timing ? clk::now() : clk::time_point{};
   if (p->h_pstat) p->stat_cands += *p->h_pstat;
+  if (p->d_stamps) fx_stamps_collect(p);
 
   for (QNode* q : v->children)
     if (q) delete_subtree(p, q);
@@ -1227,6 +1282,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   {
     const char* e = getenv("PP2_FX");
     p->fx = p->ref && !p->seq && pp2::fx_fits((int)p->n, row_ld) && !(e && e[0] == '0');
+    const char* d = getenv("PP2_FX_STAMPS");
+    if (p->fx && d && d[0] == '1' &&
+        hipMalloc(&p->d_stamps, kFxStampWGs * 8 * sizeof(unsigned long long)) != hipSuccess)
+      return fail(set_err(PP2_ENOMEM, "planner stamps allocation failed"));
   }
   if (prm->lower_bound_mode == 1) {
     p->pbvi = true;
@@ -1356,6 +1415,8 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (!p) return PP2_OK;
   DeviceGuard dg(p->ctx->device);
   (void)hipStreamSynchronize(p->ctx->stream);
+  fx_stamps_print(p);
+  if (p->d_stamps) (void)hipFree(p->d_stamps);
   pp2_planner_reset(p);
   for (Slot& s : p->slots) {
     free_planes(&s.b);

@@ -272,3 +272,45 @@ def test_fx_children_and_kept_dots_bit_exact(n):
                 want, _ = seq(b * A[i])
                 got = out[144 + 9 * c + i]
                 assert bits(got) == bits(want), f"child {c} dot {i}: {got!r} != {want!r}"
+
+
+@pytest.mark.parametrize("ksplit", [1, 4])
+def test_pbvi_candidate_filter_finds_the_first_maximum(ksplit):
+    """The opt-in PBVI candidate filter (k_pbvi_cands after the split-x MFMA
+    GEMM, its error bound priced from launch_gemm_nt's own kchunk through
+    gemm_kchunk; round-5 ADVICE) never drops the true maximum: alphas
+    clustered within a few ulps of each other, exact duplicates (the first
+    one wins) and a mixed-sign alpha, against the brute-force first argmax of
+    every sequential chain (evaluatePbviCpu, point_based_value_iteration_cuda.cu:678-699)."""
+    from path_planning_2d_amd import _lib
+    f = _lib.load().pp2_debug_pbvi_cands
+    f.argtypes = [C.c_int, C.c_int, _f32p, C.c_int, _f32p, C.c_int, C.POINTER(C.c_int), _f32p,
+                  C.POINTER(C.c_int)]
+    f.restype = C.c_int
+    rng = np.random.default_rng(40 + ksplit)
+    n, R, S = 3000, 6, 150
+    X = rng.random((R, n), dtype=np.float32)
+    X[1, rng.random(n) < 0.8] = 0.0
+    X[2] = np.ldexp(X[2], -rng.integers(0, 20, n))
+    X = (X / X.sum(axis=1, keepdims=True, dtype=np.float64)).astype(np.float32)
+    base = -(20 + 20 * rng.random(n, dtype=np.float32))
+    A = np.empty((S, n), np.float32)
+    for i in range(S):  # within a few ulps of base
+        A[i] = np.nextafter(base, np.float32(0)) if i % 3 == 0 else base
+        k = rng.integers(0, n, 5)
+        A[i, k] = base[k] + np.float32(i % 7) * np.spacing(base[k])
+    A[77] = A[13]                                  # exact duplicate: the first wins
+    A[90] = rng.random(n, dtype=np.float32) - 30.0
+    A[91] = rng.random(n, dtype=np.float32) - 0.5  # mixed sign
+    idx = np.zeros(R, np.int32)
+    val = np.zeros(R, np.float32)
+    nc = C.c_int(0)
+    st = f(n, R, _ptr(X), S, _ptr(A), ksplit, idx.ctypes.data_as(C.POINTER(C.c_int)), _ptr(val),
+           C.byref(nc))
+    assert st == 0, st
+    for r in range(R):
+        vals = np.array([seq(X[r] * A[i])[0] for i in range(S)], np.float32)
+        want = int(np.argmax(vals))
+        assert idx[r] == want, (r, idx[r], want, vals[idx[r]], vals[want])
+        assert bits(val[r]) == bits(vals[want])
+    assert 0 < nc.value < R * S  # the filter dropped some, kept the maximum
