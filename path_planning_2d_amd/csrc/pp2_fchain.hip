@@ -757,43 +757,65 @@ struct FxTerms {
   }
 };
 
-// Shared state of one chain's workgroup.
-template <int C>
+// Shared state of one chain's workgroup.  A chunk is kFxC = 64 consecutive
+// cells; the workgroup's 16 waves take 64 chunks each.  In the passes over the
+// terms a chunk is one 16-lane row of a wave (4 cells per lane): a wave's
+// 16-B loads then cover 1 KB of consecutive cells, 4 chunks per instruction.
+constexpr int kFxC = 64;
 struct FxShared {
-  uint32_t e[kFxThreads];      // chunk entries (kNoEntry: none)
-  int slot[kFxThreads];        // the chunk's stash slot, or -1
-  float start[kFxThreads];     // the chunk's exact start value (running sums)
-  __attribute__((aligned(16))) float st[kFxStash][C];
+  uint32_t e[kFxThreads];   // chunk entries (kNoEntry: none)
+  float cb[kFxThreads];     // the approximate chunk sum (A), then the running sum before it (B)
+  int slot[kFxThreads];     // the chunk's stash slot, or -1
+  float start[kFxThreads];  // the chunk's exact start value (running sums)
+  __attribute__((aligned(16))) float st[kFxStash][kFxC];
   float wsum[16];
   uint32_t flag;
   int nst;
   float res;
 };
 
+// broadcast lane i of each 16-lane row to the row (DPP row_newbcast, gfx950)
+template <int I>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x150 + I, 0xf, 0xf, false));
+}
+// the 16-lane row's total in its lane 15 (any association; float, or int below 2^31)
+__device__ __forceinline__ float row_total_f(float v) {
+  int b = __builtin_bit_cast(int, v);
+#pragma unroll
+  for (int c = 1; c < 16; c <<= 1)
+    b = __builtin_bit_cast(int, __builtin_bit_cast(float, b) +
+                                    __builtin_bit_cast(float, row_shr(b, c)));
+  return __builtin_bit_cast(float, b);
+}
+__device__ __forceinline__ int row_total_i(int v) {
+#pragma unroll
+  for (int c = 1; c < 16; c <<= 1) v += row_shr(v, c);
+  return v;
+}
+
 // Phases A-D of one chain (every thread of the workgroup calls it; returns
-// with the workgroup synchronised, the result in S.res (wave 0 wrote it) and,
-// with RUN, every chunk's exact start value in S.start); *pf the chain's sign
-// flags.  The passes form the thread's terms again from the (L2-resident)
-// rows instead of holding C of them in registers: the loops stay loops (a
-// fully unrolled kernel runs once through ~20 KB of code, which the
-// instruction cache fetches at ~70 us per launch, measured round 6), and the
-// registers stay few (two workgroups per CU).
-template <int SRC, int K, int C, bool RUN>
-__device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& T,
-                                        FxShared<C>& S, uint32_t* pf, int id, int i) {
+// with the workgroup synchronised, the result in S.res and, with RUN, every
+// chunk's exact start value in S.start); *pf the chain's sign flags.  The
+// passes form the terms again from the (L2-resident) rows instead of holding
+// them: the loops stay loops (a fully unrolled kernel runs once through ~20
+// KB of code), and the registers stay few.
+template <int SRC, int K, bool RUN>
+__device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& T, FxShared& S,
+                                        uint32_t* pf, int id, int i) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int n = a.n, nch = (n + C - 1) / C;
-  const int x0 = C * tid;
+  const int rw = lane >> 4, c16 = lane & 15;
+  const int n = a.n, nch = (n + kFxC - 1) / kFxC;
   fx_stamp(a, 0);
   if (tid == 0) {
     S.flag = 0u;
     S.nst = 0;
   }
-  // A: the terms' flags and the approximate chunk sum (FX_KEPT, partner 0:
-  // the normalised child stored on the way)
+  // A: flags and approximate chunk sums, 4 chunks per wave instruction (FX_KEPT,
+  // partner 0: the normalised child stored on the way)
   uint32_t fl = 0u;
-  float csum = 0.0f;
-  if (x0 < n) {
+  {
     float* __restrict__ store = nullptr;
     float* __restrict__ store2 = nullptr;
     if (SRC == FX_KEPT && i == 0) {
@@ -801,126 +823,157 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
       store2 = a.use_dst ? a.dst[id] : nullptr;
     }
 #pragma unroll 4
-    for (int q4 = 0; q4 < C / 4; ++q4) {
-      float b[4], t[4];
-      T.at4(x0 + 4 * q4, b, t);
-      if (SRC == FX_KEPT) {
-        if (store) *reinterpret_cast<f4a*>(store + x0 + 4 * q4) = f4a{b[0], b[1], b[2], b[3]};
-        if (store2) *reinterpret_cast<f4a*>(store2 + x0 + 4 * q4) = f4a{b[0], b[1], b[2], b[3]};
+    for (int g = 0; g < 16; ++g) {
+      const int j = 64 * w + 4 * g + rw, x = kFxC * j + 4 * c16;
+      float b[4] = {0.0f, 0.0f, 0.0f, 0.0f}, t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (x < n) T.at4(x, b, t);
+      if (SRC == FX_KEPT && x < n) {
+        if (store) *reinterpret_cast<f4a*>(store + x) = f4a{b[0], b[1], b[2], b[3]};
+        if (store2) *reinterpret_cast<f4a*>(store2 + x) = f4a{b[0], b[1], b[2], b[3]};
       }
+      float s4 = 0.0f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float v = t[q];
-        fl |= !isfinite(v) ? kBad : v > 0.0f ? kPos : v < 0.0f ? kNeg : 0u;
-        csum += fabsf(v);
+        fl |= !isfinite(t[q]) ? kBad : t[q] > 0.0f ? kPos : t[q] < 0.0f ? kNeg : 0u;
+        s4 += fabsf(t[q]);
       }
+      s4 = row_total_f(s4);
+      if (c16 == 15) S.cb[j] = s4;
     }
   }
   {
     const uint32_t f = (__ballot((fl & kPos) != 0u) ? kPos : 0u) |
                        (__ballot((fl & kNeg) != 0u) ? kNeg : 0u) |
                        (__ballot((fl & kBad) != 0u) ? kBad : 0u);
-    __syncthreads();  // (S.flag, S.nst initialised)
+    __syncthreads();  // (S.flag, S.nst initialised; S.cb written)
     fx_stamp(a, 1);
     if (lane == 0 && f) atomicOr(&S.flag, f);
   }
-  // B: the approximate running sum before the chunk
-  const float incl = wave_incl_scan_f(csum, lane);
-  if (lane == 63) S.wsum[w] = incl;
+  // B: the approximate running sum before each chunk (thread t: chunk t)
+  {
+    const float cs = S.cb[tid];
+    const float incl = wave_incl_scan_f(cs, lane);
+    if (lane == 63) S.wsum[w] = incl;
+    __syncthreads();
+    float before = incl - cs;
+    for (int v = 0; v < w; ++v) before += S.wsum[v];
+    S.cb[tid] = before;
+  }
   __syncthreads();
   fx_stamp(a, 2);
   const uint32_t f = S.flag;
   *pf = f;
   const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
-  float before = incl - csum;
-  for (int v = 0; v < w; ++v) before += S.wsum[v];
-  // C: the chunk's entry; the predicted fallbacks' |terms| into the stash
-  if (tid < nch) {
-    uint32_t e = kNoEntry;
-    bool pred = true;
-    if (!seq_all) {
+  // C: each chunk's entry; the predicted fallbacks' |terms| into the stash
+  if (!seq_all) {
+#pragma unroll 2
+    for (int g = 0; g < 16; ++g) {
+      const int j = 64 * w + 4 * g + rw, x = kFxC * j + 4 * c16;
+      if (64 * w + 4 * g >= nch) break;  // (wave-uniform)
+      float b[4] = {0.0f, 0.0f, 0.0f, 0.0f}, t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (x < n) T.at4(x, b, t);
+      const float before = S.cb[j < nch ? j : 0];
       const int E = domain_of(before);
       int d = 0;
       bool tie = false;
-#pragma unroll 4
-      for (int q4 = 0; q4 < C / 4; ++q4) {
-        float b[4], t[4];
-        T.at4(x0 + 4 * q4, b, t);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          bool tx;
-          const float r = units_of(fabsf(t[q]), E, &tx);
-          d += (int)fminf(r, (float)(kK24 + 1));
-          tie = tie || tx;
-        }
+      for (int q = 0; q < 4; ++q) {
+        bool tx;
+        const float r = units_of(fabsf(t[q]), E, &tx);
+        d += (int)fminf(r, (float)(kK24 + 1));
+        tie = tie || tx;
       }
-      if (!tie && d < kK24 && E <= 127) e = ((uint32_t)(E + 128) << 24) | (uint32_t)d;
-      const float pu = ldexpf(before, 23 - E);  // the running sum in units of E
-      pred = e == kNoEntry || tid == 0 || pu + (float)d >= (float)kK24 * (1.0f - 0x1p-12f) ||
-             pu < (float)(1 << 23) * (1.0f + 0x1p-10f);
-    }
-    S.e[tid] = e;
-    int sl = -1;
-    if (pred && !seq_all) {
-      sl = atomicAdd(&S.nst, 1);
-      if (sl < kFxStash) {
-#pragma unroll 4
-        for (int q4 = 0; q4 < C / 4; ++q4) {
-          float b[4], t[4];
-          T.at4(x0 + 4 * q4, b, t);
-          *reinterpret_cast<f4a*>(&S.st[sl][4 * q4]) =
-              f4a{fabsf(t[0]), fabsf(t[1]), fabsf(t[2]), fabsf(t[3])};
+      d = row_total_i(d);  // (<= 64 (2^24 + 1) < 2^31)
+      const bool rtie = ((__ballot(tie) >> (16 * rw)) & 0xffffull) != 0ull;
+      int sl = -1;
+      if (c16 == 15 && j < nch) {
+        uint32_t e = kNoEntry;
+        if (!rtie && d < kK24 && E <= 127) e = ((uint32_t)(E + 128) << 24) | (uint32_t)d;
+        const float pu = ldexpf(before, 23 - E);  // the running sum in units of E
+        const bool pred = e == kNoEntry || j == 0 ||
+                          pu + (float)d >= (float)kK24 * (1.0f - 0x1p-12f) ||
+                          pu < (float)(1 << 23) * (1.0f + 0x1p-10f);
+        S.e[j] = e;
+        if (pred) {
+          sl = atomicAdd(&S.nst, 1);
+          if (sl >= kFxStash) sl = -1;
         }
-      } else {
-        sl = -1;
+        S.slot[j] = sl;
       }
+      sl = __shfl(sl, lane | 15);
+      if (sl >= 0)
+        *reinterpret_cast<f4a*>(&S.st[sl][4 * c16]) =
+            f4a{fabsf(t[0]), fabsf(t[1]), fabsf(t[2]), fabsf(t[3])};
     }
-    S.slot[tid] = sl;
   }
   __syncthreads();
   fx_stamp(a, 3);
-  // D: wave 0 walks
+  // D: wave 0 walks the entries, 4 per lane (256 per step)
   if (w == 0) {
     float res;
     if (seq_all) {
       // mixed signs or a non-finite term: the reference's chain itself, the
       // next chunk's terms loaded while this one's are added
       float s = 0.0f;
-      float tn = lane < C ? T.at(lane) : 0.0f;
+      float tn = T.at(lane);
       for (int j = 0; j < nch; ++j) {
         const float tl = tn;
-        if (j + 1 < nch) tn = lane < C ? T.at(C * (j + 1) + lane) : 0.0f;
+        if (j + 1 < nch) tn = T.at(kFxC * (j + 1) + lane);
         if (RUN && lane == 0) S.start[j] = s;
 #pragma unroll 8
-        for (int q = 0; q < C; ++q) s = s + rdl(tl, q);
+        for (int q = 0; q < kFxC; ++q) s = s + rdl(tl, q);
       }
       res = s;
     } else {
       const bool neg = (f & kNeg) && !(f & kPos);
       int E = kEMin, k = 0, j = 0;
       while (j < nch) {
-        const int jj = j + lane;
-        const uint32_t e = jj < nch ? S.e[jj] : kNoEntry;
-        const bool valid = e != kNoEntry && entry_domain(e) == E;
-        const int dl = valid ? entry_units(e) : 0;
-        const int inc = wave_incl_scan(dl, lane);
-        const bool ok = valid && k + inc <= kK24;
-        const uint64_t badm = ~__ballot(ok);
-        const int fc = badm == 0ull ? 64 : __builtin_ctzll(badm);
-        if (RUN && lane < fc && jj < nch) S.start[jj] = value_of(E, k + inc - dl);
-        if (fc > 0) {
-          k += rdl(inc, fc - 1);
-          normalise(&E, &k);
+        int dq[4];
+        bool vq[4];
+        int tot = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = j + 4 * lane + q;
+          const uint32_t e = m < nch ? S.e[m] : kNoEntry;
+          vq[q] = e != kNoEntry && entry_domain(e) == E;
+          dq[q] = vq[q] ? entry_units(e) : 0;
+          tot += dq[q];
         }
+        tot = min(tot, kK24 + 1);  // (anything above 2^24 fails anyway; no scan overflow)
+        const int excl = wave_incl_scan(tot, lane) - tot;
+        // the lane's entries in order: each applies until the first that does
+        // not (its binade is not the state's, or past 2^(E+1))
+        int run = k + excl, fq = 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool stop = fq == 4 && (!vq[q] || run + dq[q] > kK24);
+          fq = stop ? q : fq;
+          run = fq == 4 ? run + dq[q] : run;
+        }
+        const uint64_t failm = __ballot(fq < 4);
+        const int L = failm ? __builtin_ctzll(failm) : 64;
+        if (RUN && lane <= L) {
+          int r2 = k + excl;
+          const int lim = lane < L ? 4 : fq;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int m = j + 4 * lane + q;
+            if (q < lim && m < nch) S.start[m] = value_of(E, r2);
+            r2 += dq[q];
+          }
+        }
+        const int fc = L < 64 ? 4 * L + rdl(fq, L) : 256;
+        k = rdl(run, L < 64 ? L : 63);
+        normalise(&E, &k);
         j += fc;
-        if (j < nch && fc < 64) {
+        if (j < nch && L < 64) {
           // chunk j term by term, one fp32 add per term
           const int sl = S.slot[j];
-          const float tl = lane < C ? (sl >= 0 ? S.st[sl][lane] : fabsf(T.at(C * j + lane))) : 0.0f;
+          const float tl = sl >= 0 ? S.st[sl][lane] : fabsf(T.at(kFxC * j + lane));
           float s = value_of(E, k);
           if (RUN && lane == 0) S.start[j] = s;
 #pragma unroll 8
-          for (int q = 0; q < C; ++q) s = s + rdl(tl, q);
+          for (int q = 0; q < kFxC; ++q) s = s + rdl(tl, q);
           state_of(s, &E, &k);
           normalise(&E, &k);
           ++j;
@@ -936,17 +989,17 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
 }
 
 // One chain per workgroup: out[id * ldo + i].
-template <int SRC, int K, int C>
+template <int SRC, int K>
 __global__ __launch_bounds__(kFxThreads) void k_fx_chain(FxArgs a) {
   constexpr int KC = K > 0 ? K : 1;
-  __shared__ FxShared<C> S;
+  __shared__ FxShared S;
   const int g = blockIdx.x / KC, i = blockIdx.x % KC;
   int id;
   if (!fx_group(a, g, &id)) return;  // (workgroup-uniform)
   FxTerms<SRC, K> T;
   T.init(a, id, i);
   uint32_t f;
-  fx_walk<SRC, K, C, false>(a, T, S, &f, id, i);
+  fx_walk<SRC, K, false>(a, T, S, &f, id, i);
   if (threadIdx.x == 0) a.out[(long long)id * a.ldo + i] = S.res;
 }
 
@@ -954,49 +1007,78 @@ __global__ __launch_bounds__(kFxThreads) void k_fx_chain(FxArgs a) {
 // and forwardSampling's 9 x N draws from it (:311-366), as k_fc_* + k_fc_cdf +
 // k_tree_sample do in four launches: out[0] = the row's sum, cdf[x] every
 // running sum, then counts[a * 16 + z] and the kept children z * 9 + a in
-// std::set order (klist, *kcount).  The state of a draw is the first x with
-// cdf[x] >= r: on a non-decreasing cdf (no negative or non-finite cell) the
-// first chunk whose last running sum reaches r (a search of S.end in LDS),
-// then the first such cell inside it; else the plain binary search.
-template <int C>
+// std::set order (klist, *kcount).  The running sums: each wave takes its
+// chunks 16 at a time through a wave-private LDS tile (coalesced loads in,
+// lane c < 16 runs chunk c's 64 adds from its exact start value, coalesced
+// stores out).  The state of a draw is the first x with cdf[x] >= r: on a
+// non-decreasing cdf (no negative or non-finite cell) the first 16 cells
+// whose last running sum reaches r (a search in LDS), then the first such
+// cell among them; else the plain binary search.
+constexpr int kFxTileLd = kFxC + 4;  // (a padded tile row: lanes 0..15 on distinct banks)
 __global__ __launch_bounds__(kFxThreads) void k_fx_cdf_sample(FxArgs a, SampleArgs s) {
-  __shared__ FxShared<C> S;
+  __shared__ FxShared S;
   __shared__ int cnt[144];
-  __shared__ float sub[kFxThreads * C / 16];  // the last running sum of every 16 cells
-  const int tid = threadIdx.x;
+  __shared__ float sub[kFxThreads * kFxC / 16];  // the last running sum of every 16 cells
+  __shared__ __attribute__((aligned(16))) float tile[16][16 * kFxTileLd];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int q = tid; q < 144; q += kFxThreads) cnt[q] = 0;
   FxTerms<FX_ROW, 0> T;
   T.init(a, a.g0, 0);
   uint32_t f;
-  fx_walk<FX_ROW, 0, C, true>(a, T, S, &f, a.g0, 0);
-  const int n = a.n, nch = (n + C - 1) / C, x0 = C * tid;
+  fx_walk<FX_ROW, 0, true>(a, T, S, &f, a.g0, 0);
+  const int n = a.n, nch = (n + kFxC - 1) / kFxC;
   const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
   const bool neg = (f & kNeg) && !(f & kPos);
-  if (tid < nch) {
-    // every running sum of the chunk from its exact start value: signed terms
-    // after a mixed chain, else |terms| (one sign) negated back; 16-B stores
-    // (x0 + C <= the row stride: cells past n get a running sum too, inside
-    // the row's zero tail)
-    float v = S.start[tid];
-#pragma unroll 4
-    for (int q4 = 0; q4 < C / 4; ++q4) {
-      float b[4], t[4];
-      T.at4(x0 + 4 * q4, b, t);
-      f4a o;
+  float* tl = tile[w];
+  for (int r16 = 0; r16 < 4; ++r16) {
+    const int j0 = 64 * w + 16 * r16;  // this round's 16 chunks = 1024 cells from x0
+    if (j0 >= nch) break;  // (wave-uniform)
+    const int x0 = kFxC * j0;
+    // in: 4 KB of terms, coalesced (signed after a mixed chain, else |terms|)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v = v + (seq_all ? t[q] : fabsf(t[q]));
-        o[q] = seq_all || !neg ? v : (v == 0.0f ? 0.0f : -v);
-      }
-      *reinterpret_cast<f4a*>(a.cdf + x0 + 4 * q4) = o;
-      if (q4 % 4 == 3) sub[(x0 + 4 * q4) / 16] = v;
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int xl = 256 * q4 + 4 * lane;  // cell within the round
+      float b[4] = {0.0f, 0.0f, 0.0f, 0.0f}, t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (x0 + xl < n) T.at4(x0 + xl, b, t);
+      const int c = xl / kFxC, o = xl % kFxC;
+      *reinterpret_cast<f4a*>(&tl[c * kFxTileLd + o]) =
+          seq_all ? f4a{t[0], t[1], t[2], t[3]}
+                  : f4a{fabsf(t[0]), fabsf(t[1]), fabsf(t[2]), fabsf(t[3])};
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // chunk j0 + lane: its 64 running sums in place, from the exact start value
+    if (lane < 16 && j0 + lane < nch) {
+      float v = S.start[j0 + lane];
+      float* row = &tl[lane * kFxTileLd];
+#pragma unroll 8
+      for (int q = 0; q < kFxC; ++q) {
+        v = v + row[q];
+        row[q] = seq_all || !neg ? v : (v == 0.0f ? 0.0f : -v);
+        if (q % 16 == 15) sub[(x0 + lane * kFxC + q) / 16] = v;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // out: coalesced 16-B stores (cells in [n, ld) get running sums inside the
+    // row's zero tail; none past the row stride)
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int xl = 256 * q4 + 4 * lane;
+      const int c = xl / kFxC, o = xl % kFxC;
+      if (x0 + xl < a.ld)
+        *reinterpret_cast<f4a*>(a.cdf + x0 + xl) =
+            *reinterpret_cast<const f4a*>(&tl[c * kFxTileLd + o]);
+    }
+    __builtin_amdgcn_wave_barrier();  // (the tile's next round)
   }
+  fx_stamp(a, 5);
   if (tid == 0) a.out[0] = S.res;
   const int N = s.N, W = s.g.width;
   if (N <= 0) return;  // (the running sums only)
   __syncthreads();  // (the cdf: stores of this workgroup, visible to it after the barrier)
-  fx_stamp(a, 5);
   const bool mono = !(f & kNeg) && !(f & kBad);
   const float* __restrict__ cdf = a.cdf;
   for (int jt = tid; jt < 9 * N; jt += kFxThreads) {
@@ -1246,31 +1328,18 @@ hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcAr
 }
 
 namespace {
-// terms per thread of a fused chain set over n cells (0: too long for one workgroup)
-int fx_terms_per_thread(int n) {
-  return n <= 0 ? 0 : n <= 16 * kFxThreads ? 16 : n <= 32 * kFxThreads ? 32
-                                                  : n <= 64 * kFxThreads ? 64 : 0;
-}
-
 template <int SRC, int K>
 hipError_t launch_fx_set(hipStream_t st, int groups, const FxArgs& a0) {
   constexpr int KC = K > 0 ? K : 1;
   FxArgs a = a0;
   a.ngroups = groups;
-  const dim3 grid((unsigned)(groups * KC)), block(kFxThreads);
-  switch (fx_terms_per_thread(a.n)) {
-    case 16: hipLaunchKernelGGL((k_fx_chain<SRC, K, 16>), grid, block, 0, st, a); break;
-    case 32: hipLaunchKernelGGL((k_fx_chain<SRC, K, 32>), grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL((k_fx_chain<SRC, K, 64>), grid, block, 0, st, a); break;
-  }
+  hipLaunchKernelGGL((k_fx_chain<SRC, K>), dim3((unsigned)(groups * KC)), dim3(kFxThreads), 0, st,
+                     a);
   return hipGetLastError();
 }
 }  // namespace
 
-bool fx_fits(int n, int ld) {
-  const int C = fx_terms_per_thread(n);
-  return C > 0 && ld >= n && ld % 64 == 0;
-}
+bool fx_fits(int n, int ld) { return n > 0 && n <= kFxC * kFxThreads && ld >= n && ld % 64 == 0; }
 
 hipError_t launch_fx(hipStream_t st, int base, int K, int groups, const FxArgs& a) {
   if (groups <= 0) return hipSuccess;
@@ -1300,11 +1369,7 @@ hipError_t launch_fx_cdf_sample(hipStream_t st, const FxArgs& a0, const SampleAr
   a.ngroups = 1;
   a.glist = nullptr;
   a.gcount = nullptr;
-  switch (fx_terms_per_thread(a.n)) {
-    case 16: hipLaunchKernelGGL(k_fx_cdf_sample<16>, dim3(1), dim3(kFxThreads), 0, st, a, s); break;
-    case 32: hipLaunchKernelGGL(k_fx_cdf_sample<32>, dim3(1), dim3(kFxThreads), 0, st, a, s); break;
-    default: hipLaunchKernelGGL(k_fx_cdf_sample<64>, dim3(1), dim3(kFxThreads), 0, st, a, s); break;
-  }
+  hipLaunchKernelGGL(k_fx_cdf_sample, dim3(1), dim3(kFxThreads), 0, st, a, s);
   return hipGetLastError();
 }
 
