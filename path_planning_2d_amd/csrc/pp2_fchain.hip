@@ -26,6 +26,7 @@
 // (:176-183); k_tree_sample restates forwardSampling's draws (:311-366).
 #include <hip/hip_runtime.h>
 #include <float.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <utility>
@@ -529,6 +530,219 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- walker (round 6)
+// k_fc_drive's job for chains of at most kWkEntries chunks (n <= 262144), in
+// fewer dependent steps: the chain's entries, flags and predicted fallback
+// chunks come in two round trips (the entries and flags together, then every
+// predicted chunk's terms together into LDS), a step of the walk takes 256
+// entries (4 per lane, branch-free), the first chunk runs as lane 0's own fp32
+// chain on VGPR operands (~7 cycles an add: it climbs through many binades,
+// an exact round each otherwise), every later fallback chunk as exact rounds
+// (chunk_exact).  Same outputs as k_fc_drive (out, and with cdf the chunk
+// start states in cst): tests/test_gpu_fchain.py runs both.
+constexpr int kWkEntries = 1024;  // chunk entries in LDS
+constexpr int kWkStash = 16;      // predicted fallback chunks staged in LDS
+
+template <int BASE, int K>
+__global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
+  constexpr int KC = K > 0 ? K : 1;
+  __shared__ uint32_t sE[kWkEntries];
+  __shared__ short sSlot[kWkEntries];
+  __shared__ __attribute__((aligned(16))) float sSt[kWkStash][kFcChunk];
+  for (int ch = blockIdx.x;; ch += gridDim.x) {  // (one wave: uniform)
+  const int g = ch / KC, i = ch % KC;
+  int id;
+  if (!group_id(a, g, &id)) return;
+  Terms<BASE, K> T;
+  T.init(a, id);
+  const int lane = threadIdx.x;
+  const int n = a.n, nch = fc_chunks(n), nseg = fc_segments(n);
+  const uint2* tab = a.tab + (long long)ch * nch;
+  const bool cdf = BASE == FC_ROW && K == 0 && a.cdf != nullptr;
+  // 1. flags and entries (one round trip); stash slots for the predicted chunks
+  uint32_t f = 0u;
+  for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)ch * nseg + s];
+  int nst = 0;
+  for (int c0 = 0; c0 < nch; c0 += 64) {
+    const int c = c0 + lane;
+    const uint2 t = c < nch ? tab[c] : make_uint2(kNoEntry, 0u);
+    const bool pr = c < nch && (t.y & kPredicted);
+    const uint64_t m = __ballot(pr);
+    const int sl = nst + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (c < nch) {
+      sE[c] = t.x;
+      sSlot[c] = (short)(pr && sl < kWkStash ? sl : -1);
+    }
+    nst += __popcll(m);
+  }
+  f = (__ballot((f & kPos) != 0u) ? kPos : 0u) | (__ballot((f & kNeg) != 0u) ? kNeg : 0u) |
+      (__ballot((f & kBad) != 0u) ? kBad : 0u);
+  if (cdf && lane == 0) a.cst[nch] = make_int2((int)f, 0);
+  const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
+  const bool neg = (f & kNeg) && !(f & kPos);
+  nst = min(nst, kWkStash);
+  __syncthreads();
+  // 2. the predicted chunks' |terms| (all in flight together)
+  if (!seq_all) {
+    int ids[kWkStash];
+#pragma unroll
+    for (int s = 0; s < kWkStash; ++s) ids[s] = -1;
+    for (int c0 = 0; c0 < nch; c0 += 64) {  // slot -> chunk
+      const int c = c0 + lane;
+      const int sl = c < nch ? sSlot[c] : -1;
+#pragma unroll
+      for (int s = 0; s < kWkStash; ++s) {
+        const uint64_t m = __ballot(sl == s);
+        if (m) ids[s] = c0 + __builtin_ctzll(m);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kWkStash; h += 8) {
+      float st[8][4];
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (h + s < nst) T.terms4(i, ids[h + s] * kFcChunk + 4 * lane, st[s]);
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (h + s < nst)
+          *reinterpret_cast<f4a*>(&sSt[h + s][4 * lane]) =
+              f4a{fabsf(st[s][0]), fabsf(st[s][1]), fabsf(st[s][2]), fabsf(st[s][3])};
+    }
+  }
+  __syncthreads();
+  float res;
+  if (seq_all) {
+    // mixed signs or a non-finite term: the reference's chain itself
+    float s = 0.0f;
+    for (int j = 0; j < nch; ++j) {
+      float t[4];
+      T.terms4(i, j * kFcChunk + 4 * lane, t);
+      float cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int l = 0; l < 64; ++l) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          s = s + rdl(t[q], l);
+          if (lane == l) cv[q] = s;
+        }
+      }
+      if (cdf) {
+        const int x0 = j * kFcChunk + 4 * lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (x0 + q < n) a.cdf[x0 + q] = cv[q];
+      }
+    }
+    res = s;
+  } else {
+    int E = kEMin, k = 0, j = 0;
+    while (j < nch) {
+      // a step: entries j .. j + 255, 4 per lane (branch-free reads)
+      uint32_t ev[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ev[q] = sE[min(j + 4 * lane + q, nch - 1)];
+      const uint32_t ebias = (uint32_t)(E + 128);
+      int dq[4], tot = 0;
+      bool vq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        vq[q] = (j + 4 * lane + q < nch) & (ev[q] != kNoEntry) & ((ev[q] >> 24) == ebias);
+        dq[q] = vq[q] ? (int)(ev[q] & 0xffffffu) : 0;
+        tot += dq[q];
+      }
+      tot = min(tot, kK24 + 1);
+      const int excl = wave_incl_scan(tot, lane) - tot;
+      int run = k + excl, fq = 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool stop = fq == 4 && (!vq[q] || run + dq[q] > kK24);
+        fq = stop ? q : fq;
+        run = fq == 4 ? run + dq[q] : run;
+      }
+      const uint64_t failm = __ballot(fq < 4);
+      const int L = failm ? __builtin_ctzll(failm) : 64;
+      if (cdf && lane <= L) {
+        int r2 = k + excl;
+        const int lim = lane < L ? 4 : fq;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = j + 4 * lane + q;
+          if (q < lim && m < nch) a.cst[m] = make_int2(E, r2);
+          r2 += dq[q];
+        }
+      }
+      const int fc = L < 64 ? 4 * L + rdl(fq, L) : 256;
+      k = rdl(run, L < 64 ? L : 63);
+      normalise(&E, &k);
+      j += fc;
+      if (j < nch && L < 64) {
+        // chunk j term by term
+        if (cdf && lane == 0) a.cst[j] = make_int2(E, k);
+        const int sl = sSlot[j];
+        if (j == 0) {
+          // from zero: lane 0's fp32 chain, 16 terms per batch of LDS reads
+          float s = value_of(E, k);
+          if (lane == 0) {
+            for (int h = 0; h < kFcChunk; h += 16) {
+              float v[16];
+              if (sl >= 0) {
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                  const f4a u = *reinterpret_cast<const f4a*>(&sSt[sl][h + 4 * q4]);
+                  v[4 * q4] = u[0];
+                  v[4 * q4 + 1] = u[1];
+                  v[4 * q4 + 2] = u[2];
+                  v[4 * q4 + 3] = u[3];
+                }
+              } else {
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                  float t[4];
+                  T.terms4(i, h + 4 * q4, t);
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) v[4 * q4 + q] = fabsf(t[q]);
+                }
+              }
+#pragma unroll
+              for (int q = 0; q < 16; ++q) s = s + v[q];
+            }
+          }
+          s = rdl(s, 0);
+          state_of(s, &E, &k);
+        } else {
+          float t[4];
+          if (sl >= 0) {
+            const f4a u = *reinterpret_cast<const f4a*>(&sSt[sl][4 * lane]);
+            t[0] = u[0];
+            t[1] = u[1];
+            t[2] = u[2];
+            t[3] = u[3];
+          } else {
+            T.terms4(i, j * kFcChunk + 4 * lane, t);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t[q] = fabsf(t[q]);
+          }
+          chunk_exact(t, lane, &E, &k, nullptr);
+        }
+        normalise(&E, &k);
+        ++j;
+      }
+    }
+    const float r = value_of(E, k);
+    res = neg ? (r == 0.0f ? 0.0f : -r) : r;
+  }
+  if (lane == 0) {
+    if (BASE == FC_LIST) {  // out[row * ldo + partner]
+      const int2 e = a.plist[id];
+      a.out[(long long)e.x * a.ldo + e.y] = res;
+    } else {
+      a.out[(long long)id * a.ldo + i] = res;
+    }
+  }
+  __syncthreads();  // (the LDS of the next chain)
+  }
+}
+
 // ---------------------------------------------------------------- running sums
 // One wave per chunk: every running sum of the row from the chunk's exact
 // start state (k_fc_drive's a.cst), term by term (chunk_exact).
@@ -644,14 +858,17 @@ __global__ __launch_bounds__(256) void k_store_kept(const int* __restrict__ klis
                                                     const float* __restrict__ pred,
                                                     const float* __restrict__ lrows,
                                                     const float* __restrict__ sums,
-                                                    float* __restrict__ dst, int n, int ld) {
+                                                    float* __restrict__ dst, int n, int ld,
+                                                    FcRowTable rows) {
   const int r = blockIdx.y;
   if (r >= *kcount) return;
   const int x = blockIdx.x * 256 + threadIdx.x;
   if (x >= n) return;
   const int c = klist[r];
   const float v = ftz(pred[(long long)(c % 9) * ld + x] * ftz(lrows[(long long)(c / 9) * ld + x]));
-  dst[(long long)c * ld + x] = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
+  const float b = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
+  dst[(long long)c * ld + x] = b;
+  if (rows.use) rows.p[c][x] = b;
 }
 
 // ================================================================ fused chain sets
@@ -675,6 +892,7 @@ __global__ __launch_bounds__(256) void k_store_kept(const int* __restrict__ klis
 // plan step's critical path, profiles/r05 kernel_stats_plan_*) become one.
 constexpr int kFxThreads = 1024;
 constexpr int kFxStash = 32;  // predicted fallback chunks whose |terms| wave 0 reads from LDS
+constexpr uint32_t kFxZero = 0xfffffffeu;  // entry of a chunk of zero terms: applies in any binade
 
 // inclusive float scan of a wave (any association: approximate running sums)
 __device__ __forceinline__ float wave_incl_scan_f(float v, int lane) {
@@ -822,7 +1040,7 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
       store = a.rows_out ? a.rows_out + (long long)id * a.ld : nullptr;
       store2 = a.use_dst ? a.dst[id] : nullptr;
     }
-#pragma unroll 4
+#pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int j = 64 * w + 4 * g + rw, x = kFxC * j + 4 * c16;
       float b[4] = {0.0f, 0.0f, 0.0f, 0.0f}, t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -866,13 +1084,16 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
   const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
   // C: each chunk's entry; the predicted fallbacks' |terms| into the stash
   if (!seq_all) {
-#pragma unroll 2
+    float bef[16];  // (the 16 chunks' running sums read together)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) bef[g] = S.cb[64 * w + 4 * g + rw];
+#pragma unroll 4
     for (int g = 0; g < 16; ++g) {
       const int j = 64 * w + 4 * g + rw, x = kFxC * j + 4 * c16;
       if (64 * w + 4 * g >= nch) break;  // (wave-uniform)
       float b[4] = {0.0f, 0.0f, 0.0f, 0.0f}, t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       if (x < n) T.at4(x, b, t);
-      const float before = S.cb[j < nch ? j : 0];
+      const float before = bef[g];
       const int E = domain_of(before);
       int d = 0;
       bool tie = false;
@@ -885,25 +1106,33 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
       }
       d = row_total_i(d);  // (<= 64 (2^24 + 1) < 2^31)
       const bool rtie = ((__ballot(tie) >> (16 * rw)) & 0xffffull) != 0ull;
-      int sl = -1;
-      if (c16 == 15 && j < nch) {
-        uint32_t e = kNoEntry;
-        if (!rtie && d < kK24 && E <= 127) e = ((uint32_t)(E + 128) << 24) | (uint32_t)d;
-        const float pu = ldexpf(before, 23 - E);  // the running sum in units of E
-        const bool pred = e == kNoEntry || j == 0 ||
-                          pu + (float)d >= (float)kK24 * (1.0f - 0x1p-12f) ||
-                          pu < (float)(1 << 23) * (1.0f + 0x1p-10f);
-        S.e[j] = e;
-        if (pred) {
+      // a chunk of +0 terms (|t|: every term +-0) leaves any state as it is
+      const bool zero = __ballot(t[0] != 0.0f || t[1] != 0.0f || t[2] != 0.0f || t[3] != 0.0f) >>
+                            (16 * rw) & 0xffffull ? false : true;
+      uint32_t e = kNoEntry;
+      if (!rtie && d < kK24 && E <= 127) e = ((uint32_t)(E + 128) << 24) | (uint32_t)d;
+      const float pu = ldexpf(before, 23 - E);  // the running sum in units of E
+      const bool pred = j < nch && (j == 0 || (!zero && (e == kNoEntry ||
+                        pu + (float)d >= (float)kK24 * (1.0f - 0x1p-12f) ||
+                        pu < (float)(1 << 23) * (1.0f + 0x1p-10f))));
+      if (zero) e = kFxZero;
+      if (c16 == 15 && j < nch) S.e[j] = e;
+      // (d, E, before are the row's in its lane 15: pred is read there)
+      const uint64_t pm = __ballot(c16 == 15 && pred);
+      if (pm) {  // a predicted fallback in this wave's 4 chunks: stash its |terms|
+        int sl = -1;
+        if (c16 == 15 && pred) {
           sl = atomicAdd(&S.nst, 1);
           if (sl >= kFxStash) sl = -1;
         }
-        S.slot[j] = sl;
+        sl = __shfl(sl, lane | 15);
+        if (sl >= 0)
+          *reinterpret_cast<f4a*>(&S.st[sl][4 * c16]) =
+              f4a{fabsf(t[0]), fabsf(t[1]), fabsf(t[2]), fabsf(t[3])};
+        if (c16 == 15 && j < nch) S.slot[j] = sl;
+      } else if (c16 == 15 && j < nch) {
+        S.slot[j] = -1;
       }
-      sl = __shfl(sl, lane | 15);
-      if (sl >= 0)
-        *reinterpret_cast<f4a*>(&S.st[sl][4 * c16]) =
-            f4a{fabsf(t[0]), fabsf(t[1]), fabsf(t[2]), fabsf(t[3])};
     }
   }
   __syncthreads();
@@ -927,16 +1156,26 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
     } else {
       const bool neg = (f & kNeg) && !(f & kPos);
       int E = kEMin, k = 0, j = 0;
+      unsigned n_it = 0, n_fb = 0, n_miss = 0;
+      unsigned long long cy_step = 0, cy_fb = 0;  // (diagnostics: shader clocks)
       while (j < nch) {
+        ++n_it;
+        const unsigned long long c0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+        // (branch-free: the 4 LDS reads go out together, one wait)
+        uint32_t ev[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ev[q] = S.e[min(j + 4 * lane + q, nch - 1)];
         int dq[4];
         bool vq[4];
         int tot = 0;
+        const uint32_t ebias = (uint32_t)(E + 128);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int m = j + 4 * lane + q;
-          const uint32_t e = m < nch ? S.e[m] : kNoEntry;
-          vq[q] = e != kNoEntry && entry_domain(e) == E;
-          dq[q] = vq[q] ? entry_units(e) : 0;
+          const uint32_t e = ev[q];
+          const bool in = j + 4 * lane + q < nch;
+          const bool z = e == kFxZero;
+          vq[q] = in & (z | ((e != kNoEntry) & ((e >> 24) == ebias)));
+          dq[q] = (vq[q] & !z) ? (int)(e & 0xffffffu) : 0;
           tot += dq[q];
         }
         tot = min(tot, kK24 + 1);  // (anything above 2^24 fails anyway; no scan overflow)
@@ -966,21 +1205,61 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
         k = rdl(run, L < 64 ? L : 63);
         normalise(&E, &k);
         j += fc;
+        const unsigned long long c1 = a.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+        cy_step += c1 - c0;
         if (j < nch && L < 64) {
-          // chunk j term by term, one fp32 add per term
+          // chunk j term by term, one fp32 add per term: lane 0 runs the
+          // chain on VGPR operands (~7 cycles an add; through readlane /
+          // SGPR operands it was ~45), from the stash or the terms formed again
           const int sl = S.slot[j];
-          const float tl = sl >= 0 ? S.st[sl][lane] : fabsf(T.at(kFxC * j + lane));
+          ++n_fb;
+          n_miss += sl < 0;
           float s = value_of(E, k);
           if (RUN && lane == 0) S.start[j] = s;
-#pragma unroll 8
-          for (int q = 0; q < kFxC; ++q) s = s + rdl(tl, q);
+          if (lane == 0) {
+#pragma unroll
+            for (int h = 0; h < kFxC / 16; ++h) {
+              float v[16];
+              if (sl >= 0) {
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                  const f4a u = *reinterpret_cast<const f4a*>(&S.st[sl][16 * h + 4 * q4]);
+                  v[4 * q4] = u[0];
+                  v[4 * q4 + 1] = u[1];
+                  v[4 * q4 + 2] = u[2];
+                  v[4 * q4 + 3] = u[3];
+                }
+              } else {
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                  float b[4], t[4];
+                  T.at4(kFxC * j + 16 * h + 4 * q4, b, t);
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) v[4 * q4 + q] = fabsf(t[q]);
+                }
+              }
+#pragma unroll
+              for (int q = 0; q < 16; ++q) s = s + v[q];
+            }
+          }
+          s = rdl(s, 0);
           state_of(s, &E, &k);
           normalise(&E, &k);
           ++j;
+          if (a.stamps) cy_fb += __builtin_amdgcn_s_memtime() - c1;
         }
       }
       const float r = value_of(E, k);
       res = neg ? (r == 0.0f ? 0.0f : -r) : r;
+      if (a.stamps && lane == 0 && !RUN) {  // the clocks of the steps and the fallbacks
+        a.stamps[8 * (long long)blockIdx.x + 5] = cy_step;
+        a.stamps[8 * (long long)blockIdx.x + 6] = cy_fb;
+      }
+      if (a.stamps && lane == 0)  // diagnostics: walk steps, fallback chunks, stash misses, predicted
+        a.stamps[8 * (long long)blockIdx.x + 7] =
+            (unsigned long long)min(n_it, 1023u) | ((unsigned long long)min(n_fb, 1023u) << 10) |
+            ((unsigned long long)min(n_miss, 1023u) << 20) |
+            ((unsigned long long)min(S.nst, 1023) << 30);
     }
     if (lane == 0) S.res = res;
   }
@@ -1282,6 +1561,14 @@ __global__ __launch_bounds__(256) void k_pbvi_cands(PbviCandArgs c) {
 constexpr int kFcGroupBlocks = 16384;  // sums / tables: segments x groups per launch
 constexpr int kFcDriveBlocks = 8192;   // drive: one wave per chain
 
+// k_fc_walk for chains of at most kWkEntries chunks (PP2_FC_WALK=0, or
+// pp2_debug_fc_walk(0): k_fc_drive everywhere)
+int g_fc_walk = -1;
+bool fc_walk_enabled() {
+  if (g_fc_walk < 0) g_fc_walk = !(getenv("PP2_FC_WALK") && getenv("PP2_FC_WALK")[0] == '0');
+  return g_fc_walk != 0;
+}
+
 template <int BASE, int K>
 hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) {
   constexpr int KC = K > 0 ? K : 1;
@@ -1294,8 +1581,12 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
     hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
   }
   if (phases & FC_DRIVE) {
-    hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(std::min(groups * KC, kFcDriveBlocks)), dim3(64),
-                       0, st, a);
+    if (fc_walk_enabled() && fc_chunks(a.n) <= kWkEntries)
+      hipLaunchKernelGGL((k_fc_walk<BASE, K>), dim3(std::min(groups * KC, kFcDriveBlocks)),
+                         dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(std::min(groups * KC, kFcDriveBlocks)),
+                         dim3(64), 0, st, a);
     if (BASE == FC_ROW && K == 0 && a.cdf)
       hipLaunchKernelGGL(k_fc_cdf, dim3((fc_chunks(a.n) + 3) / 4), dim3(256), 0, st, a);
   }
@@ -1408,10 +1699,12 @@ hipError_t launch_store_children(hipStream_t st, const FcStoreList& L, const flo
 
 hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount,
                              const float* pred, const float* lrows, const float* sums, float* dst,
-                             int n, int ld) {
+                             int n, int ld, const FcRowTable* rows) {
   if (n <= 0) return hipSuccess;
+  FcRowTable t;
+  if (rows) t = *rows;
   hipLaunchKernelGGL(k_store_kept, dim3((n + 255) / 256, 144), dim3(256), 0, st, klist, kcount,
-                     pred, lrows, sums, dst, n, ld);
+                     pred, lrows, sums, dst, n, ld, t);
   return hipGetLastError();
 }
 
@@ -1821,4 +2114,12 @@ extern "C" int pp2_debug_pbvi_cands(int n, int R, const float* x, int S, const f
                   (void*)dexact, (void*)dv, (void*)didx, (void*)dlist, (void*)dcnt})
     if (p) (void)hipFree(p);
   return st;
+}
+
+// Diagnostic (tests): choose the chain-set driver -- 1: k_fc_walk where it
+// fits (the default), 0: k_fc_drive everywhere.  Returns the previous choice.
+extern "C" int pp2_debug_fc_walk(int on) {
+  const int prev = pp2::fc_walk_enabled() ? 1 : 0;
+  pp2::g_fc_walk = on ? 1 : 0;
+  return prev;
 }

@@ -265,9 +265,14 @@ hipError_t launch_store_children(hipStream_t st, const FcStoreList& L, const flo
                                  const float* lrows, const float* sums, int n, int ld);
 // The same for the children listed on the device (klist[r], r < *kcount, at
 // most 144): child c into dst + c * ld.
+// rows (optional): child c's row also into rows->p[c] (the planner's node rows)
+struct FcRowTable {
+  int use = 0;
+  float* p[144] = {};
+};
 hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount,
                              const float* pred, const float* lrows, const float* sums, float* dst,
-                             int n, int ld);
+                             int n, int ld, const FcRowTable* rows = nullptr);
 
 // ---- pp2_pbvi_dev.hip (FTZ): the 9 action predictions of cudaBayesBeliefUpdate
 // before the likelihood product: pred[u][idx] = sum_s T[sidx][u][8-s] * b[sidx]

@@ -192,15 +192,17 @@ struct pp2_planner {
   // plan step: p50 2.54 vs 3.34-3.51 ms (profiles/r05/chain_walk_ab.txt).
   bool seq = false;
   // larger grids up to 65536 cells (PP2_FX=0: off): each chain set as ONE
-  // launch, a workgroup per chain holding its terms in registers (pp2::launch_fx,
-  // launch_fx_cdf_sample), and the kept children's rows stored straight into
-  // rows acquired for all 144 children before the expansion (pre[c])
+  // launch, a workgroup per chain (pp2::launch_fx, launch_fx_cdf_sample)
   bool fx = false;
+  // reference order: a node row for each of the 144 children, acquired before
+  // an expansion is enqueued; the kept children's rows are stored straight
+  // into theirs by the expansion's kernels (no store after the host's wait)
   std::vector<int> pre;
   // PP2_FX_STAMPS=1 (diagnostics): the fused kernels' phase clocks, 8 per
   // workgroup, summed per kernel and phase, printed when the planner goes
   unsigned long long* d_stamps = nullptr;
   double fx_phase[4][8] = {};
+  double fx_count[4][4] = {};  // walk steps, fallback chunks, stash misses, predicted chunks
   long long fx_groups[4] = {}, fx_sets = 0;
   int ref_ld = 0;               // dense row length (multiple of 64, zero tail)
   float* d_rrows = nullptr;     // [9][ld] R[.][a]
@@ -792,6 +794,11 @@ void fx_stamps_collect(pp2_planner* p) {
       const int np = k == 0 ? 6 : 4;
       for (int ph = 0; ph < np; ++ph)
         if (t[ph + 1] >= t[ph]) p->fx_phase[k][ph] += (double)(t[ph + 1] - t[ph]) * 0.01;
+      for (int c = 0; c < 4; ++c) p->fx_count[k][c] += (double)((t[7] >> (10 * c)) & 1023u);
+      if (k > 0) {  // the walker's shader clocks in steps / fallbacks (k_fx_chain)
+        p->fx_phase[k][5] += (double)t[5];
+        p->fx_phase[k][6] += (double)t[6];
+      }
       first = std::min(first, t[0]);
       last = std::max(last, t[np]);
     }
@@ -807,10 +814,15 @@ void fx_stamps_print(pp2_planner* p) {
     const double g = p->fx_groups[k] ? (double)p->fx_groups[k] : 1.0;
     std::fprintf(stderr,
                  "fx %-11s: %6.1f workgroups/set; per workgroup us: A %.2f B %.2f C %.2f walk %.2f"
-                 " cdf %.2f samples %.2f; set span %.2f us\n",
+                 " cdf %.2f samples %.2f (chains: step / fallback kclk); set span %.2f us; per"
+                 " chain: steps %.1f fallbacks %.1f misses %.1f predicted %.1f\n",
                  names[k], g / (double)p->fx_sets, p->fx_phase[k][0] / g, p->fx_phase[k][1] / g,
-                 p->fx_phase[k][2] / g, p->fx_phase[k][3] / g, p->fx_phase[k][4] / g,
-                 p->fx_phase[k][5] / g, p->fx_phase[k][7] / (double)p->fx_sets);
+                 p->fx_phase[k][2] / g, p->fx_phase[k][3] / g,
+                 k ? p->fx_phase[k][5] / g / 1e3 : p->fx_phase[k][4] / g,
+                 k ? p->fx_phase[k][6] / g / 1e3 : p->fx_phase[k][5] / g,
+                 p->fx_phase[k][7] / (double)p->fx_sets,
+                 p->fx_count[k][0] / g, p->fx_count[k][1] / g, p->fx_count[k][2] / g,
+                 p->fx_count[k][3] / g);
   }
 }
 
@@ -843,7 +855,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   for (uint32_t a = 0; a < 9; ++a)
     for (uint32_t j = 0; j < N; ++j)
       p->h_r[a * N + j] = (float)p->rng.next() / ((float)RAND_MAX + 1.0f);
-  if (p->fx) {
+  {
     // a row for each of the 144 children, before anything is enqueued (a new
     // chunk of rows is zeroed on the main stream); the kept ones are stored
     // straight into theirs, the others go back after the wait
@@ -907,22 +919,25 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     if (p->d_stamps) r.stamps = p->d_stamps + 8 * kFxStampOff[2];
     HIPCHK(pp2::launch_fx(p->side, pp2::FX_ROW, 9, 1, r));
     HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
+    // the kept children normalised (one division per cell, here only) into
+    // their rows of d_children and their node rows, then their FIB dots
+    pp2::FcRowTable rt;
+    rt.use = 1;
+    for (int cc = 0; cc < 144; ++cc) rt.p[cc] = p->slots[p->pre[cc]].row;
+    HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
+                                  p->d_csum, p->d_children, (int)n, ld, &rt));
     pp2::FxArgs kd;
     kd.n = (int)n;
     kd.ld = ld;
-    kd.pred = p->d_pred;
-    kd.lrows = p->d_lrows;
-    kd.sums = p->d_csum;
+    kd.row = p->d_children;
+    kd.row_stride = ld;
     kd.partners = p->d_frows;
     kd.glist = p->d_klist;
     kd.gcount = p->d_kcount;
     kd.out = p->d_rout + 9;
     kd.ldo = 9;
-    kd.rows_out = p->pbvi ? p->d_children : nullptr;  // (the PBVI dots read them there)
-    kd.use_dst = 1;
-    for (int cc = 0; cc < 144; ++cc) kd.dst[cc] = p->slots[p->pre[cc]].row;
     if (p->d_stamps) kd.stamps = p->d_stamps + 8 * kFxStampOff[3];
-    HIPCHK(pp2::launch_fx(c->stream, pp2::FX_KEPT, 9, 144, kd));
+    HIPCHK(pp2::launch_fx(c->stream, pp2::FX_ROW, 9, 144, kd));
     if (p->pbvi) {
       HIPCHK(hipEventRecord(p->ev_kept, c->stream));
       HIPCHK(hipStreamWaitEvent(p->side, p->ev_kept, 0));
@@ -992,8 +1007,11 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
     // main: the kept children (sampled on this stream), normalised by their
     // masses (side) into their rows of d_children -- only they become nodes
+    pp2::FcRowTable rt;  // and straight into the rows acquired for them
+    rt.use = 1;
+    for (int cc = 0; cc < 144; ++cc) rt.p[cc] = p->slots[p->pre[cc]].row;
     HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
-                                  p->d_csum, p->d_children, (int)n, ld));
+                                  p->d_csum, p->d_children, (int)n, ld, &rt));
     // side: the kept children's PBVI dots (evaluatePbviCpu, the long chains),
     // beside main's FIB dots, after the rewards already queued there
     if (p->pbvi) {
@@ -1031,8 +1049,6 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   for (QNode* q : v->children)
     if (q) delete_subtree(p, q);
   v->children.assign(9, nullptr);
-  std::vector<int> keep;
-  std::vector<float*> rows;
   long long kept = 0;
   for (uint8_t a = 0; a < 9; ++a) {
     QNode* q = new QNode();
@@ -1049,26 +1065,16 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       cv->upper_bound = first_max9(p->h_rout + 9 + 9 * row);
       cv->lower_bound = p->pbvi ? p->h_lbv[row] : p->lb_const;
       cv->heuristic = cv->upper_bound - cv->lower_bound;
-      if (p->fx) {  // (already stored there)
-        cv->slot = p->pre[row];
-        p->pre[row] = -1;
-      } else {
-        CHECK(acquire_slot(p, &cv->slot));
-        keep.push_back(row);
-        rows.push_back(p->slots[cv->slot].row);
-      }
+      cv->slot = p->pre[row];  // (its row is stored there already)
+      p->pre[row] = -1;
       q->children.push_back(cv);
     }
     qnode_update(p, q);
     v->children[a] = q;
   }
-  if (p->fx) {
-    for (int& sl : p->pre) {
-      if (sl >= 0) release_slot(p, sl);
-      sl = -1;
-    }
-  } else {
-    CHECK(ref_store_children(p, keep.data(), rows.data(), (int)keep.size()));
+  for (int& sl : p->pre) {  // the rows of the children not kept go back
+    if (sl >= 0) release_slot(p, sl);
+    sl = -1;
   }
   p->stat_rows += kept;
   vnode_update(v);

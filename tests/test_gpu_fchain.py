@@ -93,7 +93,20 @@ def test_numpy_accumulate_is_the_sequential_chain(oracle):
     assert bits(seq(t)[0]) == bits(lib.orc_sum_seq(t.size, _ptr(t)))
 
 
-def test_fchain_sums_and_running_sums_bit_exact():
+@pytest.fixture(params=[1, 0], ids=["walk", "drive"])
+def driver(request):
+    """The chain sets' third pass: k_fc_walk (round 6, the default where a
+    chain has <= 1024 chunks) or k_fc_drive (every size)."""
+    from path_planning_2d_amd import _lib
+    f = _lib.load().pp2_debug_fc_walk
+    f.argtypes = [C.c_int]
+    f.restype = C.c_int
+    prev = f(request.param)
+    yield request.param
+    f(prev)
+
+
+def test_fchain_sums_and_running_sums_bit_exact(driver):
     rng = np.random.default_rng(11)
     for name, t in rows(rng):
         want, wc = seq(t)
@@ -103,7 +116,7 @@ def test_fchain_sums_and_running_sums_bit_exact():
             f"{name}: running sums differ at {np.flatnonzero(bits(gc) != bits(wc))[:5]}"
 
 
-def test_fchain_dots_bit_exact():
+def test_fchain_dots_bit_exact(driver):
     """inner_product(x, a_i): the product rounded, then the chain."""
     rng = np.random.default_rng(12)
     for name, t in rows(rng):
@@ -124,7 +137,7 @@ def test_fchain_dots_bit_exact():
             assert bits(got[i]) == bits(want), f"{name} partner {i}: {got[i]!r} != {want!r}"
 
 
-def test_fchain_pair_dots_bit_exact():
+def test_fchain_pair_dots_bit_exact(driver):
     """The planner's PBVI leaf dots (FC_LIST: evaluatePbviCpu's inner_product
     of a row with an alpha, point_based_value_iteration_cuda.cu:678-699, for
     a device list of (row, alpha) pairs): every listed dot equal to the
