@@ -532,37 +532,72 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
 
 // ---------------------------------------------------------------- walker (round 6)
 // k_fc_drive's job for chains of at most kWkEntries chunks (n <= 262144), in
-// fewer dependent steps: the chain's entries, flags and predicted fallback
-// chunks come in two round trips (the entries and flags together, then every
-// predicted chunk's terms together into LDS), a step of the walk takes 256
-// entries (4 per lane, branch-free), the first chunk runs as lane 0's own fp32
-// chain on VGPR operands (~7 cycles an add: it climbs through many binades,
-// an exact round each otherwise), every later fallback chunk as exact rounds
-// (chunk_exact).  Same outputs as k_fc_drive (out, and with cdf the chunk
-// start states in cst): tests/test_gpu_fchain.py runs both.
+// fewer dependent steps and in little code: a walker is one wave running a
+// chain of dependent instructions, mostly once each, so its instruction fetch
+// is its cost (k_fc_drive, ~20 KB of code: 18 us alone, 40-60 us in the plan
+// step beside the other stream's kernels).  The chain's entries and flags come
+// in one round trip; every predicted fallback chunk's operand rows by LDS-DMA
+// in one more (a rolled loop of DMA issues, no registers); a step of the walk
+// takes 256 entries (4 per lane, branch-free); the first chunk runs as lane
+// 0's own fp32 chain (it climbs through many binades, an exact round each
+// otherwise), every later fallback chunk as exact rounds (chunk_exact).  Same
+// outputs as k_fc_drive (out; with cdf the chunk start states in cst):
+// tests/test_gpu_fchain.py runs both.
 constexpr int kWkEntries = 1024;  // chunk entries in LDS
 constexpr int kWkStash = 16;      // predicted fallback chunks staged in LDS
+typedef __attribute__((address_space(3))) void fc_lds_void;
+typedef __attribute__((address_space(1))) void fc_glb_void;
+
+// the operand rows of chain (g, i): the base row and, for the products, the
+// second factor (FC_CHILD: L_z; K = 9: the partner; FC_LIST: the alpha)
+template <int BASE, int K>
+struct WalkRows {
+  const float* p0;
+  const float* p1;  // nullptr: terms are p0 itself
+  __device__ __forceinline__ void init(const FcArgs& a, int id, int i) {
+    if (BASE == FC_ROW) {
+      p0 = a.row + (long long)id * a.row_stride;
+      p1 = K > 0 ? a.partners + (long long)i * a.ld : nullptr;
+    } else if (BASE == FC_LIST) {
+      const int2 e = a.plist[id];
+      p0 = a.row + (long long)e.x * a.row_stride;
+      p1 = a.partners + (long long)e.y * a.ld;
+    } else {
+      p0 = a.pred + (long long)(id % 9) * a.ld;
+      p1 = a.lrows + (long long)(id / 9) * a.ld;
+    }
+  }
+  // the term of operands (u, v): Terms' per-cell operation
+  __device__ __forceinline__ float term(float u, float v) const {
+    if (BASE == FC_CHILD) return ftz(u * ftz(v));
+    return p1 ? u * v : u;
+  }
+};
 
 template <int BASE, int K>
 __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
   constexpr int KC = K > 0 ? K : 1;
   __shared__ uint32_t sE[kWkEntries];
   __shared__ short sSlot[kWkEntries];
-  __shared__ __attribute__((aligned(16))) float sSt[kWkStash][kFcChunk];
+  __shared__ __attribute__((aligned(16))) float sRaw[2][kWkStash][kFcChunk];
   for (int ch = blockIdx.x;; ch += gridDim.x) {  // (one wave: uniform)
   const int g = ch / KC, i = ch % KC;
   int id;
   if (!group_id(a, g, &id)) return;
-  Terms<BASE, K> T;
-  T.init(a, id);
+  WalkRows<BASE, K> R;
+  R.init(a, id, i);
   const int lane = threadIdx.x;
   const int n = a.n, nch = fc_chunks(n), nseg = fc_segments(n);
   const uint2* tab = a.tab + (long long)ch * nch;
   const bool cdf = BASE == FC_ROW && K == 0 && a.cdf != nullptr;
+  const unsigned long long tk0 = a.stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  unsigned long long tk1 = 0ull, tk2 = 0ull;
+  int n_it = 0, n_fb = 0, n_rounds = 0, n_hit = 0;
   // 1. flags and entries (one round trip); stash slots for the predicted chunks
   uint32_t f = 0u;
   for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)ch * nseg + s];
   int nst = 0;
+#pragma unroll 1
   for (int c0 = 0; c0 < nch; c0 += 64) {
     const int c = c0 + lane;
     const uint2 t = c < nch ? tab[c] : make_uint2(kNoEntry, 0u);
@@ -574,6 +609,21 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
       sE[c] = t.x;
       sSlot[c] = (short)(pr && sl < kWkStash ? sl : -1);
     }
+    // 2. (issued here, at once) the predicted chunks' operand rows into LDS
+    uint64_t mm = m;
+#pragma unroll 1
+    while (mm) {
+      const int l = __builtin_ctzll(mm);
+      mm &= mm - 1;
+      const int s2 = rdl(sl, l);
+      if (s2 >= kWkStash) break;
+      long long x = (long long)(c0 + l) * kFcChunk + 4 * lane;
+      x = x < a.ld ? x : 0;  // (cells past the row stride: read at 0, masked at use)
+      __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p0 + x), (fc_lds_void*)&sRaw[0][s2][0], 16, 0, 0);
+      if (R.p1)
+        __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p1 + x), (fc_lds_void*)&sRaw[1][s2][0], 16, 0,
+                                         0);
+    }
     nst += __popcll(m);
   }
   f = (__ballot((f & kPos) != 0u) ? kPos : 0u) | (__ballot((f & kNeg) != 0u) ? kNeg : 0u) |
@@ -581,62 +631,27 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
   if (cdf && lane == 0) a.cst[nch] = make_int2((int)f, 0);
   const bool seq_all = (f & kBad) || ((f & kPos) && (f & kNeg));
   const bool neg = (f & kNeg) && !(f & kPos);
-  nst = min(nst, kWkStash);
+  if (a.stats) tk1 = __builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA has landed)
   __syncthreads();
-  // 2. the predicted chunks' |terms| (all in flight together)
-  if (!seq_all) {
-    int ids[kWkStash];
-#pragma unroll
-    for (int s = 0; s < kWkStash; ++s) ids[s] = -1;
-    for (int c0 = 0; c0 < nch; c0 += 64) {  // slot -> chunk
-      const int c = c0 + lane;
-      const int sl = c < nch ? sSlot[c] : -1;
-#pragma unroll
-      for (int s = 0; s < kWkStash; ++s) {
-        const uint64_t m = __ballot(sl == s);
-        if (m) ids[s] = c0 + __builtin_ctzll(m);
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < kWkStash; h += 8) {
-      float st[8][4];
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-        if (h + s < nst) T.terms4(i, ids[h + s] * kFcChunk + 4 * lane, st[s]);
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-        if (h + s < nst)
-          *reinterpret_cast<f4a*>(&sSt[h + s][4 * lane]) =
-              f4a{fabsf(st[s][0]), fabsf(st[s][1]), fabsf(st[s][2]), fabsf(st[s][3])};
-    }
-  }
-  __syncthreads();
+  if (a.stats) tk2 = __builtin_amdgcn_s_memrealtime();
   float res;
   if (seq_all) {
-    // mixed signs or a non-finite term: the reference's chain itself
+    // mixed signs or a non-finite term: the reference's chain itself (rare:
+    // a rolled loop, one term per iteration)
     float s = 0.0f;
-    for (int j = 0; j < nch; ++j) {
-      float t[4];
-      T.terms4(i, j * kFcChunk + 4 * lane, t);
-      float cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      for (int l = 0; l < 64; ++l) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          s = s + rdl(t[q], l);
-          if (lane == l) cv[q] = s;
-        }
-      }
-      if (cdf) {
-        const int x0 = j * kFcChunk + 4 * lane;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (x0 + q < n) a.cdf[x0 + q] = cv[q];
-      }
+#pragma unroll 1
+    for (int x = 0; x < n; ++x) {
+      const float t = R.term(R.p0[x], R.p1 ? R.p1[x] : 0.0f);
+      s = s + t;
+      if (cdf && lane == 0) a.cdf[x] = s;
     }
     res = s;
   } else {
     int E = kEMin, k = 0, j = 0;
+#pragma unroll 1
     while (j < nch) {
+      ++n_it;
       // a step: entries j .. j + 255, 4 per lane (branch-free reads)
       uint32_t ev[4];
 #pragma unroll
@@ -676,53 +691,36 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
       normalise(&E, &k);
       j += fc;
       if (j < nch && L < 64) {
-        // chunk j term by term
+        // chunk j term by term: its |terms| from the staged operand rows (or
+        // loaded now)
         if (cdf && lane == 0) a.cst[j] = make_int2(E, k);
         const int sl = sSlot[j];
+        ++n_fb;
+        n_hit += sl >= 0;
+        const int x0 = j * kFcChunk + 4 * lane;
+        f4a u, v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (sl >= 0) {
+          u = *reinterpret_cast<const f4a*>(&sRaw[0][sl][4 * lane]);
+          if (R.p1) v = *reinterpret_cast<const f4a*>(&sRaw[1][sl][4 * lane]);
+        } else {
+          const int xs = x0 < a.ld ? x0 : 0;  // (masked below)
+          u = *reinterpret_cast<const f4a*>(R.p0 + xs);
+          if (R.p1) v = *reinterpret_cast<const f4a*>(R.p1 + xs);
+        }
+        float t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = x0 + q < n ? fabsf(R.term(u[q], v[q])) : 0.0f;
         if (j == 0) {
-          // from zero: lane 0's fp32 chain, 16 terms per batch of LDS reads
+          // from zero: lane 0's own fp32 chain over the chunk's terms, 4 a lane
           float s = value_of(E, k);
-          if (lane == 0) {
-            for (int h = 0; h < kFcChunk; h += 16) {
-              float v[16];
-              if (sl >= 0) {
+#pragma unroll 1
+          for (int l = 0; l < 64; ++l) {
 #pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) {
-                  const f4a u = *reinterpret_cast<const f4a*>(&sSt[sl][h + 4 * q4]);
-                  v[4 * q4] = u[0];
-                  v[4 * q4 + 1] = u[1];
-                  v[4 * q4 + 2] = u[2];
-                  v[4 * q4 + 3] = u[3];
-                }
-              } else {
-#pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) {
-                  float t[4];
-                  T.terms4(i, h + 4 * q4, t);
-#pragma unroll
-                  for (int q = 0; q < 4; ++q) v[4 * q4 + q] = fabsf(t[q]);
-                }
-              }
-#pragma unroll
-              for (int q = 0; q < 16; ++q) s = s + v[q];
-            }
+            for (int q = 0; q < 4; ++q) s = s + rdl(t[q], l);
           }
-          s = rdl(s, 0);
           state_of(s, &E, &k);
         } else {
-          float t[4];
-          if (sl >= 0) {
-            const f4a u = *reinterpret_cast<const f4a*>(&sSt[sl][4 * lane]);
-            t[0] = u[0];
-            t[1] = u[1];
-            t[2] = u[2];
-            t[3] = u[3];
-          } else {
-            T.terms4(i, j * kFcChunk + 4 * lane, t);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) t[q] = fabsf(t[q]);
-          }
-          chunk_exact(t, lane, &E, &k, nullptr);
+          chunk_exact(t, lane, &E, &k, nullptr, &n_rounds);
         }
         normalise(&E, &k);
         ++j;
@@ -730,6 +728,18 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
     }
     const float r = value_of(E, k);
     res = neg ? (r == 0.0f ? 0.0f : -r) : r;
+  }
+  if (a.stats && lane == 0) {
+    const unsigned long long tk3 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(a.stats + 0, n_it);
+    atomicAdd(a.stats + 1, n_fb);
+    atomicAdd(a.stats + 2, n_rounds);
+    atomicAdd(a.stats + 3, n_hit);
+    // 100 MHz ticks: flags + entries + the stash issued, the stash landed, the walk; chains
+    atomicAdd(a.stats + 4, (int)(tk1 - tk0));
+    atomicAdd(a.stats + 5, (int)(tk2 - tk1));
+    atomicAdd(a.stats + 6, (int)(tk3 - tk2));
+    atomicAdd(a.stats + 7, 1);
   }
   if (lane == 0) {
     if (BASE == FC_LIST) {  // out[row * ldo + partner]
