@@ -779,6 +779,10 @@ __global__ __launch_bounds__(256) void k_fc_cdf(FcArgs a) {
     const float v = neg ? (cv[q] == 0.0f ? 0.0f : -cv[q]) : cv[q];
     if (x0 + q < n) a.cdf[x0 + q] = v;
   }
+  // the last running sum of every 16 cells (k_tree_sample's first search;
+  // past n the sums stay at the row's total)
+  if (a.sub && (lane & 3) == 3 && (x0 + 3) / 16 < (n + 15) / 16)
+    a.sub[(x0 + 3) / 16] = neg ? (cv[3] == 0.0f ? 0.0f : -cv[3]) : cv[3];
 }
 
 // ---------------------------------------------------------------- sampling
@@ -790,21 +794,48 @@ __global__ __launch_bounds__(256) void k_fc_cdf(FcArgs a) {
 // with u2[j] (host-order fp32 cumulative sums).  Then the observations'
 // counts per action, counts[a * 16 + z], and the kept children c = z * 9 + a
 // in std::set order (klist, *kcount).
+constexpr int kSampleSub = 4096;  // 16-cell running-sum ends held in LDS (n <= 65536)
 __global__ __launch_bounds__(1024) void k_tree_sample(SampleArgs s) {
   __shared__ int cnt[144];
+  __shared__ float sSub[kSampleSub];
   for (int i = threadIdx.x; i < 144; i += blockDim.x) cnt[i] = 0;
-  __syncthreads();
   const int N = s.N, n = s.n, W = s.g.width;
+  const int nsub = (n + 15) / 16;
+  // a non-decreasing cdf (no negative or non-finite cell: the chain-set
+  // flags) with its 16-cell ends: first the 16 cells, in LDS, then the cell
+  const uint32_t f = s.sub ? (uint32_t)s.cst[(n + kFcChunk - 1) / kFcChunk].x : 0u;
+  const bool two = s.sub && nsub <= kSampleSub && !(f & kNeg) && !(f & kBad);
+  if (two)
+    for (int i = threadIdx.x; i < nsub; i += blockDim.x) sSub[i] = s.sub[i];
+  __syncthreads();
   for (int jt = threadIdx.x; jt < 9 * N; jt += blockDim.x) {
     const int act = jt / N, j = jt - act * N;
     const float r = s.r[jt];
-    int lo = 0, hi = n;  // the first x with cdf[x] >= r
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (s.cdf[mid] < r) lo = mid + 1;
-      else hi = mid;
+    int s1 = n;  // the first x with cdf[x] >= r (n: none)
+    if (two) {
+      int l2 = 0, h2 = nsub;
+      while (l2 < h2) {
+        const int mid = (l2 + h2) >> 1;
+        if (sSub[mid] < r) l2 = mid + 1;
+        else h2 = mid;
+      }
+      if (l2 < nsub) {
+        float cv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) cv[q] = 16 * l2 + q < n ? s.cdf[16 * l2 + q] : INFINITY;
+#pragma unroll
+        for (int q = 15; q >= 0; --q)
+          if (cv[q] >= r) s1 = 16 * l2 + q;
+      }
+    } else {
+      int lo = 0, hi = n;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s.cdf[mid] < r) lo = mid + 1;
+        else hi = mid;
+      }
+      s1 = lo;
     }
-    int s1 = lo;
     if (s1 >= n) {  // the reference runs off its arrays: the last cell with mass
       s1 = n - 1;
       while (s1 > 0 && s.cdf[s1] == s.cdf[s1 - 1]) --s1;

@@ -143,6 +143,7 @@ struct FcArgs {
   float* out = nullptr;
   int ldo = 1;
   float* cdf = nullptr;
+  float* sub = nullptr;          // with cdf (optional): the running sum at every 16th cell's end
   // scratch (FcScratch::attach)
   float* csum = nullptr;         // [chains][chunks] approximate chunk sums
   uint32_t* cflag = nullptr;     // [chains][segments] sign flags
@@ -189,6 +190,10 @@ struct SampleArgs {
   int* counts = nullptr;  // [144]
   int* klist = nullptr;   // [144]
   int* kcount = nullptr;
+  // optional (the chain set's running sums): the 16-cell ends (FcArgs::sub)
+  // and the chunk start states, whose entry [chunks] holds the sign flags
+  const float* sub = nullptr;
+  const int2* cst = nullptr;
 };
 hipError_t launch_tree_sample(hipStream_t st, const SampleArgs& s);
 // Fused chain sets (pp2_fchain.hip, round 6): the same sums as launch_fchain,

@@ -211,6 +211,7 @@ struct pp2_planner {
   float* d_pred = nullptr;      // [9][ld] the expanded belief's predictions
   float* d_csum = nullptr;      // [144] the children's masses (accumulate)
   float* d_cdf = nullptr;       // the expanded belief's running sums
+  float* d_sub = nullptr;       // and every 16th cell's (n <= 65536; else null)
   float* h_r = nullptr;         // pinned: the expansion's rand() values [9][N]
   float* d_r = nullptr;
   float *d_u1 = nullptr, *d_u2 = nullptr;  // the curand uniforms [N]
@@ -961,6 +962,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     cd.row = brow;
     cd.out = p->d_rsum;
     cd.cdf = p->d_cdf;
+    cd.sub = p->seq ? nullptr : p->d_sub;  // (the sampler's first search)
     p->scr_main.attach(&cd);
     pp2::FcArgs ch;  // side: the 144 children's masses
     ch.n = (int)n;
@@ -991,6 +993,8 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       sa.counts = p->d_counts;
       sa.klist = p->d_klist;
       sa.kcount = p->d_kcount;
+      sa.sub = cd.sub;
+      sa.cst = cd.cst;
       HIPCHK(pp2::launch_tree_sample(c->stream, sa));
     }
     if (!p->seq) {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
@@ -1341,6 +1345,7 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         hipMalloc(&p->d_csum, 144 * sizeof(float)) != hipSuccess ||
         !host_mapped(kRefOutFloats, &p->h_rout, &p->d_rout) ||
         hipMalloc(&p->d_cdf, (size_t)row_ld * sizeof(float)) != hipSuccess ||
+        (p->n <= 65536 && hipMalloc(&p->d_sub, (p->n + 15) / 16 * sizeof(float)) != hipSuccess) ||
         !host_mapped(9 * (size_t)prm->sample_num, &p->h_r, &p->d_r) ||
         hipMalloc(&p->d_u1, (size_t)prm->sample_num * sizeof(float)) != hipSuccess ||
         hipMalloc(&p->d_u2, (size_t)prm->sample_num * sizeof(float)) != hipSuccess ||
@@ -1451,7 +1456,7 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (p->h_rout) (void)hipHostFree(p->h_rout);
   if (p->h_r) (void)hipHostFree(p->h_r);
   if (p->h_counts) (void)hipHostFree(p->h_counts);
-  for (void* d : {(void*)p->d_cdf, (void*)p->d_u1, (void*)p->d_u2, (void*)p->d_klist,
+  for (void* d : {(void*)p->d_cdf, (void*)p->d_sub, (void*)p->d_u1, (void*)p->d_u2, (void*)p->d_klist,
                   (void*)p->d_kcount})
     if (d) (void)hipFree(d);
   for (void* d : {(void*)p->d_lbidx, (void*)p->d_srow, (void*)p->d_us, (void*)p->d_zs})
