@@ -63,17 +63,17 @@ PP2_FC_HD inline int domain_of(float s) {
   return et <= 1 ? kEMin : et - 127;
 }
 
-// (E, k) of a finite s >= +0.
+// (E, k) of a finite s >= +0.  With the float's bits b (sign cleared) and
+// exponent field et, E = max(et, 1) - 127 and k = b - ((E + 126) << 23): the
+// significand with its hidden bit, or for subnormals the bits themselves --
+// branch-free (a walker runs this on the scalar unit, where every branch is
+// a pipeline refill).
 PP2_FC_HD inline void state_of(float s, int* E, int* k) {
   const uint32_t b = bits_of(s) & 0x7fffffffu;
-  const uint32_t et = b >> 23;
-  if (et <= 1) {
-    *E = kEMin;
-    *k = (int)(b & 0xffffffu);
-  } else {
-    *E = (int)et - 127;
-    *k = (int)((b & 0x7fffffu) | 0x800000u);
-  }
+  const int et = (int)(b >> 23);
+  const int e1 = et > 1 ? et : 1;
+  *E = e1 - 127;
+  *k = (int)(b - ((uint32_t)(e1 - 1) << 23));
 }
 
 // k == 2^24 is the next binade's first value.
@@ -84,12 +84,13 @@ PP2_FC_HD inline void normalise(int* E, int* k) {
   }
 }
 
-// The float k * 2^(E-23) (k <= 2^24; E = -126: any k, else k >= 2^23).
+// The float k * 2^(E-23) (k <= 2^24; E = -126: any k, else k >= 2^23): the
+// inverse of state_of, bits ((E + 126) << 23) + k -- k = 2^24 carries into the
+// next binade's first value, and past E = 127 into +inf (clamped there: an
+// overflowed sum stays +inf whatever it adds).
 PP2_FC_HD inline float value_of(int E, int k) {
-  normalise(&E, &k);
-  if (E > 127) return float_of(0x7f800000u);
-  if (E == kEMin && k < (1 << 23)) return float_of((uint32_t)k);
-  return float_of(((uint32_t)(E + 127) << 23) | ((uint32_t)k & 0x7fffffu));
+  const uint32_t b = ((uint32_t)(E + 126) << 23) + (uint32_t)k;
+  return float_of(b < 0x7f800000u ? b : 0x7f800000u);
 }
 
 // The increment of one term a = |t| (finite) in domain E: rint(a / u) as a
@@ -126,6 +127,16 @@ PP2_FC_HD inline uint32_t make_entry(int E, float d, bool tie) {
 }
 PP2_FC_HD inline int entry_domain(uint32_t e) { return (int)(e >> 24) - 128; }
 PP2_FC_HD inline int entry_units(uint32_t e) { return (int)(e & 0xffffffu); }
+// Whether an entry applies in the state's domain E: it was computed for E --
+// or it adds nothing (d = 0 with no tie: every |t| / u below 1/2) and was
+// computed for a lower domain, where at E each ratio is 2^(E_e - E) times
+// smaller, still below 1/2.  (The tail of a concentrated belief: once the
+// exact sum sits at 1.0 and the approximate one just below, every later chunk
+// was tabled for the binade below.)
+PP2_FC_HD inline bool entry_applies(uint32_t e, int E) {
+  return e != kNoEntry &&
+         (entry_domain(e) == E || (entry_units(e) == 0 && entry_domain(e) < E));
+}
 
 }  // namespace fchain
 }  // namespace pp2

@@ -61,14 +61,18 @@ __device__ __forceinline__ float rdl(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
+// (the rows' totals carried by DPP row_bcast:15 -- lane 15 of each row into
+// the next, rows 1 and 3 -- then row_bcast:31 into rows 2 and 3: no scalar
+// round trips)
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+  (void)lane;
   v += row_shr(v, 1);
   v += row_shr(v, 2);
   v += row_shr(v, 4);
   v += row_shr(v, 8);
-  const int r0 = rdl(v, 15), r1 = rdl(v, 31), r2 = rdl(v, 47);
-  const int row = lane >> 4;
-  return v + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
 }
 
 // the wave's total (uniform): any association will do for these sums
@@ -82,6 +86,23 @@ __device__ __forceinline__ float wave_sum(float v) {
   }
   const float f = __builtin_bit_cast(float, b);
   return (rdl(f, 15) + rdl(f, 31)) + (rdl(f, 47) + rdl(f, 63));
+}
+
+// the wave's maximum of non-negative float bits (uniform)
+__device__ __forceinline__ uint32_t wave_max_bits(uint32_t v) {
+#pragma unroll
+  for (int c = 1; c < 16; c <<= 1) v = max(v, (uint32_t)row_shr((int)v, c));
+  return max(max((uint32_t)rdl((int)v, 15), (uint32_t)rdl((int)v, 31)),
+             max((uint32_t)rdl((int)v, 47), (uint32_t)rdl((int)v, 63)));
+}
+
+// The lowest domain where every |t| <= the float of bits mx is below half an
+// ulp (mx < 2^(E-24)): a chunk adding nothing there adds nothing above either.
+__device__ __forceinline__ int zero_domain(uint32_t mx) {
+  if (mx == 0u) return kEMin;
+  const int et = (int)(mx >> 23);
+  const int e = et == 0 ? -127 : et - 127;  // (subnormal: below 2^-126)
+  return max(e + 25, kEMin);
 }
 
 // The device's flush of a product (FTZ build of the reference kernel).
@@ -278,17 +299,22 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
       const int E = domain_of(sP[i][jl]);
       float d = 0.0f, tt[4];
       bool tie = false;
+      uint32_t mx = 0u;
       T.terms_of(v, i, x0, tt);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         bool tx;
         d += units_of(fabsf(tt[q]), E, &tx);
         tie = tie || tx;
+        mx = max(mx, bits_of(tt[q]) & 0x7fffffffu);
       }
       const float ds = wave_sum(d);  // exact below 2^24; else no entry
       const bool anytie = __ballot(tie) != 0ull;
+      // a chunk adding nothing is tabled for the lowest domain where it adds
+      // nothing (entry_applies: every domain above too)
+      const int Ez = ds == 0.0f ? zero_domain(wave_max_bits(mx)) : E;
       if (lane == 0) {
-        const uint32_t e = make_entry(E, ds, anytie);
+        const uint32_t e = make_entry(min(E, Ez), ds, anytie);
         // predicted fallback: no entry, or the chunk's sum likely crosses
         // into the next binade (from the approximate running sum)
         const bool pred = e == kNoEntry ||
@@ -346,8 +372,10 @@ __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* 
       break;
     }
     const int lb = __builtin_ctzll(bm);
+    // (the failing term picked per lane, by selects: one readlane, no
+    // branches on the scalar unit)
+    const float tq = bad == 0 ? t[0] : bad == 1 ? t[1] : bad == 2 ? t[2] : t[3];
     const int qb = rdl(bad, lb), kbef = rdl(kb, lb);
-    const float tq = qb == 0 ? t[0] : qb == 1 ? t[1] : qb == 2 ? t[2] : t[3];
     const float tb = rdl(tq, lb);
     const float s = value_of(E, kbef) + tb;  // the reference's own add
     state_of(s, &E, &k);
@@ -468,7 +496,7 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
       }
       const int jj = j + lane;
       const uint2 e = jj < nch && jj < wbase + kFcWin ? sE[jj - wbase] : make_uint2(kNoEntry, 0u);
-      const bool valid = e.x != kNoEntry && entry_domain(e.x) == E;
+      const bool valid = entry_applies(e.x, E);
       const int dl = valid ? entry_units(e.x) : 0;
       const int incl = wave_incl_scan(dl, lane);
       const bool ok = valid && k + incl <= kK24;
@@ -661,7 +689,8 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
       bool vq[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        vq[q] = (j + 4 * lane + q < nch) & (ev[q] != kNoEntry) & ((ev[q] >> 24) == ebias);
+        vq[q] = (j + 4 * lane + q < nch) & (ev[q] != kNoEntry) &
+                (((ev[q] >> 24) == ebias) | (((ev[q] & 0xffffffu) == 0u) & ((ev[q] >> 24) < ebias)));
         dq[q] = vq[q] ? (int)(ev[q] & 0xffffffu) : 0;
         tot += dq[q];
       }
@@ -690,11 +719,23 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
       k = rdl(run, L < 64 ? L : 63);
       normalise(&E, &k);
       j += fc;
-      if (j < nch && L < 64) {
+      // (a stop at the exact top of a binade: the normalised state may take
+      // chunk j's entry after all -- the next step does)
+      const uint32_t ej = j < nch ? sE[j] : kNoEntry;
+      if (j < nch && L < 64 && !(entry_applies(ej, E) && k + entry_units(ej) <= kK24)) {
         // chunk j term by term: its |terms| from the staged operand rows (or
         // loaded now)
         if (cdf && lane == 0) a.cst[j] = make_int2(E, k);
         const int sl = sSlot[j];
+        if (a.stats && lane == 0) {  // why: no entry / another binade / the crossing
+          const uint32_t e = ej;
+          atomicAdd(a.stats + (e == kNoEntry ? 8 : (int)(e >> 24) != E + 128 ? 9 : 10), 1);
+          if (BASE == FC_ROW && K == 0) {  // (the last 1024 fallbacks: chunk, entry, state)
+            const int at = atomicAdd(a.stats + 15, 1);
+            int* tr = a.stats + 128 + 4 * (at & 1023);
+            tr[0] = j; tr[1] = (int)e; tr[2] = E; tr[3] = k;
+          }
+        }
         ++n_fb;
         n_hit += sl >= 0;
         const int x0 = j * kFcChunk + 4 * lane;
@@ -1215,7 +1256,8 @@ __device__ __forceinline__ void fx_walk(const FxArgs& a, const FxTerms<SRC, K>& 
           const uint32_t e = ev[q];
           const bool in = j + 4 * lane + q < nch;
           const bool z = e == kFxZero;
-          vq[q] = in & (z | ((e != kNoEntry) & ((e >> 24) == ebias)));
+          vq[q] = in & (z | ((e != kNoEntry) & (((e >> 24) == ebias) |
+                                                (((e & 0xffffffu) == 0u) & ((e >> 24) < ebias)))));
           dq[q] = (vq[q] & !z) ? (int)(e & 0xffffffu) : 0;
           tot += dq[q];
         }
@@ -1605,6 +1647,9 @@ constexpr int kFcDriveBlocks = 8192;   // drive: one wave per chain
 // k_fc_walk for chains of at most kWkEntries chunks (PP2_FC_WALK=0, or
 // pp2_debug_fc_walk(0): k_fc_drive everywhere)
 int g_fc_walk = -1;
+// pp2_debug_fc_stats: driver counters per set kind (8 ints each, summed over
+// launches; nullptr: off)
+int* g_fc_stats = nullptr;
 bool fc_walk_enabled() {
   if (g_fc_walk < 0) g_fc_walk = !(getenv("PP2_FC_WALK") && getenv("PP2_FC_WALK")[0] == '0');
   return g_fc_walk != 0;
@@ -1622,6 +1667,7 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
     hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
   }
   if (phases & FC_DRIVE) {
+    if (g_fc_stats && !a.stats) a.stats = g_fc_stats + 16 * (2 * BASE + (K > 0));
     if (fc_walk_enabled() && fc_chunks(a.n) <= kWkEntries)
       hipLaunchKernelGGL((k_fc_walk<BASE, K>), dim3(std::min(groups * KC, kFcDriveBlocks)),
                          dim3(64), 0, st, a);
@@ -1836,8 +1882,8 @@ extern "C" int pp2_debug_fchain_row2(int n, const float* x, const float* partner
     a.cdf = dcdf;
     scr.attach(&a);
     int* dstats = nullptr;
-    if (stats && ok(hipMalloc(&dstats, 8 * sizeof(int))) &&
-        ok(hipMemset(dstats, 0, 8 * sizeof(int))))
+    if (stats && ok(hipMalloc(&dstats, 16 * sizeof(int))) &&
+        ok(hipMemset(dstats, 0, 16 * sizeof(int))))
       a.stats = dstats;
     if (ms && st == 0) {
       hipEvent_t e0, e1;
@@ -2163,4 +2209,24 @@ extern "C" int pp2_debug_fc_walk(int on) {
   const int prev = pp2::fc_walk_enabled() ? 1 : 0;
   pp2::g_fc_walk = on ? 1 : 0;
   return prev;
+}
+
+// Diagnostic (tools/prof_planner.py, PP2_FC_STATS=1): the drivers' counters
+// summed per set kind over every launch -- out[16 * (2 * base + (K > 0)) + c],
+// c as pp2_debug_fchain_row2's stats; k_fc_walk's fallback chunks by cause in
+// c = 8 (no entry), 9 (entry for another binade), 10 (the binade crossing).
+// (128 ints; then the last 1024 row-set fallbacks {chunk, entry, E, k}, a ring (diagnostic))  enable=1 allocates (before the sets to
+// count are launched), out != nullptr copies the 64 counters out and clears them.
+extern "C" int pp2_debug_fc_stats(int* out, int enable) {
+  if (enable && !pp2::g_fc_stats) {
+    if (hipMalloc(&pp2::g_fc_stats, (128 + 4096) * sizeof(int)) != hipSuccess) return 1;
+    if (hipMemset(pp2::g_fc_stats, 0, (128 + 4096) * sizeof(int)) != hipSuccess) return 1;
+  }
+  if (out && pp2::g_fc_stats) {
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    if (hipMemcpy(out, pp2::g_fc_stats, (128 + 4096) * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+      return 1;
+    if (hipMemset(pp2::g_fc_stats, 0, (128 + 4096) * sizeof(int)) != hipSuccess) return 1;
+  }
+  return 0;
 }

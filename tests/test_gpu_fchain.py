@@ -78,6 +78,16 @@ def rows(rng):
     t = np.zeros(4096, np.float32)
     t[::2] = -0.0
     yield "-0 and +0", t
+    # a concentrated, normalised belief, then a tail far below half an ulp of
+    # its sum (entries of d = 0 tabled for the binade below the exact sum's)
+    for m, tail in ((200, "tiny"), (3000, "zeros + 2^-26")):
+        t = U(m)
+        t = (t / seq(t)[0]).astype(np.float32)
+        if tail == "tiny":
+            tl = np.ldexp(U(60000), -40)
+        else:
+            tl = np.where(np.arange(60000) % 7 == 0, np.float32(np.ldexp(1.0, -26)), 0)
+        yield f"concentrated m={m} + {tail} tail", np.concatenate([t, tl]).astype(np.float32)
     yield "empty", np.zeros(0, np.float32)
     yield "single", np.array([-3.5], np.float32)
     for n in (1, 63, 64, 65, 255, 256, 257, 4000, 65535, 262144 + 7, 1 << 20):

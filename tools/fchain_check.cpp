@@ -56,15 +56,24 @@ static float fchain_sum(const std::vector<float>& t, int chunk, Stats* st) {
   std::vector<uint32_t> tab(nch);
   for (int j = 0; j < nch; ++j) {
     const int E = domain_of(P[j]);
-    float d = 0.0f;
+    float d = 0.0f, mx = 0.0f;
     bool tie = false;
     const int x1 = std::min(n, (j + 1) * chunk);
     for (int x = x1 - 1; x >= j * chunk; --x) {
       bool tx;
       d += units_of(fabsf(t[x]), E, &tx);
       tie |= tx;
+      mx = std::max(mx, fabsf(t[x]));
     }
-    tab[j] = make_entry(E, d, tie);
+    // a chunk adding nothing: tabled for the lowest domain where it adds
+    // nothing (k_fc_tables' zero_domain)
+    int Ez = E;
+    if (d == 0.0f) {
+      const uint32_t b = bits_of(mx);
+      const int et = (int)(b >> 23);
+      Ez = b == 0u ? kEMin : std::max((et == 0 ? -127 : et - 127) + 25, kEMin);
+    }
+    tab[j] = make_entry(std::min(E, Ez), d, tie);
   }
   // driver: 64 chunks per step
   int E = kEMin, k = 0;
@@ -76,7 +85,7 @@ static float fchain_sum(const std::vector<float>& t, int chunk, Stats* st) {
     for (int l = 0; l < 64; ++l) {
       const int jj = j + l;
       const uint32_t e = jj < nch ? tab[jj] : kNoEntry;
-      const bool valid = e != kNoEntry && entry_domain(e) == E;
+      const bool valid = entry_applies(e, E);
       acc += valid ? entry_units(e) : 0;
       incl[l] = acc;
       ok[l] = valid && k + acc <= kK24;
@@ -185,6 +194,19 @@ int main(int argc, char** argv) {
     std::vector<float> t = {0.5f, 0.25f, 0.25f};
     for (int i = 0; i < 3000; ++i) t.push_back(ldexpf(1.0f, -25));
     for (int c : chunks) check("onto 2^k", t, c, &st);
+  }
+  // a concentrated, normalised belief: the exact sum ends at or next to 1.0,
+  // the approximate one on the other side, then a long tail far below half an
+  // ulp (entries of d = 0 tabled for the binade below: entry_applies)
+  for (int rep = 0; rep < 40; ++rep) {
+    const int m = 50 + (int)(rng() % 3000);
+    std::vector<float> t;
+    float s = 0.0f;
+    for (int i = 0; i < m; ++i) t.push_back(U(rng)), s = s + t.back();
+    for (float& v : t) v = v / s;
+    for (int i = 0; i < 60000; ++i)
+      t.push_back(rep % 2 ? ldexpf(U(rng), -40) : (i % 7 ? 0.0f : ldexpf(1.0f, -26)));
+    for (int c : chunks) check("concentrated + tail", t, c, &st);
   }
   // all zeros, -0, empty, single
   {
