@@ -317,8 +317,9 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
         const uint32_t e = make_entry(min(E, Ez), ds, anytie);
         // predicted fallback: no entry, or the chunk's sum likely crosses
         // into the next binade (from the approximate running sum)
+        // (a chunk adding nothing crosses nothing)
         const bool pred = e == kNoEntry ||
-                          ldexpf(sP[i][jl], 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f);
+                          (ds > 0.0f && ldexpf(sP[i][jl], 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f));
         a.tab[(long long)(g * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
       }
     }
@@ -333,10 +334,48 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
 // from `done` on up to the first that does not apply (a tie, or past
 // 2^(E+1)), adds that one in fp32, and goes on after it (add_exact, in
 // parallel).  With cv, every running value (cv[q] of term 4l + q).
+//
+// A round is ~130 instructions of one wave (~850 cycles in the plan step,
+// beside the other stream's kernels); the chain itself is 256 dependent adds
+// (~8000 cycles there: ~31 a term).  So a chunk of many events (the climb of
+// a chain through binades, runs of ties: 6 .. 14 in a belief's first nonzero
+// chunks) runs as rounds up to max_rounds and then, with sT (the wave's
+// 256-float LDS buffer), as the fp32 chain for the rest -- every lane the
+// same adds over broadcast LDS reads, terms before `done` read as +0.0
+// (s + 0 = s for s >= +0); cv from the value at each lane's first term,
+// recorded on the way, and the lane's own 4 adds again.
 __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* pE, int* pk,
-                                            float (*cv)[4], int* rounds = nullptr) {
+                                            float (*cv)[4], int* rounds = nullptr,
+                                            float* sT = nullptr, int max_rounds = 1 << 30) {
   int E = *pE, k = *pk, done = 0;
-  for (;;) {
+  for (int rd = 0;; ++rd) {
+    if (sT && rd >= max_rounds) {
+      // the rest as the chain itself
+      *reinterpret_cast<f4a*>(&sT[4 * lane]) = f4a{t[0], t[1], t[2], t[3]};
+      float s = value_of(E, k), s0 = s;
+#pragma unroll 1
+      for (int xb = done & ~63; xb < kFcChunk; xb += 64) {
+#pragma unroll
+        for (int gq = 0; gq < 16; ++gq) {
+          const int x = xb + 4 * gq;
+          if (cv && lane == x / 4) s0 = s;  // (lane x/4's first term comes next)
+          const f4a w = *reinterpret_cast<const f4a*>(&sT[x]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) s = s + (x + q >= done ? w[q] : 0.0f);
+        }
+      }
+      if (cv) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (4 * lane + q >= done) {
+            s0 = s0 + t[q];
+            (*cv)[q] = s0;
+          }
+        }
+      }
+      state_of(rdl(s, 0), &E, &k);
+      break;
+    }
     if (rounds) ++*rounds;
     int r[4];
     bool tie[4];
@@ -559,18 +598,18 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
 }
 
 // ---------------------------------------------------------------- walker (round 6)
-// k_fc_drive's job for chains of at most kWkEntries chunks (n <= 262144), in
-// fewer dependent steps and in little code: a walker is one wave running a
-// chain of dependent instructions, mostly once each, so its instruction fetch
-// is its cost (k_fc_drive, ~20 KB of code: 18 us alone, 40-60 us in the plan
-// step beside the other stream's kernels).  The chain's entries and flags come
-// in one round trip; every predicted fallback chunk's operand rows by LDS-DMA
-// in one more (a rolled loop of DMA issues, no registers); a step of the walk
-// takes 256 entries (4 per lane, branch-free); the first chunk runs as lane
-// 0's own fp32 chain (it climbs through many binades, an exact round each
-// otherwise), every later fallback chunk as exact rounds (chunk_exact).  Same
-// outputs as k_fc_drive (out; with cdf the chunk start states in cst):
-// tests/test_gpu_fchain.py runs both.
+// k_fc_walk (below): k_fc_drive's job for chains of at most kWkEntries
+// chunks (n <= 262144).  The first chunk runs as the fp32 chain itself (it
+// climbs through many binades, an exact round each otherwise), every later
+// exact chunk as exact rounds, the chain itself after eight (chunk_exact).
+// (build knobs for same-box A/B builds, tools/ab_planner.sh: the walker's
+// issue priority, the exact rounds before an exact chunk's chain tail)
+#ifndef PP2_WALK_PRIO
+#define PP2_WALK_PRIO 1
+#endif
+#ifndef PP2_WALK_TAIL
+#define PP2_WALK_TAIL 8
+#endif
 constexpr int kWkEntries = 1024;  // chunk entries in LDS
 constexpr int kWkStash = 16;      // predicted fallback chunks staged in LDS
 typedef __attribute__((address_space(3))) void fc_lds_void;
@@ -602,12 +641,68 @@ struct WalkRows {
   }
 };
 
+// Segment records of the walker (below): a chunk's increments summed from
+// its segment's head, saturated at 2^25, and its domain keys (hi 16 bits: the
+// largest entry domain; lo 16 bits: 255 - the smallest domain of an entry
+// adding something), both as running values from the head -- segmented wave
+// scans on DPP (row shifts, then row_bcast:15 / :31).
+constexpr uint32_t kSegSat = 1u << 25;
+constexpr int kSegSlow = 1 << 20;  // sSeg[].x: the segment was walked chunk by chunk
+
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+  return max(a & 0xffff0000u, b & 0xffff0000u) | max(a & 0xffffu, b & 0xffffu);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dppu(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ void seg_step(uint32_t& f, uint32_t& s, uint32_t& k) {
+  const uint32_t pf = dppu<CTRL, RM>(f), ps = dppu<CTRL, RM>(s), pk = dppu<CTRL, RM>(k);
+  const bool head = f != 0u;
+  s = head ? s : min(ps + s, kSegSat);
+  k = head ? k : pk_max(pk, k);
+  f |= pf;
+}
+// inclusive segmented scan over the lanes (f: a head in or before the lane)
+__device__ __forceinline__ void wave_seg_scan(uint32_t& f, uint32_t& s, uint32_t& k) {
+  seg_step<0x111, 0xf>(f, s, k);
+  seg_step<0x112, 0xf>(f, s, k);
+  seg_step<0x114, 0xf>(f, s, k);
+  seg_step<0x118, 0xf>(f, s, k);
+  seg_step<0x142, 0xa>(f, s, k);
+  seg_step<0x143, 0xc>(f, s, k);
+}
+
+// k_fc_drive's job for chains of at most kWkEntries chunks, as a walk over
+// SEGMENTS.  The tables mark the chunks a chain will likely not take from its
+// entry (kPredicted: no entry, or the approximate running sum crosses a
+// binade in it) -- the breaks.  Between two breaks lies a segment whose
+// entries all apply at once when the state's domain is the one they were
+// tabled for; one pass over the entries (4 per lane, segmented scans)
+// records each segment's saturated increment and domain range, so the walk
+// itself is a scalar loop: per segment one check and one add (a mispredicted
+// segment walks its chunks as before), per break one exact chunk from the
+// operand rows the same pass staged into LDS.  A walker is one wave running
+// a chain of dependent instructions; what it saves is steps (a walk step over
+// 256 entries was ~1000 cycles, a segment is tens).  With cdf the chunk start
+// states go to cst: the breaks' as they are walked, every segment chunk's
+// after the walk from its segment's start state and running increment.  Same
+// outputs as k_fc_drive: tests/test_gpu_fchain.py runs both.
 template <int BASE, int K>
 __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
   constexpr int KC = K > 0 ? K : 1;
   __shared__ uint32_t sE[kWkEntries];
-  __shared__ short sSlot[kWkEntries];
+  __shared__ uint32_t sInc[kWkEntries];  // increments from the segment head (saturated)
+  __shared__ uint32_t sKey[kWkEntries];  // domain keys from the segment head
+  __shared__ short sOrd[kWkEntries];     // breaks before the chunk; a break: -(ordinal + 1)
+  __shared__ short sBrk[kWkEntries];     // the breaks' chunks in order
+  __shared__ int2 sSeg[kWkEntries + 1];  // (cdf) each segment's start state
   __shared__ __attribute__((aligned(16))) float sRaw[2][kWkStash][kFcChunk];
+  __shared__ __attribute__((aligned(16))) float sT[kFcChunk];  // (chunk_exact's chain tails)
+  // (a walker is latency: first in its SIMD's issue arbitration, ahead of
+  // the bandwidth kernels of the other stream sharing it)
+  if (PP2_WALK_PRIO) __builtin_amdgcn_s_setprio(3);
   for (int ch = blockIdx.x;; ch += gridDim.x) {  // (one wave: uniform)
   const int g = ch / KC, i = ch % KC;
   int id;
@@ -620,39 +715,94 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
   const bool cdf = BASE == FC_ROW && K == 0 && a.cdf != nullptr;
   const unsigned long long tk0 = a.stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
   unsigned long long tk1 = 0ull, tk2 = 0ull;
-  int n_it = 0, n_fb = 0, n_rounds = 0, n_hit = 0;
-  // 1. flags and entries (one round trip); stash slots for the predicted chunks
+  int n_it = 0, n_fb = 0, n_rounds = 0, n_hit = 0, n_slow = 0;
+  // 1. flags; entries, breaks and segment records (4 chunks a lane); the
+  //    first kWkStash breaks' operand rows into LDS
   uint32_t f = 0u;
   for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)ch * nseg + s];
-  int nst = 0;
+  int nb = 0;
+  uint32_t cs = 0u, ck = 0u;  // the records of the last chunk so far
 #pragma unroll 1
-  for (int c0 = 0; c0 < nch; c0 += 64) {
-    const int c = c0 + lane;
-    const uint2 t = c < nch ? tab[c] : make_uint2(kNoEntry, 0u);
-    const bool pr = c < nch && (t.y & kPredicted);
-    const uint64_t m = __ballot(pr);
-    const int sl = nst + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (c < nch) {
-      sE[c] = t.x;
-      sSlot[c] = (short)(pr && sl < kWkStash ? sl : -1);
+  for (int c0 = 0; c0 < nch; c0 += 4 * 64) {
+    uint2 t[4];
+    bool br[4];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + 4 * lane + q;
+      t[q] = c < nch ? tab[c] : make_uint2(0u, 0u);
+      br[q] = c < nch && ((t[q].y & kPredicted) || t[q].x == kNoEntry);
+      cnt += br[q];
     }
-    // 2. (issued here, at once) the predicted chunks' operand rows into LDS
-    uint64_t mm = m;
+    const int incl = wave_incl_scan(cnt, lane);
+    int o = nb + incl - cnt;
+    nb += rdl(incl, 63);
+    uint32_t lf = 0u, ls = 0u, lk = 0u, vs[4], vk[4];
+    bool vf[4];
+    int oq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + 4 * lane + q;
+      const uint32_t e = t[q].x;
+      const uint32_t d = br[q] ? 0u : (uint32_t)entry_units(e);
+      const uint32_t key = br[q] ? 0u : ((e >> 24) << 16) | (d > 0u ? 255u - (e >> 24) : 0u);
+      const bool head = br[q] || c == 0;
+      ls = head ? d : min(ls + d, kSegSat);
+      lk = head ? key : pk_max(lk, key);
+      lf |= head;
+      vs[q] = ls;
+      vk[q] = lk;
+      vf[q] = lf != 0u;
+      oq[q] = o;
+      o += br[q];
+      if (c < nch) {
+        sE[c] = e;
+        sOrd[c] = (short)(br[q] ? -(oq[q] + 1) : oq[q]);
+        if (br[q]) sBrk[oq[q]] = (short)c;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint64_t m = __ballot(br[q] && oq[q] < kWkStash);
 #pragma unroll 1
-    while (mm) {
-      const int l = __builtin_ctzll(mm);
-      mm &= mm - 1;
-      const int s2 = rdl(sl, l);
-      if (s2 >= kWkStash) break;
-      long long x = (long long)(c0 + l) * kFcChunk + 4 * lane;
-      x = x < a.ld ? x : 0;  // (cells past the row stride: read at 0, masked at use)
-      __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p0 + x), (fc_lds_void*)&sRaw[0][s2][0], 16, 0, 0);
-      if (R.p1)
-        __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p1 + x), (fc_lds_void*)&sRaw[1][s2][0], 16, 0,
-                                         0);
+      while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        const int s2 = rdl(oq[q], l);
+        long long x = (long long)(c0 + 4 * l + q) * kFcChunk + 4 * lane;
+        x = x < a.ld ? x : 0;  // (cells past the row stride: read at 0, masked at use)
+        __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p0 + x), (fc_lds_void*)&sRaw[0][s2][0], 16,
+                                         0, 0);
+        if (R.p1)
+          __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p1 + x), (fc_lds_void*)&sRaw[1][s2][0],
+                                           16, 0, 0);
+      }
     }
-    nst += __popcll(m);
+    // the lanes' records: the carry into lane 0, the segmented scan, each
+    // chunk's from the lane before (lane 0: the carry)
+    uint32_t wf = lf, ws = ls, wk = lk;
+    if (lane == 0 && !lf) {
+      ws = min(cs + ws, kSegSat);
+      wk = pk_max(ck, wk);
+    }
+    wave_seg_scan(wf, ws, wk);
+    uint32_t es = dppu<0x138, 0xf>(ws), ek = dppu<0x138, 0xf>(wk);  // (wave_shr:1)
+    es = lane == 0 ? cs : es;
+    ek = lane == 0 ? ck : ek;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + 4 * lane + q;
+      if (!vf[q]) {
+        vs[q] = min(es + vs[q], kSegSat);
+        vk[q] = pk_max(ek, vk[q]);
+      }
+      if (c < nch) {
+        sInc[c] = vs[q];
+        sKey[c] = vk[q];
+      }
+    }
+    cs = (uint32_t)rdl((int)vs[3], 63);
+    ck = (uint32_t)rdl((int)vk[3], 63);
   }
   f = (__ballot((f & kPos) != 0u) ? kPos : 0u) | (__ballot((f & kNeg) != 0u) ? kNeg : 0u) |
       (__ballot((f & kBad) != 0u) ? kBad : 0u);
@@ -676,96 +826,180 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
     }
     res = s;
   } else {
-    int E = kEMin, k = 0, j = 0;
+    int E = kEMin, k = 0;
+    unsigned long long c_step = 0ull, c_fetch = 0ull, c_exact = 0ull, c_zero = 0ull, c0 = 0ull;
+    // chunk j term by term from the state: operands u, v of the lane's 4
+    // cells (from stash slot sl, or sl < 0: loaded from the rows)
+    auto exact_chunk = [&](int j, int sl, f4a u, f4a v) {
+      if (cdf && lane == 0) a.cst[j] = make_int2(E, k);
+      ++n_fb;
+      n_hit += sl >= 0;
+      const int x0 = j * kFcChunk + 4 * lane;
+      float t[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = x0 + q < n ? fabsf(R.term(u[q], v[q])) : 0.0f;
+      if (a.stats) {
+        const float tt = t[0] + t[1] + t[2] + t[3];  // (the fetch has landed)
+        asm volatile("" ::"v"(tt));
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+        c_fetch += c1 - c0;
+        c0 = c1;
+      }
+      // (from zero, the chunk climbs through many binades: the chain itself
+      // at once; else exact rounds, the chain itself after eight)
+      chunk_exact(t, lane, &E, &k, nullptr, &n_rounds, sT, j == 0 ? 0 : PP2_WALK_TAIL);
+      normalise(&E, &k);
+      if (a.stats) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+        (j == 0 ? c_zero : c_exact) += c1 - c0;
+        c0 = c1;
+      }
+    };
+    // operands of chunk j (stash slot sl, or from the rows)
+    auto operands = [&](int j, int sl, f4a* u, f4a* v) {
+      *v = f4a{0.0f, 0.0f, 0.0f, 0.0f};
+      if (sl >= 0) {
+        *u = *reinterpret_cast<const f4a*>(&sRaw[0][sl][4 * lane]);
+        if (R.p1) *v = *reinterpret_cast<const f4a*>(&sRaw[1][sl][4 * lane]);
+      } else {
+        const int x0 = j * kFcChunk + 4 * lane;
+        const int xs = x0 < a.ld ? x0 : 0;  // (masked at use)
+        *u = *reinterpret_cast<const f4a*>(R.p0 + xs);
+        if (R.p1) *v = *reinterpret_cast<const f4a*>(R.p1 + xs);
+      }
+    };
+    // a mispredicted segment [j, end): walk steps over its entries (256 a
+    // step, 4 a lane, branch-free), each failing chunk exactly
+    auto walk_steps = [&](int j, int end) {
 #pragma unroll 1
-    while (j < nch) {
-      ++n_it;
-      // a step: entries j .. j + 255, 4 per lane (branch-free reads)
-      uint32_t ev[4];
+      while (j < end) {
+        ++n_it;
+        uint32_t ev[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ev[q] = sE[min(j + 4 * lane + q, nch - 1)];
-      const uint32_t ebias = (uint32_t)(E + 128);
-      int dq[4], tot = 0;
-      bool vq[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        vq[q] = (j + 4 * lane + q < nch) & (ev[q] != kNoEntry) &
-                (((ev[q] >> 24) == ebias) | (((ev[q] & 0xffffffu) == 0u) & ((ev[q] >> 24) < ebias)));
-        dq[q] = vq[q] ? (int)(ev[q] & 0xffffffu) : 0;
-        tot += dq[q];
-      }
-      tot = min(tot, kK24 + 1);
-      const int excl = wave_incl_scan(tot, lane) - tot;
-      int run = k + excl, fq = 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool stop = fq == 4 && (!vq[q] || run + dq[q] > kK24);
-        fq = stop ? q : fq;
-        run = fq == 4 ? run + dq[q] : run;
-      }
-      const uint64_t failm = __ballot(fq < 4);
-      const int L = failm ? __builtin_ctzll(failm) : 64;
-      if (cdf && lane <= L) {
-        int r2 = k + excl;
-        const int lim = lane < L ? 4 : fq;
+        for (int q = 0; q < 4; ++q) ev[q] = sE[min(j + 4 * lane + q, nch - 1)];
+        const uint32_t ebias = (uint32_t)(E + 128);
+        int dq[4], tot = 0;
+        bool vq[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int m = j + 4 * lane + q;
-          if (q < lim && m < nch) a.cst[m] = make_int2(E, r2);
-          r2 += dq[q];
+          vq[q] = (j + 4 * lane + q < end) & (ev[q] != kNoEntry) &
+                  (((ev[q] >> 24) == ebias) | (((ev[q] & 0xffffffu) == 0u) & ((ev[q] >> 24) < ebias)));
+          dq[q] = vq[q] ? (int)(ev[q] & 0xffffffu) : 0;
+          tot += dq[q];
         }
-      }
-      const int fc = L < 64 ? 4 * L + rdl(fq, L) : 256;
-      k = rdl(run, L < 64 ? L : 63);
-      normalise(&E, &k);
-      j += fc;
-      // (a stop at the exact top of a binade: the normalised state may take
-      // chunk j's entry after all -- the next step does)
-      const uint32_t ej = j < nch ? sE[j] : kNoEntry;
-      if (j < nch && L < 64 && !(entry_applies(ej, E) && k + entry_units(ej) <= kK24)) {
-        // chunk j term by term: its |terms| from the staged operand rows (or
-        // loaded now)
-        if (cdf && lane == 0) a.cst[j] = make_int2(E, k);
-        const int sl = sSlot[j];
-        if (a.stats && lane == 0) {  // why: no entry / another binade / the crossing
-          const uint32_t e = ej;
-          atomicAdd(a.stats + (e == kNoEntry ? 8 : (int)(e >> 24) != E + 128 ? 9 : 10), 1);
-          if (BASE == FC_ROW && K == 0) {  // (the last 1024 fallbacks: chunk, entry, state)
-            const int at = atomicAdd(a.stats + 15, 1);
-            int* tr = a.stats + 128 + 4 * (at & 1023);
-            tr[0] = j; tr[1] = (int)e; tr[2] = E; tr[3] = k;
+        tot = min(tot, kK24 + 1);
+        const int excl = wave_incl_scan(tot, lane) - tot;
+        int run = k + excl, fq = 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool stop = fq == 4 && (!vq[q] || run + dq[q] > kK24);
+          fq = stop ? q : fq;
+          run = fq == 4 ? run + dq[q] : run;
+        }
+        const uint64_t failm = __ballot(fq < 4);
+        const int L = failm ? __builtin_ctzll(failm) : 64;
+        if (cdf && lane <= L) {
+          int r2 = k + excl;
+          const int lim = lane < L ? 4 : fq;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int m = j + 4 * lane + q;
+            if (q < lim && m < end) a.cst[m] = make_int2(E, r2);
+            r2 += dq[q];
           }
         }
-        ++n_fb;
-        n_hit += sl >= 0;
-        const int x0 = j * kFcChunk + 4 * lane;
-        f4a u, v = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (sl >= 0) {
-          u = *reinterpret_cast<const f4a*>(&sRaw[0][sl][4 * lane]);
-          if (R.p1) v = *reinterpret_cast<const f4a*>(&sRaw[1][sl][4 * lane]);
-        } else {
-          const int xs = x0 < a.ld ? x0 : 0;  // (masked below)
-          u = *reinterpret_cast<const f4a*>(R.p0 + xs);
-          if (R.p1) v = *reinterpret_cast<const f4a*>(R.p1 + xs);
-        }
-        float t[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = x0 + q < n ? fabsf(R.term(u[q], v[q])) : 0.0f;
-        if (j == 0) {
-          // from zero: lane 0's own fp32 chain over the chunk's terms, 4 a lane
-          float s = value_of(E, k);
-#pragma unroll 1
-          for (int l = 0; l < 64; ++l) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) s = s + rdl(t[q], l);
-          }
-          state_of(s, &E, &k);
-        } else {
-          chunk_exact(t, lane, &E, &k, nullptr, &n_rounds);
-        }
+        const int fc = L < 64 ? 4 * L + rdl(fq, L) : 256;
+        k = rdl(run, L < 64 ? L : 63);
         normalise(&E, &k);
-        ++j;
+        j += fc;
+        // (a stop at the exact top of a binade: the normalised state may take
+        // chunk j's entry after all -- the next step does)
+        const uint32_t ej = j < end ? sE[j] : kNoEntry;
+        if (j < end && L < 64 && !(entry_applies(ej, E) && k + entry_units(ej) <= kK24)) {
+          f4a u, v;
+          operands(j, -1, &u, &v);
+          exact_chunk(j, -1, u, v);
+          ++j;
+        }
       }
+    };
+    // the first 64 segments' records in registers (lane l: segment l's end,
+    // increment and keys; an empty segment's are neutral)
+    int rb = nch;
+    uint32_t rS = 0u, rK = 0u;
+    if (lane <= nb) {
+      rb = lane < nb ? (int)sBrk[lane] : nch;
+      const int ra = lane == 0 ? 0 : (int)sBrk[lane - 1] + 1;
+      if (ra < rb) {
+        rS = sInc[rb - 1];
+        rK = sKey[rb - 1];
+      }
+    }
+    f4a nu = {0.0f, 0.0f, 0.0f, 0.0f}, nv = nu;  // (break 0's operands, staged one break ahead)
+    if (nb > 0 && kWkStash > 0) operands(0, 0, &nu, &nv);
+    if (a.stats) c0 = __builtin_amdgcn_s_memtime();
+    // 2. the walk: segment i (from break i - 1 to break i), then break i
+    int a0 = 0;
+#pragma unroll 1
+    for (int bi = 0;; ++bi) {
+      normalise(&E, &k);
+      int b;
+      uint32_t S, ky;
+      if (bi < 64) {
+        b = rdl(rb, bi);
+        S = (uint32_t)rdl((int)rS, bi);
+        ky = (uint32_t)rdl((int)rK, bi);
+      } else {
+        b = bi < nb ? (int)sBrk[bi] : nch;
+        S = a0 < b ? sInc[b - 1] : 0u;
+        ky = a0 < b ? sKey[b - 1] : 0u;
+      }
+      if (a0 < b) {
+        const int eb = E + 128;
+        const bool fast =
+            (int)(ky >> 16) <= eb && 255 - (int)(ky & 0xffffu) >= eb && (int)S <= kK24 - k;
+        if (fast) {
+          if (cdf && lane == 0) sSeg[bi] = make_int2(E, k);
+          k += (int)S;
+        } else {
+          if (cdf && lane == 0) sSeg[bi] = make_int2(kSegSlow, 0);
+          ++n_slow;
+          walk_steps(a0, b);
+        }
+      }
+      if (a.stats) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+        c_step += c1 - c0;
+        c0 = c1;
+      }
+      if (bi >= nb) break;
+      normalise(&E, &k);
+      const int sl = bi < kWkStash ? bi : -1;
+      f4a u = nu, v = nv;
+      if (sl < 0) operands(b, -1, &u, &v);
+      if (bi + 1 < nb && bi + 1 < kWkStash) operands(0, bi + 1, &nu, &nv);  // (the next break's, ahead)
+      exact_chunk(b, sl, u, v);
+      a0 = b + 1;
+    }
+    // 3. (cdf) every segment chunk's start state
+    if (cdf) {
+#pragma unroll 1
+      for (int m = lane; m < nch; m += 64) {
+        const int o = sOrd[m];
+        if (o < 0) continue;  // (a break: walked above)
+        const int2 st = sSeg[o];
+        if (st.x == kSegSlow) continue;
+        a.cst[m] = make_int2(st.x, st.y + (int)(sInc[m] - (uint32_t)entry_units(sE[m])));
+      }
+    }
+    if (a.stats && lane == 0) {  // (s_memtime cycles: segments, fetches, exact rounds, chunk 0)
+      atomicAdd(a.stats + 8, nb);
+      atomicAdd(a.stats + 9, n_slow);
+      atomicAdd(a.stats + 10, n_fb - nb);
+      atomicAdd(a.stats + 11, (int)c_step);
+      atomicAdd(a.stats + 12, (int)c_fetch);
+      atomicAdd(a.stats + 13, (int)c_exact);
+      atomicAdd(a.stats + 14, (int)c_zero);
     }
     const float r = value_of(E, k);
     res = neg ? (r == 0.0f ? 0.0f : -r) : r;
@@ -798,6 +1032,7 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
 // One wave per chunk: every running sum of the row from the chunk's exact
 // start state (k_fc_drive's a.cst), term by term (chunk_exact).
 __global__ __launch_bounds__(256) void k_fc_cdf(FcArgs a) {
+  __shared__ __attribute__((aligned(16))) float sT[4][kFcChunk];  // (chunk_exact's chain tails)
   const int lane = threadIdx.x & 63;
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = a.n, nch = fc_chunks(n);
@@ -814,7 +1049,7 @@ __global__ __launch_bounds__(256) void k_fc_cdf(FcArgs a) {
   for (int q = 0; q < 4; ++q) t[q] = fabsf(t[q]);
   int E = a.cst[j].x, k = a.cst[j].y;
   float cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  chunk_exact(t, lane, &E, &k, &cv);
+  chunk_exact(t, lane, &E, &k, &cv, nullptr, sT[threadIdx.x >> 6], PP2_WALK_TAIL);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const float v = neg ? (cv[q] == 0.0f ? 0.0f : -cv[q]) : cv[q];
@@ -2214,19 +2449,20 @@ extern "C" int pp2_debug_fc_walk(int on) {
 // Diagnostic (tools/prof_planner.py, PP2_FC_STATS=1): the drivers' counters
 // summed per set kind over every launch -- out[16 * (2 * base + (K > 0)) + c],
 // c as pp2_debug_fchain_row2's stats; k_fc_walk's fallback chunks by cause in
-// c = 8 (no entry), 9 (entry for another binade), 10 (the binade crossing).
-// (128 ints; then the last 1024 row-set fallbacks {chunk, entry, E, k}, a ring (diagnostic))  enable=1 allocates (before the sets to
+// k_fc_walk's c = 8 (breaks), 9 (mispredicted segments), 10 (their failing
+// chunks), 11 .. 14 (s_memtime cycles in segments, fetches of exact chunks,
+// exact rounds, chunk 0).  (128 ints)  enable=1 allocates (before the sets to
 // count are launched), out != nullptr copies the 64 counters out and clears them.
 extern "C" int pp2_debug_fc_stats(int* out, int enable) {
   if (enable && !pp2::g_fc_stats) {
-    if (hipMalloc(&pp2::g_fc_stats, (128 + 4096) * sizeof(int)) != hipSuccess) return 1;
-    if (hipMemset(pp2::g_fc_stats, 0, (128 + 4096) * sizeof(int)) != hipSuccess) return 1;
+    if (hipMalloc(&pp2::g_fc_stats, 128 * sizeof(int)) != hipSuccess) return 1;
+    if (hipMemset(pp2::g_fc_stats, 0, 128 * sizeof(int)) != hipSuccess) return 1;
   }
   if (out && pp2::g_fc_stats) {
     if (hipDeviceSynchronize() != hipSuccess) return 1;
-    if (hipMemcpy(out, pp2::g_fc_stats, (128 + 4096) * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(out, pp2::g_fc_stats, 128 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
       return 1;
-    if (hipMemset(pp2::g_fc_stats, 0, (128 + 4096) * sizeof(int)) != hipSuccess) return 1;
+    if (hipMemset(pp2::g_fc_stats, 0, 128 * sizeof(int)) != hipSuccess) return 1;
   }
   return 0;
 }

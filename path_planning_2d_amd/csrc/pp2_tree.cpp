@@ -1291,7 +1291,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   p->ref_ld = row_ld;
   {
     const char* e = getenv("PP2_FX");
-    p->fx = p->ref && !p->seq && pp2::fx_fits((int)p->n, row_ld) && !(e && e[0] == '0');
+    // (opt-in: on the 256^2 plan step the fused sets run 0.56-0.57 ms p50
+    // against 0.45-0.47 for the three-launch sets with k_fc_walk,
+    // tools/ab_planner.sh)
+    p->fx = p->ref && !p->seq && pp2::fx_fits((int)p->n, row_ld) && e && e[0] == '1';
     const char* d = getenv("PP2_FX_STAMPS");
     if (p->fx && d && d[0] == '1' &&
         hipMalloc(&p->d_stamps, kFxStampWGs * 8 * sizeof(unsigned long long)) != hipSuccess)
