@@ -103,17 +103,27 @@ PP2_FC_HD inline float units_of(float a, int E, bool* tie) {
   return r;
 }
 
-// One term a = |t| (finite) added to the state exactly: its increment when
-// that applies (no tie, the sum stays within 2^(E+1)), else the fp32 add
-// itself.  (k == 2^24 is left as is: a later increment of 0 keeps it, any
-// other goes through the fp32 add from value_of, which normalises.)  A wave
-// applies this to a chunk's terms in parallel: the increments' prefix sum up
-// to the first term that does not apply, that term's fp32 add, and again.
+// A tie, t/u = m + 1/2, rounds to the even one of k + m and k + m + 1: its
+// increment is m + ((k + m) & 1) -- it depends on k only through k's parity,
+// and leaves k even.  (m = q - 1/2, exact: q is a half-integer below 2^26.)
+PP2_FC_HD inline int tie_increment(float q, int k) {
+  const int m = (int)(q - 0.5f);
+  return m + ((k + m) & 1);
+}
+
+// One term a = |t| (finite) added to the state exactly: its increment (a
+// tie's by the parity of k) when that applies (the sum stays within
+// 2^(E+1)), else the fp32 add itself.  (k == 2^24 is left as is: a later
+// increment of 0 keeps it, any other goes through the fp32 add from
+// value_of, which carries.)  A wave applies this to a chunk's terms in
+// parallel: the increments' prefix sum up to the first term that does not
+// apply, that term's fp32 add, and again (chunk_exact).
 PP2_FC_HD inline void add_exact(int* E, int* k, float a) {
   bool tie;
   const float r = units_of(a, *E, &tie);
-  if (!tie && *k + (int)r <= kK24) {
-    *k += (int)r;
+  const int inc = tie ? tie_increment(ldexpf(a, 23 - *E), *k) : (int)r;
+  if (*k + inc <= kK24) {
+    *k += inc;
   } else {
     const float s = value_of(*E, *k) + a;
     state_of(s, E, k);

@@ -75,6 +75,38 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+// Segment records of the walker (k_fc_walk): a chunk's increments summed from
+// its segment's head, saturated at 2^25, and its domain keys (hi 16 bits: the
+// largest entry domain; lo 16 bits: 255 - the smallest domain of an entry
+// adding something), both as running values from the head -- segmented wave
+// scans on DPP (row shifts, then row_bcast:15 / :31).
+constexpr uint32_t kSegSat = 1u << 25;
+
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+  return max(a & 0xffff0000u, b & 0xffff0000u) | max(a & 0xffffu, b & 0xffffu);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dppu(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ void seg_step(uint32_t& f, uint32_t& s, uint32_t& k) {
+  const uint32_t pf = dppu<CTRL, RM>(f), ps = dppu<CTRL, RM>(s), pk = dppu<CTRL, RM>(k);
+  const bool head = f != 0u;
+  s = head ? s : min(ps + s, kSegSat);
+  k = head ? k : pk_max(pk, k);
+  f |= pf;
+}
+// inclusive segmented scan over the lanes (f: a head in or before the lane)
+__device__ __forceinline__ void wave_seg_scan(uint32_t& f, uint32_t& s, uint32_t& k) {
+  seg_step<0x111, 0xf>(f, s, k);
+  seg_step<0x112, 0xf>(f, s, k);
+  seg_step<0x114, 0xf>(f, s, k);
+  seg_step<0x118, 0xf>(f, s, k);
+  seg_step<0x142, 0xa>(f, s, k);
+  seg_step<0x143, 0xc>(f, s, k);
+}
+
 // the wave's total (uniform): any association will do for these sums
 // (approximate running sums, or integer-valued floats below 2^24)
 __device__ __forceinline__ float wave_sum(float v) {
@@ -334,6 +366,10 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
 // from `done` on up to the first that does not apply (a tie, or past
 // 2^(E+1)), adds that one in fp32, and goes on after it (add_exact, in
 // parallel).  With cv, every running value (cv[q] of term 4l + q).
+// (Ties could go by the parity of the state before them, tie_increment, a
+// segmented XOR scan a round: measured in the 256^2 plan step, its chains'
+// events are binade crossings, and the longer round cost more than the
+// ties it saved.)
 //
 // A round is ~130 instructions of one wave (~850 cycles in the plan step,
 // beside the other stream's kernels); the chain itself is 256 dependent adds
@@ -379,7 +415,6 @@ __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* 
     if (rounds) ++*rounds;
     int r[4];
     bool tie[4];
-    int tot = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       bool tx;
@@ -387,8 +422,10 @@ __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* 
       const bool act = 4 * lane + q >= done;
       r[q] = act ? (int)rf : 0;
       tie[q] = act && tx;
-      tot += r[q];
     }
+    int tot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tot += r[q];
     tot = min(tot, kK24 + 1);  // no scan overflow; anything above 2^24 fails anyway
     const int incl = wave_incl_scan(tot, lane);
     // the lane's terms in order: each applies (k grows by its increment)
@@ -641,38 +678,7 @@ struct WalkRows {
   }
 };
 
-// Segment records of the walker (below): a chunk's increments summed from
-// its segment's head, saturated at 2^25, and its domain keys (hi 16 bits: the
-// largest entry domain; lo 16 bits: 255 - the smallest domain of an entry
-// adding something), both as running values from the head -- segmented wave
-// scans on DPP (row shifts, then row_bcast:15 / :31).
-constexpr uint32_t kSegSat = 1u << 25;
 constexpr int kSegSlow = 1 << 20;  // sSeg[].x: the segment was walked chunk by chunk
-
-__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
-  return max(a & 0xffff0000u, b & 0xffff0000u) | max(a & 0xffffu, b & 0xffffu);
-}
-template <int CTRL, int RM>
-__device__ __forceinline__ uint32_t dppu(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xf, false);
-}
-template <int CTRL, int RM>
-__device__ __forceinline__ void seg_step(uint32_t& f, uint32_t& s, uint32_t& k) {
-  const uint32_t pf = dppu<CTRL, RM>(f), ps = dppu<CTRL, RM>(s), pk = dppu<CTRL, RM>(k);
-  const bool head = f != 0u;
-  s = head ? s : min(ps + s, kSegSat);
-  k = head ? k : pk_max(pk, k);
-  f |= pf;
-}
-// inclusive segmented scan over the lanes (f: a head in or before the lane)
-__device__ __forceinline__ void wave_seg_scan(uint32_t& f, uint32_t& s, uint32_t& k) {
-  seg_step<0x111, 0xf>(f, s, k);
-  seg_step<0x112, 0xf>(f, s, k);
-  seg_step<0x114, 0xf>(f, s, k);
-  seg_step<0x118, 0xf>(f, s, k);
-  seg_step<0x142, 0xa>(f, s, k);
-  seg_step<0x143, 0xc>(f, s, k);
-}
 
 // k_fc_drive's job for chains of at most kWkEntries chunks, as a walk over
 // SEGMENTS.  The tables mark the chunks a chain will likely not take from its
@@ -1015,6 +1021,17 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
     atomicAdd(a.stats + 5, (int)(tk2 - tk1));
     atomicAdd(a.stats + 6, (int)(tk3 - tk2));
     atomicAdd(a.stats + 7, 1);
+    // (the longest chain, 100 MHz ticks, and -- racy, a diagnostic -- its
+    // breaks, exact rounds, mispredicted segments, stash hits, entries)
+    const int dur = (int)(tk3 - tk0);
+    if (atomicMax(a.stats + 15, dur) < dur) {
+      a.stats[16] = n_fb;
+      a.stats[17] = n_rounds;
+      a.stats[18] = n_it;
+      a.stats[19] = n_hit;
+      a.stats[20] = nch;
+      a.stats[21] = id;
+    }
   }
   if (lane == 0) {
     if (BASE == FC_LIST) {  // out[row * ldo + partner]
@@ -1902,7 +1919,7 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
     hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
   }
   if (phases & FC_DRIVE) {
-    if (g_fc_stats && !a.stats) a.stats = g_fc_stats + 16 * (2 * BASE + (K > 0));
+    if (g_fc_stats && !a.stats) a.stats = g_fc_stats + 32 * (2 * BASE + (K > 0));
     if (fc_walk_enabled() && fc_chunks(a.n) <= kWkEntries)
       hipLaunchKernelGGL((k_fc_walk<BASE, K>), dim3(std::min(groups * KC, kFcDriveBlocks)),
                          dim3(64), 0, st, a);
@@ -2451,18 +2468,19 @@ extern "C" int pp2_debug_fc_walk(int on) {
 // c as pp2_debug_fchain_row2's stats; k_fc_walk's fallback chunks by cause in
 // k_fc_walk's c = 8 (breaks), 9 (mispredicted segments), 10 (their failing
 // chunks), 11 .. 14 (s_memtime cycles in segments, fetches of exact chunks,
-// exact rounds, chunk 0).  (128 ints)  enable=1 allocates (before the sets to
+// exact rounds, chunk 0), 15 .. 21 (the longest chain and its counts).
+// (256 ints)  enable=1 allocates (before the sets to
 // count are launched), out != nullptr copies the 64 counters out and clears them.
 extern "C" int pp2_debug_fc_stats(int* out, int enable) {
   if (enable && !pp2::g_fc_stats) {
-    if (hipMalloc(&pp2::g_fc_stats, 128 * sizeof(int)) != hipSuccess) return 1;
-    if (hipMemset(pp2::g_fc_stats, 0, 128 * sizeof(int)) != hipSuccess) return 1;
+    if (hipMalloc(&pp2::g_fc_stats, 256 * sizeof(int)) != hipSuccess) return 1;
+    if (hipMemset(pp2::g_fc_stats, 0, 256 * sizeof(int)) != hipSuccess) return 1;
   }
   if (out && pp2::g_fc_stats) {
     if (hipDeviceSynchronize() != hipSuccess) return 1;
-    if (hipMemcpy(out, pp2::g_fc_stats, 128 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(out, pp2::g_fc_stats, 256 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
       return 1;
-    if (hipMemset(pp2::g_fc_stats, 0, 128 * sizeof(int)) != hipSuccess) return 1;
+    if (hipMemset(pp2::g_fc_stats, 0, 256 * sizeof(int)) != hipSuccess) return 1;
   }
   return 0;
 }

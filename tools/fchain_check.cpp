@@ -208,6 +208,22 @@ int main(int argc, char** argv) {
       t.push_back(rep % 2 ? ldexpf(U(rng), -40) : (i % 7 ? 0.0f : ldexpf(1.0f, -26)));
     for (int c : chunks) check("concentrated + tail", t, c, &st);
   }
+  // ties one by one: a term of (m + 1/2) ulps on a random state -- the
+  // increment by k's parity (tie_increment) against the fp32 add
+  for (int rep = 0; rep < 2000000; ++rep) {
+    const int E = -126 + (int)(rng() % 250);
+    const int k = (E == kEMin ? 0 : (1 << 23)) + (int)(rng() % (1u << 23));
+    const int m = (int)(rng() % 5 == 0 ? rng() % 4 : rng() % (1u << (rng() % 23)));
+    const float t = ldexpf((float)m + 0.5f, E - 23);
+    if (!std::isfinite(t) || t == 0.0f) continue;
+    int E2 = E, k2 = k;
+    add_exact(&E2, &k2, t);
+    const float want = value_of(E, k) + t;
+    if (bits_of(value_of(E2, k2)) != bits_of(want)) {
+      if (g_exact_fail < 5) printf("TIE E=%d k=%d m=%d\n", E, k, m);
+      ++g_exact_fail;
+    }
+  }
   // all zeros, -0, empty, single
   {
     std::vector<float> z(1000, 0.0f), mz(1000, -0.0f), e, one(1, -3.5f);

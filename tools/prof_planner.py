@@ -51,7 +51,7 @@ def main():
         stats.argtypes = [C.c_void_p, C.c_int]
         stats.restype = C.c_int
         assert stats(None, 1) == 0
-        buf = np.zeros(128, np.int32)
+        buf = np.zeros(256, np.int32)
         stats(buf.ctypes.data, 0)  # (clears the warm-up's counts)
     with planner() as pl:
         t0 = time.perf_counter()
@@ -62,7 +62,7 @@ def main():
         assert stats(buf.ctypes.data, 0) == 0
         names = ["row", "row x9", "child", "child x9", "list", "list x9", "-", "-"]
         for kind in range(8):
-            c = buf[16 * kind:16 * kind + 16].view(np.uint32).astype(np.int64)  # (wrapping sums)
+            c = buf[32 * kind:32 * kind + 32].view(np.uint32).astype(np.int64)  # (wrapping sums)
             if c[7]:
                 print(f"set {names[kind]:8s}: chains {c[7]}, per chain: iterations {c[0] / c[7]:.1f}, "
                       f"fallbacks {c[1] / c[7]:.1f}, exact rounds {c[2] / c[7]:.1f}, stash hits "
@@ -70,7 +70,9 @@ def main():
                       f"walk {c[6] / c[7] / 100:.2f}; fallbacks: no entry {c[8] / c[7]:.1f}, other "
                       f"binade {c[9] / c[7]:.1f}, crossing {c[10] / c[7]:.1f}; s_memtime per chain: steps "
                       f"{c[11] / c[7]:.0f}, fetches {c[12] / c[7]:.0f}, exact {c[13] / c[7]:.0f}, "
-                      f"chunk 0 {c[14] / c[7]:.0f}", flush=True)
+                      f"chunk 0 {c[14] / c[7]:.0f}; longest chain {c[15] / 100:.2f} us (exact chunks {c[16]}, "
+                      f"rounds {c[17]}, slow steps {c[18]}, stash hits {c[19]}, chunks {c[20]}, "
+                      f"group {c[21]})", flush=True)
     ctx.close()
     print(f"case {case} lb {lb} reference_order={ref}: {steps} plan steps: p50 "
           f"{np.percentile(ms, 50):.3f} ms, mean {ms.mean():.3f} ms, wall {el * 1e3:.1f} ms, "
