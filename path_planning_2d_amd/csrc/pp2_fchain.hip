@@ -137,6 +137,19 @@ __device__ __forceinline__ int zero_domain(uint32_t mx) {
   return max(e + 25, kEMin);
 }
 
+// inclusive float scan of a wave (any association: approximate running sums)
+__device__ __forceinline__ float wave_incl_scan_f(float v, int lane) {
+  int b = __builtin_bit_cast(int, v);
+#pragma unroll
+  for (int c = 1; c < 16; c <<= 1)
+    b = __builtin_bit_cast(int, __builtin_bit_cast(float, b) +
+                                    __builtin_bit_cast(float, row_shr(b, c)));
+  const float f = __builtin_bit_cast(float, b);
+  const float r0 = rdl(f, 15), r1 = rdl(f, 31), r2 = rdl(f, 47);
+  const int row = lane >> 4;
+  return f + (row >= 1 ? r0 : 0.0f) + (row >= 2 ? r1 : 0.0f) + (row >= 3 ? r2 : 0.0f);
+}
+
 // The device's flush of a product (FTZ build of the reference kernel).
 __device__ __forceinline__ float ftz(float v) {
   return fabsf(v) < FLT_MIN ? copysignf(0.0f, v) : v;
@@ -162,12 +175,17 @@ struct Terms {
   const float* __restrict__ lr;  // FC_CHILD: the likelihood row of observation z
   const float* __restrict__ part;
   int n, ld;
+  float m;  // FC_KEPT: the child's mass (set by the kernel)
 
   __device__ __forceinline__ void init(const FcArgs& a, int id) {
     n = a.n;
     ld = a.ld;
     part = a.partners;
-    if (BASE == FC_ROW) {
+    m = 1.0f;
+    if (BASE == FC_KEPT) {
+      pr = a.pred + (long long)(id % 9) * ld;
+      lr = a.lrows + (long long)(id / 9) * ld;
+    } else if (BASE == FC_ROW) {
       pr = a.row + (long long)id * a.row_stride;
       lr = nullptr;
     } else if (BASE == FC_LIST) {  // row plist[id].x times partner plist[id].y
@@ -184,6 +202,7 @@ struct Terms {
   __device__ __forceinline__ float base(int x) const {
     if (BASE == FC_ROW) return pr[x];
     if (BASE == FC_LIST) return pr[x] * lr[x];
+    if (BASE == FC_KEPT) return ftz(pr[x] * ftz(lr[x])) / m;  // (search_tree_cuda.cu:228-229)
     return ftz(pr[x] * ftz(lr[x]));
   }
   __device__ __forceinline__ float term(float v, int i, int x) const {
@@ -215,6 +234,10 @@ struct Terms {
         const f4a l = *reinterpret_cast<const f4a*>(lr + x0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = ftz(p[q] * ftz(l[q]));
+      } else if (BASE == FC_KEPT) {
+        const f4a l = *reinterpret_cast<const f4a*>(lr + x0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ftz(p[q] * ftz(l[q])) / m;
       } else if (BASE == FC_LIST) {
         const f4a l = *reinterpret_cast<const f4a*>(lr + x0);
 #pragma unroll
@@ -235,6 +258,16 @@ struct Terms {
   }
 };
 
+// FC_KEPT: the child's mass -- exact (mass) or, for the sums, approximate
+// (the children set's chunk sums; any value will do there: it only scales
+// the chunk sums the binades are predicted from)
+__device__ __forceinline__ float kept_mass(const FcArgs& a, int id, int nch, int lane) {
+  if (a.mass) return a.mass[id];
+  float acc = 0.0f;
+  for (int c = lane; c < nch; c += 64) acc += a.msum[(long long)id * nch + c];
+  return wave_sum(acc);
+}
+
 // ---------------------------------------------------------------- pass 1
 template <int BASE, int K>
 __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
@@ -248,6 +281,8 @@ __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
   T.init(a, id);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = fc_chunks(a.n), nseg = fc_segments(a.n);
+  const int gc = a.by_id ? id : g;  // (the scratch chains' index)
+  if (BASE == FC_KEPT) T.m = kept_mass(a, id, nch, lane);
   if (threadIdx.x < KC) sFlags[threadIdx.x] = 0u;
   __syncthreads();
   uint32_t fl[KC];
@@ -269,7 +304,7 @@ __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
         fl[i] |= !isfinite(t) ? kBad : t > 0.0f ? kPos : t < 0.0f ? kNeg : 0u;
       }
       const float sum = wave_sum(acc);
-      if (lane == 0) a.csum[(long long)(g * KC + i) * nch + j] = sum;
+      if (lane == 0) a.csum[(long long)(gc * KC + i) * nch + j] = sum;
     }
   }
 #pragma unroll
@@ -281,8 +316,127 @@ __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
   }
   __syncthreads();
   if (threadIdx.x < KC)
-    a.cflag[(long long)(g * KC + threadIdx.x) * nseg + seg] = sFlags[threadIdx.x];
+    a.cflag[(long long)(gc * KC + threadIdx.x) * nseg + seg] = sFlags[threadIdx.x];
   __syncthreads();  // (sFlags of the next group)
+  }
+}
+
+// ---------------------------------------------------------------- crossing plans
+// A predicted chunk (kPredicted: the approximate running sum crosses a
+// binade in it, or no entry) is where a walker leaves its entries for exact
+// rounds.  Most such chunks hold one to three binade crossings and nothing
+// else; their walk is then known up to the crossing terms' exact adds: the
+// tables kernel predicts the crossing terms from the approximate running sum
+// (sP + the chunk's fp32 prefix of |t|) and records
+//   E0, the domain it assumed at the chunk start,
+//   d_0, the increments in E0 of the terms before the first crossing,
+//   for each crossing s = 1 .. nc: the term t*_s, its domain after, D_s, and
+//   d_s, the increments in D_s of the terms up to the next crossing,
+// valid only with no tie among the non-crossing terms and every d_s < 2^24.
+// A walker arriving in state (E, k) follows it as the scalar chain
+//   E == E0, k + d_0 <= 2^24; then per crossing s = fl(value_of(E, k) + t*_s)
+//   (the reference's own add), state_of(s) in domain D_s, k + d_s <= 2^24
+// and falls back to exact rounds on any failed check -- so the plan only
+// decides the speed.  (A term before a crossing applies iff no tie and the
+// sum stays <= 2^24, which the checks guarantee for the whole run.)
+// Record: two uint4 per chunk, w0 = valid | nc << 1 | (E0 + 128) << 8 |
+// (D_1 - E0) << 16 | (D_2 - E0) << 20 | (D_3 - E0) << 24, w1 = d_0,
+// then (t*_s bits, d_s) for s = 1 .. 3.
+constexpr int kPlanMax = 3;
+
+__device__ __forceinline__ void chunk_plan(const float (&tt)[4], float sp, int E, int lane,
+                                           uint4* out) {
+  // the approximate running sum after each term (DPP float scan), its domain
+  float c[4], acc = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    acc += fabsf(tt[q]);
+    c[q] = acc;
+  }
+  int fb = __builtin_bit_cast(int, acc);
+#pragma unroll
+  for (int sh = 1; sh < 16; sh <<= 1)
+    fb = __builtin_bit_cast(int, __builtin_bit_cast(float, fb) +
+                                     __builtin_bit_cast(float, row_shr(fb, sh)));
+  fb = __builtin_bit_cast(int, __builtin_bit_cast(float, fb) +
+                                   __builtin_bit_cast(float, (int)dppu<0x142, 0xa>((uint32_t)fb)));
+  fb = __builtin_bit_cast(int, __builtin_bit_cast(float, fb) +
+                                   __builtin_bit_cast(float, (int)dppu<0x143, 0xc>((uint32_t)fb)));
+  const float ex = __builtin_bit_cast(float, fb) - acc;
+  int D[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) D[q] = domain_of(sp + (ex + c[q]));
+  int prev = (int)dppu<0x138, 0xf>((uint32_t)D[3]);  // (wave_shr:1: the lane before's last)
+  prev = lane == 0 ? E : prev;
+  bool cr[4];
+  int ncl = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    cr[q] = D[q] > prev;
+    prev = D[q];
+    ncl += cr[q];
+  }
+  const int nci = wave_incl_scan(ncl, lane);
+  const int nc = rdl(nci, 63);
+  uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  if (nc >= 1 && nc <= kPlanMax) {
+    // the non-crossing terms' increments in their domains, their running
+    // sum over the chunk (a crossing term adds none: it is an fp32 add)
+    int u[4], pu[4], acu = 0, ci[4], cnt = nci - ncl;
+    bool tie = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bool tx = false;
+      const float uf = cr[q] ? 0.0f : units_of(fabsf(tt[q]), D[q], &tx);
+      tie = tie || tx;
+      u[q] = (int)fminf(uf, (float)kK24);  // (no scan overflow: >= 2^24 fails)
+      acu += u[q];
+      pu[q] = acu;
+      cnt += cr[q];
+      ci[q] = cnt;
+    }
+    // (a lane adding 2^24 or more holds a run that cannot apply: no plan; so
+    // the scan below stays under 2^30)
+    bool valid = __ballot(tie || acu > kK24) == 0ull;
+    const int pincl = wave_incl_scan(min(acu, kK24), lane), pex = pincl - min(acu, kK24);
+    // P_s: the running increment at crossing s; d_s = P_{s+1} - P_s (P_0 = 0,
+    // P_{nc+1} = the chunk's total)
+    int Pprev = 0;
+    w[0] = 1u | ((uint32_t)nc << 1) | ((uint32_t)(E + 128) << 8);
+#pragma unroll
+    for (int sg = 1; sg <= kPlanMax; ++sg) {
+      if (sg <= nc) {
+        uint32_t tv = 0u;
+        int dv = 0, pv = 0;
+        bool has = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool me = cr[q] && ci[q] == sg;
+          tv = me ? bits_of(fabsf(tt[q])) : tv;
+          dv = me ? D[q] : dv;
+          pv = me ? pex + pu[q] : pv;
+          has = has || me;
+        }
+        const uint64_t m = __ballot(has);
+        const int L = m ? __builtin_ctzll(m) : 0;
+        const int off = rdl(dv, L) - E, P = rdl(pv, L);
+        valid = valid && m != 0ull && off >= 1 && off <= 15 && P - Pprev < kK24;
+        w[0] |= (uint32_t)(off & 15) << (12 + 4 * sg);
+        w[2 * sg - 1] = (uint32_t)(P - Pprev);
+        w[2 * sg] = (uint32_t)rdl((int)tv, L);
+        Pprev = P;
+      }
+    }
+    const int tot = rdl(pincl, 63);
+    valid = valid && tot - Pprev < kK24;
+#pragma unroll
+    for (int sg = 1; sg <= kPlanMax; ++sg)  // (d_nc: selects, no dynamic index)
+      w[2 * sg + 1] = sg == nc ? (uint32_t)(tot - Pprev) : w[2 * sg + 1];
+    if (!valid) w[0] = 0u;
+  }
+  if (lane == 0) {
+    out[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    out[1] = make_uint4(w[4], w[5], w[6], w[7]);
   }
 }
 
@@ -301,10 +455,12 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = fc_chunks(a.n);
   const int j0 = seg * kFcSegChunks;
+  const int gc = a.by_id ? id : g;  // (the scratch chains' index)
+  if (BASE == FC_KEPT) T.m = a.mass[id];
   // the approximate running sum before this segment, and inside it
 #pragma unroll
   for (int i = 0; i < KC; ++i) {
-    const float* cs = a.csum + (long long)(g * KC + i) * nch;
+    const float* cs = a.csum + (long long)(gc * KC + i) * nch;
     float acc = 0.0f;
     for (int t = threadIdx.x; t < j0; t += 256) acc += cs[t];
     acc = wave_sum(acc);
@@ -313,7 +469,7 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
   __syncthreads();
   if (threadIdx.x < KC) {
     const int i = threadIdx.x;
-    const float* cs = a.csum + (long long)(g * KC + i) * nch;
+    const float* cs = a.csum + (long long)(gc * KC + i) * nch;
     float run = (sPart[i][0] + sPart[i][1]) + (sPart[i][2] + sPart[i][3]);
     for (int c = 0; c < kFcSegChunks; ++c) {
       sP[i][c] = run;
@@ -326,6 +482,19 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
     const int x0 = j * kFcChunk + 4 * lane;
     float v[4];
     T.terms4(-1, x0, v);
+    if (BASE == FC_KEPT && a.kept_rows) {
+      // the kept child's normalised cells (k_store_kept's job): its dense row
+      // for the drive, and its node row
+      float* kr = a.kept_rows + (long long)id * a.ld;
+      float* nr = a.rowptr ? a.rowptr[id] : nullptr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (x0 + q < a.n) {
+          kr[x0 + q] = v[q];
+          if (nr) nr[x0 + q] = v[q];
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
       const int E = domain_of(sP[i][jl]);
@@ -344,15 +513,22 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
       const bool anytie = __ballot(tie) != 0ull;
       // a chunk adding nothing is tabled for the lowest domain where it adds
       // nothing (entry_applies: every domain above too)
-      const int Ez = ds == 0.0f ? zero_domain(wave_max_bits(mx)) : E;
-      if (lane == 0) {
-        const uint32_t e = make_entry(min(E, Ez), ds, anytie);
-        // predicted fallback: no entry, or the chunk's sum likely crosses
-        // into the next binade (from the approximate running sum)
-        // (a chunk adding nothing crosses nothing)
-        const bool pred = e == kNoEntry ||
-                          (ds > 0.0f && ldexpf(sP[i][jl], 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f));
-        a.tab[(long long)(g * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
+      int Ez = E;
+      if (ds == 0.0f) Ez = zero_domain(wave_max_bits(mx));  // (uniform)
+      const uint32_t e = make_entry(min(E, Ez), ds, anytie);
+      // predicted fallback: no entry, or the chunk's sum likely crosses
+      // into the next binade (from the approximate running sum)
+      // (a chunk adding nothing crosses nothing)
+      const bool pred = e == kNoEntry ||
+                        (ds > 0.0f && ldexpf(sP[i][jl], 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f));
+      if (lane == 0) a.tab[(long long)(gc * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
+      if (pred && a.plan) {
+        const unsigned long long p0 = a.stats ? __builtin_amdgcn_s_memtime() : 0ull;
+        chunk_plan(tt, sP[i][jl], E, lane, a.plan + 2 * ((long long)(gc * KC + i) * nch + j));
+        if (a.stats && lane == 0) {  // (plans: count, s_memtime cycles)
+          atomicAdd(a.stats + 22, 1);
+          atomicAdd(a.stats + 23, (int)(__builtin_amdgcn_s_memtime() - p0));
+        }
       }
     }
   }
@@ -448,9 +624,12 @@ __device__ __forceinline__ void chunk_exact(const float (&t)[4], int lane, int* 
       break;
     }
     const int lb = __builtin_ctzll(bm);
-    // (the failing term picked per lane, by selects: one readlane, no
-    // branches on the scalar unit)
-    const float tq = bad == 0 ? t[0] : bad == 1 ? t[1] : bad == 2 ? t[2] : t[3];
+    // (the failing term picked per lane by masks -- no branches on the
+    // scalar unit, and no dynamic index the compiler would put in scratch)
+    const uint32_t tqb =
+        (bits_of(t[0]) & (0u - (uint32_t)(bad == 0))) | (bits_of(t[1]) & (0u - (uint32_t)(bad == 1))) |
+        (bits_of(t[2]) & (0u - (uint32_t)(bad == 2))) | (bits_of(t[3]) & (0u - (uint32_t)(bad == 3)));
+    const float tq = __builtin_bit_cast(float, tqb);
     const int qb = rdl(bad, lb), kbef = rdl(kb, lb);
     const float tb = rdl(tq, lb);
     const float s = value_of(E, kbef) + tb;  // the reference's own add
@@ -483,12 +662,13 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
   T.init(a, id);
   const int lane = threadIdx.x;
   const int n = a.n, nch = fc_chunks(n), nseg = fc_segments(n);
-  const uint2* tab = a.tab + (long long)ch * nch;
+  const int cx = a.by_id ? id * KC + i : ch;  // (the scratch chain)
+  const uint2* tab = a.tab + (long long)cx * nch;
   const bool cdf = BASE == FC_ROW && K == 0 && a.cdf != nullptr;
   const unsigned long long tk0 = a.stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
   unsigned long long tk1 = 0ull, tk2 = 0ull;
   uint32_t f = 0u;
-  for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)ch * nseg + s];
+  for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)cx * nseg + s];
   f = (__ballot((f & kPos) != 0u) ? kPos : 0u) | (__ballot((f & kNeg) != 0u) ? kNeg : 0u) |
       (__ballot((f & kBad) != 0u) ? kBad : 0u);
   if (a.stats) tk1 = __builtin_amdgcn_s_memrealtime();
@@ -649,6 +829,7 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
 #endif
 constexpr int kWkEntries = 1024;  // chunk entries in LDS
 constexpr int kWkStash = 16;      // predicted fallback chunks staged in LDS
+constexpr int kWkPlan = 128;      // predicted chunks whose crossing plans are staged in LDS
 typedef __attribute__((address_space(3))) void fc_lds_void;
 typedef __attribute__((address_space(1))) void fc_glb_void;
 
@@ -706,6 +887,7 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
   __shared__ int2 sSeg[kWkEntries + 1];  // (cdf) each segment's start state
   __shared__ __attribute__((aligned(16))) float sRaw[2][kWkStash][kFcChunk];
   __shared__ __attribute__((aligned(16))) float sT[kFcChunk];  // (chunk_exact's chain tails)
+  __shared__ __attribute__((aligned(16))) uint32_t sPlan[kWkPlan][8];  // the first breaks' plans
   // (a walker is latency: first in its SIMD's issue arbitration, ahead of
   // the bandwidth kernels of the other stream sharing it)
   if (PP2_WALK_PRIO) __builtin_amdgcn_s_setprio(3);
@@ -717,15 +899,16 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
   R.init(a, id, i);
   const int lane = threadIdx.x;
   const int n = a.n, nch = fc_chunks(n), nseg = fc_segments(n);
-  const uint2* tab = a.tab + (long long)ch * nch;
+  const int cx = a.by_id ? id * KC + i : ch;  // (the scratch chain)
+  const uint2* tab = a.tab + (long long)cx * nch;
   const bool cdf = BASE == FC_ROW && K == 0 && a.cdf != nullptr;
   const unsigned long long tk0 = a.stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
   unsigned long long tk1 = 0ull, tk2 = 0ull;
-  int n_it = 0, n_fb = 0, n_rounds = 0, n_hit = 0, n_slow = 0;
+  int n_it = 0, n_fb = 0, n_rounds = 0, n_hit = 0, n_slow = 0, n_plan = 0;
   // 1. flags; entries, breaks and segment records (4 chunks a lane); the
   //    first kWkStash breaks' operand rows into LDS
   uint32_t f = 0u;
-  for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)ch * nseg + s];
+  for (int s = lane; s < nseg; s += 64) f |= a.cflag[(long long)cx * nseg + s];
   int nb = 0;
   uint32_t cs = 0u, ck = 0u;  // the records of the last chunk so far
 #pragma unroll 1
@@ -769,19 +952,25 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      uint64_t m = __ballot(br[q] && oq[q] < kWkStash);
+      uint64_t m = __ballot(br[q] && oq[q] < (a.plan ? kWkPlan : kWkStash));
 #pragma unroll 1
       while (m) {
         const int l = __builtin_ctzll(m);
         m &= m - 1;
         const int s2 = rdl(oq[q], l);
-        long long x = (long long)(c0 + 4 * l + q) * kFcChunk + 4 * lane;
-        x = x < a.ld ? x : 0;  // (cells past the row stride: read at 0, masked at use)
-        __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p0 + x), (fc_lds_void*)&sRaw[0][s2][0], 16,
-                                         0, 0);
-        if (R.p1)
-          __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p1 + x), (fc_lds_void*)&sRaw[1][s2][0],
+        if (s2 < kWkStash) {
+          long long x = (long long)(c0 + 4 * l + q) * kFcChunk + 4 * lane;
+          x = x < a.ld ? x : 0;  // (cells past the row stride: read at 0, masked at use)
+          __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p0 + x), (fc_lds_void*)&sRaw[0][s2][0],
                                            16, 0, 0);
+          if (R.p1)
+            __builtin_amdgcn_global_load_lds((fc_glb_void*)(R.p1 + x), (fc_lds_void*)&sRaw[1][s2][0],
+                                             16, 0, 0);
+        }
+        if (a.plan && lane < 2)  // (the chunk's crossing plan: 2 x 16 B)
+          __builtin_amdgcn_global_load_lds(
+              (fc_glb_void*)(a.plan + 2 * ((long long)cx * nch + c0 + 4 * l + q) + lane),
+              (fc_lds_void*)&sPlan[s2][0], 16, 0, 0);
       }
     }
     // the lanes' records: the carry into lane 0, the segmented scan, each
@@ -834,13 +1023,60 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
   } else {
     int E = kEMin, k = 0;
     unsigned long long c_step = 0ull, c_fetch = 0ull, c_exact = 0ull, c_zero = 0ull, c0 = 0ull;
-    // chunk j term by term from the state: operands u, v of the lane's 4
-    // cells (from stash slot sl, or sl < 0: loaded from the rows)
-    auto exact_chunk = [&](int j, int sl, f4a u, f4a v) {
+    // operands of chunk j (stash slot sl, or from the rows)
+    auto operands = [&](int j, int sl, f4a* u, f4a* v) {
+      *v = f4a{0.0f, 0.0f, 0.0f, 0.0f};
+      if (sl >= 0) {
+        *u = *reinterpret_cast<const f4a*>(&sRaw[0][sl][4 * lane]);
+        if (R.p1) *v = *reinterpret_cast<const f4a*>(&sRaw[1][sl][4 * lane]);
+      } else {
+        const int x0 = j * kFcChunk + 4 * lane;
+        const int xs = x0 < a.ld ? x0 : 0;  // (masked at use)
+        *u = *reinterpret_cast<const f4a*>(R.p0 + xs);
+        if (R.p1) *v = *reinterpret_cast<const f4a*>(R.p1 + xs);
+      }
+    };
+    // chunk j from the state: by its crossing plan (plan words pw, lane l
+    // holding word l; plan: whether it has one), else term by term from
+    // operands u, v of the lane's 4 cells (stash slot sl; sl < 0: loaded
+    // from the rows here)
+    auto exact_chunk = [&](int j, int sl, f4a u, f4a v, uint32_t pw, bool plan) {
       if (cdf && lane == 0) a.cst[j] = make_int2(E, k);
       ++n_fb;
       n_hit += sl >= 0;
       const int x0 = j * kFcChunk + 4 * lane;
+      const uint32_t w0 = plan ? (uint32_t)rdl((int)pw, 0) : 0u;
+      if (w0 & 1u) {
+        // d_0 in E0, then per crossing the reference's own add and the
+        // increments of the run after it
+        const int nc = (int)((w0 >> 1) & 3u);
+        int Ep = E, kp = k + rdl((int)pw, 1);
+        bool ok = E == (int)((w0 >> 8) & 255u) - 128 && kp <= kK24;
+#pragma unroll
+        for (int sg = 1; sg <= kPlanMax; ++sg) {
+          if (ok && sg <= nc) {
+            const float sv = value_of(Ep, kp) + rdl(__builtin_bit_cast(float, pw), 2 * sg);
+            state_of(__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                                   __builtin_bit_cast(int, sv))),
+                     &Ep, &kp);
+            kp += rdl((int)pw, 2 * sg + 1);
+            ok = Ep == E + (int)((w0 >> (12 + 4 * sg)) & 15u) && kp <= kK24;
+          }
+        }
+        if (ok) {
+          E = Ep;
+          k = kp;
+          normalise(&E, &k);
+          ++n_plan;
+          if (a.stats) {
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+            c_fetch += c1 - c0;
+            c0 = c1;
+          }
+          return;
+        }
+      }
+      if (sl < 0) operands(j, -1, &u, &v);
       float t[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) t[q] = x0 + q < n ? fabsf(R.term(u[q], v[q])) : 0.0f;
@@ -859,19 +1095,6 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
         const unsigned long long c1 = __builtin_amdgcn_s_memtime();
         (j == 0 ? c_zero : c_exact) += c1 - c0;
         c0 = c1;
-      }
-    };
-    // operands of chunk j (stash slot sl, or from the rows)
-    auto operands = [&](int j, int sl, f4a* u, f4a* v) {
-      *v = f4a{0.0f, 0.0f, 0.0f, 0.0f};
-      if (sl >= 0) {
-        *u = *reinterpret_cast<const f4a*>(&sRaw[0][sl][4 * lane]);
-        if (R.p1) *v = *reinterpret_cast<const f4a*>(&sRaw[1][sl][4 * lane]);
-      } else {
-        const int x0 = j * kFcChunk + 4 * lane;
-        const int xs = x0 < a.ld ? x0 : 0;  // (masked at use)
-        *u = *reinterpret_cast<const f4a*>(R.p0 + xs);
-        if (R.p1) *v = *reinterpret_cast<const f4a*>(R.p1 + xs);
       }
     };
     // a mispredicted segment [j, end): walk steps over its entries (256 a
@@ -922,9 +1145,7 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
         // chunk j's entry after all -- the next step does)
         const uint32_t ej = j < end ? sE[j] : kNoEntry;
         if (j < end && L < 64 && !(entry_applies(ej, E) && k + entry_units(ej) <= kK24)) {
-          f4a u, v;
-          operands(j, -1, &u, &v);
-          exact_chunk(j, -1, u, v);
+          exact_chunk(j, -1, f4a{0.0f, 0.0f, 0.0f, 0.0f}, f4a{0.0f, 0.0f, 0.0f, 0.0f}, 0u, false);
           ++j;
         }
       }
@@ -941,8 +1162,11 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
         rK = sKey[rb - 1];
       }
     }
-    f4a nu = {0.0f, 0.0f, 0.0f, 0.0f}, nv = nu;  // (break 0's operands, staged one break ahead)
+    // (break 0's operands and plan words, staged one break ahead)
+    f4a nu = {0.0f, 0.0f, 0.0f, 0.0f}, nv = nu;
     if (nb > 0 && kWkStash > 0) operands(0, 0, &nu, &nv);
+    const int npl = a.plan ? min(nb, kWkPlan) : 0;
+    uint32_t npw = npl > 0 ? sPlan[0][lane & 7] : 0u;
     if (a.stats) c0 = __builtin_amdgcn_s_memtime();
     // 2. the walk: segment i (from break i - 1 to break i), then break i
     int a0 = 0;
@@ -981,10 +1205,12 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
       if (bi >= nb) break;
       normalise(&E, &k);
       const int sl = bi < kWkStash ? bi : -1;
-      f4a u = nu, v = nv;
-      if (sl < 0) operands(b, -1, &u, &v);
-      if (bi + 1 < nb && bi + 1 < kWkStash) operands(0, bi + 1, &nu, &nv);  // (the next break's, ahead)
-      exact_chunk(b, sl, u, v);
+      const f4a u = nu, v = nv;
+      const uint32_t pw = npw;
+      // (the next break's, ahead)
+      if (bi + 1 < nb && bi + 1 < kWkStash) operands(0, bi + 1, &nu, &nv);
+      if (bi + 1 < npl) npw = sPlan[bi + 1][lane & 7];
+      exact_chunk(b, sl, u, v, pw, bi < npl);
       a0 = b + 1;
     }
     // 3. (cdf) every segment chunk's start state
@@ -1001,7 +1227,7 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
     if (a.stats && lane == 0) {  // (s_memtime cycles: segments, fetches, exact rounds, chunk 0)
       atomicAdd(a.stats + 8, nb);
       atomicAdd(a.stats + 9, n_slow);
-      atomicAdd(a.stats + 10, n_fb - nb);
+      atomicAdd(a.stats + 10, n_plan);
       atomicAdd(a.stats + 11, (int)c_step);
       atomicAdd(a.stats + 12, (int)c_fetch);
       atomicAdd(a.stats + 13, (int)c_exact);
@@ -1162,14 +1388,21 @@ __global__ __launch_bounds__(1024) void k_tree_sample(SampleArgs s) {
     atomicAdd(&cnt[act * 16 + o], 1);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int m = 0;
-    for (int act = 0; act < 9; ++act)
-      for (int z = 0; z < 16; ++z)
-        if (cnt[act * 16 + z]) s.klist[m++] = z * 9 + act;
-    *s.kcount = m;
+  // the kept children z * 9 + act in std::set order (act-major, z inner): a
+  // compaction of cnt[act * 16 + z] > 0 over its 144 entries (3 waves)
+  __shared__ int wtot[3];
+  const int i = threadIdx.x, lane = i & 63, wv = i >> 6;
+  const bool kept = i < 144 && cnt[i] > 0;
+  const uint64_t m = __ballot(kept);
+  const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (wv < 3 && lane == 0) wtot[wv] = __popcll(m);
+  __syncthreads();
+  if (i < 144) {
+    const int off = (wv >= 1 ? wtot[0] : 0) + (wv >= 2 ? wtot[1] : 0);
+    if (kept) s.klist[off + pre] = (i & 15) * 9 + (i >> 4);
+    s.counts[i] = cnt[i];
+    if (i == 0) *s.kcount = wtot[0] + wtot[1] + wtot[2];
   }
-  for (int i = threadIdx.x; i < 144; i += blockDim.x) s.counts[i] = cnt[i];
 }
 
 // dst_r[x] = fl(pred_a[x] * L_z[x]) / sums[c_r], c_r = z * 9 + a.
@@ -1227,19 +1460,6 @@ __global__ __launch_bounds__(256) void k_store_kept(const int* __restrict__ klis
 constexpr int kFxThreads = 1024;
 constexpr int kFxStash = 32;  // predicted fallback chunks whose |terms| wave 0 reads from LDS
 constexpr uint32_t kFxZero = 0xfffffffeu;  // entry of a chunk of zero terms: applies in any binade
-
-// inclusive float scan of a wave (any association: approximate running sums)
-__device__ __forceinline__ float wave_incl_scan_f(float v, int lane) {
-  int b = __builtin_bit_cast(int, v);
-#pragma unroll
-  for (int c = 1; c < 16; c <<= 1)
-    b = __builtin_bit_cast(int, __builtin_bit_cast(float, b) +
-                                    __builtin_bit_cast(float, row_shr(b, c)));
-  const float f = __builtin_bit_cast(float, b);
-  const float r0 = rdl(f, 15), r1 = rdl(f, 31), r2 = rdl(f, 47);
-  const int row = lane >> 4;
-  return f + (row >= 1 ? r0 : 0.0f) + (row >= 2 ? r1 : 0.0f) + (row >= 3 ? r2 : 0.0f);
-}
 
 // diagnostics: workgroup thread 0 stamps the 100 MHz clock at phase k
 __device__ __forceinline__ void fx_stamp(const FxArgs& a, int k) {
@@ -1895,6 +2115,7 @@ __global__ __launch_bounds__(256) void k_pbvi_cands(PbviCandArgs c) {
 // nor dispatches a workgroup per inactive group.
 constexpr int kFcGroupBlocks = 16384;  // sums / tables: segments x groups per launch
 constexpr int kFcDriveBlocks = 8192;   // drive: one wave per chain
+constexpr int kFcDevGroups = 64;       // groups dispatched for a device group count (gcount)
 
 // k_fc_walk for chains of at most kWkEntries chunks (PP2_FC_WALK=0, or
 // pp2_debug_fc_walk(0): k_fc_drive everywhere)
@@ -1912,22 +2133,40 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
   constexpr int KC = K > 0 ? K : 1;
   FcArgs a = a0;
   a.ngroups = groups;
+  // crossing plans for single-chain groups only: the 9 chains of a K = 9
+  // group (one row, 9 partners) predict crossings in the same chunks, and a
+  // wave working 9 plans (~1600 cycles each) makes the tables kernel's tail
+  // longer than the walk it shortens (256^2 plan step: +14 / -8 us)
+  if (K > 0) a.plan = nullptr;
   const int nseg = fc_segments(a.n);
-  if (phases & FC_TABLES) {
-    const int gy = std::min(groups, std::max(1, kFcGroupBlocks / nseg));
+  if (g_fc_stats && !a.stats) a.stats = g_fc_stats + 32 * (2 * BASE + (K > 0));
+  if (BASE == FC_KEPT) a.by_id = 1;
+  // a device group list (the kept children: ~40 of 144 on the 256^2 plan
+  // step) -- workgroups for 64 groups, looping over more: dispatching the
+  // 144-group grid's idle workgroups costs the dispatcher several us
+  const int gdisp = a.glist && a.gcount ? std::min(groups, kFcDevGroups) : groups;
+  const int gy = std::min(gdisp, std::max(1, kFcGroupBlocks / nseg));
+  if (phases & (FC_TABLES | FC_SUMS))
     hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+  if (phases & (FC_TABLES | FC_TAB))
     hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
-  }
   if (phases & FC_DRIVE) {
-    if (g_fc_stats && !a.stats) a.stats = g_fc_stats + 32 * (2 * BASE + (K > 0));
-    if (fc_walk_enabled() && fc_chunks(a.n) <= kWkEntries)
-      hipLaunchKernelGGL((k_fc_walk<BASE, K>), dim3(std::min(groups * KC, kFcDriveBlocks)),
-                         dim3(64), 0, st, a);
-    else
-      hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(std::min(groups * KC, kFcDriveBlocks)),
-                         dim3(64), 0, st, a);
-    if (BASE == FC_ROW && K == 0 && a.cdf)
-      hipLaunchKernelGGL(k_fc_cdf, dim3((fc_chunks(a.n) + 3) / 4), dim3(256), 0, st, a);
+    if constexpr (BASE == FC_KEPT) {
+      // the dots of the normalised rows the tables stored: FC_ROW chains
+      FcArgs w = a;
+      w.row = a.kept_rows;
+      w.row_stride = a.ld;
+      return launch_set<FC_ROW, K>(st, groups, w, FC_DRIVE);
+    } else {
+      if (fc_walk_enabled() && fc_chunks(a.n) <= kWkEntries)
+        hipLaunchKernelGGL((k_fc_walk<BASE, K>), dim3(std::min(gdisp * KC, kFcDriveBlocks)),
+                           dim3(64), 0, st, a);
+      else
+        hipLaunchKernelGGL((k_fc_drive<BASE, K>), dim3(std::min(gdisp * KC, kFcDriveBlocks)),
+                           dim3(64), 0, st, a);
+      if (BASE == FC_ROW && K == 0 && a.cdf)
+        hipLaunchKernelGGL(k_fc_cdf, dim3((fc_chunks(a.n) + 3) / 4), dim3(256), 0, st, a);
+    }
   }
   return hipGetLastError();
 }
@@ -1937,9 +2176,19 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
 hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a,
                          int phases) {
   if (groups <= 0) return hipSuccess;
+  const int kc = K > 0 ? K : 1;
   if (a.n <= 0 || a.n > kFcMaxCells || (K != 0 && K != 9) || !a.out || !a.csum || !a.cflag ||
-      !a.tab || groups * (K > 0 ? K : 1) > a.max_chains || fc_chunks(a.n) > a.max_chunks)
+      !a.tab || (base == FC_KEPT || a.by_id ? 144 : groups) * kc > a.max_chains ||
+      fc_chunks(a.n) > a.max_chunks)
     return hipErrorInvalidValue;
+  if (base == FC_KEPT) {
+    if (K != 9 || !a.pred || !a.lrows || a.row || a.cdf || groups > 144 ||
+        (!a.glist && a.g0 + groups > 144))
+      return hipErrorInvalidValue;
+    if ((phases & (FC_TABLES | FC_SUMS)) && !a.mass && !a.msum) return hipErrorInvalidValue;
+    if ((phases & (FC_TABLES | FC_TAB | FC_DRIVE)) && (!a.mass || !a.kept_rows))
+      return hipErrorInvalidValue;
+  }
   if (a.ld < a.n || a.ld % 4 != 0) return hipErrorInvalidValue;
   if (base == FC_CHILD && (!a.pred || !a.lrows || K != 0)) return hipErrorInvalidValue;
   if (base == FC_ROW && !a.row) return hipErrorInvalidValue;
@@ -1954,6 +2203,7 @@ hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcAr
   if (base == FC_ROW) return hipErrorInvalidValue;
   if (base == FC_CHILD) return launch_set<FC_CHILD, 0>(st, groups, a, phases);
   if (base == FC_LIST) return launch_set<FC_LIST, 0>(st, groups, a, phases);
+  if (base == FC_KEPT) return launch_set<FC_KEPT, 9>(st, groups, a, phases);
   return hipErrorInvalidValue;
 }
 
@@ -2048,12 +2298,13 @@ hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount
 }
 
 void FcScratch::release() {
-  for (void* p : {(void*)csum, (void*)cflag, (void*)tab, (void*)cst})
+  for (void* p : {(void*)csum, (void*)cflag, (void*)tab, (void*)cst, (void*)plan})
     if (p) (void)hipFree(p);
   csum = nullptr;
   cflag = nullptr;
   tab = nullptr;
   cst = nullptr;
+  plan = nullptr;
   chains = 0;
   chunks = 0;
 }
@@ -2065,7 +2316,8 @@ bool FcScratch::reserve(int n, int max_chains) {
   if (hipMalloc(&csum, mc * nch * sizeof(float)) != hipSuccess ||
       hipMalloc(&cflag, mc * nseg * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&tab, mc * nch * sizeof(uint2)) != hipSuccess ||
-      hipMalloc(&cst, (nch + 1) * sizeof(int2)) != hipSuccess) {
+      hipMalloc(&cst, (nch + 1) * sizeof(int2)) != hipSuccess ||
+      hipMalloc(&plan, mc * nch * 2 * sizeof(uint4)) != hipSuccess) {
     release();
     return false;
   }
@@ -2075,10 +2327,12 @@ bool FcScratch::reserve(int n, int max_chains) {
 }
 
 void FcScratch::attach(FcArgs* a) const {
+  static const bool plans = !(getenv("PP2_FC_PLAN") && getenv("PP2_FC_PLAN")[0] == '0');
   a->csum = csum;
   a->cflag = cflag;
   a->tab = tab;
   a->cst = cst;
+  a->plan = plans ? plan : nullptr;  // (PP2_FC_PLAN=0: no crossing plans, for A/B runs)
   a->max_chains = chains;
   a->max_chunks = chunks;
 }
@@ -2466,9 +2720,10 @@ extern "C" int pp2_debug_fc_walk(int on) {
 // Diagnostic (tools/prof_planner.py, PP2_FC_STATS=1): the drivers' counters
 // summed per set kind over every launch -- out[16 * (2 * base + (K > 0)) + c],
 // c as pp2_debug_fchain_row2's stats; k_fc_walk's fallback chunks by cause in
-// k_fc_walk's c = 8 (breaks), 9 (mispredicted segments), 10 (their failing
-// chunks), 11 .. 14 (s_memtime cycles in segments, fetches of exact chunks,
-// exact rounds, chunk 0), 15 .. 21 (the longest chain and its counts).
+// k_fc_walk's c = 8 (breaks), 9 (mispredicted segments), 10 (breaks walked
+// by their crossing plans), 11 .. 14 (s_memtime cycles in segments, fetches of exact chunks,
+// exact rounds, chunk 0), 15 .. 21 (the longest chain and its counts), 22 / 23
+// (the tables' crossing plans and their s_memtime cycles).
 // (256 ints)  enable=1 allocates (before the sets to
 // count are launched), out != nullptr copies the 64 counters out and clears them.
 extern "C" int pp2_debug_fc_stats(int* out, int enable) {

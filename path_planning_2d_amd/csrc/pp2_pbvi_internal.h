@@ -123,7 +123,16 @@ hipError_t launch_sum_splits(hipStream_t st, const float* C, int splits, long lo
 //             fl(row[r][x] * partners[i][x]) (evaluatePbviCpu) -- out[r * ldo + i]
 // out[id * ldo + i] = the chain's sum; with cdf (FC_ROW, K = 0, one group)
 // also every running sum, cdf[x] (std::partial_sum).  Scratch: FcScratch.
-enum FcBase { FC_ROW = 0, FC_CHILD = 1, FC_LIST = 2 };
+//   FC_KEPT:  (K = 9) group g's id c < 144 is a child of the expansion: its
+//             normalised belief fl(ftz(pred[c % 9][x] * ftz(L_{c / 9}[x])) / m_c)
+//             (search_tree_cuda.cu:228-229) times partner i: the FIB dots of
+//             the kept children.  Sums phase: m_c approximate (msum: the
+//             children set's chunk sums) over any group list; tables phase:
+//             m_c = mass[c] exact, and each chunk's normalised cells written
+//             to kept_rows[c] (and rowptr[c]); the drive walks kept_rows.
+//             Scratch chains are indexed by c (by_id), so the phases may run
+//             over different group lists.
+enum FcBase { FC_ROW = 0, FC_CHILD = 1, FC_LIST = 2, FC_KEPT = 3 };
 constexpr int kFcMaxCells = 1 << 28;
 constexpr int kFcSegChunks = 4;  // chunks per k_fc_sums / k_fc_tables workgroup (1 per wave)
 inline __host__ __device__ int fc_chunks(int n) { return (n + 255) / 256; }
@@ -149,10 +158,17 @@ struct FcArgs {
   uint32_t* cflag = nullptr;     // [chains][segments] sign flags
   uint2* tab = nullptr;          // [chains][chunks] chunk entries
   int2* cst = nullptr;           // [chunks + 1] chunk start states (cdf)
+  uint4* plan = nullptr;         // [chains][chunks][2] crossing plans of predicted chunks (optional)
   int max_chains = 0, max_chunks = 0;
   int* stats = nullptr;          // diagnostics: driver {iterations, fallbacks, exact rounds, stash hits}
   const int2* plist = nullptr;   // FC_LIST: device (row, partner) pairs, *gcount of them
   int ngroups = 0;               // (set by launch_fchain: the launch's group count)
+  // FC_KEPT
+  const float* mass = nullptr;   // [144] the children's exact masses (tables, drive)
+  const float* msum = nullptr;   // [144][chunks] the children's approximate chunk sums (sums)
+  float* kept_rows = nullptr;    // [144][ld] normalised kept children (written by tables)
+  float* const* rowptr = nullptr;  // optional device [144]: their node rows too
+  int by_id = 0;                 // scratch chain index (id * K + i) instead of (g * K + i)
 };
 // Device scratch of one stream's chain sets (a set may not overlap another
 // set using the same scratch).
@@ -161,6 +177,7 @@ struct FcScratch {
   uint32_t* cflag = nullptr;
   uint2* tab = nullptr;
   int2* cst = nullptr;
+  uint4* plan = nullptr;
   int chains = 0, chunks = 0;
   FcScratch() = default;
   FcScratch(const FcScratch&) = delete;
@@ -173,7 +190,9 @@ struct FcScratch {
 // phases (bit mask): 1 = the chunk sums and tables, 2 = the driver (and the
 // running sums): a caller may enqueue other work between the two, with the
 // same FcArgs and scratch.
-enum : int { FC_TABLES = 1, FC_DRIVE = 2, FC_ALL = 3 };
+// FC_SUMS / FC_TAB split FC_TABLES (FC_KEPT: the sums early, over every
+// child, on another stream)
+enum : int { FC_TABLES = 1, FC_DRIVE = 2, FC_ALL = 3, FC_SUMS = 4, FC_TAB = 8 };
 hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a,
                          int phases = FC_ALL);
 // forwardSampling of the 9 actions from the expanded belief's running sums

@@ -220,6 +220,15 @@ struct pp2_planner {
   int* d_klist = nullptr;       // the kept children z * 9 + a, and their number
   int* d_kcount = nullptr;
   pp2::FcScratch scr_main, scr_side;  // chain-set scratch of the two streams
+  // the kept children's FIB dots (FC_KEPT): their chunk sums on main right
+  // after the samples (beside the children's walk), then their tables and
+  // walk once the masses are in; the rewards' own scratch (the FIB sums read
+  // scr_side's chunk sums)
+  pp2::FcScratch scr_fib, scr_rew;
+  hipStream_t side2 = nullptr;  // (spare)
+  hipEvent_t ev_csum = nullptr, ev_fsum = nullptr;
+  float** h_rowptr = nullptr;   // pinned, mapped: the 144 children's node rows
+  float** d_rowptr = nullptr;
   // reference order, PBVI leaves: every row's candidate alphas (those whose
   // exact chain can reach the row's maximum, from the split-x GEMM's
   // approximate dots and a rigorous bound) as one exact chain set (FC_LIST)
@@ -237,6 +246,7 @@ struct pp2_planner {
   // the time from there to the next expansion's first launch
   bool timing = false;
   double t_enq = 0, t_post = 0, t_between = 0;
+  double t_mark[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (enqueue phases, tmark())
   long long t_n = 0;
   std::chrono::steady_clock::time_point t_last_store{};
   unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
@@ -851,6 +861,13 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   const size_t n = p->n;
   const int ld = p->ref_ld;
   const uint32_t N = p->prm.sample_num;
+  clk::time_point t_prev = t_begin;
+  auto tmark = [&](int i) {  // (PP2_PLAN_TIMING: host time of the enqueue phases)
+    if (!p->timing) return;
+    const clk::time_point t = clk::now();
+    p->t_mark[i] += std::chrono::duration<double, std::micro>(t - t_prev).count();
+    t_prev = t;
+  };
   CHECK(ref_frows(p));
   // the rand() values of the 9 QNode constructors, in the reference's order
   for (uint32_t a = 0; a < 9; ++a)
@@ -863,14 +880,17 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     p->pre.assign(144, -1);
     for (int cc = 0; cc < 144; ++cc) CHECK(acquire_slot(p, &p->pre[cc]));
   }
+  tmark(0);
   HIPCHK(hipEventRecord(p->ev_fork, c->stream));  // brow and the previous stores are in place
   HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
+  tmark(1);
   // The two streams' launches are interleaved phase by phase, so that
   // neither waits for the host to enqueue the other's (a launch costs the
   // host several us): predictions (side), the cdf chain's tables (main), the
   // children's tables (side), the cdf driver and running sums (main), the
   // children's driver (side), the samples (main); the rewards last (side).
   HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred, tree_sparse_t(c)));
+  tmark(2);
   if (p->fx) {
     // main: the expanded belief's running sums and the 9 x N samples (one
     // launch); side: the 144 children's masses, then the 9 rewards (a launch
@@ -972,12 +992,26 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     ch.out = p->d_csum;
     ch.ldo = 1;
     p->scr_side.attach(&ch);
+    // the kept children's FIB dots (evaluateFibCpu) of their normalised rows
+    pp2::FcArgs kd;
+    kd.n = (int)n;
+    kd.ld = ld;
+    kd.pred = p->d_pred;
+    kd.lrows = p->d_lrows;
+    kd.partners = p->d_frows;
+    kd.msum = ch.csum;  // (sums: masses from the children's chunk sums)
+    kd.out = p->d_rout + 9;
+    kd.ldo = 9;
+    p->scr_fib.attach(&kd);
     if (!p->seq) {
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
+      HIPCHK(hipEventRecord(p->ev_csum, p->side));  // (the children's chunk sums)
+      tmark(3);
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
       HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
+      tmark(4);
     }
     {
       pp2::SampleArgs sa;
@@ -997,6 +1031,14 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       sa.cst = cd.cst;
       HIPCHK(pp2::launch_tree_sample(c->stream, sa));
     }
+    if (!p->seq) {
+      // main, beside the children's walk: the kept children's FIB chunk sums
+      // (their masses approximated by the children's chunk sums)
+      HIPCHK(hipStreamWaitEvent(c->stream, p->ev_csum, 0));
+      kd.glist = p->d_klist;
+      kd.gcount = p->d_kcount;
+      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_SUMS));
+    }
     if (!p->seq) {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
       pp2::FcArgs r;
       r.n = (int)n;
@@ -1005,17 +1047,31 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       r.partners = p->d_rrows;
       r.out = p->d_rout;
       r.ldo = 9;
-      p->scr_side.attach(&r);
+      p->scr_rew.attach(&r);
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
     }
+    tmark(5);
     HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
-    // main: the kept children (sampled on this stream), normalised by their
-    // masses (side) into their rows of d_children -- only they become nodes
-    pp2::FcRowTable rt;  // and straight into the rows acquired for them
-    rt.use = 1;
-    for (int cc = 0; cc < 144; ++cc) rt.p[cc] = p->slots[p->pre[cc]].row;
-    HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
-                                  p->d_csum, p->d_children, (int)n, ld, &rt));
+    // the node rows acquired for the 144 children: the kept ones are stored
+    // straight into theirs
+    for (int cc = 0; cc < 144; ++cc) p->h_rowptr[cc] = p->slots[p->pre[cc]].row;
+    if (p->seq) {
+      // main: the kept children (sampled on this stream), normalised by their
+      // masses (side) into their rows of d_children and their node rows
+      pp2::FcRowTable rt;
+      rt.use = 1;
+      for (int cc = 0; cc < 144; ++cc) rt.p[cc] = p->h_rowptr[cc];
+      HIPCHK(pp2::launch_store_kept(c->stream, p->d_klist, p->d_kcount, p->d_pred, p->d_lrows,
+                                    p->d_csum, p->d_children, (int)n, ld, &rt));
+    } else {
+      // main: the kept children's FIB tables -- which store their normalised
+      // rows (d_children, node rows) on the way -- then their walk
+      kd.mass = p->d_csum;
+      kd.kept_rows = p->d_children;
+      kd.rowptr = p->d_rowptr;
+      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_TAB));
+    }
+    tmark(6);
     // side: the kept children's PBVI dots (evaluatePbviCpu, the long chains),
     // beside main's FIB dots, after the rewards already queued there
     if (p->pbvi) {
@@ -1026,24 +1082,14 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     if (p->seq) {  // main: the kept children's FIB dots (evaluateFibCpu), sequential chains
       HIPCHK(pp2::launch_pair_seq_small(c->stream, pp2::PAIR_DOT, p->d_children, 144, p->d_frows, 9,
                                         ld, (int)n, p->d_rout + 9, 9, p->d_klist, p->d_kcount));
-    } else {  // main: the kept children's FIB dots (evaluateFibCpu)
-      pp2::FcArgs a;
-      a.n = (int)n;
-      a.ld = ld;
-      a.row = p->d_children;
-      a.row_stride = ld;
-      a.glist = p->d_klist;
-      a.gcount = p->d_kcount;
-      a.partners = p->d_frows;
-      a.out = p->d_rout + 9;
-      a.ldo = 9;
-      p->scr_main.attach(&a);
-      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 9, 144, a));
+    } else {
+      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_DRIVE));
     }
   }  // (!p->fx)
   HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards, the PBVI dots)
   HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
+  tmark(7);
   const clk::time_point t_enq = p->timing ? clk::now() : clk::time_point{};
   HIPCHK(hipEventSynchronize(p->ev_done));
   const clk::time_point t_ret = p->timing ? clk::now() : clk::time_point{};
@@ -1277,7 +1323,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_kids, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ev_kept, hipEventDisableTiming) != hipSuccess ||
-      hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess)
+      hipEventCreateWithFlags(&p->ev_csum, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_fsum, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(PP2_ENOMEM, "planner scratch allocation failed"));
   p->ref = prm->reference_order == 1;
   {
@@ -1356,7 +1405,10 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
                      reinterpret_cast<float**>(&p->d_counts)) ||
         hipMalloc(&p->d_klist, 144 * sizeof(int)) != hipSuccess ||
         hipMalloc(&p->d_kcount, sizeof(int)) != hipSuccess ||
-        !p->scr_main.reserve((int)p->n, 144 * 9) || !p->scr_side.reserve((int)p->n, 144))
+        !p->scr_main.reserve((int)p->n, 144 * 9) || !p->scr_side.reserve((int)p->n, 144) ||
+        !p->scr_fib.reserve((int)p->n, 144 * 9) || !p->scr_rew.reserve((int)p->n, 9) ||
+        !host_mapped(2 * 144, reinterpret_cast<float**>(&p->h_rowptr),
+                     reinterpret_cast<float**>(&p->d_rowptr)))
       return fail(set_err(PP2_ENOMEM, "planner reference-order scratch allocation failed"));
     std::vector<int> srow(144, 0);
     std::vector<uint8_t> us(144), zs(144);
@@ -1449,6 +1501,12 @@ int pp2_planner_destroy(pp2_planner* p) {
             "after the wait .. children stored %.1f, .. next expansion %.1f; kept children "
             "per expansion %.1f\n", p->t_n, p->t_enq / p->t_n, p->t_post / p->t_n,
             p->t_between / (p->t_n > 1 ? p->t_n - 1 : 1), (double)p->stat_rows / (double)p->t_n);
+  if (p->timing && p->t_n > 0)
+    fprintf(stderr, "pp2 planner: enqueue phases us: rand+slots %.1f, fork %.1f, pred %.1f, tables "
+            "%.1f, drives %.1f, sample+rewards %.1f, store %.1f, dots+join %.1f\n",
+            p->t_mark[0] / p->t_n, p->t_mark[1] / p->t_n, p->t_mark[2] / p->t_n,
+            p->t_mark[3] / p->t_n, p->t_mark[4] / p->t_n, p->t_mark[5] / p->t_n,
+            p->t_mark[6] / p->t_n, p->t_mark[7] / p->t_n);
   if (p->h_pstat) {
     if (p->stat_sets > 0)
       fprintf(stderr, "pp2 planner: PBVI candidate chains %lld over %lld rows in %lld sets "
@@ -1459,6 +1517,7 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (p->h_rout) (void)hipHostFree(p->h_rout);
   if (p->h_r) (void)hipHostFree(p->h_r);
   if (p->h_counts) (void)hipHostFree(p->h_counts);
+  if (p->h_rowptr) (void)hipHostFree(p->h_rowptr);
   for (void* d : {(void*)p->d_cdf, (void*)p->d_sub, (void*)p->d_u1, (void*)p->d_u2, (void*)p->d_klist,
                   (void*)p->d_kcount})
     if (d) (void)hipFree(d);
@@ -1469,11 +1528,12 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (p->h_belief) (void)hipHostFree(p->h_belief);
   if (p->ev_belief) (void)hipEventDestroy(p->ev_belief);
   if (p->ev_done) (void)hipEventDestroy(p->ev_done);
-  for (hipEvent_t e : {p->ev_fork, p->ev_join, p->ev_kids, p->ev_kept})
+  for (hipEvent_t e : {p->ev_fork, p->ev_join, p->ev_kids, p->ev_kept, p->ev_csum, p->ev_fsum})
     if (e) (void)hipEventDestroy(e);
-  if (p->side) {
-    (void)hipStreamSynchronize(p->side);
-    (void)hipStreamDestroy(p->side);
+  for (hipStream_t st : {p->side, p->side2}) {
+    if (!st) continue;
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
   }
   delete p;
   return PP2_OK;

@@ -28,8 +28,49 @@ static float seq_sum(const std::vector<float>& t) {
 static long g_exact_fail = 0;
 
 struct Stats {
-  long chunks = 0, fallback = 0;
+  long chunks = 0, fallback = 0, planned = 0;
 };
+
+static long g_plan_fail = 0;
+
+// k_fc_tables' crossing plan of the terms [x0, x1) from the approximate sum
+// before them (sp), followed from the state (E, k) as k_fc_walk does: true
+// with the state after the chunk when every check passes.
+static bool follow_plan(const std::vector<float>& t, int x0, int x1, float sp, int* pE, int* pk) {
+  const int E0 = domain_of(sp);
+  float a = sp;
+  int prev = E0, nc = 0, D[4] = {E0, 0, 0, 0};
+  float ts[4] = {0, 0, 0, 0}, d[4] = {0, 0, 0, 0};
+  for (int x = x0; x < x1; ++x) {
+    a += fabsf(t[x]);
+    const int Dx = domain_of(a);
+    if (Dx > prev) {  // a crossing term
+      if (++nc > 3) return false;
+      D[nc] = Dx;
+      ts[nc] = fabsf(t[x]);
+    } else {
+      bool tie;
+      d[nc] += units_of(fabsf(t[x]), Dx, &tie);
+      if (tie) return false;
+    }
+    prev = Dx;
+  }
+  if (nc < 1) return false;
+  for (int sg = 0; sg <= nc; ++sg)
+    if (!(d[sg] < (float)kK24) || (sg > 0 && (D[sg] - E0 < 1 || D[sg] - E0 > 15))) return false;
+  if (*pE != E0) return false;
+  int Ep = *pE, kp = *pk + (int)d[0];
+  if (kp > kK24) return false;
+  for (int sg = 1; sg <= nc; ++sg) {
+    const float sv = value_of(Ep, kp) + ts[sg];
+    state_of(sv, &Ep, &kp);
+    kp += (int)d[sg];
+    if (Ep != D[sg] || kp > kK24) return false;
+  }
+  *pE = Ep;
+  *pk = kp;
+  return true;
+}
 
 // The device algorithm, chunk = `chunk` terms.
 static float fchain_sum(const std::vector<float>& t, int chunk, Stats* st) {
@@ -99,6 +140,12 @@ static float fchain_sum(const std::vector<float>& t, int chunk, Stats* st) {
     st->chunks += f;
     j += f;
     if (j < nch && f < 64) {
+      // the chunk's crossing plan (k_fc_tables' chunk_plan, followed as
+      // k_fc_walk does): where its checks pass, its state must be the
+      // term-by-term one below
+      const int x1p = std::min(n, (j + 1) * chunk);
+      int Ep = E, kp = k;
+      const bool planned = follow_plan(t, j * chunk, x1p, P[j], &Ep, &kp);
       // the failing chunk term by term, each increment applied exactly
       // (add_exact: the device's per-element scan) -- and checked against
       // the plain fp32 adds
@@ -111,6 +158,13 @@ static float fchain_sum(const std::vector<float>& t, int chunk, Stats* st) {
         if (bits_of(value_of(E2, k2)) != bits_of(s)) ++g_exact_fail;
       }
       state_of(s, &E, &k);
+      if (planned) {
+        ++st->planned;
+        normalise(&Ep, &kp);
+        int En = E, kn = k;
+        normalise(&En, &kn);
+        if (Ep != En || kp != kn) ++g_plan_fail;
+      }
       ++st->chunks;
       ++st->fallback;
       ++j;
@@ -242,8 +296,9 @@ int main(int argc, char** argv) {
     check("belief", b, 256, &st);
     check("belief dot", d, 256, &st);
   }
-  printf("fchain_check: %d mismatches; %ld chunks, %ld term-by-term (%.2f %%); "
-         "%ld add_exact mismatches\n", fails, st.chunks, st.fallback,
-         st.chunks ? 100.0 * st.fallback / st.chunks : 0.0, g_exact_fail);
-  return fails || g_exact_fail ? 1 : 0;
+  printf("fchain_check: %d mismatches; %ld chunks, %ld term-by-term (%.2f %%), %ld of them "
+         "planned; %ld add_exact mismatches, %ld plan mismatches\n", fails, st.chunks,
+         st.fallback, st.chunks ? 100.0 * st.fallback / st.chunks : 0.0, st.planned, g_exact_fail,
+         g_plan_fail);
+  return fails || g_exact_fail || g_plan_fail ? 1 : 0;
 }

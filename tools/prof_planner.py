@@ -72,7 +72,8 @@ def main():
                       f"{c[11] / c[7]:.0f}, fetches {c[12] / c[7]:.0f}, exact {c[13] / c[7]:.0f}, "
                       f"chunk 0 {c[14] / c[7]:.0f}; longest chain {c[15] / 100:.2f} us (exact chunks {c[16]}, "
                       f"rounds {c[17]}, slow steps {c[18]}, stash hits {c[19]}, chunks {c[20]}, "
-                      f"group {c[21]})", flush=True)
+                      f"group {c[21]}); tables: {c[22] / c[7]:.1f} plans per chain, "
+                      f"{c[23] / max(c[22], 1):.0f} cycles each", flush=True)
     ctx.close()
     print(f"case {case} lb {lb} reference_order={ref}: {steps} plan steps: p50 "
           f"{np.percentile(ms, 50):.3f} ms, mean {ms.mean():.3f} ms, wall {el * 1e3:.1f} ms, "
