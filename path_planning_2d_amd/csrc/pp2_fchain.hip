@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <utility>
 
 #define PP2_FC_HD __host__ __device__
@@ -441,6 +442,66 @@ __device__ __forceinline__ void chunk_plan(const float (&tt)[4], float sp, int E
 }
 
 // ---------------------------------------------------------------- pass 2
+// One chunk's table entries (and crossing plans, and FC_KEPT's normalised
+// cells) from its base values v and the approximate running sums before it,
+// sP[i] of chain i: k_fc_tables' and k_fc_sumtab's common part.
+template <int BASE, int K>
+__device__ __forceinline__ void chunk_entries(const FcArgs& a, const Terms<BASE, K>& T,
+                                              const float (&v)[4], int x0, int j, int gc, int id,
+                                              const float* sP, int sPstride, int lane, int nch) {
+  constexpr int KC = K > 0 ? K : 1;
+  if (BASE == FC_KEPT && a.kept_rows) {
+    // the kept child's normalised cells (k_store_kept's job): its dense row
+    // for the drive, and its node row
+    float* kr = a.kept_rows + (long long)id * a.ld;
+    float* nr = a.rowptr ? a.rowptr[id] : nullptr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (x0 + q < a.n) {
+        kr[x0 + q] = v[q];
+        if (nr) nr[x0 + q] = v[q];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < KC; ++i) {
+    const float sp = sP[i * sPstride];
+    const int E = domain_of(sp);
+    float d = 0.0f, tt[4];
+    bool tie = false;
+    uint32_t mx = 0u;
+    T.terms_of(v, i, x0, tt);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bool tx;
+      d += units_of(fabsf(tt[q]), E, &tx);
+      tie = tie || tx;
+      mx = max(mx, bits_of(tt[q]) & 0x7fffffffu);
+    }
+    const float ds = wave_sum(d);  // exact below 2^24; else no entry
+    const bool anytie = __ballot(tie) != 0ull;
+    // a chunk adding nothing is tabled for the lowest domain where it adds
+    // nothing (entry_applies: every domain above too)
+    int Ez = E;
+    if (ds == 0.0f) Ez = zero_domain(wave_max_bits(mx));  // (uniform)
+    const uint32_t e = make_entry(min(E, Ez), ds, anytie);
+    // predicted fallback: no entry, or the chunk's sum likely crosses
+    // into the next binade (from the approximate running sum)
+    // (a chunk adding nothing crosses nothing)
+    const bool pred = e == kNoEntry ||
+                      (ds > 0.0f && ldexpf(sp, 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f));
+    if (lane == 0) a.tab[(long long)(gc * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
+    if (pred && a.plan) {
+      const unsigned long long p0 = a.stats ? __builtin_amdgcn_s_memtime() : 0ull;
+      chunk_plan(tt, sp, E, lane, a.plan + 2 * ((long long)(gc * KC + i) * nch + j));
+      if (a.stats && lane == 0) {  // (plans: count, s_memtime cycles)
+        atomicAdd(a.stats + 22, 1);
+        atomicAdd(a.stats + 23, (int)(__builtin_amdgcn_s_memtime() - p0));
+      }
+    }
+  }
+}
+
 template <int BASE, int K>
 __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
   constexpr int KC = K > 0 ? K : 1;
@@ -482,57 +543,110 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
     const int x0 = j * kFcChunk + 4 * lane;
     float v[4];
     T.terms4(-1, x0, v);
-    if (BASE == FC_KEPT && a.kept_rows) {
-      // the kept child's normalised cells (k_store_kept's job): its dense row
-      // for the drive, and its node row
-      float* kr = a.kept_rows + (long long)id * a.ld;
-      float* nr = a.rowptr ? a.rowptr[id] : nullptr;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (x0 + q < a.n) {
-          kr[x0 + q] = v[q];
-          if (nr) nr[x0 + q] = v[q];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      const int E = domain_of(sP[i][jl]);
-      float d = 0.0f, tt[4];
-      bool tie = false;
-      uint32_t mx = 0u;
-      T.terms_of(v, i, x0, tt);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bool tx;
-        d += units_of(fabsf(tt[q]), E, &tx);
-        tie = tie || tx;
-        mx = max(mx, bits_of(tt[q]) & 0x7fffffffu);
-      }
-      const float ds = wave_sum(d);  // exact below 2^24; else no entry
-      const bool anytie = __ballot(tie) != 0ull;
-      // a chunk adding nothing is tabled for the lowest domain where it adds
-      // nothing (entry_applies: every domain above too)
-      int Ez = E;
-      if (ds == 0.0f) Ez = zero_domain(wave_max_bits(mx));  // (uniform)
-      const uint32_t e = make_entry(min(E, Ez), ds, anytie);
-      // predicted fallback: no entry, or the chunk's sum likely crosses
-      // into the next binade (from the approximate running sum)
-      // (a chunk adding nothing crosses nothing)
-      const bool pred = e == kNoEntry ||
-                        (ds > 0.0f && ldexpf(sP[i][jl], 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f));
-      if (lane == 0) a.tab[(long long)(gc * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
-      if (pred && a.plan) {
-        const unsigned long long p0 = a.stats ? __builtin_amdgcn_s_memtime() : 0ull;
-        chunk_plan(tt, sP[i][jl], E, lane, a.plan + 2 * ((long long)(gc * KC + i) * nch + j));
-        if (a.stats && lane == 0) {  // (plans: count, s_memtime cycles)
-          atomicAdd(a.stats + 22, 1);
-          atomicAdd(a.stats + 23, (int)(__builtin_amdgcn_s_memtime() - p0));
-        }
-      }
-    }
+    chunk_entries<BASE, K>(a, T, v, x0, j, gc, id, &sP[0][jl], kFcSegChunks, lane, nch);
   }
   __syncthreads();  // (sPart / sP of the next group)
+  }
+}
+
+// ---------------------------------------------------------------- sums + tables
+// k_fc_sums and k_fc_tables as one launch: each workgroup (segment seg of
+// group g, a chunk per wave) forms its chunk sums, publishes their total --
+// one 64-bit agent-scope store of (launch tag, float bits) per chain and
+// segment -- and takes the approximate running sum before its segment from
+// the totals its predecessors publish (lanes poll one each), then tables its
+// chunks.  Dependencies point to lower segments of the same group only, and
+// workgroups dispatch in increasing order, so the earliest unfinished
+// workgroup can always proceed.  Saves the second launch, its dependency
+// wait, the terms' second pass and k_fc_tables' O(segments) prefix loads.
+template <int BASE, int K>
+__global__ __launch_bounds__(256) void k_fc_sumtab(FcArgs a) {
+  constexpr int KC = K > 0 ? K : 1;
+  __shared__ uint32_t sFlags[KC];
+  __shared__ float sCS[KC][kFcSegChunks];
+  __shared__ float sPre[KC];
+  __shared__ float sP[KC][kFcSegChunks];
+  const int seg = blockIdx.x;
+  for (int g = blockIdx.y;; g += gridDim.y) {  // (block-uniform)
+  int id;
+  if (!group_id(a, g, &id)) return;
+  Terms<BASE, K> T;
+  T.init(a, id);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nch = fc_chunks(a.n), nseg = fc_segments(a.n);
+  const int gc = a.by_id ? id : g;  // (the scratch chains' index)
+  if (BASE == FC_KEPT) T.m = kept_mass(a, id, nch, lane);
+  if (threadIdx.x < KC) sFlags[threadIdx.x] = 0u;
+  __syncthreads();
+  // 1. the chunk sums (k_fc_sums)
+  const int j = seg * kFcSegChunks + w;
+  const int x0 = j * kFcChunk + 4 * lane;
+  float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t fl[KC];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) fl[i] = 0u;
+  if (j < nch) T.terms4(-1, x0, v);
+#pragma unroll
+  for (int i = 0; i < KC; ++i) {
+    float acc = 0.0f, tt[4];
+    T.terms_of(v, i, x0, tt);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float t = tt[q];
+      acc += fabsf(t);
+      fl[i] |= !isfinite(t) ? kBad : t > 0.0f ? kPos : t < 0.0f ? kNeg : 0u;
+    }
+    const float sum = wave_sum(acc);  // (0 past the chunks)
+    if (lane == 0) {
+      sCS[i][w] = sum;
+      if (j < nch) a.csum[(long long)(gc * KC + i) * nch + j] = sum;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < KC; ++i) {
+    const uint32_t f = (__ballot((fl[i] & kPos) != 0u) ? kPos : 0u) |
+                       (__ballot((fl[i] & kNeg) != 0u) ? kNeg : 0u) |
+                       (__ballot((fl[i] & kBad) != 0u) ? kBad : 0u);
+    if (lane == 0 && f) atomicOr(&sFlags[i], f);
+  }
+  __syncthreads();
+  // 2. publish the segment's totals; the running sum before the segment
+  if (threadIdx.x < KC) {
+    const int i = threadIdx.x;
+    a.cflag[(long long)(gc * KC + i) * nseg + seg] = sFlags[i];
+    const float tot = (sCS[i][0] + sCS[i][1]) + (sCS[i][2] + sCS[i][3]);
+    __hip_atomic_store(a.agg + (long long)(gc * KC + i) * nseg + seg,
+                       ((unsigned long long)a.epoch << 32) | bits_of(tot), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int i = w; i < KC; i += 4) {  // (wave w: chains w, w + 4, ...)
+    const unsigned long long* ag = a.agg + (long long)(gc * KC + i) * nseg;
+    float pv = 0.0f;
+    for (int s2 = lane; s2 < seg; s2 += 64) {
+      unsigned long long x;
+      for (;;) {
+        x = __hip_atomic_load(ag + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(x >> 32) == a.epoch) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      pv += __builtin_bit_cast(float, (uint32_t)x);
+    }
+    const float pre = wave_sum(pv);
+    if (lane == 0) sPre[i] = pre;
+  }
+  __syncthreads();
+  if (threadIdx.x < KC) {
+    const int i = threadIdx.x;
+    float run = sPre[i];
+    for (int c = 0; c < kFcSegChunks; ++c) {
+      sP[i][c] = run;
+      run += sCS[i][c];
+    }
+  }
+  __syncthreads();
+  // 3. the entries (k_fc_tables)
+  if (j < nch) chunk_entries<BASE, K>(a, T, v, x0, j, gc, id, &sP[0][w], kFcSegChunks, lane, nch);
+  __syncthreads();  // (LDS of the next group)
   }
 }
 
@@ -2120,6 +2234,16 @@ constexpr int kFcDevGroups = 64;       // groups dispatched for a device group c
 // k_fc_walk for chains of at most kWkEntries chunks (PP2_FC_WALK=0, or
 // pp2_debug_fc_walk(0): k_fc_drive everywhere)
 int g_fc_walk = -1;
+// k_fc_sumtab for sums + tables (PP2_FC_SUMTAB=0: the two launches); its
+// launch tags, unique over the process (stale totals never match)
+int g_fc_sumtab = -1;
+bool fc_sumtab_enabled() {
+  if (g_fc_sumtab < 0)
+    g_fc_sumtab = !(getenv("PP2_FC_SUMTAB") && getenv("PP2_FC_SUMTAB")[0] == '0');
+  return g_fc_sumtab != 0;
+}
+std::atomic<unsigned> g_epoch{0};
+unsigned next_epoch() { return ++g_epoch; }
 // pp2_debug_fc_stats: driver counters per set kind (8 ints each, summed over
 // launches; nullptr: off)
 int* g_fc_stats = nullptr;
@@ -2146,10 +2270,14 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
   // 144-group grid's idle workgroups costs the dispatcher several us
   const int gdisp = a.glist && a.gcount ? std::min(groups, kFcDevGroups) : groups;
   const int gy = std::min(gdisp, std::max(1, kFcGroupBlocks / nseg));
-  if (phases & (FC_TABLES | FC_SUMS))
-    hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
-  if (phases & (FC_TABLES | FC_TAB))
-    hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+  const bool sums = phases & (FC_TABLES | FC_SUMS), tabs = phases & (FC_TABLES | FC_TAB);
+  if (sums && tabs && a.agg && fc_sumtab_enabled()) {
+    a.epoch = next_epoch();
+    hipLaunchKernelGGL((k_fc_sumtab<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+  } else {
+    if (sums) hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+    if (tabs) hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+  }
   if (phases & FC_DRIVE) {
     if constexpr (BASE == FC_KEPT) {
       // the dots of the normalised rows the tables stored: FC_ROW chains
@@ -2172,6 +2300,8 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
 }
 
 }  // namespace
+
+bool fc_sumtab_active() { return fc_sumtab_enabled(); }
 
 hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a,
                          int phases) {
@@ -2298,8 +2428,9 @@ hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount
 }
 
 void FcScratch::release() {
-  for (void* p : {(void*)csum, (void*)cflag, (void*)tab, (void*)cst, (void*)plan})
+  for (void* p : {(void*)csum, (void*)cflag, (void*)tab, (void*)cst, (void*)plan, (void*)agg})
     if (p) (void)hipFree(p);
+  agg = nullptr;
   csum = nullptr;
   cflag = nullptr;
   tab = nullptr;
@@ -2317,7 +2448,9 @@ bool FcScratch::reserve(int n, int max_chains) {
       hipMalloc(&cflag, mc * nseg * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&tab, mc * nch * sizeof(uint2)) != hipSuccess ||
       hipMalloc(&cst, (nch + 1) * sizeof(int2)) != hipSuccess ||
-      hipMalloc(&plan, mc * nch * 2 * sizeof(uint4)) != hipSuccess) {
+      hipMalloc(&plan, mc * nch * 2 * sizeof(uint4)) != hipSuccess ||
+      hipMalloc(&agg, mc * nseg * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(agg, 0, mc * nseg * sizeof(unsigned long long)) != hipSuccess) {
     release();
     return false;
   }
@@ -2333,6 +2466,7 @@ void FcScratch::attach(FcArgs* a) const {
   a->tab = tab;
   a->cst = cst;
   a->plan = plans ? plan : nullptr;  // (PP2_FC_PLAN=0: no crossing plans, for A/B runs)
+  a->agg = agg;
   a->max_chains = chains;
   a->max_chunks = chunks;
 }
@@ -2738,4 +2872,12 @@ extern "C" int pp2_debug_fc_stats(int* out, int enable) {
     if (hipMemset(pp2::g_fc_stats, 0, 256 * sizeof(int)) != hipSuccess) return 1;
   }
   return 0;
+}
+
+// Diagnostic (tests): sums + tables as one launch (1, the default) or two (0).
+// Returns the previous choice.
+extern "C" int pp2_debug_fc_sumtab(int on) {
+  const int prev = pp2::fc_sumtab_enabled() ? 1 : 0;
+  pp2::g_fc_sumtab = on ? 1 : 0;
+  return prev;
 }

@@ -159,6 +159,8 @@ struct FcArgs {
   uint2* tab = nullptr;          // [chains][chunks] chunk entries
   int2* cst = nullptr;           // [chunks + 1] chunk start states (cdf)
   uint4* plan = nullptr;         // [chains][chunks][2] crossing plans of predicted chunks (optional)
+  unsigned long long* agg = nullptr;  // [chains][segments] k_fc_sumtab's published segment sums
+  unsigned epoch = 0;            // (set by launch_fchain: the tag of this launch's agg entries)
   int max_chains = 0, max_chunks = 0;
   int* stats = nullptr;          // diagnostics: driver {iterations, fallbacks, exact rounds, stash hits}
   const int2* plist = nullptr;   // FC_LIST: device (row, partner) pairs, *gcount of them
@@ -178,6 +180,7 @@ struct FcScratch {
   uint2* tab = nullptr;
   int2* cst = nullptr;
   uint4* plan = nullptr;
+  unsigned long long* agg = nullptr;
   int chains = 0, chunks = 0;
   FcScratch() = default;
   FcScratch(const FcScratch&) = delete;
@@ -195,6 +198,8 @@ struct FcScratch {
 enum : int { FC_TABLES = 1, FC_DRIVE = 2, FC_ALL = 3, FC_SUMS = 4, FC_TAB = 8 };
 hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcArgs& a,
                          int phases = FC_ALL);
+// whether sums + tables run as one launch (k_fc_sumtab; PP2_FC_SUMTAB)
+bool fc_sumtab_active();
 // forwardSampling of the 9 actions from the expanded belief's running sums
 // cdf[n]: r[9 * N] the host's rand() values (action-major), u1 / u2 [N] the
 // curand uniforms; counts[a * 16 + z] and the kept children z * 9 + a.

@@ -245,6 +245,7 @@ struct pp2_planner {
   // the wait), the tree work after the wait .. store_children enqueued, and
   // the time from there to the next expansion's first launch
   bool timing = false;
+  bool spin = true;             // wait_event: poll (PP2_SPIN_WAIT)
   double t_enq = 0, t_post = 0, t_between = 0;
   double t_mark[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (enqueue phases, tmark())
   long long t_n = 0;
@@ -837,6 +838,17 @@ void fx_stamps_print(pp2_planner* p) {
   }
 }
 
+// The host's wait for an expansion: a poll of the event (PP2_SPIN_WAIT=1,
+// the default) -- the blocking wait's wake-up is a scheduler round trip on
+// the plan step's critical path -- or hipEventSynchronize (0).
+hipError_t wait_event(pp2_planner* p, hipEvent_t ev) {
+  if (!p->spin) return hipEventSynchronize(ev);
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+  }
+}
+
 // VNode::expand in reference order.  Every grid-wide sum of the reference's
 // 9 QNode constructors (search_tree_cuda.cu:161-242) is formed on the device
 // with the bits of its x-ordered fp32 host chain (pp2_fchain.hip), and the
@@ -1031,12 +1043,13 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       sa.cst = cd.cst;
       HIPCHK(pp2::launch_tree_sample(c->stream, sa));
     }
-    if (!p->seq) {
+    const bool sumtab = pp2::fc_sumtab_active();
+    kd.glist = p->d_klist;
+    kd.gcount = p->d_kcount;
+    if (!p->seq && !sumtab) {
       // main, beside the children's walk: the kept children's FIB chunk sums
       // (their masses approximated by the children's chunk sums)
       HIPCHK(hipStreamWaitEvent(c->stream, p->ev_csum, 0));
-      kd.glist = p->d_klist;
-      kd.gcount = p->d_kcount;
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_SUMS));
     }
     if (!p->seq) {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
@@ -1066,10 +1079,12 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     } else {
       // main: the kept children's FIB tables -- which store their normalised
       // rows (d_children, node rows) on the way -- then their walk
+      // (with k_fc_sumtab: the sums too, in the same launch, exact masses)
       kd.mass = p->d_csum;
       kd.kept_rows = p->d_children;
       kd.rowptr = p->d_rowptr;
-      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_TAB));
+      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd,
+                                sumtab ? pp2::FC_TABLES : pp2::FC_TAB));
     }
     tmark(6);
     // side: the kept children's PBVI dots (evaluatePbviCpu, the long chains),
@@ -1091,7 +1106,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
   tmark(7);
   const clk::time_point t_enq = p->timing ? clk::now() : clk::time_point{};
-  HIPCHK(hipEventSynchronize(p->ev_done));
+  HIPCHK(wait_event(p, p->ev_done));
   const clk::time_point t_ret = p->timing ? clk::now() : clk::time_point{};
   if (p->h_pstat) p->stat_cands += *p->h_pstat;
   if (p->d_stamps) fx_stamps_collect(p);
@@ -1465,6 +1480,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
   {
     const char* tm = getenv("PP2_PLAN_TIMING");
     p->timing = tm && tm[0] == '1';
+    const char* sw = getenv("PP2_SPIN_WAIT");
+    p->spin = !(sw && sw[0] == '0');
   }
   *out = p;
   return PP2_OK;

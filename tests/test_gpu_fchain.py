@@ -103,17 +103,21 @@ def test_numpy_accumulate_is_the_sequential_chain(oracle):
     assert bits(seq(t)[0]) == bits(lib.orc_sum_seq(t.size, _ptr(t)))
 
 
-@pytest.fixture(params=[1, 0], ids=["walk", "drive"])
+@pytest.fixture(params=[1, 0], ids=["walk+sumtab", "drive+two-launch"])
 def driver(request):
-    """The chain sets' third pass: k_fc_walk (round 6, the default where a
-    chain has <= 1024 chunks) or k_fc_drive (every size)."""
+    """The chain sets' passes: k_fc_sumtab (sums and tables as one launch,
+    round 6, the default) with k_fc_walk (the default where a chain has <=
+    1024 chunks), or k_fc_sums + k_fc_tables with k_fc_drive (every size)."""
     from path_planning_2d_amd import _lib
-    f = _lib.load().pp2_debug_fc_walk
-    f.argtypes = [C.c_int]
-    f.restype = C.c_int
-    prev = f(request.param)
+    lib = _lib.load()
+    f, g = lib.pp2_debug_fc_walk, lib.pp2_debug_fc_sumtab
+    for h in (f, g):
+        h.argtypes = [C.c_int]
+        h.restype = C.c_int
+    prev, prev2 = f(request.param), g(request.param)
     yield request.param
     f(prev)
+    g(prev2)
 
 
 def test_fchain_sums_and_running_sums_bit_exact(driver):

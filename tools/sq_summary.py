@@ -11,7 +11,8 @@ the 8 XCDs, so GRBM_GUI_ACTIVE / 8 is the dispatch's wall clock in cycles.
     lds_busy  = SQ_LDS_IDX_ACTIVE / (CUs * wall)
 Usage: python tools/sq_summary.py <round dir, e.g. r03> <steps per launch>
        [kernel substring, default k_loop_resident] [pmc dir under gpurun_out]
-       [output name, default resident_sq.json]
+       [output name, default resident_sq.json] [driver, as collect_lds_pmc.sh's
+       DRIVER, default "tools/coded_loop_timing.py at 1024^2"]
 """
 import csv
 import json
@@ -49,7 +50,8 @@ def main():
         "kernel": kernel,
         "steps_per_launch": steps,
         "source": "tools/collect_lds_pmc.sh (rocprofv3 --pmc, two passes) of "
-                  "tools/coded_loop_timing.py at 1024^2; the longest dispatch",
+                  + (sys.argv[6] if len(sys.argv) > 6 else "tools/coded_loop_timing.py at 1024^2")
+                  + "; the longest dispatch",
         "counters": c,
         "wall_cycles_per_step": wall / steps,
         "valu_busy": 4.0 * c["SQ_ACTIVE_INST_VALU"] / (4 * CUS * wall),
