@@ -2234,12 +2234,15 @@ constexpr int kFcDevGroups = 64;       // groups dispatched for a device group c
 // k_fc_walk for chains of at most kWkEntries chunks (PP2_FC_WALK=0, or
 // pp2_debug_fc_walk(0): k_fc_drive everywhere)
 int g_fc_walk = -1;
-// k_fc_sumtab for sums + tables (PP2_FC_SUMTAB=0: the two launches); its
-// launch tags, unique over the process (stale totals never match)
+// k_fc_sumtab for sums + tables (opt-in, PP2_FC_SUMTAB=1: on the 256^2
+// plan step the children's set took 41 us in it against 11 + 19 in the two
+// launches -- workgroups spinning on their predecessors' totals hold slots
+// the later segments' need); its launch tags, unique over the process
+// (stale totals never match)
 int g_fc_sumtab = -1;
 bool fc_sumtab_enabled() {
   if (g_fc_sumtab < 0)
-    g_fc_sumtab = !(getenv("PP2_FC_SUMTAB") && getenv("PP2_FC_SUMTAB")[0] == '0');
+    g_fc_sumtab = getenv("PP2_FC_SUMTAB") && getenv("PP2_FC_SUMTAB")[0] == '1';
   return g_fc_sumtab != 0;
 }
 std::atomic<unsigned> g_epoch{0};
@@ -2874,7 +2877,7 @@ extern "C" int pp2_debug_fc_stats(int* out, int enable) {
   return 0;
 }
 
-// Diagnostic (tests): sums + tables as one launch (1, the default) or two (0).
+// Diagnostic (tests): sums + tables as one launch (1) or two (0, the default).
 // Returns the previous choice.
 extern "C" int pp2_debug_fc_sumtab(int on) {
   const int prev = pp2::fc_sumtab_enabled() ? 1 : 0;

@@ -106,8 +106,9 @@ def test_numpy_accumulate_is_the_sequential_chain(oracle):
 @pytest.fixture(params=[1, 0], ids=["walk+sumtab", "drive+two-launch"])
 def driver(request):
     """The chain sets' passes: k_fc_sumtab (sums and tables as one launch,
-    round 6, the default) with k_fc_walk (the default where a chain has <=
-    1024 chunks), or k_fc_sums + k_fc_tables with k_fc_drive (every size)."""
+    round 6, opt-in) with k_fc_walk (the default where a chain has <= 1024
+    chunks), or k_fc_sums + k_fc_tables (the default) with k_fc_drive (every
+    size)."""
     from path_planning_2d_amd import _lib
     lib = _lib.load()
     f, g = lib.pp2_debug_fc_walk, lib.pp2_debug_fc_sumtab
