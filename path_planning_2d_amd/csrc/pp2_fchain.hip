@@ -445,59 +445,150 @@ __device__ __forceinline__ void chunk_plan(const float (&tt)[4], float sp, int E
 // One chunk's table entries (and crossing plans, and FC_KEPT's normalised
 // cells) from its base values v and the approximate running sums before it,
 // sP[i] of chain i: k_fc_tables' and k_fc_sumtab's common part.
+// One chain's entry (and crossing plan) of chunk j: its terms tt and the
+// approximate running sum sp before the chunk; chain = the scratch chain.
+__device__ __forceinline__ void chain_chunk_entry(const FcArgs& a, const float (&tt)[4], float sp,
+                                                  int j, long long chain, int lane, int nch) {
+  const int E = domain_of(sp);
+  float d = 0.0f;
+  bool tie = false;
+  uint32_t mx = 0u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    bool tx;
+    d += units_of(fabsf(tt[q]), E, &tx);
+    tie = tie || tx;
+    mx = max(mx, bits_of(tt[q]) & 0x7fffffffu);
+  }
+  const float ds = wave_sum(d);  // exact below 2^24; else no entry
+  const bool anytie = __ballot(tie) != 0ull;
+  // a chunk adding nothing is tabled for the lowest domain where it adds
+  // nothing (entry_applies: every domain above too)
+  int Ez = E;
+  if (ds == 0.0f) Ez = zero_domain(wave_max_bits(mx));  // (uniform)
+  const uint32_t e = make_entry(min(E, Ez), ds, anytie);
+  // predicted fallback: no entry, or the chunk's sum likely crosses
+  // into the next binade (from the approximate running sum)
+  // (a chunk adding nothing crosses nothing)
+  const bool pred = e == kNoEntry ||
+                    (ds > 0.0f && ldexpf(sp, 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f));
+  if (lane == 0) a.tab[chain * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
+  if (pred && a.plan) {
+    const unsigned long long p0 = a.stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    chunk_plan(tt, sp, E, lane, a.plan + 2 * (chain * nch + j));
+    if (a.stats && lane == 0) {  // (plans: count, s_memtime cycles)
+      atomicAdd(a.stats + 22, 1);
+      atomicAdd(a.stats + 23, (int)(__builtin_amdgcn_s_memtime() - p0));
+    }
+  }
+}
+
+// FC_KEPT: the kept child's normalised cells of a chunk (k_store_kept's
+// job): its dense row for the drive, and its node row
+__device__ __forceinline__ void store_kept_cells(const FcArgs& a, const float (&v)[4], int x0, int id) {
+  float* kr = a.kept_rows + (long long)id * a.ld;
+  float* nr = a.rowptr ? a.rowptr[id] : nullptr;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (x0 + q < a.n) {
+      kr[x0 + q] = v[q];
+      if (nr) nr[x0 + q] = v[q];
+    }
+  }
+}
+
+// One chunk's table entries (and crossing plans, and FC_KEPT's normalised
+// cells) from its base values v and the approximate running sums before it,
+// sP[i] of chain i: k_fc_tables' and k_fc_sumtab's common part.
 template <int BASE, int K>
 __device__ __forceinline__ void chunk_entries(const FcArgs& a, const Terms<BASE, K>& T,
                                               const float (&v)[4], int x0, int j, int gc, int id,
                                               const float* sP, int sPstride, int lane, int nch) {
   constexpr int KC = K > 0 ? K : 1;
-  if (BASE == FC_KEPT && a.kept_rows) {
-    // the kept child's normalised cells (k_store_kept's job): its dense row
-    // for the drive, and its node row
-    float* kr = a.kept_rows + (long long)id * a.ld;
-    float* nr = a.rowptr ? a.rowptr[id] : nullptr;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (x0 + q < a.n) {
-        kr[x0 + q] = v[q];
-        if (nr) nr[x0 + q] = v[q];
-      }
-    }
-  }
+  if (BASE == FC_KEPT && a.kept_rows) store_kept_cells(a, v, x0, id);
 #pragma unroll
   for (int i = 0; i < KC; ++i) {
-    const float sp = sP[i * sPstride];
-    const int E = domain_of(sp);
-    float d = 0.0f, tt[4];
-    bool tie = false;
-    uint32_t mx = 0u;
+    float tt[4];
     T.terms_of(v, i, x0, tt);
+    chain_chunk_entry(a, tt, sP[i * sPstride], j, (long long)gc * KC + i, lane, nch);
+  }
+}
+
+// ---------------------------------------------------------------- K = 9: a wave per chain
+// The sums and tables of K = 9 sets with a wave per chain (576-thread
+// workgroups: 9 waves over the segment's 4 chunks): a wave's dependent
+// sequence is 4 chunks of one chain, not 9 chains of one chunk -- the
+// tables of a one-group set are latency, not throughput (12 us for the 9
+// rewards), and a chunk's 9 crossing plans spread over 9 waves.
+template <int BASE>
+__global__ __launch_bounds__(576) void k_fc_sums9(FcArgs a) {
+  const int seg = blockIdx.x;
+  const int lane = threadIdx.x & 63, i = threadIdx.x >> 6;
+  for (int g = blockIdx.y;; g += gridDim.y) {  // (block-uniform)
+    int id;
+    if (!group_id(a, g, &id)) return;
+    Terms<BASE, 9> T;
+    T.init(a, id);
+    const int nch = fc_chunks(a.n), nseg = fc_segments(a.n);
+    const int gc = a.by_id ? id : g;
+    if (BASE == FC_KEPT) T.m = kept_mass(a, id, nch, lane);
+    const long long chain = (long long)gc * 9 + i;
+    uint32_t fl = 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      bool tx;
-      d += units_of(fabsf(tt[q]), E, &tx);
-      tie = tie || tx;
-      mx = max(mx, bits_of(tt[q]) & 0x7fffffffu);
-    }
-    const float ds = wave_sum(d);  // exact below 2^24; else no entry
-    const bool anytie = __ballot(tie) != 0ull;
-    // a chunk adding nothing is tabled for the lowest domain where it adds
-    // nothing (entry_applies: every domain above too)
-    int Ez = E;
-    if (ds == 0.0f) Ez = zero_domain(wave_max_bits(mx));  // (uniform)
-    const uint32_t e = make_entry(min(E, Ez), ds, anytie);
-    // predicted fallback: no entry, or the chunk's sum likely crosses
-    // into the next binade (from the approximate running sum)
-    // (a chunk adding nothing crosses nothing)
-    const bool pred = e == kNoEntry ||
-                      (ds > 0.0f && ldexpf(sp, 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f));
-    if (lane == 0) a.tab[(long long)(gc * KC + i) * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
-    if (pred && a.plan) {
-      const unsigned long long p0 = a.stats ? __builtin_amdgcn_s_memtime() : 0ull;
-      chunk_plan(tt, sp, E, lane, a.plan + 2 * ((long long)(gc * KC + i) * nch + j));
-      if (a.stats && lane == 0) {  // (plans: count, s_memtime cycles)
-        atomicAdd(a.stats + 22, 1);
-        atomicAdd(a.stats + 23, (int)(__builtin_amdgcn_s_memtime() - p0));
+    for (int c = 0; c < kFcSegChunks; ++c) {
+      const int j = seg * kFcSegChunks + c;
+      if (j >= nch) break;
+      const int x0 = j * kFcChunk + 4 * lane;
+      float v[4], tt[4], acc = 0.0f;
+      T.terms4(-1, x0, v);
+      T.terms_of(v, i, x0, tt);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc += fabsf(tt[q]);
+        fl |= !isfinite(tt[q]) ? kBad : tt[q] > 0.0f ? kPos : tt[q] < 0.0f ? kNeg : 0u;
       }
+      const float sum = wave_sum(acc);
+      if (lane == 0) a.csum[chain * nch + j] = sum;
+    }
+    const uint32_t f = (__ballot((fl & kPos) != 0u) ? kPos : 0u) |
+                       (__ballot((fl & kNeg) != 0u) ? kNeg : 0u) |
+                       (__ballot((fl & kBad) != 0u) ? kBad : 0u);
+    if (lane == 0) a.cflag[chain * nseg + seg] = f;
+  }
+}
+
+template <int BASE>
+__global__ __launch_bounds__(576) void k_fc_tables9(FcArgs a) {
+  const int seg = blockIdx.x;
+  const int lane = threadIdx.x & 63, i = threadIdx.x >> 6;
+  for (int g = blockIdx.y;; g += gridDim.y) {  // (block-uniform)
+    int id;
+    if (!group_id(a, g, &id)) return;
+    Terms<BASE, 9> T;
+    T.init(a, id);
+    const int nch = fc_chunks(a.n);
+    const int gc = a.by_id ? id : g;
+    if (BASE == FC_KEPT) T.m = a.mass[id];
+    const long long chain = (long long)gc * 9 + i;
+    const float* cs = a.csum + chain * nch;
+    const int j0 = seg * kFcSegChunks;
+    // the approximate running sum before the segment; the segment's own
+    // chunk sums (lanes 0 .. 3)
+    float acc = 0.0f;
+    for (int t = lane; t < j0; t += 64) acc += cs[t];
+    float run = wave_sum(acc);
+    const float own = lane < kFcSegChunks && j0 + lane < nch ? cs[j0 + lane] : 0.0f;
+#pragma unroll
+    for (int c = 0; c < kFcSegChunks; ++c) {
+      const int j = j0 + c;
+      if (j >= nch) break;
+      const int x0 = j * kFcChunk + 4 * lane;
+      float v[4], tt[4];
+      T.terms4(-1, x0, v);
+      if (BASE == FC_KEPT && a.kept_rows && i == 0) store_kept_cells(a, v, x0, id);
+      T.terms_of(v, i, x0, tt);
+      chain_chunk_entry(a, tt, run, j, chain, lane, nch);
+      run += rdl(own, c);
     }
   }
 }
@@ -2245,6 +2336,11 @@ bool fc_sumtab_enabled() {
     g_fc_sumtab = getenv("PP2_FC_SUMTAB") && getenv("PP2_FC_SUMTAB")[0] == '1';
   return g_fc_sumtab != 0;
 }
+int g_fc_plan9 = -1;
+bool fc_plan9_enabled() {
+  if (g_fc_plan9 < 0) g_fc_plan9 = getenv("PP2_FC_PLAN9") && getenv("PP2_FC_PLAN9")[0] == '1';
+  return g_fc_plan9 != 0;
+}
 std::atomic<unsigned> g_epoch{0};
 unsigned next_epoch() { return ++g_epoch; }
 // pp2_debug_fc_stats: driver counters per set kind (8 ints each, summed over
@@ -2260,11 +2356,9 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
   constexpr int KC = K > 0 ? K : 1;
   FcArgs a = a0;
   a.ngroups = groups;
-  // crossing plans for single-chain groups only: the 9 chains of a K = 9
-  // group (one row, 9 partners) predict crossings in the same chunks, and a
-  // wave working 9 plans (~1600 cycles each) makes the tables kernel's tail
-  // longer than the walk it shortens (256^2 plan step: +14 / -8 us)
-  if (K > 0) a.plan = nullptr;
+  // (K = 9 crossing plans: PP2_FC_PLAN9=1 -- tabled by k_fc_tables9, a wave
+  // per chain)
+  if (K > 0 && !fc_plan9_enabled()) a.plan = nullptr;
   const int nseg = fc_segments(a.n);
   if (g_fc_stats && !a.stats) a.stats = g_fc_stats + 32 * (2 * BASE + (K > 0));
   if (BASE == FC_KEPT) a.by_id = 1;
@@ -2278,8 +2372,16 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
     a.epoch = next_epoch();
     hipLaunchKernelGGL((k_fc_sumtab<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
   } else {
-    if (sums) hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
-    if (tabs) hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+    // (a wave per chain for one-group K = 9 sets, whose tables are latency:
+    // the 9 rewards' 12 -> 8 us; with many groups the 9 waves' repeated base
+    // values cost more -- the kept children's FIB sets: 31 -> 47 us)
+    if (K == 9 && groups == 1 && !a.gcount) {
+      if (sums) hipLaunchKernelGGL((k_fc_sums9<BASE>), dim3(nseg, gy), dim3(576), 0, st, a);
+      if (tabs) hipLaunchKernelGGL((k_fc_tables9<BASE>), dim3(nseg, gy), dim3(576), 0, st, a);
+    } else {
+      if (sums) hipLaunchKernelGGL((k_fc_sums<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+      if (tabs) hipLaunchKernelGGL((k_fc_tables<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
+    }
   }
   if (phases & FC_DRIVE) {
     if constexpr (BASE == FC_KEPT) {
