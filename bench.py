@@ -749,6 +749,8 @@ def config4_leg(args, ws, rank, local, stream):
                 proj["unsharded_1gpu_us_per_step"] = t1
                 proj["speedup_vs_unsharded_1gpu"] = [t1 / proj["us_per_step"][1],
                                                      t1 / proj["us_per_step"][0]]
+                # the share's SQ counters (its 2-D resident instance), newest round
+                rank_share["sq_counters"] = sq_counters("c4_share_sq.json")
                 out["rank_share_8"] = rank_share
     if ws > 1:
         dist.barrier()
@@ -897,11 +899,11 @@ def weak_rank_share(args, local, stream, n1_cells_per_s):
                         "a projection, not a measurement (one GPU)"}}
 
 
-def sq_counters():
+def sq_counters(name="resident_sq.json"):
     """LDS / VALU busy fractions of k_loop_resident from the newest committed
-    SQ-counter summary (profiles/r*/resident_sq.json, tools/collect_lds_pmc.sh
-    + tools/sq_summary.py), or None."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "resident_sq.json")))
+    SQ-counter summary (profiles/r*/<name>, tools/collect_lds_pmc.sh +
+    tools/sq_summary.py; c4_share_sq.json: config 4's rank share), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)))
     for f in reversed(files):
         try:
             d = json.load(open(f))
