@@ -1,6 +1,6 @@
 #!/bin/bash
 # The GPU driver: one script, one mode per step argument (tools/README.md);
-# ROUND (default r05) names the PMC summary directories.
+# ROUND (default r06) names the PMC summary directories.
 #   tests    full `pytest -m gpu` suite
 #   planner  tests/test_gpu_planner.py only
 #   bench    driver-style bench (N=1, 20 steps)
@@ -33,8 +33,8 @@ run_planner() { timeout -k 10 600 python -u -m pytest tests/test_gpu_planner.py 
 run_smoke()   { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; }
 run_bench()   { timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; }
 run_prof()    { timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --profile --steps 20 --warmup 20 > $OUT/prof.log 2>&1; }
-run_pmc()     { PMC_DIR=pmc_${ROUND:-r05} timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmc.log 2>&1; }
-run_pmcx()    { PP2_LIBRARY=$PWD/tools/_var/c_xcd.so PMC_DIR=pmc_${ROUND:-r05}x timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmcx.log 2>&1; }
+run_pmc()     { PMC_DIR=pmc_${ROUND:-r06} timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmc.log 2>&1; }
+run_pmcx()    { PP2_LIBRARY=$PWD/tools/_var/c_xcd.so PMC_DIR=pmc_${ROUND:-r06}x timeout -k 10 900 bash tools/collect_pmc.sh > $OUT/pmcx.log 2>&1; }
 run_shards()  { timeout -k 10 600 python -u -m pytest tests/test_gpu_shards.py tests/test_gpu_resident.py -x -v $T > $OUT/pytest_shards.log 2>&1; }
 run_ab()      { timeout -k 10 900 bash tools/ab_builds.sh > $OUT/ab.log 2>&1; }
 run_copy()    { timeout -k 10 120 tools/micro/copy_bw 2048 > $OUT/copy_bw.txt 2>&1; }
