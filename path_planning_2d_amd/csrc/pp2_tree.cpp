@@ -893,8 +893,16 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     for (int cc = 0; cc < 144; ++cc) CHECK(acquire_slot(p, &p->pre[cc]));
   }
   tmark(0);
-  HIPCHK(hipEventRecord(p->ev_fork, c->stream));  // brow and the previous stores are in place
-  HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
+  // side waits for main's work so far (brow and the previous stores in
+  // place) -- unless main is idle (the usual case right after the previous
+  // expansion's wait): a stream query costs the host less than the fork
+  const hipError_t mq = hipStreamQuery(c->stream);
+  if (mq == hipErrorNotReady) {
+    HIPCHK(hipEventRecord(p->ev_fork, c->stream));
+    HIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
+  } else {
+    HIPCHK(mq);
+  }
   tmark(1);
   // The two streams' launches are interleaved phase by phase, so that
   // neither waits for the host to enqueue the other's (a launch costs the
