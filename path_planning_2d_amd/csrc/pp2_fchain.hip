@@ -209,6 +209,31 @@ struct Terms {
   __device__ __forceinline__ float term(float v, int i, int x) const {
     return K > 0 ? v * part[(long long)i * ld + x] : v;
   }
+  // every chain's partner values of the 4 cells x0 .. x0+3 (0 past n), all
+  // loads issued before any is used (K = 9: one round trip, not nine)
+  __device__ __forceinline__ void partner_quads(int x0, float (&w)[K > 0 ? K : 1][4]) const {
+    constexpr int KC = K > 0 ? K : 1;
+    if (K == 0) return;
+    if (x0 + 4 <= n) {
+#pragma unroll
+      for (int i = 0; i < KC; ++i) {
+        const f4a q = *reinterpret_cast<const f4a*>(part + (long long)i * ld + x0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[i][c] = q[c];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KC; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[i][c] = x0 + c < n ? part[(long long)i * ld + x0 + c] : 0.0f;
+    }
+  }
+  // chain i's terms from the base values and the partner quads
+  __device__ __forceinline__ void terms_with(const float (&v)[4], const float (&w)[K > 0 ? K : 1][4],
+                                             int i, float (&t)[4]) const {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = K > 0 ? v[q] * w[i][q] : v[q];
+  }
   // chain i's terms of the 4 cells x0 .. x0+3 from their base values v (0
   // past n: v is)
   __device__ __forceinline__ void terms_of(const float (&v)[4], int i, int x0,
@@ -264,8 +289,14 @@ struct Terms {
 // the chunk sums the binades are predicted from)
 __device__ __forceinline__ float kept_mass(const FcArgs& a, int id, int nch, int lane) {
   if (a.mass) return a.mass[id];
+  const float* m = a.msum + (long long)id * nch;
   float acc = 0.0f;
-  for (int c = lane; c < nch; c += 64) acc += a.msum[(long long)id * nch + c];
+  int c = lane;
+  for (; c + 192 < nch; c += 256) {  // (four loads in flight)
+    const float m0 = m[c], m1 = m[c + 64], m2 = m[c + 128], m3 = m[c + 192];
+    acc += (m0 + m1) + (m2 + m3);
+  }
+  for (; c < nch; c += 64) acc += m[c];
   return wave_sum(acc);
 }
 
@@ -292,12 +323,13 @@ __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
   const int j = seg * kFcSegChunks + w;
   if (j < nch) {
     const int x0 = j * kFcChunk + 4 * lane;
-    float v[4];
+    float v[4], wq[KC][4];
     T.terms4(-1, x0, v);  // the base terms
+    T.partner_quads(x0, wq);
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
       float acc = 0.0f, tt[4];
-      T.terms_of(v, i, x0, tt);
+      T.terms_with(v, wq, i, tt);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float t = tt[q];
@@ -506,10 +538,12 @@ __device__ __forceinline__ void chunk_entries(const FcArgs& a, const Terms<BASE,
                                               const float* sP, int sPstride, int lane, int nch) {
   constexpr int KC = K > 0 ? K : 1;
   if (BASE == FC_KEPT && a.kept_rows) store_kept_cells(a, v, x0, id);
+  float wq[KC][4];
+  T.partner_quads(x0, wq);
 #pragma unroll
   for (int i = 0; i < KC; ++i) {
     float tt[4];
-    T.terms_of(v, i, x0, tt);
+    T.terms_with(v, wq, i, tt);
     chain_chunk_entry(a, tt, sP[i * sPstride], j, (long long)gc * KC + i, lane, nch);
   }
 }
@@ -609,23 +643,35 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
   const int j0 = seg * kFcSegChunks;
   const int gc = a.by_id ? id : g;  // (the scratch chains' index)
   if (BASE == FC_KEPT) T.m = a.mass[id];
-  // the approximate running sum before this segment, and inside it
+  // the approximate running sum before this segment, and inside it (every
+  // chain's loads issued before the first is used: one round trip)
+  {
+    const float* cs0 = a.csum + (long long)(gc * KC) * nch;
+    float acc[KC];
 #pragma unroll
-  for (int i = 0; i < KC; ++i) {
-    const float* cs = a.csum + (long long)(gc * KC + i) * nch;
-    float acc = 0.0f;
-    for (int t = threadIdx.x; t < j0; t += 256) acc += cs[t];
-    acc = wave_sum(acc);
-    if (lane == 0) sPart[i][w] = acc;
+    for (int i = 0; i < KC; ++i) acc[i] = (int)threadIdx.x < j0 ? cs0[(long long)i * nch + threadIdx.x] : 0.0f;
+    for (int t = threadIdx.x + 256; t < j0; t += 256)
+#pragma unroll
+      for (int i = 0; i < KC; ++i) acc[i] += cs0[(long long)i * nch + t];
+    // the segment's own chunk sums: thread i * 4 + c (i < KC, c < 4)
+    const int oi = threadIdx.x >> 2, oc = threadIdx.x & 3;
+    const float own = oi < KC && j0 + oc < nch ? cs0[(long long)oi * nch + j0 + oc] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const float s2 = wave_sum(acc[i]);
+      if (lane == 0) sPart[i][w] = s2;
+    }
+    if (oi < KC) sP[oi][oc] = own;  // (the chunk sums, turned into running sums below)
   }
   __syncthreads();
   if (threadIdx.x < KC) {
     const int i = threadIdx.x;
-    const float* cs = a.csum + (long long)(gc * KC + i) * nch;
     float run = (sPart[i][0] + sPart[i][1]) + (sPart[i][2] + sPart[i][3]);
+#pragma unroll
     for (int c = 0; c < kFcSegChunks; ++c) {
+      const float cs = sP[i][c];
       sP[i][c] = run;
-      if (j0 + c < nch) run += cs[j0 + c];
+      run += cs;
     }
   }
   __syncthreads();
@@ -1519,8 +1565,9 @@ __global__ __launch_bounds__(256) void k_fc_cdf(FcArgs a) {
 // counts per action, counts[a * 16 + z], and the kept children c = z * 9 + a
 // in std::set order (klist, *kcount).
 constexpr int kSampleSub = 4096;  // 16-cell running-sum ends held in LDS (n <= 65536)
-__global__ __launch_bounds__(1024) void k_tree_sample(SampleArgs s) {
+__global__ __launch_bounds__(1024) void k_tree_sample(SampleArgs s, FcRowTable rows) {
   __shared__ int cnt[144];
+  if (s.rows_out && threadIdx.x < 144) s.rows_out[threadIdx.x] = rows.p[threadIdx.x];
   __shared__ float sSub[kSampleSub];
   for (int i = threadIdx.x; i < 144; i += blockDim.x) cnt[i] = 0;
   const int N = s.N, n = s.n, W = s.g.width;
@@ -1641,6 +1688,26 @@ __global__ __launch_bounds__(256) void k_store_kept(const int* __restrict__ klis
   const float b = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
   dst[(long long)c * ld + x] = b;
   if (rows.use) rows.p[c][x] = b;
+}
+
+// The kept children's dense rows (src + c * ld) into their node rows
+// rows.p[c] -- beside the FIB walk that reads the dense ones.
+__global__ __launch_bounds__(256) void k_copy_kept(const int* __restrict__ klist,
+                                                   const int* __restrict__ kcount,
+                                                   const float* __restrict__ src, int n, int ld,
+                                                   FcRowTable rows) {
+  const int r = blockIdx.y;
+  if (r >= *kcount) return;
+  const int c = klist[r];
+  const int x = 4 * (blockIdx.x * 256 + threadIdx.x);
+  if (x >= n) return;
+  const float* s = src + (long long)c * ld + x;
+  float* d = rows.p[c] + x;
+  if (x + 4 <= n) {
+    *reinterpret_cast<f4a*>(d) = *reinterpret_cast<const f4a*>(s);
+  } else {
+    for (int q = 0; x + q < n; ++q) d[q] = s[q];
+  }
 }
 
 // ================================================================ fused chain sets
@@ -2508,7 +2575,10 @@ hipError_t launch_tree_sample(hipStream_t st, const SampleArgs& s) {
   if (s.N <= 0 || s.n <= 0 || !s.cdf || !s.r || !s.u1 || !s.u2 || !s.counts || !s.klist ||
       !s.kcount)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_tree_sample, dim3(1), dim3(1024), 0, st, s);
+  if (!s.rows != !s.rows_out) return hipErrorInvalidValue;
+  FcRowTable t;
+  if (s.rows) t = *s.rows;
+  hipLaunchKernelGGL(k_tree_sample, dim3(1), dim3(1024), 0, st, s, t);
   return hipGetLastError();
 }
 
@@ -2529,6 +2599,15 @@ hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount
   if (rows) t = *rows;
   hipLaunchKernelGGL(k_store_kept, dim3((n + 255) / 256, 144), dim3(256), 0, st, klist, kcount,
                      pred, lrows, sums, dst, n, ld, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_kept(hipStream_t st, const int* klist, const int* kcount, const float* src,
+                            int n, int ld, const FcRowTable* rows) {
+  if (n <= 0) return hipSuccess;
+  if (!rows || ld % 4 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_copy_kept, dim3((n + 1023) / 1024, 144), dim3(256), 0, st, klist, kcount,
+                     src, n, ld, *rows);
   return hipGetLastError();
 }
 

@@ -218,6 +218,10 @@ struct SampleArgs {
   // and the chunk start states, whose entry [chunks] holds the sign flags
   const float* sub = nullptr;
   const int2* cst = nullptr;
+  // optional: a table of row pointers to publish to the device on the way
+  // (*rows, carried in the kernel's arguments, into rows_out[144])
+  const struct FcRowTable* rows = nullptr;
+  float** rows_out = nullptr;
 };
 hipError_t launch_tree_sample(hipStream_t st, const SampleArgs& s);
 // Fused chain sets (pp2_fchain.hip, round 6): the same sums as launch_fchain,
@@ -299,6 +303,9 @@ struct FcRowTable {
   int use = 0;
   float* p[144] = {};
 };
+// the kept children's dense rows src + c * ld into rows->p[c] (n cells)
+hipError_t launch_copy_kept(hipStream_t st, const int* klist, const int* kcount, const float* src,
+                            int n, int ld, const FcRowTable* rows);
 hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount,
                              const float* pred, const float* lrows, const float* sums, float* dst,
                              int n, int ld, const FcRowTable* rows = nullptr);

@@ -229,6 +229,7 @@ struct pp2_planner {
   hipEvent_t ev_csum = nullptr, ev_fsum = nullptr;
   float** h_rowptr = nullptr;   // pinned, mapped: the 144 children's node rows
   float** d_rowptr = nullptr;
+  float** d_rowdev = nullptr;   // device: the same, published by k_tree_sample
   // reference order, PBVI leaves: every row's candidate alphas (those whose
   // exact chain can reach the row's maximum, from the split-x GEMM's
   // approximate dots and a rigorous bound) as one exact chain set (FC_LIST)
@@ -248,6 +249,11 @@ struct pp2_planner {
   bool spin = true;             // wait_event: poll (PP2_SPIN_WAIT)
   double t_enq = 0, t_post = 0, t_between = 0;
   double t_mark[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (enqueue phases, tmark())
+  // (plan steps: entry .. the first expansion, the last expansion .. return,
+  // the caller's time between steps)
+  double t_upd = 0, t_tail = 0, t_out = 0;
+  long long t_steps = 0;
+  std::chrono::steady_clock::time_point t_ret_step{};
   long long t_n = 0;
   std::chrono::steady_clock::time_point t_last_store{};
   unsigned frows_version = 0;   // the context's fib_version d_frows was packed from (0: never)
@@ -1049,6 +1055,15 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       sa.kcount = p->d_kcount;
       sa.sub = cd.sub;
       sa.cst = cd.cst;
+      // (the 144 children's node rows, acquired above, published to the
+      // device in the sampler's arguments for the FIB tables that store them)
+      pp2::FcRowTable rt;
+      rt.use = 1;
+      for (int cc = 0; cc < 144; ++cc) rt.p[cc] = p->slots[p->pre[cc]].row;
+      if (!p->seq) {
+        sa.rows = &rt;
+        sa.rows_out = p->d_rowdev;
+      }
       HIPCHK(pp2::launch_tree_sample(c->stream, sa));
     }
     const bool sumtab = pp2::fc_sumtab_active();
@@ -1056,7 +1071,9 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     kd.gcount = p->d_kcount;
     if (!p->seq && !sumtab) {
       // main, beside the children's walk: the kept children's FIB chunk sums
-      // (their masses approximated by the children's chunk sums)
+      // (their masses approximated by the children's chunk sums; waiting
+      // for the walk here instead, one cross-stream wait fewer, started the
+      // sums ~12 us after the samples)
       HIPCHK(hipStreamWaitEvent(c->stream, p->ev_csum, 0));
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_SUMS));
     }
@@ -1090,7 +1107,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       // (with k_fc_sumtab: the sums too, in the same launch, exact masses)
       kd.mass = p->d_csum;
       kd.kept_rows = p->d_children;
-      kd.rowptr = p->d_rowptr;
+      kd.rowptr = p->d_rowdev;
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd,
                                 sumtab ? pp2::FC_TABLES : pp2::FC_TAB));
     }
@@ -1431,7 +1448,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         !p->scr_main.reserve((int)p->n, 144 * 9) || !p->scr_side.reserve((int)p->n, 144) ||
         !p->scr_fib.reserve((int)p->n, 144 * 9) || !p->scr_rew.reserve((int)p->n, 9) ||
         !host_mapped(2 * 144, reinterpret_cast<float**>(&p->h_rowptr),
-                     reinterpret_cast<float**>(&p->d_rowptr)))
+                     reinterpret_cast<float**>(&p->d_rowptr)) ||
+        hipMalloc(&p->d_rowdev, 144 * sizeof(float*)) != hipSuccess)
       return fail(set_err(PP2_ENOMEM, "planner reference-order scratch allocation failed"));
     std::vector<int> srow(144, 0);
     std::vector<uint8_t> us(144), zs(144);
@@ -1519,13 +1537,17 @@ int pp2_planner_destroy(pp2_planner* p) {
                    p->d_lbpart, p->d_lbdots, p->d_rrows, p->d_frows, p->d_rsum, p->d_lrows,
                    p->d_pred, p->d_csum, p->d_lbapprox, p->d_amax})
     if (d) (void)hipFree(d);
-  for (void* d : {(void*)p->d_aflag, (void*)p->d_plist, (void*)p->d_pcount})
+  for (void* d : {(void*)p->d_aflag, (void*)p->d_plist, (void*)p->d_pcount, (void*)p->d_rowdev})
     if (d) (void)hipFree(d);
   if (p->timing && p->t_n > 0)
     fprintf(stderr, "pp2 planner: %lld expansions, host us per expansion: enqueue %.1f, "
             "after the wait .. children stored %.1f, .. next expansion %.1f; kept children "
             "per expansion %.1f\n", p->t_n, p->t_enq / p->t_n, p->t_post / p->t_n,
             p->t_between / (p->t_n > 1 ? p->t_n - 1 : 1), (double)p->stat_rows / (double)p->t_n);
+  if (p->timing && p->t_steps > 1)
+    fprintf(stderr, "pp2 planner: per plan step us: entry .. first expansion %.1f, last "
+            "expansion .. return %.1f, the caller between steps %.1f\n", p->t_upd / p->t_steps,
+            p->t_tail / p->t_steps, p->t_out / (p->t_steps - 1));
   if (p->timing && p->t_n > 0)
     fprintf(stderr, "pp2 planner: enqueue phases us: rand+slots %.1f, fork %.1f, pred %.1f, tables "
             "%.1f, drives %.1f, sample+rewards %.1f, store %.1f, dots+join %.1f\n",
@@ -1567,6 +1589,10 @@ int pp2_planner_destroy(pp2_planner* p) {
 int pp2_planner_step(pp2_planner* p, uint8_t action, uint8_t observation,
                      const float* belief, uint8_t* new_action, float* new_value) {
   if (!p) return set_err(PP2_EINVAL, "null planner");
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t_in = p->timing ? clk::now() : clk::time_point{};
+  if (p->timing && p->t_steps > 0)
+    p->t_out += std::chrono::duration<double, std::micro>(t_in - p->t_ret_step).count();
   pp2_ctx* c = p->ctx;
   DeviceGuard dg(c->device);
   if (!p->root) {
@@ -1590,9 +1616,11 @@ int pp2_planner_step(pp2_planner* p, uint8_t action, uint8_t observation,
   // while (getDepth() < max_search_tree_depth &&
   //        update_counter++ < max_online_iteration) expand();   (:219-223)
   int counter = 0;
+  if (p->timing) p->t_upd += std::chrono::duration<double, std::micro>(clk::now() - t_in).count();
   while (p->root->depth < (uint32_t)p->prm.max_search_tree_depth &&
          counter++ < p->prm.max_online_iteration)
     CHECK(tree_expand(p));
+  const clk::time_point t_loop = p->timing ? clk::now() : clk::time_point{};
   // SearchTree::getOptimalAction (search_tree_cuda.cu:510-524)
   uint8_t a = 0;
   float r = -FLT_MAX;
@@ -1603,6 +1631,11 @@ int pp2_planner_step(pp2_planner* p, uint8_t action, uint8_t observation,
     }
   if (new_action) *new_action = a;
   if (new_value) *new_value = r;
+  if (p->timing) {
+    p->t_ret_step = clk::now();
+    p->t_tail += std::chrono::duration<double, std::micro>(p->t_ret_step - t_loop).count();
+    ++p->t_steps;
+  }
   return PP2_OK;
 }
 
