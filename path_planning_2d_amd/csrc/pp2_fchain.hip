@@ -477,8 +477,10 @@ __device__ __forceinline__ void chunk_plan(const float (&tt)[4], float sp, int E
 // One chunk's table entries (and crossing plans, and FC_KEPT's normalised
 // cells) from its base values v and the approximate running sums before it,
 // sP[i] of chain i: k_fc_tables' and k_fc_sumtab's common part.
-// One chain's entry (and crossing plan) of chunk j: its terms tt and the
-// approximate running sum sp before the chunk; chain = the scratch chain.
+// One chain's entry (and crossing plan, PLANS) of chunk j: its terms tt and
+// the approximate running sum sp before the chunk; chain = the scratch chain.
+// (Branch-free but for the plan: the K = 9 loop's chains interleave.)
+template <bool PLANS = true>
 __device__ __forceinline__ void chain_chunk_entry(const FcArgs& a, const float (&tt)[4], float sp,
                                                   int j, long long chain, int lane, int nch) {
   const int E = domain_of(sp);
@@ -496,8 +498,7 @@ __device__ __forceinline__ void chain_chunk_entry(const FcArgs& a, const float (
   const bool anytie = __ballot(tie) != 0ull;
   // a chunk adding nothing is tabled for the lowest domain where it adds
   // nothing (entry_applies: every domain above too)
-  int Ez = E;
-  if (ds == 0.0f) Ez = zero_domain(wave_max_bits(mx));  // (uniform)
+  const int Ez = ds == 0.0f ? zero_domain(wave_max_bits(mx)) : E;
   const uint32_t e = make_entry(min(E, Ez), ds, anytie);
   // predicted fallback: no entry, or the chunk's sum likely crosses
   // into the next binade (from the approximate running sum)
@@ -505,7 +506,7 @@ __device__ __forceinline__ void chain_chunk_entry(const FcArgs& a, const float (
   const bool pred = e == kNoEntry ||
                     (ds > 0.0f && ldexpf(sp, 23 - E) + ds >= (float)kK24 * (1.0f - 0x1p-12f));
   if (lane == 0) a.tab[chain * nch + j] = make_uint2(e, pred ? kPredicted : 0u);
-  if (pred && a.plan) {
+  if (PLANS && pred && a.plan) {
     const unsigned long long p0 = a.stats ? __builtin_amdgcn_s_memtime() : 0ull;
     chunk_plan(tt, sp, E, lane, a.plan + 2 * (chain * nch + j));
     if (a.stats && lane == 0) {  // (plans: count, s_memtime cycles)
@@ -544,7 +545,9 @@ __device__ __forceinline__ void chunk_entries(const FcArgs& a, const Terms<BASE,
   for (int i = 0; i < KC; ++i) {
     float tt[4];
     T.terms_with(v, wq, i, tt);
-    chain_chunk_entry(a, tt, sP[i * sPstride], j, (long long)gc * KC + i, lane, nch);
+    // (K = 9: no crossing plans, launch_set; compiled out so the chains'
+    // code interleaves)
+    chain_chunk_entry<K == 0>(a, tt, sP[i * sPstride], j, (long long)gc * KC + i, lane, nch);
   }
 }
 
@@ -556,6 +559,7 @@ __device__ __forceinline__ void chunk_entries(const FcArgs& a, const Terms<BASE,
 // rewards), and a chunk's 9 crossing plans spread over 9 waves.
 template <int BASE>
 __global__ __launch_bounds__(576) void k_fc_sums9(FcArgs a) {
+  __shared__ __attribute__((aligned(16))) float sV[kFcSegChunks][kFcChunk];  // base values
   const int seg = blockIdx.x;
   const int lane = threadIdx.x & 63, i = threadIdx.x >> 6;
   for (int g = blockIdx.y;; g += gridDim.y) {  // (block-uniform)
@@ -565,16 +569,27 @@ __global__ __launch_bounds__(576) void k_fc_sums9(FcArgs a) {
     T.init(a, id);
     const int nch = fc_chunks(a.n), nseg = fc_segments(a.n);
     const int gc = a.by_id ? id : g;
-    if (BASE == FC_KEPT) T.m = kept_mass(a, id, nch, lane);
     const long long chain = (long long)gc * 9 + i;
+    const int j0 = seg * kFcSegChunks;
+    // the segment's base values, once: waves 0 .. 3 a chunk each (FC_KEPT:
+    // the normalisation's division done once, not per chain)
+    if (i < kFcSegChunks) {
+      if (BASE == FC_KEPT) T.m = kept_mass(a, id, nch, lane);
+      const int j = j0 + i, x0 = j * kFcChunk + 4 * lane;
+      float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (j < nch) T.terms4(-1, x0, v);
+      *reinterpret_cast<f4a*>(&sV[i][4 * lane]) = f4a{v[0], v[1], v[2], v[3]};
+    }
+    __syncthreads();
     uint32_t fl = 0u;
 #pragma unroll
     for (int c = 0; c < kFcSegChunks; ++c) {
-      const int j = seg * kFcSegChunks + c;
+      const int j = j0 + c;
       if (j >= nch) break;
       const int x0 = j * kFcChunk + 4 * lane;
-      float v[4], tt[4], acc = 0.0f;
-      T.terms4(-1, x0, v);
+      const f4a vv = *reinterpret_cast<const f4a*>(&sV[c][4 * lane]);
+      const float v[4] = {vv[0], vv[1], vv[2], vv[3]};
+      float tt[4], acc = 0.0f;
       T.terms_of(v, i, x0, tt);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -588,11 +603,13 @@ __global__ __launch_bounds__(576) void k_fc_sums9(FcArgs a) {
                        (__ballot((fl & kNeg) != 0u) ? kNeg : 0u) |
                        (__ballot((fl & kBad) != 0u) ? kBad : 0u);
     if (lane == 0) a.cflag[chain * nseg + seg] = f;
+    __syncthreads();  // (sV of the next group)
   }
 }
 
 template <int BASE>
 __global__ __launch_bounds__(576) void k_fc_tables9(FcArgs a) {
+  __shared__ __attribute__((aligned(16))) float sV[kFcSegChunks][kFcChunk];  // base values
   const int seg = blockIdx.x;
   const int lane = threadIdx.x & 63, i = threadIdx.x >> 6;
   for (int g = blockIdx.y;; g += gridDim.y) {  // (block-uniform)
@@ -602,28 +619,41 @@ __global__ __launch_bounds__(576) void k_fc_tables9(FcArgs a) {
     T.init(a, id);
     const int nch = fc_chunks(a.n);
     const int gc = a.by_id ? id : g;
-    if (BASE == FC_KEPT) T.m = a.mass[id];
     const long long chain = (long long)gc * 9 + i;
     const float* cs = a.csum + chain * nch;
     const int j0 = seg * kFcSegChunks;
     // the approximate running sum before the segment; the segment's own
-    // chunk sums (lanes 0 .. 3)
+    // chunk sums (lanes 0 .. 3) -- loads first
     float acc = 0.0f;
     for (int t = lane; t < j0; t += 64) acc += cs[t];
-    float run = wave_sum(acc);
     const float own = lane < kFcSegChunks && j0 + lane < nch ? cs[j0 + lane] : 0.0f;
+    // the segment's base values, once: waves 0 .. 3 a chunk each (FC_KEPT:
+    // the normalised cells, stored to their rows here too)
+    if (i < kFcSegChunks) {
+      if (BASE == FC_KEPT) T.m = a.mass[id];
+      const int j = j0 + i, x0 = j * kFcChunk + 4 * lane;
+      float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (j < nch) {
+        T.terms4(-1, x0, v);
+        if (BASE == FC_KEPT && a.kept_rows) store_kept_cells(a, v, x0, id);
+      }
+      *reinterpret_cast<f4a*>(&sV[i][4 * lane]) = f4a{v[0], v[1], v[2], v[3]};
+    }
+    float run = wave_sum(acc);
+    __syncthreads();
 #pragma unroll
     for (int c = 0; c < kFcSegChunks; ++c) {
       const int j = j0 + c;
       if (j >= nch) break;
       const int x0 = j * kFcChunk + 4 * lane;
-      float v[4], tt[4];
-      T.terms4(-1, x0, v);
-      if (BASE == FC_KEPT && a.kept_rows && i == 0) store_kept_cells(a, v, x0, id);
+      const f4a vv = *reinterpret_cast<const f4a*>(&sV[c][4 * lane]);
+      const float v[4] = {vv[0], vv[1], vv[2], vv[3]};
+      float tt[4];
       T.terms_of(v, i, x0, tt);
       chain_chunk_entry(a, tt, run, j, chain, lane, nch);
       run += rdl(own, c);
     }
+    __syncthreads();  // (sV of the next group)
   }
 }
 
@@ -2403,6 +2433,11 @@ bool fc_sumtab_enabled() {
     g_fc_sumtab = getenv("PP2_FC_SUMTAB") && getenv("PP2_FC_SUMTAB")[0] == '1';
   return g_fc_sumtab != 0;
 }
+int g_fc_k9wave = -1;  // (PP2_FC_K9WAVE=1: every K = 9 set a wave per chain)
+bool fc_k9wave_enabled() {
+  if (g_fc_k9wave < 0) g_fc_k9wave = getenv("PP2_FC_K9WAVE") && getenv("PP2_FC_K9WAVE")[0] == '1';
+  return g_fc_k9wave != 0;
+}
 int g_fc_plan9 = -1;
 bool fc_plan9_enabled() {
   if (g_fc_plan9 < 0) g_fc_plan9 = getenv("PP2_FC_PLAN9") && getenv("PP2_FC_PLAN9")[0] == '1';
@@ -2442,7 +2477,7 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
     // (a wave per chain for one-group K = 9 sets, whose tables are latency:
     // the 9 rewards' 12 -> 8 us; with many groups the 9 waves' repeated base
     // values cost more -- the kept children's FIB sets: 31 -> 47 us)
-    if (K == 9 && groups == 1 && !a.gcount) {
+    if (K == 9 && ((groups == 1 && !a.gcount) || fc_k9wave_enabled())) {
       if (sums) hipLaunchKernelGGL((k_fc_sums9<BASE>), dim3(nseg, gy), dim3(576), 0, st, a);
       if (tabs) hipLaunchKernelGGL((k_fc_tables9<BASE>), dim3(nseg, gy), dim3(576), 0, st, a);
     } else {
