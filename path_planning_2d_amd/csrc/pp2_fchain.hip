@@ -541,8 +541,10 @@ __device__ __forceinline__ void chunk_entries(const FcArgs& a, const Terms<BASE,
   if (BASE == FC_KEPT && a.kept_rows) store_kept_cells(a, v, x0, id);
   float wq[KC][4];
   T.partner_quads(x0, wq);
+  const uint32_t cm = K > 0 && a.cmask ? a.cmask[id] : 0xffffu;
 #pragma unroll
   for (int i = 0; i < KC; ++i) {
+    if (!((cm >> i) & 1u)) continue;  // (uniform: not a candidate)
     float tt[4];
     T.terms_with(v, wq, i, tt);
     // (K = 9: no crossing plans, launch_set; compiled out so the chains'
@@ -640,11 +642,13 @@ __global__ __launch_bounds__(576) void k_fc_tables9(FcArgs a) {
       *reinterpret_cast<f4a*>(&sV[i][4 * lane]) = f4a{v[0], v[1], v[2], v[3]};
     }
     float run = wave_sum(acc);
+    // (not a candidate, launch_fib_cands: the wave only stages base values)
+    const bool skip = a.cmask && !((a.cmask[id] >> i) & 1u);
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < kFcSegChunks; ++c) {
       const int j = j0 + c;
-      if (j >= nch) break;
+      if (j >= nch || skip) break;
       const int x0 = j * kFcChunk + 4 * lane;
       const f4a vv = *reinterpret_cast<const f4a*>(&sV[c][4 * lane]);
       const float v[4] = {vv[0], vv[1], vv[2], vv[3]};
@@ -939,6 +943,7 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
   const int g = ch / KC, i = ch % KC;
   int id;
   if (!group_id(a, g, &id)) return;
+  if (K > 0 && a.cmask && !((a.cmask[id] >> i) & 1u)) continue;  // (not a candidate)
   Terms<BASE, K> T;
   T.init(a, id);
   const int lane = threadIdx.x;
@@ -1176,6 +1181,7 @@ __global__ __launch_bounds__(64) void k_fc_walk(FcArgs a) {
   const int g = ch / KC, i = ch % KC;
   int id;
   if (!group_id(a, g, &id)) return;
+  if (K > 0 && a.cmask && !((a.cmask[id] >> i) & 1u)) continue;  // (not a candidate)
   WalkRows<BASE, K> R;
   R.init(a, id, i);
   const int lane = threadIdx.x;
@@ -1718,6 +1724,78 @@ __global__ __launch_bounds__(256) void k_store_kept(const int* __restrict__ klis
   const float b = v / sums[c];  // b[x] /= sum (search_tree_cuda.cu:228-229)
   dst[(long long)c * ld + x] = b;
   if (rows.use) rows.p[c][x] = b;
+}
+
+// The kept children's FIB candidates (launch_fib_cands).  The sums pass
+// formed chain i's chunk sums A_j of |t'|, t' = fl(fl(w / m') alpha) with the
+// approximate mass m' (kept_mass from msum); the chain's terms are
+// t = fl(fl(w / m) alpha) with the exact mass m, so the chunk sums C_j of |t|
+// are within A_j m' / m (1 +- 2^-15) -- the sums' rounding, < 2^-18, and 4
+// roundings per term -- plus an absolute n 2^-100 for subnormal results
+// (|alpha| < 2^40).  When no term is positive or non-finite, the reference's
+// x-ordered fp32 chain R is <= 0, and each of its n adds rounds by at most u
+// (= 2^-24) times its partial sum, itself at most (1 + n u / (1 - n u)) times
+// the prefix of |t| through the add's chunk: | |R| - T | <= u (1 + ...) 256
+// sum_j (nch - j) C_j (T = sum |t|).  A chain whose lowest |R| exceeds
+// another's highest has the lower dot, never evaluateFibCpu's first maximum:
+// out = -inf, and it is neither tabled nor walked.
+__global__ __launch_bounds__(64) void k_fib_cands(FcArgs a, uint16_t* __restrict__ cmask) {
+  const int lane = threadIdx.x;
+  for (int g = blockIdx.x;; g += gridDim.x) {
+    int id;
+    if (!group_id(a, g, &id)) return;
+    const int nch = fc_chunks(a.n), nseg = fc_segments(a.n);
+    FcArgs ap = a;
+    ap.mass = nullptr;  // (the sums pass's m')
+    const double mp = kept_mass(ap, id, nch, lane), m = a.mass[id];
+    const double nu = (double)a.n * 0x1p-24, rel = nu / (1.0 - nu);
+    const double absl = (double)a.n * 0x1p-100;
+    const bool mok = mp > 0.0 && m > 0.0 && isfinite(mp) && isfinite(m) && nu < 0.5;
+    double lo[9], hi[9];
+    bool bounded[9];
+    // (every chain's loads issued before any sum: one round trip per 64 chunks)
+    float acc[9], wacc[9];  // sum A_j, sum (nch - j) A_j
+    uint32_t f[9];
+    const float* cs = a.csum + (long long)id * 9 * nch;
+    const uint32_t* cf = a.cflag + (long long)id * 9 * nseg;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      acc[i] = wacc[i] = 0.0f;
+      f[i] = 0u;
+    }
+    for (int c = lane; c < nch; c += 64)
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const float x = cs[(long long)i * nch + c];
+        acc[i] += x;
+        wacc[i] = __builtin_fmaf((float)(nch - c), x, wacc[i]);
+      }
+    for (int c = lane; c < nseg; c += 64)
+#pragma unroll
+      for (int i = 0; i < 9; ++i) f[i] |= cf[(long long)i * nseg + c];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const double A = mok ? (double)wave_sum(acc[i]) * (mp / m) : INFINITY;
+      const double W = mok ? (double)wave_sum(wacc[i]) * (mp / m) * (1.0 + 0x1p-15) : INFINITY;
+      const double err = 0x1p-24 * (1.0 + rel) * 256.0 * W + absl;
+      lo[i] = A * (1.0 - 0x1p-15) - err;
+      hi[i] = A * (1.0 + 0x1p-15) + err;
+      bounded[i] = __ballot((f[i] & (kPos | kBad)) != 0u) == 0ull && hi[i] < 0x1p126;
+    }
+    // the smallest upper bound of |R| over the bounded chains
+    double hi_min = INFINITY;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+      if (bounded[i]) hi_min = fmin(hi_min, hi[i]);
+    uint32_t cm = 0u;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const bool cand = !bounded[i] || lo[i] <= hi_min;
+      cm |= cand ? 1u << i : 0u;
+      if (!cand && lane == 0) a.out[(long long)id * a.ldo + i] = -INFINITY;
+    }
+    if (lane == 0) cmask[id] = (uint16_t)cm;
+  }
 }
 
 // The kept children's dense rows (src + c * ld) into their node rows
@@ -2634,6 +2712,16 @@ hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount
   if (rows) t = *rows;
   hipLaunchKernelGGL(k_store_kept, dim3((n + 255) / 256, 144), dim3(256), 0, st, klist, kcount,
                      pred, lrows, sums, dst, n, ld, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_fib_cands(hipStream_t st, const FcArgs& a, uint16_t* cmask) {
+  if (!cmask || !a.glist || !a.gcount || !a.csum || !a.cflag || !a.out || !a.mass || !a.msum ||
+      a.n <= 0)
+    return hipErrorInvalidValue;
+  FcArgs b = a;
+  b.ngroups = 144;  // (the kept children: at most 144, gcount of them)
+  hipLaunchKernelGGL(k_fib_cands, dim3(kFcDevGroups), dim3(64), 0, st, b, cmask);
   return hipGetLastError();
 }
 

@@ -171,7 +171,16 @@ struct FcArgs {
   float* kept_rows = nullptr;    // [144][ld] normalised kept children (written by tables)
   float* const* rowptr = nullptr;  // optional device [144]: their node rows too
   int by_id = 0;                 // scratch chain index (id * K + i) instead of (g * K + i)
+  // K = 9, by_id: chain i of group id is tabled and walked only when bit i of
+  // cmask[id] is set (launch_fib_cands); the others' out entries hold -inf
+  const uint16_t* cmask = nullptr;
 };
+// The kept children's FIB candidates (evaluateFibCpu keeps only the first
+// maximum of the 9 dots): after an FC_KEPT sums pass (a's csum / cflag / msum,
+// by id) and with the exact masses (a.mass), each chain's |dot| is bounded;
+// bit i of cmask[id] is set unless chain i's dot is certainly below another's,
+// whose out[id * ldo + i] is set to -inf.  glist / gcount: the kept children.
+hipError_t launch_fib_cands(hipStream_t st, const FcArgs& a, uint16_t* cmask);
 // Device scratch of one stream's chain sets (a set may not overlap another
 // set using the same scratch).
 struct FcScratch {

@@ -230,6 +230,8 @@ struct pp2_planner {
   float** h_rowptr = nullptr;   // pinned, mapped: the 144 children's node rows
   float** d_rowptr = nullptr;
   float** d_rowdev = nullptr;   // device: the same, published by k_tree_sample
+  uint16_t* d_cmask = nullptr;  // the kept children's FIB candidates (launch_fib_cands)
+  bool fib_cands = false;       // PP2_FIB_CANDS=1: the FIB chains below another skipped
   // reference order, PBVI leaves: every row's candidate alphas (those whose
   // exact chain can reach the row's maximum, from the split-x GEMM's
   // approximate dots and a rigorous bound) as one exact chain set (FC_LIST)
@@ -1108,6 +1110,13 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       kd.mass = p->d_csum;
       kd.kept_rows = p->d_children;
       kd.rowptr = p->d_rowdev;
+      // only the first maximum of a child's 9 dots is kept: the chains
+      // certainly below another (their sums against the exact masses) are
+      // neither tabled nor walked (-inf)
+      if (p->fib_cands && !sumtab) {
+        HIPCHK(pp2::launch_fib_cands(c->stream, kd, p->d_cmask));
+        kd.cmask = p->d_cmask;
+      }
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd,
                                 sumtab ? pp2::FC_TABLES : pp2::FC_TAB));
     }
@@ -1449,7 +1458,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
         !p->scr_fib.reserve((int)p->n, 144 * 9) || !p->scr_rew.reserve((int)p->n, 9) ||
         !host_mapped(2 * 144, reinterpret_cast<float**>(&p->h_rowptr),
                      reinterpret_cast<float**>(&p->d_rowptr)) ||
-        hipMalloc(&p->d_rowdev, 144 * sizeof(float*)) != hipSuccess)
+        hipMalloc(&p->d_rowdev, 144 * sizeof(float*)) != hipSuccess ||
+        hipMalloc(&p->d_cmask, 144 * sizeof(uint16_t)) != hipSuccess)
       return fail(set_err(PP2_ENOMEM, "planner reference-order scratch allocation failed"));
     std::vector<int> srow(144, 0);
     std::vector<uint8_t> us(144), zs(144);
@@ -1508,6 +1518,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
     p->timing = tm && tm[0] == '1';
     const char* sw = getenv("PP2_SPIN_WAIT");
     p->spin = !(sw && sw[0] == '0');
+    const char* fc = getenv("PP2_FIB_CANDS");
+    p->fib_cands = fc && fc[0] == '1';
   }
   *out = p;
   return PP2_OK;
@@ -1537,7 +1549,8 @@ int pp2_planner_destroy(pp2_planner* p) {
                    p->d_lbpart, p->d_lbdots, p->d_rrows, p->d_frows, p->d_rsum, p->d_lrows,
                    p->d_pred, p->d_csum, p->d_lbapprox, p->d_amax})
     if (d) (void)hipFree(d);
-  for (void* d : {(void*)p->d_aflag, (void*)p->d_plist, (void*)p->d_pcount, (void*)p->d_rowdev})
+  for (void* d : {(void*)p->d_aflag, (void*)p->d_plist, (void*)p->d_pcount, (void*)p->d_rowdev,
+                   (void*)p->d_cmask})
     if (d) (void)hipFree(d);
   if (p->timing && p->t_n > 0)
     fprintf(stderr, "pp2 planner: %lld expansions, host us per expansion: enqueue %.1f, "

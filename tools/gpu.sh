@@ -21,6 +21,7 @@
 #   p256     rocprofv3 kernel trace of the config-2 plan step (256^2, depth 3, FIB leaves)
 #   fxab     config-2 plan steps with the fused chain sets (PP2_FX=1) and without (0), interleaved
 #   fxtests  tests/test_gpu_fchain.py + test_gpu_planner.py (the chain sets and the planner)
+#   candab   config-2 plan steps with the FIB candidate masks (PP2_FIB_CANDS=1) and without (0), interleaved
 # Every GPU step has its own time limit, steps are chained with &&.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -51,13 +52,14 @@ run_profplan() { PP2_CASE=node PP2_STEPS=30 timeout -k 10 240 rocprofv3 --kernel
 run_quick()   { timeout -k 10 900 python -u -m pytest tests/test_gpu_shards.py tests/test_gpu_coded.py tests/test_gpu_rollout.py -x -v $T > $OUT/pytest_quick.log 2>&1; }
 run_p256()    { PP2_CASE=256 PP2_STEPS=60 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_p256 -o run -- python3 tools/prof_planner.py > $OUT/prof_p256.log 2>&1; }
 run_fxab()    { for rep in 1 2; do for fx in 1 0; do PP2_FX=$fx PP2_CASE=256 PP2_STEPS=200 timeout -k 10 120 python3 tools/prof_planner.py 2>&1 | sed "s/^/fx=$fx /" >> $OUT/fxab.txt || return 1; done; done; cat $OUT/fxab.txt; }
+run_candab()  { for rep in 1 2 3; do for c in 1 0; do PP2_FIB_CANDS=$c PP2_CASE=256 PP2_STEPS=200 timeout -k 10 120 python3 tools/prof_planner.py 2>&1 | sed "s/^/cands=$c /" >> $OUT/candab.txt || return 1; done; done; cat $OUT/candab.txt; }
 run_fxtests() { timeout -k 10 900 python -u -m pytest tests/test_gpu_fchain.py tests/test_gpu_planner.py -x -v $T > $OUT/pytest_fx.log 2>&1; }
 rc=0
 for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     tests) run_tests ;; planner) run_planner ;; smoke) run_smoke ;; bench) run_bench ;;
-    prof) run_prof ;; pmc) run_pmc ;; pbvitests) run_pbvitests ;; dots) run_dots ;; rollsq) run_rollsq ;; abroll) run_abroll ;; abfib) run_abfib ;; pmcx) run_pmcx ;; fchain) run_fchain ;; copy) run_copy ;; shards) run_shards ;; ab) run_ab ;; pbvi) run_pbvi ;; profplan) run_profplan ;; quick) run_quick ;; p256) run_p256 ;; fxab) run_fxab ;; fxtests) run_fxtests ;;
+    prof) run_prof ;; pmc) run_pmc ;; pbvitests) run_pbvitests ;; dots) run_dots ;; rollsq) run_rollsq ;; abroll) run_abroll ;; abfib) run_abfib ;; pmcx) run_pmcx ;; fchain) run_fchain ;; copy) run_copy ;; shards) run_shards ;; ab) run_ab ;; pbvi) run_pbvi ;; profplan) run_profplan ;; quick) run_quick ;; p256) run_p256 ;; fxab) run_fxab ;; fxtests) run_fxtests ;; candab) run_candab ;;
     *) echo "unknown step $step"; false ;;
   esac
   rc=$?
