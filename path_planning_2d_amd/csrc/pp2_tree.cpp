@@ -250,6 +250,7 @@ struct pp2_planner {
   bool timing = false;
   bool spin = true;             // wait_event: poll (PP2_SPIN_WAIT)
   double t_enq = 0, t_post = 0, t_between = 0;
+  double t_pa = 0, t_pb = 0;  // (t_post: .. the nodes' first row read, .. the nodes built)
   double t_mark[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (enqueue phases, tmark())
   // (plan steps: entry .. the first expansion, the last expansion .. return,
   // the caller's time between steps)
@@ -268,6 +269,10 @@ struct pp2_planner {
 
   VNode* root = nullptr;
   uint32_t n_vnodes = 0, n_qnodes = 0, expansions = 0;
+  // deleted nodes, kept for reuse (an expansion builds ~50: malloc / free
+  // per node cost the host several us per expansion)
+  std::vector<VNode*> vpool;
+  std::vector<QNode*> qpool;
 };
 
 namespace {
@@ -334,12 +339,27 @@ void release_slot(pp2_planner* p, int s) {
 void delete_vnode_only(pp2_planner* p, VNode* v) {
   release_slot(p, v->slot);
   --p->n_vnodes;
-  delete v;
+  p->vpool.push_back(v);
 }
 
 void delete_qnode_only(pp2_planner* p, QNode* q) {
   --p->n_qnodes;
-  delete q;
+  p->qpool.push_back(q);
+}
+
+// A node as freshly constructed, from the pool when it has one (the
+// children vectors keep their capacity)
+QNode* alloc_qnode(pp2_planner* p) {
+  ++p->n_qnodes;
+  if (p->qpool.empty()) return new QNode();
+  QNode* q = p->qpool.back();
+  p->qpool.pop_back();
+  std::vector<VNode*> keep;
+  keep.swap(q->children);
+  *q = QNode();
+  keep.clear();
+  q->children.swap(keep);
+  return q;
 }
 
 void delete_subtree(pp2_planner* p, VNode* v);
@@ -357,7 +377,18 @@ void delete_subtree(pp2_planner* p, VNode* v) {
 }
 
 VNode* new_vnode(pp2_planner* p, uint8_t z, float w, QNode* parent) {
-  VNode* v = new VNode();
+  VNode* v;
+  if (p->vpool.empty()) {
+    v = new VNode();
+  } else {
+    v = p->vpool.back();
+    p->vpool.pop_back();
+    std::vector<QNode*> keep;
+    keep.swap(v->children);
+    *v = VNode();
+    keep.clear();
+    v->children.swap(keep);
+  }
   v->observation = z;
   v->weight = w;
   v->parent = parent;
@@ -773,8 +804,7 @@ int expand_vnode(pp2_planner* p, VNode* v) {
   const float mass = p->h_out[kOutMass];
   const float* stats = p->h_out + kOutStats;
   for (uint8_t a = 0; a < 9; ++a) {
-    QNode* q = new QNode();
-    ++p->n_qnodes;
+    QNode* q = alloc_qnode(p);
     q->action = a;
     q->parent = v;
     q->reward = p->h_out[kOutRewards + a] / mass;
@@ -1142,19 +1172,33 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   const clk::time_point t_enq = p->timing ? clk::now() : clk::time_point{};
   HIPCHK(wait_event(p, p->ev_done));
   const clk::time_point t_ret = p->timing ? clk::now() : clk::time_point{};
+  // the device-written host rows (counts, rewards and FIB dots, PBVI bounds)
+  // are cache misses: request every line at once, not one miss at a time
+  // in the loop below
+  for (int i = 0; i < 144; i += 16) __builtin_prefetch(p->h_counts + i);
+  for (int i = 0; i < kRefOutFloats; i += 16) __builtin_prefetch(p->h_rout + i);
+  if (p->pbvi)
+    for (int i = 0; i < 144; i += 16) __builtin_prefetch(p->h_lbv + i);
   if (p->h_pstat) p->stat_cands += *p->h_pstat;
   if (p->d_stamps) fx_stamps_collect(p);
+  if (p->timing) {
+    volatile float sink = p->h_rout[9 + 9 * 143] + (float)p->h_counts[143];
+    (void)sink;
+    p->t_pa += std::chrono::duration<double, std::micro>(clk::now() - t_ret).count();
+  }
 
   for (QNode* q : v->children)
     if (q) delete_subtree(p, q);
   v->children.assign(9, nullptr);
   long long kept = 0;
   for (uint8_t a = 0; a < 9; ++a) {
-    QNode* q = new QNode();
-    ++p->n_qnodes;
+    QNode* q = alloc_qnode(p);
     q->action = a;
     q->parent = v;
     q->reward = p->h_rout[a];
+    int nk = 0;
+    for (uint8_t z = 0; z < 16; ++z) nk += p->h_counts[a * 16 + z] != 0;
+    q->children.reserve(nk);  // (one allocation, not a growth sequence)
     for (uint8_t z = 0; z < 16; ++z) {  // std::set order
       const int cnt = p->h_counts[a * 16 + z];
       if (!cnt) continue;
@@ -1171,6 +1215,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     qnode_update(p, q);
     v->children[a] = q;
   }
+  if (p->timing) p->t_pb += std::chrono::duration<double, std::micro>(clk::now() - t_ret).count();
   for (int& sl : p->pre) {  // the rows of the children not kept go back
     if (sl >= 0) release_slot(p, sl);
     sl = -1;
@@ -1539,6 +1584,8 @@ int pp2_planner_destroy(pp2_planner* p) {
   fx_stamps_print(p);
   if (p->d_stamps) (void)hipFree(p->d_stamps);
   pp2_planner_reset(p);
+  for (VNode* v : p->vpool) delete v;
+  for (QNode* q : p->qpool) delete q;
   for (Slot& s : p->slots) {
     free_planes(&s.b);
     if (s.mass && !p->ref) (void)hipFree(s.mass);
@@ -1555,8 +1602,10 @@ int pp2_planner_destroy(pp2_planner* p) {
   if (p->timing && p->t_n > 0)
     fprintf(stderr, "pp2 planner: %lld expansions, host us per expansion: enqueue %.1f, "
             "after the wait .. children stored %.1f, .. next expansion %.1f; kept children "
-            "per expansion %.1f\n", p->t_n, p->t_enq / p->t_n, p->t_post / p->t_n,
-            p->t_between / (p->t_n > 1 ? p->t_n - 1 : 1), (double)p->stat_rows / (double)p->t_n);
+            "per expansion %.1f (after the wait: first rows read %.1f, nodes built %.1f)\n",
+            p->t_n, p->t_enq / p->t_n, p->t_post / p->t_n,
+            p->t_between / (p->t_n > 1 ? p->t_n - 1 : 1), (double)p->stat_rows / (double)p->t_n,
+            p->t_pa / p->t_n, p->t_pb / p->t_n);
   if (p->timing && p->t_steps > 1)
     fprintf(stderr, "pp2 planner: per plan step us: entry .. first expansion %.1f, last "
             "expansion .. return %.1f, the caller between steps %.1f\n", p->t_upd / p->t_steps,
