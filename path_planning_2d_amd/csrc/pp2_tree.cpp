@@ -232,6 +232,7 @@ struct pp2_planner {
   float** d_rowdev = nullptr;   // device: the same, published by k_tree_sample
   uint16_t* d_cmask = nullptr;  // the kept children's FIB candidates (launch_fib_cands)
   bool fib_cands = false;       // PP2_FIB_CANDS=1: the FIB chains below another skipped
+  bool row_first = false;       // PP2_ROW_FIRST=1: the cdf chain enqueued before the predictions
   // reference order, PBVI leaves: every row's candidate alphas (those whose
   // exact chain can reach the row's maximum, from the split-x GEMM's
   // approximate dots and a rigorous bound) as one exact chain set (FC_LIST)
@@ -942,6 +943,24 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     HIPCHK(mq);
   }
   tmark(1);
+  // main: the expanded belief's running sums (cdf chain: tables, walk, cdf,
+  // then the samples).  PP2_ROW_FIRST=1 enqueues them first, before the side
+  // stream's predictions and children (a rocprofv3 trace shows 30 us less
+  // per expansion; without the profiler the plan step is 0.40 against 0.39
+  // ms: opt-in, tools/ab_row_first.sh)
+  pp2::FcArgs rowc;
+  rowc.n = (int)n;
+  rowc.ld = ld;
+  rowc.row = brow;
+  rowc.out = p->d_rsum;
+  rowc.cdf = p->d_cdf;
+  rowc.sub = p->seq ? nullptr : p->d_sub;  // (the sampler's first search)
+  const bool row_first = !p->fx && !p->seq && p->row_first;
+  if (!p->fx) p->scr_main.attach(&rowc);
+  if (row_first) {
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, rowc, pp2::FC_TABLES));
+    HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, rowc, pp2::FC_DRIVE));
+  }
   // The two streams' launches are interleaved phase by phase, so that
   // neither waits for the host to enqueue the other's (a launch costs the
   // host several us): predictions (side), the cdf chain's tables (main), the
@@ -1034,14 +1053,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
                                       p->d_rout, 9));
   }
   if (!p->fx) {
-    pp2::FcArgs cd;  // main: the expanded belief's running sums
-    cd.n = (int)n;
-    cd.ld = ld;
-    cd.row = brow;
-    cd.out = p->d_rsum;
-    cd.cdf = p->d_cdf;
-    cd.sub = p->seq ? nullptr : p->d_sub;  // (the sampler's first search)
-    p->scr_main.attach(&cd);
+    pp2::FcArgs& cd = rowc;  // main: the expanded belief's running sums
     pp2::FcArgs ch;  // side: the 144 children's masses
     ch.n = (int)n;
     ch.ld = ld;
@@ -1062,11 +1074,11 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     kd.ldo = 9;
     p->scr_fib.attach(&kd);
     if (!p->seq) {
-      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
+      if (!row_first) HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
       HIPCHK(hipEventRecord(p->ev_csum, p->side));  // (the children's chunk sums)
       tmark(3);
-      HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
+      if (!row_first) HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
       HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
       tmark(4);
@@ -1109,17 +1121,9 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       HIPCHK(hipStreamWaitEvent(c->stream, p->ev_csum, 0));
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_SUMS));
     }
-    if (!p->seq) {  // side: the 9 rewards inner_product(b, R[.][a]), off the critical path
-      pp2::FcArgs r;
-      r.n = (int)n;
-      r.ld = ld;
-      r.row = brow;
-      r.partners = p->d_rrows;
-      r.out = p->d_rout;
-      r.ldo = 9;
-      p->scr_rew.attach(&r);
-      HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
-    }
+    // (side: the 9 rewards, off the critical path, are enqueued after the
+    // kept children's FIB launches: each launch ahead of those costs the
+    // critical chain its host time)
     tmark(5);
     HIPCHK(hipStreamWaitEvent(c->stream, p->ev_kids, 0));
     // the node rows acquired for the 144 children: the kept ones are stored
@@ -1151,18 +1155,29 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
                                 sumtab ? pp2::FC_TABLES : pp2::FC_TAB));
     }
     tmark(6);
-    // side: the kept children's PBVI dots (evaluatePbviCpu, the long chains),
-    // beside main's FIB dots, after the rewards already queued there
-    if (p->pbvi) {
-      HIPCHK(hipEventRecord(p->ev_kept, c->stream));
-      HIPCHK(hipStreamWaitEvent(p->side, p->ev_kept, 0));
-      CHECK(ref_pbvi_bounds(p, p->d_children, 144, p->d_klist, p->d_kcount, p->side));
-    }
+    // the kept children's rows are in place: their PBVI dots (evaluatePbviCpu,
+    // the long chains) may start on side
+    if (p->pbvi) HIPCHK(hipEventRecord(p->ev_kept, c->stream));
     if (p->seq) {  // main: the kept children's FIB dots (evaluateFibCpu), sequential chains
       HIPCHK(pp2::launch_pair_seq_small(c->stream, pp2::PAIR_DOT, p->d_children, 144, p->d_frows, 9,
                                         ld, (int)n, p->d_rout + 9, 9, p->d_klist, p->d_kcount));
     } else {
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_DRIVE));
+      // side: the 9 rewards inner_product(b, R[.][a])
+      pp2::FcArgs r;
+      r.n = (int)n;
+      r.ld = ld;
+      r.row = brow;
+      r.partners = p->d_rrows;
+      r.out = p->d_rout;
+      r.ldo = 9;
+      p->scr_rew.attach(&r);
+      HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
+    }
+    // side: the PBVI dots, beside main's FIB dots
+    if (p->pbvi) {
+      HIPCHK(hipStreamWaitEvent(p->side, p->ev_kept, 0));
+      CHECK(ref_pbvi_bounds(p, p->d_children, 144, p->d_klist, p->d_kcount, p->side));
     }
   }  // (!p->fx)
   HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards, the PBVI dots)
@@ -1565,6 +1580,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
     p->spin = !(sw && sw[0] == '0');
     const char* fc = getenv("PP2_FIB_CANDS");
     p->fib_cands = fc && fc[0] == '1';
+    const char* rf = getenv("PP2_ROW_FIRST");
+    p->row_first = rf && rf[0] == '1';
   }
   *out = p;
   return PP2_OK;
