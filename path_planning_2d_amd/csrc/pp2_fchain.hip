@@ -542,6 +542,18 @@ __device__ __forceinline__ void chunk_entries(const FcArgs& a, const Terms<BASE,
   float wq[KC][4];
   T.partner_quads(x0, wq);
   const uint32_t cm = K > 0 && a.cmask ? a.cmask[id] : 0xffffu;
+  if (K > 0 && BASE == FC_KEPT && a.plan) {
+    // (the kept children's FIB sets with PP2_FC_PLAN9=1: crossing plans for
+    // the candidate chains)
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      if (!((cm >> i) & 1u)) continue;
+      float tt[4];
+      T.terms_with(v, wq, i, tt);
+      chain_chunk_entry<true>(a, tt, sP[i * sPstride], j, (long long)gc * KC + i, lane, nch);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < KC; ++i) {
     if (!((cm >> i) & 1u)) continue;  // (uniform: not a candidate)

@@ -227,6 +227,12 @@ struct pp2_planner {
   pp2::FcScratch scr_fib, scr_rew;
   hipStream_t side2 = nullptr;  // (spare)
   hipEvent_t ev_csum = nullptr, ev_fsum = nullptr;
+  // PP2_PLAN_EVENTS=1: timing events at the expansion's phase ends (device
+  // time from the expansion's start on main), summed over expansions
+  bool pev = false;
+  hipEvent_t tev[10] = {};
+  double tev_sum[10] = {};
+  long long tev_n = 0;
   float** h_rowptr = nullptr;   // pinned, mapped: the 144 children's node rows
   float** d_rowptr = nullptr;
   float** d_rowdev = nullptr;   // device: the same, published by k_tree_sample
@@ -919,6 +925,9 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     p->t_mark[i] += std::chrono::duration<double, std::micro>(t - t_prev).count();
     t_prev = t;
   };
+  auto tev = [&](int i, hipStream_t st) {  // (PP2_PLAN_EVENTS)
+    if (p->pev) (void)hipEventRecord(p->tev[i], st);
+  };
   CHECK(ref_frows(p));
   // the rand() values of the 9 QNode constructors, in the reference's order
   for (uint32_t a = 0; a < 9; ++a)
@@ -943,6 +952,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     HIPCHK(mq);
   }
   tmark(1);
+  tev(0, c->stream);
   // main: the expanded belief's running sums (cdf chain: tables, walk, cdf,
   // then the samples).  PP2_ROW_FIRST=1 enqueues them first, before the side
   // stream's predictions and children (a rocprofv3 trace shows 30 us less
@@ -960,6 +970,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   if (row_first) {
     HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, rowc, pp2::FC_TABLES));
     HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, rowc, pp2::FC_DRIVE));
+    tev(3, c->stream);
   }
   // The two streams' launches are interleaved phase by phase, so that
   // neither waits for the host to enqueue the other's (a launch costs the
@@ -967,6 +978,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
   // children's tables (side), the cdf driver and running sums (main), the
   // children's driver (side), the samples (main); the rewards last (side).
   HIPCHK(pp2::launch_tree_pred(p->side, c->g, c->T.v, brow, ld, p->d_pred, tree_sparse_t(c)));
+  tev(1, p->side);
   tmark(2);
   if (p->fx) {
     // main: the expanded belief's running sums and the 9 x N samples (one
@@ -1077,9 +1089,14 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       if (!row_first) HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
       HIPCHK(hipEventRecord(p->ev_csum, p->side));  // (the children's chunk sums)
+      tev(2, p->side);
       tmark(3);
-      if (!row_first) HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
+      if (!row_first) {
+        HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
+        tev(3, c->stream);
+      }
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
+      tev(4, p->side);
       HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
       tmark(4);
     }
@@ -1109,6 +1126,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
         sa.rows_out = p->d_rowdev;
       }
       HIPCHK(pp2::launch_tree_sample(c->stream, sa));
+      tev(5, c->stream);
     }
     const bool sumtab = pp2::fc_sumtab_active();
     kd.glist = p->d_klist;
@@ -1120,6 +1138,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       // sums ~12 us after the samples)
       HIPCHK(hipStreamWaitEvent(c->stream, p->ev_csum, 0));
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_SUMS));
+      tev(6, c->stream);
     }
     // (side: the 9 rewards, off the critical path, are enqueued after the
     // kept children's FIB launches: each launch ahead of those costs the
@@ -1153,6 +1172,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       }
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd,
                                 sumtab ? pp2::FC_TABLES : pp2::FC_TAB));
+      tev(7, c->stream);
     }
     tmark(6);
     // the kept children's rows are in place: their PBVI dots (evaluatePbviCpu,
@@ -1163,6 +1183,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
                                         ld, (int)n, p->d_rout + 9, 9, p->d_klist, p->d_kcount));
     } else {
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_DRIVE));
+      tev(8, c->stream);
       // side: the 9 rewards inner_product(b, R[.][a])
       pp2::FcArgs r;
       r.n = (int)n;
@@ -1173,6 +1194,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       r.ldo = 9;
       p->scr_rew.attach(&r);
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_ROW, 9, 1, r));
+      tev(9, p->side);
     }
     // side: the PBVI dots, beside main's FIB dots
     if (p->pbvi) {
@@ -1196,6 +1218,13 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     for (int i = 0; i < 144; i += 16) __builtin_prefetch(p->h_lbv + i);
   if (p->h_pstat) p->stat_cands += *p->h_pstat;
   if (p->d_stamps) fx_stamps_collect(p);
+  if (p->pev && !p->fx && !p->seq) {
+    for (int i = 1; i < 10; ++i) {
+      float ms = 0.0f;
+      if (hipEventElapsedTime(&ms, p->tev[0], p->tev[i]) == hipSuccess) p->tev_sum[i] += 1e3 * ms;
+    }
+    ++p->tev_n;
+  }
   if (p->timing) {
     volatile float sink = p->h_rout[9 + 9 * 143] + (float)p->h_counts[143];
     (void)sink;
@@ -1580,6 +1609,12 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
     p->spin = !(sw && sw[0] == '0');
     const char* fc = getenv("PP2_FIB_CANDS");
     p->fib_cands = fc && fc[0] == '1';
+    const char* pe = getenv("PP2_PLAN_EVENTS");
+    if (pe && pe[0] == '1') {
+      p->pev = true;
+      for (hipEvent_t& e : p->tev)
+        if (hipEventCreate(&e) != hipSuccess) return fail(set_err(PP2_EHIP, "planner timing events"));
+    }
     const char* rf = getenv("PP2_ROW_FIRST");
     p->row_first = rf && rf[0] == '1';
   }
@@ -1616,6 +1651,17 @@ int pp2_planner_destroy(pp2_planner* p) {
   for (void* d : {(void*)p->d_aflag, (void*)p->d_plist, (void*)p->d_pcount, (void*)p->d_rowdev,
                    (void*)p->d_cmask})
     if (d) (void)hipFree(d);
+  if (p->pev && p->tev_n > 0) {
+    static const char* names[10] = {"start", "pred", "children tables", "row walk+cdf",
+                                    "children walk", "sample", "FIB sums", "FIB tables",
+                                    "FIB walk", "rewards"};
+    fprintf(stderr, "pp2 planner: device us from an expansion's start (main), mean of %lld:",
+            p->tev_n);
+    for (int i = 1; i < 10; ++i) fprintf(stderr, " %s %.1f;", names[i], p->tev_sum[i] / p->tev_n);
+    fprintf(stderr, "\n");
+  }
+  for (hipEvent_t e : p->tev)
+    if (e) (void)hipEventDestroy(e);
   if (p->timing && p->t_n > 0)
     fprintf(stderr, "pp2 planner: %lld expansions, host us per expansion: enqueue %.1f, "
             "after the wait .. children stored %.1f, .. next expansion %.1f; kept children "
