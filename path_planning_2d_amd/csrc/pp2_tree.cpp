@@ -258,7 +258,7 @@ struct pp2_planner {
   bool spin = true;             // wait_event: poll (PP2_SPIN_WAIT)
   double t_enq = 0, t_post = 0, t_between = 0;
   double t_pa = 0, t_pb = 0;  // (t_post: .. the nodes' first row read, .. the nodes built)
-  double t_mark[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (enqueue phases, tmark())
+  double t_mark[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // (enqueue phases, tmark())
   // (plan steps: entry .. the first expansion, the last expansion .. return,
   // the caller's time between steps)
   double t_upd = 0, t_tail = 0, t_out = 0;
@@ -1127,6 +1127,7 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       }
       HIPCHK(pp2::launch_tree_sample(c->stream, sa));
       tev(5, c->stream);
+      tmark(8);
     }
     const bool sumtab = pp2::fc_sumtab_active();
     kd.glist = p->d_klist;
@@ -1675,10 +1676,11 @@ int pp2_planner_destroy(pp2_planner* p) {
             p->t_tail / p->t_steps, p->t_out / (p->t_steps - 1));
   if (p->timing && p->t_n > 0)
     fprintf(stderr, "pp2 planner: enqueue phases us: rand+slots %.1f, fork %.1f, pred %.1f, tables "
-            "%.1f, drives %.1f, sample+rewards %.1f, store %.1f, dots+join %.1f\n",
+            "%.1f, drives %.1f, sample %.1f, FIB sums %.1f, FIB tables %.1f, FIB walk+rewards+join "
+            "%.1f\n",
             p->t_mark[0] / p->t_n, p->t_mark[1] / p->t_n, p->t_mark[2] / p->t_n,
-            p->t_mark[3] / p->t_n, p->t_mark[4] / p->t_n, p->t_mark[5] / p->t_n,
-            p->t_mark[6] / p->t_n, p->t_mark[7] / p->t_n);
+            p->t_mark[3] / p->t_n, p->t_mark[4] / p->t_n, p->t_mark[8] / p->t_n,
+            p->t_mark[5] / p->t_n, p->t_mark[6] / p->t_n, p->t_mark[7] / p->t_n);
   if (p->h_pstat) {
     if (p->stat_sets > 0)
       fprintf(stderr, "pp2 planner: PBVI candidate chains %lld over %lld rows in %lld sets "
