@@ -536,11 +536,19 @@ __device__ __forceinline__ void store_kept_cells(const FcArgs& a, const float (&
 template <int BASE, int K>
 __device__ __forceinline__ void chunk_entries(const FcArgs& a, const Terms<BASE, K>& T,
                                               const float (&v)[4], int x0, int j, int gc, int id,
-                                              const float* sP, int sPstride, int lane, int nch) {
+                                              const float* sP, int sPstride, int lane, int nch,
+                                              const float (*wq0)[4] = nullptr) {
   constexpr int KC = K > 0 ? K : 1;
   if (BASE == FC_KEPT && a.kept_rows) store_kept_cells(a, v, x0, id);
   float wq[KC][4];
-  T.partner_quads(x0, wq);
+  if (wq0) {
+#pragma unroll
+    for (int i = 0; i < KC; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wq[i][q] = wq0[i][q];
+  } else {
+    T.partner_quads(x0, wq);
+  }
   const uint32_t cm = K > 0 && a.cmask ? a.cmask[id] : 0xffffu;
   if (K > 0 && BASE == FC_KEPT && a.plan) {
     // (the kept children's FIB sets with PP2_FC_PLAN9=1: crossing plans for
@@ -679,6 +687,20 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
   __shared__ float sPart[KC][4];
   __shared__ float sP[KC][kFcSegChunks];
   const int seg = blockIdx.x;
+  // FC_KEPT: every group (kept child) has the same partner rows, so a
+  // workgroup looping over several stages its segment's partner quads in
+  // LDS once (in registers across the loop they spill)
+  __shared__ __attribute__((aligned(16))) float sWq[BASE == FC_KEPT ? KC : 1][kFcSegChunks][kFcChunk];
+  if (BASE == FC_KEPT) {
+    Terms<BASE, K> T0;
+    T0.init(a, 0);
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    float w0[KC][4];
+    T0.partner_quads((seg * kFcSegChunks + wv) * kFcChunk + 4 * ln, w0);
+#pragma unroll
+    for (int i = 0; i < KC; ++i)
+      *reinterpret_cast<f4a*>(&sWq[i][wv][4 * ln]) = f4a{w0[i][0], w0[i][1], w0[i][2], w0[i][3]};
+  }
   for (int g = blockIdx.y;; g += gridDim.y) {  // (block-uniform)
   int id;
   if (!group_id(a, g, &id)) return;
@@ -726,7 +748,18 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
     const int x0 = j * kFcChunk + 4 * lane;
     float v[4];
     T.terms4(-1, x0, v);
-    chunk_entries<BASE, K>(a, T, v, x0, j, gc, id, &sP[0][jl], kFcSegChunks, lane, nch);
+    if constexpr (BASE == FC_KEPT) {
+      float wq[KC][4];
+#pragma unroll
+      for (int i = 0; i < KC; ++i) {
+        const f4a q = *reinterpret_cast<const f4a*>(&sWq[i][jl][4 * lane]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wq[i][c] = q[c];
+      }
+      chunk_entries<BASE, K>(a, T, v, x0, j, gc, id, &sP[0][jl], kFcSegChunks, lane, nch, wq);
+    } else {
+      chunk_entries<BASE, K>(a, T, v, x0, j, gc, id, &sP[0][jl], kFcSegChunks, lane, nch);
+    }
   }
   __syncthreads();  // (sPart / sP of the next group)
   }
@@ -2528,6 +2561,14 @@ bool fc_k9wave_enabled() {
   if (g_fc_k9wave < 0) g_fc_k9wave = getenv("PP2_FC_K9WAVE") && getenv("PP2_FC_K9WAVE")[0] == '1';
   return g_fc_k9wave != 0;
 }
+int g_fc_kept_gy = -2;
+int fc_kept_gy() {
+  if (g_fc_kept_gy == -2) {
+    const char* e = getenv("PP2_FC_KEPT_GY");
+    g_fc_kept_gy = e ? atoi(e) : 0;
+  }
+  return g_fc_kept_gy;
+}
 int g_fc_plan9 = -1;
 bool fc_plan9_enabled() {
   if (g_fc_plan9 < 0) g_fc_plan9 = getenv("PP2_FC_PLAN9") && getenv("PP2_FC_PLAN9")[0] == '1';
@@ -2558,8 +2599,11 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
   // step) -- workgroups for 64 groups, looping over more: dispatching the
   // 144-group grid's idle workgroups costs the dispatcher several us
   const int gdisp = a.glist && a.gcount ? std::min(groups, kFcDevGroups) : groups;
-  const int gy = std::min(gdisp, std::max(1, kFcGroupBlocks / nseg));
+  int gy = std::min(gdisp, std::max(1, kFcGroupBlocks / nseg));
   const bool sums = phases & (FC_TABLES | FC_SUMS), tabs = phases & (FC_TABLES | FC_TAB);
+  // (PP2_FC_KEPT_GY: the kept children's tables over fewer workgroup rows,
+  // each looping over several children with its partner quads loaded once)
+  if (BASE == FC_KEPT && tabs && !sums && fc_kept_gy() > 0) gy = std::min(gy, fc_kept_gy());
   if (sums && tabs && a.agg && fc_sumtab_enabled()) {
     a.epoch = next_epoch();
     hipLaunchKernelGGL((k_fc_sumtab<BASE, K>), dim3(nseg, gy), dim3(256), 0, st, a);
