@@ -243,6 +243,8 @@ def compare_exact(gi, oi, where):
     # most are)
     ("sparse_map_100x40", 50, 0, 0, 6, "0", "cands"),
     ("sparse_map_100x40", 5, 1, 500, 3, "0", "cands"),
+    # and with the cdf chain enqueued before the predictions (PP2_ROW_FIRST=1)
+    ("sparse_map_100x40", 5, 1, 500, 3, "0", "rowfirst"),
 ])
 def test_planner_reference_order_bit_exact(oracle, monkeypatch, name, max_depth, lb, S, steps,
                                            seq_max, walk):
@@ -256,13 +258,16 @@ def test_planner_reference_order_bit_exact(oracle, monkeypatch, name, max_depth,
     Grids up to PP2_SEQ_CHAIN_MAX cells (seq_max; default 8192) run the sums
     as walked chains, larger ones as exact parallel chain sets; seq_max "0"
     forces the latter on the small grids, walk "2" the walk whose terms are
-    formed beside it (PP2_CHAIN_WALK), walk "cands" the FIB candidate masks."""
+    formed beside it (PP2_CHAIN_WALK), walk "cands" the FIB candidate masks,
+    "rowfirst" the cdf chain enqueued first."""
     import path_planning_2d_amd as P
     from path_planning_2d_amd import synthetic as S_
     if seq_max is not None:
         monkeypatch.setenv("PP2_SEQ_CHAIN_MAX", seq_max)
     if walk == "cands":
         monkeypatch.setenv("PP2_FIB_CANDS", "1")
+    elif walk == "rowfirst":
+        monkeypatch.setenv("PP2_ROW_FIRST", "1")
     elif walk is not None:
         monkeypatch.setenv("PP2_CHAIN_WALK", walk)
     grid = golden_map(name)
