@@ -288,6 +288,7 @@ struct Terms {
 // (the children set's chunk sums; any value will do there: it only scales
 // the chunk sums the binades are predicted from)
 __device__ __forceinline__ float kept_mass(const FcArgs& a, int id, int nch, int lane) {
+  if (a.kept_unit) return 1.0f;
   if (a.mass) return a.mass[id];
   const float* m = a.msum + (long long)id * nch;
   float acc = 0.0f;
@@ -326,6 +327,10 @@ __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
     float v[4], wq[KC][4];
     T.terms4(-1, x0, v);  // the base terms
     T.partner_quads(x0, wq);
+    // kept_unit: the terms here are fl(w alpha), the chain's fl(fl(w / m)
+    // alpha) (0 < w <= m); the signs come from w and alpha, which an
+    // underflow of either product cannot hide
+    const bool unit = BASE == FC_KEPT && a.kept_unit;
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
       float acc = 0.0f, tt[4];
@@ -334,7 +339,8 @@ __global__ __launch_bounds__(256) void k_fc_sums(FcArgs a) {
       for (int q = 0; q < 4; ++q) {
         const float t = tt[q];
         acc += fabsf(t);
-        fl[i] |= !isfinite(t) ? kBad : t > 0.0f ? kPos : t < 0.0f ? kNeg : 0u;
+        const float sg = unit ? (v[q] != 0.0f ? wq[i][q] : 0.0f) : t;
+        fl[i] |= !isfinite(t) ? kBad : sg > 0.0f ? kPos : sg < 0.0f ? kNeg : 0u;
       }
       const float sum = wave_sum(acc);
       if (lane == 0) a.csum[(long long)(gc * KC + i) * nch + j] = sum;
@@ -661,7 +667,8 @@ __global__ __launch_bounds__(576) void k_fc_tables9(FcArgs a) {
       }
       *reinterpret_cast<f4a*>(&sV[i][4 * lane]) = f4a{v[0], v[1], v[2], v[3]};
     }
-    float run = wave_sum(acc);
+    const float sc9 = BASE == FC_KEPT && a.kept_unit ? 1.0f / a.mass[id] : 1.0f;
+    float run = wave_sum(acc) * sc9;
     // (not a candidate, launch_fib_cands: the wave only stages base values)
     const bool skip = a.cmask && !((a.cmask[id] >> i) & 1u);
     __syncthreads();
@@ -675,7 +682,7 @@ __global__ __launch_bounds__(576) void k_fc_tables9(FcArgs a) {
       float tt[4];
       T.terms_of(v, i, x0, tt);
       chain_chunk_entry(a, tt, run, j, chain, lane, nch);
-      run += rdl(own, c);
+      run += rdl(own, c) * sc9;
     }
     __syncthreads();  // (sV of the next group)
   }
@@ -734,10 +741,12 @@ __global__ __launch_bounds__(256) void k_fc_tables(FcArgs a) {
   __syncthreads();
   if (threadIdx.x < KC) {
     const int i = threadIdx.x;
-    float run = (sPart[i][0] + sPart[i][1]) + (sPart[i][2] + sPart[i][3]);
+    // (kept_unit: the sums were of the unnormalised cells)
+    const float sc = BASE == FC_KEPT && a.kept_unit ? 1.0f / T.m : 1.0f;
+    float run = ((sPart[i][0] + sPart[i][1]) + (sPart[i][2] + sPart[i][3])) * sc;
 #pragma unroll
     for (int c = 0; c < kFcSegChunks; ++c) {
-      const float cs = sP[i][c];
+      const float cs = sP[i][c] * sc;
       sP[i][c] = run;
       run += cs;
     }
@@ -1791,10 +1800,12 @@ __global__ __launch_bounds__(64) void k_fib_cands(FcArgs a, uint16_t* __restrict
     if (!group_id(a, g, &id)) return;
     const int nch = fc_chunks(a.n), nseg = fc_segments(a.n);
     FcArgs ap = a;
-    ap.mass = nullptr;  // (the sums pass's m')
+    ap.mass = nullptr;  // (the sums pass's m'; kept_unit: 1)
     const double mp = kept_mass(ap, id, nch, lane), m = a.mass[id];
     const double nu = (double)a.n * 0x1p-24, rel = nu / (1.0 - nu);
-    const double absl = (double)a.n * 0x1p-100;
+    // (subnormal results: the chain's terms, and the sums pass's rescaled by
+    // m' / m -- with kept_unit m' = 1 and m can be small)
+    const double absl = (double)a.n * (0x1p-100 + 0x1p-148 * (mp / m));
     const bool mok = mp > 0.0 && m > 0.0 && isfinite(mp) && isfinite(m) && nu < 0.5;
     double lo[9], hi[9];
     bool bounded[9];
@@ -2611,7 +2622,10 @@ hipError_t launch_set(hipStream_t st, int groups, const FcArgs& a0, int phases) 
     // (a wave per chain for one-group K = 9 sets, whose tables are latency:
     // the 9 rewards' 12 -> 8 us; with many groups the 9 waves' repeated base
     // values cost more -- the kept children's FIB sets: 31 -> 47 us)
-    if (K == 9 && ((groups == 1 && !a.gcount) || fc_k9wave_enabled())) {
+    // (kept_unit sums: k_fc_sums, whose flags come from the cells' and
+    // partners' signs)
+    if (K == 9 && ((groups == 1 && !a.gcount) || fc_k9wave_enabled()) &&
+        !(BASE == FC_KEPT && a.kept_unit && sums)) {
       if (sums) hipLaunchKernelGGL((k_fc_sums9<BASE>), dim3(nseg, gy), dim3(576), 0, st, a);
       if (tabs) hipLaunchKernelGGL((k_fc_tables9<BASE>), dim3(nseg, gy), dim3(576), 0, st, a);
     } else {
@@ -2656,7 +2670,11 @@ hipError_t launch_fchain(hipStream_t st, int base, int K, int groups, const FcAr
     if (K != 9 || !a.pred || !a.lrows || a.row || a.cdf || groups > 144 ||
         (!a.glist && a.g0 + groups > 144))
       return hipErrorInvalidValue;
-    if ((phases & (FC_TABLES | FC_SUMS)) && !a.mass && !a.msum) return hipErrorInvalidValue;
+    if ((phases & (FC_TABLES | FC_SUMS)) && !a.mass && !a.msum && !a.kept_unit)
+      return hipErrorInvalidValue;
+    // (kept_unit: the sums pass alone -- a fused sums + tables launch would
+    // table the unnormalised cells)
+    if (a.kept_unit && (phases & FC_TABLES)) return hipErrorInvalidValue;
     if ((phases & (FC_TABLES | FC_TAB | FC_DRIVE)) && (!a.mass || !a.kept_rows))
       return hipErrorInvalidValue;
   }
@@ -2772,8 +2790,8 @@ hipError_t launch_store_kept(hipStream_t st, const int* klist, const int* kcount
 }
 
 hipError_t launch_fib_cands(hipStream_t st, const FcArgs& a, uint16_t* cmask) {
-  if (!cmask || !a.glist || !a.gcount || !a.csum || !a.cflag || !a.out || !a.mass || !a.msum ||
-      a.n <= 0)
+  if (!cmask || !a.glist || !a.gcount || !a.csum || !a.cflag || !a.out || !a.mass ||
+      (!a.msum && !a.kept_unit) || a.n <= 0)
     return hipErrorInvalidValue;
   FcArgs b = a;
   b.ngroups = 144;  // (the kept children: at most 144, gcount of them)

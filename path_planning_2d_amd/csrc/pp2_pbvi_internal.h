@@ -171,6 +171,9 @@ struct FcArgs {
   float* kept_rows = nullptr;    // [144][ld] normalised kept children (written by tables)
   float* const* rowptr = nullptr;  // optional device [144]: their node rows too
   int by_id = 0;                 // scratch chain index (id * K + i) instead of (g * K + i)
+  // FC_KEPT: the sums pass runs with mass 1 (needs neither mass nor msum);
+  // the tables scale its running sums by 1 / mass
+  int kept_unit = 0;
   // K = 9, by_id: chain i of group id is tabled and walked only when bit i of
   // cmask[id] is set (launch_fib_cands); the others' out entries hold -inf
   const uint16_t* cmask = nullptr;

@@ -239,6 +239,7 @@ struct pp2_planner {
   uint16_t* d_cmask = nullptr;  // the kept children's FIB candidates (launch_fib_cands)
   bool fib_cands = false;       // PP2_FIB_CANDS=1: the FIB chains below another skipped
   bool row_first = false;       // PP2_ROW_FIRST=1: the cdf chain enqueued before the predictions
+  bool fib_unit = true;         // PP2_FIB_UNIT=0: the FIB sums wait for the children's chunk sums
   // reference order, PBVI leaves: every row's candidate alphas (those whose
   // exact chain can reach the row's maximum, from the split-x GEMM's
   // approximate dots and a rigorous bound) as one exact chain set (FC_LIST)
@@ -1088,7 +1089,8 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     if (!p->seq) {
       if (!row_first) HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
-      HIPCHK(hipEventRecord(p->ev_csum, p->side));  // (the children's chunk sums)
+      if (!p->fib_unit)
+        HIPCHK(hipEventRecord(p->ev_csum, p->side));  // (the children's chunk sums)
       tev(2, p->side);
       tmark(3);
       if (!row_first) {
@@ -1137,7 +1139,14 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
       // (their masses approximated by the children's chunk sums; waiting
       // for the walk here instead, one cross-stream wait fewer, started the
       // sums ~12 us after the samples)
-      HIPCHK(hipStreamWaitEvent(c->stream, p->ev_csum, 0));
+      // (PP2_FIB_UNIT, default: the sums of the unnormalised cells, which
+      // need nothing from side -- no cross-stream wait -- and which the
+      // tables scale by 1 / mass)
+      if (p->fib_unit) {
+        kd.kept_unit = 1;
+      } else {
+        HIPCHK(hipStreamWaitEvent(c->stream, p->ev_csum, 0));
+      }
       HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_KEPT, 9, 144, kd, pp2::FC_SUMS));
       tev(6, c->stream);
     }
@@ -1616,6 +1625,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
       for (hipEvent_t& e : p->tev)
         if (hipEventCreate(&e) != hipSuccess) return fail(set_err(PP2_EHIP, "planner timing events"));
     }
+    const char* fu = getenv("PP2_FIB_UNIT");
+    p->fib_unit = !(fu && fu[0] == '0');
     const char* rf = getenv("PP2_ROW_FIRST");
     p->row_first = rf && rf[0] == '1';
   }
