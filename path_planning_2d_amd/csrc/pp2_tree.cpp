@@ -240,6 +240,7 @@ struct pp2_planner {
   bool fib_cands = false;       // PP2_FIB_CANDS=1: the FIB chains below another skipped
   bool row_first = false;       // PP2_ROW_FIRST=1: the cdf chain enqueued before the predictions
   bool fib_unit = true;         // PP2_FIB_UNIT=0: the FIB sums wait for the children's chunk sums
+  bool host_join = true;        // PP2_HOST_JOIN=0: main joins side on the device
   // reference order, PBVI leaves: every row's candidate alphas (those whose
   // exact chain can reach the row's maximum, from the split-x GEMM's
   // approximate dots and a rigorous bound) as one exact chain set (FC_LIST)
@@ -1213,11 +1214,14 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     }
   }  // (!p->fx)
   HIPCHK(hipEventRecord(p->ev_join, p->side));  // (the rewards, the PBVI dots)
-  HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
+  // (PP2_HOST_JOIN, default: the host waits for both streams' last events;
+  // else main waits for side's on the device, one cross-stream wait more)
+  if (!p->host_join) HIPCHK(hipStreamWaitEvent(c->stream, p->ev_join, 0));
   HIPCHK(hipEventRecord(p->ev_done, c->stream));
   tmark(7);
   const clk::time_point t_enq = p->timing ? clk::now() : clk::time_point{};
   HIPCHK(wait_event(p, p->ev_done));
+  if (p->host_join) HIPCHK(wait_event(p, p->ev_join));
   const clk::time_point t_ret = p->timing ? clk::now() : clk::time_point{};
   // the device-written host rows (counts, rewards and FIB dots, PBVI bounds)
   // are cache misses: request every line at once, not one miss at a time
@@ -1627,6 +1631,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
     }
     const char* fu = getenv("PP2_FIB_UNIT");
     p->fib_unit = !(fu && fu[0] == '0');
+    const char* hj = getenv("PP2_HOST_JOIN");
+    p->host_join = !(hj && hj[0] == '0');
     const char* rf = getenv("PP2_ROW_FIRST");
     p->row_first = rf && rf[0] == '1';
   }
