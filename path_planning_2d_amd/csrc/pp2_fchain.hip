@@ -1164,6 +1164,9 @@ __global__ __launch_bounds__(64) void k_fc_drive(FcArgs a) {
 #ifndef PP2_WALK_PRIO
 #define PP2_WALK_PRIO 1
 #endif
+#ifndef PP2_CDF_TAIL  // (k_fc_cdf's exact rounds before the serial tail; A/B builds)
+#define PP2_CDF_TAIL 8
+#endif
 #ifndef PP2_WALK_TAIL
 #define PP2_WALK_TAIL 8
 #endif
@@ -1633,7 +1636,7 @@ __global__ __launch_bounds__(256) void k_fc_cdf(FcArgs a) {
   for (int q = 0; q < 4; ++q) t[q] = fabsf(t[q]);
   int E = a.cst[j].x, k = a.cst[j].y;
   float cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  chunk_exact(t, lane, &E, &k, &cv, nullptr, sT[threadIdx.x >> 6], PP2_WALK_TAIL);
+  chunk_exact(t, lane, &E, &k, &cv, nullptr, sT[threadIdx.x >> 6], PP2_CDF_TAIL);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const float v = neg ? (cv[q] == 0.0f ? 0.0f : -cv[q]) : cv[q];
