@@ -3042,15 +3042,25 @@ extern "C" int pp2_debug_fchain_pairs(int n, int R, const float* x, int S, const
 //   L[16][n]: out[c] = accumulate of child c = z * 9 + a (FX_CHILD, all 144),
 //   then for the kcount children klist[] the normalised rows (rows[c][n]) and
 //   their 9 dots with partners (out[144 + 9 c + i], FX_KEPT).
+// mode 2: as mode 1 through the planner's chain sets instead (pp2_tree.cpp):
+//   FC_CHILD tables + drive, then the kept children's FC_KEPT sums, tables,
+//   drive; K's bit 0 = kept_unit (the sums over the unnormalised cells), bit
+//   1 = the FIB candidate masks (launch_fib_cands: pruned dots are -inf).
 // ms (if set): the set's event time, median of 5 runs after a warm-up.  Synchronous.
 extern "C" int pp2_debug_fx(int mode, int n, const float* x, const float* partners, int K,
                             const float* pred, const float* lrows, const int* klist, int kcount,
                             float* out, float* cdf, float* rows, float* ms) {
-  if (n <= 0 || n > 65536 || (K != 0 && K != 9) || !out || (mode == 0 && !x) ||
-      (mode == 1 && (!pred || !lrows || !partners || kcount < 0 || kcount > 144 ||
+  if (n <= 0 || n > 65536 || (mode != 2 && K != 0 && K != 9) || (mode == 2 && (K < 0 || K > 3)) ||
+      !out || (mode == 0 && !x) ||
+      (mode >= 1 && (!pred || !lrows || !partners || kcount < 0 || kcount > 144 ||
                      (kcount > 0 && !klist))) ||
-      (mode != 0 && mode != 1) || (K == 9 && !partners && mode == 0))
+      (mode != 0 && mode != 1 && mode != 2) || (K == 9 && !partners && mode == 0))
     return 1;
+  pp2::FcScratch sc_child, sc_kept;
+  uint16_t* dcm = nullptr;
+  if (mode == 2 && (!sc_child.reserve(n, 144) || !sc_kept.reserve(n, 144 * 9) ||
+                    hipMalloc(&dcm, 144 * sizeof(uint16_t)) != hipSuccess))
+    return 2;
   const size_t ld = ((size_t)n + 63) / 64 * 64;
   float *dx = nullptr, *dp = nullptr, *dout = nullptr, *dcdf = nullptr, *dpred = nullptr,
         *dl = nullptr, *drows = nullptr;
@@ -3070,12 +3080,47 @@ extern "C" int pp2_debug_fx(int mode, int n, const float* x, const float* partne
   if (ok(hipMalloc(&dout, nout * sizeof(float))) && ok(hipMemset(dout, 0, nout * sizeof(float))) &&
       (mode != 0 || up(&dx, x, 1)) && (!partners || up(&dp, partners, 9)) &&
       (mode != 0 || !cdf || up(&dcdf, nullptr, 1)) &&
-      (mode != 1 || (up(&dpred, pred, 9) && up(&dl, lrows, 16) && up(&drows, nullptr, 144) &&
+      (mode == 0 || (up(&dpred, pred, 9) && up(&dl, lrows, 16) && up(&drows, nullptr, 144) &&
                      ok(hipMalloc(&dk, 145 * sizeof(int))) &&
                      (kcount == 0 || ok(hipMemcpy(dk, klist, kcount * sizeof(int),
                                                   hipMemcpyHostToDevice))) &&
                      ok(hipMemcpy(dk + 144, &kcount, sizeof(int), hipMemcpyHostToDevice))))) {
     auto run = [&]() -> hipError_t {
+      if (mode == 2) {
+        pp2::FcArgs ch;
+        ch.n = n;
+        ch.ld = (int)ld;
+        ch.pred = dpred;
+        ch.lrows = dl;
+        ch.out = dout;
+        ch.ldo = 1;
+        sc_child.attach(&ch);
+        hipError_t e = pp2::launch_fchain(nullptr, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES);
+        if (e == hipSuccess) e = pp2::launch_fchain(nullptr, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE);
+        pp2::FcArgs kd;
+        kd.n = n;
+        kd.ld = (int)ld;
+        kd.pred = dpred;
+        kd.lrows = dl;
+        kd.partners = dp;
+        kd.msum = ch.csum;
+        kd.out = dout + 144;
+        kd.ldo = 9;
+        kd.glist = dk;
+        kd.gcount = dk + 144;
+        kd.kept_unit = K & 1;
+        sc_kept.attach(&kd);
+        if (e == hipSuccess) e = pp2::launch_fchain(nullptr, pp2::FC_KEPT, 9, 144, kd, pp2::FC_SUMS);
+        kd.mass = dout;
+        kd.kept_rows = drows;
+        if (e == hipSuccess && (K & 2)) {
+          e = pp2::launch_fib_cands(nullptr, kd, dcm);
+          kd.cmask = dcm;
+        }
+        if (e == hipSuccess) e = pp2::launch_fchain(nullptr, pp2::FC_KEPT, 9, 144, kd, pp2::FC_TAB);
+        if (e == hipSuccess) e = pp2::launch_fchain(nullptr, pp2::FC_KEPT, 9, 144, kd, pp2::FC_DRIVE);
+        return e;
+      }
       pp2::FxArgs a;
       a.n = n;
       a.ld = (int)ld;
@@ -3135,7 +3180,7 @@ extern "C" int pp2_debug_fx(int mode, int n, const float* x, const float* partne
     }
   }
   for (void* p : {(void*)dx, (void*)dp, (void*)dout, (void*)dcdf, (void*)dpred, (void*)dl,
-                  (void*)drows, (void*)dk})
+                  (void*)drows, (void*)dk, (void*)dcm})
     if (p) (void)hipFree(p);
   return st;
 }

@@ -302,6 +302,55 @@ def test_fx_children_and_kept_dots_bit_exact(n):
                 assert bits(got) == bits(want), f"child {c} dot {i}: {got!r} != {want!r}"
 
 
+@pytest.mark.parametrize("n,opts", [(9000, 0), (9000, 1), (9000, 3), (65536, 1), (65536, 3)])
+def test_fc_kept_sets_bit_exact(n, opts):
+    """The planner's chain sets for an expansion (pp2_debug_fx mode 2, as
+    pp2_tree.cpp runs them): FC_CHILD masses, then the kept children's
+    FC_KEPT sums, tables (normalised rows stored) and walk -- with the sums
+    over the unnormalised cells (opts bit 0, kept_unit) and the FIB candidate
+    masks (bit 1: a pruned dot is -inf, the first maximum stays) -- against
+    numpy: masses, rows and dots bit for bit.  Alphas: negative, one mixed-sign
+    row, one positive row, one row of tiny magnitudes (products that underflow
+    unnormalised, not normalised)."""
+    rng = np.random.default_rng(n + 7 * opts)
+    pred = (rng.random((9, n), dtype=np.float32) / np.float32(n)).astype(np.float32)
+    pred[:, rng.random(n) < 0.3] = 0.0
+    pred[3] = np.ldexp(pred[3], -100)                 # products into the FTZ range
+    L = rng.random((16, n), dtype=np.float32)
+    L[5, ::7] = np.float32(1e-39)                     # subnormal likelihoods flushed
+    L[9] = 0.0
+    A = -(20 + 20 * rng.random((9, n), dtype=np.float32))
+    A[4] = rng.random(n, dtype=np.float32) - 0.5
+    A[7] = 20 + 20 * rng.random(n, dtype=np.float32)
+    A[8] = -np.ldexp(rng.random(n, dtype=np.float32) + 0.5, -30)
+    live = [c for c in range(144) if seq(ftz(pred[c % 9] * ftz(L[c // 9])))[0] > 0]
+    klist = np.array(sorted(rng.choice(live, 46, replace=False)), np.int32)
+    out = np.zeros(144 + 144 * 9, np.float32)
+    rows_ = np.zeros((144, n), np.float32)
+    st = _fx()(2, n, None, _ptr(A), opts, _ptr(pred), _ptr(L),
+               klist.ctypes.data_as(C.POINTER(C.c_int)), len(klist), _ptr(out), None,
+               _ptr(rows_), None)
+    assert st == 0, st
+    for c in range(144):
+        a, z = c % 9, c // 9
+        v = ftz(pred[a] * ftz(L[z]))
+        m, _ = seq(v)
+        assert bits(out[c]) == bits(m), f"child {c}: mass {out[c]!r} != {m!r}"
+        if c not in klist:
+            continue
+        b = (v / m).astype(np.float32)
+        assert np.array_equal(bits(rows_[c]), bits(b)), f"child {c}: row"
+        want = np.array([seq(b * A[i])[0] for i in range(9)], np.float32)
+        got = out[144 + 9 * c:144 + 9 * c + 9]
+        if opts & 2:
+            # (first_max9: the value of the first maximum)
+            assert bits(np.float32(max(got.tolist()))) == bits(np.float32(max(want.tolist()))), c
+            kept = got != -np.inf
+            assert np.array_equal(bits(got[kept]), bits(want[kept])), f"child {c}: kept dots"
+        else:
+            assert np.array_equal(bits(got), bits(want)), f"child {c}: dots {got} != {want}"
+
+
 @pytest.mark.parametrize("ksplit", [1, 4])
 def test_pbvi_candidate_filter_finds_the_first_maximum(ksplit):
     """The opt-in PBVI candidate filter (k_pbvi_cands after the split-x MFMA
