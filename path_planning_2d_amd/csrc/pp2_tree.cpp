@@ -241,6 +241,7 @@ struct pp2_planner {
   bool row_first = false;       // PP2_ROW_FIRST=1: the cdf chain enqueued before the predictions
   bool fib_unit = true;         // PP2_FIB_UNIT=0: the FIB sums wait for the children's chunk sums
   bool host_join = true;        // PP2_HOST_JOIN=0: main joins side on the device
+  bool kids_first = false;      // PP2_KIDS_FIRST=1: the children's launches ahead of the cdf chain's
   // reference order, PBVI leaves: every row's candidate alphas (those whose
   // exact chain can reach the row's maximum, from the split-x GEMM's
   // approximate dots and a rigorous bound) as one exact chain set (FC_LIST)
@@ -1088,19 +1089,28 @@ int expand_vnode_ref(pp2_planner* p, VNode* v) {
     kd.ldo = 9;
     p->scr_fib.attach(&kd);
     if (!p->seq) {
-      if (!row_first) HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
+      // (PP2_KIDS_FIRST=1: each phase's children launch before the cdf
+      // chain's)
+      const bool kids_first = p->kids_first && !row_first;
+      if (!row_first && !kids_first)
+        HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_TABLES));
       if (!p->fib_unit)
         HIPCHK(hipEventRecord(p->ev_csum, p->side));  // (the children's chunk sums)
       tev(2, p->side);
+      if (kids_first) HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_TABLES));
       tmark(3);
-      if (!row_first) {
+      if (!row_first && !kids_first) {
         HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
         tev(3, c->stream);
       }
       HIPCHK(pp2::launch_fchain(p->side, pp2::FC_CHILD, 0, 144, ch, pp2::FC_DRIVE));
       tev(4, p->side);
       HIPCHK(hipEventRecord(p->ev_kids, p->side));  // (the children's masses)
+      if (kids_first) {
+        HIPCHK(pp2::launch_fchain(c->stream, pp2::FC_ROW, 0, 1, cd, pp2::FC_DRIVE));
+        tev(3, c->stream);
+      }
       tmark(4);
     }
     {
@@ -1633,6 +1643,8 @@ int pp2_planner_create(pp2_planner** out, pp2_ctx* c, const pp2_planner_params* 
     p->fib_unit = !(fu && fu[0] == '0');
     const char* hj = getenv("PP2_HOST_JOIN");
     p->host_join = !(hj && hj[0] == '0');
+    const char* kf = getenv("PP2_KIDS_FIRST");
+    p->kids_first = kf && kf[0] == '1';
     const char* rf = getenv("PP2_ROW_FIRST");
     p->row_first = rf && rf[0] == '1';
   }
